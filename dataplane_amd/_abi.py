@@ -1,0 +1,249 @@
+# SPDX-License-Identifier: Apache-2.0
+"""ctypes mirror of include/dpgpu.h and the library loaders.
+
+The product library is ``dataplane_amd/lib/libdpgpu.so`` (HIP kernels +
+C ABI).  It is loaded from the source tree only; if it is missing or a GPU is
+not present the calls fail loudly -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_DIR = os.path.join(HERE, "lib")
+
+ABI_VERSION = 1
+HEADROOM = 96
+
+# DoneReason (net/src/packet/meta.rs:84-119)
+DONE_NAMES = [
+    "InternalFailure", "InterfaceUnknown", "InterfaceDetached", "InterfaceAdmDown",
+    "InterfaceOperDown", "InterfaceUnsupported", "NotEthernet", "Unhandled", "MacNotForUs",
+    "InvalidDstMac", "MissingEtherType", "NotIp", "RouteFailure", "RouteDrop",
+    "HopLimitExceeded", "MissL2resolution", "VxlanDecapFailure", "VxlanEncapFailure",
+    "Filtered", "AclDropped", "NatOutOfResources", "FlowCapacityExceeded",
+    "NatUnsupportedProto", "NatFailure", "NatNotPortForwarded", "Malformed", "Unroutable",
+    "InvalidChecksum", "IcmpErrorIncomplete", "InternalDrop", "Local", "Delivered",
+    "DeparseError", "NoHeadRoom",
+]
+DONE = {n: i for i, n in enumerate(DONE_NAMES)}
+DONE_COUNT = len(DONE_NAMES)
+DONE_NONE = 255
+
+# MetaFlags (net/src/packet/meta.rs:121-136)
+META = dict(INITIALIZED=1 << 0, IS_L2_BCAST=1 << 1, NATTED_SRC=1 << 2, NATTED_DST=1 << 3,
+            REFR_CHKSUM=1 << 4, KEEP=1 << 5, IS_OVERLAY=1 << 6, REQ_MASQUERADE=1 << 7,
+            REQ_PORT_FORWARDING=1 << 8, REQ_STATIC_NAT_SRC=1 << 9, REQ_STATIC_NAT_DST=1 << 10)
+
+IN_SEEDED_OVERLAY = 1
+
+PKT_IN = np.dtype([("off", "<u4"), ("len", "<u2"), ("flags", "<u2"), ("iif", "<u4"),
+                   ("src_vni", "<u4")])
+PKT_OUT = np.dtype([("off", "<u4"), ("len", "<u2"), ("done", "u1"), ("acl", "u1"),
+                    ("meta_flags", "<u4"), ("oif", "<u4"), ("dst_vni", "<u4"),
+                    ("src_vni", "<u4"), ("fib_entry", "<u4"), ("acl_rule", "<u4")])
+assert PKT_IN.itemsize == 16 and PKT_OUT.itemsize == 32
+
+
+class IpAddr(C.Structure):
+    _fields_ = [("family", C.c_uint8), ("pad", C.c_uint8 * 3), ("addr", C.c_uint8 * 16)]
+
+
+class Prefix(C.Structure):
+    _fields_ = [("family", C.c_uint8), ("len", C.c_uint8), ("pad", C.c_uint8 * 2),
+                ("addr", C.c_uint8 * 16)]
+
+
+class Fib(C.Structure):
+    _fields_ = [("vrf_id", C.c_uint32), ("flags", C.c_uint32), ("vtep_ip", IpAddr),
+                ("vtep_mac", C.c_uint8 * 6), ("pad", C.c_uint8 * 2)]
+
+
+class VniFib(C.Structure):
+    _fields_ = [("vni", C.c_uint32), ("fib", C.c_uint32)]
+
+
+class Instr(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("flags", C.c_uint32), ("ifindex", C.c_uint32),
+                ("vni", C.c_uint32), ("addr", IpAddr), ("mac", C.c_uint8 * 6),
+                ("pad", C.c_uint8 * 2)]
+
+
+class FibEntry(C.Structure):
+    _fields_ = [("first_instr", C.c_uint32), ("n_instr", C.c_uint32)]
+
+
+class RouteNh(C.Structure):
+    _fields_ = [("first_entry", C.c_uint32), ("n_entries", C.c_uint32)]
+
+
+class Route(C.Structure):
+    _fields_ = [("prefix", Prefix), ("fib", C.c_uint32), ("nh", C.c_uint32)]
+
+
+class Iface(C.Structure):
+    _fields_ = [("ifindex", C.c_uint32), ("admin_state", C.c_uint8), ("oper_state", C.c_uint8),
+                ("iftype", C.c_uint8), ("attach", C.c_uint8), ("vrf_id", C.c_uint32),
+                ("mac", C.c_uint8 * 6), ("pad", C.c_uint8 * 2)]
+
+
+class Adjacency(C.Structure):
+    _fields_ = [("addr", IpAddr), ("ifindex", C.c_uint32), ("mac", C.c_uint8 * 6),
+                ("pad", C.c_uint8 * 2)]
+
+
+class Rule(C.Structure):
+    _fields_ = [("proto_val", C.c_uint8), ("proto_mask", C.c_uint8), ("family", C.c_uint8),
+                ("gate", C.c_uint8), ("vni_a", C.c_uint32), ("vni_b", C.c_uint32),
+                ("sport_lo", C.c_uint16), ("sport_hi", C.c_uint16), ("dport_lo", C.c_uint16),
+                ("dport_hi", C.c_uint16), ("priority", C.c_uint32), ("src", Prefix),
+                ("dst", Prefix), ("action", C.c_uint32), ("action2", C.c_uint32)]
+
+
+class AclDefault(C.Structure):
+    _fields_ = [("src_vni", C.c_uint32), ("dst_vni", C.c_uint32), ("action", C.c_uint32)]
+
+
+class NatTable(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("src_vni", C.c_uint32), ("dst_vni", C.c_uint32),
+                ("first_entry", C.c_uint32), ("n_entries", C.c_uint32)]
+
+
+class NatEntry(C.Structure):
+    _fields_ = [("prefix", Prefix), ("is_pat", C.c_uint32), ("first_port_range", C.c_uint32),
+                ("n_port_ranges", C.c_uint32), ("first_range", C.c_uint32),
+                ("n_ranges", C.c_uint32), ("pad", C.c_uint32), ("size", C.c_uint64)]
+
+
+class PortRange(C.Structure):
+    _fields_ = [("lo", C.c_uint16), ("hi", C.c_uint16)]
+
+
+class NatRange(C.Structure):
+    _fields_ = [("orig_lo_ip", C.c_uint8 * 4), ("orig_hi_ip", C.c_uint8 * 4),
+                ("orig_lo_port", C.c_uint16), ("orig_hi_port", C.c_uint16),
+                ("tgt_lo_ip", C.c_uint8 * 4), ("tgt_hi_ip", C.c_uint8 * 4),
+                ("tgt_lo_port", C.c_uint16), ("tgt_hi_port", C.c_uint16),
+                ("offset", C.c_uint64)]
+
+
+def _arr(t):
+    return [("%s" % t[0], C.POINTER(t[1])), ("n_%s" % t[0], t[2])]
+
+
+class TablesDesc(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("pad0", C.c_uint32), ("genid", C.c_int64),
+                ("fibs", C.POINTER(Fib)), ("n_fibs", C.c_uint32),
+                ("vni_fibs", C.POINTER(VniFib)), ("n_vni_fibs", C.c_uint32),
+                ("routes", C.POINTER(Route)), ("n_routes", C.c_uint64),
+                ("route_nhs", C.POINTER(RouteNh)), ("n_route_nhs", C.c_uint32),
+                ("entries", C.POINTER(FibEntry)), ("n_entries", C.c_uint32),
+                ("instrs", C.POINTER(Instr)), ("n_instrs", C.c_uint32),
+                ("ifaces", C.POINTER(Iface)), ("n_ifaces", C.c_uint32),
+                ("adjs", C.POINTER(Adjacency)), ("n_adjs", C.c_uint32),
+                ("acl_v4", C.POINTER(Rule)), ("n_acl_v4", C.c_uint32),
+                ("acl_v6", C.POINTER(Rule)), ("n_acl_v6", C.c_uint32),
+                ("acl_defaults", C.POINTER(AclDefault)), ("n_acl_defaults", C.c_uint32),
+                ("ff_remote_v4", C.POINTER(Rule)), ("n_ff_remote_v4", C.c_uint32),
+                ("ff_local_v4", C.POINTER(Rule)), ("n_ff_local_v4", C.c_uint32),
+                ("ff_remote_v6", C.POINTER(Rule)), ("n_ff_remote_v6", C.c_uint32),
+                ("ff_local_v6", C.POINTER(Rule)), ("n_ff_local_v6", C.c_uint32),
+                ("nat_tables", C.POINTER(NatTable)), ("n_nat_tables", C.c_uint32),
+                ("nat_entries", C.POINTER(NatEntry)), ("n_nat_entries", C.c_uint32),
+                ("nat_port_ranges", C.POINTER(PortRange)), ("n_nat_port_ranges", C.c_uint32),
+                ("nat_ranges", C.POINTER(NatRange)), ("n_nat_ranges", C.c_uint32)]
+
+
+STRUCTS = dict(dp_ipaddr_t=IpAddr, dp_prefix_t=Prefix, dp_fib_t=Fib, dp_vni_fib_t=VniFib,
+               dp_instr_t=Instr, dp_fib_entry_t=FibEntry, dp_route_nh_t=RouteNh,
+               dp_route_t=Route, dp_iface_t=Iface, dp_adjacency_t=Adjacency, dp_rule_t=Rule,
+               dp_acl_default_t=AclDefault, dp_nat_table_t=NatTable, dp_nat_entry_t=NatEntry,
+               dp_port_range_t=PortRange, dp_nat_range_t=NatRange, dp_tables_desc_t=TablesDesc)
+
+# every symbol include/dpgpu.h declares
+GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_publish",
+               "dp_tables_genid", "dp_process_burst", "dp_process_burst_device",
+               "dp_ctx_synchronize", "dp_tables_device_bytes", "dp_last_error"]
+
+_VP = C.c_void_p
+_U8P = C.POINTER(C.c_uint8)
+
+
+def _load(path: str) -> C.CDLL:
+    if not os.path.exists(path):
+        raise RuntimeError(f"native library missing: {path} (run __graft_entry__.build())")
+    return C.CDLL(path)
+
+
+_gpu = None
+
+
+def gpu_lib() -> C.CDLL:
+    """The product library (HIP).  Raises if it is not built."""
+    global _gpu
+    if _gpu is None:
+        lib = _load(os.path.join(LIB_DIR, "libdpgpu.so"))
+        lib.dp_abi_version.restype = C.c_uint32
+        lib.dp_ctx_create.argtypes = [C.c_int, C.POINTER(_VP)]
+        lib.dp_ctx_destroy.argtypes = [_VP]
+        lib.dp_tables_publish.argtypes = [_VP, C.POINTER(TablesDesc)]
+        lib.dp_tables_genid.argtypes = [_VP]
+        lib.dp_tables_genid.restype = C.c_int64
+        lib.dp_process_burst.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, C.c_uint32, _VP]
+        lib.dp_process_burst_device.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, C.c_uint32,
+                                                _VP, _VP]
+        lib.dp_ctx_synchronize.argtypes = [_VP]
+        lib.dp_tables_device_bytes.argtypes = [_VP]
+        lib.dp_tables_device_bytes.restype = C.c_uint64
+        lib.dp_last_error.restype = C.c_char_p
+        if lib.dp_abi_version() != ABI_VERSION:
+            raise RuntimeError("libdpgpu.so ABI version mismatch")
+        _gpu = lib
+    return _gpu
+
+
+_work = None
+
+
+class WorkloadConfig(C.Structure):
+    _fields_ = [("config", C.c_uint32), ("n_packets", C.c_uint32), ("seed", C.c_uint64),
+                ("n_routes_v4", C.c_uint32), ("n_routes_v6", C.c_uint32),
+                ("n_acl", C.c_uint32), ("n_nat", C.c_uint32), ("n_vni", C.c_uint32),
+                ("tcp_percent", C.c_uint32), ("pad", C.c_uint32)]
+
+
+def work_lib() -> C.CDLL:
+    """Synthetic workload generator (harness library, host only)."""
+    global _work
+    if _work is None:
+        lib = _load(os.path.join(LIB_DIR, "libdpwork.so"))
+        lib.dpw_build.argtypes = [C.POINTER(WorkloadConfig), C.POINTER(_VP)]
+        lib.dpw_free.argtypes = [_VP]
+        lib.dpw_tables.argtypes = [_VP]
+        lib.dpw_tables.restype = C.POINTER(TablesDesc)
+        lib.dpw_buf.argtypes = [_VP]
+        lib.dpw_buf.restype = _U8P
+        lib.dpw_buf_bytes.argtypes = [_VP]
+        lib.dpw_buf_bytes.restype = C.c_uint64
+        lib.dpw_in.argtypes = [_VP]
+        lib.dpw_in.restype = _VP
+        lib.dpw_n.argtypes = [_VP]
+        lib.dpw_n.restype = C.c_uint32
+        lib.dpw_frame_bytes.argtypes = [_VP]
+        lib.dpw_frame_bytes.restype = C.c_uint64
+        lib.dpw_sizeof.argtypes = [C.c_char_p]
+        lib.dpw_sizeof.restype = C.c_uint32
+        _work = lib
+    return _work
+
+
+def check(rc: int, what: str, lib=None) -> None:
+    if rc != 0:
+        msg = ""
+        if lib is not None and hasattr(lib, "dp_last_error"):
+            msg = (lib.dp_last_error() or b"").decode(errors="replace")
+        raise RuntimeError(f"{what} failed: rc={rc} {msg}")

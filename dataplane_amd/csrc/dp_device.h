@@ -1,0 +1,206 @@
+// SPDX-License-Identifier: Apache-2.0
+//
+// Device table image layout (HBM).  Produced by the host table compiler
+// (dp_tables.cpp) from the lowered descriptors of include/dpgpu.h, consumed
+// by the pipeline kernel (dp_kernel.hip).  One contiguous allocation; every
+// "ptr" below is a byte offset from the image base, fixed up to a device
+// pointer by the runtime before launch.
+//
+// Structures (see DESIGN.md "Data layout in HBM"):
+//  - open-addressing hash maps (VNI -> FIB, VRF -> FIB, ifindex -> iface,
+//    (ifindex, ip) -> adjacency MAC, classifier group keys, NAT table keys)
+//  - per-FIB Poptrie-style LPM (direct-pointing table + 6-bit stride nodes
+//    with popcount-compressed child/leaf arrays) for v4 and v6
+//  - classifier = per-(vni_a, vni_b, gate) group bit-vector classifier
+//    (Lakshman-Stiliadis): per-field elementary-interval index -> rule
+//    bit-vector rows, ANDed word by word behind a summary (ABV) level;
+//    first set bit = first match in precedence order
+//  - static NAT = per-table elementary-interval index over NAT prefixes ->
+//    longest covering entry, parent chain for shorter covers, sorted ranges
+#pragma once
+#include <stdint.h>
+
+#ifndef __HIPCC__
+#ifndef __host__
+#define __host__
+#endif
+#ifndef __device__
+#define __device__
+#endif
+#endif
+
+#define DPD_MAX_INSTR 4
+
+namespace dpd {
+
+struct HashSlot {      // generic 16-byte open-addressing slot
+  uint32_t k0, k1, k2; // key words; k2 bit31 = occupied
+  uint32_t val;
+};
+
+struct HashMap {
+  uint64_t slots;      // offset of HashSlot[mask+1]
+  uint32_t mask;       // capacity - 1 (power of two), 0 if empty map
+  uint32_t count;
+};
+
+// Poptrie node (6-bit stride): children bitmap + leaf-run bitmap
+struct PtNode {
+  uint64_t vec;        // bit v: slot v has a child node
+  uint64_t leafvec;    // bit v: slot v starts a leaf run (non-child slots)
+  uint32_t base1;      // first child node index
+  uint32_t base0;      // first leaf index
+  uint64_t pad;
+};
+
+struct Lpm {
+  uint64_t direct;     // offset of uint32_t[1 << dbits]; bit31 = leaf(nh) else node idx
+  uint32_t dbits;      // direct-pointing bits (16..24)
+  uint32_t width;      // 32 or 128
+};
+
+struct FibRec {
+  uint32_t vrf_id;
+  uint32_t flags;      // dp_fib_flag
+  uint8_t vtep_fam;
+  uint8_t vtep_mac[6];
+  uint8_t pad0;
+  uint8_t vtep_ip[16];
+  Lpm v4, v6;
+};
+
+struct Instr {         // compacted dp_instr_t
+  uint8_t kind, flags, fam, pad;
+  uint32_t ifindex;
+  uint32_t vni;
+  uint8_t mac[6];
+  uint8_t pad2[2];
+  uint8_t addr[16];
+};
+
+struct Entry {
+  uint32_t first_instr, n_instr;
+};
+
+struct RouteNh {
+  uint32_t first_entry, n_entries;
+};
+
+struct Iface {
+  uint32_t ifindex;
+  uint8_t admin, oper, iftype, attach;
+  uint32_t vrf_id;
+  uint8_t mac[6];
+  uint8_t pad[2];
+};
+
+struct Adj {           // adjacency slot (open addressing, keyed ifindex+ip)
+  uint32_t ifindex;
+  uint8_t fam, used, pad[2];
+  uint8_t addr[16];
+  uint8_t mac[6];
+  uint8_t pad2[2];
+};
+
+struct AdjMap {
+  uint64_t slots;      // Adj[mask+1]
+  uint32_t mask;
+  uint32_t count;
+};
+
+// --- classifier -----------------------------------------------------------
+// Field order: 0 src ip, 1 dst ip, 2 sport, 3 dport.  Keys are 128-bit
+// (hi, lo); v4 addresses and ports use hi = 0.
+struct FieldIdx {
+  uint64_t bounds;     // offset of uint64_t[2*n] (hi, lo) interval starts, ascending
+  uint64_t rows;       // offset of uint32_t[n] row index per interval
+  uint32_t n;          // number of intervals (>= 1; bounds[0] = 0)
+  uint32_t pad;
+};
+
+struct Group {
+  uint32_t n_rules;
+  uint32_t words;      // W = ceil(n_rules / 64)
+  uint32_t sum_words;  // S = ceil(W / 64)
+  uint32_t rule_base;  // index of rule 0 of this group in the table's rule arrays
+  uint64_t pool;       // offset of uint64_t rows[row][S + W]
+  uint64_t proto_rows; // offset of uint16_t[256]
+  FieldIdx f[4];
+};
+
+struct Classifier {
+  HashMap groups;      // (vni_a, vni_b, gate) -> group index
+  uint64_t group_recs; // Group[]
+  uint64_t action;     // uint32_t[n_rules_total]
+  uint64_t action2;    // uint32_t[n_rules_total]
+  uint64_t orig;       // uint32_t[n_rules_total] (index in the caller's array)
+  uint32_t n_groups;
+  uint32_t n_rules;
+};
+
+// --- static NAT ------------------------------------------------------------
+struct NatRange {
+  uint32_t olo_ip, ohi_ip;   // host order
+  uint16_t olo_port, ohi_port;
+  uint32_t tlo_ip, thi_ip;
+  uint16_t tlo_port, thi_port;
+  uint32_t pad;
+  uint64_t offset;
+};
+
+struct NatEnt {
+  uint32_t net;              // prefix network (host order)
+  uint8_t len, is_pat, covers_all, pad;
+  int32_t parent;            // next shorter covering entry in this table, -1
+  uint32_t first_pr, n_pr;   // uint32_t packed (lo | hi<<16)
+  uint32_t first_range, n_ranges;
+  uint64_t size;
+};
+
+struct NatTab {
+  uint64_t bounds;           // uint32_t[n] interval starts (host order)
+  uint64_t longest;          // int32_t[n] longest covering entry (global idx) or -1
+  uint32_t n;
+  uint32_t pad;
+};
+
+struct Image {
+  uint64_t bytes;
+  int64_t genid;
+  HashMap vni_fib;           // vni -> fib index
+  HashMap vrf_fib;           // vrf id -> fib index
+  uint64_t fibs;             // FibRec[]
+  uint32_t n_fibs;
+  uint32_t drop_nh;          // route nh of the default /0 drop route
+  uint64_t pt_nodes;         // PtNode[]
+  uint64_t pt_leaves;        // uint32_t[]
+  uint64_t route_nhs;        // RouteNh[]
+  uint64_t entries;          // Entry[]
+  uint64_t instrs;           // Instr[]
+  HashMap ifaces;            // ifindex -> iface record index
+  uint64_t iface_recs;       // Iface[]
+  AdjMap adjs;
+  Classifier acl[2];         // [0] v4, [1] v6
+  HashMap acl_default;       // (src_vni, dst_vni) -> action + 1
+  Classifier ff_remote[2];
+  Classifier ff_local[2];
+  HashMap nat_tabs;          // (kind, src_vni, dst_vni) -> NatTab index
+  HashMap nat_pervni;        // src_vni -> 1 (PerVniTable exists)
+  uint64_t nat_tab_recs;     // NatTab[]
+  uint64_t nat_ents;         // NatEnt[]
+  uint64_t nat_prs;          // uint32_t[]
+  uint64_t nat_ranges;       // NatRange[]
+};
+
+// 32-bit mixing hash for the open-addressing maps (host and device agree)
+__host__ __device__ inline uint32_t hmix(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t h = a * 0x9E3779B1u;
+  h ^= (b + 0x7F4A7C15u) * 0x85EBCA77u;
+  h ^= (c + 0x165667B1u) * 0xC2B2AE3Du;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return h;
+}
+
+}  // namespace dpd

@@ -1,0 +1,1350 @@
+// SPDX-License-Identifier: Apache-2.0
+//
+// MI355X (gfx950) per-burst packet pipeline kernel.
+//
+// One work-item per packet, 128-thread workgroups (2 wave64s).  Each
+// work-item stages its frame's first WIN bytes into a private LDS slab with
+// 16-byte global loads (the frame's header window; bytes beyond it are read
+// from HBM directly), walks the stage sequence of the reference router
+// pipeline (dataplane/src/packet_processor/mod.rs:130-145) against the
+// device table image (dp_device.h), and serializes the result in place:
+//  - patch mode (layout unchanged, the common case): only the changed fields
+//    are stored (MACs, TTL, addresses, ports, checksums);
+//  - rewrite mode (VXLAN encap, parse-limit quirks): the whole header stack
+//    is re-emitted from the LDS snapshot as aligned dword stores.
+// The L4 checksum is always fully recomputed over the payload, as
+// Packet::serialize does (net/src/packet/mod.rs:342-354).
+// DoneReason counts are reduced per workgroup in LDS, one atomic per bin.
+#ifdef DP_EMU
+#include DP_EMU  // tests/emu: host build of the same per-packet code (debug harness)
+#else
+#include <hip/hip_runtime.h>
+#endif
+#include <stdint.h>
+
+#include "../../include/dpgpu.h"
+#include "dp_device.h"
+
+namespace {
+
+using namespace dpd;
+
+constexpr int TPB = 128;
+constexpr int WIN = 256;          // header window bytes per packet
+constexpr int SLAB = WIN + 4;     // 65 dwords: conflict-free byte reads
+constexpr uint8_t DONE_NONE = 255;
+
+// ---------------------------------------------------------------------------
+// Image access
+// ---------------------------------------------------------------------------
+struct Img {
+  const uint8_t *base;
+  Image im;
+  template <class T> __device__ __forceinline__ const T *at(uint64_t off) const {
+    return reinterpret_cast<const T *>(base + off);
+  }
+};
+
+__device__ __forceinline__ bool hash_find(const Img &g, const HashMap &m, uint32_t k0,
+                                          uint32_t k1, uint32_t k2, uint32_t &val) {
+  if (m.count == 0) return false;
+  const HashSlot *s = g.at<HashSlot>(m.slots);
+  uint32_t key2 = k2 | 0x80000000u;
+  uint32_t i = hmix(k0, k1, k2) & m.mask;
+  for (uint32_t probe = 0; probe <= m.mask; probe++) {
+    HashSlot e = s[i];
+    if (!(e.k2 & 0x80000000u)) return false;
+    if (e.k0 == k0 && e.k1 == k1 && e.k2 == key2) { val = e.val; return true; }
+    i = (i + 1) & m.mask;
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// Frame window: byte f of the frame is slab[shift + f] if inside the window,
+// else read from HBM.
+// ---------------------------------------------------------------------------
+struct Frame {
+  uint8_t *lds;     // this work-item's slab
+  uint8_t *g;       // frame start in HBM
+  int shift;        // frame start & 15
+  int len;
+  __device__ __forceinline__ uint8_t b(int f) const {
+    int o = shift + f;
+    return o < WIN ? lds[o] : g[f];
+  }
+  __device__ __forceinline__ uint16_t be16(int f) const { return (uint16_t)((b(f) << 8) | b(f + 1)); }
+  __device__ __forceinline__ uint32_t be32(int f) const {
+    return ((uint32_t)b(f) << 24) | ((uint32_t)b(f + 1) << 16) | ((uint32_t)b(f + 2) << 8) | b(f + 3);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Parsed header stack (offsets are frame-relative)
+// ---------------------------------------------------------------------------
+enum { L4_NONE = 0, L4_TCP = 1, L4_UDP = 2, L4_ICMP4 = 3, L4_ICMP6 = 4 };
+enum { HK_NONE = 0, HK_VLAN, HK_V4, HK_V6, HK_EXT_RAW, HK_EXT_FRAG, HK_EXT_AUTH, HK_TCP, HK_UDP,
+       HK_ICMP4, HK_ICMP6, HK_VXLAN };
+
+struct Hdr {
+  int hb;           // header stack start (eth)
+  int nvlan;
+  int net;          // 0 / 4 / 6
+  int net_off, net_hlen;
+  int next;         // number of kept ext headers
+  int ext_off[3];
+  uint8_t ext_kind[3];
+  int ext_len;      // bytes of kept ext headers
+  int l4, l4_off, l4_hlen;
+  bool vx;
+  int vx_off;
+  uint32_t vni;
+  int consumed;     // bytes consumed from hb
+  int size;         // deparse size of the kept stack
+};
+
+// try to parse one header of kind `k` at frame offset `pos`; returns its
+// length (0 on failure)
+__device__ int try_parse(const Frame &F, int k, int pos, uint32_t &aux) {
+  int rem = F.len - pos;
+  switch (k) {
+    case HK_VLAN: {  // Vlan::parse: VID 0 / 4095 invalid
+      if (rem < 4) return 0;
+      uint16_t vid = F.be16(pos) & 0x0fff;
+      if (vid == 0 || vid == 4095) return 0;
+      return 4;
+    }
+    case HK_V4: {  // Ipv4HeaderSlice::from_slice + unicast source
+      if (rem < 20) return 0;
+      uint8_t v = F.b(pos);
+      if ((v >> 4) != 4) return 0;
+      int ihl = v & 0xf;
+      if (ihl < 5) return 0;
+      int hl = ihl * 4;
+      if (rem < hl) return 0;
+      if (F.be16(pos + 2) < hl) return 0;
+      uint32_t src = F.be32(pos + 12);
+      if ((src >> 28) == 0xe || src == 0xffffffffu) return 0;
+      return hl;
+    }
+    case HK_V6: {
+      if (rem < 40) return 0;
+      if ((F.b(pos) >> 4) != 6) return 0;
+      if (F.b(pos + 8) == 0xff) return 0;
+      return 40;
+    }
+    case HK_EXT_RAW: {
+      if (rem < 8) return 0;
+      int n = ((int)F.b(pos + 1) + 1) * 8;
+      return rem < n ? 0 : n;
+    }
+    case HK_EXT_FRAG: return rem < 8 ? 0 : 8;
+    case HK_EXT_AUTH: {
+      if (rem < 12) return 0;
+      uint8_t pl = F.b(pos + 1);
+      if (pl == 0) return 0;
+      int n = ((int)pl + 2) * 4;
+      return rem < n ? 0 : n;
+    }
+    case HK_TCP: {
+      if (rem < 20) return 0;
+      int doff = F.b(pos + 12) >> 4;
+      if (doff < 5 || rem < doff * 4) return 0;
+      if (F.be16(pos) == 0 || F.be16(pos + 2) == 0) return 0;
+      return doff * 4;
+    }
+    case HK_UDP: {
+      if (rem < 8) return 0;
+      if (F.be16(pos) == 0 || F.be16(pos + 2) == 0) return 0;
+      return 8;
+    }
+    case HK_ICMP4: {
+      if (rem < 8) return 0;
+      uint8_t t = F.b(pos), c = F.b(pos + 1);
+      int n = ((t == 13 || t == 14) && c == 0) ? 20 : 8;
+      return rem < n ? 0 : n;
+    }
+    case HK_ICMP6: return rem < 8 ? 0 : 8;
+    case HK_VXLAN: {
+      if (rem < 8) return 0;
+      if ((F.b(pos) & 0x08) != 0x08) return 0;
+      if (F.b(pos + 1) | F.b(pos + 2) | F.b(pos + 3) | F.b(pos + 7)) return 0;
+      uint32_t v = ((uint32_t)F.b(pos + 4) << 16) | ((uint32_t)F.b(pos + 5) << 8) | F.b(pos + 6);
+      if (v == 0) return 0;
+      aux = v;
+      return 8;
+    }
+  }
+  return 0;
+}
+
+__device__ __forceinline__ int kind_of_ethertype(uint16_t et) {
+  if (et == 0x0800) return HK_V4;
+  if (et == 0x86dd) return HK_V6;
+  if (et == 0x8100 || et == 0x9100 || et == 0x88a8) return HK_VLAN;
+  return HK_NONE;
+}
+
+// next header kind after an IP-ish header given proto, v4 / v6 context
+__device__ __forceinline__ int kind_of_proto(uint8_t p, bool v6) {
+  switch (p) {
+    case 6: return HK_TCP;
+    case 17: return HK_UDP;
+    case 1: return v6 ? HK_NONE : HK_ICMP4;
+    case 58: return v6 ? HK_ICMP6 : HK_NONE;
+    case 51: return HK_EXT_AUTH;
+    case 0: case 43: case 60: return v6 ? HK_EXT_RAW : HK_NONE;
+    case 44: return v6 ? HK_EXT_FRAG : HK_NONE;
+  }
+  return HK_NONE;
+}
+
+// Headers::parse (net/src/headers/mod.rs:474-578) incl. the MAX_VLANS /
+// MAX_NET_EXTENSIONS quirk.  Returns false if the Ethernet header is invalid.
+__device__ bool parse(const Frame &F, int hb, Hdr &H) {
+  H.hb = hb; H.nvlan = 0; H.net = 0; H.next = 0; H.ext_len = 0; H.l4 = L4_NONE;
+  H.vx = false; H.vni = 0; H.net_off = H.net_hlen = 0; H.l4_off = H.l4_hlen = 0; H.vx_off = 0;
+  int rem = F.len - hb;
+  if (rem < 14) return false;
+  uint8_t d0 = 0, s0 = F.b(hb + 6), dz = 0, sz = 0;
+  for (int i = 0; i < 6; i++) { uint8_t x = F.b(hb + i); dz |= x; if (i == 0) d0 = x; sz |= F.b(hb + 6 + i); }
+  (void)d0;
+  if (dz == 0 || sz == 0 || (s0 & 1)) return false;
+  int pos = hb + 14;
+  bool v6ctx = false;
+  uint32_t aux = 0;
+  int cur = kind_of_ethertype(F.be16(hb + 12));
+  int cur_len = cur ? try_parse(F, cur, pos, aux) : 0;
+  if (cur_len == 0) { H.consumed = pos - hb; H.size = 14; return true; }
+  int cur_pos = pos;
+  uint32_t cur_aux = aux;
+  pos += cur_len;
+  for (int guard = 0; guard < 16; guard++) {
+    // next header from cur's payload
+    int nk = HK_NONE;
+    switch (cur) {
+      case HK_VLAN: nk = kind_of_ethertype(F.be16(cur_pos + 2)); break;
+      case HK_V4: nk = kind_of_proto(F.b(cur_pos + 9), false); break;
+      case HK_V6: nk = kind_of_proto(F.b(cur_pos + 6), true); break;
+      case HK_EXT_RAW: case HK_EXT_FRAG: nk = kind_of_proto(F.b(cur_pos), true); break;
+      case HK_EXT_AUTH: {
+        uint8_t p = F.b(cur_pos);
+        if (v6ctx) nk = kind_of_proto(p, true);
+        else nk = (p == 6 || p == 17 || p == 1 || p == 51) ? kind_of_proto(p, false) : HK_NONE;
+        break;
+      }
+      case HK_UDP: nk = F.be16(cur_pos + 2) == 4789 ? HK_VXLAN : HK_NONE; break;
+      default: nk = HK_NONE;
+    }
+    uint32_t naux = 0;
+    int nlen = nk ? try_parse(F, nk, pos, naux) : 0;
+    int npos = pos;
+    if (nlen) pos += nlen;
+    bool brk = false;
+    switch (cur) {
+      case HK_VLAN: if (H.nvlan < 4) H.nvlan++; else brk = true; break;
+      case HK_V4: H.net = 4; H.net_off = cur_pos; H.net_hlen = cur_len; v6ctx = false; break;
+      case HK_V6: H.net = 6; H.net_off = cur_pos; H.net_hlen = 40; v6ctx = true; break;
+      case HK_EXT_RAW: case HK_EXT_FRAG: case HK_EXT_AUTH:
+        if (H.next < 3) {
+          H.ext_off[H.next] = cur_pos;
+          H.ext_kind[H.next] = (uint8_t)cur;
+          H.ext_len += cur_len;
+          H.next++;
+        } else brk = true;
+        break;
+      case HK_TCP: H.l4 = L4_TCP; H.l4_off = cur_pos; H.l4_hlen = cur_len; break;
+      case HK_UDP: H.l4 = L4_UDP; H.l4_off = cur_pos; H.l4_hlen = 8; break;
+      case HK_ICMP4: H.l4 = L4_ICMP4; H.l4_off = cur_pos; H.l4_hlen = cur_len; break;
+      case HK_ICMP6: H.l4 = L4_ICMP6; H.l4_off = cur_pos; H.l4_hlen = cur_len; break;
+      case HK_VXLAN: H.vx = true; H.vx_off = cur_pos; H.vni = cur_aux; break;
+    }
+    if (brk || !nlen) break;
+    cur = nk; cur_pos = npos; cur_len = nlen; cur_aux = naux;
+  }
+  H.consumed = pos - hb;
+  int sz2 = 14 + 4 * H.nvlan;
+  if (H.net) {
+    sz2 += H.net_hlen + H.ext_len;
+    if (H.l4) { sz2 += H.l4_hlen; if (H.vx) sz2 += 8; }
+  }
+  H.size = sz2;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Mutable per-packet state (values that differ from the frame bytes)
+// ---------------------------------------------------------------------------
+struct Addr16 { uint32_t w[4]; };  // network order bytes packed big-endian per word
+
+struct State {
+  uint8_t done;
+  uint32_t flags;
+  bool has_vrf;
+  uint32_t vrf;
+  uint32_t src_vni, dst_vni;
+  bool has_oif;
+  uint32_t oif;
+  bool has_nh;
+  uint8_t nh_fam;
+  Addr16 nh;
+  bool has_dscp;
+  uint8_t dscp, ecn;
+  uint32_t fib_entry, acl_rule;
+  uint8_t acl;
+  // current header field values
+  uint8_t emac[12];      // dst(6) src(6)
+  bool eth_dirty;
+  uint8_t ttl;           // v4 ttl / v6 hop limit
+  uint32_t v4src, v4dst; // host order
+  uint16_t sport, dport;
+  // encap
+  bool encap;
+  uint8_t o_fam;
+  Addr16 o_src, o_dst;
+  uint32_t o_vni;
+  uint16_t o_sport, o_len;
+  uint8_t o_tos;         // dscp<<2|ecn for the outer header
+  bool inner_l4_ck;      // inner L4 checksum recomputed at encap
+  uint16_t inner_v4_ck, inner_l4_ck_val;
+  bool o_eth;            // Egress added the outer Ethernet header
+  uint8_t o_mac[12];
+  int pay_start;         // frame-relative payload start (inner after decap)
+};
+
+__device__ __forceinline__ void done(State &S, uint8_t r) { if (S.done == DONE_NONE) S.done = r; }
+
+__device__ __forceinline__ void load_fields(const Frame &F, const Hdr &H, State &S) {
+  for (int i = 0; i < 12; i++) S.emac[i] = F.b(H.hb + i);
+  S.eth_dirty = false;
+  if (H.net == 4) {
+    S.ttl = F.b(H.net_off + 8);
+    S.v4src = F.be32(H.net_off + 12);
+    S.v4dst = F.be32(H.net_off + 16);
+  } else if (H.net == 6) {
+    S.ttl = F.b(H.net_off + 7);
+  }
+  if (H.l4 == L4_TCP || H.l4 == L4_UDP) {
+    S.sport = F.be16(H.l4_off);
+    S.dport = F.be16(H.l4_off + 2);
+  } else {
+    S.sport = S.dport = 0;
+  }
+  S.pay_start = H.hb + H.consumed;
+}
+
+__device__ __forceinline__ uint8_t net_proto(const Frame &F, const Hdr &H) {
+  return H.net == 4 ? F.b(H.net_off + 9) : F.b(H.net_off + 6);
+}
+
+__device__ __forceinline__ Addr16 addr16(const Frame &F, int off) {
+  Addr16 a;
+  for (int i = 0; i < 4; i++) a.w[i] = F.be32(off + 4 * i);
+  return a;
+}
+
+// current destination address (after NAT) as a 16-byte key
+__device__ __forceinline__ void cur_dst(const Frame &F, const Hdr &H, const State &S, uint8_t &fam, Addr16 &a) {
+  if (S.encap) { fam = S.o_fam; a = S.o_dst; return; }
+  fam = (uint8_t)H.net;
+  if (H.net == 4) { a.w[0] = S.v4dst; a.w[1] = a.w[2] = a.w[3] = 0; }
+  else a = addr16(F, H.net_off + 24);
+}
+
+__device__ __forceinline__ bool icmp_is_error(const Frame &F, const Hdr &H) {
+  if (H.l4 == L4_ICMP4) { uint8_t t = F.b(H.l4_off); return t == 3 || t == 5 || t == 11 || t == 12; }
+  if (H.l4 == L4_ICMP6) { uint8_t t = F.b(H.l4_off); return t >= 1 && t <= 4; }
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// rapidhash-style hash (same restatement as the oracle; parity vs the
+// reference is UNPINNED)
+// ---------------------------------------------------------------------------
+struct HBuf { uint8_t b[64]; int n; };
+__device__ __forceinline__ void hb_put(HBuf &h, uint8_t x) { h.b[h.n++] = x; }
+__device__ __forceinline__ void mum(uint64_t &a, uint64_t &b) {
+  uint64_t lo = a * b, hi = __umul64hi(a, b);
+  a = lo; b = hi;
+}
+__device__ __forceinline__ uint64_t mixh(uint64_t a, uint64_t b) { mum(a, b); return a ^ b; }
+__device__ __forceinline__ uint64_t rd64(const uint8_t *p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
+  return v;
+}
+__device__ __forceinline__ uint64_t rd32(const uint8_t *p) {
+  return (uint64_t)p[0] | ((uint64_t)p[1] << 8) | ((uint64_t)p[2] << 16) | ((uint64_t)p[3] << 24);
+}
+__device__ uint64_t rapid(const uint8_t *p, int len) {
+  const uint64_t s0 = 0x2d358dccaa6c78a5ull, s1 = 0x8bb84b93962eacc9ull, s2 = 0x4b33a62ed433d4a3ull;
+  uint64_t seed = 0xbdd89aa982704029ull;
+  seed ^= mixh(seed ^ s0, s1) ^ (uint64_t)len;
+  uint64_t a, b;
+  if (len <= 16) {
+    if (len >= 4) {
+      const uint8_t *pl = p + len - 4;
+      a = (rd32(p) << 32) | rd32(pl);
+      uint64_t delta = ((uint64_t)(len & 24)) >> (len >> 3);
+      b = (rd32(p + delta) << 32) | rd32(pl - delta);
+    } else if (len > 0) {
+      a = ((uint64_t)p[0] << 56) | ((uint64_t)p[len >> 1] << 32) | p[len - 1];
+      b = 0;
+    } else {
+      a = b = 0;
+    }
+  } else {
+    int i = len;
+    if (i > 48) {
+      uint64_t see1 = seed, see2 = seed;
+      while (i >= 48) {
+        seed = mixh(rd64(p) ^ s0, rd64(p + 8) ^ seed);
+        see1 = mixh(rd64(p + 16) ^ s1, rd64(p + 24) ^ see1);
+        see2 = mixh(rd64(p + 32) ^ s2, rd64(p + 40) ^ see2);
+        p += 48;
+        i -= 48;
+      }
+      seed ^= see1 ^ see2;
+    }
+    if (i > 16) {
+      seed = mixh(rd64(p) ^ s2, rd64(p + 8) ^ seed ^ s1);
+      if (i > 32) seed = mixh(rd64(p + 16) ^ s2, rd64(p + 24) ^ seed);
+    }
+    a = rd64(p + i - 16);
+    b = rd64(p + i - 8);
+  }
+  a ^= s1;
+  b ^= seed;
+  mum(a, b);
+  return mixh(a ^ s0 ^ (uint64_t)len, b ^ s1);
+}
+
+__device__ void hash_ip_fields(const Frame &F, const Hdr &H, const State &S, HBuf &h) {
+  if (H.net == 4) {
+    for (int i = 0; i < 4; i++) hb_put(h, (uint8_t)(S.v4src >> (24 - 8 * i)));
+    for (int i = 0; i < 4; i++) hb_put(h, (uint8_t)(S.v4dst >> (24 - 8 * i)));
+    hb_put(h, F.b(H.net_off + 9));
+  } else if (H.net == 6) {
+    for (int i = 0; i < 32; i++) hb_put(h, F.b(H.net_off + 8 + i));
+    hb_put(h, F.b(H.net_off + 6));
+  } else {
+    return;
+  }
+  if (H.l4 == L4_TCP || H.l4 == L4_UDP) {
+    hb_put(h, S.sport >> 8); hb_put(h, S.sport & 0xff);
+    hb_put(h, S.dport >> 8); hb_put(h, S.dport & 0xff);
+  } else if (H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) {
+    uint8_t t = F.b(H.l4_off);
+    bool echo = H.l4 == L4_ICMP4 ? (t == 0 || t == 8) : (t == 128 || t == 129);
+    if (echo) { hb_put(h, F.b(H.l4_off + 4)); hb_put(h, F.b(H.l4_off + 5)); }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LPM (Poptrie-style, see dp_tables.cpp build_poptrie)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t key_bits(const Addr16 &a, int off, int n, int width) {
+  // bits [off, off+n) of the key, zero-padded beyond `width`
+  uint32_t v = 0;
+  for (int i = 0; i < n; i++) {
+    int bit = off + i;
+    uint32_t x = 0;
+    if (bit < width) x = (a.w[bit >> 5] >> (31 - (bit & 31))) & 1;
+    v = (v << 1) | x;
+  }
+  return v;
+}
+
+__device__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
+  const uint32_t *direct = g.at<uint32_t>(L.direct);
+  uint32_t idx;
+  if (L.width == 32) idx = a.w[0] >> (32 - L.dbits);
+  else idx = a.w[0] >> (32 - L.dbits);  // dbits <= 32
+  uint32_t e = direct[idx];
+  if (e & 0x80000000u) return e & 0x7fffffffu;
+  const PtNode *nodes = g.at<PtNode>(g.im.pt_nodes);
+  const uint32_t *leaves = g.at<uint32_t>(g.im.pt_leaves);
+  int off = (int)L.dbits;
+  uint32_t ni = e;
+  for (int guard = 0; guard < 24; guard++) {
+    const PtNode &nd = nodes[ni];
+    uint64_t vec = nd.vec, lv = nd.leafvec;
+    uint32_t v = key_bits(a, off, 6, (int)L.width);
+    uint64_t bit = 1ull << v;
+    if (vec & bit) {
+      ni = nd.base1 + (uint32_t)__popcll(vec & (bit - 1));
+      off += 6;
+      continue;
+    }
+    uint64_t m = (v == 63) ? ~0ull : ((bit << 1) - 1);
+    return leaves[nd.base0 + (uint32_t)__popcll(lv & m) - 1];
+  }
+  return g.im.drop_nh;  // unreachable for a well-formed image
+}
+
+// ---------------------------------------------------------------------------
+// Classifier (bit-vector, first match)
+// ---------------------------------------------------------------------------
+struct Key128 { uint64_t hi, lo; };
+
+__device__ __forceinline__ uint32_t interval_row(const Img &g, const FieldIdx &f, Key128 k) {
+  const uint64_t *b = g.at<uint64_t>(f.bounds);
+  uint32_t lo = 0, hi = f.n;  // find last j with bounds[j] <= k
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    uint64_t bh = b[2 * mid], bl = b[2 * mid + 1];
+    bool le = bh < k.hi || (bh == k.hi && bl <= k.lo);
+    if (le) lo = mid; else hi = mid;
+  }
+  return g.at<uint32_t>(f.rows)[lo];
+}
+
+// returns global rule index or -1
+__device__ int64_t classify(const Img &g, const Classifier &C, uint32_t a, uint32_t bb, uint32_t gate,
+                            uint8_t proto, Key128 src, Key128 dst, uint16_t sp, uint16_t dp) {
+  uint32_t gi;
+  if (!hash_find(g, C.groups, a, bb, gate, gi)) return -1;
+  const Group G = g.at<Group>(C.group_recs)[gi];
+  const uint64_t *pool = g.at<uint64_t>(G.pool);
+  uint32_t stride = G.sum_words + G.words;
+  uint32_t r0 = g.at<uint16_t>(G.proto_rows)[proto];
+  uint32_t r1 = interval_row(g, G.f[0], src);
+  uint32_t r2 = interval_row(g, G.f[1], dst);
+  uint32_t r3 = interval_row(g, G.f[2], Key128{0, sp});
+  uint32_t r4 = interval_row(g, G.f[3], Key128{0, dp});
+  const uint64_t *p0 = pool + (uint64_t)r0 * stride, *p1 = pool + (uint64_t)r1 * stride;
+  const uint64_t *p2 = pool + (uint64_t)r2 * stride, *p3 = pool + (uint64_t)r3 * stride;
+  const uint64_t *p4 = pool + (uint64_t)r4 * stride;
+  for (uint32_t s = 0; s < G.sum_words; s++) {
+    uint64_t m = p0[s] & p1[s] & p2[s] & p3[s] & p4[s];
+    while (m) {
+      uint32_t w = s * 64 + (uint32_t)__ffsll((unsigned long long)m) - 1;
+      uint32_t o = G.sum_words + w;
+      uint64_t x = p0[o] & p1[o] & p2[o] & p3[o] & p4[o];
+      if (x) return (int64_t)G.rule_base + (int64_t)w * 64 + (__ffsll((unsigned long long)x) - 1);
+      m &= m - 1;
+    }
+  }
+  return -1;
+}
+
+// ---------------------------------------------------------------------------
+// Static NAT
+// ---------------------------------------------------------------------------
+__device__ bool nat_find(const Img &g, uint32_t kind, uint32_t svni, uint32_t dvni, uint32_t addr,
+                         bool has_port, uint16_t port, uint32_t &na, bool &hp, uint16_t &np) {
+  uint32_t ti;
+  if (!hash_find(g, g.im.nat_tabs, kind, svni, kind ? dvni : 0, ti)) return false;
+  const NatTab T = g.at<NatTab>(g.im.nat_tab_recs)[ti];
+  if (T.n == 0) return false;
+  const uint32_t *b = g.at<uint32_t>(T.bounds);
+  uint32_t lo = 0, hi = T.n;
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (b[mid] <= addr) lo = mid; else hi = mid;
+  }
+  int32_t ei = g.at<int32_t>(T.longest)[lo];
+  const NatEnt *ents = g.at<NatEnt>(g.im.nat_ents);
+  const uint32_t *prs = g.at<uint32_t>(g.im.nat_prs);
+  // IpPortPrefixTrie::lookup: longest matching prefix first
+  while (ei >= 0) {
+    const NatEnt &E = ents[ei];
+    bool cov = false;
+    if (has_port) {
+      if (!E.is_pat) cov = true;
+      else
+        for (uint32_t k = 0; k < E.n_pr; k++) {
+          uint32_t pr = prs[E.first_pr + k];
+          if ((pr & 0xffff) <= port && port <= (pr >> 16)) { cov = true; break; }
+        }
+    }
+    if (cov || E.covers_all) break;
+    ei = E.parent;
+  }
+  if (ei < 0) return false;
+  const NatEnt E = ents[ei];
+  const NatRange *R = g.at<NatRange>(g.im.nat_ranges) + E.first_range;
+  uint64_t ip_off = (uint64_t)(addr - E.net);
+  if (!E.is_pat) {
+    if (ip_off >= E.size) return false;
+    int sel = -1;  // last range with olo <= addr
+    uint32_t l = 0, h = E.n_ranges;
+    while (l < h) { uint32_t m = (l + h) >> 1; if (R[m].olo_ip <= addr) l = m + 1; else h = m; }
+    sel = (int)l - 1;
+    if (sel < 0 || addr > R[sel].ohi_ip) return false;
+    uint64_t o2 = ip_off - R[sel].offset;
+    uint64_t tl = (uint64_t)R[sel].thi_ip - R[sel].tlo_ip + 1;
+    if (o2 >= tl) return false;
+    na = R[sel].tlo_ip + (uint32_t)o2;
+    hp = false;
+    return true;
+  }
+  if (!has_port) return false;
+  int pk = -1;
+  for (uint32_t k = 0; k < E.n_pr; k++) {
+    uint32_t pr = prs[E.first_pr + k];
+    if ((pr & 0xffff) <= port && port <= (pr >> 16)) { pk = (int)k; break; }
+  }
+  if (pk < 0) return false;
+  uint32_t pr = prs[E.first_pr + pk];
+  uint64_t plen = (uint64_t)(pr >> 16) - (pr & 0xffff) + 1;
+  uint64_t eo = ip_off * plen + (uint64_t)(port - (pr & 0xffff));
+  if (eo >= E.size) return false;
+  uint32_t l = 0, h = E.n_ranges;
+  while (l < h) {
+    uint32_t m = (l + h) >> 1;
+    bool le = R[m].olo_ip < addr || (R[m].olo_ip == addr && R[m].olo_port <= port);
+    if (le) l = m + 1; else h = m;
+  }
+  int sel = (int)l - 1;
+  if (sel < 0) return false;
+  const NatRange RR = R[sel];
+  if (addr > RR.ohi_ip || (addr == RR.ohi_ip && port > RR.ohi_port)) return false;
+  uint64_t o2 = eo - RR.offset;
+  uint64_t tpl = (uint64_t)RR.thi_port - RR.tlo_port + 1;
+  uint64_t tip = (uint64_t)RR.thi_ip - RR.tlo_ip + 1;
+  if (o2 >= tip * tpl) return false;
+  na = RR.tlo_ip + (uint32_t)(o2 / tpl);
+  np = (uint16_t)(RR.tlo_port + (o2 % tpl));
+  if (np == 0) return false;
+  hp = true;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// One's complement sums
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t fold(uint64_t s) {
+  while (s >> 16) s = (s & 0xffff) + (s >> 16);
+  return (uint32_t)s;
+}
+__device__ __forceinline__ uint16_t bswap16(uint32_t v) { return (uint16_t)(((v & 0xff) << 8) | ((v >> 8) & 0xff)); }
+
+// Sum of the big-endian 16-bit words of frame bytes [a, e) (word pairing
+// starts at a), returned folded (not complemented).
+__device__ uint32_t sum_frame(const Frame &F, int a, int e) {
+  if (e <= a) return 0;
+  // absolute alignment: the LDS window starts 16-aligned, frame byte f sits
+  // at window position shift + f, which has the same alignment as HBM.
+  int wa = F.shift + a, we = F.shift + e;  // window coordinates
+  int d0 = wa & ~3, d1 = (we + 3) & ~3;
+  uint64_t s = 0;
+  const uint8_t *gbase = F.g - F.shift;  // 16-aligned HBM address of window pos 0
+  for (int d = d0; d < d1; d += 4) {
+    uint32_t w;
+    if (d + 4 <= WIN) w = *reinterpret_cast<const uint32_t *>(F.lds + d);
+    else {
+      // whole 16-byte chunks from HBM when possible
+      if ((d & 15) == 0 && d + 16 <= d1) {
+        uint4 q = *reinterpret_cast<const uint4 *>(gbase + d);
+        uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+        for (int k = 0; k < 4; k++) {
+          uint32_t x = ws[k];
+          int dd = d + 4 * k;
+          if (dd < wa) x &= 0xffffffffu << (8 * (wa - dd));
+          if (dd + 4 > we) x &= 0xffffffffu >> (8 * (dd + 4 - we));
+          s += x;
+        }
+        d += 12;
+        continue;
+      }
+      w = *reinterpret_cast<const uint32_t *>(gbase + d);
+    }
+    if (d < wa) w &= 0xffffffffu << (8 * (wa - d));
+    if (d + 4 > we) w &= 0xffffffffu >> (8 * (d + 4 - we));
+    s += w;
+  }
+  uint32_t le = fold(s);  // sum of little-endian words at even absolute offsets
+  return (wa & 1) ? le : bswap16(le);
+}
+
+// ---------------------------------------------------------------------------
+// Stages
+// ---------------------------------------------------------------------------
+__device__ bool find_iface(const Img &g, uint32_t ifx, Iface &out) {
+  uint32_t idx;
+  if (!hash_find(g, g.im.ifaces, ifx, 0, 0, idx)) return false;
+  out = g.at<Iface>(g.im.iface_recs)[idx];
+  return true;
+}
+
+__device__ void stage_ingress(const Img &g, const Frame &F, const Hdr &H, State &S, uint32_t iif) {
+  if (S.done != DONE_NONE) return;
+  Iface I;
+  if (!find_iface(g, iif, I)) { done(S, DP_DONE_INTERFACE_UNKNOWN); return; }
+  if (I.admin == DP_IF_DOWN) { done(S, DP_DONE_INTERFACE_ADM_DOWN); return; }
+  if (!(I.iftype == DP_IFT_ETHERNET || I.iftype == DP_IFT_DOT1Q)) { done(S, DP_DONE_INTERFACE_UNSUPPORTED); return; }
+  bool bc = true, mine = true;
+  for (int i = 0; i < 6; i++) { bc &= S.emac[i] == 0xff; mine &= S.emac[i] == I.mac[i]; }
+  if (bc) { S.flags |= DP_META_IS_L2_BCAST; done(S, DP_DONE_UNHANDLED); return; }
+  if (!mine) { done(S, DP_DONE_MAC_NOT_FOR_US); return; }
+  if (I.attach == DP_ATTACH_VRF) {
+    if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
+    S.has_vrf = true;
+    S.vrf = I.vrf_id;
+  } else if (I.attach == DP_ATTACH_BRIDGE) {
+    done(S, DP_DONE_INTERFACE_UNSUPPORTED);
+  } else {
+    done(S, DP_DONE_INTERFACE_DETACHED);
+  }
+}
+
+__device__ void decrement_ttl(State &S) {
+  if (S.ttl == 0) { done(S, DP_DONE_HOP_LIMIT_EXCEEDED); return; }
+  S.ttl--;
+  if (S.ttl == 0) done(S, DP_DONE_HOP_LIMIT_EXCEEDED);
+}
+
+// IPv4 header checksum of the current inner header (with current fields)
+__device__ uint16_t ipv4_csum(const Frame &F, const Hdr &H, const State &S) {
+  int o = H.net_off;
+  uint64_t s = 0;
+  s += ((uint32_t)F.b(o) << 8) | F.b(o + 1);
+  s += F.be16(o + 2);
+  s += F.be16(o + 4);
+  s += ((uint32_t)(F.b(o + 6) & 0x7f) << 8) | F.b(o + 7);  // reserved bit not kept
+  s += ((uint32_t)S.ttl << 8) | F.b(o + 9);
+  s += (S.v4src >> 16) + (S.v4src & 0xffff) + (S.v4dst >> 16) + (S.v4dst & 0xffff);
+  for (int i = 20; i < H.net_hlen; i += 2) s += F.be16(o + i);
+  return (uint16_t)~fold(s);
+}
+
+// Full L4 checksum of the current (inner) headers over the payload
+__device__ uint16_t l4_csum(const Frame &F, const Hdr &H, const State &S) {
+  int plen = F.len - S.pay_start;
+  uint32_t pay = sum_frame(F, S.pay_start, F.len);
+  uint64_t s = pay;
+  if (H.l4 == L4_UDP) {
+    uint16_t ulen = F.be16(H.l4_off + 4);
+    if (H.net == 4) s += (S.v4src >> 16) + (S.v4src & 0xffff) + (S.v4dst >> 16) + (S.v4dst & 0xffff) + 17 + ulen;
+    else { for (int i = 0; i < 32; i += 2) s += F.be16(H.net_off + 8 + i); s += ulen + 17; }
+    s += S.sport + S.dport + ulen;
+    uint16_t c = (uint16_t)~fold(s);
+    return c == 0 ? 0xffff : c;
+  }
+  if (H.l4 == L4_TCP) {
+    uint32_t tl = (uint32_t)H.l4_hlen + (uint32_t)plen;
+    if (H.net == 4) s += (S.v4src >> 16) + (S.v4src & 0xffff) + (S.v4dst >> 16) + (S.v4dst & 0xffff) + 6 + (tl & 0xffff);
+    else { for (int i = 0; i < 32; i += 2) s += F.be16(H.net_off + 8 + i); s += (tl >> 16) + (tl & 0xffff) + 6; }
+    int o = H.l4_off;
+    s += S.sport + S.dport;
+    s += F.be16(o + 4) + F.be16(o + 6) + F.be16(o + 8) + F.be16(o + 10);
+    s += ((uint32_t)(F.b(o + 12) & 0xf1) << 8) | F.b(o + 13);  // reserved bits not kept
+    s += F.be16(o + 14) + F.be16(o + 18);
+    for (int i = 20; i < H.l4_hlen; i += 2) s += F.be16(o + i);
+    return (uint16_t)~fold(s);
+  }
+  if (H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) {
+    int o = H.l4_off;
+    s += F.be16(o);
+    for (int i = 4; i < H.l4_hlen; i += 2) s += F.be16(o + i);
+    if (H.l4 == L4_ICMP6) {
+      uint32_t tl = (uint32_t)H.l4_hlen + (uint32_t)plen;
+      for (int i = 0; i < 32; i += 2) s += F.be16(H.net_off + 8 + i);
+      s += (tl >> 16) + (tl & 0xffff) + 58;
+    }
+    return (uint16_t)~fold(s);
+  }
+  return 0;
+}
+
+__device__ void vxlan_encap(const Img &g, const Frame &F, const Hdr &H, State &S, const Instr &in, const FibRec &fb) {
+  if (!(fb.flags & DP_FIB_VTEP_HAS_MAC)) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  if (!(in.flags & DP_INSTR_HAS_DMAC)) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  uint8_t vz = 0, dz = 0;
+  for (int i = 0; i < 6; i++) { vz |= fb.vtep_mac[i]; dz |= in.mac[i]; }
+  if (vz == 0 || (fb.vtep_mac[0] & 1)) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  for (int i = 0; i < 6; i++) S.emac[6 + i] = fb.vtep_mac[i];
+  if (dz == 0) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); S.eth_dirty = true; return; }
+  for (int i = 0; i < 6; i++) S.emac[i] = in.mac[i];
+  S.eth_dirty = true;
+  if (S.flags & DP_META_REFR_CHKSUM) {
+    if (H.net == 4) S.inner_v4_ck = ipv4_csum(F, H, S);
+    S.inner_l4_ck = (H.l4 != L4_NONE) && !H.vx;
+    if (S.inner_l4_ck) S.inner_l4_ck_val = l4_csum(F, H, S);
+    S.flags &= ~DP_META_REFR_CHKSUM;
+  } else if (H.net == 4) {
+    S.inner_v4_ck = ipv4_csum(F, H, S);
+    S.inner_l4_ck = false;
+  } else {
+    done(S, DP_DONE_INTERNAL_FAILURE);  // unreachable!() in the reference
+    return;
+  }
+  if (!(fb.flags & DP_FIB_VTEP_HAS_IP)) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  if (fb.vtep_fam == 4 && in.fam == 4) {
+    uint32_t s4 = ((uint32_t)fb.vtep_ip[0] << 24) | ((uint32_t)fb.vtep_ip[1] << 16) | ((uint32_t)fb.vtep_ip[2] << 8) | fb.vtep_ip[3];
+    if ((s4 >> 28) == 0xe || s4 == 0xffffffffu) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+    S.o_fam = 4;
+  } else if (fb.vtep_fam == 6 && in.fam == 6) {
+    if (fb.vtep_ip[0] == 0xff) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+    S.o_fam = 6;
+  } else {
+    done(S, DP_DONE_VXLAN_ENCAP_FAILURE);
+    return;
+  }
+  for (int i = 0; i < 4; i++) {
+    S.o_src.w[i] = ((uint32_t)fb.vtep_ip[4 * i] << 24) | ((uint32_t)fb.vtep_ip[4 * i + 1] << 16) | ((uint32_t)fb.vtep_ip[4 * i + 2] << 8) | fb.vtep_ip[4 * i + 3];
+    S.o_dst.w[i] = ((uint32_t)in.addr[4 * i] << 24) | ((uint32_t)in.addr[4 * i + 1] << 16) | ((uint32_t)in.addr[4 * i + 2] << 8) | in.addr[4 * i + 3];
+  }
+  if (S.o_fam == 4) { S.o_src.w[1] = S.o_src.w[2] = S.o_src.w[3] = 0; S.o_dst.w[1] = S.o_dst.w[2] = S.o_dst.w[3] = 0; }
+  // headroom check of the prepend (Packet::vxlan_encap): inner headers go
+  // right before the payload; we only fail if they would not fit at all.
+  int inner_start = S.pay_start - H.size;
+  if (inner_start < -(int)DP_HEADROOM) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  // packet_hash_vxlan over the (updated) inner headers
+  HBuf hbuf; hbuf.n = 0;
+  for (int i = 0; i < 6; i++) hb_put(hbuf, S.emac[6 + i]);
+  for (int i = 0; i < 6; i++) hb_put(hbuf, S.emac[i]);
+  hb_put(hbuf, F.b(H.hb + 12)); hb_put(hbuf, F.b(H.hb + 13));
+  for (int v = 0; v < H.nvlan; v++) {
+    uint16_t vid = F.be16(H.hb + 14 + 4 * v) & 0x0fff;
+    hb_put(hbuf, vid >> 8); hb_put(hbuf, vid & 0xff);
+  }
+  hash_ip_fields(F, H, S, hbuf);
+  uint64_t x = rapid(hbuf.b, hbuf.n);
+  S.o_sport = (uint16_t)(x % 16384 + 49152);
+  S.o_len = (uint16_t)((F.len - S.pay_start) + H.size + 16);
+  S.o_tos = S.has_dscp ? (uint8_t)((S.dscp << 2) | S.ecn) : 0;
+  S.o_vni = in.vni;
+  S.encap = true;
+  S.dst_vni = in.vni;
+}
+
+__device__ void stage_ipforward(const Img &g, const Frame &F, Hdr &H, State &S) {
+  if (S.done != DONE_NONE) return;
+  bool had_vrf = S.has_vrf;
+  uint32_t vrf0 = S.vrf;
+  uint32_t fi;
+  if (S.dst_vni) {
+    if (H.net == 0 && !S.encap) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
+    if (!hash_find(g, g.im.vni_fib, S.dst_vni, 0, 0, fi)) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
+  } else if (S.has_vrf) {
+    if (H.net == 0) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
+    if (!hash_find(g, g.im.vrf_fib, S.vrf, 0, 0, fi)) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
+  } else {
+    if (S.flags & DP_META_IS_OVERLAY) done(S, DP_DONE_INTERNAL_FAILURE);
+    return;
+  }
+  if (S.encap) { done(S, DP_DONE_INTERNAL_FAILURE); return; }  // routing an encapsulated packet again: unsupported
+  const FibRec fb = g.at<FibRec>(g.im.fibs)[fi];
+  uint8_t fam; Addr16 dst;
+  cur_dst(F, H, S, fam, dst);
+  uint32_t nhi = lpm_lookup(g, fam == 4 ? fb.v4 : fb.v6, dst);
+  const RouteNh nh = g.at<RouteNh>(g.im.route_nhs)[nhi];
+  uint32_t idx = 0;
+  if (nh.n_entries > 1) {
+    HBuf hbuf; hbuf.n = 0;
+    hash_ip_fields(F, H, S, hbuf);
+    idx = (uint32_t)(rapid(hbuf.b, hbuf.n) % nh.n_entries);
+  }
+  uint32_t ei = nh.first_entry + idx;
+  const Entry E = g.at<Entry>(g.im.entries)[ei];
+  S.fib_entry = ei;
+  const Instr *ins = g.at<Instr>(g.im.instrs) + E.first_instr;
+  bool iplocal = E.n_instr == 1 && ins[0].kind == DP_INSTR_LOCAL;
+  if (!iplocal) {
+    decrement_ttl(S);
+    if (S.done != DONE_NONE) return;
+  }
+  for (uint32_t k = 0; k < E.n_instr; k++) {
+    const Instr in = ins[k];
+    switch (in.kind) {
+      case DP_INSTR_DROP: done(S, DP_DONE_ROUTE_DROP); break;
+      case DP_INSTR_LOCAL: {
+        if (!H.vx) { done(S, DP_DONE_LOCAL); break; }
+        uint8_t tos = 0;
+        bool has_q = H.net != 0;
+        if (H.net == 4) tos = F.b(H.net_off + 1);
+        if (H.net == 6) tos = (uint8_t)(((F.b(H.net_off) & 0xf) << 4) | (F.b(H.net_off + 1) >> 4));
+        uint32_t vni = H.vni;
+        Hdr I;
+        if (!parse(F, H.hb + H.consumed, I)) { done(S, DP_DONE_VXLAN_DECAP_FAILURE); break; }
+        H = I;
+        load_fields(F, H, S);
+        if (has_q) { S.has_dscp = true; S.dscp = tos >> 2; S.ecn = tos & 3; }
+        uint32_t nf;
+        if (!hash_find(g, g.im.vni_fib, vni, 0, 0, nf)) { done(S, DP_DONE_UNROUTABLE); break; }
+        S.src_vni = vni;
+        S.has_vrf = true;
+        S.vrf = g.at<FibRec>(g.im.fibs)[nf].vrf_id;
+        S.flags |= DP_META_IS_OVERLAY;
+        break;
+      }
+      case DP_INSTR_ENCAP_VXLAN: vxlan_encap(g, F, H, S, in, fb); break;
+      case DP_INSTR_EGRESS:
+        S.has_oif = in.flags & DP_INSTR_HAS_IFINDEX;
+        S.oif = in.ifindex;
+        S.has_nh = in.flags & DP_INSTR_HAS_ADDR;
+        if (S.has_nh) {
+          S.nh_fam = in.fam;
+          for (int i = 0; i < 4; i++)
+            S.nh.w[i] = ((uint32_t)in.addr[4 * i] << 24) | ((uint32_t)in.addr[4 * i + 1] << 16) | ((uint32_t)in.addr[4 * i + 2] << 8) | in.addr[4 * i + 3];
+          if (in.fam == 4) S.nh.w[1] = S.nh.w[2] = S.nh.w[3] = 0;
+        }
+        break;
+    }
+    if (S.done != DONE_NONE) return;
+  }
+  if (S.has_vrf == had_vrf && (!had_vrf || S.vrf == vrf0)) S.has_vrf = false;
+}
+
+__device__ __forceinline__ Key128 key_of(const Frame &F, const Hdr &H, const State &S, bool src) {
+  if (H.net == 4) return Key128{0, src ? S.v4src : S.v4dst};
+  int o = H.net_off + (src ? 8 : 24);
+  Key128 k;
+  k.hi = ((uint64_t)F.be32(o) << 32) | F.be32(o + 4);
+  k.lo = ((uint64_t)F.be32(o + 8) << 32) | F.be32(o + 12);
+  return k;
+}
+
+__device__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, State &S) {
+  if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY) || S.dst_vni) return;
+  if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
+  if (!S.src_vni) { done(S, DP_DONE_UNROUTABLE); return; }
+  uint8_t proto = net_proto(F, H);
+  int t = H.net == 4 ? 0 : 1;
+  Key128 src = key_of(F, H, S, true), dst = key_of(F, H, S, false);
+  int64_t ri = classify(g, g.im.ff_remote[t], S.src_vni, 0, 0, proto, Key128{0, 0}, dst, 0, S.dport);
+  if (ri < 0) { done(S, DP_DONE_FILTERED); return; }
+  uint32_t dvni = g.at<uint32_t>(g.im.ff_remote[t].action)[ri];
+  uint32_t dnat = g.at<uint32_t>(g.im.ff_remote[t].action2)[ri];
+  int64_t li = classify(g, g.im.ff_local[t], S.src_vni, dvni, 0, proto, src, Key128{0, 0}, S.sport, 0);
+  if (li < 0) { done(S, DP_DONE_FILTERED); return; }
+  uint32_t snat = g.at<uint32_t>(g.im.ff_local[t].action)[li];
+  S.dst_vni = dvni;
+  if (snat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
+  if (dnat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_DST;
+}
+
+__device__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S) {
+  if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY)) return;
+  if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
+  if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
+  uint8_t proto = net_proto(F, H);
+  int t = H.net == 4 ? 0 : 1;
+  int64_t ri = classify(g, g.im.acl[t], S.src_vni, S.dst_vni, 0, proto, key_of(F, H, S, true),
+                        key_of(F, H, S, false), S.sport, S.dport);
+  uint32_t action;
+  if (ri >= 0) {
+    action = g.at<uint32_t>(g.im.acl[t].action)[ri];
+    S.acl_rule = g.at<uint32_t>(g.im.acl[t].orig)[ri];
+    S.acl = action == DP_ACL_DENY ? 2 : 1;
+  } else {
+    uint32_t v;
+    if (hash_find(g, g.im.acl_default, S.src_vni, S.dst_vni, 0, v)) {
+      action = v - 1;
+      S.acl = action == DP_ACL_DENY ? 4 : 3;
+    } else {
+      action = DP_ACL_ALLOW;
+      S.acl = 5;
+    }
+  }
+  if (action == DP_ACL_DENY) done(S, DP_DONE_ACL_DROPPED);
+}
+
+__device__ void stage_static_nat(const Img &g, const Frame &F, const Hdr &H, State &S) {
+  if (S.done != DONE_NONE) return;
+  if (!(S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST))) return;
+  if (S.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) return;
+  if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
+  uint32_t one;
+  if (!hash_find(g, g.im.nat_pervni, S.src_vni, 0, 0, one)) { done(S, DP_DONE_UNROUTABLE); return; }
+  if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
+  bool has_p = H.l4 == L4_TCP || H.l4 == L4_UDP;
+  bool modified = false;
+  if (S.flags & DP_META_REQ_STATIC_NAT_SRC) {
+    bool mod = false;
+    uint32_t na; bool hp; uint16_t np = 0;
+    if (H.net == 4 && nat_find(g, 1, S.src_vni, S.dst_vni, S.v4src, has_p, S.sport, na, hp, np)) {
+      if (!((na >> 28) == 0xe || na == 0xffffffffu)) {
+        if (na != S.v4src) { S.v4src = na; mod = true; }
+        if (has_p && hp && np != S.sport) { S.sport = np; mod = true; }
+      }
+    }
+    if (mod) S.flags |= DP_META_NATTED_SRC;
+    modified |= mod;
+  }
+  if (S.flags & DP_META_REQ_STATIC_NAT_DST) {
+    bool mod = false;
+    uint32_t na; bool hp; uint16_t np = 0;
+    if (H.net == 4 && nat_find(g, 0, S.src_vni, 0, S.v4dst, has_p, S.dport, na, hp, np)) {
+      if (na != S.v4dst) { S.v4dst = na; mod = true; }
+      if (has_p && hp && np != S.dport) { S.dport = np; mod = true; }
+    }
+    if (mod) S.flags |= DP_META_NATTED_DST;
+    modified |= mod;
+  }
+  if (modified) S.flags |= DP_META_REFR_CHKSUM;
+}
+
+__device__ bool adj_find(const Img &g, uint32_t oif, uint8_t fam, const Addr16 &a, uint8_t mac[6]) {
+  const AdjMap &m = g.im.adjs;
+  if (m.count == 0) return false;
+  const Adj *s = g.at<Adj>(m.slots);
+  uint32_t h = hmix(oif ^ (fam << 24), a.w[0] ^ a.w[2], a.w[1] ^ a.w[3]) & m.mask;
+  for (uint32_t probe = 0; probe <= m.mask; probe++) {
+    const Adj &e = s[h];
+    if (!e.used) return false;
+    if (e.ifindex == oif && e.fam == fam) {
+      bool eq = true;
+      int n = fam == 4 ? 4 : 16;
+      for (int i = 0; i < n; i++) eq &= e.addr[i] == (uint8_t)(a.w[i >> 2] >> (24 - 8 * (i & 3)));
+      if (eq) { for (int i = 0; i < 6; i++) mac[i] = e.mac[i]; return true; }
+    }
+    h = (h + 1) & m.mask;
+  }
+  return false;
+}
+
+__device__ void stage_egress(const Img &g, const Frame &F, const Hdr &H, State &S) {
+  if (S.done != DONE_NONE) return;
+  if (!S.has_oif) { done(S, DP_DONE_ROUTE_FAILURE); return; }
+  uint8_t fam; Addr16 a;
+  if (S.has_nh) { fam = S.nh_fam; a = S.nh; }
+  else if (S.encap || H.net) cur_dst(F, H, S, fam, a);
+  else { done(S, DP_DONE_NOT_IP); return; }
+  uint8_t dmac[6];
+  if (!adj_find(g, S.oif, fam, a, dmac)) { done(S, DP_DONE_MISS_L2_RESOLUTION); return; }
+  uint8_t z = 0;
+  for (int i = 0; i < 6; i++) z |= dmac[i];
+  if (z == 0) { done(S, DP_DONE_INVALID_DST_MAC); return; }
+  Iface I;
+  if (!find_iface(g, S.oif, I)) { done(S, DP_DONE_INTERFACE_UNKNOWN); return; }
+  if (I.admin == DP_IF_DOWN) { done(S, DP_DONE_INTERFACE_ADM_DOWN); return; }
+  if (I.oper == DP_IF_DOWN) { done(S, DP_DONE_INTERFACE_OPER_DOWN); return; }
+  if (!(I.iftype == DP_IFT_ETHERNET || I.iftype == DP_IFT_DOT1Q)) { done(S, DP_DONE_INTERFACE_UNSUPPORTED); return; }
+  if (S.encap) {
+    S.o_eth = true;
+    for (int i = 0; i < 6; i++) { S.o_mac[i] = dmac[i]; S.o_mac[6 + i] = I.mac[i]; }
+  } else {
+    for (int i = 0; i < 6; i++) { S.emac[i] = dmac[i]; S.emac[6 + i] = I.mac[i]; }
+    S.eth_dirty = true;
+  }
+  done(S, DP_DONE_DELIVERED);
+}
+
+// ---------------------------------------------------------------------------
+// Serialize
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void st8(uint8_t *p, uint8_t v) { *p = v; }
+__device__ __forceinline__ void st16be(uint8_t *p, uint16_t v) {
+  if (((uintptr_t)p & 1) == 0) *reinterpret_cast<uint16_t *>(p) = (uint16_t)((v >> 8) | (v << 8));
+  else { p[0] = v >> 8; p[1] = v & 0xff; }
+}
+__device__ __forceinline__ void st32be(uint8_t *p, uint32_t v) {
+  uint32_t s = __builtin_bswap32(v);
+  uintptr_t a = (uintptr_t)p;
+  if ((a & 3) == 0) *reinterpret_cast<uint32_t *>(p) = s;
+  else if ((a & 1) == 0) { *reinterpret_cast<uint16_t *>(p) = (uint16_t)s; *reinterpret_cast<uint16_t *>(p + 2) = (uint16_t)(s >> 16); }
+  else { p[0] = v >> 24; p[1] = (v >> 16) & 0xff; p[2] = (v >> 8) & 0xff; p[3] = v & 0xff; }
+}
+
+// Byte-stream writer for rewrite mode: accumulates bytes and flushes
+// aligned dwords; the last dword merges the untouched payload bytes.
+struct OW {
+  uint8_t *p;       // next output address
+  uint32_t acc;
+  __device__ __forceinline__ void put(uint8_t b) {
+    uintptr_t a = (uintptr_t)p;
+    int sh = (int)(a & 3);
+    if (sh == 0) acc = 0;
+    acc |= (uint32_t)b << (8 * sh);
+    if (sh == 3) *reinterpret_cast<uint32_t *>(p - 3) = acc;
+    p++;
+  }
+  __device__ __forceinline__ void put16(uint16_t v) { put(v >> 8); put(v & 0xff); }
+  __device__ __forceinline__ void put32(uint32_t v) { put(v >> 24); put((v >> 16) & 0xff); put((v >> 8) & 0xff); put(v & 0xff); }
+  // finish: the output ends where the payload starts; merge payload bytes
+  __device__ __forceinline__ void finish(const Frame &F, int pay_start) {
+    uintptr_t a = (uintptr_t)p;
+    int sh = (int)(a & 3);
+    if (sh == 0) return;
+    for (int k = sh, f = pay_start; k < 4; k++, f++) {
+      uint8_t b = f < F.len ? F.b(f) : p[k - sh];
+      acc |= (uint32_t)b << (8 * k);
+    }
+    *reinterpret_cast<uint32_t *>(p - sh) = acc;
+  }
+};
+
+// emit the inner header stack H (with current field values) via the writer
+__device__ void emit_stack(OW &w, const Frame &F, const Hdr &H, const State &S, bool v4ck_given,
+                           uint16_t v4ck, bool l4ck_given, uint16_t l4ck) {
+  for (int i = 0; i < 12; i++) w.put(S.emac[i]);
+  w.put(F.b(H.hb + 12)); w.put(F.b(H.hb + 13));
+  for (int i = 0; i < 4 * H.nvlan; i++) w.put(F.b(H.hb + 14 + i));
+  if (!H.net) return;
+  int o = H.net_off;
+  if (H.net == 4) {
+    w.put(F.b(o)); w.put(F.b(o + 1)); w.put(F.b(o + 2)); w.put(F.b(o + 3));
+    w.put(F.b(o + 4)); w.put(F.b(o + 5)); w.put(F.b(o + 6) & 0x7f); w.put(F.b(o + 7));
+    w.put(S.ttl); w.put(F.b(o + 9));
+    if (v4ck_given) w.put16(v4ck); else { w.put(F.b(o + 10)); w.put(F.b(o + 11)); }
+    w.put32(S.v4src); w.put32(S.v4dst);
+    for (int i = 20; i < H.net_hlen; i++) w.put(F.b(o + i));
+  } else {
+    for (int i = 0; i < 7; i++) w.put(F.b(o + i));
+    w.put(S.ttl);
+    for (int i = 8; i < 40; i++) w.put(F.b(o + i));
+  }
+  for (int e = 0; e < H.next; e++) {
+    int eo = H.ext_off[e];
+    int n = H.ext_kind[e] == HK_EXT_RAW ? ((int)F.b(eo + 1) + 1) * 8
+          : H.ext_kind[e] == HK_EXT_FRAG ? 8 : ((int)F.b(eo + 1) + 2) * 4;
+    for (int i = 0; i < n; i++) {
+      uint8_t b = F.b(eo + i);
+      if (H.ext_kind[e] == HK_EXT_FRAG && i == 1) b = 0;
+      if (H.ext_kind[e] == HK_EXT_FRAG && i == 3) b &= 0xf9;
+      if (H.ext_kind[e] == HK_EXT_AUTH && (i == 2 || i == 3)) b = 0;
+      w.put(b);
+    }
+  }
+  if (!H.l4) return;
+  int l = H.l4_off;
+  if (H.l4 == L4_TCP || H.l4 == L4_UDP) {
+    w.put16(S.sport); w.put16(S.dport);
+    if (H.l4 == L4_UDP) {
+      w.put(F.b(l + 4)); w.put(F.b(l + 5));
+      if (l4ck_given) w.put16(l4ck); else { w.put(F.b(l + 6)); w.put(F.b(l + 7)); }
+    } else {
+      for (int i = 4; i < 12; i++) w.put(F.b(l + i));
+      w.put(F.b(l + 12) & 0xf1); w.put(F.b(l + 13)); w.put(F.b(l + 14)); w.put(F.b(l + 15));
+      if (l4ck_given) w.put16(l4ck); else { w.put(F.b(l + 16)); w.put(F.b(l + 17)); }
+      for (int i = 18; i < H.l4_hlen; i++) w.put(F.b(l + i));
+    }
+  } else {
+    w.put(F.b(l)); w.put(F.b(l + 1));
+    if (l4ck_given) w.put16(l4ck); else { w.put(F.b(l + 2)); w.put(F.b(l + 3)); }
+    for (int i = 4; i < H.l4_hlen; i++) w.put(F.b(l + i));
+  }
+  if (H.vx) {
+    w.put(0x08); w.put(0); w.put(0); w.put(0);
+    w.put((H.vni >> 16) & 0xff); w.put((H.vni >> 8) & 0xff); w.put(H.vni & 0xff); w.put(0);
+  }
+}
+
+// Packet::serialize.  Returns the frame-relative output start.
+__device__ int serialize(const Frame &F, const Hdr &H, State &S) {
+  if (S.encap) {
+    int inner = H.size;
+    int outer = 14 + (S.o_fam == 4 ? 20 : 40) + 16;
+    int start = S.pay_start - inner - outer;
+    if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
+    OW w{F.g + start, 0};
+    // outer Ethernet (added by Egress)
+    for (int i = 0; i < 12; i++) w.put(S.o_mac[i]);
+    w.put16(S.o_fam == 4 ? 0x0800 : 0x86dd);
+    if (S.o_fam == 4) {
+      // Ipv4Header::default() + src/dst/ttl/proto + payload len + checksum
+      uint16_t tot = (uint16_t)(20 + S.o_len);
+      uint64_t s = 0x4500u | S.o_tos;
+      s += tot; s += 0x4000; s += (64u << 8) | 17;
+      s += (S.o_src.w[0] >> 16) + (S.o_src.w[0] & 0xffff) + (S.o_dst.w[0] >> 16) + (S.o_dst.w[0] & 0xffff);
+      uint16_t ck = (uint16_t)~fold(s);
+      w.put(0x45); w.put(S.o_tos); w.put16(tot); w.put16(0); w.put16(0x4000);
+      w.put(64); w.put(17); w.put16(ck); w.put32(S.o_src.w[0]); w.put32(S.o_dst.w[0]);
+    } else {
+      w.put(0x60 | (S.o_tos >> 4)); w.put((S.o_tos & 0xf) << 4); w.put(0); w.put(0);
+      w.put16(S.o_len); w.put(17); w.put(64);
+      for (int i = 0; i < 4; i++) w.put32(S.o_src.w[i]);
+      for (int i = 0; i < 4; i++) w.put32(S.o_dst.w[i]);
+    }
+    w.put16(S.o_sport); w.put16(4789); w.put16(S.o_len); w.put16(0);
+    w.put(0x08); w.put(0); w.put(0); w.put(0);
+    w.put((S.o_vni >> 16) & 0xff); w.put((S.o_vni >> 8) & 0xff); w.put(S.o_vni & 0xff); w.put(0);
+    emit_stack(w, F, H, S, H.net == 4, S.inner_v4_ck, S.inner_l4_ck, S.inner_l4_ck_val);
+    w.finish(F, S.pay_start);
+    return start;
+  }
+  // update_checksums over the current stack
+  bool v4 = H.net == 4;
+  uint16_t v4ck = v4 ? ipv4_csum(F, H, S) : 0;
+  bool l4 = H.net && H.l4 != L4_NONE && !H.vx;
+  uint16_t l4ck = l4 ? l4_csum(F, H, S) : 0;
+  int start = S.pay_start - H.size;
+  if (start == H.hb) {
+    // patch mode: layout unchanged
+    uint8_t *q = F.g + H.hb;
+    if (S.eth_dirty) {
+      if (((uintptr_t)q & 1) == 0) {
+        for (int i = 0; i < 12; i += 2) *reinterpret_cast<uint16_t *>(q + i) = (uint16_t)(S.emac[i] | (S.emac[i + 1] << 8));
+      } else {
+        for (int i = 0; i < 12; i++) q[i] = S.emac[i];
+      }
+    }
+    if (H.net == 4) {
+      uint8_t *n = F.g + H.net_off;
+      uint8_t fl = F.b(H.net_off + 6);
+      if (fl & 0x80) st8(n + 6, fl & 0x7f);
+      st8(n + 8, S.ttl);
+      st16be(n + 10, v4ck);
+      st32be(n + 12, S.v4src);
+      st32be(n + 16, S.v4dst);
+    } else if (H.net == 6) {
+      st8(F.g + H.net_off + 7, S.ttl);
+    }
+    for (int e = 0; e < H.next; e++) {
+      uint8_t *x = F.g + H.ext_off[e];
+      if (H.ext_kind[e] == HK_EXT_FRAG) { st8(x + 1, 0); st8(x + 3, F.b(H.ext_off[e] + 3) & 0xf9); }
+      if (H.ext_kind[e] == HK_EXT_AUTH) { st8(x + 2, 0); st8(x + 3, 0); }
+    }
+    if (H.net && H.l4) {
+      uint8_t *l = F.g + H.l4_off;
+      if (H.l4 == L4_TCP || H.l4 == L4_UDP) { st16be(l, S.sport); st16be(l + 2, S.dport); }
+      if (H.l4 == L4_TCP) { uint8_t x = F.b(H.l4_off + 12); if (x & 0x0e) st8(l + 12, x & 0xf1); }
+      if (l4) {
+        if (H.l4 == L4_UDP) st16be(l + 6, l4ck);
+        else if (H.l4 == L4_TCP) st16be(l + 16, l4ck);
+        else st16be(l + 2, l4ck);
+      }
+      if (H.vx) { uint8_t *v = F.g + H.vx_off; if (F.b(H.vx_off) != 0x08) st8(v, 0x08); }
+    }
+    return start;
+  }
+  // rewrite mode (parse-limit quirk): re-emit the kept stack before the payload
+  if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
+  OW w{F.g + start, 0};
+  emit_stack(w, F, H, S, v4, v4ck, l4, l4ck);
+  w.finish(F, S.pay_start);
+  return start;
+}
+
+// ---------------------------------------------------------------------------
+// Per-packet body
+// ---------------------------------------------------------------------------
+__device__ uint8_t process_packet(const Img &g, uint8_t *slab, uint8_t *buf, uint64_t buf_bytes,
+                                  const dp_pkt_in_t &pin, dp_pkt_out_t &o) {
+  if (pin.off < DP_HEADROOM || (((uint64_t)pin.off + pin.len + 15) & ~15ull) > buf_bytes) {
+    // layout contract violated: never touch memory outside the buffer
+    o.off = pin.off; o.len = pin.len; o.done = DP_DONE_INTERNAL_FAILURE; o.acl = 0;
+    o.meta_flags = 0; o.oif = 0; o.dst_vni = 0; o.src_vni = 0;
+    o.fib_entry = 0xffffffffu; o.acl_rule = 0xffffffffu;
+    return o.done;
+  }
+  Frame F;
+  F.lds = slab;
+  F.g = buf + pin.off;
+  F.shift = (int)(pin.off & 15);
+  F.len = pin.len;
+  // stage the header window: 16-byte loads, stored as 4 dword LDS writes
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(buf + (pin.off & ~15u));
+    int nchunk = (F.shift + F.len + 15) >> 4;
+    if (nchunk > WIN / 16) nchunk = WIN / 16;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(F.lds);
+    for (int c = 0; c < nchunk; c++) {
+      uint4 q = src[c];
+      dst[4 * c] = q.x; dst[4 * c + 1] = q.y; dst[4 * c + 2] = q.z; dst[4 * c + 3] = q.w;
+    }
+  }
+  o.off = pin.off; o.len = pin.len; o.acl = 0; o.oif = 0; o.dst_vni = 0; o.src_vni = 0;
+  o.fib_entry = 0xffffffffu; o.acl_rule = 0xffffffffu;
+  Hdr H;
+  if (!parse(F, 0, H)) {
+    o.done = DP_DONE_NOT_ETHERNET;
+    o.meta_flags = 0;
+    return o.done;
+  }
+  State S;
+  S.done = DONE_NONE;
+  S.flags = DP_META_INITIALIZED | DP_META_KEEP;
+  S.has_vrf = false; S.vrf = 0; S.src_vni = 0; S.dst_vni = 0;
+  S.has_oif = false; S.oif = 0; S.has_nh = false; S.nh_fam = 0;
+  S.has_dscp = false; S.dscp = S.ecn = 0;
+  S.fib_entry = 0xffffffffu; S.acl_rule = 0xffffffffu; S.acl = 0;
+  S.encap = false; S.o_eth = false; S.inner_l4_ck = false; S.inner_v4_ck = 0; S.inner_l4_ck_val = 0;
+  S.ttl = 0; S.v4src = S.v4dst = 0;
+  load_fields(F, H, S);
+  if (pin.flags & DP_IN_SEEDED_OVERLAY) {
+    uint32_t fi;
+    if (!hash_find(g, g.im.vni_fib, pin.src_vni, 0, 0, fi)) done(S, DP_DONE_UNROUTABLE);
+    else {
+      S.src_vni = pin.src_vni;
+      S.has_vrf = true;
+      S.vrf = g.at<FibRec>(g.im.fibs)[fi].vrf_id;
+      S.flags |= DP_META_IS_OVERLAY;
+    }
+  } else {
+    stage_ingress(g, F, H, S, pin.iif);
+    stage_ipforward(g, F, H, S);  // IP-Forward-1
+  }
+  // IcmpErrorHandler: overlay ICMP errors need flow state (outside the slice)
+  if (S.done == DONE_NONE && (S.flags & DP_META_IS_OVERLAY) && icmp_is_error(F, H)) done(S, DP_DONE_UNHANDLED);
+  stage_flow_filter(g, F, H, S);
+  stage_acl(g, F, H, S);
+  stage_static_nat(g, F, H, S);
+  stage_ipforward(g, F, H, S);  // IP-Forward-2
+  stage_egress(g, F, H, S);
+  if (S.done == DP_DONE_DELIVERED) {
+    if (!S.encap && icmp_is_error(F, H)) S.done = DP_DONE_UNHANDLED;
+    else {
+      int st = serialize(F, H, S);
+      S.flags &= ~DP_META_REFR_CHKSUM;
+      if (S.done == DP_DONE_DELIVERED) {
+        o.off = (uint32_t)((int)pin.off + st);
+        o.len = (uint16_t)(F.len - st);
+      }
+    }
+  }
+  o.done = S.done;
+  o.meta_flags = S.flags;
+  o.oif = S.has_oif ? S.oif : 0;
+  o.dst_vni = S.dst_vni;
+  o.src_vni = S.src_vni;
+  o.fib_entry = S.fib_entry;
+  o.acl_rule = S.acl_rule;
+  o.acl = S.acl;
+  return o.done;
+}
+
+#ifndef DP_EMU
+// ---------------------------------------------------------------------------
+// Kernel
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(TPB)
+dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__restrict__ buf,
+                   uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
+                   dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) uint8_t slab_all[TPB * SLAB];
+  __shared__ uint32_t hist[DP_DONE_COUNT + 1];
+  const int tid = threadIdx.x;
+  if (tid < DP_DONE_COUNT + 1) hist[tid] = 0;
+  const uint32_t i = blockIdx.x * TPB + tid;
+  uint8_t done_code = DONE_NONE;
+  if (i < n) {
+    Img g{img_base, im};
+    const dp_pkt_in_t pin = in[i];
+    dp_pkt_out_t o;
+    done_code = process_packet(g, slab_all + tid * SLAB, buf, buf_bytes, pin, o);
+    out[i] = o;
+  }
+  __syncthreads();
+  if (i < n && done_code < DP_DONE_COUNT) atomicAdd(&hist[done_code], 1u);
+  __syncthreads();
+  if (stats && tid < DP_DONE_COUNT && hist[tid]) atomicAdd(&stats[tid], (unsigned long long)hist[tid]);
+}
+#endif
+
+}  // namespace
+
+#ifdef DP_EMU
+// Host emulation entry (tests/emu only): runs the per-packet body serially.
+extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
+                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n) {
+  static uint8_t slab[SLAB + 16];
+  Img g{img_base, *reinterpret_cast<const Image *>(image_struct)};
+  for (uint32_t i = 0; i < n; i++) process_packet(g, slab, buf, buf_bytes, in[i], out[i]);
+}
+#else
+// Launch wrapper used by the runtime (dp_runtime.cpp).
+extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
+                                   uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
+                                   uint32_t n, uint64_t *stats, hipStream_t stream) {
+  if (n == 0) return 0;
+  Image im = *reinterpret_cast<const Image *>(image_struct);
+  uint32_t blocks = (n + TPB - 1) / TPB;
+  hipLaunchKernelGGL(dp_pipeline_kernel, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
+                     buf_bytes, in, out, n, reinterpret_cast<unsigned long long *>(stats));
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+#endif

@@ -1,0 +1,662 @@
+// SPDX-License-Identifier: Apache-2.0
+//
+// Host table compiler: lowers the dp_tables_desc_t arrays (include/dpgpu.h)
+// into the device table image (dp_device.h).  Runs on the publishing
+// (mgmt) thread; the result is uploaded once per generation.
+//
+// Semantics preserved from the reference builders:
+//  - Fib::default() installs /0 -> drop for v4 and v6 unless a /0 route is
+//    given (routing/src/fib/fibtype.rs:76-91); inserting a prefix twice keeps
+//    the last value (PrefixMap::insert).
+//  - Flow-filter tables match in stable descending-priority order
+//    (flow-filter/src/context/tables.rs:373-380); ACL tables in array order
+//    (acl-filter/src/context.rs:447-452).
+//  - NAT tables: IpPortPrefixTrie keyed by prefix, last insert wins
+//    (nat/src/static_nat/setup/mod.rs:73-95).
+#include "dp_tables.h"
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace dpd {
+namespace {
+
+typedef unsigned __int128 u128;
+
+struct ImgBuf {
+  std::vector<uint8_t> b;
+  uint64_t alloc(uint64_t n, uint64_t align = 16) {
+    uint64_t o = (b.size() + align - 1) & ~(align - 1);
+    b.resize(o + (n ? n : align), 0);
+    return o;
+  }
+  template <class T> uint64_t put(const std::vector<T> &v) {
+    uint64_t o = alloc(sizeof(T) * v.size(), alignof(T) < 16 ? 16 : alignof(T));
+    if (!v.empty()) memcpy(b.data() + o, v.data(), sizeof(T) * v.size());
+    return o;
+  }
+};
+
+inline uint32_t be32(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+inline bool bit_at(const uint8_t *a, int i) { return (a[i >> 3] >> (7 - (i & 7))) & 1; }
+
+bool valid_prefix(const dp_prefix_t &p) {
+  if (p.family != 4 && p.family != 6) return false;
+  int bits = p.family == 4 ? 32 : 128;
+  if (p.len > bits) return false;
+  for (int i = p.len; i < bits; i++)
+    if (bit_at(p.addr, i)) return false;
+  return true;
+}
+
+// 128-bit key, MSB-aligned (bit 0 of the address is the top bit)
+u128 key128(uint8_t fam, const uint8_t *a) {
+  u128 k = 0;
+  int n = fam == 4 ? 4 : 16;
+  for (int i = 0; i < n; i++) k = (k << 8) | a[i];
+  if (fam == 4) k <<= 96;
+  return k;
+}
+
+// ------------------------------------------------------------------ hashing
+struct KV { uint32_t k0, k1, k2, v; };
+
+HashMap build_hash(ImgBuf &ib, const std::vector<KV> &kv) {
+  HashMap m{};
+  if (kv.empty()) { m.slots = ib.alloc(sizeof(HashSlot)); m.mask = 0; m.count = 0; return m; }
+  uint32_t cap = 2;
+  while (cap < 2 * kv.size()) cap <<= 1;
+  std::vector<HashSlot> s(cap);
+  memset(s.data(), 0, sizeof(HashSlot) * cap);
+  uint32_t count = 0;
+  for (auto &e : kv) {
+    uint32_t i = hmix(e.k0, e.k1, e.k2) & (cap - 1);
+    uint32_t key2 = e.k2 | 0x80000000u;
+    for (;;) {
+      if (!(s[i].k2 & 0x80000000u)) { s[i] = HashSlot{e.k0, e.k1, key2, e.v}; count++; break; }
+      if (s[i].k0 == e.k0 && s[i].k1 == e.k1 && s[i].k2 == key2) { s[i].val = e.v; break; }
+      i = (i + 1) & (cap - 1);
+    }
+  }
+  m.slots = ib.put(s);
+  m.mask = cap - 1;
+  m.count = count;
+  return m;
+}
+
+// ------------------------------------------------------------------ poptrie
+struct PRoute { u128 key; int len; uint32_t nh; };
+
+inline uint32_t kbits(u128 k, int off, int nb) {
+  if (off >= 128) return 0;
+  return (uint32_t)((k << off) >> (128 - nb));
+}
+
+struct PtBuilder {
+  std::vector<PtNode> nodes;
+  std::vector<uint32_t> leaves;
+
+  void build_node(uint32_t idx, const PRoute *r, size_t n, uint32_t d, int off) {
+    uint32_t slot[64];
+    for (int v = 0; v < 64; v++) slot[v] = d;
+    std::vector<const PRoute *> shortr;
+    for (size_t i = 0; i < n; i++)
+      if (r[i].len <= off + 6) shortr.push_back(&r[i]);
+    std::stable_sort(shortr.begin(), shortr.end(),
+                     [](const PRoute *a, const PRoute *b) { return a->len < b->len; });
+    for (auto *p : shortr) {
+      int L = p->len - off;  // 1..6
+      uint32_t v0 = kbits(p->key, off, 6) & ~((1u << (6 - L)) - 1);
+      for (uint32_t v = v0; v < v0 + (1u << (6 - L)); v++) slot[v] = p->nh;
+    }
+    uint64_t vec = 0;
+    // long routes grouped by slot (r sorted by key -> contiguous)
+    size_t gbeg[64], gend[64];
+    for (int v = 0; v < 64; v++) gbeg[v] = gend[v] = 0;
+    for (size_t i = 0; i < n; i++) {
+      if (r[i].len <= off + 6) continue;
+      uint32_t v = kbits(r[i].key, off, 6);
+      if (!(vec & (1ull << v))) { vec |= 1ull << v; gbeg[v] = i; }
+      gend[v] = i + 1;
+    }
+    uint32_t nchild = (uint32_t)__builtin_popcountll(vec);
+    uint32_t base1 = (uint32_t)nodes.size();
+    nodes.resize(nodes.size() + nchild);
+    uint32_t base0 = (uint32_t)leaves.size();
+    uint64_t leafvec = 0;
+    bool first = true;
+    uint32_t prev = 0;
+    for (int v = 0; v < 64; v++) {
+      if (vec & (1ull << v)) continue;
+      if (first || slot[v] != prev) {
+        leafvec |= 1ull << v;
+        leaves.push_back(slot[v]);
+        prev = slot[v];
+        first = false;
+      }
+    }
+    nodes[idx] = PtNode{vec, leafvec, base1, base0, 0};
+    uint32_t k = 0;
+    for (int v = 0; v < 64; v++) {
+      if (!(vec & (1ull << v))) continue;
+      // routes in [gbeg, gend) with len > off+6 (short ones may interleave)
+      std::vector<PRoute> sub;
+      for (size_t i = gbeg[v]; i < gend[v]; i++)
+        if (r[i].len > off + 6) sub.push_back(r[i]);
+      build_node(base1 + k, sub.data(), sub.size(), slot[v], off + 6);
+      k++;
+    }
+  }
+};
+
+// Build one FIB/family LPM; routes must include a /0.
+Lpm build_lpm(ImgBuf &ib, PtBuilder &pb, std::vector<PRoute> &routes, int width, uint32_t dbits) {
+  // sort by (key, len), keep the last insert of a duplicate prefix
+  std::stable_sort(routes.begin(), routes.end(), [](const PRoute &a, const PRoute &b) {
+    if (a.key != b.key) return a.key < b.key;
+    return a.len < b.len;
+  });
+  std::vector<PRoute> uniq;
+  for (size_t i = 0; i < routes.size(); i++) {
+    if (!uniq.empty() && uniq.back().key == routes[i].key && uniq.back().len == routes[i].len)
+      uniq.back() = routes[i];
+    else
+      uniq.push_back(routes[i]);
+  }
+  std::vector<uint32_t> direct((size_t)1 << dbits, 0);
+  std::vector<uint32_t> dval((size_t)1 << dbits, 0);
+  // paint short routes in increasing length
+  std::vector<const PRoute *> shortr;
+  for (auto &r : uniq)
+    if (r.len <= (int)dbits) shortr.push_back(&r);
+  std::stable_sort(shortr.begin(), shortr.end(),
+                   [](const PRoute *a, const PRoute *b) { return a->len < b->len; });
+  for (auto *p : shortr) {
+    uint64_t s0 = kbits(p->key, 0, dbits) & ~(((uint64_t)1 << (dbits - p->len)) - 1);
+    uint64_t cnt = (uint64_t)1 << (dbits - p->len);
+    std::fill(dval.begin() + s0, dval.begin() + s0 + cnt, p->nh);
+  }
+  for (size_t s = 0; s < dval.size(); s++) direct[s] = 0x80000000u | dval[s];
+  // long routes: one node per direct slot
+  size_t i = 0;
+  while (i < uniq.size()) {
+    if (uniq[i].len <= (int)dbits) { i++; continue; }
+    uint32_t s = kbits(uniq[i].key, 0, dbits);
+    std::vector<PRoute> sub;
+    size_t j = i;
+    while (j < uniq.size() && kbits(uniq[j].key, 0, dbits) == s) {
+      if (uniq[j].len > (int)dbits) sub.push_back(uniq[j]);
+      j++;
+    }
+    uint32_t idx = (uint32_t)pb.nodes.size();
+    pb.nodes.emplace_back();
+    pb.build_node(idx, sub.data(), sub.size(), dval[s], (int)dbits);
+    direct[s] = idx;
+    i = j;
+  }
+  Lpm L{};
+  L.direct = ib.put(direct);
+  L.dbits = dbits;
+  L.width = (uint32_t)width;
+  return L;
+}
+
+// ------------------------------------------------------------- classifier
+struct CRule { dp_rule_t r; uint32_t orig; };
+
+struct Iv { u128 lo, hi; };  // inclusive
+
+Iv prefix_iv(const dp_prefix_t &p, int fam) {
+  int w = fam == 4 ? 32 : 128;
+  u128 k = key128(fam, p.addr);
+  if (fam == 4) k >>= 96;
+  u128 span = p.len == w ? (u128)0 : ((w == 128 && p.len == 0) ? ~(u128)0 : (((u128)1 << (w - p.len)) - 1));
+  return Iv{k, k + span};
+}
+
+Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam) {
+  Classifier C{};
+  // groups in first-appearance order, rules keep their match order
+  std::vector<std::vector<uint32_t>> groups;
+  std::vector<KV> gkv;
+  std::unordered_map<std::string, uint32_t> gidx;
+  for (uint32_t i = 0; i < rules.size(); i++) {
+    const dp_rule_t &r = rules[i].r;
+    std::string k((const char *)&r.vni_a, 4);
+    k.append((const char *)&r.vni_b, 4);
+    k.push_back((char)r.gate);
+    auto it = gidx.find(k);
+    if (it == gidx.end()) {
+      uint32_t g = (uint32_t)groups.size();
+      gidx[k] = g;
+      groups.emplace_back();
+      gkv.push_back(KV{r.vni_a, r.vni_b, r.gate, g});
+      it = gidx.find(k);
+    }
+    groups[it->second].push_back(i);
+  }
+  std::vector<uint32_t> action, action2, orig;
+  std::vector<Group> grecs;
+  for (auto &gr : groups) {
+    Group G{};
+    uint32_t n = (uint32_t)gr.size();
+    G.n_rules = n;
+    G.words = (n + 63) / 64;
+    G.sum_words = (G.words + 63) / 64;
+    G.rule_base = (uint32_t)action.size();
+    for (uint32_t ri : gr) {
+      action.push_back(rules[ri].r.action);
+      action2.push_back(rules[ri].r.action2);
+      orig.push_back(rules[ri].orig);
+    }
+    uint32_t W = G.words, S = G.sum_words;
+    std::vector<uint64_t> pool;
+    std::unordered_map<std::string, uint32_t> rowid;
+    auto add_row = [&](const std::vector<uint64_t> &bv) -> uint32_t {
+      std::string key((const char *)bv.data(), bv.size() * 8);
+      auto it = rowid.find(key);
+      if (it != rowid.end()) return it->second;
+      uint32_t id = (uint32_t)(pool.size() / (S + W));
+      for (uint32_t s = 0; s < S; s++) {
+        uint64_t m = 0;
+        for (uint32_t w = s * 64; w < std::min(W, s * 64 + 64); w++)
+          if (bv[w]) m |= 1ull << (w - s * 64);
+        pool.push_back(m);
+      }
+      pool.insert(pool.end(), bv.begin(), bv.end());
+      rowid[key] = id;
+      return id;
+    };
+    // protocol (Mask predicate)
+    std::vector<uint16_t> prow(256);
+    for (int p = 0; p < 256; p++) {
+      std::vector<uint64_t> bv(W, 0);
+      for (uint32_t j = 0; j < n; j++) {
+        const dp_rule_t &r = rules[gr[j]].r;
+        if ((p & r.proto_mask) == (r.proto_val & r.proto_mask)) bv[j >> 6] |= 1ull << (j & 63);
+      }
+      prow[p] = (uint16_t)add_row(bv);
+    }
+    // four interval fields
+    for (int f = 0; f < 4; f++) {
+      u128 maxv = f >= 2 ? (u128)65535 : (fam == 4 ? (u128)0xffffffffu : ~(u128)0);
+      std::vector<Iv> iv(n);
+      for (uint32_t j = 0; j < n; j++) {
+        const dp_rule_t &r = rules[gr[j]].r;
+        if (f == 0) iv[j] = prefix_iv(r.src, fam);
+        else if (f == 1) iv[j] = prefix_iv(r.dst, fam);
+        else if (f == 2) iv[j] = Iv{r.sport_lo, r.sport_hi};
+        else iv[j] = Iv{r.dport_lo, r.dport_hi};
+      }
+      std::vector<u128> bnd;
+      bnd.push_back(0);
+      for (auto &x : iv) {
+        if (x.lo > x.hi) continue;  // empty range: never matches
+        bnd.push_back(x.lo);
+        if (x.hi < maxv) bnd.push_back(x.hi + 1);
+      }
+      std::sort(bnd.begin(), bnd.end());
+      bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+      size_t m = bnd.size();
+      std::vector<std::vector<uint32_t>> adds(m + 1), dels(m + 1);
+      for (uint32_t j = 0; j < n; j++) {
+        if (iv[j].lo > iv[j].hi) continue;
+        size_t s = std::lower_bound(bnd.begin(), bnd.end(), iv[j].lo) - bnd.begin();
+        size_t e = iv[j].hi < maxv ? (size_t)(std::lower_bound(bnd.begin(), bnd.end(), iv[j].hi + 1) - bnd.begin()) : m;
+        adds[s].push_back(j);
+        dels[e].push_back(j);
+      }
+      std::vector<uint64_t> cur(W, 0);
+      std::vector<uint64_t> bounds;
+      std::vector<uint32_t> rows;
+      for (size_t k = 0; k < m; k++) {
+        for (uint32_t j : dels[k]) cur[j >> 6] &= ~(1ull << (j & 63));
+        for (uint32_t j : adds[k]) cur[j >> 6] |= 1ull << (j & 63);
+        bounds.push_back((uint64_t)(bnd[k] >> 64));
+        bounds.push_back((uint64_t)bnd[k]);
+        rows.push_back(add_row(cur));
+      }
+      G.f[f].bounds = ib.put(bounds);
+      G.f[f].rows = ib.put(rows);
+      G.f[f].n = (uint32_t)m;
+    }
+    G.proto_rows = ib.put(prow);
+    G.pool = ib.put(pool);
+    grecs.push_back(G);
+  }
+  C.groups = build_hash(ib, gkv);
+  C.group_recs = ib.put(grecs);
+  C.action = ib.put(action);
+  C.action2 = ib.put(action2);
+  C.orig = ib.put(orig);
+  C.n_groups = (uint32_t)grecs.size();
+  C.n_rules = (uint32_t)action.size();
+  return C;
+}
+
+int load_rules(const dp_rule_t *rs, uint32_t n, int fam, bool by_prio, int kind,
+               std::vector<CRule> &out) {
+  for (uint32_t i = 0; i < n; i++) {
+    const dp_rule_t &r = rs[i];
+    if (!valid_prefix(r.src) || !valid_prefix(r.dst)) return DP_EINVAL;
+    if (r.src.family != fam || r.dst.family != fam) return DP_EINVAL;
+    if (kind == 0 && r.gate != 0) return DP_EINVAL;                      // ACL
+    if (kind == 1) {                                                      // FF remote
+      if (r.src.len != 0 || r.sport_lo != 0 || r.sport_hi != 65535 || r.gate != 0) return DP_EINVAL;
+      if (r.action2 == DP_NAT_MASQUERADE || r.action2 == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
+    }
+    if (kind == 2) {                                                      // FF local
+      if (r.dst.len != 0 || r.dport_lo != 0 || r.dport_hi != 65535) return DP_EINVAL;
+      if (r.action == DP_NAT_MASQUERADE || r.action == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
+    }
+    out.push_back(CRule{r, i});
+  }
+  if (by_prio)
+    std::stable_sort(out.begin(), out.end(),
+                     [](const CRule &a, const CRule &b) { return a.r.priority > b.r.priority; });
+  return 0;
+}
+
+}  // namespace
+
+int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
+  if (!d || d->abi_version != DPGPU_ABI_VERSION) return DP_EINVAL;
+  ImgBuf ib;
+  ib.alloc(64);  // offset 0 is never a valid structure
+  Image im{};
+  im.genid = d->genid;
+
+  // --- FIB objects
+  for (uint32_t i = 0; i < d->n_entries; i++) {
+    const dp_fib_entry_t &e = d->entries[i];
+    if (e.n_instr == 0 || e.n_instr > DPD_MAX_INSTR || (uint64_t)e.first_instr + e.n_instr > d->n_instrs) return DP_EINVAL;
+    int encaps = 0;
+    for (uint32_t k = 0; k < e.n_instr; k++) {
+      uint32_t kd = d->instrs[e.first_instr + k].kind;
+      if (kd > DP_INSTR_EGRESS) return DP_EINVAL;
+      if (encaps && (kd == DP_INSTR_LOCAL || kd == DP_INSTR_ENCAP_VXLAN)) return DP_ENOTSUP;
+      if (kd == DP_INSTR_ENCAP_VXLAN) encaps++;
+    }
+  }
+  for (uint32_t i = 0; i < d->n_route_nhs; i++) {
+    const dp_route_nh_t &n = d->route_nhs[i];
+    if (n.n_entries == 0 || (uint64_t)n.first_entry + n.n_entries > d->n_entries) return DP_EINVAL;
+  }
+  std::vector<Instr> instrs;
+  for (uint32_t i = 0; i < d->n_instrs; i++) {
+    const dp_instr_t &s = d->instrs[i];
+    Instr x{};
+    x.kind = (uint8_t)s.kind;
+    x.flags = (uint8_t)s.flags;
+    x.fam = s.addr.family;
+    x.ifindex = s.ifindex;
+    x.vni = s.vni;
+    memcpy(x.mac, s.mac, 6);
+    memcpy(x.addr, s.addr.addr, s.addr.family == 6 ? 16 : 4);
+    instrs.push_back(x);
+  }
+  std::vector<Entry> entries;
+  for (uint32_t i = 0; i < d->n_entries; i++) entries.push_back(Entry{d->entries[i].first_instr, d->entries[i].n_instr});
+  std::vector<RouteNh> nhs;
+  for (uint32_t i = 0; i < d->n_route_nhs; i++) nhs.push_back(RouteNh{d->route_nhs[i].first_entry, d->route_nhs[i].n_entries});
+  // default drop route object
+  Instr drop{};
+  drop.kind = DP_INSTR_DROP;
+  instrs.push_back(drop);
+  entries.push_back(Entry{(uint32_t)instrs.size() - 1, 1});
+  nhs.push_back(RouteNh{(uint32_t)entries.size() - 1, 1});
+  uint32_t drop_nh = (uint32_t)nhs.size() - 1;
+  im.drop_nh = drop_nh;
+
+  // routes per fib / family
+  std::vector<std::vector<PRoute>> r4(d->n_fibs), r6(d->n_fibs);
+  for (uint32_t f = 0; f < d->n_fibs; f++) {
+    r4[f].push_back(PRoute{0, 0, drop_nh});
+    r6[f].push_back(PRoute{0, 0, drop_nh});
+  }
+  for (uint64_t i = 0; i < d->n_routes; i++) {
+    const dp_route_t &r = d->routes[i];
+    if (r.fib >= d->n_fibs || r.nh >= d->n_route_nhs || !valid_prefix(r.prefix)) return DP_EINVAL;
+    PRoute p{key128(r.prefix.family, r.prefix.addr), r.prefix.len, r.nh};
+    (r.prefix.family == 4 ? r4 : r6)[r.fib].push_back(p);
+  }
+  PtBuilder pb;
+  std::vector<FibRec> fibs;
+  std::vector<KV> vrfkv, vnikv;
+  for (uint32_t f = 0; f < d->n_fibs; f++) {
+    const dp_fib_t &s = d->fibs[f];
+    FibRec fr{};
+    fr.vrf_id = s.vrf_id;
+    fr.flags = s.flags;
+    fr.vtep_fam = s.vtep_ip.family;
+    memcpy(fr.vtep_mac, s.vtep_mac, 6);
+    memcpy(fr.vtep_ip, s.vtep_ip.addr, s.vtep_ip.family == 6 ? 16 : 4);
+    uint32_t d4 = r4[f].size() > 65536 ? 24 : 16;
+    fr.v4 = build_lpm(ib, pb, r4[f], 32, d4);
+    fr.v6 = build_lpm(ib, pb, r6[f], 128, 16);
+    fibs.push_back(fr);
+    vrfkv.push_back(KV{s.vrf_id, 0, 0, f});
+  }
+  for (uint32_t i = 0; i < d->n_vni_fibs; i++) {
+    if (d->vni_fibs[i].fib >= d->n_fibs) return DP_EINVAL;
+    vnikv.push_back(KV{d->vni_fibs[i].vni, 0, 0, d->vni_fibs[i].fib});
+  }
+  if (pb.nodes.empty()) pb.nodes.emplace_back();
+  if (pb.leaves.empty()) pb.leaves.push_back(drop_nh);
+  im.pt_nodes = ib.put(pb.nodes);
+  im.pt_leaves = ib.put(pb.leaves);
+  im.fibs = ib.put(fibs);
+  im.n_fibs = d->n_fibs;
+  im.vrf_fib = build_hash(ib, vrfkv);
+  im.vni_fib = build_hash(ib, vnikv);
+  im.route_nhs = ib.put(nhs);
+  im.entries = ib.put(entries);
+  im.instrs = ib.put(instrs);
+
+  // --- interfaces / adjacencies
+  std::vector<Iface> ifs;
+  std::vector<KV> ifkv;
+  for (uint32_t i = 0; i < d->n_ifaces; i++) {
+    const dp_iface_t &s = d->ifaces[i];
+    Iface x{};
+    x.ifindex = s.ifindex;
+    x.admin = s.admin_state;
+    x.oper = s.oper_state;
+    x.iftype = s.iftype;
+    x.attach = s.attach;
+    x.vrf_id = s.vrf_id;
+    memcpy(x.mac, s.mac, 6);
+    ifkv.push_back(KV{s.ifindex, 0, 0, (uint32_t)ifs.size()});
+    ifs.push_back(x);
+  }
+  im.ifaces = build_hash(ib, ifkv);
+  im.iface_recs = ib.put(ifs);
+  {
+    uint32_t cap = 2;
+    while (cap < 2 * std::max<uint32_t>(1, d->n_adjs)) cap <<= 1;
+    std::vector<Adj> slots(cap);
+    memset(slots.data(), 0, sizeof(Adj) * cap);
+    uint32_t count = 0;
+    for (uint32_t i = 0; i < d->n_adjs; i++) {
+      const dp_adjacency_t &s = d->adjs[i];
+      if (s.addr.family != 4 && s.addr.family != 6) return DP_EINVAL;
+      uint8_t a[16] = {0};
+      memcpy(a, s.addr.addr, s.addr.family == 6 ? 16 : 4);
+      uint32_t w[4] = {be32(a), be32(a + 4), be32(a + 8), be32(a + 12)};
+      uint32_t h = hmix(s.ifindex ^ ((uint32_t)s.addr.family << 24), w[0] ^ w[2], w[1] ^ w[3]) & (cap - 1);
+      for (;;) {
+        Adj &e = slots[h];
+        if (!e.used) {
+          e.used = 1; e.ifindex = s.ifindex; e.fam = s.addr.family;
+          memcpy(e.addr, a, 16); memcpy(e.mac, s.mac, 6);
+          count++;
+          break;
+        }
+        if (e.ifindex == s.ifindex && e.fam == s.addr.family && memcmp(e.addr, a, 16) == 0) {
+          memcpy(e.mac, s.mac, 6);  // HashMap insert replaces
+          break;
+        }
+        h = (h + 1) & (cap - 1);
+      }
+    }
+    im.adjs.slots = ib.put(slots);
+    im.adjs.mask = cap - 1;
+    im.adjs.count = count;
+  }
+
+  // --- classifiers
+  int rc;
+  std::vector<CRule> tmp;
+  struct T { const dp_rule_t *r; uint32_t n; int fam; bool prio; int kind; Classifier *dst; };
+  T tabs[6] = {
+      {d->acl_v4, d->n_acl_v4, 4, false, 0, &im.acl[0]},
+      {d->acl_v6, d->n_acl_v6, 6, false, 0, &im.acl[1]},
+      {d->ff_remote_v4, d->n_ff_remote_v4, 4, true, 1, &im.ff_remote[0]},
+      {d->ff_remote_v6, d->n_ff_remote_v6, 6, true, 1, &im.ff_remote[1]},
+      {d->ff_local_v4, d->n_ff_local_v4, 4, true, 2, &im.ff_local[0]},
+      {d->ff_local_v6, d->n_ff_local_v6, 6, true, 2, &im.ff_local[1]},
+  };
+  for (auto &t : tabs) {
+    tmp.clear();
+    if ((rc = load_rules(t.r, t.n, t.fam, t.prio, t.kind, tmp))) return rc;
+    *t.dst = build_classifier(ib, tmp, t.fam);
+  }
+  std::vector<KV> defkv;
+  for (uint32_t i = 0; i < d->n_acl_defaults; i++)
+    defkv.push_back(KV{d->acl_defaults[i].src_vni, d->acl_defaults[i].dst_vni, 0, d->acl_defaults[i].action + 1});
+  im.acl_default = build_hash(ib, defkv);
+
+  // --- static NAT
+  std::vector<NatTab> ntabs;
+  std::vector<NatEnt> nents;
+  std::vector<uint32_t> nprs;
+  std::vector<NatRange> nranges;
+  std::vector<KV> ntkv, pervni;
+  // merge descriptors with the same key (PerVniTable semantics)
+  std::vector<std::pair<KV, std::vector<const dp_nat_entry_t *>>> merged;
+  std::unordered_map<std::string, size_t> midx;
+  for (uint32_t i = 0; i < d->n_nat_tables; i++) {
+    const dp_nat_table_t &t = d->nat_tables[i];
+    if (t.kind > 1 || (uint64_t)t.first_entry + t.n_entries > d->n_nat_entries) return DP_EINVAL;
+    KV k{t.kind, t.src_vni, t.kind ? t.dst_vni : 0, 0};
+    std::string ks((const char *)&k, 12);
+    auto it = midx.find(ks);
+    if (it == midx.end()) { midx[ks] = merged.size(); merged.push_back({k, {}}); it = midx.find(ks); }
+    for (uint32_t j = 0; j < t.n_entries; j++) merged[it->second].second.push_back(&d->nat_entries[t.first_entry + j]);
+    pervni.push_back(KV{t.src_vni, 0, 0, 1});
+  }
+  for (auto &mt : merged) {
+    // dedupe by prefix: last insert wins, position of first
+    std::vector<const dp_nat_entry_t *> es;
+    for (auto *e : mt.second) {
+      if (e->prefix.family != 4 || !valid_prefix(e->prefix)) return DP_ENOTSUP;  // NAT44 only
+      if ((uint64_t)e->first_port_range + e->n_port_ranges > d->n_nat_port_ranges) return DP_EINVAL;
+      if ((uint64_t)e->first_range + e->n_ranges > d->n_nat_ranges) return DP_EINVAL;
+      bool rep = false;
+      for (auto &x : es)
+        if (x->prefix.len == e->prefix.len && memcmp(x->prefix.addr, e->prefix.addr, 4) == 0) { x = e; rep = true; break; }
+      if (!rep) es.push_back(e);
+    }
+    uint32_t base = (uint32_t)nents.size();
+    for (auto *e : es) {
+      NatEnt ne{};
+      ne.net = be32(e->prefix.addr);
+      ne.len = e->prefix.len;
+      ne.is_pat = e->is_pat ? 1 : 0;
+      ne.size = e->size;
+      ne.first_pr = (uint32_t)nprs.size();
+      ne.n_pr = e->n_port_ranges;
+      uint64_t tot = 0;
+      for (uint32_t k = 0; k < e->n_port_ranges; k++) {
+        const dp_port_range_t &pr = d->nat_port_ranges[e->first_port_range + k];
+        nprs.push_back((uint32_t)pr.lo | ((uint32_t)pr.hi << 16));
+        tot += (uint64_t)pr.hi - pr.lo + 1;
+      }
+      ne.covers_all = (!e->is_pat || tot == 65536) ? 1 : 0;
+      std::vector<NatRange> rs;
+      for (uint32_t k = 0; k < e->n_ranges; k++) {
+        const dp_nat_range_t &s = d->nat_ranges[e->first_range + k];
+        NatRange x{};
+        x.olo_ip = be32(s.orig_lo_ip); x.ohi_ip = be32(s.orig_hi_ip);
+        x.olo_port = s.orig_lo_port; x.ohi_port = s.orig_hi_port;
+        x.tlo_ip = be32(s.tgt_lo_ip); x.thi_ip = be32(s.tgt_hi_ip);
+        x.tlo_port = s.tgt_lo_port; x.thi_port = s.tgt_hi_port;
+        x.offset = s.offset;
+        rs.push_back(x);
+      }
+      std::stable_sort(rs.begin(), rs.end(), [](const NatRange &a, const NatRange &b) {
+        if (a.olo_ip != b.olo_ip) return a.olo_ip < b.olo_ip;
+        return a.olo_port < b.olo_port;
+      });
+      ne.first_range = (uint32_t)nranges.size();
+      ne.n_ranges = (uint32_t)rs.size();
+      nranges.insert(nranges.end(), rs.begin(), rs.end());
+      ne.parent = -1;
+      nents.push_back(ne);
+    }
+    uint32_t cnt = (uint32_t)es.size();
+    auto covers = [](const NatEnt &p, uint32_t a) {
+      uint32_t m = p.len == 0 ? 0 : (0xffffffffu << (32 - p.len));
+      return (a & m) == p.net;
+    };
+    for (uint32_t i = 0; i < cnt; i++) {
+      NatEnt &e = nents[base + i];
+      int best = -1;
+      for (uint32_t j = 0; j < cnt; j++) {
+        const NatEnt &f = nents[base + j];
+        if (j == i || f.len >= e.len || !covers(f, e.net)) continue;
+        if (best < 0 || f.len > nents[base + best].len) best = (int)j;
+      }
+      e.parent = best < 0 ? -1 : (int32_t)(base + best);
+    }
+    std::vector<uint64_t> bnd{0};
+    for (uint32_t i = 0; i < cnt; i++) {
+      const NatEnt &e = nents[base + i];
+      bnd.push_back(e.net);
+      uint64_t end = (uint64_t)e.net + (e.len == 0 ? (1ull << 32) : (1ull << (32 - e.len)));
+      if (end <= 0xffffffffull) bnd.push_back(end);
+    }
+    std::sort(bnd.begin(), bnd.end());
+    bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+    std::vector<uint32_t> b32;
+    std::vector<int32_t> longest;
+    for (uint64_t b : bnd) {
+      b32.push_back((uint32_t)b);
+      int best = -1;
+      for (uint32_t i = 0; i < cnt; i++) {
+        const NatEnt &e = nents[base + i];
+        if (!covers(e, (uint32_t)b)) continue;
+        if (best < 0 || e.len > nents[base + best].len) best = (int)i;
+      }
+      longest.push_back(best < 0 ? -1 : (int32_t)(base + best));
+    }
+    NatTab t{};
+    t.bounds = ib.put(b32);
+    t.longest = ib.put(longest);
+    t.n = (uint32_t)b32.size();
+    KV k = mt.first;
+    k.v = (uint32_t)ntabs.size();
+    ntkv.push_back(k);
+    ntabs.push_back(t);
+  }
+  im.nat_tabs = build_hash(ib, ntkv);
+  im.nat_pervni = build_hash(ib, pervni);
+  im.nat_tab_recs = ib.put(ntabs);
+  im.nat_ents = ib.put(nents);
+  im.nat_prs = ib.put(nprs);
+  im.nat_ranges = ib.put(nranges);
+
+  ib.alloc(64);
+  im.bytes = ib.b.size();
+  out.bytes.swap(ib.b);
+  out.im = im;
+  out.pt_nodes = pb.nodes.size();
+  return 0;
+}
+
+}  // namespace dpd

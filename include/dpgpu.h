@@ -1,0 +1,435 @@
+/* SPDX-License-Identifier: Apache-2.0
+ *
+ * dpgpu.h -- C ABI of the MI355X (gfx950) per-burst packet path.
+ *
+ * This is the drop-in boundary for the reference's packet hot loop
+ * (githedgehog/dataplane).  The reference composes the path from NetworkFunction
+ * stages (pipeline/src/static_nf.rs:12-32) assembled in
+ * dataplane/src/packet_processor/mod.rs:130-145:
+ *
+ *   Ingress -> IP-Forward-1 -> IcmpErrorHandler -> FlowLookup -> FlowFilter ->
+ *   AclFilter -> StaticNat -> PortForwarder -> Masquerade -> IP-Forward-2 -> Egress
+ *
+ * followed by Packet::serialize (net/src/packet/mod.rs:363-374).  One call of
+ * dp_process_burst*() runs that whole block for a burst, on the GPU, with the
+ * stateless-slice preconditions of SURVEY.md §8a A7 (empty flow table, no
+ * masquerade / port-forwarding exposes: those stages are identity).
+ *
+ * A Rust `GpuPathNf: NetworkFunction` materialises the burst
+ * exactly like FlowFilter::process does (flow-filter/src/lib.rs:357-362),
+ * stages the frames + metadata into the buffers below, calls this ABI and
+ * applies the returned DoneReason / metadata to each Packet.
+ *
+ * Conventions
+ *  - Every function returns 0 on success or a negative errno value.  Per-packet
+ *    failures are never status codes: they are DoneReason values in dp_pkt_out_t
+ *    (net/src/packet/meta.rs:84-119).  A whole-burst failure marks every packet
+ *    DP_DONE_INTERNAL_FAILURE, as the reference stages do for unreadable tables
+ *    (dataplane/src/packet_processor/ipforward.rs:89-98).
+ *  - Addresses, MACs and prefixes are in network byte order.
+ *  - The library never retains caller memory past a call.
+ *  - A context is used by one thread (one dp-worker); dp_tables_publish may be
+ *    called from another thread (mgmt) and only swaps a pointer for bursts
+ *    that start after it returns (left-right / ArcSwap semantics,
+ *    routing/src/fib/fibtype.rs:323-392, flow-filter/src/context/mod.rs:40-90).
+ */
+#ifndef DPGPU_H
+#define DPGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPGPU_ABI_VERSION 1u
+
+/* Bytes every frame must have in front of it (its own scratch, owned by the
+ * packet).  Output headers are written in place into this headroom: VXLAN
+ * encap over an IPv6 underlay grows the frame by at most 14+40+8+8 = 70 B.
+ * Mirrors TestBuffer's 96 B headroom (net/src/buffer/test_buffer.rs:45-50). */
+#define DP_HEADROOM 96u
+
+/* ------------------------------------------------------------------------ */
+/* DoneReason, in the reference's declaration order (u8 ordinals),           */
+/* net/src/packet/meta.rs:84-119.                                            */
+/* ------------------------------------------------------------------------ */
+enum dp_done_reason {
+    DP_DONE_INTERNAL_FAILURE = 0,
+    DP_DONE_INTERFACE_UNKNOWN = 1,
+    DP_DONE_INTERFACE_DETACHED = 2,
+    DP_DONE_INTERFACE_ADM_DOWN = 3,
+    DP_DONE_INTERFACE_OPER_DOWN = 4,
+    DP_DONE_INTERFACE_UNSUPPORTED = 5,
+    DP_DONE_NOT_ETHERNET = 6,
+    DP_DONE_UNHANDLED = 7,
+    DP_DONE_MAC_NOT_FOR_US = 8,
+    DP_DONE_INVALID_DST_MAC = 9,
+    DP_DONE_MISSING_ETHER_TYPE = 10,
+    DP_DONE_NOT_IP = 11,
+    DP_DONE_ROUTE_FAILURE = 12,
+    DP_DONE_ROUTE_DROP = 13,
+    DP_DONE_HOP_LIMIT_EXCEEDED = 14,
+    DP_DONE_MISS_L2_RESOLUTION = 15,
+    DP_DONE_VXLAN_DECAP_FAILURE = 16,
+    DP_DONE_VXLAN_ENCAP_FAILURE = 17,
+    DP_DONE_FILTERED = 18,
+    DP_DONE_ACL_DROPPED = 19,
+    DP_DONE_NAT_OUT_OF_RESOURCES = 20,
+    DP_DONE_FLOW_CAPACITY_EXCEEDED = 21,
+    DP_DONE_NAT_UNSUPPORTED_PROTO = 22,
+    DP_DONE_NAT_FAILURE = 23,
+    DP_DONE_NAT_NOT_PORT_FORWARDED = 24,
+    DP_DONE_MALFORMED = 25,
+    DP_DONE_UNROUTABLE = 26,
+    DP_DONE_INVALID_CHECKSUM = 27,
+    DP_DONE_ICMP_ERROR_INCOMPLETE = 28,
+    DP_DONE_INTERNAL_DROP = 29,
+    DP_DONE_LOCAL = 30,
+    DP_DONE_DELIVERED = 31,
+    DP_DONE_DEPARSE_ERROR = 32,
+    DP_DONE_NO_HEAD_ROOM = 33,
+    DP_DONE_COUNT = 34,
+    /* "not done": only ever seen if a stage sequence leaves a packet pending,
+     * which the router pipeline never does (Egress always decides). */
+    DP_DONE_NONE = 255
+};
+
+/* PacketMeta flags, bit-identical to MetaFlags (net/src/packet/meta.rs:121-136). */
+enum dp_meta_flag {
+    DP_META_INITIALIZED = 1u << 0,
+    DP_META_IS_L2_BCAST = 1u << 1,
+    DP_META_NATTED_SRC = 1u << 2,
+    DP_META_NATTED_DST = 1u << 3,
+    DP_META_REFR_CHKSUM = 1u << 4,
+    DP_META_KEEP = 1u << 5,
+    DP_META_IS_OVERLAY = 1u << 6,
+    DP_META_REQ_MASQUERADE = 1u << 7,
+    DP_META_REQ_PORT_FORWARDING = 1u << 8,
+    DP_META_REQ_STATIC_NAT_SRC = 1u << 9,
+    DP_META_REQ_STATIC_NAT_DST = 1u << 10
+};
+
+/* ------------------------------------------------------------------------ */
+/* Burst descriptors (SoA-friendly fixed-size records, 16 B in / 32 B out).  */
+/* ------------------------------------------------------------------------ */
+
+/* dp_pkt_in_t.flags */
+enum dp_in_flag {
+    /* Harness idiom of nat/src/static_nat/test.rs:285-296 and
+     * flow-filter tests: the frame is the INNER frame of a VXLAN packet that
+     * IP-Forward-1 has already decapsulated.  src_vni is the VNI it arrived
+     * on; Ingress and IP-Forward-1 are skipped and the metadata is set exactly
+     * as packet_exec_instruction_local sets it after a successful decap
+     * (dataplane/src/packet_processor/ipforward.rs:140-161): src_vpcd=VNI,
+     * vrf=fib(VNI).id, IS_OVERLAY; an unregistered VNI gives Unroutable. */
+    DP_IN_SEEDED_OVERLAY = 1u << 0
+};
+
+typedef struct dp_pkt_in {
+    uint32_t off;      /* frame start inside the burst buffer; >= DP_HEADROOM
+                          bytes in front of it belong to this packet */
+    uint16_t len;      /* frame length (mbuf data_len, FCS stripped) */
+    uint16_t flags;    /* enum dp_in_flag */
+    uint32_t iif;      /* PacketMeta.iif, set by the driver */
+    uint32_t src_vni;  /* only with DP_IN_SEEDED_OVERLAY */
+} dp_pkt_in_t;
+
+typedef struct dp_pkt_out {
+    uint32_t off;        /* serialized frame start (only valid if Delivered) */
+    uint16_t len;        /* serialized frame length (only valid if Delivered) */
+    uint8_t done;        /* enum dp_done_reason */
+    uint8_t acl;         /* 0: ACL not consulted, 1: allow (rule), 2: deny (rule),
+                            3: allow (peering default), 4: deny (peering default),
+                            5: allow (no ACL for peering) */
+    uint32_t meta_flags; /* enum dp_meta_flag */
+    uint32_t oif;        /* PacketMeta.oif (0 if None) */
+    uint32_t dst_vni;    /* PacketMeta.dst_vpcd VNI (0 if None) */
+    uint32_t src_vni;    /* PacketMeta.src_vpcd VNI (0 if None) */
+    uint32_t fib_entry;  /* index of the last FibEntry executed (UINT32_MAX: none) */
+    uint32_t acl_rule;   /* index of the matching ACL rule in its table (UINT32_MAX: none) */
+} dp_pkt_out_t;
+
+/* ------------------------------------------------------------------------ */
+/* Table descriptors: host arrays lowered from the reference's structures.  */
+/* ------------------------------------------------------------------------ */
+
+typedef struct dp_ipaddr {
+    uint8_t family;  /* 4 or 6 (0: none) */
+    uint8_t pad[3];
+    uint8_t addr[16]; /* v4 uses addr[0..4] */
+} dp_ipaddr_t;
+
+typedef struct dp_prefix {
+    uint8_t family;  /* 4 or 6 */
+    uint8_t len;     /* prefix length; host bits must be zero
+                        (lpm/src/prefix/ip.rs:148-165) */
+    uint8_t pad[2];
+    uint8_t addr[16];
+} dp_prefix_t;
+
+/* FIB: routing/src/fib/fibtype.rs:54-61.  One per VRF. */
+enum dp_fib_flag {
+    DP_FIB_VTEP_HAS_IP = 1u << 0,
+    DP_FIB_VTEP_HAS_MAC = 1u << 1
+};
+typedef struct dp_fib {
+    uint32_t vrf_id;        /* FibKey::Id */
+    uint32_t flags;         /* enum dp_fib_flag */
+    dp_ipaddr_t vtep_ip;    /* Vtep (routing/src/evpn/vtep.rs:11-14) */
+    uint8_t vtep_mac[6];
+    uint8_t pad[2];
+} dp_fib_t;
+
+/* FibTable VNI registration (routing/src/fib/fibtable.rs:46-56). */
+typedef struct dp_vni_fib {
+    uint32_t vni;
+    uint32_t fib;           /* index into fibs[] */
+} dp_vni_fib_t;
+
+/* PktInstruction (routing/src/fib/fibobjects.rs:258-264). */
+enum dp_instr_kind {
+    DP_INSTR_DROP = 0,
+    DP_INSTR_LOCAL = 1,
+    DP_INSTR_ENCAP_VXLAN = 2,
+    DP_INSTR_EGRESS = 3
+};
+enum dp_instr_flag {
+    DP_INSTR_HAS_IFINDEX = 1u << 0, /* EgressObject.ifindex is Some */
+    DP_INSTR_HAS_ADDR = 1u << 1,    /* EgressObject.address is Some */
+    DP_INSTR_HAS_DMAC = 1u << 2     /* VxlanEncapsulation.dmac is Some */
+};
+typedef struct dp_instr {
+    uint32_t kind;          /* enum dp_instr_kind */
+    uint32_t flags;         /* enum dp_instr_flag */
+    uint32_t ifindex;       /* LOCAL / EGRESS */
+    uint32_t vni;           /* ENCAP_VXLAN */
+    dp_ipaddr_t addr;       /* EGRESS next-hop / ENCAP_VXLAN remote */
+    uint8_t mac[6];         /* ENCAP_VXLAN dmac */
+    uint8_t pad[2];
+} dp_instr_t;
+
+/* FibEntry = ordered instruction list (fibobjects.rs:142-144). */
+typedef struct dp_fib_entry {
+    uint32_t first_instr;
+    uint32_t n_instr;       /* 1..4 */
+} dp_fib_entry_t;
+
+/* FibRoute = its FibGroups' entries, flattened in group order
+ * (routing/src/fib/fibgroupstore.rs:195-234). */
+typedef struct dp_route_nh {
+    uint32_t first_entry;
+    uint32_t n_entries;     /* >= 1; > 1 selects by packet_hash_ecmp */
+} dp_route_nh_t;
+
+typedef struct dp_route {
+    dp_prefix_t prefix;
+    uint32_t fib;           /* index into fibs[] */
+    uint32_t nh;            /* index into route_nhs[] */
+} dp_route_t;
+
+/* Interface table (routing/src/interfaces/interface.rs). */
+enum dp_if_state { DP_IF_UNKNOWN = 0, DP_IF_DOWN = 1, DP_IF_UP = 2 };
+enum dp_if_type { DP_IFT_UNKNOWN = 0, DP_IFT_ETHERNET = 1, DP_IFT_DOT1Q = 2,
+                  DP_IFT_LOOPBACK = 3, DP_IFT_VXLAN = 4 };
+enum dp_if_attach { DP_ATTACH_NONE = 0, DP_ATTACH_VRF = 1, DP_ATTACH_BRIDGE = 2 };
+typedef struct dp_iface {
+    uint32_t ifindex;
+    uint8_t admin_state;    /* enum dp_if_state */
+    uint8_t oper_state;     /* enum dp_if_state */
+    uint8_t iftype;         /* enum dp_if_type (Ethernet/Dot1q carry a MAC) */
+    uint8_t attach;         /* enum dp_if_attach */
+    uint32_t vrf_id;        /* Attachment::Vrf(fibkey) */
+    uint8_t mac[6];
+    uint8_t pad[2];
+} dp_iface_t;
+
+/* Adjacency table, keyed (ifindex, ip) (routing/src/atable/adjacency.rs:51-82). */
+typedef struct dp_adjacency {
+    dp_ipaddr_t addr;
+    uint32_t ifindex;
+    uint8_t mac[6];
+    uint8_t pad[2];
+} dp_adjacency_t;
+
+/* Classifier rule: the union of the reference's three MatchKeys
+ *   AclKey    (acl-filter/src/context.rs:168-190)
+ *   RemoteKey (flow-filter/src/context/tables.rs:192-207)
+ *   LocalKey  (flow-filter/src/context/tables.rs:211-229)
+ * with match-action predicate semantics (match-action/src/predicate.rs):
+ * proto = Mask, vni_a/vni_b/gate = Exact, src/dst = Prefix, ports = Range
+ * (inclusive).  Unused fields are wildcards (prefix len 0, range 0..65535).
+ *   ACL:       vni_a=src_vni, vni_b=dst_vni, gate=0
+ *   FF remote: vni_a=src_vni, vni_b=GateVni (0 = ungated), src wildcard,
+ *              sport wildcard
+ *   FF local:  vni_a=src_vni, vni_b=dst_vni, gate=SourceGate, dst wildcard,
+ *              dport wildcard */
+typedef struct dp_rule {
+    uint8_t proto_val;
+    uint8_t proto_mask;     /* 0xff exact, 0x00 any */
+    uint8_t family;         /* 4 or 6: which table */
+    uint8_t gate;
+    uint32_t vni_a;
+    uint32_t vni_b;
+    uint16_t sport_lo, sport_hi;
+    uint16_t dport_lo, dport_hi;
+    uint32_t priority;      /* flow-filter only: rule_priority(); tables are
+                               matched in stable descending-priority order
+                               (flow-filter/src/context/tables.rs:373-380);
+                               ACL tables match in array order (first match,
+                               acl-filter/src/context.rs:447-452) */
+    dp_prefix_t src;
+    dp_prefix_t dst;
+    uint32_t action;        /* ACL: 0 Allow / 1 Deny.  FF remote: dst VNI.
+                               FF local: enum dp_nat_mode (source NAT mode). */
+    uint32_t action2;       /* FF remote: enum dp_nat_mode (destination NAT) */
+} dp_rule_t;
+
+enum dp_acl_action { DP_ACL_ALLOW = 0, DP_ACL_DENY = 1 };
+/* NatRequirement (flow-filter/src/lib.rs NatMode = Option<NatRequirement>). */
+enum dp_nat_mode { DP_NAT_NONE = 0, DP_NAT_STATIC = 1, DP_NAT_MASQUERADE = 2,
+                   DP_NAT_PORT_FORWARDING = 3 };
+
+/* Per-peering ACL default (acl-filter/src/context.rs:564-566). */
+typedef struct dp_acl_default {
+    uint32_t src_vni;
+    uint32_t dst_vni;
+    uint32_t action;        /* enum dp_acl_action */
+} dp_acl_default_t;
+
+/* Static NAT tables (nat/src/static_nat/setup/tables.rs), NAT44.
+ * NatTables: src_vni -> PerVniTable{ dst_nat, src_nat[dst_vni] }. */
+enum dp_nat_table_kind { DP_NAT_TABLE_DST = 0, DP_NAT_TABLE_SRC = 1 };
+typedef struct dp_nat_table {
+    uint32_t kind;          /* enum dp_nat_table_kind */
+    uint32_t src_vni;       /* owning PerVniTable */
+    uint32_t dst_vni;       /* DP_NAT_TABLE_SRC only: src_nat key */
+    uint32_t first_entry;
+    uint32_t n_entries;
+} dp_nat_table_t;
+
+/* One IpPortPrefixTrie entry: prefix -> NatTableValue. */
+typedef struct dp_nat_entry {
+    dp_prefix_t prefix;
+    uint32_t is_pat;        /* NatTableValue::Pat (else ::Nat) */
+    uint32_t first_port_range, n_port_ranges; /* Pat: prefix_port_ranges */
+    uint32_t first_range, n_ranges;           /* ranges_tree, sorted by key */
+    uint32_t pad;
+    uint64_t size;          /* Nat: ip_len(); Pat: size() (ips x ports) */
+} dp_nat_entry_t;
+
+typedef struct dp_port_range {
+    uint16_t lo, hi;        /* inclusive */
+} dp_port_range_t;
+
+/* ranges_tree element.  Nat:  key IpRange [orig_lo_ip, orig_hi_ip] ->
+ * (target IpRange, offset).  Pat: key IpPortRangeBounds
+ * [(orig_lo_ip,orig_lo_port), (orig_hi_ip,orig_hi_port)] ->
+ * (IpPortRange{target ip range, target port range}, offset). */
+typedef struct dp_nat_range {
+    uint8_t orig_lo_ip[4];
+    uint8_t orig_hi_ip[4];
+    uint16_t orig_lo_port, orig_hi_port;
+    uint8_t tgt_lo_ip[4];
+    uint8_t tgt_hi_ip[4];
+    uint16_t tgt_lo_port, tgt_hi_port;
+    uint64_t offset;
+} dp_nat_range_t;
+
+typedef struct dp_tables_desc {
+    uint32_t abi_version;   /* DPGPU_ABI_VERSION */
+    uint32_t pad0;
+    int64_t genid;          /* PipelineData.genid (pipeline/src/pipeline.rs:22-42) */
+
+    const dp_fib_t *fibs;            uint32_t n_fibs;
+    const dp_vni_fib_t *vni_fibs;    uint32_t n_vni_fibs;
+    const dp_route_t *routes;        uint64_t n_routes;
+    const dp_route_nh_t *route_nhs;  uint32_t n_route_nhs;
+    const dp_fib_entry_t *entries;   uint32_t n_entries;
+    const dp_instr_t *instrs;        uint32_t n_instrs;
+    const dp_iface_t *ifaces;        uint32_t n_ifaces;
+    const dp_adjacency_t *adjs;      uint32_t n_adjs;
+
+    const dp_rule_t *acl_v4;         uint32_t n_acl_v4;
+    const dp_rule_t *acl_v6;         uint32_t n_acl_v6;
+    const dp_acl_default_t *acl_defaults; uint32_t n_acl_defaults;
+
+    const dp_rule_t *ff_remote_v4;   uint32_t n_ff_remote_v4;
+    const dp_rule_t *ff_local_v4;    uint32_t n_ff_local_v4;
+    const dp_rule_t *ff_remote_v6;   uint32_t n_ff_remote_v6;
+    const dp_rule_t *ff_local_v6;    uint32_t n_ff_local_v6;
+
+    const dp_nat_table_t *nat_tables; uint32_t n_nat_tables;
+    const dp_nat_entry_t *nat_entries; uint32_t n_nat_entries;
+    const dp_port_range_t *nat_port_ranges; uint32_t n_nat_port_ranges;
+    const dp_nat_range_t *nat_ranges; uint32_t n_nat_ranges;
+} dp_tables_desc_t;
+
+/* ------------------------------------------------------------------------ */
+/* Errors (negative errno).                                                  */
+/* ------------------------------------------------------------------------ */
+#define DP_OK 0
+#define DP_EINVAL (-22)
+#define DP_ENOMEM (-12)
+#define DP_ENODEV (-19)
+#define DP_ENOTSUP (-95)   /* e.g. masquerade / port-forwarding NAT modes */
+#define DP_EIO (-5)        /* HIP runtime failure */
+#define DP_ENOTABLES (-61) /* no tables published yet (ENODATA) */
+
+/* ------------------------------------------------------------------------ */
+/* Entry points.                                                             */
+/* ------------------------------------------------------------------------ */
+typedef struct dp_ctx dp_ctx_t;
+
+/* Library / ABI version (for the FFI loader's sanity check). */
+uint32_t dp_abi_version(void);
+
+/* One context per worker thread (worker.rs:175 builds one pipeline per
+ * worker); owns one HIP stream and the device-side staging scratch.  Tables
+ * are shared by all contexts on the same device (refcounted image). */
+int dp_ctx_create(int device_ordinal, dp_ctx_t **out);
+int dp_ctx_destroy(dp_ctx_t *ctx);
+
+/* Compile the lowered tables into the device image and publish it.
+ * Replaces left-right FibWriter publish / NatTablesWriter::update_nat_tables /
+ * FlowFilterContextWriter::store / AclFilterContextWriter::store
+ *  for every context on the device.  Never blocks a burst
+ * beyond a pointer swap; the old image is retired once bursts using it end. */
+int dp_tables_publish(dp_ctx_t *ctx, const dp_tables_desc_t *tables);
+
+/* Current generation id (PipelineData::genid). */
+int64_t dp_tables_genid(const dp_ctx_t *ctx);
+
+/* Host-origin burst: `buf` is caller-owned (pinned for best speed) host
+ * memory holding every frame at in[i].off with DP_HEADROOM bytes in front.
+ * Frames are rewritten in place; out[i] tells where each serialized frame
+ * now starts.  Synchronous.  `stats` (may be NULL) receives DP_DONE_COUNT
+ * counters (PacketStatsNF, pipeline/src/sample_nfs.rs:225-273). */
+int dp_process_burst(dp_ctx_t *ctx, uint8_t *buf, uint64_t buf_bytes,
+                     const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
+                     uint64_t *stats);
+
+/* Device-resident burst: every pointer is device memory; enqueued on
+ * `stream` (a hipStream_t; NULL = the context's stream).  Asynchronous.
+ * `dev_buf` must be 16-byte aligned and `buf_bytes` must cover every frame
+ * end rounded up to 16 bytes (frames are staged with 16-byte loads); a
+ * packet violating the layout contract is marked DP_DONE_INTERNAL_FAILURE
+ * without touching memory.  `dev_stats` (may be NULL) is accumulated into
+ * (DP_DONE_COUNT u64). */
+int dp_process_burst_device(dp_ctx_t *ctx, uint8_t *dev_buf, uint64_t buf_bytes,
+                            const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out,
+                            uint32_t n, uint64_t *dev_stats, void *stream);
+
+/* Wait for the context's stream. */
+int dp_ctx_synchronize(dp_ctx_t *ctx);
+
+/* Introspection: bytes of the device table image and its parts (for
+ * DESIGN.md / bench), and the last HIP error string. */
+uint64_t dp_tables_device_bytes(const dp_ctx_t *ctx);
+const char *dp_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPGPU_H */

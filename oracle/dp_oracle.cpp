@@ -1,0 +1,1625 @@
+// SPDX-License-Identifier: Apache-2.0
+//
+// TEST INFRASTRUCTURE -- NOT PRODUCT CODE (see dp_oracle.h).
+//
+// CPU restatement of the reference per-burst packet path.  Structure follows
+// the reference on purpose: a parsed `Headers` value with optional layers
+// (net/src/headers/mod.rs:67-75), stage functions in pipeline order
+// (dataplane/src/packet_processor/mod.rs:130-145), deparse-on-serialize
+// (net/src/packet/mod.rs:342-374).  Lookup structures are the simple
+// reference ones: binary trie LPM (prefix-trie semantics), linear first-match
+// classifiers (acl/src/reference/table.rs:94-101), linear NAT range search.
+#include "dp_oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Small helpers
+// ---------------------------------------------------------------------------
+inline uint16_t be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+inline uint32_t be32(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+inline void put16(uint8_t *p, uint16_t v) { p[0] = v >> 8; p[1] = v & 0xff; }
+inline void put32(uint8_t *p, uint32_t v) {
+  p[0] = v >> 24; p[1] = (v >> 16) & 0xff; p[2] = (v >> 8) & 0xff; p[3] = v & 0xff;
+}
+
+struct Ip {  // std::net::IpAddr
+  uint8_t fam = 0;  // 4 / 6
+  uint8_t b[16] = {0};
+  bool operator==(const Ip &o) const {
+    return fam == o.fam && memcmp(b, o.b, fam == 4 ? 4 : 16) == 0;
+  }
+};
+
+inline Ip ip4(const uint8_t *a) { Ip r; r.fam = 4; memcpy(r.b, a, 4); return r; }
+inline Ip ip6(const uint8_t *a) { Ip r; r.fam = 6; memcpy(r.b, a, 16); return r; }
+
+inline bool bit_at(const uint8_t *a, int i) { return (a[i >> 3] >> (7 - (i & 7))) & 1; }
+
+// prefix covers address (match-action Prefix::matches semantics,
+// match-action/src/predicate.rs:50-53,246-264)
+bool prefix_covers(const uint8_t *pfx, int len, const uint8_t *addr) {
+  int full = len / 8, rem = len % 8;
+  if (memcmp(pfx, addr, full) != 0) return false;
+  if (rem) {
+    uint8_t m = (uint8_t)(0xff << (8 - rem));
+    if ((pfx[full] & m) != (addr[full] & m)) return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// One's complement checksum (etherparse checksum::Sum16BitWords)
+// ---------------------------------------------------------------------------
+struct Sum16 {
+  uint64_t s = 0;
+  void add2(uint8_t a, uint8_t b) { s += (uint32_t)((a << 8) | b); }
+  void add_u16(uint16_t v) { s += v; }
+  void add_slice(const uint8_t *p, size_t n) {
+    size_t i = 0;
+    for (; i + 1 < n; i += 2) s += (uint32_t)((p[i] << 8) | p[i + 1]);
+    if (i < n) s += (uint32_t)(p[i] << 8);  // odd trailing byte padded with 0
+  }
+  uint16_t ones_complement() const {
+    uint64_t v = s;
+    while (v >> 16) v = (v & 0xffff) + (v >> 16);
+    return (uint16_t)~v;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// rapidhash-style hash (restatement; parity vs reference UNPINNED,
+// rapidhash 4.5.1 over Rust `Hash` encodings)
+// ---------------------------------------------------------------------------
+const uint64_t kSecret[3] = {0x2d358dccaa6c78a5ull, 0x8bb84b93962eacc9ull,
+                             0x4b33a62ed433d4a3ull};
+const uint64_t kSeed = 0xbdd89aa982704029ull;
+inline void mum(uint64_t *a, uint64_t *b) {
+  unsigned __int128 r = (unsigned __int128)(*a) * (*b);
+  *a = (uint64_t)r;
+  *b = (uint64_t)(r >> 64);
+}
+inline uint64_t mix(uint64_t a, uint64_t b) { mum(&a, &b); return a ^ b; }
+inline uint64_t r64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
+inline uint64_t r32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+
+uint64_t rapid(const uint8_t *p, size_t len) {
+  uint64_t seed = kSeed;
+  seed ^= mix(seed ^ kSecret[0], kSecret[1]) ^ len;
+  uint64_t a, b;
+  if (len <= 16) {
+    if (len >= 4) {
+      const uint8_t *plast = p + len - 4;
+      a = (r32(p) << 32) | r32(plast);
+      const uint64_t delta = ((len & 24) >> (len >> 3));
+      b = (r32(p + delta) << 32) | r32(plast - delta);
+    } else if (len > 0) {
+      a = ((uint64_t)p[0] << 56) | ((uint64_t)p[len >> 1] << 32) | p[len - 1];
+      b = 0;
+    } else {
+      a = b = 0;
+    }
+  } else {
+    size_t i = len;
+    if (i > 48) {
+      uint64_t see1 = seed, see2 = seed;
+      while (i >= 48) {
+        seed = mix(r64(p) ^ kSecret[0], r64(p + 8) ^ seed);
+        see1 = mix(r64(p + 16) ^ kSecret[1], r64(p + 24) ^ see1);
+        see2 = mix(r64(p + 32) ^ kSecret[2], r64(p + 40) ^ see2);
+        p += 48;
+        i -= 48;
+      }
+      seed ^= see1 ^ see2;
+    }
+    if (i > 16) {
+      seed = mix(r64(p) ^ kSecret[2], r64(p + 8) ^ seed ^ kSecret[1]);
+      if (i > 32) seed = mix(r64(p + 16) ^ kSecret[2], r64(p + 24) ^ seed);
+    }
+    a = r64(p + i - 16);
+    b = r64(p + i - 8);
+  }
+  a ^= kSecret[1];
+  b ^= seed;
+  mum(&a, &b);
+  return mix(a ^ kSecret[0] ^ len, b ^ kSecret[1]);
+}
+
+// ---------------------------------------------------------------------------
+// Parsed headers (net/src/headers/mod.rs:67-75)
+// ---------------------------------------------------------------------------
+enum L4Kind { L4_NONE = 0, L4_TCP, L4_UDP, L4_ICMP4, L4_ICMP6 };
+enum ExtKind { EXT_RAW = 0, EXT_FRAG, EXT_AUTH };
+
+struct Eth {  // etherparse Ethernet2Header
+  uint8_t dst[6], src[6];
+  uint16_t type;
+};
+struct Vlan {  // etherparse SingleVlanHeader: round-trips exactly
+  uint16_t tci, inner;
+  uint16_t vid() const { return tci & 0x0fff; }
+};
+struct Ipv4 {  // etherparse Ipv4Header (no reserved flag bit: dropped on deparse)
+  uint8_t dscp, ecn;
+  uint16_t total_len, id;
+  bool df, mf;
+  uint16_t frag;
+  uint8_t ttl, proto;
+  uint16_t csum;
+  uint8_t src[4], dst[4];
+  uint8_t opts[40];
+  uint8_t opt_len;
+  int hlen() const { return 20 + opt_len; }
+};
+struct Ipv6 {
+  uint8_t tc;
+  uint32_t flow;
+  uint16_t plen;
+  uint8_t nh, hop;
+  uint8_t src[16], dst[16];
+};
+struct Ext {  // HopByHop/DestOpts/Routing raw, Fragment, Auth (normalized bytes)
+  int kind;
+  uint8_t nh;
+  std::vector<uint8_t> bytes;
+};
+struct Tcp {  // etherparse TcpHeader: reserved bits dropped on deparse
+  uint16_t sport, dport;
+  uint32_t seq, ack;
+  uint8_t doff;
+  bool ns;
+  uint8_t flags;
+  uint16_t win, csum, urg;
+  uint8_t opts[40];
+  int hlen() const { return doff * 4; }
+};
+struct Udp {
+  uint16_t sport, dport, len, csum;
+};
+struct Icmp {  // type, code, checksum, rest (4 or 16 bytes)
+  uint8_t raw[20];
+  int hlen;
+};
+
+struct Headers {
+  bool has_eth = false;
+  Eth eth{};
+  std::vector<Vlan> vlans;
+  int net = 0;  // 0 none, 4, 6
+  Ipv4 v4{};
+  Ipv6 v6{};
+  std::vector<Ext> ext;
+  int l4 = L4_NONE;
+  Tcp tcp{};
+  Udp udp{};
+  Icmp icmp{};
+  bool has_vxlan = false;
+  uint32_t vni = 0;
+
+  int size() const {
+    int s = has_eth ? 14 : 0;
+    s += 4 * (int)vlans.size();
+    if (net == 4) s += v4.hlen();
+    if (net == 6) s += 40;
+    if (net) for (auto &e : ext) s += (int)e.bytes.size();
+    if (net && l4 == L4_TCP) s += tcp.hlen();
+    if (net && l4 == L4_UDP) s += 8;
+    if (net && (l4 == L4_ICMP4 || l4 == L4_ICMP6)) s += icmp.hlen;
+    if (net && l4 != L4_NONE && has_vxlan) s += 8;
+    return s;
+  }
+};
+
+struct Meta {
+  int done = -1;  // DoneReason or -1 (None)
+  uint32_t flags = DP_META_INITIALIZED | DP_META_KEEP;
+  bool has_vrf = false;
+  uint32_t vrf = 0;
+  uint32_t src_vni = 0, dst_vni = 0;  // 0 = None
+  bool has_oif = false;
+  uint32_t oif = 0;
+  bool has_nh = false;
+  Ip nh;
+  bool has_dscp = false;
+  uint8_t dscp = 0, ecn = 0;
+  uint32_t fib_entry = UINT32_MAX;
+  uint32_t acl_rule = UINT32_MAX;
+  uint8_t acl = 0;
+};
+
+struct Packet {
+  Headers h;
+  uint8_t *buf;
+  uint64_t pay_start, pay_end;  // payload is buf[pay_start, pay_end)
+  uint64_t room_start;          // first byte this packet may write
+  Meta m;
+  void done(int r) { if (m.done < 0) m.done = r; }
+  void done_force(int r) { m.done = r; }
+  bool is_done() const { return m.done >= 0; }
+  bool overlay() const { return m.flags & DP_META_IS_OVERLAY; }
+};
+
+// ---------------------------------------------------------------------------
+// Parse (Headers::parse, net/src/headers/mod.rs:474-578)
+// ---------------------------------------------------------------------------
+struct Reader {
+  const uint8_t *p;
+  size_t len, pos;
+  size_t remaining() const { return len - pos; }
+  const uint8_t *cur() const { return p + pos; }
+};
+
+// Eth::parse (net/src/eth/mod.rs:111-146): dst != 0, src != 0 && !multicast
+bool parse_eth(Reader &r, Eth &e) {
+  if (r.remaining() < 14) return false;
+  const uint8_t *q = r.cur();
+  memcpy(e.dst, q, 6);
+  memcpy(e.src, q + 6, 6);
+  e.type = be16(q + 12);
+  static const uint8_t zero[6] = {0};
+  if (memcmp(e.dst, zero, 6) == 0) return false;
+  if (memcmp(e.src, zero, 6) == 0) return false;
+  if (e.src[0] & 1) return false;
+  r.pos += 14;
+  return true;
+}
+
+// Vlan::parse (net/src/vlan/mod.rs:327-354); Vid 0 and 4095 invalid (:74-81)
+bool parse_vlan(Reader &r, Vlan &v) {
+  if (r.remaining() < 4) return false;
+  const uint8_t *q = r.cur();
+  v.tci = be16(q);
+  v.inner = be16(q + 2);
+  uint16_t vid = v.tci & 0x0fff;
+  if (vid == 0 || vid == 4095) return false;
+  r.pos += 4;
+  return true;
+}
+
+// Ipv4::parse (net/src/ipv4/mod.rs:351-373) over etherparse
+// Ipv4HeaderSlice::from_slice: version 4, ihl >= 5, len >= ihl*4,
+// total_len >= ihl*4; then source must be unicast (not multicast/broadcast).
+bool parse_ipv4(Reader &r, Ipv4 &h) {
+  if (r.remaining() < 20) return false;
+  const uint8_t *q = r.cur();
+  if ((q[0] >> 4) != 4) return false;
+  int ihl = q[0] & 0xf;
+  if (ihl < 5) return false;
+  int hlen = ihl * 4;
+  if ((int)r.remaining() < hlen) return false;
+  uint16_t total = be16(q + 2);
+  if (total < hlen) return false;
+  h.dscp = q[1] >> 2;
+  h.ecn = q[1] & 3;
+  h.total_len = total;
+  h.id = be16(q + 4);
+  h.df = (q[6] >> 6) & 1;
+  h.mf = (q[6] >> 5) & 1;
+  h.frag = (uint16_t)(((q[6] & 0x1f) << 8) | q[7]);
+  h.ttl = q[8];
+  h.proto = q[9];
+  h.csum = be16(q + 10);
+  memcpy(h.src, q + 12, 4);
+  memcpy(h.dst, q + 16, 4);
+  h.opt_len = (uint8_t)(hlen - 20);
+  memcpy(h.opts, q + 20, h.opt_len);
+  // UnicastIpv4Addr::new: not multicast (224/4) and not broadcast
+  if ((h.src[0] & 0xf0) == 0xe0) return false;
+  if (h.src[0] == 255 && h.src[1] == 255 && h.src[2] == 255 && h.src[3] == 255) return false;
+  r.pos += hlen;
+  return true;
+}
+
+// Ipv6::parse (net/src/ipv6/mod.rs:309-335): version 6, src not multicast
+bool parse_ipv6(Reader &r, Ipv6 &h) {
+  if (r.remaining() < 40) return false;
+  const uint8_t *q = r.cur();
+  if ((q[0] >> 4) != 6) return false;
+  h.tc = (uint8_t)(((q[0] & 0xf) << 4) | (q[1] >> 4));
+  h.flow = ((uint32_t)(q[1] & 0xf) << 16) | ((uint32_t)q[2] << 8) | q[3];
+  h.plen = be16(q + 4);
+  h.nh = q[6];
+  h.hop = q[7];
+  memcpy(h.src, q + 8, 16);
+  memcpy(h.dst, q + 24, 16);
+  if (h.src[0] == 0xff) return false;
+  r.pos += 40;
+  return true;
+}
+
+// Ipv6RawExtHeader (HopByHop 0 / Routing 43 / DestOpts 60): (len+1)*8 bytes
+bool parse_ext_raw(Reader &r, Ext &e) {
+  if (r.remaining() < 8) return false;
+  const uint8_t *q = r.cur();
+  size_t n = ((size_t)q[1] + 1) * 8;
+  if (r.remaining() < n) return false;
+  e.kind = EXT_RAW;
+  e.nh = q[0];
+  e.bytes.assign(q, q + n);
+  r.pos += n;
+  return true;
+}
+// Ipv6FragmentHeader (44): 8 bytes; reserved bits not kept by etherparse
+bool parse_ext_frag(Reader &r, Ext &e) {
+  if (r.remaining() < 8) return false;
+  const uint8_t *q = r.cur();
+  e.kind = EXT_FRAG;
+  e.nh = q[0];
+  e.bytes.assign(q, q + 8);
+  e.bytes[1] = 0;                        // reserved
+  e.bytes[3] = (uint8_t)(q[3] & 0xf9);   // res bits 1-2 zeroed, M kept
+  r.pos += 8;
+  return true;
+}
+// IpAuthHeader (51): (payload_len+2)*4 bytes, payload_len >= 1; reserved zeroed
+bool parse_ext_auth(Reader &r, Ext &e) {
+  if (r.remaining() < 12) return false;
+  const uint8_t *q = r.cur();
+  if (q[1] == 0) return false;
+  size_t n = ((size_t)q[1] + 2) * 4;
+  if (r.remaining() < n) return false;
+  e.kind = EXT_AUTH;
+  e.nh = q[0];
+  e.bytes.assign(q, q + n);
+  e.bytes[2] = 0;
+  e.bytes[3] = 0;
+  r.pos += n;
+  return true;
+}
+
+// Tcp::parse (net/src/tcp/mod.rs:330-365)
+bool parse_tcp(Reader &r, Tcp &t) {
+  if (r.remaining() < 20) return false;
+  const uint8_t *q = r.cur();
+  int doff = q[12] >> 4;
+  if (doff < 5) return false;
+  if ((int)r.remaining() < doff * 4) return false;
+  t.sport = be16(q);
+  t.dport = be16(q + 2);
+  if (t.sport == 0 || t.dport == 0) return false;
+  t.seq = be32(q + 4);
+  t.ack = be32(q + 8);
+  t.doff = (uint8_t)doff;
+  t.ns = q[12] & 1;
+  t.flags = q[13];
+  t.win = be16(q + 14);
+  t.csum = be16(q + 16);
+  t.urg = be16(q + 18);
+  memcpy(t.opts, q + 20, doff * 4 - 20);
+  r.pos += doff * 4;
+  return true;
+}
+
+// Udp::parse (net/src/udp/mod.rs:180-211)
+bool parse_udp(Reader &r, Udp &u) {
+  if (r.remaining() < 8) return false;
+  const uint8_t *q = r.cur();
+  u.sport = be16(q);
+  u.dport = be16(q + 2);
+  u.len = be16(q + 4);
+  u.csum = be16(q + 6);
+  if (u.sport == 0 || u.dport == 0) return false;
+  r.pos += 8;
+  return true;
+}
+
+// Icmpv4Header / Icmpv6Header: 8 bytes (v4 timestamp request/reply: 20)
+bool parse_icmp(Reader &r, Icmp &ic, bool v6) {
+  if (r.remaining() < 8) return false;
+  const uint8_t *q = r.cur();
+  int n = 8;
+  if (!v6 && (q[0] == 13 || q[0] == 14) && q[1] == 0) n = 20;
+  if ((int)r.remaining() < n) return false;
+  memcpy(ic.raw, q, n);
+  ic.hlen = n;
+  r.pos += n;
+  return true;
+}
+
+// Vxlan::parse (net/src/vxlan/mod.rs:91-122)
+bool parse_vxlan(Reader &r, uint32_t &vni) {
+  if (r.remaining() < 8) return false;
+  const uint8_t *q = r.cur();
+  if ((q[0] & 0x08) != 0x08) return false;
+  if (q[1] || q[2] || q[3] || q[7]) return false;
+  uint32_t v = ((uint32_t)q[4] << 16) | ((uint32_t)q[5] << 8) | q[6];
+  if (v == 0) return false;
+  vni = v;
+  r.pos += 8;
+  return true;
+}
+
+bool icmp_is_error(const Headers &h) {
+  if (h.l4 == L4_ICMP4) {
+    uint8_t t = h.icmp.raw[0];
+    return t == 3 || t == 5 || t == 11 || t == 12;
+  }
+  if (h.l4 == L4_ICMP6) {
+    uint8_t t = h.icmp.raw[0];
+    return t >= 1 && t <= 4;
+  }
+  return false;
+}
+
+// Headers::parse loop, including its MAX_VLANS / MAX_NET_EXTENSIONS quirk:
+// the header after the limit is still consumed but not recorded.
+// Returns consumed bytes, or -1 on Eth failure.
+enum HKind { H_ETH, H_VLAN, H_V4, H_V6, H_EXT, H_TCP, H_UDP, H_ICMP4, H_ICMP6, H_VXLAN };
+struct HeaderVal {
+  int kind;
+  Vlan vlan;
+  Ipv4 v4;
+  Ipv6 v6;
+  Ext ext;
+  Tcp tcp;
+  Udp udp;
+  Icmp icmp;
+  uint32_t vni;
+};
+
+bool parse_by_ethertype(uint16_t et, Reader &r, HeaderVal &out) {
+  switch (et) {
+    case 0x0800: out.kind = H_V4; return parse_ipv4(r, out.v4);
+    case 0x86dd: out.kind = H_V6; return parse_ipv6(r, out.v6);
+    case 0x8100: case 0x9100: case 0x88a8: out.kind = H_VLAN; return parse_vlan(r, out.vlan);
+    default: return false;
+  }
+}
+
+bool parse_by_proto(uint8_t proto, bool v6_ctx, bool v4_ctx, Reader &r, HeaderVal &out) {
+  switch (proto) {
+    case 6: out.kind = H_TCP; return parse_tcp(r, out.tcp);
+    case 17: out.kind = H_UDP; return parse_udp(r, out.udp);
+    case 1:
+      if (!v4_ctx) return false;
+      out.kind = H_ICMP4; return parse_icmp(r, out.icmp, false);
+    case 58:
+      if (!v6_ctx) return false;
+      out.kind = H_ICMP6; return parse_icmp(r, out.icmp, true);
+    case 51: out.kind = H_EXT; return parse_ext_auth(r, out.ext);
+    case 0: if (!v6_ctx) return false; out.kind = H_EXT; return parse_ext_raw(r, out.ext);
+    case 43: if (!v6_ctx) return false; out.kind = H_EXT; return parse_ext_raw(r, out.ext);
+    case 60: if (!v6_ctx) return false; out.kind = H_EXT; return parse_ext_raw(r, out.ext);
+    case 44: if (!v6_ctx) return false; out.kind = H_EXT; return parse_ext_frag(r, out.ext);
+    default: return false;
+  }
+}
+
+// The v4/v6 context of an AH header: Ipv4Auth parses v4 payload protocols
+// (TCP/UDP/ICMP/AH), Ipv6Auth the v6 ones (net/src/ip_auth/v4.rs:42-60).
+bool parse_next_ctx(const HeaderVal &prior, Reader &r, HeaderVal &out, bool v6ctx) {
+  switch (prior.kind) {
+    case H_ETH: return false;  // handled by caller
+    case H_VLAN: return parse_by_ethertype(prior.vlan.inner, r, out);
+    case H_V4: return parse_by_proto(prior.v4.proto, false, true, r, out);
+    case H_V6: return parse_by_proto(prior.v6.nh, true, false, r, out);
+    case H_EXT: {
+      // Ipv4Auth::parse_payload: TCP/UDP/ICMP/AH only (net/src/ip_auth)
+      uint8_t nh = prior.ext.nh;
+      if (!v6ctx) {
+        if (nh == 6 || nh == 17 || nh == 1 || nh == 51) return parse_by_proto(nh, false, true, r, out);
+        return false;
+      }
+      return parse_by_proto(nh, true, false, r, out);  // ext_parse.rs dispatch
+    }
+    case H_UDP:
+      // Udp::parse_payload: VXLAN only on dport 4789 (net/src/udp/mod.rs:152-166)
+      if (prior.udp.dport == 4789) {
+        out.kind = H_VXLAN;
+        return parse_vxlan(r, out.vni);
+      }
+      return false;
+    default:
+      // TCP / VXLAN: no further parse.  ICMP errors would parse an embedded
+      // packet; ICMP error messages are outside this slice (handled by the
+      // caller, see DESIGN.md "scope").
+      return false;
+  }
+}
+
+int parse_headers(const uint8_t *p, size_t len, Headers &h) {
+  Reader r{p, len, 0};
+  if (len > 65535) return -1;
+  if (!parse_eth(r, h.eth)) return -1;
+  h.has_eth = true;
+  HeaderVal prior{};
+  // first hop after Eth
+  HeaderVal nxt{};
+  bool ok = parse_by_ethertype(h.eth.type, r, nxt);
+  bool v6ctx = false;
+  if (!ok) return (int)r.pos;
+  prior = nxt;
+  for (;;) {
+    HeaderVal next{};
+    bool have_next = parse_next_ctx(prior, r, next, v6ctx);
+    bool brk = false;
+    switch (prior.kind) {
+      case H_V4: h.net = 4; h.v4 = prior.v4; v6ctx = false; break;
+      case H_V6: h.net = 6; h.v6 = prior.v6; v6ctx = true; break;
+      case H_TCP: h.l4 = L4_TCP; h.tcp = prior.tcp; break;
+      case H_UDP: h.l4 = L4_UDP; h.udp = prior.udp; break;
+      case H_ICMP4: h.l4 = L4_ICMP4; h.icmp = prior.icmp; break;
+      case H_ICMP6: h.l4 = L4_ICMP6; h.icmp = prior.icmp; break;
+      case H_VXLAN: h.has_vxlan = true; h.vni = prior.vni; break;
+      case H_VLAN:
+        if (h.vlans.size() < 4) h.vlans.push_back(prior.vlan); else brk = true;
+        break;
+      case H_EXT:
+        if (h.ext.size() < 3) h.ext.push_back(prior.ext); else brk = true;
+        break;
+    }
+    if (brk || !have_next) break;
+    prior = next;
+  }
+  return (int)r.pos;
+}
+
+// ---------------------------------------------------------------------------
+// Deparse (Headers::deparse, net/src/headers/mod.rs:617-691)
+// ---------------------------------------------------------------------------
+int deparse_ipv4(const Ipv4 &h, uint8_t *q) {
+  int hl = h.hlen();
+  q[0] = (uint8_t)(0x40 | (hl / 4));
+  q[1] = (uint8_t)((h.dscp << 2) | h.ecn);
+  put16(q + 2, h.total_len);
+  put16(q + 4, h.id);
+  q[6] = (uint8_t)((h.df ? 0x40 : 0) | (h.mf ? 0x20 : 0) | ((h.frag >> 8) & 0x1f));
+  q[7] = h.frag & 0xff;
+  q[8] = h.ttl;
+  q[9] = h.proto;
+  put16(q + 10, h.csum);
+  memcpy(q + 12, h.src, 4);
+  memcpy(q + 16, h.dst, 4);
+  memcpy(q + 20, h.opts, h.opt_len);
+  return hl;
+}
+
+// etherparse Ipv4Header::calc_header_checksum (no 0 -> 0xffff mapping)
+uint16_t ipv4_checksum(const Ipv4 &h) {
+  uint8_t tmp[60];
+  Ipv4 c = h;
+  c.csum = 0;
+  int n = deparse_ipv4(c, tmp);
+  Sum16 s;
+  s.add_slice(tmp, n);
+  return s.ones_complement();
+}
+
+int deparse_ipv6(const Ipv6 &h, uint8_t *q) {
+  q[0] = (uint8_t)(0x60 | (h.tc >> 4));
+  q[1] = (uint8_t)(((h.tc & 0xf) << 4) | ((h.flow >> 16) & 0xf));
+  q[2] = (h.flow >> 8) & 0xff;
+  q[3] = h.flow & 0xff;
+  put16(q + 4, h.plen);
+  q[6] = h.nh;
+  q[7] = h.hop;
+  memcpy(q + 8, h.src, 16);
+  memcpy(q + 24, h.dst, 16);
+  return 40;
+}
+
+int deparse_tcp(const Tcp &t, uint8_t *q) {
+  put16(q, t.sport);
+  put16(q + 2, t.dport);
+  put32(q + 4, t.seq);
+  put32(q + 8, t.ack);
+  q[12] = (uint8_t)((t.doff << 4) | (t.ns ? 1 : 0));
+  q[13] = t.flags;
+  put16(q + 14, t.win);
+  put16(q + 16, t.csum);
+  put16(q + 18, t.urg);
+  memcpy(q + 20, t.opts, t.hlen() - 20);
+  return t.hlen();
+}
+
+int deparse_headers(const Headers &h, uint8_t *q) {
+  int o = 0;
+  if (h.has_eth) {
+    memcpy(q, h.eth.dst, 6);
+    memcpy(q + 6, h.eth.src, 6);
+    put16(q + 12, h.eth.type);
+    o = 14;
+  }
+  for (auto &v : h.vlans) {
+    put16(q + o, v.tci);
+    put16(q + o + 2, v.inner);
+    o += 4;
+  }
+  if (h.net == 0) return o;
+  if (h.net == 4) o += deparse_ipv4(h.v4, q + o);
+  else o += deparse_ipv6(h.v6, q + o);
+  for (auto &e : h.ext) {
+    memcpy(q + o, e.bytes.data(), e.bytes.size());
+    o += (int)e.bytes.size();
+  }
+  switch (h.l4) {
+    case L4_NONE: return o;
+    case L4_TCP: o += deparse_tcp(h.tcp, q + o); break;
+    case L4_UDP:
+      put16(q + o, h.udp.sport); put16(q + o + 2, h.udp.dport);
+      put16(q + o + 4, h.udp.len); put16(q + o + 6, h.udp.csum);
+      o += 8;
+      break;
+    default:
+      memcpy(q + o, h.icmp.raw, h.icmp.hlen);
+      o += h.icmp.hlen;
+      break;
+  }
+  if (h.has_vxlan) {
+    // Vxlan::deparse (net/src/vxlan/mod.rs:132-145): flags normalized
+    q[o] = 0x08; q[o + 1] = q[o + 2] = q[o + 3] = 0;
+    q[o + 4] = (h.vni >> 16) & 0xff; q[o + 5] = (h.vni >> 8) & 0xff; q[o + 6] = h.vni & 0xff;
+    q[o + 7] = 0;
+    o += 8;
+  }
+  return o;
+}
+
+// Headers::update_checksums (net/src/headers/mod.rs:894-929)
+void update_checksums(Headers &h, const uint8_t *pay, size_t plen) {
+  if (h.net == 0) return;
+  if (h.net == 4) h.v4.csum = ipv4_checksum(h.v4);
+  if (h.has_vxlan) return;
+  Sum16 s;
+  switch (h.l4) {
+    case L4_NONE: return;
+    case L4_UDP: {
+      // etherparse UdpHeader::calc_checksum_ipv4/6: pseudo header uses the
+      // header's length field; 0 result -> 0xffff
+      if (h.net == 4) { s.add_slice(h.v4.src, 4); s.add_slice(h.v4.dst, 4); s.add2(0, 17); s.add_u16(h.udp.len); }
+      else { s.add_slice(h.v6.src, 16); s.add_slice(h.v6.dst, 16);
+             s.add_u16(0); s.add_u16(h.udp.len); s.add2(0, 0); s.add2(0, 17); }
+      s.add_u16(h.udp.sport); s.add_u16(h.udp.dport); s.add_u16(h.udp.len);
+      s.add_slice(pay, plen);
+      uint16_t c = s.ones_complement();
+      h.udp.csum = c == 0 ? 0xffff : c;
+      return;
+    }
+    case L4_TCP: {
+      // etherparse TcpHeader::calc_checksum_ipv4/6: tcp_len = header_len + payload
+      uint32_t tl = (uint32_t)h.tcp.hlen() + (uint32_t)plen;
+      if (h.net == 4) { s.add_slice(h.v4.src, 4); s.add_slice(h.v4.dst, 4); s.add2(0, 6); s.add_u16((uint16_t)tl); }
+      else { s.add_slice(h.v6.src, 16); s.add_slice(h.v6.dst, 16);
+             s.add_u16((uint16_t)(tl >> 16)); s.add_u16((uint16_t)tl); s.add2(0, 0); s.add2(0, 6); }
+      Tcp t = h.tcp;
+      t.csum = 0;
+      uint8_t tmp[60];
+      int n = deparse_tcp(t, tmp);
+      s.add_slice(tmp, n);
+      s.add_slice(pay, plen);
+      h.tcp.csum = s.ones_complement();
+      return;
+    }
+    case L4_ICMP4: {
+      if (h.net != 4) return;  // debug!("illegal") in the reference
+      Icmp c = h.icmp;
+      c.raw[2] = c.raw[3] = 0;
+      s.add_slice(c.raw, c.hlen);
+      s.add_slice(pay, plen);
+      uint16_t v = s.ones_complement();
+      put16(h.icmp.raw + 2, v);
+      return;
+    }
+    case L4_ICMP6: {
+      if (h.net != 6) return;
+      uint32_t tl = (uint32_t)h.icmp.hlen + (uint32_t)plen;
+      s.add_slice(h.v6.src, 16); s.add_slice(h.v6.dst, 16);
+      s.add_u16((uint16_t)(tl >> 16)); s.add_u16((uint16_t)tl); s.add2(0, 0); s.add2(0, 58);
+      Icmp c = h.icmp;
+      c.raw[2] = c.raw[3] = 0;
+      s.add_slice(c.raw, c.hlen);
+      s.add_slice(pay, plen);
+      put16(h.icmp.raw + 2, s.ones_complement());
+      return;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Tables
+// ---------------------------------------------------------------------------
+struct Trie {  // binary trie with LPM (prefix-trie get_lpm semantics)
+  struct Node { int32_t child[2]; int64_t val; };
+  std::vector<Node> nodes;
+  Trie() { nodes.push_back({{-1, -1}, -1}); }
+  void insert(const uint8_t *a, int len, int64_t v) {
+    int32_t n = 0;
+    for (int i = 0; i < len; i++) {
+      int b = bit_at(a, i);
+      if (nodes[n].child[b] < 0) {
+        nodes[n].child[b] = (int32_t)nodes.size();
+        nodes.push_back({{-1, -1}, -1});
+      }
+      n = nodes[n].child[b];
+    }
+    nodes[n].val = v;  // insert replaces (PrefixMap::insert)
+  }
+  int64_t lpm(const uint8_t *a, int bits) const {
+    int64_t best = nodes[0].val;
+    int32_t n = 0;
+    for (int i = 0; i < bits; i++) {
+      n = nodes[n].child[bit_at(a, i)];
+      if (n < 0) break;
+      if (nodes[n].val >= 0) best = nodes[n].val;
+    }
+    return best;
+  }
+};
+
+struct Fib {
+  dp_fib_t d;
+  Trie v4, v6;
+};
+
+struct Rule {
+  dp_rule_t r;
+  uint32_t orig_index;
+};
+
+struct NatEntry {
+  dp_nat_entry_t e;
+  std::vector<dp_port_range_t> prs;
+  std::vector<dp_nat_range_t> ranges;
+};
+struct NatTable {
+  std::vector<NatEntry> entries;
+};
+
+struct MacKey {
+  uint32_t ifindex;
+  Ip ip;
+  bool operator<(const MacKey &o) const {
+    if (ifindex != o.ifindex) return ifindex < o.ifindex;
+    if (ip.fam != o.ip.fam) return ip.fam < o.ip.fam;
+    return memcmp(ip.b, o.ip.b, 16) < 0;
+  }
+};
+
+}  // namespace
+
+struct dpo_tables {
+  int64_t genid = 0;
+  std::vector<Fib> fibs;
+  std::unordered_map<uint32_t, uint32_t> vni_fib;  // vni -> fib index
+  std::unordered_map<uint32_t, uint32_t> vrf_fib;  // vrf id -> fib index
+  std::vector<dp_route_nh_t> nhs;
+  std::vector<dp_fib_entry_t> entries;
+  std::vector<dp_instr_t> instrs;
+  std::unordered_map<uint32_t, dp_iface_t> ifaces;
+  std::map<MacKey, dp_adjacency_t> adjs;
+  std::vector<Rule> acl4, acl6;
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> acl_default;
+  std::vector<Rule> ffr4, ffl4, ffr6, ffl6;
+  std::map<uint32_t, NatTable> nat_dst;                          // src_vni
+  std::map<std::pair<uint32_t, uint32_t>, NatTable> nat_src;     // (src_vni, dst_vni)
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Classifier: first match over rules in match order
+// (acl/src/reference/table.rs:94-101; predicates match-action/src/predicate.rs)
+// ---------------------------------------------------------------------------
+struct Key {
+  uint8_t proto;
+  uint32_t a, b;
+  uint8_t gate;
+  const uint8_t *src, *dst;
+  uint16_t sport, dport;
+};
+
+bool rule_matches(const dp_rule_t &r, const Key &k, int fam) {
+  if ((k.proto & r.proto_mask) != (r.proto_val & r.proto_mask)) return false;
+  if (k.a != r.vni_a || k.b != r.vni_b || k.gate != r.gate) return false;
+  (void)fam;
+  if (!prefix_covers(r.src.addr, r.src.len, k.src)) return false;
+  if (!prefix_covers(r.dst.addr, r.dst.len, k.dst)) return false;
+  if (k.sport < r.sport_lo || k.sport > r.sport_hi) return false;
+  if (k.dport < r.dport_lo || k.dport > r.dport_hi) return false;
+  return true;
+}
+
+int64_t classify(const std::vector<Rule> &rules, const Key &k, int fam) {
+  for (size_t i = 0; i < rules.size(); i++)
+    if (rule_matches(rules[i].r, k, fam)) return (int64_t)i;
+  return -1;
+}
+
+// ---------------------------------------------------------------------------
+// Static NAT lookups (nat/src/static_nat/setup/tables.rs:94-209,
+// lpm/src/trie/ip_port_prefix_trie.rs:80-97, lpm/src/prefix/range_map.rs:68-81)
+// ---------------------------------------------------------------------------
+bool covers_port(const NatEntry &e, uint16_t port) {
+  if (!e.e.is_pat) return true;
+  for (auto &pr : e.prs) if (pr.lo <= port && port <= pr.hi) return true;
+  return false;
+}
+bool covers_all_ports(const NatEntry &e) {
+  if (!e.e.is_pat) return true;
+  uint64_t sum = 0;
+  for (auto &pr : e.prs) sum += (uint64_t)pr.hi - pr.lo + 1;
+  return sum == 65536;
+}
+
+// returns 1 and new addr (+ port, has_new_port) or 0
+int nat_find_mapping(const NatTable &t, const uint8_t *addr, bool has_port, uint16_t port,
+                     uint32_t &new_addr, bool &has_new_port, uint16_t &new_port) {
+  // IpPortPrefixTrie::lookup: matching prefixes, longest first
+  std::vector<const NatEntry *> match;
+  for (auto &e : t.entries)
+    if (e.e.prefix.family == 4 && prefix_covers(e.e.prefix.addr, e.e.prefix.len, addr))
+      match.push_back(&e);
+  std::stable_sort(match.begin(), match.end(), [](const NatEntry *x, const NatEntry *y) {
+    return x->e.prefix.len > y->e.prefix.len;
+  });
+  const NatEntry *hit = nullptr;
+  for (auto *e : match) {
+    if (has_port && covers_port(*e, port)) { hit = e; break; }
+    if (covers_all_ports(*e)) { hit = e; break; }
+  }
+  if (!hit) return 0;
+  uint32_t a = be32(addr);
+  uint32_t net = be32(hit->e.prefix.addr);
+  uint64_t ip_off = (uint64_t)(a - net);
+  if (!hit->e.is_pat) {
+    // AddrTranslationValue::get_entry
+    uint64_t entry_offset = ip_off;
+    if (entry_offset >= hit->e.size) return 0;
+    // ranges_tree.lookup(addr): greatest key start <= addr, then addr <= end
+    const dp_nat_range_t *rg = nullptr;
+    for (auto &r : hit->ranges)
+      if (be32(r.orig_lo_ip) <= a) rg = &r;  // sorted ascending
+    if (!rg || a > be32(rg->orig_hi_ip)) return 0;
+    uint64_t o2 = entry_offset - rg->offset;
+    uint64_t tlen = (uint64_t)be32(rg->tgt_hi_ip) - be32(rg->tgt_lo_ip) + 1;
+    if (o2 >= tlen) return 0;
+    new_addr = (uint32_t)(be32(rg->tgt_lo_ip) + o2);
+    has_new_port = false;
+    return 1;
+  }
+  // PAT: a port is required
+  if (!has_port) return 0;
+  const dp_port_range_t *ppr = nullptr;
+  for (auto &pr : hit->prs) if (pr.lo <= port && port <= pr.hi) { ppr = &pr; break; }
+  if (!ppr) return 0;  // unreachable in the reference
+  uint64_t plen = (uint64_t)ppr->hi - ppr->lo + 1;
+  uint64_t entry_offset = ip_off * plen + (uint64_t)(port - ppr->lo);
+  if (entry_offset >= hit->e.size) return 0;
+  // ranges_tree.lookup(IpPort): lexicographic (ip, port)
+  const dp_nat_range_t *rg = nullptr;
+  for (auto &r : hit->ranges) {
+    uint32_t lo = be32(r.orig_lo_ip);
+    if (lo < a || (lo == a && r.orig_lo_port <= port)) rg = &r;
+  }
+  if (!rg) return 0;
+  uint32_t hi = be32(rg->orig_hi_ip);
+  if (a > hi || (a == hi && port > rg->orig_hi_port)) return 0;
+  uint64_t o2 = entry_offset - rg->offset;
+  uint64_t tpl = (uint64_t)rg->tgt_hi_port - rg->tgt_lo_port + 1;
+  uint64_t tip = (uint64_t)be32(rg->tgt_hi_ip) - be32(rg->tgt_lo_ip) + 1;
+  if (o2 >= tip * tpl) return 0;
+  uint64_t io = o2 / tpl, po = o2 % tpl;
+  new_addr = (uint32_t)(be32(rg->tgt_lo_ip) + io);
+  new_port = (uint16_t)(rg->tgt_lo_port + po);
+  if (new_port == 0) return 0;  // "Found port 0 ... cannot use it for PAT"
+  has_new_port = true;
+  return 1;
+}
+
+// ---------------------------------------------------------------------------
+// Pipeline stages
+// ---------------------------------------------------------------------------
+const dp_iface_t *find_iface(const dpo_tables &T, uint32_t ifindex) {
+  auto it = T.ifaces.find(ifindex);
+  return it == T.ifaces.end() ? nullptr : &it->second;
+}
+
+bool iface_has_mac(const dp_iface_t &i) {
+  return i.iftype == DP_IFT_ETHERNET || i.iftype == DP_IFT_DOT1Q;
+}
+
+// Ingress (dataplane/src/packet_processor/ingress.rs:153-182)
+void stage_ingress(const dpo_tables &T, Packet &p, uint32_t iif) {
+  if (p.is_done()) return;
+  const dp_iface_t *i = find_iface(T, iif);
+  if (!i) { p.done(DP_DONE_INTERFACE_UNKNOWN); return; }
+  if (i->admin_state == DP_IF_DOWN) { p.done(DP_DONE_INTERFACE_ADM_DOWN); return; }
+  if (!iface_has_mac(*i)) { p.done(DP_DONE_INTERFACE_UNSUPPORTED); return; }
+  if (!p.h.has_eth) { p.done(DP_DONE_NOT_ETHERNET); return; }
+  static const uint8_t bcast[6] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
+  if (memcmp(p.h.eth.dst, bcast, 6) == 0) {
+    p.m.flags |= DP_META_IS_L2_BCAST;
+    p.done(DP_DONE_UNHANDLED);
+  } else if (memcmp(p.h.eth.dst, i->mac, 6) == 0) {
+    switch (i->attach) {
+      case DP_ATTACH_VRF:
+        if (p.h.net == 0) { p.done(DP_DONE_NOT_IP); return; }
+        p.m.has_vrf = true;
+        p.m.vrf = i->vrf_id;
+        break;
+      case DP_ATTACH_BRIDGE: p.done(DP_DONE_INTERFACE_UNSUPPORTED); break;
+      default: p.done(DP_DONE_INTERFACE_DETACHED); break;
+    }
+  } else {
+    p.done(DP_DONE_MAC_NOT_FOR_US);
+  }
+}
+
+Ip ip_dst(const Headers &h) { return h.net == 4 ? ip4(h.v4.dst) : ip6(h.v6.dst); }
+
+void hash_ip_bytes(const Headers &h, std::vector<uint8_t> &o) {
+  if (h.net == 0) return;
+  if (h.net == 4) { o.insert(o.end(), h.v4.src, h.v4.src + 4); o.insert(o.end(), h.v4.dst, h.v4.dst + 4); o.push_back(h.v4.proto); }
+  else { o.insert(o.end(), h.v6.src, h.v6.src + 16); o.insert(o.end(), h.v6.dst, h.v6.dst + 16); o.push_back(h.v6.nh); }
+  uint8_t b[4];
+  if (h.l4 == L4_TCP) { put16(b, h.tcp.sport); put16(b + 2, h.tcp.dport); o.insert(o.end(), b, b + 4); }
+  else if (h.l4 == L4_UDP) { put16(b, h.udp.sport); put16(b + 2, h.udp.dport); o.insert(o.end(), b, b + 4); }
+  else if (h.l4 == L4_ICMP4 && (h.icmp.raw[0] == 0 || h.icmp.raw[0] == 8)) o.insert(o.end(), h.icmp.raw + 4, h.icmp.raw + 6);
+  else if (h.l4 == L4_ICMP6 && (h.icmp.raw[0] == 128 || h.icmp.raw[0] == 129)) o.insert(o.end(), h.icmp.raw + 4, h.icmp.raw + 6);
+}
+
+// packet_hash_ecmp (net/src/packet/hash.rs:74-78)
+uint64_t hash_ecmp(const Headers &h) {
+  std::vector<uint8_t> o;
+  hash_ip_bytes(h, o);
+  return rapid(o.data(), o.size());
+}
+// packet_hash_vxlan (net/src/packet/hash.rs:84-88)
+uint16_t hash_vxlan(const Headers &h) {
+  std::vector<uint8_t> o;
+  if (h.has_eth) {
+    o.insert(o.end(), h.eth.src, h.eth.src + 6);
+    o.insert(o.end(), h.eth.dst, h.eth.dst + 6);
+    uint8_t b[2]; put16(b, h.eth.type); o.insert(o.end(), b, b + 2);
+  }
+  for (auto &v : h.vlans) { uint8_t b[2]; put16(b, v.vid()); o.insert(o.end(), b, b + 2); }
+  hash_ip_bytes(h, o);
+  uint64_t x = rapid(o.data(), o.size());
+  return (uint16_t)(x % 16384 + 49152);
+}
+
+int64_t fib_lpm(const Fib &f, const Ip &a) {
+  return a.fam == 4 ? f.v4.lpm(a.b, 32) : f.v6.lpm(a.b, 128);
+}
+
+// Packet::vxlan_decap (net/src/packet/mod.rs:227-259)
+// returns 1 ok, 0 not vxlan, -1 inner parse error
+int vxlan_decap(Packet &p, uint32_t &vni) {
+  if (!p.h.has_vxlan) return 0;
+  bool has_q = p.h.net != 0;
+  uint8_t dscp = 0, ecn = 0;
+  if (p.h.net == 4) { dscp = p.h.v4.dscp; ecn = p.h.v4.ecn; }
+  if (p.h.net == 6) { dscp = p.h.v6.tc >> 2; ecn = p.h.v6.tc & 3; }
+  Headers inner;
+  int c = parse_headers(p.buf + p.pay_start, p.pay_end - p.pay_start, inner);
+  if (c < 0) return -1;
+  vni = p.h.vni;
+  p.pay_start += (uint64_t)c;
+  p.h = inner;
+  if (has_q) { p.m.has_dscp = true; p.m.dscp = dscp; p.m.ecn = ecn; }
+  return 1;
+}
+
+void ipf_decrement_ttl(Packet &p) {  // ipforward.rs:369-390
+  if (p.h.net == 4) {
+    if (p.h.v4.ttl == 0) { p.done(DP_DONE_HOP_LIMIT_EXCEEDED); return; }
+    p.h.v4.ttl--;
+    if (p.h.v4.ttl == 0) p.done(DP_DONE_HOP_LIMIT_EXCEEDED);
+  } else {
+    if (p.h.v6.hop == 0) { p.done(DP_DONE_HOP_LIMIT_EXCEEDED); return; }
+    p.h.v6.hop--;
+    if (p.h.v6.hop == 0) p.done(DP_DONE_HOP_LIMIT_EXCEEDED);
+  }
+}
+
+// IpForwarder::vxlan_encap (ipforward.rs:222-289) + Packet::vxlan_encap
+// (net/src/packet/mod.rs:279-326) + build_vxlan_headers (ipforward.rs:181-219)
+void ipf_vxlan_encap(const dpo_tables &T, Packet &p, const dp_instr_t &in, const Fib &f) {
+  if (!(f.d.flags & DP_FIB_VTEP_HAS_MAC)) { p.done(DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  if (!(in.flags & DP_INSTR_HAS_DMAC)) { p.done(DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  static const uint8_t zero[6] = {0};
+  // set_eth_source: SourceMac::new (non-zero, unicast); no-op without Eth
+  if (memcmp(f.d.vtep_mac, zero, 6) == 0 || (f.d.vtep_mac[0] & 1)) { p.done(DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  if (p.h.has_eth) memcpy(p.h.eth.src, f.d.vtep_mac, 6);
+  // set_eth_destination: DestinationMac::new (non-zero)
+  if (memcmp(in.mac, zero, 6) == 0) { p.done(DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  if (p.h.has_eth) memcpy(p.h.eth.dst, in.mac, 6);
+  if (p.m.flags & DP_META_REFR_CHKSUM) {
+    update_checksums(p.h, p.buf + p.pay_start, p.pay_end - p.pay_start);
+    p.m.flags &= ~DP_META_REFR_CHKSUM;
+  } else if (p.h.net == 4) {
+    p.h.v4.csum = ipv4_checksum(p.h.v4);
+  } else {
+    // `unreachable!()` in the reference (non-IPv4 without refresh): panic.
+    p.done(DP_DONE_INTERNAL_FAILURE);
+    return;
+  }
+  // build_vxlan_headers
+  if (!(f.d.flags & DP_FIB_VTEP_HAS_IP)) { p.done(DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+  const dp_ipaddr_t &sip = f.d.vtep_ip;
+  const dp_ipaddr_t &dip = in.addr;
+  Headers outer;
+  if (sip.family == 4 && dip.family == 4) {
+    if ((sip.addr[0] & 0xf0) == 0xe0 || (sip.addr[0] == 255 && sip.addr[1] == 255 && sip.addr[2] == 255 && sip.addr[3] == 255)) {
+      p.done(DP_DONE_VXLAN_ENCAP_FAILURE); return;
+    }
+    outer.net = 4;
+    Ipv4 &o = outer.v4;
+    memset(&o, 0, sizeof(o));
+    // etherparse Ipv4Header::default(): DF set, id 0, ttl 0, proto 255
+    // (assumption; DESIGN.md "unpinned"); then src/dst/ttl 64/proto UDP
+    o.df = true;
+    memcpy(o.src, sip.addr, 4);
+    memcpy(o.dst, dip.addr, 4);
+    o.ttl = 64;
+    o.proto = 17;
+  } else if (sip.family == 6 && dip.family == 6) {
+    if (sip.addr[0] == 0xff) { p.done(DP_DONE_VXLAN_ENCAP_FAILURE); return; }
+    outer.net = 6;
+    Ipv6 &o = outer.v6;
+    memset(&o, 0, sizeof(o));
+    memcpy(o.src, sip.addr, 16);
+    memcpy(o.dst, dip.addr, 16);
+    o.hop = 64;
+    o.nh = 17;
+  } else {
+    p.done(DP_DONE_VXLAN_ENCAP_FAILURE);
+    return;
+  }
+  // Packet::vxlan_encap: deparse inner headers into the payload front
+  int need = p.h.size();
+  if ((int64_t)p.pay_start - need < (int64_t)p.room_start) {
+    p.done(DP_DONE_VXLAN_ENCAP_FAILURE);  // Prepend error
+    return;
+  }
+  uint16_t sport = hash_vxlan(p.h);
+  deparse_headers(p.h, p.buf + p.pay_start - need);
+  p.pay_start -= (uint64_t)need;
+  uint64_t len = (p.pay_end - p.pay_start) + 16;
+  outer.l4 = L4_UDP;
+  outer.udp.sport = sport;
+  outer.udp.dport = 4789;
+  outer.udp.len = (uint16_t)len;
+  outer.udp.csum = 0;
+  outer.has_vxlan = true;
+  outer.vni = in.vni;
+  // apply_outer_qos_to_ip_headers (net/src/packet/mod.rs:163-188)
+  if (outer.net == 4) {
+    if (p.m.has_dscp) { outer.v4.dscp = p.m.dscp; outer.v4.ecn = p.m.ecn; }
+    outer.v4.total_len = (uint16_t)(outer.v4.hlen() + len);
+    outer.v4.csum = ipv4_checksum(outer.v4);
+  } else {
+    if (p.m.has_dscp) outer.v6.tc = (uint8_t)((p.m.dscp << 2) | p.m.ecn);
+    outer.v6.plen = (uint16_t)len;
+  }
+  p.h = outer;  // no Eth: Egress adds it
+  p.m.dst_vni = in.vni;
+}
+
+void ipf_exec(const dpo_tables &T, Packet &p, const dp_instr_t &in, const Fib &f) {
+  switch (in.kind) {
+    case DP_INSTR_DROP: p.done(DP_DONE_ROUTE_DROP); break;
+    case DP_INSTR_LOCAL: {
+      uint32_t vni = 0;
+      int r = vxlan_decap(p, vni);
+      if (r == 0) { p.done(DP_DONE_LOCAL); break; }
+      if (r < 0) { p.done(DP_DONE_VXLAN_DECAP_FAILURE); break; }
+      auto it = T.vni_fib.find(vni);
+      if (it == T.vni_fib.end()) { p.done(DP_DONE_UNROUTABLE); break; }
+      p.m.src_vni = vni;
+      p.m.has_vrf = true;
+      p.m.vrf = T.fibs[it->second].d.vrf_id;
+      p.m.flags |= DP_META_IS_OVERLAY;
+      break;
+    }
+    case DP_INSTR_ENCAP_VXLAN: ipf_vxlan_encap(T, p, in, f); break;
+    case DP_INSTR_EGRESS:
+      p.m.has_oif = in.flags & DP_INSTR_HAS_IFINDEX;
+      p.m.oif = in.ifindex;
+      p.m.has_nh = in.flags & DP_INSTR_HAS_ADDR;
+      if (p.m.has_nh) { p.m.nh.fam = in.addr.family; memcpy(p.m.nh.b, in.addr.addr, 16); }
+      break;
+  }
+}
+
+// IpForwarder::forward_packet (ipforward.rs:54-121)
+void stage_ipforward(const dpo_tables &T, Packet &p) {
+  if (p.is_done()) return;
+  bool had_vrf = p.m.has_vrf;
+  uint32_t vrf0 = p.m.vrf;
+  const Fib *f = nullptr;
+  if (p.m.dst_vni) {
+    auto it = T.vni_fib.find(p.m.dst_vni);
+    if (p.h.net == 0) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+    if (it == T.vni_fib.end()) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+    f = &T.fibs[it->second];
+  } else if (p.m.has_vrf) {
+    auto it = T.vrf_fib.find(p.m.vrf);
+    if (p.h.net == 0) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+    if (it == T.vrf_fib.end()) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+    f = &T.fibs[it->second];
+  } else {
+    if (p.overlay()) p.done(DP_DONE_INTERNAL_FAILURE);
+    return;
+  }
+  Ip dst = ip_dst(p.h);
+  int64_t nhi = fib_lpm(*f, dst);
+  if (nhi < 0) { p.done(DP_DONE_INTERNAL_FAILURE); return; }  // a /0 always exists
+  const dp_route_nh_t &nh = T.nhs[nhi];
+  uint32_t idx = 0;
+  if (nh.n_entries > 1) idx = (uint32_t)(hash_ecmp(p.h) % nh.n_entries);
+  uint32_t ei = nh.first_entry + idx;
+  const dp_fib_entry_t &e = T.entries[ei];
+  p.m.fib_entry = ei;
+  bool iplocal = e.n_instr == 1 && T.instrs[e.first_instr].kind == DP_INSTR_LOCAL;
+  if (!iplocal) {
+    ipf_decrement_ttl(p);
+    if (p.is_done()) return;
+  }
+  for (uint32_t k = 0; k < e.n_instr; k++) {
+    ipf_exec(T, p, T.instrs[e.first_instr + k], *f);
+    if (p.is_done()) return;
+  }
+  if (p.m.has_vrf == had_vrf && (!had_vrf || p.m.vrf == vrf0)) p.m.has_vrf = false;
+}
+
+// FlowFilter (flow-filter/src/lib.rs:75-246, context/tables.rs:800-915)
+void stage_flow_filter(const dpo_tables &T, Packet &p) {
+  if (p.is_done() || !p.overlay() || p.m.dst_vni) return;
+  if (p.h.net == 0) { p.done(DP_DONE_NOT_IP); return; }
+  if (!p.m.src_vni) { p.done(DP_DONE_UNROUTABLE); return; }
+  uint8_t proto = p.h.net == 4 ? p.h.v4.proto : p.h.v6.nh;
+  uint16_t sp = 0, dpp = 0;
+  if (p.h.l4 == L4_TCP) { sp = p.h.tcp.sport; dpp = p.h.tcp.dport; }
+  if (p.h.l4 == L4_UDP) { sp = p.h.udp.sport; dpp = p.h.udp.dport; }
+  const uint8_t *src = p.h.net == 4 ? p.h.v4.src : p.h.v6.src;
+  const uint8_t *dst = p.h.net == 4 ? p.h.v4.dst : p.h.v6.dst;
+  const auto &rem = p.h.net == 4 ? T.ffr4 : T.ffr6;
+  const auto &loc = p.h.net == 4 ? T.ffl4 : T.ffl6;
+  static const uint8_t zero16[16] = {0};
+  // RemoteKey has no source fields (flow-filter/src/context/tables.rs:192-207)
+  Key k{proto, p.m.src_vni, 0 /* GateVni: dst_vpcd None */, 0, zero16, dst, 0, dpp};
+  int64_t ri = classify(rem, k, p.h.net);
+  if (ri < 0) { p.done(DP_DONE_FILTERED); return; }  // DestinationMiss
+  const dp_rule_t &rv = rem[ri].r;
+  // LocalKey has no destination fields (tables.rs:211-229)
+  Key k2{proto, p.m.src_vni, rv.action, 0 /* SourceGate::Ungated */, src, zero16, sp, 0};
+  int64_t li = classify(loc, k2, p.h.net);
+  if (li < 0) { p.done(DP_DONE_FILTERED); return; }  // SourceMiss
+  uint32_t src_nat = loc[li].r.action, dst_nat = rv.action2;
+  p.m.dst_vni = rv.action;
+  // set_nat_requirements (flow-filter/src/lib.rs:233-246)
+  auto apply = [&](uint32_t mode, uint32_t stat_flag) {
+    if (mode == DP_NAT_MASQUERADE) p.m.flags |= DP_META_REQ_MASQUERADE;
+    if (mode == DP_NAT_STATIC) p.m.flags |= stat_flag;
+    if (mode == DP_NAT_PORT_FORWARDING) p.m.flags |= DP_META_REQ_PORT_FORWARDING;
+  };
+  apply(src_nat, DP_META_REQ_STATIC_NAT_SRC);
+  apply(dst_nat, DP_META_REQ_STATIC_NAT_DST);
+}
+
+// AclFilter (acl-filter/src/lib.rs:51-152)
+void stage_acl(const dpo_tables &T, Packet &p) {
+  if (p.is_done() || !p.overlay()) return;
+  if (!p.m.src_vni || !p.m.dst_vni) { p.done(DP_DONE_UNROUTABLE); return; }
+  if (p.h.net == 0) { p.done(DP_DONE_NOT_IP); return; }
+  uint8_t proto = p.h.net == 4 ? p.h.v4.proto : p.h.v6.nh;
+  uint16_t sp = 0, dpp = 0;
+  if (p.h.l4 == L4_TCP) { sp = p.h.tcp.sport; dpp = p.h.tcp.dport; }
+  if (p.h.l4 == L4_UDP) { sp = p.h.udp.sport; dpp = p.h.udp.dport; }
+  const uint8_t *src = p.h.net == 4 ? p.h.v4.src : p.h.v6.src;
+  const uint8_t *dst = p.h.net == 4 ? p.h.v4.dst : p.h.v6.dst;
+  const auto &tab = p.h.net == 4 ? T.acl4 : T.acl6;
+  Key k{proto, p.m.src_vni, p.m.dst_vni, 0, src, dst, sp, dpp};
+  int64_t ri = classify(tab, k, p.h.net);
+  uint32_t action;
+  if (ri >= 0) {
+    action = tab[ri].r.action;
+    p.m.acl_rule = tab[ri].orig_index;
+    p.m.acl = action == DP_ACL_DENY ? 2 : 1;
+  } else {
+    auto it = T.acl_default.find({p.m.src_vni, p.m.dst_vni});
+    if (it != T.acl_default.end()) {
+      action = it->second;
+      p.m.acl = action == DP_ACL_DENY ? 4 : 3;
+    } else {
+      action = DP_ACL_ALLOW;
+      p.m.acl = 5;
+    }
+  }
+  if (action == DP_ACL_DENY) p.done(DP_DONE_ACL_DROPPED);
+}
+
+// StaticNat (nat/src/static_nat/nf.rs:158-368)
+void stage_static_nat(const dpo_tables &T, Packet &p) {
+  if (p.is_done()) return;
+  uint32_t need = DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST;
+  if (!(p.m.flags & need)) return;
+  if (p.m.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) return;  // no ICMP errors here
+  if (!p.m.src_vni || !p.m.dst_vni) { p.done(DP_DONE_UNROUTABLE); return; }
+  auto dt = T.nat_dst.find(p.m.src_vni);
+  bool has_src_tables = false;
+  for (auto &kv : T.nat_src) if (kv.first.first == p.m.src_vni) { has_src_tables = true; break; }
+  if (dt == T.nat_dst.end() && !has_src_tables) { p.done(DP_DONE_UNROUTABLE); return; }  // MissingTable
+  if (p.h.net == 0) { p.done(DP_DONE_NOT_IP); return; }
+  bool modified = false;
+  bool has_sp = p.h.l4 == L4_TCP || p.h.l4 == L4_UDP;
+  uint16_t *psp = p.h.l4 == L4_TCP ? &p.h.tcp.sport : &p.h.udp.sport;
+  uint16_t *pdp = p.h.l4 == L4_TCP ? &p.h.tcp.dport : &p.h.udp.dport;
+  if ((p.m.flags & DP_META_REQ_STATIC_NAT_SRC) && !(p.m.flags & DP_META_NATTED_SRC)) {
+    bool mod = false;
+    auto st = T.nat_src.find({p.m.src_vni, p.m.dst_vni});
+    if (st != T.nat_src.end() && p.h.net == 4) {
+      uint32_t na; bool hp; uint16_t np;
+      if (nat_find_mapping(st->second, p.h.v4.src, has_sp, has_sp ? *psp : 0, na, hp, np)) {
+        // UnicastIpAddr::try_from: not multicast / broadcast
+        bool unicast = !((na >> 28) == 0xe || na == 0xffffffffu);
+        if (unicast) {
+          if (na != be32(p.h.v4.src)) { put32(p.h.v4.src, na); mod = true; }
+          if (has_sp && hp && np != *psp) { *psp = np; mod = true; }
+        }
+      }
+    }
+    if (mod) p.m.flags |= DP_META_NATTED_SRC;
+    modified |= mod;
+  }
+  if ((p.m.flags & DP_META_REQ_STATIC_NAT_DST) && !(p.m.flags & DP_META_NATTED_DST)) {
+    bool mod = false;
+    if (dt != T.nat_dst.end() && p.h.net == 4) {
+      uint32_t na; bool hp; uint16_t np;
+      if (nat_find_mapping(dt->second, p.h.v4.dst, has_sp, has_sp ? *pdp : 0, na, hp, np)) {
+        if (na != be32(p.h.v4.dst)) { put32(p.h.v4.dst, na); mod = true; }
+        if (has_sp && hp && np != *pdp) { *pdp = np; mod = true; }
+      }
+    }
+    if (mod) p.m.flags |= DP_META_NATTED_DST;
+    modified |= mod;
+  }
+  if (modified) p.m.flags |= DP_META_REFR_CHKSUM;
+}
+
+bool adj_lookup(const dpo_tables &T, const Ip &ip, uint32_t oif, uint8_t mac[6]) {
+  MacKey k{oif, ip};
+  if (k.ip.fam == 4) memset(k.ip.b + 4, 0, 12);
+  auto it = T.adjs.find(k);
+  if (it == T.adjs.end()) return false;
+  memcpy(mac, it->second.mac, 6);
+  return true;
+}
+
+// Egress (dataplane/src/packet_processor/egress.rs:54-208)
+void stage_egress(const dpo_tables &T, Packet &p) {
+  if (p.is_done()) return;
+  if (!p.m.has_oif) { p.done(DP_DONE_ROUTE_FAILURE); return; }
+  uint32_t oif = p.m.oif;
+  Ip nh;
+  if (p.m.has_nh) nh = p.m.nh;
+  else if (p.h.net) nh = ip_dst(p.h);
+  else { p.done(DP_DONE_NOT_IP); return; }
+  uint8_t dmac[6];
+  if (!adj_lookup(T, nh, oif, dmac)) { p.done(DP_DONE_MISS_L2_RESOLUTION); return; }
+  static const uint8_t zero[6] = {0};
+  if (memcmp(dmac, zero, 6) == 0) { p.done(DP_DONE_INVALID_DST_MAC); return; }
+  const dp_iface_t *i = find_iface(T, oif);
+  if (!i) { p.done(DP_DONE_INTERFACE_UNKNOWN); return; }
+  if (i->admin_state == DP_IF_DOWN) { p.done(DP_DONE_INTERFACE_ADM_DOWN); return; }
+  if (i->oper_state == DP_IF_DOWN) { p.done(DP_DONE_INTERFACE_OPER_DOWN); return; }
+  if (!iface_has_mac(*i)) { p.done(DP_DONE_INTERFACE_UNSUPPORTED); return; }
+  if (p.h.has_eth) {
+    memcpy(p.h.eth.src, i->mac, 6);
+    memcpy(p.h.eth.dst, dmac, 6);
+  } else {
+    uint16_t et;
+    if (p.h.net == 4) et = 0x0800;
+    else if (p.h.net == 6) et = 0x86dd;
+    else { p.done(DP_DONE_MISSING_ETHER_TYPE); return; }
+    p.h.has_eth = true;
+    memcpy(p.h.eth.src, i->mac, 6);
+    memcpy(p.h.eth.dst, dmac, 6);
+    p.h.eth.type = et;
+  }
+  p.done(DP_DONE_DELIVERED);
+}
+
+// Packet::serialize (net/src/packet/mod.rs:342-374)
+void serialize(Packet &p) {
+  update_checksums(p.h, p.buf + p.pay_start, p.pay_end - p.pay_start);
+  p.m.flags &= ~DP_META_REFR_CHKSUM;
+  int need = p.h.size();
+  if ((int64_t)p.pay_start - need < (int64_t)p.room_start) {
+    p.done_force(DP_DONE_NO_HEAD_ROOM);
+    return;
+  }
+  deparse_headers(p.h, p.buf + p.pay_start - need);
+  p.pay_start -= (uint64_t)need;
+}
+
+void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pkt_out_t &out) {
+  Packet p;
+  p.buf = buf;
+  p.room_start = in.off >= DP_HEADROOM ? in.off - DP_HEADROOM : 0;
+  out.off = in.off;
+  out.len = in.len;
+  out.acl = 0;
+  out.oif = out.dst_vni = out.src_vni = 0;
+  out.fib_entry = out.acl_rule = UINT32_MAX;
+  int c = parse_headers(buf + in.off, in.len, p.h);
+  if (c < 0) {  // Packet::new fails: frame rejected by the driver (worker.rs:409-421)
+    out.done = DP_DONE_NOT_ETHERNET;
+    out.meta_flags = 0;
+    return;
+  }
+  p.pay_start = in.off + (uint64_t)c;
+  p.pay_end = in.off + (uint64_t)in.len;
+
+  if (in.flags & DP_IN_SEEDED_OVERLAY) {
+    // state right after IP-Forward-1's decap (ipforward.rs:140-161)
+    auto it = T.vni_fib.find(in.src_vni);
+    if (it == T.vni_fib.end()) p.done(DP_DONE_UNROUTABLE);
+    else {
+      p.m.src_vni = in.src_vni;
+      p.m.has_vrf = true;
+      p.m.vrf = T.fibs[it->second].d.vrf_id;
+      p.m.flags |= DP_META_IS_OVERLAY;
+    }
+  } else {
+    stage_ingress(T, p, in.iif);
+    stage_ipforward(T, p);  // IP-Forward-1
+  }
+  // IcmpErrorHandler (nat/src/icmp_handler/nf.rs:184-194): overlay ICMP
+  // error messages need the stateful handler -- outside this slice.
+  if (!p.is_done() && p.overlay() && icmp_is_error(p.h)) p.done(DP_DONE_UNHANDLED);
+  // FlowLookup: identity with an empty flow table
+  stage_flow_filter(T, p);
+  stage_acl(T, p);
+  stage_static_nat(T, p);
+  // PortForwarder / Masquerade: identity (no REQ_* flags from static-only tables)
+  if (!p.is_done() && (p.m.flags & (DP_META_REQ_MASQUERADE | DP_META_REQ_PORT_FORWARDING)))
+    p.done(DP_DONE_INTERNAL_FAILURE);
+  stage_ipforward(T, p);  // IP-Forward-2
+  stage_egress(T, p);
+  if (p.m.done == DP_DONE_DELIVERED) {
+    // Underlay ICMP error messages carry embedded headers whose checksums the
+    // reference refreshes too: outside this slice.
+    if (icmp_is_error(p.h)) p.done_force(DP_DONE_UNHANDLED);
+    else serialize(p);
+  }
+  out.done = p.m.done < 0 ? (uint8_t)DP_DONE_NONE : (uint8_t)p.m.done;
+  out.meta_flags = p.m.flags;
+  out.oif = p.m.has_oif ? p.m.oif : 0;
+  out.dst_vni = p.m.dst_vni;
+  out.src_vni = p.m.src_vni;
+  out.fib_entry = p.m.fib_entry;
+  out.acl_rule = p.m.acl_rule;
+  out.acl = p.m.acl;
+  if (p.m.done == DP_DONE_DELIVERED) {
+    out.off = (uint32_t)p.pay_start;
+    out.len = (uint16_t)(p.pay_end - p.pay_start);
+  }
+}
+
+bool valid_prefix(const dp_prefix_t &p) {
+  int bits = p.family == 4 ? 32 : 128;
+  if (p.family != 4 && p.family != 6) return false;
+  if (p.len > bits) return false;
+  for (int i = p.len; i < bits; i++) if (bit_at(p.addr, i)) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dpo_tables_build(const dp_tables_desc_t *d, dpo_tables_t **out) {
+  if (!d || !out) return DP_EINVAL;
+  auto T = std::make_unique<dpo_tables>();
+  T->genid = d->genid;
+  for (uint32_t i = 0; i < d->n_fibs; i++) {
+    Fib f;
+    f.d = d->fibs[i];
+    T->fibs.push_back(std::move(f));
+    T->vrf_fib[d->fibs[i].vrf_id] = i;
+  }
+  for (uint32_t i = 0; i < d->n_vni_fibs; i++) {
+    if (d->vni_fibs[i].fib >= d->n_fibs) return DP_EINVAL;
+    T->vni_fib[d->vni_fibs[i].vni] = d->vni_fibs[i].fib;
+  }
+  T->nhs.assign(d->route_nhs, d->route_nhs + d->n_route_nhs);
+  T->entries.assign(d->entries, d->entries + d->n_entries);
+  T->instrs.assign(d->instrs, d->instrs + d->n_instrs);
+  for (auto &e : T->entries) {
+    if (e.n_instr == 0 || e.n_instr > 4 || e.first_instr + e.n_instr > d->n_instrs) return DP_EINVAL;
+    // Supported instruction forms: at most one Encap, and no Local/Encap
+    // after an Encap (a re-encapsulated packet is never routed again here).
+    int encaps = 0;
+    for (uint32_t k = 0; k < e.n_instr; k++) {
+      uint32_t kd = d->instrs[e.first_instr + k].kind;
+      if (kd > DP_INSTR_EGRESS) return DP_EINVAL;
+      if (encaps && (kd == DP_INSTR_LOCAL || kd == DP_INSTR_ENCAP_VXLAN)) return DP_ENOTSUP;
+      if (kd == DP_INSTR_ENCAP_VXLAN) encaps++;
+    }
+  }
+  for (auto &n : T->nhs)
+    if (n.n_entries == 0 || n.first_entry + n.n_entries > d->n_entries) return DP_EINVAL;
+  // Fib::default(): /0 -> drop group for v4 and v6 (routing/src/fib/fibtype.rs:76-91)
+  uint32_t drop_nh = (uint32_t)T->nhs.size();
+  T->instrs.push_back(dp_instr_t{DP_INSTR_DROP, 0, 0, 0, {}, {0}, {0}});
+  T->entries.push_back(dp_fib_entry_t{(uint32_t)T->instrs.size() - 1, 1});
+  T->nhs.push_back(dp_route_nh_t{(uint32_t)T->entries.size() - 1, 1});
+  for (auto &f : T->fibs) {
+    uint8_t z[16] = {0};
+    f.v4.insert(z, 0, drop_nh);
+    f.v6.insert(z, 0, drop_nh);
+  }
+  for (uint64_t i = 0; i < d->n_routes; i++) {
+    const dp_route_t &r = d->routes[i];
+    if (r.fib >= d->n_fibs || r.nh >= d->n_route_nhs || !valid_prefix(r.prefix)) return DP_EINVAL;
+    Fib &f = T->fibs[r.fib];
+    if (r.prefix.family == 4) f.v4.insert(r.prefix.addr, r.prefix.len, r.nh);
+    else f.v6.insert(r.prefix.addr, r.prefix.len, r.nh);
+  }
+  for (uint32_t i = 0; i < d->n_ifaces; i++) T->ifaces[d->ifaces[i].ifindex] = d->ifaces[i];
+  for (uint32_t i = 0; i < d->n_adjs; i++) {
+    MacKey k{d->adjs[i].ifindex, Ip{}};
+    k.ip.fam = d->adjs[i].addr.family;
+    memcpy(k.ip.b, d->adjs[i].addr.addr, 16);
+    if (k.ip.fam == 4) memset(k.ip.b + 4, 0, 12);
+    T->adjs[k] = d->adjs[i];
+  }
+  auto load = [&](const dp_rule_t *rs, uint32_t n, std::vector<Rule> &dst, bool sort_prio) -> int {
+    for (uint32_t i = 0; i < n; i++) {
+      if (!valid_prefix(rs[i].src) || !valid_prefix(rs[i].dst)) return DP_EINVAL;
+      dst.push_back(Rule{rs[i], i});
+    }
+    if (sort_prio)
+      std::stable_sort(dst.begin(), dst.end(), [](const Rule &a, const Rule &b) {
+        return a.r.priority > b.r.priority;
+      });
+    return 0;
+  };
+  int rc;
+  if ((rc = load(d->acl_v4, d->n_acl_v4, T->acl4, false))) return rc;
+  if ((rc = load(d->acl_v6, d->n_acl_v6, T->acl6, false))) return rc;
+  if ((rc = load(d->ff_remote_v4, d->n_ff_remote_v4, T->ffr4, true))) return rc;
+  if ((rc = load(d->ff_local_v4, d->n_ff_local_v4, T->ffl4, true))) return rc;
+  if ((rc = load(d->ff_remote_v6, d->n_ff_remote_v6, T->ffr6, true))) return rc;
+  if ((rc = load(d->ff_local_v6, d->n_ff_local_v6, T->ffl6, true))) return rc;
+  for (auto *v : {&T->ffr4, &T->ffr6})
+    for (auto &r : *v) {
+      if (r.r.action2 == DP_NAT_MASQUERADE || r.r.action2 == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
+      if (r.r.src.len != 0 || r.r.sport_lo != 0 || r.r.sport_hi != 65535 || r.r.gate != 0) return DP_EINVAL;
+    }
+  for (auto *v : {&T->ffl4, &T->ffl6})
+    for (auto &r : *v) {
+      if (r.r.action == DP_NAT_MASQUERADE || r.r.action == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
+      if (r.r.dst.len != 0 || r.r.dport_lo != 0 || r.r.dport_hi != 65535) return DP_EINVAL;
+    }
+  for (auto *v : {&T->acl4, &T->acl6})
+    for (auto &r : *v)
+      if (r.r.gate != 0) return DP_EINVAL;
+  for (uint32_t i = 0; i < d->n_acl_defaults; i++)
+    T->acl_default[{d->acl_defaults[i].src_vni, d->acl_defaults[i].dst_vni}] = d->acl_defaults[i].action;
+  for (uint32_t i = 0; i < d->n_nat_tables; i++) {
+    const dp_nat_table_t &nt = d->nat_tables[i];
+    NatTable *tab;
+    if (nt.kind == DP_NAT_TABLE_DST) tab = &T->nat_dst[nt.src_vni];
+    else tab = &T->nat_src[{nt.src_vni, nt.dst_vni}];
+    if (nt.first_entry + nt.n_entries > d->n_nat_entries) return DP_EINVAL;
+    for (uint32_t j = 0; j < nt.n_entries; j++) {
+      const dp_nat_entry_t &e = d->nat_entries[nt.first_entry + j];
+      if (e.prefix.family != 4 || !valid_prefix(e.prefix)) return DP_ENOTSUP;  // NAT44 only
+      NatEntry ne;
+      ne.e = e;
+      if (e.first_port_range + e.n_port_ranges > d->n_nat_port_ranges) return DP_EINVAL;
+      if (e.first_range + e.n_ranges > d->n_nat_ranges) return DP_EINVAL;
+      ne.prs.assign(d->nat_port_ranges + e.first_port_range, d->nat_port_ranges + e.first_port_range + e.n_port_ranges);
+      ne.ranges.assign(d->nat_ranges + e.first_range, d->nat_ranges + e.first_range + e.n_ranges);
+      // IpPortPrefixTrie::insert: a later insert of the same prefix replaces
+      bool replaced = false;
+      for (auto &x : tab->entries)
+        if (x.e.prefix.len == e.prefix.len && memcmp(x.e.prefix.addr, e.prefix.addr, 4) == 0) {
+          x = ne; replaced = true; break;
+        }
+      if (!replaced) tab->entries.push_back(std::move(ne));
+    }
+  }
+  *out = T.release();
+  return 0;
+}
+
+void dpo_tables_free(dpo_tables_t *t) { delete t; }
+
+int dpo_process_burst(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes,
+                      const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, uint64_t *stats) {
+  if (!t || (!buf && n)) return DP_EINVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    if (in[i].off < DP_HEADROOM || (uint64_t)in[i].off + in[i].len > buf_bytes) return DP_EINVAL;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    process_one(*t, buf, in[i], out[i]);
+    if (stats && out[i].done < DP_DONE_COUNT) stats[out[i].done]++;
+  }
+  return 0;
+}
+
+int dpo_process_parallel(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes,
+                         const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
+                         uint32_t burst, uint32_t threads) {
+  if (!t || threads == 0 || burst == 0) return DP_EINVAL;
+  std::atomic<uint32_t> next{0};
+  std::vector<std::thread> th;
+  for (uint32_t k = 0; k < threads; k++) {
+    th.emplace_back([&]() {
+      for (;;) {
+        uint32_t s = next.fetch_add(burst);
+        if (s >= n) break;
+        uint32_t e = std::min(n, s + burst);
+        dpo_process_burst(t, buf, buf_bytes, in + s, out + s, e - s, nullptr);
+      }
+    });
+  }
+  for (auto &x : th) x.join();
+  return 0;
+}
+
+uint16_t dpo_checksum_ipv4_header(const uint8_t *hdr, uint32_t hlen) {
+  uint8_t tmp[60];
+  memcpy(tmp, hdr, hlen);
+  tmp[10] = tmp[11] = 0;
+  Sum16 s;
+  s.add_slice(tmp, hlen);
+  return s.ones_complement();
+}
+
+int64_t dpo_lpm(const dpo_tables_t *t, uint32_t fib, uint8_t family, const uint8_t *addr) {
+  if (!t || fib >= t->fibs.size()) return -1;
+  Ip a;
+  a.fam = family;
+  memcpy(a.b, addr, family == 4 ? 4 : 16);
+  return fib_lpm(t->fibs[fib], a);
+}
+
+int64_t dpo_acl_lookup(const dpo_tables_t *t, uint8_t family, uint8_t proto, uint32_t src_vni,
+                       uint32_t dst_vni, const uint8_t *src, const uint8_t *dst, int has_ports,
+                       uint16_t sport, uint16_t dport) {
+  Key k{proto, src_vni, dst_vni, 0, src, dst, (uint16_t)(has_ports ? sport : 0),
+        (uint16_t)(has_ports ? dport : 0)};
+  const auto &tab = family == 4 ? t->acl4 : t->acl6;
+  int64_t r = classify(tab, k, family);
+  return r < 0 ? -1 : (int64_t)tab[r].orig_index;
+}
+
+int dpo_nat_lookup(const dpo_tables_t *t, uint32_t kind, uint32_t src_vni, uint32_t dst_vni,
+                   const uint8_t *addr4, int has_port, uint16_t port, uint8_t *new_addr4,
+                   uint16_t *new_port) {
+  const NatTable *tab = nullptr;
+  if (kind == 0) {
+    auto it = t->nat_dst.find(src_vni);
+    if (it != t->nat_dst.end()) tab = &it->second;
+  } else {
+    auto it = t->nat_src.find({src_vni, dst_vni});
+    if (it != t->nat_src.end()) tab = &it->second;
+  }
+  if (!tab) return 0;
+  uint32_t na; bool hp; uint16_t np = 0;
+  if (!nat_find_mapping(*tab, addr4, has_port != 0, port, na, hp, np)) return 0;
+  if (kind == 1 && ((na >> 28) == 0xe || na == 0xffffffffu)) return 0;
+  put32(new_addr4, na);
+  *new_port = hp ? np : 0;
+  return 1;
+}
+
+uint64_t dpo_hash_bytes(const uint8_t *p, uint32_t len) { return rapid(p, len); }
+
+}  // extern "C"

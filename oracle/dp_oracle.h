@@ -1,0 +1,73 @@
+/* SPDX-License-Identifier: Apache-2.0
+ *
+ * TEST INFRASTRUCTURE -- NOT PRODUCT CODE.
+ *
+ * CPU oracle: a plain C++ restatement of the reference (githedgehog/dataplane)
+ * per-burst packet path, used only as the parity checker by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg.  The product
+ * (dataplane_amd/, libdpgpu.so) never links or calls it.
+ *
+ * Parity pinning: the reference is Rust and cannot be compiled here (no
+ * cargo/rustc).  This restatement is pinned by the
+ * reference's own known-answer tests transcribed into tests/golden/ (NAT
+ * KATs of nat/src/static_nat/test.rs, ACL first-match of
+ * acl/src/reference/table.rs, flow-filter priority, prefix masks, TTL chain,
+ * VXLAN QoS preservation) -- see tests/test_oracle_kats.py.  Third-party
+ * arithmetic (etherparse 0.21.0, prefix-trie 0.10.1, rapidhash 4.5.1) is
+ * restated from their published behaviour; rapidhash-dependent values (ECMP
+ * index, VXLAN UDP source port) are "parity unpinned" (SURVEY.md §8c).
+ *
+ * It exposes the same descriptor types as include/dpgpu.h so tests compare
+ * the GPU path and the oracle on identical inputs.
+ */
+#ifndef DP_ORACLE_H
+#define DP_ORACLE_H
+
+#include "../include/dpgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dpo_tables dpo_tables_t;
+
+/* Build oracle tables from the lowered descriptors (same semantics as
+ * dp_tables_publish).  Returns 0 / negative errno. */
+int dpo_tables_build(const dp_tables_desc_t *desc, dpo_tables_t **out);
+void dpo_tables_free(dpo_tables_t *t);
+
+/* Run the reference stage sequence over a burst, in place, exactly like
+ * dp_process_burst.  Single-threaded per call. */
+int dpo_process_burst(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes,
+                      const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
+                      uint64_t *stats);
+
+/* Multi-threaded CPU baseline: splits the burst into bursts of `burst`
+ * packets (DPDK PKT_BURST_SIZE = 64, dpdk/src/queue/rx.rs:174) over
+ * `threads` threads.  Returns 0 / negative errno. */
+int dpo_process_parallel(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes,
+                         const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
+                         uint32_t burst, uint32_t threads);
+
+/* Primitive restatements exposed for unit tests. */
+uint16_t dpo_checksum_ipv4_header(const uint8_t *hdr, uint32_t hlen);
+/* LPM of one address in one FIB: returns route nh index or -1. */
+int64_t dpo_lpm(const dpo_tables_t *t, uint32_t fib, uint8_t family,
+                const uint8_t *addr);
+/* First-match ACL over a table: returns rule index or -1. */
+int64_t dpo_acl_lookup(const dpo_tables_t *t, uint8_t family, uint8_t proto,
+                       uint32_t src_vni, uint32_t dst_vni, const uint8_t *src,
+                       const uint8_t *dst, int has_ports, uint16_t sport,
+                       uint16_t dport);
+/* Static NAT find_{src,dst}_mapping: returns 1 if mapped (new addr/port
+ * written, port 0 = unchanged), 0 if not. kind: 0 dst, 1 src. */
+int dpo_nat_lookup(const dpo_tables_t *t, uint32_t kind, uint32_t src_vni,
+                   uint32_t dst_vni, const uint8_t *addr4, int has_port,
+                   uint16_t port, uint8_t *new_addr4, uint16_t *new_port);
+/* rapidhash-style 64-bit hash restatement (parity unpinned). */
+uint64_t dpo_hash_bytes(const uint8_t *p, uint32_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

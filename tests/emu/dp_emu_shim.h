@@ -1,0 +1,23 @@
+// TEST INFRASTRUCTURE: host build of the per-packet kernel body
+// (dataplane_amd/csrc/dp_kernel.hip compiled with -DDP_EMU) so the GPU
+// algorithm can be debugged against the oracle without a GPU.  Never part
+// of the product: libdpgpu.so is built from the same file without DP_EMU.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#ifndef __device__
+#define __device__
+#endif
+#ifndef __host__
+#define __host__
+#endif
+#define __global__
+#define __forceinline__ inline
+#define __launch_bounds__(x)
+#define __shared__
+struct uint4 { uint32_t x, y, z, w; };
+static inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+static inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x); }
+static inline uint64_t __umul64hi(uint64_t a, uint64_t b) {
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+}
