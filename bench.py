@@ -1,0 +1,197 @@
+# SPDX-License-Identifier: Apache-2.0
+"""Benchmark of the MI355X per-burst packet path (BASELINE.json metric).
+
+One step = one pass of the whole path (parse -> Ingress/IP-Forward/flow-filter/
+ACL/static NAT/IP-Forward/Egress -> serialize) over one resident burst of
+synthetic packets.  Bursts are pre-staged in HBM (one copy per
+step, so every step processes pristine packets in place); the timed region
+contains only the kernel launches.  Multi-GPU: one process per GPU, each
+processing its own shard (packets are independent: weak scaling, no
+data-path collective).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from dataplane_amd import GpuPathNf, _abi as A  # noqa: E402
+from dataplane_amd.workload import ALGO_BYTES, CONFIG_NAMES, Workload  # noqa: E402
+
+METRIC = "Mpps device-resident (64B IPv4, 1M-route LPM + 10k ACL + NAT) at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(w: Workload, sample: int, budget_s: float) -> dict:
+    """The CPU oracle (C++ restatement of the reference pipeline) on this
+    host's cores, DPDK-sized bursts of 64, on a bounded sample."""
+    from oracle.pyoracle import Oracle  # test-infrastructure checker, timed as the baseline
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    o = Oracle(w.tables)
+    n = min(sample, w.n)
+    inp = w.inp[:n].copy()
+    out = np.zeros(n, dtype=A.PKT_OUT)
+    done, t_total, reps = 0, 0.0, 0
+    while t_total < budget_s and reps < 50:
+        buf = w.fresh_buf()
+        t0 = time.perf_counter()
+        o.process_parallel(buf, inp, out, threads=threads, burst=64)
+        t_total += time.perf_counter() - t0
+        done += n
+        reps += 1
+    o.close()
+    return {"value": round(done / t_total / 1e6, 4), "unit": "Mpps", "cores": threads,
+            "kind": "port",
+            "sample": f"{reps} x {n} packets of the same workload, bursts of 64, "
+                      f"C++ restatement of the reference pipeline (oracle/), {t_total:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--packets", type=int, default=2_000_000, help="packets per step per GPU")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-sample", type=int, default=500_000)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    cfg = args.config
+    t0 = time.perf_counter()
+    w = Workload(cfg, args.packets, seed=args.seed + 1000 * rank)
+    log(rank, f"[bench] workload C{cfg}: {w.n} packets, built in {time.perf_counter() - t0:.1f}s")
+    nf = GpuPathNf(local)
+    t0 = time.perf_counter()
+    nf.publish(w.tables)
+    log(rank, f"[bench] tables published in {time.perf_counter() - t0:.1f}s, "
+              f"{nf.device_table_bytes() / 2**20:.1f} MiB device image")
+
+    n = w.n
+    bb = (w.buf.nbytes + 255) & ~255
+    nbuf = args.warmup + args.steps
+    pristine = torch.from_numpy(w.buf).to(dev)
+    bufs = torch.empty((nbuf, bb), dtype=torch.uint8, device=dev)
+    for k in range(nbuf):
+        bufs[k, :w.buf.nbytes].copy_(pristine)
+    dinp = torch.from_numpy(w.inp.view(np.uint8)).to(dev)
+    dout = torch.empty(n * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+    dstats = torch.zeros(A.DONE_COUNT, dtype=torch.int64, device=dev)
+    # a dedicated (non-default) stream: the kernel and the timing events must
+    # share it (the default stream's handle is 0, which the ABI maps to the
+    # context's own stream)
+    stream = torch.cuda.Stream(dev)
+    sptr = stream.cuda_stream
+    torch.cuda.synchronize(dev)
+
+    def step(k):
+        nf.process_device(bufs[k].data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n,
+                          dstats.data_ptr(), sptr)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    dstats.zero_()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    ev0.record(stream)
+    for k in range(args.steps):
+        step(args.warmup + k)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+        st = dstats.clone()
+        torch.distributed.all_reduce(st)
+        hist = st.cpu().numpy()
+    else:
+        hist = dstats.cpu().numpy()
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_pkts = world * n * args.steps
+    value = total_pkts / elapsed / 1e6
+    delivered = int(hist[A.DONE["Delivered"]])
+    if int(hist.sum()) != total_pkts or delivered == 0:
+        raise RuntimeError(f"bad DoneReason histogram: {hist.tolist()}")
+
+    result = None
+    if rank == 0:
+        achieved = n * ALGO_BYTES[cfg] / (kernel_ms / 1e3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "kernel": "dp_pipeline_kernel", "kernel_ms": round(kernel_ms, 4),
+                    "bytes_per_pkt": ALGO_BYTES[cfg]}
+        result = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mpps", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded, SURVEY.md §8d)",
+            "config": {"workload": f"C{cfg}: " + CONFIG_NAMES[cfg], "packets_per_step_per_gpu": n,
+                       "frame_bytes_per_step_per_gpu": w.frame_bytes, "seed": args.seed,
+                       "parallelism": f"dp{world} (independent shards)"},
+            "roofline": roofline,
+            "done_histogram": {A.DONE_NAMES[i]: int(c) for i, c in enumerate(hist) if c},
+        }
+        if world == 1 and not args.no_host:
+            # host-origin rate: pinned host buffers, H2D + kernel + D2H per burst
+            pinned = torch.empty(w.buf.nbytes, dtype=torch.uint8).pin_memory()
+            pnp = pinned.numpy()
+            reps, t_host = 3, 0.0
+            for _ in range(reps + 1):
+                pnp[:] = w.buf
+                t0 = time.perf_counter()
+                nf.process_arrays(pnp, w.inp)
+                dt = time.perf_counter() - t0
+                if _ > 0:
+                    t_host += dt
+            result["host_inclusive_mpps"] = round(reps * n / t_host / 1e6, 3)
+        if world == 1 and not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(w, args.cpu_sample, args.cpu_budget)
+        print(json.dumps(result), flush=True)
+    nf.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,137 @@
+# SPDX-License-Identifier: Apache-2.0
+"""Host-side mirror of the reference's stage API for this path.
+
+The reference drives the path through ``NetworkFunction`` stages
+(``pipeline/src/static_nf.rs:12-32``)::
+
+    fn process(&mut self, input: impl Iterator<Item = Packet<Buf>>) -> impl Iterator<Item = Packet<Buf>>
+    fn set_data(&mut self, data: Arc<PipelineData>)
+
+``GpuPathNf`` keeps that shape: ``process`` materialises the burst (as
+``FlowFilter::process`` does, ``flow-filter/src/lib.rs:357-362``), runs the
+whole Ingress..Egress + serialize block on the GPU through the C ABI, applies
+the returned DoneReason / metadata to every packet and yields them all
+(``KEEP`` semantics: packets are marked, never removed).  ``set_data`` carries
+the generation id.  Device-resident bursts go through ``process_device``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Iterable, Iterator, List, Optional
+
+import numpy as np
+
+from . import _abi as A
+
+
+@dataclass
+class PipelineData:
+    """pipeline/src/pipeline.rs:22-42"""
+    genid: int = 0
+
+
+@dataclass
+class Packet:
+    """A frame plus the PacketMeta fields this path reads and writes."""
+    frame: bytes
+    iif: int = 1
+    src_vni: int = 0            # seeded src_vpcd (harness idiom, DP_IN_SEEDED_OVERLAY)
+    seeded_overlay: bool = False
+    # results (net/src/packet/meta.rs:138-154)
+    done: Optional[str] = None
+    meta_flags: int = 0
+    oif: Optional[int] = None
+    dst_vni: Optional[int] = None
+    fib_entry: Optional[int] = None
+    acl_rule: Optional[int] = None
+
+    def is_done(self) -> bool:
+        return self.done is not None
+
+
+class GpuPathNf:
+    """One context per worker thread (worker.rs:175); one HIP stream each."""
+
+    def __init__(self, device: int = 0, name: str = "gpu-path"):
+        self.name = name
+        self.lib = A.gpu_lib()
+        h = C.c_void_p()
+        A.check(self.lib.dp_ctx_create(device, C.byref(h)), "dp_ctx_create", self.lib)
+        self.ctx = h
+        self.data = PipelineData()
+        self._keep = None
+
+    # -- table publication --------------------------------
+    def publish(self, tables_ptr) -> None:
+        """Publish lowered tables (a POINTER(TablesDesc)); bursts that start
+        after this returns see the new generation."""
+        A.check(self.lib.dp_tables_publish(self.ctx, tables_ptr), "dp_tables_publish", self.lib)
+        self.data.genid = int(self.lib.dp_tables_genid(self.ctx))
+
+    def set_data(self, data: PipelineData) -> None:
+        self.data = data
+
+    # -- NetworkFunction::process -------------------------------------------
+    def process(self, packets: Iterable[Packet]) -> Iterator[Packet]:
+        burst: List[Packet] = list(packets)
+        if not burst:
+            return iter(())
+        offs, total = [], 0
+        for p in burst:
+            total += A.HEADROOM
+            offs.append(total)
+            total = (total + len(p.frame) + 15) & ~15
+        buf = np.zeros(total + 16, dtype=np.uint8)
+        inp = np.zeros(len(burst), dtype=A.PKT_IN)
+        for i, p in enumerate(burst):
+            buf[offs[i]:offs[i] + len(p.frame)] = np.frombuffer(p.frame, dtype=np.uint8)
+            inp[i] = (offs[i], len(p.frame), A.IN_SEEDED_OVERLAY if p.seeded_overlay else 0,
+                      p.iif, p.src_vni)
+        out = self.process_arrays(buf, inp)
+        for i, p in enumerate(burst):
+            r = out[i]
+            d = int(r["done"])
+            p.done = A.DONE_NAMES[d] if d < A.DONE_COUNT else None
+            p.meta_flags = int(r["meta_flags"])
+            p.oif = int(r["oif"]) or None
+            p.dst_vni = int(r["dst_vni"]) or None
+            p.fib_entry = None if r["fib_entry"] == 0xFFFFFFFF else int(r["fib_entry"])
+            p.acl_rule = None if r["acl_rule"] == 0xFFFFFFFF else int(r["acl_rule"])
+            if d == A.DONE["Delivered"]:
+                p.frame = bytes(buf[r["off"]:r["off"] + r["len"]])
+        return iter(burst)
+
+    def process_arrays(self, buf: np.ndarray, inp: np.ndarray,
+                       stats: Optional[np.ndarray] = None) -> np.ndarray:
+        """Host-origin burst, in place (dp_process_burst)."""
+        out = np.zeros(len(inp), dtype=A.PKT_OUT)
+        sp = stats.ctypes.data if stats is not None else None
+        A.check(self.lib.dp_process_burst(self.ctx, buf.ctypes.data, buf.nbytes, inp.ctypes.data,
+                                          out.ctypes.data, len(inp), sp),
+                "dp_process_burst", self.lib)
+        return out
+
+    def process_device(self, dev_buf: int, buf_bytes: int, dev_in: int, dev_out: int, n: int,
+                       dev_stats: Optional[int] = None, stream: Optional[int] = None) -> None:
+        """Device-resident burst (dp_process_burst_device): raw device pointers."""
+        A.check(self.lib.dp_process_burst_device(self.ctx, dev_buf, buf_bytes, dev_in, dev_out,
+                                                 n, dev_stats, stream),
+                "dp_process_burst_device", self.lib)
+
+    def synchronize(self) -> None:
+        A.check(self.lib.dp_ctx_synchronize(self.ctx), "dp_ctx_synchronize", self.lib)
+
+    def device_table_bytes(self) -> int:
+        return int(self.lib.dp_tables_device_bytes(self.ctx))
+
+    def close(self) -> None:
+        if self.ctx:
+            self.lib.dp_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

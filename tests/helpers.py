@@ -1,0 +1,27 @@
+"""Shared test helpers: compare two runs of the path (GPU / emulation vs oracle)."""
+import numpy as np
+
+from dataplane_amd import _abi as A
+
+
+def compare(out_ref, buf_ref, out_dut, buf_dut, inp, label=""):
+    """Bit-exact: every dp_pkt_out_t field, and every serialized byte of every
+    Delivered packet (plus the whole buffer, which also pins that nothing else
+    was touched)."""
+    mism = np.nonzero(out_ref != out_dut)[0]
+    msg = []
+    for i in mism[:5]:
+        msg.append(f"pkt {i}: ref {out_ref[i]} dut {out_dut[i]}")
+    assert len(mism) == 0, f"{label}: {len(mism)} metadata mismatches\n" + "\n".join(msg)
+    deliv = np.nonzero(out_ref["done"] == A.DONE["Delivered"])[0]
+    for i in deliv:
+        o, l = int(out_ref[i]["off"]), int(out_ref[i]["len"])
+        if not np.array_equal(buf_ref[o:o + l], buf_dut[o:o + l]):
+            d = np.nonzero(buf_ref[o:o + l] != buf_dut[o:o + l])[0]
+            raise AssertionError(f"{label}: pkt {i} bytes differ at {d[:8]}")
+    assert np.array_equal(buf_ref, buf_dut), f"{label}: buffers differ outside delivered frames"
+
+
+def hist(out):
+    h = np.bincount(out["done"].astype(np.int64), minlength=256)
+    return {A.DONE_NAMES[i] if i < A.DONE_COUNT else str(i): int(c) for i, c in enumerate(h) if c}

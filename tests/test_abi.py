@@ -1,0 +1,43 @@
+"""The C-ABI library loads and exports every symbol include/dpgpu.h declares;
+the ctypes mirror matches the C struct layouts.  No GPU compute here."""
+import ctypes as C
+import os
+import re
+
+from dataplane_amd import _abi as A
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "dpgpu.h")).read()
+    return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(dp_\w+)\(", src, flags=re.M)))
+
+
+def test_header_symbols_match_list():
+    assert declared_symbols() == sorted(A.GPU_SYMBOLS)
+
+
+def test_library_exports_every_symbol():
+    lib = A.gpu_lib()
+    for s in A.GPU_SYMBOLS:
+        assert hasattr(lib, s), s
+    assert lib.dp_abi_version() == A.ABI_VERSION
+
+
+def test_struct_layouts_match_c():
+    lib = A.work_lib()
+    for name, st in A.STRUCTS.items():
+        assert C.sizeof(st) == lib.dpw_sizeof(name.encode()), name
+    assert lib.dpw_sizeof(b"dp_pkt_in_t") == A.PKT_IN.itemsize
+    assert lib.dpw_sizeof(b"dp_pkt_out_t") == A.PKT_OUT.itemsize
+
+
+def test_ctx_create_without_gpu_fails_loudly():
+    """No silent CPU fallback: without a device the context cannot be created."""
+    import torch
+    if torch.cuda.is_available():
+        return
+    lib = A.gpu_lib()
+    h = C.c_void_p()
+    assert lib.dp_ctx_create(0, C.byref(h)) == -19  # DP_ENODEV

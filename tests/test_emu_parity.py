@@ -1,0 +1,20 @@
+"""CPU: the GPU kernel's per-packet code, compiled for the host (tests/emu),
+against the oracle on seeded workloads of every config shape."""
+import pytest
+
+from dataplane_amd import _abi as A
+from dataplane_amd.workload import Workload
+from oracle.pyoracle import Oracle
+import pyemu
+
+from helpers import compare
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
+def test_emu_matches_oracle(cfg):
+    w = Workload(cfg, 3000, seed=100 + cfg, n_routes_v4=3000, n_routes_v6=1500, n_acl=400,
+                 n_nat=48, tcp_percent=25)
+    b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
+    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+    o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT)
+    compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg}")
