@@ -73,6 +73,11 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
+    # ablation knobs (0 = the config's default table sizes)
+    ap.add_argument("--routes-v4", type=int, default=0)
+    ap.add_argument("--routes-v6", type=int, default=0)
+    ap.add_argument("--acl", type=int, default=0)
+    ap.add_argument("--nat", type=int, default=0)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -90,7 +95,8 @@ def main() -> None:
 
     cfg = args.config
     t0 = time.perf_counter()
-    w = Workload(cfg, args.packets, seed=args.seed + 1000 * rank)
+    w = Workload(cfg, args.packets, seed=args.seed + 1000 * rank, n_routes_v4=args.routes_v4,
+                 n_routes_v6=args.routes_v6, n_acl=args.acl, n_nat=args.nat)
     log(rank, f"[bench] workload C{cfg}: {w.n} packets, built in {time.perf_counter() - t0:.1f}s")
     nf = GpuPathNf(local)
     t0 = time.perf_counter()
@@ -168,6 +174,9 @@ def main() -> None:
             "data": "synthetic (seeded, SURVEY.md §8d)",
             "config": {"workload": f"C{cfg}: " + CONFIG_NAMES[cfg], "packets_per_step_per_gpu": n,
                        "frame_bytes_per_step_per_gpu": w.frame_bytes, "seed": args.seed,
+                       "table_overrides": {k: v for k, v in dict(routes_v4=args.routes_v4,
+                                           routes_v6=args.routes_v6, acl=args.acl,
+                                           nat=args.nat).items() if v},
                        "parallelism": f"dp{world} (independent shards)"},
             "roofline": roofline,
             "done_histogram": {A.DONE_NAMES[i]: int(c) for i, c in enumerate(hist) if c},

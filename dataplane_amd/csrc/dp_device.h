@@ -114,8 +114,10 @@ struct AdjMap {
 struct FieldIdx {
   uint64_t bounds;     // offset of uint64_t[2*n] (hi, lo) interval starts, ascending
   uint64_t rows;       // offset of uint32_t[n] row index per interval
+  uint64_t jump;       // offset of uint32_t[65537]: interval containing the start of
+                       // each 16-bit top-bits bucket (0: no jump table, n small)
   uint32_t n;          // number of intervals (>= 1; bounds[0] = 0)
-  uint32_t pad;
+  uint32_t shift;      // key >> shift = bucket (v4 ip: 16, port: 0, v6: hi >> 48)
 };
 
 struct Group {
@@ -160,6 +162,7 @@ struct NatEnt {
 struct NatTab {
   uint64_t bounds;           // uint32_t[n] interval starts (host order)
   uint64_t longest;          // int32_t[n] longest covering entry (global idx) or -1
+  uint64_t jump;             // uint32_t[65537] bucket (addr >> 16) -> interval (0: none)
   uint32_t n;
   uint32_t pad;
 };

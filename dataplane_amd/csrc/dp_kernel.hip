@@ -30,7 +30,7 @@ namespace {
 using namespace dpd;
 
 constexpr int TPB = 128;
-constexpr int WIN = 256;          // header window bytes per packet
+constexpr int WIN = 128;          // header window bytes per packet (rest read from HBM)
 constexpr int SLAB = WIN + 4;     // 65 dwords: conflict-free byte reads
 constexpr uint8_t DONE_NONE = 255;
 
@@ -66,6 +66,7 @@ __device__ __forceinline__ bool hash_find(const Img &g, const HashMap &m, uint32
 // ---------------------------------------------------------------------------
 struct Frame {
   uint8_t *lds;     // this work-item's slab
+  uint8_t *hs;      // this work-item's 64-byte LDS hash scratch
   uint8_t *g;       // frame start in HBM
   int shift;        // frame start & 15
   int len;
@@ -78,6 +79,18 @@ struct Frame {
     return ((uint32_t)b(f) << 24) | ((uint32_t)b(f + 1) << 16) | ((uint32_t)b(f + 2) << 8) | b(f + 3);
   }
 };
+
+__device__ __forceinline__ uint64_t mac_at(const Frame &F, int f) {
+  uint64_t m = 0;
+  for (int i = 0; i < 6; i++) m = (m << 8) | F.b(f + i);
+  return m;
+}
+__device__ __forceinline__ uint64_t load_mac(const uint8_t *p) {
+  uint64_t m = 0;
+  for (int i = 0; i < 6; i++) m = (m << 8) | p[i];
+  return m;
+}
+__device__ __forceinline__ uint8_t mac_b(uint64_t m, int i) { return (uint8_t)(m >> (40 - 8 * i)); }
 
 // ---------------------------------------------------------------------------
 // Parsed header stack (offsets are frame-relative)
@@ -105,7 +118,7 @@ struct Hdr {
 
 // try to parse one header of kind `k` at frame offset `pos`; returns its
 // length (0 on failure)
-__device__ int try_parse(const Frame &F, int k, int pos, uint32_t &aux) {
+__device__ __forceinline__ int try_parse(const Frame &F, int k, int pos, uint32_t &aux) {
   int rem = F.len - pos;
   switch (k) {
     case HK_VLAN: {  // Vlan::parse: VID 0 / 4095 invalid
@@ -201,7 +214,7 @@ __device__ __forceinline__ int kind_of_proto(uint8_t p, bool v6) {
 
 // Headers::parse (net/src/headers/mod.rs:474-578) incl. the MAX_VLANS /
 // MAX_NET_EXTENSIONS quirk.  Returns false if the Ethernet header is invalid.
-__device__ bool parse(const Frame &F, int hb, Hdr &H) {
+__device__ __forceinline__ bool parse(const Frame &F, int hb, Hdr &H) {
   H.hb = hb; H.nvlan = 0; H.net = 0; H.next = 0; H.ext_len = 0; H.l4 = L4_NONE;
   H.vx = false; H.vni = 0; H.net_off = H.net_hlen = 0; H.l4_off = H.l4_hlen = 0; H.vx_off = 0;
   int rem = F.len - hb;
@@ -247,8 +260,9 @@ __device__ bool parse(const Frame &F, int hb, Hdr &H) {
       case HK_V6: H.net = 6; H.net_off = cur_pos; H.net_hlen = 40; v6ctx = true; break;
       case HK_EXT_RAW: case HK_EXT_FRAG: case HK_EXT_AUTH:
         if (H.next < 3) {
-          H.ext_off[H.next] = cur_pos;
-          H.ext_kind[H.next] = (uint8_t)cur;
+          if (H.next == 0) { H.ext_off[0] = cur_pos; H.ext_kind[0] = (uint8_t)cur; }
+          else if (H.next == 1) { H.ext_off[1] = cur_pos; H.ext_kind[1] = (uint8_t)cur; }
+          else { H.ext_off[2] = cur_pos; H.ext_kind[2] = (uint8_t)cur; }
           H.ext_len += cur_len;
           H.next++;
         } else brk = true;
@@ -293,7 +307,7 @@ struct State {
   uint32_t fib_entry, acl_rule;
   uint8_t acl;
   // current header field values
-  uint8_t emac[12];      // dst(6) src(6)
+  uint64_t edst, esrc;   // current Ethernet dst / src (48-bit, byte 0 on top)
   bool eth_dirty;
   uint8_t ttl;           // v4 ttl / v6 hop limit
   uint32_t v4src, v4dst; // host order
@@ -308,14 +322,15 @@ struct State {
   bool inner_l4_ck;      // inner L4 checksum recomputed at encap
   uint16_t inner_v4_ck, inner_l4_ck_val;
   bool o_eth;            // Egress added the outer Ethernet header
-  uint8_t o_mac[12];
+  uint64_t odst, osrc;   // outer Ethernet (encap)
   int pay_start;         // frame-relative payload start (inner after decap)
 };
 
 __device__ __forceinline__ void done(State &S, uint8_t r) { if (S.done == DONE_NONE) S.done = r; }
 
 __device__ __forceinline__ void load_fields(const Frame &F, const Hdr &H, State &S) {
-  for (int i = 0; i < 12; i++) S.emac[i] = F.b(H.hb + i);
+  S.edst = mac_at(F, H.hb);
+  S.esrc = mac_at(F, H.hb + 6);
   S.eth_dirty = false;
   if (H.net == 4) {
     S.ttl = F.b(H.net_off + 8);
@@ -361,7 +376,7 @@ __device__ __forceinline__ bool icmp_is_error(const Frame &F, const Hdr &H) {
 // rapidhash-style hash (same restatement as the oracle; parity vs the
 // reference is UNPINNED)
 // ---------------------------------------------------------------------------
-struct HBuf { uint8_t b[64]; int n; };
+struct HBuf { uint8_t *b; int n; };  // per-thread LDS scratch (no private-array scratch)
 __device__ __forceinline__ void hb_put(HBuf &h, uint8_t x) { h.b[h.n++] = x; }
 __device__ __forceinline__ void mum(uint64_t &a, uint64_t &b) {
   uint64_t lo = a * b, hi = __umul64hi(a, b);
@@ -376,7 +391,7 @@ __device__ __forceinline__ uint64_t rd64(const uint8_t *p) {
 __device__ __forceinline__ uint64_t rd32(const uint8_t *p) {
   return (uint64_t)p[0] | ((uint64_t)p[1] << 8) | ((uint64_t)p[2] << 16) | ((uint64_t)p[3] << 24);
 }
-__device__ uint64_t rapid(const uint8_t *p, int len) {
+__device__ __forceinline__ uint64_t rapid(const uint8_t *p, int len) {
   const uint64_t s0 = 0x2d358dccaa6c78a5ull, s1 = 0x8bb84b93962eacc9ull, s2 = 0x4b33a62ed433d4a3ull;
   uint64_t seed = 0xbdd89aa982704029ull;
   seed ^= mixh(seed ^ s0, s1) ^ (uint64_t)len;
@@ -419,7 +434,7 @@ __device__ uint64_t rapid(const uint8_t *p, int len) {
   return mixh(a ^ s0 ^ (uint64_t)len, b ^ s1);
 }
 
-__device__ void hash_ip_fields(const Frame &F, const Hdr &H, const State &S, HBuf &h) {
+__device__ __forceinline__ void hash_ip_fields(const Frame &F, const Hdr &H, const State &S, HBuf &h) {
   if (H.net == 4) {
     for (int i = 0; i < 4; i++) hb_put(h, (uint8_t)(S.v4src >> (24 - 8 * i)));
     for (int i = 0; i < 4; i++) hb_put(h, (uint8_t)(S.v4dst >> (24 - 8 * i)));
@@ -443,19 +458,18 @@ __device__ void hash_ip_fields(const Frame &F, const Hdr &H, const State &S, HBu
 // ---------------------------------------------------------------------------
 // LPM (Poptrie-style, see dp_tables.cpp build_poptrie)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t key_bits(const Addr16 &a, int off, int n, int width) {
-  // bits [off, off+n) of the key, zero-padded beyond `width`
-  uint32_t v = 0;
-  for (int i = 0; i < n; i++) {
-    int bit = off + i;
-    uint32_t x = 0;
-    if (bit < width) x = (a.w[bit >> 5] >> (31 - (bit & 31))) & 1;
-    v = (v << 1) | x;
-  }
-  return v;
+// 6 bits of the key at [off, off+6), zero-padded past the address width
+// (v4 keys carry zeros in w[1..3]); the key is held as two u64 halves.
+__device__ __forceinline__ uint32_t key6(uint64_t hi, uint64_t lo, int off) {
+  uint64_t x;
+  if (off == 0) x = hi;
+  else if (off < 64) x = (hi << off) | (lo >> (64 - off));
+  else if (off < 128) x = lo << (off - 64);
+  else x = 0;
+  return (uint32_t)(x >> 58);
 }
 
-__device__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
+__device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
   const uint32_t *direct = g.at<uint32_t>(L.direct);
   uint32_t idx;
   if (L.width == 32) idx = a.w[0] >> (32 - L.dbits);
@@ -466,10 +480,11 @@ __device__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
   const uint32_t *leaves = g.at<uint32_t>(g.im.pt_leaves);
   int off = (int)L.dbits;
   uint32_t ni = e;
+  const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1], klo = ((uint64_t)a.w[2] << 32) | a.w[3];
   for (int guard = 0; guard < 24; guard++) {
     const PtNode &nd = nodes[ni];
     uint64_t vec = nd.vec, lv = nd.leafvec;
-    uint32_t v = key_bits(a, off, 6, (int)L.width);
+    uint32_t v = key6(khi, klo, off);
     uint64_t bit = 1ull << v;
     if (vec & bit) {
       ni = nd.base1 + (uint32_t)__popcll(vec & (bit - 1));
@@ -487,31 +502,54 @@ __device__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
 // ---------------------------------------------------------------------------
 struct Key128 { uint64_t hi, lo; };
 
-__device__ __forceinline__ uint32_t interval_row(const Img &g, const FieldIdx &f, Key128 k) {
-  const uint64_t *b = g.at<uint64_t>(f.bounds);
-  uint32_t lo = 0, hi = f.n;  // find last j with bounds[j] <= k
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    uint64_t bh = b[2 * mid], bl = b[2 * mid + 1];
-    bool le = bh < k.hi || (bh == k.hi && bl <= k.lo);
-    if (le) lo = mid; else hi = mid;
-  }
-  return g.at<uint32_t>(f.rows)[lo];
+// bucket of a key for a field's jump table
+__device__ __forceinline__ uint32_t bucket_of(const FieldIdx &f, Key128 k) {
+  return f.shift == 48 ? (uint32_t)(k.hi >> 48) : (uint32_t)(k.lo >> f.shift) & 0xffff;
 }
 
-// returns global rule index or -1
-__device__ int64_t classify(const Img &g, const Classifier &C, uint32_t a, uint32_t bb, uint32_t gate,
-                            uint8_t proto, Key128 src, Key128 dst, uint16_t sp, uint16_t dp) {
+// returns global rule index or -1.  The four field searches (elementary
+// interval containing the key) run in lockstep so their loads overlap.
+__device__ __forceinline__ int64_t classify(const Img &g, const Classifier &C, uint32_t a, uint32_t bb,
+                                            uint32_t gate, uint8_t proto, Key128 src, Key128 dst,
+                                            uint16_t sp, uint16_t dp) {
   uint32_t gi;
   if (!hash_find(g, C.groups, a, bb, gate, gi)) return -1;
   const Group G = g.at<Group>(C.group_recs)[gi];
+  Key128 key[4] = {src, dst, Key128{0, sp}, Key128{0, dp}};
+  uint32_t lo[4], hi[4];
+#pragma unroll
+  for (int f = 0; f < 4; f++) {
+    lo[f] = 0;
+    hi[f] = G.f[f].n;
+    if (G.f[f].jump) {
+      const uint32_t *jt = g.at<uint32_t>(G.f[f].jump);
+      uint32_t t = bucket_of(G.f[f], key[f]);
+      lo[f] = jt[t];
+      hi[f] = jt[t + 1] + 1;
+    }
+  }
+  for (int it = 0; it < 20; it++) {
+    bool any = false;
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+      if (hi[f] - lo[f] > 1) {
+        uint32_t mid = (lo[f] + hi[f]) >> 1;
+        const uint64_t *b = g.at<uint64_t>(G.f[f].bounds) + 2 * (uint64_t)mid;
+        uint64_t bh = b[0], bl = b[1];
+        bool le = bh < key[f].hi || (bh == key[f].hi && bl <= key[f].lo);
+        if (le) lo[f] = mid; else hi[f] = mid;
+        any = true;
+      }
+    }
+    if (!any) break;
+  }
   const uint64_t *pool = g.at<uint64_t>(G.pool);
   uint32_t stride = G.sum_words + G.words;
   uint32_t r0 = g.at<uint16_t>(G.proto_rows)[proto];
-  uint32_t r1 = interval_row(g, G.f[0], src);
-  uint32_t r2 = interval_row(g, G.f[1], dst);
-  uint32_t r3 = interval_row(g, G.f[2], Key128{0, sp});
-  uint32_t r4 = interval_row(g, G.f[3], Key128{0, dp});
+  uint32_t r1 = g.at<uint32_t>(G.f[0].rows)[lo[0]];
+  uint32_t r2 = g.at<uint32_t>(G.f[1].rows)[lo[1]];
+  uint32_t r3 = g.at<uint32_t>(G.f[2].rows)[lo[2]];
+  uint32_t r4 = g.at<uint32_t>(G.f[3].rows)[lo[3]];
   const uint64_t *p0 = pool + (uint64_t)r0 * stride, *p1 = pool + (uint64_t)r1 * stride;
   const uint64_t *p2 = pool + (uint64_t)r2 * stride, *p3 = pool + (uint64_t)r3 * stride;
   const uint64_t *p4 = pool + (uint64_t)r4 * stride;
@@ -531,7 +569,7 @@ __device__ int64_t classify(const Img &g, const Classifier &C, uint32_t a, uint3
 // ---------------------------------------------------------------------------
 // Static NAT
 // ---------------------------------------------------------------------------
-__device__ bool nat_find(const Img &g, uint32_t kind, uint32_t svni, uint32_t dvni, uint32_t addr,
+__device__ __forceinline__ bool nat_find(const Img &g, uint32_t kind, uint32_t svni, uint32_t dvni, uint32_t addr,
                          bool has_port, uint16_t port, uint32_t &na, bool &hp, uint16_t &np) {
   uint32_t ti;
   if (!hash_find(g, g.im.nat_tabs, kind, svni, kind ? dvni : 0, ti)) return false;
@@ -539,6 +577,11 @@ __device__ bool nat_find(const Img &g, uint32_t kind, uint32_t svni, uint32_t dv
   if (T.n == 0) return false;
   const uint32_t *b = g.at<uint32_t>(T.bounds);
   uint32_t lo = 0, hi = T.n;
+  if (T.jump) {
+    const uint32_t *jt = g.at<uint32_t>(T.jump);
+    lo = jt[addr >> 16];
+    hi = jt[(addr >> 16) + 1] + 1;
+  }
   while (hi - lo > 1) {
     uint32_t mid = (lo + hi) >> 1;
     if (b[mid] <= addr) lo = mid; else hi = mid;
@@ -622,7 +665,7 @@ __device__ __forceinline__ uint16_t bswap16(uint32_t v) { return (uint16_t)(((v 
 
 // Sum of the big-endian 16-bit words of frame bytes [a, e) (word pairing
 // starts at a), returned folded (not complemented).
-__device__ uint32_t sum_frame(const Frame &F, int a, int e) {
+__device__ __forceinline__ uint32_t sum_frame(const Frame &F, int a, int e) {
   if (e <= a) return 0;
   // absolute alignment: the LDS window starts 16-aligned, frame byte f sits
   // at window position shift + f, which has the same alignment as HBM.
@@ -661,21 +704,22 @@ __device__ uint32_t sum_frame(const Frame &F, int a, int e) {
 // ---------------------------------------------------------------------------
 // Stages
 // ---------------------------------------------------------------------------
-__device__ bool find_iface(const Img &g, uint32_t ifx, Iface &out) {
+__device__ __forceinline__ bool find_iface(const Img &g, uint32_t ifx, Iface &out) {
   uint32_t idx;
   if (!hash_find(g, g.im.ifaces, ifx, 0, 0, idx)) return false;
   out = g.at<Iface>(g.im.iface_recs)[idx];
   return true;
 }
 
-__device__ void stage_ingress(const Img &g, const Frame &F, const Hdr &H, State &S, uint32_t iif) {
+__device__ __forceinline__ void stage_ingress(const Img &g, const Frame &F, const Hdr &H, State &S, uint32_t iif) {
   if (S.done != DONE_NONE) return;
   Iface I;
   if (!find_iface(g, iif, I)) { done(S, DP_DONE_INTERFACE_UNKNOWN); return; }
   if (I.admin == DP_IF_DOWN) { done(S, DP_DONE_INTERFACE_ADM_DOWN); return; }
   if (!(I.iftype == DP_IFT_ETHERNET || I.iftype == DP_IFT_DOT1Q)) { done(S, DP_DONE_INTERFACE_UNSUPPORTED); return; }
-  bool bc = true, mine = true;
-  for (int i = 0; i < 6; i++) { bc &= S.emac[i] == 0xff; mine &= S.emac[i] == I.mac[i]; }
+  bool bc, mine;
+  bc = S.edst == 0xffffffffffffull;
+  mine = S.edst == load_mac(I.mac);
   if (bc) { S.flags |= DP_META_IS_L2_BCAST; done(S, DP_DONE_UNHANDLED); return; }
   if (!mine) { done(S, DP_DONE_MAC_NOT_FOR_US); return; }
   if (I.attach == DP_ATTACH_VRF) {
@@ -689,14 +733,14 @@ __device__ void stage_ingress(const Img &g, const Frame &F, const Hdr &H, State 
   }
 }
 
-__device__ void decrement_ttl(State &S) {
+__device__ __forceinline__ void decrement_ttl(State &S) {
   if (S.ttl == 0) { done(S, DP_DONE_HOP_LIMIT_EXCEEDED); return; }
   S.ttl--;
   if (S.ttl == 0) done(S, DP_DONE_HOP_LIMIT_EXCEEDED);
 }
 
 // IPv4 header checksum of the current inner header (with current fields)
-__device__ uint16_t ipv4_csum(const Frame &F, const Hdr &H, const State &S) {
+__device__ __forceinline__ uint16_t ipv4_csum(const Frame &F, const Hdr &H, const State &S) {
   int o = H.net_off;
   uint64_t s = 0;
   s += ((uint32_t)F.b(o) << 8) | F.b(o + 1);
@@ -710,7 +754,7 @@ __device__ uint16_t ipv4_csum(const Frame &F, const Hdr &H, const State &S) {
 }
 
 // Full L4 checksum of the current (inner) headers over the payload
-__device__ uint16_t l4_csum(const Frame &F, const Hdr &H, const State &S) {
+__device__ __forceinline__ uint16_t l4_csum(const Frame &F, const Hdr &H, const State &S) {
   int plen = F.len - S.pay_start;
   uint32_t pay = sum_frame(F, S.pay_start, F.len);
   uint64_t s = pay;
@@ -748,15 +792,15 @@ __device__ uint16_t l4_csum(const Frame &F, const Hdr &H, const State &S) {
   return 0;
 }
 
-__device__ void vxlan_encap(const Img &g, const Frame &F, const Hdr &H, State &S, const Instr &in, const FibRec &fb) {
+__device__ __forceinline__ void vxlan_encap(const Img &g, const Frame &F, const Hdr &H, State &S, const Instr &in, const FibRec &fb) {
   if (!(fb.flags & DP_FIB_VTEP_HAS_MAC)) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
   if (!(in.flags & DP_INSTR_HAS_DMAC)) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
   uint8_t vz = 0, dz = 0;
   for (int i = 0; i < 6; i++) { vz |= fb.vtep_mac[i]; dz |= in.mac[i]; }
   if (vz == 0 || (fb.vtep_mac[0] & 1)) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
-  for (int i = 0; i < 6; i++) S.emac[6 + i] = fb.vtep_mac[i];
+  S.esrc = load_mac(fb.vtep_mac);
   if (dz == 0) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); S.eth_dirty = true; return; }
-  for (int i = 0; i < 6; i++) S.emac[i] = in.mac[i];
+  S.edst = load_mac(in.mac);
   S.eth_dirty = true;
   if (S.flags & DP_META_REFR_CHKSUM) {
     if (H.net == 4) S.inner_v4_ck = ipv4_csum(F, H, S);
@@ -792,9 +836,9 @@ __device__ void vxlan_encap(const Img &g, const Frame &F, const Hdr &H, State &S
   int inner_start = S.pay_start - H.size;
   if (inner_start < -(int)DP_HEADROOM) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
   // packet_hash_vxlan over the (updated) inner headers
-  HBuf hbuf; hbuf.n = 0;
-  for (int i = 0; i < 6; i++) hb_put(hbuf, S.emac[6 + i]);
-  for (int i = 0; i < 6; i++) hb_put(hbuf, S.emac[i]);
+  HBuf hbuf{F.hs, 0};
+  for (int i = 0; i < 6; i++) hb_put(hbuf, mac_b(S.esrc, i));
+  for (int i = 0; i < 6; i++) hb_put(hbuf, mac_b(S.edst, i));
   hb_put(hbuf, F.b(H.hb + 12)); hb_put(hbuf, F.b(H.hb + 13));
   for (int v = 0; v < H.nvlan; v++) {
     uint16_t vid = F.be16(H.hb + 14 + 4 * v) & 0x0fff;
@@ -810,7 +854,7 @@ __device__ void vxlan_encap(const Img &g, const Frame &F, const Hdr &H, State &S
   S.dst_vni = in.vni;
 }
 
-__device__ void stage_ipforward(const Img &g, const Frame &F, Hdr &H, State &S) {
+__device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hdr &H, State &S) {
   if (S.done != DONE_NONE) return;
   bool had_vrf = S.has_vrf;
   uint32_t vrf0 = S.vrf;
@@ -833,7 +877,7 @@ __device__ void stage_ipforward(const Img &g, const Frame &F, Hdr &H, State &S) 
   const RouteNh nh = g.at<RouteNh>(g.im.route_nhs)[nhi];
   uint32_t idx = 0;
   if (nh.n_entries > 1) {
-    HBuf hbuf; hbuf.n = 0;
+    HBuf hbuf{F.hs, 0};
     hash_ip_fields(F, H, S, hbuf);
     idx = (uint32_t)(rapid(hbuf.b, hbuf.n) % nh.n_entries);
   }
@@ -897,7 +941,7 @@ __device__ __forceinline__ Key128 key_of(const Frame &F, const Hdr &H, const Sta
   return k;
 }
 
-__device__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, State &S) {
+__device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, State &S) {
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY) || S.dst_vni) return;
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
   if (!S.src_vni) { done(S, DP_DONE_UNROUTABLE); return; }
@@ -916,7 +960,7 @@ __device__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, St
   if (dnat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_DST;
 }
 
-__device__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S) {
+__device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S) {
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY)) return;
   if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
@@ -942,7 +986,7 @@ __device__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S) 
   if (action == DP_ACL_DENY) done(S, DP_DONE_ACL_DROPPED);
 }
 
-__device__ void stage_static_nat(const Img &g, const Frame &F, const Hdr &H, State &S) {
+__device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, const Hdr &H, State &S) {
   if (S.done != DONE_NONE) return;
   if (!(S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST))) return;
   if (S.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) return;
@@ -977,7 +1021,7 @@ __device__ void stage_static_nat(const Img &g, const Frame &F, const Hdr &H, Sta
   if (modified) S.flags |= DP_META_REFR_CHKSUM;
 }
 
-__device__ bool adj_find(const Img &g, uint32_t oif, uint8_t fam, const Addr16 &a, uint8_t mac[6]) {
+__device__ __forceinline__ bool adj_find(const Img &g, uint32_t oif, uint8_t fam, const Addr16 &a, uint8_t mac[6]) {
   const AdjMap &m = g.im.adjs;
   if (m.count == 0) return false;
   const Adj *s = g.at<Adj>(m.slots);
@@ -996,7 +1040,7 @@ __device__ bool adj_find(const Img &g, uint32_t oif, uint8_t fam, const Addr16 &
   return false;
 }
 
-__device__ void stage_egress(const Img &g, const Frame &F, const Hdr &H, State &S) {
+__device__ __forceinline__ void stage_egress(const Img &g, const Frame &F, const Hdr &H, State &S) {
   if (S.done != DONE_NONE) return;
   if (!S.has_oif) { done(S, DP_DONE_ROUTE_FAILURE); return; }
   uint8_t fam; Addr16 a;
@@ -1015,9 +1059,11 @@ __device__ void stage_egress(const Img &g, const Frame &F, const Hdr &H, State &
   if (!(I.iftype == DP_IFT_ETHERNET || I.iftype == DP_IFT_DOT1Q)) { done(S, DP_DONE_INTERFACE_UNSUPPORTED); return; }
   if (S.encap) {
     S.o_eth = true;
-    for (int i = 0; i < 6; i++) { S.o_mac[i] = dmac[i]; S.o_mac[6 + i] = I.mac[i]; }
+    S.odst = load_mac(dmac);
+    S.osrc = load_mac(I.mac);
   } else {
-    for (int i = 0; i < 6; i++) { S.emac[i] = dmac[i]; S.emac[6 + i] = I.mac[i]; }
+    S.edst = load_mac(dmac);
+    S.esrc = load_mac(I.mac);
     S.eth_dirty = true;
   }
   done(S, DP_DONE_DELIVERED);
@@ -1068,9 +1114,10 @@ struct OW {
 };
 
 // emit the inner header stack H (with current field values) via the writer
-__device__ void emit_stack(OW &w, const Frame &F, const Hdr &H, const State &S, bool v4ck_given,
+__device__ __forceinline__ void emit_stack(OW &w, const Frame &F, const Hdr &H, const State &S, bool v4ck_given,
                            uint16_t v4ck, bool l4ck_given, uint16_t l4ck) {
-  for (int i = 0; i < 12; i++) w.put(S.emac[i]);
+  for (int i = 0; i < 6; i++) w.put(mac_b(S.edst, i));
+  for (int i = 0; i < 6; i++) w.put(mac_b(S.esrc, i));
   w.put(F.b(H.hb + 12)); w.put(F.b(H.hb + 13));
   for (int i = 0; i < 4 * H.nvlan; i++) w.put(F.b(H.hb + 14 + i));
   if (!H.net) return;
@@ -1087,7 +1134,9 @@ __device__ void emit_stack(OW &w, const Frame &F, const Hdr &H, const State &S, 
     w.put(S.ttl);
     for (int i = 8; i < 40; i++) w.put(F.b(o + i));
   }
-  for (int e = 0; e < H.next; e++) {
+#pragma unroll
+  for (int e = 0; e < 3; e++) {
+    if (e >= H.next) break;
     int eo = H.ext_off[e];
     int n = H.ext_kind[e] == HK_EXT_RAW ? ((int)F.b(eo + 1) + 1) * 8
           : H.ext_kind[e] == HK_EXT_FRAG ? 8 : ((int)F.b(eo + 1) + 2) * 4;
@@ -1124,7 +1173,7 @@ __device__ void emit_stack(OW &w, const Frame &F, const Hdr &H, const State &S, 
 }
 
 // Packet::serialize.  Returns the frame-relative output start.
-__device__ int serialize(const Frame &F, const Hdr &H, State &S) {
+__device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S) {
   if (S.encap) {
     int inner = H.size;
     int outer = 14 + (S.o_fam == 4 ? 20 : 40) + 16;
@@ -1132,7 +1181,8 @@ __device__ int serialize(const Frame &F, const Hdr &H, State &S) {
     if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
     OW w{F.g + start, 0};
     // outer Ethernet (added by Egress)
-    for (int i = 0; i < 12; i++) w.put(S.o_mac[i]);
+    for (int i = 0; i < 6; i++) w.put(mac_b(S.odst, i));
+    for (int i = 0; i < 6; i++) w.put(mac_b(S.osrc, i));
     w.put16(S.o_fam == 4 ? 0x0800 : 0x86dd);
     if (S.o_fam == 4) {
       // Ipv4Header::default() + src/dst/ttl/proto + payload len + checksum
@@ -1167,9 +1217,10 @@ __device__ int serialize(const Frame &F, const Hdr &H, State &S) {
     uint8_t *q = F.g + H.hb;
     if (S.eth_dirty) {
       if (((uintptr_t)q & 1) == 0) {
-        for (int i = 0; i < 12; i += 2) *reinterpret_cast<uint16_t *>(q + i) = (uint16_t)(S.emac[i] | (S.emac[i + 1] << 8));
+        for (int i = 0; i < 6; i += 2) *reinterpret_cast<uint16_t *>(q + i) = (uint16_t)(mac_b(S.edst, i) | (mac_b(S.edst, i + 1) << 8));
+        for (int i = 0; i < 6; i += 2) *reinterpret_cast<uint16_t *>(q + 6 + i) = (uint16_t)(mac_b(S.esrc, i) | (mac_b(S.esrc, i + 1) << 8));
       } else {
-        for (int i = 0; i < 12; i++) q[i] = S.emac[i];
+        for (int i = 0; i < 6; i++) { q[i] = mac_b(S.edst, i); q[6 + i] = mac_b(S.esrc, i); }
       }
     }
     if (H.net == 4) {
@@ -1183,7 +1234,9 @@ __device__ int serialize(const Frame &F, const Hdr &H, State &S) {
     } else if (H.net == 6) {
       st8(F.g + H.net_off + 7, S.ttl);
     }
-    for (int e = 0; e < H.next; e++) {
+#pragma unroll
+    for (int e = 0; e < 3; e++) {
+      if (e >= H.next) break;
       uint8_t *x = F.g + H.ext_off[e];
       if (H.ext_kind[e] == HK_EXT_FRAG) { st8(x + 1, 0); st8(x + 3, F.b(H.ext_off[e] + 3) & 0xf9); }
       if (H.ext_kind[e] == HK_EXT_AUTH) { st8(x + 2, 0); st8(x + 3, 0); }
@@ -1212,7 +1265,7 @@ __device__ int serialize(const Frame &F, const Hdr &H, State &S) {
 // ---------------------------------------------------------------------------
 // Per-packet body
 // ---------------------------------------------------------------------------
-__device__ uint8_t process_packet(const Img &g, uint8_t *slab, uint8_t *buf, uint64_t buf_bytes,
+__device__ __forceinline__ uint8_t process_packet(const Img &g, uint8_t *slab, uint8_t *hs, uint8_t *buf, uint64_t buf_bytes,
                                   const dp_pkt_in_t &pin, dp_pkt_out_t &o) {
   if (pin.off < DP_HEADROOM || (((uint64_t)pin.off + pin.len + 15) & ~15ull) > buf_bytes) {
     // layout contract violated: never touch memory outside the buffer
@@ -1223,6 +1276,7 @@ __device__ uint8_t process_packet(const Img &g, uint8_t *slab, uint8_t *buf, uin
   }
   Frame F;
   F.lds = slab;
+  F.hs = hs;
   F.g = buf + pin.off;
   F.shift = (int)(pin.off & 15);
   F.len = pin.len;
@@ -1306,6 +1360,7 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__re
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
                    dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ stats) {
   __shared__ __attribute__((aligned(16))) uint8_t slab_all[TPB * SLAB];
+  __shared__ uint8_t hash_all[TPB * 64];
   __shared__ uint32_t hist[DP_DONE_COUNT + 1];
   const int tid = threadIdx.x;
   if (tid < DP_DONE_COUNT + 1) hist[tid] = 0;
@@ -1315,7 +1370,7 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__re
     Img g{img_base, im};
     const dp_pkt_in_t pin = in[i];
     dp_pkt_out_t o;
-    done_code = process_packet(g, slab_all + tid * SLAB, buf, buf_bytes, pin, o);
+    done_code = process_packet(g, slab_all + tid * SLAB, hash_all + tid * 64, buf, buf_bytes, pin, o);
     out[i] = o;
   }
   __syncthreads();
@@ -1332,8 +1387,9 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__re
 extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
                           uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n) {
   static uint8_t slab[SLAB + 16];
+  static uint8_t hs[64];
   Img g{img_base, *reinterpret_cast<const Image *>(image_struct)};
-  for (uint32_t i = 0; i < n; i++) process_packet(g, slab, buf, buf_bytes, in[i], out[i]);
+  for (uint32_t i = 0; i < n; i++) process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i]);
 }
 #else
 // Launch wrapper used by the runtime (dp_runtime.cpp).

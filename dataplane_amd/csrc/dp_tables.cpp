@@ -324,6 +324,21 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
       G.f[f].bounds = ib.put(bounds);
       G.f[f].rows = ib.put(rows);
       G.f[f].n = (uint32_t)m;
+      G.f[f].jump = 0;
+      // bucket = top 16 bits of the key: v4 address >> 16, port itself,
+      // v6 address hi64 >> 48
+      G.f[f].shift = f >= 2 ? 0 : (fam == 4 ? 16 : 48);
+      if (m > 16) {
+        std::vector<uint32_t> jump(65537);
+        size_t j = 0;
+        for (uint32_t b = 0; b < 65536; b++) {
+          u128 start = f >= 2 ? (u128)b : (fam == 4 ? ((u128)b << 16) : ((u128)b << 112));
+          while (j + 1 < m && bnd[j + 1] <= start) j++;
+          jump[b] = (uint32_t)j;
+        }
+        jump[65536] = (uint32_t)(m - 1);
+        G.f[f].jump = ib.put(jump);
+      }
     }
     G.proto_rows = ib.put(prow);
     G.pool = ib.put(pool);
@@ -639,6 +654,18 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     t.bounds = ib.put(b32);
     t.longest = ib.put(longest);
     t.n = (uint32_t)b32.size();
+    t.jump = 0;
+    if (t.n > 16) {
+      std::vector<uint32_t> jump(65537);
+      size_t j = 0;
+      for (uint32_t b = 0; b < 65536; b++) {
+        uint64_t start = (uint64_t)b << 16;
+        while (j + 1 < b32.size() && b32[j + 1] <= start) j++;
+        jump[b] = (uint32_t)j;
+      }
+      jump[65536] = t.n - 1;
+      t.jump = ib.put(jump);
+    }
     KV k = mt.first;
     k.v = (uint32_t)ntabs.size();
     ntkv.push_back(k);
