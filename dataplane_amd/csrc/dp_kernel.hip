@@ -1090,6 +1090,12 @@ __device__ __forceinline__ void st32be(uint8_t *p, uint32_t v) {
 struct OW {
   uint8_t *p;       // next output address
   uint32_t acc;
+  // keep the bytes in front of an unaligned start (headroom) intact
+  __device__ __forceinline__ void begin(uint8_t *q) {
+    p = q;
+    int sh = (int)((uintptr_t)q & 3);
+    acc = sh ? (*reinterpret_cast<const uint32_t *>(q - sh) & ((1u << (8 * sh)) - 1)) : 0;
+  }
   __device__ __forceinline__ void put(uint8_t b) {
     uintptr_t a = (uintptr_t)p;
     int sh = (int)(a & 3);
@@ -1113,9 +1119,52 @@ struct OW {
   }
 };
 
+// recorded extension header e: size and normalised bytes (Headers::deparse)
+__device__ __forceinline__ int ext_len(const Frame &F, const Hdr &H, int e) {
+  int eo = H.ext_off[e];
+  return H.ext_kind[e] == HK_EXT_RAW ? ((int)F.b(eo + 1) + 1) * 8
+       : H.ext_kind[e] == HK_EXT_FRAG ? 8 : ((int)F.b(eo + 1) + 2) * 4;
+}
+__device__ __forceinline__ int ext_bytes(const Frame &F, const Hdr &H) {
+  int t = 0;
+#pragma unroll
+  for (int e = 0; e < 3; e++) if (e < H.next) t += ext_len(F, H, e);
+  return t;
+}
+__device__ __forceinline__ uint8_t ext_byte(const Frame &F, const Hdr &H, int e, int eo, int i) {
+  uint8_t b = F.b(eo + i);
+  if (H.ext_kind[e] == HK_EXT_FRAG && i == 1) b = 0;
+  if (H.ext_kind[e] == HK_EXT_FRAG && i == 3) b &= 0xf9;
+  if (H.ext_kind[e] == HK_EXT_AUTH && (i == 2 || i == 3)) b = 0;
+  return b;
+}
+
+// The recorded extension headers are contiguous in the source and in the
+// output.  When the parse-limit quirk dropped headers behind them, their
+// output position d0 lies after their source; bytes beyond the LDS window
+// are read from the very buffer being rewritten, so before anything else is
+// written the block is moved back to front (memmove order) and the forward
+// writer re-reads the moved bytes.  Returns the bytes moved (0: not moved;
+// the sizes must be taken before the move, which may overwrite them).
+__device__ __forceinline__ int move_exts(const Frame &F, const Hdr &H, int d0) {
+  if (!H.next || d0 <= H.ext_off[0]) return 0;
+  const int eo0 = H.ext_off[0];
+  const int tot = ext_bytes(F, H);
+#pragma unroll
+  for (int e = 2; e >= 0; e--) {
+    if (e >= H.next) continue;
+    int eo = H.ext_off[e], d = d0 + (eo - eo0);
+    for (int i = ext_len(F, H, e) - 1; i >= 0; i--) F.g[d + i] = ext_byte(F, H, e, eo, i);
+  }
+  return tot;
+}
+__device__ __forceinline__ int ext_out_off(const Hdr &H) {  // within the emitted stack
+  return 14 + 4 * H.nvlan + (H.net == 4 ? H.net_hlen : 40);
+}
+
 // emit the inner header stack H (with current field values) via the writer
 __device__ __forceinline__ void emit_stack(OW &w, const Frame &F, const Hdr &H, const State &S, bool v4ck_given,
-                           uint16_t v4ck, bool l4ck_given, uint16_t l4ck) {
+                           uint16_t v4ck, bool l4ck_given, uint16_t l4ck, int moved) {
   for (int i = 0; i < 6; i++) w.put(mac_b(S.edst, i));
   for (int i = 0; i < 6; i++) w.put(mac_b(S.esrc, i));
   w.put(F.b(H.hb + 12)); w.put(F.b(H.hb + 13));
@@ -1134,18 +1183,18 @@ __device__ __forceinline__ void emit_stack(OW &w, const Frame &F, const Hdr &H, 
     w.put(S.ttl);
     for (int i = 8; i < 40; i++) w.put(F.b(o + i));
   }
+  if (H.next) {
+    if (moved) {
+      const int d0 = (int)(w.p - F.g);
+      for (int i = 0; i < moved; i++) w.put(F.g[d0 + i]);
+    } else {
 #pragma unroll
-  for (int e = 0; e < 3; e++) {
-    if (e >= H.next) break;
-    int eo = H.ext_off[e];
-    int n = H.ext_kind[e] == HK_EXT_RAW ? ((int)F.b(eo + 1) + 1) * 8
-          : H.ext_kind[e] == HK_EXT_FRAG ? 8 : ((int)F.b(eo + 1) + 2) * 4;
-    for (int i = 0; i < n; i++) {
-      uint8_t b = F.b(eo + i);
-      if (H.ext_kind[e] == HK_EXT_FRAG && i == 1) b = 0;
-      if (H.ext_kind[e] == HK_EXT_FRAG && i == 3) b &= 0xf9;
-      if (H.ext_kind[e] == HK_EXT_AUTH && (i == 2 || i == 3)) b = 0;
-      w.put(b);
+      for (int e = 0; e < 3; e++) {
+        if (e >= H.next) break;
+        int eo = H.ext_off[e];
+        int n = ext_len(F, H, e);
+        for (int i = 0; i < n; i++) w.put(ext_byte(F, H, e, eo, i));
+      }
     }
   }
   if (!H.l4) return;
@@ -1179,7 +1228,9 @@ __device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S)
     int outer = 14 + (S.o_fam == 4 ? 20 : 40) + 16;
     int start = S.pay_start - inner - outer;
     if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
-    OW w{F.g + start, 0};
+    const int moved = move_exts(F, H, start + outer + ext_out_off(H));
+    OW w;
+    w.begin(F.g + start);
     // outer Ethernet (added by Egress)
     for (int i = 0; i < 6; i++) w.put(mac_b(S.odst, i));
     for (int i = 0; i < 6; i++) w.put(mac_b(S.osrc, i));
@@ -1202,7 +1253,7 @@ __device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S)
     w.put16(S.o_sport); w.put16(4789); w.put16(S.o_len); w.put16(0);
     w.put(0x08); w.put(0); w.put(0); w.put(0);
     w.put((S.o_vni >> 16) & 0xff); w.put((S.o_vni >> 8) & 0xff); w.put(S.o_vni & 0xff); w.put(0);
-    emit_stack(w, F, H, S, H.net == 4, S.inner_v4_ck, S.inner_l4_ck, S.inner_l4_ck_val);
+    emit_stack(w, F, H, S, H.net == 4, S.inner_v4_ck, S.inner_l4_ck, S.inner_l4_ck_val, moved);
     w.finish(F, S.pay_start);
     return start;
   }
@@ -1256,8 +1307,10 @@ __device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S)
   }
   // rewrite mode (parse-limit quirk): re-emit the kept stack before the payload
   if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
-  OW w{F.g + start, 0};
-  emit_stack(w, F, H, S, v4, v4ck, l4, l4ck);
+  const int moved = move_exts(F, H, start + ext_out_off(H));
+  OW w;
+  w.begin(F.g + start);
+  emit_stack(w, F, H, S, v4, v4ck, l4, l4ck, moved);
   w.finish(F, S.pay_start);
   return start;
 }

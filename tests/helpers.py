@@ -19,7 +19,22 @@ def compare(out_ref, buf_ref, out_dut, buf_dut, inp, label=""):
         if not np.array_equal(buf_ref[o:o + l], buf_dut[o:o + l]):
             d = np.nonzero(buf_ref[o:o + l] != buf_dut[o:o + l])[0]
             raise AssertionError(f"{label}: pkt {i} bytes differ at {d[:8]}")
-    assert np.array_equal(buf_ref, buf_dut), f"{label}: buffers differ outside delivered frames"
+    # A dropped packet's buffer is released by the reference (its bytes are
+    # unobservable; e.g. Packet::vxlan_encap has already prepended the inner
+    # headers when Egress then fails), so its slot is excluded.  Everything
+    # else -- delivered frames, their headroom, gaps -- must match.
+    diff = buf_ref != buf_dut
+    dropped = np.nonzero(out_ref["done"] != A.DONE["Delivered"])[0]
+    if len(dropped):
+        starts = inp["off"].astype(np.int64) - A.HEADROOM
+        ends = np.append(starts[1:], len(buf_ref))
+        for i in dropped:
+            diff[starts[i]:ends[i]] = False
+    if diff.any():
+        d = np.nonzero(diff)[0]
+        owner = int(np.searchsorted(inp["off"].astype(np.int64) - A.HEADROOM, d[0], "right")) - 1
+        raise AssertionError(f"{label}: buffers differ outside delivered frames at {d[:8]} "
+                             f"(packet {owner}: {out_ref[owner]} / {out_dut[owner]})")
 
 
 def hist(out):

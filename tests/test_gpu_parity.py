@@ -7,6 +7,7 @@ from dataplane_amd import GpuPathNf, _abi as A
 from dataplane_amd.workload import Workload
 from oracle.pyoracle import Oracle
 
+from edgecase import edge_frames, edge_tables, pack_burst
 from helpers import compare, hist
 
 pytestmark = pytest.mark.gpu
@@ -32,3 +33,88 @@ def test_gpu_matches_oracle(nf, cfg):
     h = hist(o_ref)
     assert int(stats.sum()) == w.n
     assert int(stats[A.DONE["Delivered"]]) == h.get("Delivered", 0)
+
+
+@pytest.fixture(scope="module")
+def edge():
+    t = edge_tables()
+    return t, t.build()
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13, 14, 15, 16])
+def test_gpu_edge_corpus(nf, edge, seed):
+    """Malformed / boundary frames and every table branch (tests/edgecase.py)."""
+    _, tp = edge
+    nf.publish(tp)
+    buf, inp = pack_burst(edge_frames(20000, seed))
+    b_ref, b_dut = buf.copy(), buf.copy()
+    o_ref = Oracle(tp).process(b_ref, inp, A.PKT_OUT)
+    o_dut = nf.process_arrays(b_dut, inp)
+    compare(o_ref, b_ref, o_dut, b_dut, inp, f"edge {seed}")
+
+
+@pytest.mark.parametrize("cfg", [2, 4, 5])
+def test_gpu_full_size(nf, cfg):
+    """BASELINE.json table sizes (1M v4 routes, 200k v6 on C5, 10k ACL rules
+    per family, 256 NAT maps) at 1M packets, bit-exact against the oracle run
+    on all host cores."""
+    import os
+    w = Workload(cfg, 1_000_000, seed=300 + cfg, tcp_percent=20)
+    nf.publish(w.tables)
+    b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
+    o_ref = np.zeros(w.n, dtype=A.PKT_OUT)
+    orc = Oracle(w.tables)
+    orc.process_parallel(b_ref, w.inp, o_ref, threads=max(1, min(16, len(os.sched_getaffinity(0)))))
+    o_dut = nf.process_arrays(b_dut, w.inp)
+    compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} full")
+    assert hist(o_ref).get("Delivered", 0) > w.n // 4
+
+
+def test_gpu_device_path_and_determinism(nf):
+    """dp_process_burst_device on torch-allocated HBM, on a caller stream;
+    processing the same pristine burst twice gives identical results."""
+    import torch
+    w = Workload(2, 50000, seed=77, n_routes_v4=50000, n_acl=2000, n_nat=64, tcp_percent=30)
+    nf.publish(w.tables)
+    b_ref = w.fresh_buf()
+    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    outs = []
+    for _ in range(2):
+        db = torch.from_numpy(w.fresh_buf()).to(dev)
+        di = torch.from_numpy(w.inp.view(np.uint8)).to(dev)
+        do = torch.zeros(w.n * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+        st = torch.zeros(A.DONE_COUNT, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
+        nf.process_device(db.data_ptr(), db.numel(), di.data_ptr(), do.data_ptr(), w.n,
+                          st.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        o = do.cpu().numpy().view(A.PKT_OUT)
+        b = db.cpu().numpy()
+        compare(o_ref, b_ref, o, b, w.inp, "device path")
+        assert int(st.sum()) == w.n
+        outs.append((o, b))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_gpu_republish_and_empty(nf, edge):
+    """A burst after dp_tables_publish sees the new generation; n == 0 is a
+    no-op; offsets outside the buffer contract are InternalFailure and touch
+    nothing."""
+    _, tp = edge
+    w = Workload(1, 4096, seed=5)
+    nf.publish(w.tables)
+    g1 = nf.data.genid
+    nf.publish(tp)
+    assert nf.data.genid != g1
+    buf, inp = pack_burst(edge_frames(4096, 21))
+    b_ref, b_dut = buf.copy(), buf.copy()
+    compare(Oracle(tp).process(b_ref, inp, A.PKT_OUT), b_ref, nf.process_arrays(b_dut, inp),
+            b_dut, inp, "after republish")
+    assert len(nf.process_arrays(buf.copy(), inp[:0])) == 0
+    bad = inp[:4].copy()
+    bad["off"] = [0, 16, len(buf) - 8, len(buf) + 4096]
+    b = buf.copy()
+    with pytest.raises(RuntimeError):   # the host path validates the layout
+        nf.process_arrays(b, bad)
