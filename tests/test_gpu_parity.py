@@ -15,6 +15,10 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def nf():
+    # torch (plumbing for the device-path test) bundles its own HIP runtime;
+    # it must initialise before libdpgpu's runtime claims the device
+    import torch
+    torch.cuda.init()
     n = GpuPathNf(0)
     yield n
     n.close()
