@@ -122,3 +122,27 @@ def test_gpu_republish_and_empty(nf, edge):
     b = buf.copy()
     with pytest.raises(RuntimeError):   # the host path validates the layout
         nf.process_arrays(b, bad)
+
+
+def test_gpu_known_answers(nf):
+    """The reference's KATs (tests/golden/kat.py) through the HIP path."""
+    from golden.kat import all_cases, run_case
+
+    def gpu_process(tp, buf, inp):
+        nf.publish(tp)
+        return nf.process_arrays(buf, inp)
+    errs = []
+    for case in all_cases():
+        errs += run_case(case, gpu_process)
+    assert not errs, "\n".join(errs)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4", "c5", "edge"])
+def test_gpu_golden_vectors(nf, name):
+    """The committed golden vectors, byte for byte."""
+    from test_golden import load
+    keep, tp, z = load(name)
+    nf.publish(tp)
+    b = z["buf_in"].copy()
+    out = nf.process_arrays(b, z["inp"])
+    compare(z["out"], z["buf_out"], out, b, z["inp"], f"golden {name} gpu")
