@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from dataplane_amd import GpuPathNf, _abi as A  # noqa: E402
+from dataplane_amd.shard import reduce_over_ranks, shard_seed  # noqa: E402
 from dataplane_amd.workload import ALGO_BYTES, CONFIG_NAMES, Workload  # noqa: E402
 
 METRIC = "Mpps device-resident (64B IPv4, 1M-route LPM + 10k ACL + NAT) at 1/2/4/8 GPU"
@@ -95,7 +96,7 @@ def main() -> None:
 
     cfg = args.config
     t0 = time.perf_counter()
-    w = Workload(cfg, args.packets, seed=args.seed + 1000 * rank, n_routes_v4=args.routes_v4,
+    w = Workload(cfg, args.packets, seed=shard_seed(args.seed, rank), n_routes_v4=args.routes_v4,
                  n_routes_v6=args.routes_v6, n_acl=args.acl, n_nat=args.nat)
     log(rank, f"[bench] workload C{cfg}: {w.n} packets, built in {time.perf_counter() - t0:.1f}s")
     nf = GpuPathNf(local)
@@ -143,15 +144,7 @@ def main() -> None:
     elapsed = time.perf_counter() - t_start
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-        st = dstats.clone()
-        torch.distributed.all_reduce(st)
-        hist = st.cpu().numpy()
-    else:
-        hist = dstats.cpu().numpy()
+    elapsed, hist = reduce_over_ranks(elapsed, dstats.cpu().numpy(), dev)
 
     ms_per_step = elapsed * 1e3 / args.steps
     total_pkts = world * n * args.steps
