@@ -186,7 +186,8 @@ def gpu_lib() -> C.CDLL:
     """The product library (HIP).  Raises if it is not built."""
     global _gpu
     if _gpu is None:
-        lib = _load(os.path.join(LIB_DIR, "libdpgpu.so"))
+        # DPGPU_LIB selects a diagnostic build (e.g. lib/libdpgpu_timing.so)
+        lib = _load(os.environ.get("DPGPU_LIB") or os.path.join(LIB_DIR, "libdpgpu.so"))
         lib.dp_abi_version.restype = C.c_uint32
         lib.dp_ctx_create.argtypes = [C.c_int, C.POINTER(_VP)]
         lib.dp_ctx_destroy.argtypes = [_VP]

@@ -69,13 +69,23 @@ struct FibRec {
   Lpm v4, v6;
 };
 
-struct Instr {         // compacted dp_instr_t
-  uint8_t kind, flags, fam, pad;
+// Egress outcome resolved at publish time (Egress::egress_process depends
+// only on (oif, next hop) and the interface / adjacency tables, which are
+// part of the same immutable generation).
+#define DPD_EG_NEED_ADJ 254u   // no next-hop address: adjacency of the packet's dst at run time
+
+struct Instr {         // compacted dp_instr_t + resolved egress (64 B)
+  uint8_t kind, flags, fam;
+  uint8_t eg_code;     // EGRESS: DoneReason of Egress (DELIVERED = ok) or DPD_EG_NEED_ADJ
   uint32_t ifindex;
   uint32_t vni;
   uint8_t mac[6];
-  uint8_t pad2[2];
+  uint8_t if_code;     // EGRESS: oif checks alone (255 = ok); used with DPD_EG_NEED_ADJ
+  uint8_t pad2;
   uint8_t addr[16];
+  uint64_t eg_dmac;    // adjacency MAC (48-bit, first byte most significant)
+  uint64_t eg_smac;    // oif MAC
+  uint64_t pad3;
 };
 
 struct Entry {
@@ -86,12 +96,39 @@ struct RouteNh {
   uint32_t first_entry, n_entries;
 };
 
-struct Iface {
+// Interface record with Ingress's table-only checks pre-evaluated
+// (dataplane/src/packet_processor/ingress.rs:153-182)
+struct IfRec {         // 32 B
   uint32_t ifindex;
-  uint8_t admin, oper, iftype, attach;
+  uint8_t valid;       // 0: no such interface (InterfaceUnknown)
+  uint8_t pre_code;    // admin down / unsupported type, checked before the MAC (255 = ok)
+  uint8_t post_code;   // attach: bridge -> Unsupported, none -> Detached (255 = VRF)
+  uint8_t pad;
   uint32_t vrf_id;
-  uint8_t mac[6];
-  uint8_t pad[2];
+  int32_t fib;         // FIB of vrf_id (-1: none -> InternalFailure in IP-Forward)
+  uint64_t mac;        // 48-bit
+  uint64_t pad2;
+};
+
+// Per source VNI context (value of the VNI map)
+struct VniRec {        // 32 B
+  uint32_t vni;
+  uint32_t fib;        // FIB index of the VNI
+  uint32_t vrf_id;
+  int32_t ffr[2];      // flow-filter remote group (vni, 0, 0) v4 / v6, -1
+  int32_t nat_dst;     // NAT dst table of the VNI's PerVniTable, -1
+  uint32_t pervni;     // a PerVniTable exists for the VNI
+  uint32_t pad;
+};
+
+// Per (src VNI, dst VNI) context: target of a flow-filter remote verdict
+struct PairRec {       // 32 B
+  int32_t ffl[2];      // flow-filter local group (src, dst, 0) v4 / v6
+  int32_t acl[2];      // ACL group (src, dst, 0) v4 / v6
+  uint32_t acl_def;    // default action + 1, 0 = none
+  int32_t nat_src;     // NAT src table (src -> dst), -1
+  int32_t dst_fib;     // FIB of the dst VNI, -1
+  uint32_t dst_vni;
 };
 
 struct Adj {           // adjacency slot (open addressing, keyed ifindex+ip)
@@ -131,11 +168,12 @@ struct Group {
 };
 
 struct Classifier {
-  HashMap groups;      // (vni_a, vni_b, gate) -> group index
+  HashMap groups;      // (vni_a, vni_b, gate) -> group index (host side / fallback)
   uint64_t group_recs; // Group[]
   uint64_t action;     // uint32_t[n_rules_total]
   uint64_t action2;    // uint32_t[n_rules_total]
   uint64_t orig;       // uint32_t[n_rules_total] (index in the caller's array)
+  uint64_t aux;        // uint32_t[n_rules_total]: flow-filter remote -> PairRec index
   uint32_t n_groups;
   uint32_t n_rules;
 };
@@ -170,7 +208,7 @@ struct NatTab {
 struct Image {
   uint64_t bytes;
   int64_t genid;
-  HashMap vni_fib;           // vni -> fib index
+  HashMap vni_fib;           // vni -> VniRec index
   HashMap vrf_fib;           // vrf id -> fib index
   uint64_t fibs;             // FibRec[]
   uint32_t n_fibs;
@@ -180,8 +218,14 @@ struct Image {
   uint64_t route_nhs;        // RouteNh[]
   uint64_t entries;          // Entry[]
   uint64_t instrs;           // Instr[]
-  HashMap ifaces;            // ifindex -> iface record index
-  uint64_t iface_recs;       // Iface[]
+  HashMap ifaces;            // ifindex -> IfRec index
+  uint64_t if_recs;          // IfRec[]
+  uint64_t if_direct;        // IfRec[if_direct_n], indexed by ifindex (small ifindexes)
+  uint32_t if_direct_n;
+  uint32_t n_vni_recs;
+  uint64_t vni_recs;         // VniRec[] (values of vni_fib)
+  HashMap pairs;             // (src vni, dst vni) -> PairRec index
+  uint64_t pair_recs;        // PairRec[]
   AdjMap adjs;
   Classifier acl[2];         // [0] v4, [1] v6
   HashMap acl_default;       // (src_vni, dst_vni) -> action + 1

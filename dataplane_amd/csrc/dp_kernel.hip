@@ -30,6 +30,26 @@ namespace {
 using namespace dpd;
 
 constexpr int TPB = 128;
+// LDS pointers carry their address space explicitly so every access is a
+// ds_read/ds_write (a generic pointer would turn them into flat loads)
+#ifdef DP_EMU
+#define LDS_AS
+#else
+#define LDS_AS __attribute__((address_space(3)))
+#endif
+typedef LDS_AS uint8_t lds_u8;
+typedef LDS_AS uint32_t lds_u32;
+// Optional per-stage wave timing (build with -DDP_TIMING; scripts/stage_timing.py)
+#if defined(DP_TIMING) && !defined(DP_EMU)
+__device__ unsigned long long g_stage_cycles[16];
+#define TS_DECL uint64_t ts_acc[12] = {0}; uint64_t ts_last = clock64();
+#define TS(k) do { uint64_t ts_now = clock64(); ts_acc[k] += ts_now - ts_last; ts_last = ts_now; } while (0)
+#define TS_FLUSH() do { if ((threadIdx.x & 63) == 0) for (int q = 0; q < 12; q++) atomicAdd(&g_stage_cycles[q], (unsigned long long)ts_acc[q]); } while (0)
+#else
+#define TS_DECL
+#define TS(k) do {} while (0)
+#define TS_FLUSH() do {} while (0)
+#endif
 constexpr int WIN = 128;          // header window bytes per packet (rest read from HBM)
 constexpr int SLAB = WIN + 4;     // 65 dwords: conflict-free byte reads
 constexpr uint8_t DONE_NONE = 255;
@@ -65,14 +85,19 @@ __device__ __forceinline__ bool hash_find(const Img &g, const HashMap &m, uint32
 // else read from HBM.
 // ---------------------------------------------------------------------------
 struct Frame {
-  uint8_t *lds;     // this work-item's slab
-  uint8_t *hs;      // this work-item's 64-byte LDS hash scratch
+  lds_u8 *lds;      // this work-item's slab
+  lds_u8 *hs;       // this work-item's 64-byte LDS hash scratch
   uint8_t *g;       // frame start in HBM
   int shift;        // frame start & 15
   int len;
+  // The LDS read is unconditional (clamped index) so the compiler keeps it a
+  // ds_read and never fuses the two loads into one generic (flat) load
+  // through a select of pointers; the HBM read stays behind a branch.
   __device__ __forceinline__ uint8_t b(int f) const {
     int o = shift + f;
-    return o < WIN ? lds[o] : g[f];
+    uint8_t v = lds[o < WIN ? o : 0];
+    if (o >= WIN) v = g[f];
+    return v;
   }
   __device__ __forceinline__ uint16_t be16(int f) const { return (uint16_t)((b(f) << 8) | b(f + 1)); }
   __device__ __forceinline__ uint32_t be32(int f) const {
@@ -299,9 +324,11 @@ struct State {
   uint32_t src_vni, dst_vni;
   bool has_oif;
   uint32_t oif;
-  bool has_nh;
-  uint8_t nh_fam;
-  Addr16 nh;
+  uint8_t eg_code, if_code;  // resolved Egress outcome of the last Egress instruction
+  uint64_t eg_dmac, eg_smac;
+  int32_t fib;           // FIB of `vrf` (precomputed), -1 none
+  int32_t vni_idx;       // VniRec of src_vni, -1
+  int32_t pair;          // PairRec of (src_vni, dst_vni), -1 unknown
   bool has_dscp;
   uint8_t dscp, ecn;
   uint32_t fib_entry, acl_rule;
@@ -376,29 +403,29 @@ __device__ __forceinline__ bool icmp_is_error(const Frame &F, const Hdr &H) {
 // rapidhash-style hash (same restatement as the oracle; parity vs the
 // reference is UNPINNED)
 // ---------------------------------------------------------------------------
-struct HBuf { uint8_t *b; int n; };  // per-thread LDS scratch (no private-array scratch)
+struct HBuf { lds_u8 *b; int n; };  // per-thread LDS scratch (no private-array scratch)
 __device__ __forceinline__ void hb_put(HBuf &h, uint8_t x) { h.b[h.n++] = x; }
 __device__ __forceinline__ void mum(uint64_t &a, uint64_t &b) {
   uint64_t lo = a * b, hi = __umul64hi(a, b);
   a = lo; b = hi;
 }
 __device__ __forceinline__ uint64_t mixh(uint64_t a, uint64_t b) { mum(a, b); return a ^ b; }
-__device__ __forceinline__ uint64_t rd64(const uint8_t *p) {
+__device__ __forceinline__ uint64_t rd64(const lds_u8 *p) {
   uint64_t v = 0;
   for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
   return v;
 }
-__device__ __forceinline__ uint64_t rd32(const uint8_t *p) {
+__device__ __forceinline__ uint64_t rd32(const lds_u8 *p) {
   return (uint64_t)p[0] | ((uint64_t)p[1] << 8) | ((uint64_t)p[2] << 16) | ((uint64_t)p[3] << 24);
 }
-__device__ __forceinline__ uint64_t rapid(const uint8_t *p, int len) {
+__device__ __forceinline__ uint64_t rapid(const lds_u8 *p, int len) {
   const uint64_t s0 = 0x2d358dccaa6c78a5ull, s1 = 0x8bb84b93962eacc9ull, s2 = 0x4b33a62ed433d4a3ull;
   uint64_t seed = 0xbdd89aa982704029ull;
   seed ^= mixh(seed ^ s0, s1) ^ (uint64_t)len;
   uint64_t a, b;
   if (len <= 16) {
     if (len >= 4) {
-      const uint8_t *pl = p + len - 4;
+      const lds_u8 *pl = p + len - 4;
       a = (rd32(p) << 32) | rd32(pl);
       uint64_t delta = ((uint64_t)(len & 24)) >> (len >> 3);
       b = (rd32(p + delta) << 32) | rd32(pl - delta);
@@ -502,6 +529,10 @@ __device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const
 // ---------------------------------------------------------------------------
 struct Key128 { uint64_t hi, lo; };
 
+// field of the v4 ([0]) or v6 ([1]) classifier; a select, never a dynamic
+// index into the kernel-argument image header (which would force a private copy)
+#define CLS(arr, t, field) ((t) ? g.im.arr[1].field : g.im.arr[0].field)
+
 // bucket of a key for a field's jump table
 __device__ __forceinline__ uint32_t bucket_of(const FieldIdx &f, Key128 k) {
   return f.shift == 48 ? (uint32_t)(k.hi >> 48) : (uint32_t)(k.lo >> f.shift) & 0xffff;
@@ -509,12 +540,11 @@ __device__ __forceinline__ uint32_t bucket_of(const FieldIdx &f, Key128 k) {
 
 // returns global rule index or -1.  The four field searches (elementary
 // interval containing the key) run in lockstep so their loads overlap.
-__device__ __forceinline__ int64_t classify(const Img &g, const Classifier &C, uint32_t a, uint32_t bb,
-                                            uint32_t gate, uint8_t proto, Key128 src, Key128 dst,
+__device__ __forceinline__ int64_t classify(const Img &g, uint64_t group_recs, int32_t gi,
+                                            uint8_t proto, Key128 src, Key128 dst,
                                             uint16_t sp, uint16_t dp) {
-  uint32_t gi;
-  if (!hash_find(g, C.groups, a, bb, gate, gi)) return -1;
-  const Group G = g.at<Group>(C.group_recs)[gi];
+  if (gi < 0) return -1;
+  const Group G = g.at<Group>(group_recs)[gi];
   Key128 key[4] = {src, dst, Key128{0, sp}, Key128{0, dp}};
   uint32_t lo[4], hi[4];
 #pragma unroll
@@ -569,10 +599,9 @@ __device__ __forceinline__ int64_t classify(const Img &g, const Classifier &C, u
 // ---------------------------------------------------------------------------
 // Static NAT
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool nat_find(const Img &g, uint32_t kind, uint32_t svni, uint32_t dvni, uint32_t addr,
+__device__ __forceinline__ bool nat_find(const Img &g, int32_t ti, uint32_t addr,
                          bool has_port, uint16_t port, uint32_t &na, bool &hp, uint16_t &np) {
-  uint32_t ti;
-  if (!hash_find(g, g.im.nat_tabs, kind, svni, kind ? dvni : 0, ti)) return false;
+  if (ti < 0) return false;
   const NatTab T = g.at<NatTab>(g.im.nat_tab_recs)[ti];
   if (T.n == 0) return false;
   const uint32_t *b = g.at<uint32_t>(T.bounds);
@@ -675,7 +704,7 @@ __device__ __forceinline__ uint32_t sum_frame(const Frame &F, int a, int e) {
   const uint8_t *gbase = F.g - F.shift;  // 16-aligned HBM address of window pos 0
   for (int d = d0; d < d1; d += 4) {
     uint32_t w;
-    if (d + 4 <= WIN) w = *reinterpret_cast<const uint32_t *>(F.lds + d);
+    if (d + 4 <= WIN) w = *reinterpret_cast<const lds_u32 *>(F.lds + d);
     else {
       // whole 16-byte chunks from HBM when possible
       if ((d & 15) == 0 && d + 16 <= d1) {
@@ -704,33 +733,52 @@ __device__ __forceinline__ uint32_t sum_frame(const Frame &F, int a, int e) {
 // ---------------------------------------------------------------------------
 // Stages
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool find_iface(const Img &g, uint32_t ifx, Iface &out) {
+__device__ __forceinline__ bool find_iface(const Img &g, uint32_t ifx, IfRec &out) {
+  if (ifx < g.im.if_direct_n) {
+    out = g.at<IfRec>(g.im.if_direct)[ifx];
+    return out.valid != 0;
+  }
   uint32_t idx;
   if (!hash_find(g, g.im.ifaces, ifx, 0, 0, idx)) return false;
-  out = g.at<Iface>(g.im.iface_recs)[idx];
+  out = g.at<IfRec>(g.im.if_recs)[idx];
   return true;
 }
 
 __device__ __forceinline__ void stage_ingress(const Img &g, const Frame &F, const Hdr &H, State &S, uint32_t iif) {
   if (S.done != DONE_NONE) return;
-  Iface I;
+  IfRec I;
   if (!find_iface(g, iif, I)) { done(S, DP_DONE_INTERFACE_UNKNOWN); return; }
-  if (I.admin == DP_IF_DOWN) { done(S, DP_DONE_INTERFACE_ADM_DOWN); return; }
-  if (!(I.iftype == DP_IFT_ETHERNET || I.iftype == DP_IFT_DOT1Q)) { done(S, DP_DONE_INTERFACE_UNSUPPORTED); return; }
-  bool bc, mine;
-  bc = S.edst == 0xffffffffffffull;
-  mine = S.edst == load_mac(I.mac);
-  if (bc) { S.flags |= DP_META_IS_L2_BCAST; done(S, DP_DONE_UNHANDLED); return; }
-  if (!mine) { done(S, DP_DONE_MAC_NOT_FOR_US); return; }
-  if (I.attach == DP_ATTACH_VRF) {
-    if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
-    S.has_vrf = true;
-    S.vrf = I.vrf_id;
-  } else if (I.attach == DP_ATTACH_BRIDGE) {
-    done(S, DP_DONE_INTERFACE_UNSUPPORTED);
-  } else {
-    done(S, DP_DONE_INTERFACE_DETACHED);
+  if (I.pre_code != 255) { done(S, I.pre_code); return; }
+  if (S.edst == 0xffffffffffffull) { S.flags |= DP_META_IS_L2_BCAST; done(S, DP_DONE_UNHANDLED); return; }
+  if (S.edst != I.mac) { done(S, DP_DONE_MAC_NOT_FOR_US); return; }
+  if (I.post_code != 255) { done(S, I.post_code); return; }
+  if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
+  S.has_vrf = true;
+  S.vrf = I.vrf_id;
+  S.fib = I.fib;
+}
+
+// VNI -> VniRec (the VNI's FIB, VRF and per-VNI tables)
+__device__ __forceinline__ bool enter_vni(const Img &g, State &S, uint32_t vni) {
+  uint32_t vi;
+  if (!hash_find(g, g.im.vni_fib, vni, 0, 0, vi)) return false;
+  const VniRec R = g.at<VniRec>(g.im.vni_recs)[vi];
+  S.src_vni = vni;
+  S.has_vrf = true;
+  S.vrf = R.vrf_id;
+  S.fib = (int32_t)R.fib;
+  S.vni_idx = (int32_t)vi;
+  S.flags |= DP_META_IS_OVERLAY;
+  return true;
+}
+
+// PairRec of (src_vni, dst_vni): from the flow-filter verdict, else by lookup
+__device__ __forceinline__ int32_t pair_of(const Img &g, State &S) {
+  if (S.pair < 0) {
+    uint32_t pi;
+    if (hash_find(g, g.im.pairs, S.src_vni, S.dst_vni, 0, pi)) S.pair = (int32_t)pi;
   }
+  return S.pair;
 }
 
 __device__ __forceinline__ void decrement_ttl(State &S) {
@@ -858,13 +906,20 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   if (S.done != DONE_NONE) return;
   bool had_vrf = S.has_vrf;
   uint32_t vrf0 = S.vrf;
-  uint32_t fi;
+  int32_t fi;
   if (S.dst_vni) {
     if (H.net == 0 && !S.encap) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
-    if (!hash_find(g, g.im.vni_fib, S.dst_vni, 0, 0, fi)) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
+    int32_t pi = pair_of(g, S);
+    if (pi >= 0) fi = g.at<PairRec>(g.im.pair_recs)[pi].dst_fib;
+    else {
+      uint32_t vi;
+      fi = hash_find(g, g.im.vni_fib, S.dst_vni, 0, 0, vi) ? (int32_t)g.at<VniRec>(g.im.vni_recs)[vi].fib : -1;
+    }
+    if (fi < 0) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
   } else if (S.has_vrf) {
     if (H.net == 0) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
-    if (!hash_find(g, g.im.vrf_fib, S.vrf, 0, 0, fi)) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
+    fi = S.fib;
+    if (fi < 0) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
   } else {
     if (S.flags & DP_META_IS_OVERLAY) done(S, DP_DONE_INTERNAL_FAILURE);
     return;
@@ -906,25 +961,17 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
         H = I;
         load_fields(F, H, S);
         if (has_q) { S.has_dscp = true; S.dscp = tos >> 2; S.ecn = tos & 3; }
-        uint32_t nf;
-        if (!hash_find(g, g.im.vni_fib, vni, 0, 0, nf)) { done(S, DP_DONE_UNROUTABLE); break; }
-        S.src_vni = vni;
-        S.has_vrf = true;
-        S.vrf = g.at<FibRec>(g.im.fibs)[nf].vrf_id;
-        S.flags |= DP_META_IS_OVERLAY;
+        if (!enter_vni(g, S, vni)) { done(S, DP_DONE_UNROUTABLE); break; }
         break;
       }
       case DP_INSTR_ENCAP_VXLAN: vxlan_encap(g, F, H, S, in, fb); break;
       case DP_INSTR_EGRESS:
         S.has_oif = in.flags & DP_INSTR_HAS_IFINDEX;
         S.oif = in.ifindex;
-        S.has_nh = in.flags & DP_INSTR_HAS_ADDR;
-        if (S.has_nh) {
-          S.nh_fam = in.fam;
-          for (int i = 0; i < 4; i++)
-            S.nh.w[i] = ((uint32_t)in.addr[4 * i] << 24) | ((uint32_t)in.addr[4 * i + 1] << 16) | ((uint32_t)in.addr[4 * i + 2] << 8) | in.addr[4 * i + 3];
-          if (in.fam == 4) S.nh.w[1] = S.nh.w[2] = S.nh.w[3] = 0;
-        }
+        S.eg_code = in.eg_code;
+        S.if_code = in.if_code;
+        S.eg_dmac = in.eg_dmac;
+        S.eg_smac = in.eg_smac;
         break;
     }
     if (S.done != DONE_NONE) return;
@@ -948,14 +995,18 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   uint8_t proto = net_proto(F, H);
   int t = H.net == 4 ? 0 : 1;
   Key128 src = key_of(F, H, S, true), dst = key_of(F, H, S, false);
-  int64_t ri = classify(g, g.im.ff_remote[t], S.src_vni, 0, 0, proto, Key128{0, 0}, dst, 0, S.dport);
+  const int32_t rg = g.at<VniRec>(g.im.vni_recs)[S.vni_idx].ffr[t];
+  int64_t ri = classify(g, CLS(ff_remote, t, group_recs), rg, proto, Key128{0, 0}, dst, 0, S.dport);
   if (ri < 0) { done(S, DP_DONE_FILTERED); return; }
-  uint32_t dvni = g.at<uint32_t>(g.im.ff_remote[t].action)[ri];
-  uint32_t dnat = g.at<uint32_t>(g.im.ff_remote[t].action2)[ri];
-  int64_t li = classify(g, g.im.ff_local[t], S.src_vni, dvni, 0, proto, src, Key128{0, 0}, S.sport, 0);
+  uint32_t dvni = g.at<uint32_t>(CLS(ff_remote, t, action))[ri];
+  uint32_t dnat = g.at<uint32_t>(CLS(ff_remote, t, action2))[ri];
+  int32_t pi = (int32_t)g.at<uint32_t>(CLS(ff_remote, t, aux))[ri];
+  int32_t lg = g.at<PairRec>(g.im.pair_recs)[pi].ffl[t];
+  int64_t li = classify(g, CLS(ff_local, t, group_recs), lg, proto, src, Key128{0, 0}, S.sport, 0);
   if (li < 0) { done(S, DP_DONE_FILTERED); return; }
-  uint32_t snat = g.at<uint32_t>(g.im.ff_local[t].action)[li];
+  uint32_t snat = g.at<uint32_t>(CLS(ff_local, t, action))[li];
   S.dst_vni = dvni;
+  S.pair = pi;
   if (snat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
   if (dnat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_DST;
 }
@@ -966,16 +1017,18 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
   uint8_t proto = net_proto(F, H);
   int t = H.net == 4 ? 0 : 1;
-  int64_t ri = classify(g, g.im.acl[t], S.src_vni, S.dst_vni, 0, proto, key_of(F, H, S, true),
+  const int32_t pi = pair_of(g, S);
+  const int32_t ag = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].acl[t] : -1;
+  int64_t ri = classify(g, CLS(acl, t, group_recs), ag, proto, key_of(F, H, S, true),
                         key_of(F, H, S, false), S.sport, S.dport);
   uint32_t action;
   if (ri >= 0) {
-    action = g.at<uint32_t>(g.im.acl[t].action)[ri];
-    S.acl_rule = g.at<uint32_t>(g.im.acl[t].orig)[ri];
+    action = g.at<uint32_t>(CLS(acl, t, action))[ri];
+    S.acl_rule = g.at<uint32_t>(CLS(acl, t, orig))[ri];
     S.acl = action == DP_ACL_DENY ? 2 : 1;
   } else {
-    uint32_t v;
-    if (hash_find(g, g.im.acl_default, S.src_vni, S.dst_vni, 0, v)) {
+    uint32_t v = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].acl_def : 0;
+    if (v) {
       action = v - 1;
       S.acl = action == DP_ACL_DENY ? 4 : 3;
     } else {
@@ -991,15 +1044,17 @@ __device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, c
   if (!(S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST))) return;
   if (S.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) return;
   if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
-  uint32_t one;
-  if (!hash_find(g, g.im.nat_pervni, S.src_vni, 0, 0, one)) { done(S, DP_DONE_UNROUTABLE); return; }
+  const VniRec VR = g.at<VniRec>(g.im.vni_recs)[S.vni_idx];
+  if (!VR.pervni) { done(S, DP_DONE_UNROUTABLE); return; }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
+  const int32_t pi = pair_of(g, S);
+  const int32_t st = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].nat_src : -1;
   bool has_p = H.l4 == L4_TCP || H.l4 == L4_UDP;
   bool modified = false;
   if (S.flags & DP_META_REQ_STATIC_NAT_SRC) {
     bool mod = false;
     uint32_t na; bool hp; uint16_t np = 0;
-    if (H.net == 4 && nat_find(g, 1, S.src_vni, S.dst_vni, S.v4src, has_p, S.sport, na, hp, np)) {
+    if (H.net == 4 && nat_find(g, st, S.v4src, has_p, S.sport, na, hp, np)) {
       if (!((na >> 28) == 0xe || na == 0xffffffffu)) {
         if (na != S.v4src) { S.v4src = na; mod = true; }
         if (has_p && hp && np != S.sport) { S.sport = np; mod = true; }
@@ -1011,7 +1066,7 @@ __device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, c
   if (S.flags & DP_META_REQ_STATIC_NAT_DST) {
     bool mod = false;
     uint32_t na; bool hp; uint16_t np = 0;
-    if (H.net == 4 && nat_find(g, 0, S.src_vni, 0, S.v4dst, has_p, S.dport, na, hp, np)) {
+    if (H.net == 4 && nat_find(g, VR.nat_dst, S.v4dst, has_p, S.dport, na, hp, np)) {
       if (na != S.v4dst) { S.v4dst = na; mod = true; }
       if (has_p && hp && np != S.dport) { S.dport = np; mod = true; }
     }
@@ -1043,27 +1098,28 @@ __device__ __forceinline__ bool adj_find(const Img &g, uint32_t oif, uint8_t fam
 __device__ __forceinline__ void stage_egress(const Img &g, const Frame &F, const Hdr &H, State &S) {
   if (S.done != DONE_NONE) return;
   if (!S.has_oif) { done(S, DP_DONE_ROUTE_FAILURE); return; }
-  uint8_t fam; Addr16 a;
-  if (S.has_nh) { fam = S.nh_fam; a = S.nh; }
-  else if (S.encap || H.net) cur_dst(F, H, S, fam, a);
-  else { done(S, DP_DONE_NOT_IP); return; }
-  uint8_t dmac[6];
-  if (!adj_find(g, S.oif, fam, a, dmac)) { done(S, DP_DONE_MISS_L2_RESOLUTION); return; }
-  uint8_t z = 0;
-  for (int i = 0; i < 6; i++) z |= dmac[i];
-  if (z == 0) { done(S, DP_DONE_INVALID_DST_MAC); return; }
-  Iface I;
-  if (!find_iface(g, S.oif, I)) { done(S, DP_DONE_INTERFACE_UNKNOWN); return; }
-  if (I.admin == DP_IF_DOWN) { done(S, DP_DONE_INTERFACE_ADM_DOWN); return; }
-  if (I.oper == DP_IF_DOWN) { done(S, DP_DONE_INTERFACE_OPER_DOWN); return; }
-  if (!(I.iftype == DP_IFT_ETHERNET || I.iftype == DP_IFT_DOT1Q)) { done(S, DP_DONE_INTERFACE_UNSUPPORTED); return; }
+  uint64_t dmac = S.eg_dmac;
+  if (S.eg_code == DPD_EG_NEED_ADJ) {
+    // no next-hop address: adjacency of the packet's (current) destination
+    uint8_t fam; Addr16 a;
+    if (S.encap || H.net) cur_dst(F, H, S, fam, a);
+    else { done(S, DP_DONE_NOT_IP); return; }
+    uint8_t m[6];
+    if (!adj_find(g, S.oif, fam, a, m)) { done(S, DP_DONE_MISS_L2_RESOLUTION); return; }
+    dmac = load_mac(m);
+    if (dmac == 0) { done(S, DP_DONE_INVALID_DST_MAC); return; }
+    if (S.if_code != 255) { done(S, S.if_code); return; }
+  } else if (S.eg_code != DP_DONE_DELIVERED) {
+    done(S, S.eg_code);
+    return;
+  }
   if (S.encap) {
     S.o_eth = true;
-    S.odst = load_mac(dmac);
-    S.osrc = load_mac(I.mac);
+    S.odst = dmac;
+    S.osrc = S.eg_smac;
   } else {
-    S.edst = load_mac(dmac);
-    S.esrc = load_mac(I.mac);
+    S.edst = dmac;
+    S.esrc = S.eg_smac;
     S.eth_dirty = true;
   }
   done(S, DP_DONE_DELIVERED);
@@ -1318,7 +1374,7 @@ __device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S)
 // ---------------------------------------------------------------------------
 // Per-packet body
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint8_t process_packet(const Img &g, uint8_t *slab, uint8_t *hs, uint8_t *buf, uint64_t buf_bytes,
+__device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, lds_u8 *hs, uint8_t *buf, uint64_t buf_bytes,
                                   const dp_pkt_in_t &pin, dp_pkt_out_t &o) {
   if (pin.off < DP_HEADROOM || (((uint64_t)pin.off + pin.len + 15) & ~15ull) > buf_bytes) {
     // layout contract violated: never touch memory outside the buffer
@@ -1327,6 +1383,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, uint8_t *slab, u
     o.fib_entry = 0xffffffffu; o.acl_rule = 0xffffffffu;
     return o.done;
   }
+  TS_DECL
   Frame F;
   F.lds = slab;
   F.hs = hs;
@@ -1338,7 +1395,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, uint8_t *slab, u
     const uint4 *src = reinterpret_cast<const uint4 *>(buf + (pin.off & ~15u));
     int nchunk = (F.shift + F.len + 15) >> 4;
     if (nchunk > WIN / 16) nchunk = WIN / 16;
-    uint32_t *dst = reinterpret_cast<uint32_t *>(F.lds);
+    lds_u32 *dst = reinterpret_cast<lds_u32 *>(F.lds);
     for (int c = 0; c < nchunk; c++) {
       uint4 q = src[c];
       dst[4 * c] = q.x; dst[4 * c + 1] = q.y; dst[4 * c + 2] = q.z; dst[4 * c + 3] = q.w;
@@ -1346,6 +1403,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, uint8_t *slab, u
   }
   o.off = pin.off; o.len = pin.len; o.acl = 0; o.oif = 0; o.dst_vni = 0; o.src_vni = 0;
   o.fib_entry = 0xffffffffu; o.acl_rule = 0xffffffffu;
+  TS(0);
   Hdr H;
   if (!parse(F, 0, H)) {
     o.done = DP_DONE_NOT_ETHERNET;
@@ -1356,32 +1414,33 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, uint8_t *slab, u
   S.done = DONE_NONE;
   S.flags = DP_META_INITIALIZED | DP_META_KEEP;
   S.has_vrf = false; S.vrf = 0; S.src_vni = 0; S.dst_vni = 0;
-  S.has_oif = false; S.oif = 0; S.has_nh = false; S.nh_fam = 0;
+  S.has_oif = false; S.oif = 0; S.eg_code = DP_DONE_ROUTE_FAILURE; S.if_code = 255;
+  S.eg_dmac = S.eg_smac = 0; S.fib = -1; S.vni_idx = -1; S.pair = -1;
   S.has_dscp = false; S.dscp = S.ecn = 0;
   S.fib_entry = 0xffffffffu; S.acl_rule = 0xffffffffu; S.acl = 0;
   S.encap = false; S.o_eth = false; S.inner_l4_ck = false; S.inner_v4_ck = 0; S.inner_l4_ck_val = 0;
   S.ttl = 0; S.v4src = S.v4dst = 0;
   load_fields(F, H, S);
+  TS(1);
   if (pin.flags & DP_IN_SEEDED_OVERLAY) {
-    uint32_t fi;
-    if (!hash_find(g, g.im.vni_fib, pin.src_vni, 0, 0, fi)) done(S, DP_DONE_UNROUTABLE);
-    else {
-      S.src_vni = pin.src_vni;
-      S.has_vrf = true;
-      S.vrf = g.at<FibRec>(g.im.fibs)[fi].vrf_id;
-      S.flags |= DP_META_IS_OVERLAY;
-    }
+    if (!enter_vni(g, S, pin.src_vni)) done(S, DP_DONE_UNROUTABLE);
   } else {
     stage_ingress(g, F, H, S, pin.iif);
     stage_ipforward(g, F, H, S);  // IP-Forward-1
   }
+  TS(2);
   // IcmpErrorHandler: overlay ICMP errors need flow state (outside the slice)
   if (S.done == DONE_NONE && (S.flags & DP_META_IS_OVERLAY) && icmp_is_error(F, H)) done(S, DP_DONE_UNHANDLED);
   stage_flow_filter(g, F, H, S);
+  TS(3);
   stage_acl(g, F, H, S);
+  TS(4);
   stage_static_nat(g, F, H, S);
+  TS(5);
   stage_ipforward(g, F, H, S);  // IP-Forward-2
+  TS(6);
   stage_egress(g, F, H, S);
+  TS(7);
   if (S.done == DP_DONE_DELIVERED) {
     if (!S.encap && icmp_is_error(F, H)) S.done = DP_DONE_UNHANDLED;
     else {
@@ -1401,6 +1460,8 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, uint8_t *slab, u
   o.fib_entry = S.fib_entry;
   o.acl_rule = S.acl_rule;
   o.acl = S.acl;
+  TS(8);
+  TS_FLUSH();
   return o.done;
 }
 
@@ -1423,7 +1484,7 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__re
     Img g{img_base, im};
     const dp_pkt_in_t pin = in[i];
     dp_pkt_out_t o;
-    done_code = process_packet(g, slab_all + tid * SLAB, hash_all + tid * 64, buf, buf_bytes, pin, o);
+    done_code = process_packet(g, (lds_u8 *)(slab_all + tid * SLAB), (lds_u8 *)(hash_all + tid * 64), buf, buf_bytes, pin, o);
     out[i] = o;
   }
   __syncthreads();
@@ -1446,6 +1507,16 @@ extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uin
 }
 #else
 // Launch wrapper used by the runtime (dp_runtime.cpp).
+#if defined(DP_TIMING)
+extern "C" int dp_debug_stage_cycles(unsigned long long *out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stage_cycles), 16 * sizeof(unsigned long long)) != hipSuccess) return -5;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, sizeof(z)) != hipSuccess) return -5;
+  }
+  return 0;
+}
+#endif
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    uint32_t n, uint64_t *stats, hipStream_t stream) {

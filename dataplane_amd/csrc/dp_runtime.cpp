@@ -47,10 +47,10 @@ struct DevImage {
   ~DevImage() {
     if (dev) {
       int prev = 0;
-      hipGetDevice(&prev);
-      hipSetDevice(device);
+      (void)hipGetDevice(&prev);
+      (void)hipSetDevice(device);
       (void)hipFree(dev);
-      hipSetDevice(prev);
+      (void)hipSetDevice(prev);
     }
   }
 };
@@ -110,14 +110,14 @@ int dp_ctx_create(int device_ordinal, dp_ctx_t **out) {
 
 int dp_ctx_destroy(dp_ctx_t *c) {
   if (!c) return DP_EINVAL;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->pinned.reset();
-  if (c->d_buf) hipFree(c->d_buf);
-  if (c->d_in) hipFree(c->d_in);
-  if (c->d_out) hipFree(c->d_out);
-  if (c->d_stats) hipFree(c->d_stats);
-  if (c->stream) hipStreamDestroy(c->stream);
+  if (c->d_buf) (void)hipFree(c->d_buf);
+  if (c->d_in) (void)hipFree(c->d_in);
+  if (c->d_out) (void)hipFree(c->d_out);
+  if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
 }
@@ -127,7 +127,7 @@ int dp_tables_publish(dp_ctx_t *c, const dp_tables_desc_t *tables) {
   dpd::BuiltImage bi;
   int rc = dpd::build_image(tables, bi);
   if (rc) return fail(rc, "table compile rejected the descriptors");
-  hipSetDevice(c->device);
+  (void)hipSetDevice(c->device);
   auto img = std::make_shared<DevImage>();
   img->device = c->device;
   hipError_t e = hipMalloc(&img->dev, bi.bytes.size());
@@ -189,18 +189,18 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
   for (uint32_t i = 0; i < n; i++)
     if (in[i].off < DP_HEADROOM || (uint64_t)in[i].off + in[i].len > buf_bytes)
       return fail(DP_EINVAL, "frame outside the burst buffer / headroom");
-  hipSetDevice(c->device);
+  (void)hipSetDevice(c->device);
   hipError_t e;
   uint64_t need = ((buf_bytes + 15) & ~15ull) + 16;
   if (need > c->d_buf_cap) {
-    if (c->d_buf) hipFree(c->d_buf);
+    if (c->d_buf) (void)hipFree(c->d_buf);
     c->d_buf = nullptr;
     if ((e = hipMalloc(&c->d_buf, need)) != hipSuccess) { c->d_buf_cap = 0; return fail(DP_ENOMEM, "hipMalloc burst", e); }
     c->d_buf_cap = need;
   }
   if (n > c->cap_n) {
-    if (c->d_in) hipFree(c->d_in);
-    if (c->d_out) hipFree(c->d_out);
+    if (c->d_in) (void)hipFree(c->d_in);
+    if (c->d_out) (void)hipFree(c->d_out);
     c->d_in = nullptr; c->d_out = nullptr; c->cap_n = 0;
     if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess) return fail(DP_ENOMEM, "hipMalloc in", e);
     if ((e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess) return fail(DP_ENOMEM, "hipMalloc out", e);

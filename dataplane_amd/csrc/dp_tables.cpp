@@ -219,7 +219,10 @@ Iv prefix_iv(const dp_prefix_t &p, int fam) {
   return Iv{k, k + span};
 }
 
-Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam) {
+// `gkv_out`: group keys -> group index; `order_out`: rules in global rule
+// index order (the order of the action arrays).
+Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam,
+                            std::vector<KV> *gkv_out, std::vector<const dp_rule_t *> *order_out) {
   Classifier C{};
   // groups in first-appearance order, rules keep their match order
   std::vector<std::vector<uint32_t>> groups;
@@ -250,6 +253,7 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
     G.sum_words = (G.words + 63) / 64;
     G.rule_base = (uint32_t)action.size();
     for (uint32_t ri : gr) {
+      if (order_out) order_out->push_back(&rules[ri].r);
       action.push_back(rules[ri].r.action);
       action2.push_back(rules[ri].r.action2);
       orig.push_back(rules[ri].orig);
@@ -345,6 +349,7 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
     grecs.push_back(G);
   }
   C.groups = build_hash(ib, gkv);
+  if (gkv_out) *gkv_out = gkv;
   C.group_recs = ib.put(grecs);
   C.action = ib.put(action);
   C.action2 = ib.put(action2);
@@ -402,6 +407,37 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     const dp_route_nh_t &n = d->route_nhs[i];
     if (n.n_entries == 0 || (uint64_t)n.first_entry + n.n_entries > d->n_entries) return DP_EINVAL;
   }
+  // host views of the interface and adjacency tables (last insert wins, as
+  // the reference's maps do)
+  std::unordered_map<uint32_t, const dp_iface_t *> ifmap;
+  for (uint32_t i = 0; i < d->n_ifaces; i++) ifmap[d->ifaces[i].ifindex] = &d->ifaces[i];
+  std::unordered_map<std::string, const dp_adjacency_t *> adjmap;
+  auto adj_key = [](uint32_t oif, uint8_t fam, const uint8_t *addr) {
+    std::string k((const char *)&oif, 4);
+    k.push_back((char)fam);
+    k.append((const char *)addr, fam == 6 ? 16 : 4);
+    return k;
+  };
+  for (uint32_t i = 0; i < d->n_adjs; i++) {
+    const dp_adjacency_t &a = d->adjs[i];
+    if (a.addr.family != 4 && a.addr.family != 6) return DP_EINVAL;
+    adjmap[adj_key(a.ifindex, a.addr.family, a.addr.addr)] = &a;
+  }
+  auto mac48 = [](const uint8_t *m) {
+    uint64_t x = 0;
+    for (int i = 0; i < 6; i++) x = (x << 8) | m[i];
+    return x;
+  };
+  // Egress::egress_process's interface checks (egress.rs:168-190)
+  auto oif_code = [&](uint32_t oif) -> uint8_t {
+    auto it = ifmap.find(oif);
+    if (it == ifmap.end()) return DP_DONE_INTERFACE_UNKNOWN;
+    const dp_iface_t &f = *it->second;
+    if (f.admin_state == DP_IF_DOWN) return DP_DONE_INTERFACE_ADM_DOWN;
+    if (f.oper_state == DP_IF_DOWN) return DP_DONE_INTERFACE_OPER_DOWN;
+    if (!(f.iftype == DP_IFT_ETHERNET || f.iftype == DP_IFT_DOT1Q)) return DP_DONE_INTERFACE_UNSUPPORTED;
+    return 255;
+  };
   std::vector<Instr> instrs;
   for (uint32_t i = 0; i < d->n_instrs; i++) {
     const dp_instr_t &s = d->instrs[i];
@@ -413,6 +449,26 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     x.vni = s.vni;
     memcpy(x.mac, s.mac, 6);
     memcpy(x.addr, s.addr.addr, s.addr.family == 6 ? 16 : 4);
+    x.if_code = 255;
+    if (s.kind == DP_INSTR_EGRESS) {
+      auto it = ifmap.find(s.ifindex);
+      if (it != ifmap.end()) x.eg_smac = mac48(it->second->mac);
+      x.if_code = oif_code(s.ifindex);
+      if (!(s.flags & DP_INSTR_HAS_IFINDEX)) {
+        x.eg_code = DP_DONE_ROUTE_FAILURE;
+      } else if (!(s.flags & DP_INSTR_HAS_ADDR)) {
+        x.eg_code = DPD_EG_NEED_ADJ;
+      } else {
+        if (s.addr.family != 4 && s.addr.family != 6) return DP_EINVAL;
+        auto a = adjmap.find(adj_key(s.ifindex, s.addr.family, s.addr.addr));
+        if (a == adjmap.end()) x.eg_code = DP_DONE_MISS_L2_RESOLUTION;
+        else if (mac48(a->second->mac) == 0) x.eg_code = DP_DONE_INVALID_DST_MAC;
+        else {
+          x.eg_dmac = mac48(a->second->mac);
+          x.eg_code = x.if_code != 255 ? x.if_code : (uint8_t)DP_DONE_DELIVERED;
+        }
+      }
+    }
     instrs.push_back(x);
   }
   std::vector<Entry> entries;
@@ -468,29 +524,51 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
   im.fibs = ib.put(fibs);
   im.n_fibs = d->n_fibs;
   im.vrf_fib = build_hash(ib, vrfkv);
-  im.vni_fib = build_hash(ib, vnikv);
+  std::unordered_map<uint32_t, uint32_t> vrf2fib, vni2fib;  // last insert wins
+  for (auto &e : vrfkv) vrf2fib[e.k0] = e.v;
+  std::vector<uint32_t> vni_order;
+  for (auto &e : vnikv) {
+    if (!vni2fib.count(e.k0)) vni_order.push_back(e.k0);
+    vni2fib[e.k0] = e.v;
+  }
   im.route_nhs = ib.put(nhs);
   im.entries = ib.put(entries);
   im.instrs = ib.put(instrs);
 
   // --- interfaces / adjacencies
-  std::vector<Iface> ifs;
+  std::vector<IfRec> ifs;
   std::vector<KV> ifkv;
-  for (uint32_t i = 0; i < d->n_ifaces; i++) {
-    const dp_iface_t &s = d->ifaces[i];
-    Iface x{};
+  uint32_t max_if = 0;
+  auto if_rec = [&](const dp_iface_t &s) {
+    IfRec x{};
     x.ifindex = s.ifindex;
-    x.admin = s.admin_state;
-    x.oper = s.oper_state;
-    x.iftype = s.iftype;
-    x.attach = s.attach;
+    x.valid = 1;
+    x.pre_code = s.admin_state == DP_IF_DOWN ? (uint8_t)DP_DONE_INTERFACE_ADM_DOWN
+               : !(s.iftype == DP_IFT_ETHERNET || s.iftype == DP_IFT_DOT1Q) ? (uint8_t)DP_DONE_INTERFACE_UNSUPPORTED
+               : 255;
+    x.post_code = s.attach == DP_ATTACH_VRF ? 255
+                : s.attach == DP_ATTACH_BRIDGE ? (uint8_t)DP_DONE_INTERFACE_UNSUPPORTED
+                : (uint8_t)DP_DONE_INTERFACE_DETACHED;
     x.vrf_id = s.vrf_id;
-    memcpy(x.mac, s.mac, 6);
-    ifkv.push_back(KV{s.ifindex, 0, 0, (uint32_t)ifs.size()});
-    ifs.push_back(x);
+    auto f = vrf2fib.find(s.vrf_id);
+    x.fib = f == vrf2fib.end() ? -1 : (int32_t)f->second;
+    x.mac = mac48(s.mac);
+    return x;
+  };
+  for (auto &kv : ifmap) {
+    ifkv.push_back(KV{kv.first, 0, 0, (uint32_t)ifs.size()});
+    ifs.push_back(if_rec(*kv.second));
+    max_if = std::max(max_if, kv.first);
   }
   im.ifaces = build_hash(ib, ifkv);
-  im.iface_recs = ib.put(ifs);
+  im.if_recs = ib.put(ifs);
+  if (!ifmap.empty() && max_if < 65536) {
+    std::vector<IfRec> direct(max_if + 1);
+    memset(direct.data(), 0, sizeof(IfRec) * direct.size());
+    for (auto &kv : ifmap) direct[kv.first] = if_rec(*kv.second);
+    im.if_direct = ib.put(direct);
+    im.if_direct_n = max_if + 1;
+  }
   {
     uint32_t cap = 2;
     while (cap < 2 * std::max<uint32_t>(1, d->n_adjs)) cap <<= 1;
@@ -526,7 +604,6 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
 
   // --- classifiers
   int rc;
-  std::vector<CRule> tmp;
   struct T { const dp_rule_t *r; uint32_t n; int fam; bool prio; int kind; Classifier *dst; };
   T tabs[6] = {
       {d->acl_v4, d->n_acl_v4, 4, false, 0, &im.acl[0]},
@@ -536,11 +613,25 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
       {d->ff_local_v4, d->n_ff_local_v4, 4, true, 2, &im.ff_local[0]},
       {d->ff_local_v6, d->n_ff_local_v6, 6, true, 2, &im.ff_local[1]},
   };
-  for (auto &t : tabs) {
-    tmp.clear();
-    if ((rc = load_rules(t.r, t.n, t.fam, t.prio, t.kind, tmp))) return rc;
-    *t.dst = build_classifier(ib, tmp, t.fam);
+  std::vector<KV> gkv[6];
+  std::vector<std::vector<CRule>> keep(6);
+  std::vector<const dp_rule_t *> ffr_order[2];
+  for (int ti = 0; ti < 6; ti++) {
+    auto &t = tabs[ti];
+    if ((rc = load_rules(t.r, t.n, t.fam, t.prio, t.kind, keep[ti]))) return rc;
+    *t.dst = build_classifier(ib, keep[ti], t.fam, &gkv[ti], ti == 2 || ti == 3 ? &ffr_order[ti - 2] : nullptr);
   }
+  auto gkey = [](uint32_t a, uint32_t b, uint32_t c) {
+    return ((unsigned __int128)a << 64) | ((unsigned __int128)b << 32) | c;
+  };
+  struct U128Hash { size_t operator()(unsigned __int128 x) const { return std::hash<uint64_t>()((uint64_t)x ^ (uint64_t)(x >> 64) * 0x9E3779B97F4A7C15ull); } };
+  std::unordered_map<unsigned __int128, int32_t, U128Hash> gmap[6];
+  for (int ti = 0; ti < 6; ti++)
+    for (auto &e : gkv[ti]) gmap[ti][gkey(e.k0, e.k1, e.k2)] = (int32_t)e.v;
+  auto group_of = [&](int ti, uint32_t a, uint32_t b) -> int32_t {
+    auto it = gmap[ti].find(gkey(a, b, 0));
+    return it == gmap[ti].end() ? -1 : it->second;
+  };
   std::vector<KV> defkv;
   for (uint32_t i = 0; i < d->n_acl_defaults; i++)
     defkv.push_back(KV{d->acl_defaults[i].src_vni, d->acl_defaults[i].dst_vni, 0, d->acl_defaults[i].action + 1});
@@ -673,6 +764,70 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
   }
   im.nat_tabs = build_hash(ib, ntkv);
   im.nat_pervni = build_hash(ib, pervni);
+
+  // --- per-VNI and per-VNI-pair contexts (precomputed joins)
+  std::unordered_map<unsigned __int128, int32_t, U128Hash> ntmap;
+  std::unordered_map<uint32_t, uint32_t> has_pervni;
+  for (auto &e : ntkv) ntmap[gkey(e.k0, e.k1, e.k2)] = (int32_t)e.v;
+  for (auto &e : pervni) has_pervni[e.k0] = 1;
+  auto nat_tab = [&](uint32_t kind, uint32_t sv, uint32_t dv) -> int32_t {
+    auto it = ntmap.find(gkey(kind, sv, dv));
+    return it == ntmap.end() ? -1 : it->second;
+  };
+  std::vector<VniRec> vrecs;
+  std::vector<KV> vnikv2;
+  for (uint32_t vni : vni_order) {
+    VniRec r{};
+    r.vni = vni;
+    r.fib = vni2fib[vni];
+    r.vrf_id = d->fibs[r.fib].vrf_id;
+    r.ffr[0] = group_of(2, vni, 0);
+    r.ffr[1] = group_of(3, vni, 0);
+    r.nat_dst = nat_tab(0, vni, 0);
+    r.pervni = has_pervni.count(vni) ? 1 : 0;
+    vnikv2.push_back(KV{vni, 0, 0, (uint32_t)vrecs.size()});
+    vrecs.push_back(r);
+  }
+  im.vni_fib = build_hash(ib, vnikv2);
+  im.vni_recs = ib.put(vrecs);
+  im.n_vni_recs = (uint32_t)vrecs.size();
+  std::unordered_map<uint64_t, uint32_t> pidx;
+  std::vector<PairRec> prs;
+  std::vector<KV> pkv;
+  std::unordered_map<uint64_t, uint32_t> defmap;
+  for (auto &e : defkv) defmap[((uint64_t)e.k0 << 32) | e.k1] = e.v;
+  auto pair_of = [&](uint32_t sv, uint32_t dv) -> uint32_t {
+    uint64_t k = ((uint64_t)sv << 32) | dv;
+    auto it = pidx.find(k);
+    if (it != pidx.end()) return it->second;
+    PairRec r{};
+    r.ffl[0] = group_of(4, sv, dv);
+    r.ffl[1] = group_of(5, sv, dv);
+    r.acl[0] = group_of(0, sv, dv);
+    r.acl[1] = group_of(1, sv, dv);
+    auto dm = defmap.find(k);
+    r.acl_def = dm == defmap.end() ? 0 : dm->second;
+    r.nat_src = nat_tab(1, sv, dv);
+    auto f = vni2fib.find(dv);
+    r.dst_fib = f == vni2fib.end() ? -1 : (int32_t)f->second;
+    r.dst_vni = dv;
+    uint32_t id = (uint32_t)prs.size();
+    pidx[k] = id;
+    pkv.push_back(KV{sv, dv, 0, id});
+    prs.push_back(r);
+    return id;
+  };
+  for (int t = 0; t < 2; t++) {
+    std::vector<uint32_t> aux;
+    for (const dp_rule_t *r : ffr_order[t]) aux.push_back(pair_of(r->vni_a, r->action));
+    im.ff_remote[t].aux = ib.put(aux);
+  }
+  for (int ti : {0, 1, 4, 5})
+    for (auto &e : gkv[ti]) if (e.k2 == 0) pair_of(e.k0, e.k1);
+  for (auto &e : defkv) pair_of(e.k0, e.k1);
+  for (auto &e : ntkv) if (e.k0 == 1) pair_of(e.k1, e.k2);
+  im.pairs = build_hash(ib, pkv);
+  im.pair_recs = ib.put(prs);
   im.nat_tab_recs = ib.put(ntabs);
   im.nat_ents = ib.put(nents);
   im.nat_prs = ib.put(nprs);
