@@ -148,13 +148,25 @@ struct AdjMap {
 // --- classifier -----------------------------------------------------------
 // Field order: 0 src ip, 1 dst ip, 2 sport, 3 dport.  Keys are 128-bit
 // (hi, lo); v4 addresses and ports use hi = 0.
+// Elementary-interval index of one field.  Two forms:
+//  - multibit table (v4 addresses, ports; root != 0): root[key >> (kbits - s0)]
+//    then 8-bit blocks; an entry with bit 31 set is the interval's row id,
+//    otherwise the index of the next 256-entry block (<= 3 more levels);
+//  - sorted bounds (v6, or few intervals): binary search, narrowed by an
+//    optional 16-bit jump table, then rows[interval].
+#define DPD_LEAF 0x80000000u
 struct FieldIdx {
   uint64_t bounds;     // offset of uint64_t[2*n] (hi, lo) interval starts, ascending
   uint64_t rows;       // offset of uint32_t[n] row index per interval
   uint64_t jump;       // offset of uint32_t[65537]: interval containing the start of
                        // each 16-bit top-bits bucket (0: no jump table, n small)
+  uint64_t root;       // multibit root uint32_t[1 << s0] (0: bounds form)
+  uint64_t blocks;     // multibit blocks uint32_t[256 * k]
   uint32_t n;          // number of intervals (>= 1; bounds[0] = 0)
-  uint32_t shift;      // key >> shift = bucket (v4 ip: 16, port: 0, v6: hi >> 48)
+  uint8_t shift;       // key >> shift = bucket (v4 ip: 16, port: 0, v6: hi >> 48)
+  uint8_t s0;          // multibit root stride (bits)
+  uint8_t kbits;       // multibit key width (32 or 16)
+  uint8_t pad;
 };
 
 struct Group {
@@ -200,9 +212,11 @@ struct NatEnt {
 struct NatTab {
   uint64_t bounds;           // uint32_t[n] interval starts (host order)
   uint64_t longest;          // int32_t[n] longest covering entry (global idx) or -1
-  uint64_t jump;             // uint32_t[65537] bucket (addr >> 16) -> interval (0: none)
+  uint64_t root;             // multibit table (0: bounds form); leaf = DPD_LEAF | (entry + 1)
+  uint64_t blocks;
   uint32_t n;
-  uint32_t pad;
+  uint8_t s0;                // root stride (16, or 8 for configurations with many tables)
+  uint8_t pad[3];
 };
 
 struct Image {

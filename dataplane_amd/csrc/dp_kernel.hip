@@ -546,18 +546,37 @@ __device__ __forceinline__ int64_t classify(const Img &g, uint64_t group_recs, i
   if (gi < 0) return -1;
   const Group G = g.at<Group>(group_recs)[gi];
   Key128 key[4] = {src, dst, Key128{0, sp}, Key128{0, dp}};
-  uint32_t lo[4], hi[4];
+  uint32_t lo[4], hi[4], e[4];
+  // level 0 of every field: multibit root entry, or the jump-table range
 #pragma unroll
   for (int f = 0; f < 4; f++) {
     lo[f] = 0;
     hi[f] = G.f[f].n;
-    if (G.f[f].jump) {
+    e[f] = DPD_LEAF;
+    if (G.f[f].root) {
+      uint32_t k = (uint32_t)key[f].lo;
+      e[f] = g.at<uint32_t>(G.f[f].root)[k >> (G.f[f].kbits - G.f[f].s0)];
+      hi[f] = lo[f] + 1;  // no bounds search
+    } else if (G.f[f].jump) {
       const uint32_t *jt = g.at<uint32_t>(G.f[f].jump);
       uint32_t t = bucket_of(G.f[f], key[f]);
       lo[f] = jt[t];
       hi[f] = jt[t + 1] + 1;
     }
   }
+  // multibit levels (8 bits each), in lockstep
+#pragma unroll
+  for (int l = 1; l <= 3; l++) {
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+      if (!(e[f] & DPD_LEAF)) {
+        int rem = (int)G.f[f].kbits - (int)G.f[f].s0 - 8 * l;
+        uint32_t k = (uint32_t)key[f].lo;
+        e[f] = g.at<uint32_t>(G.f[f].blocks)[(e[f] << 8) | ((k >> rem) & 0xff)];
+      }
+    }
+  }
+  // bounds form: binary search in lockstep
   for (int it = 0; it < 20; it++) {
     bool any = false;
 #pragma unroll
@@ -573,13 +592,14 @@ __device__ __forceinline__ int64_t classify(const Img &g, uint64_t group_recs, i
     }
     if (!any) break;
   }
+  uint32_t rr[4];
+#pragma unroll
+  for (int f = 0; f < 4; f++)
+    rr[f] = G.f[f].root ? (e[f] & ~DPD_LEAF) : g.at<uint32_t>(G.f[f].rows)[lo[f]];
   const uint64_t *pool = g.at<uint64_t>(G.pool);
   uint32_t stride = G.sum_words + G.words;
   uint32_t r0 = g.at<uint16_t>(G.proto_rows)[proto];
-  uint32_t r1 = g.at<uint32_t>(G.f[0].rows)[lo[0]];
-  uint32_t r2 = g.at<uint32_t>(G.f[1].rows)[lo[1]];
-  uint32_t r3 = g.at<uint32_t>(G.f[2].rows)[lo[2]];
-  uint32_t r4 = g.at<uint32_t>(G.f[3].rows)[lo[3]];
+  uint32_t r1 = rr[0], r2 = rr[1], r3 = rr[2], r4 = rr[3];
   const uint64_t *p0 = pool + (uint64_t)r0 * stride, *p1 = pool + (uint64_t)r1 * stride;
   const uint64_t *p2 = pool + (uint64_t)r2 * stride, *p3 = pool + (uint64_t)r3 * stride;
   const uint64_t *p4 = pool + (uint64_t)r4 * stride;
@@ -599,88 +619,156 @@ __device__ __forceinline__ int64_t classify(const Img &g, uint64_t group_recs, i
 // ---------------------------------------------------------------------------
 // Static NAT
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool nat_find(const Img &g, int32_t ti, uint32_t addr,
-                         bool has_port, uint16_t port, uint32_t &na, bool &hp, uint16_t &np) {
-  if (ti < 0) return false;
-  const NatTab T = g.at<NatTab>(g.im.nat_tab_recs)[ti];
-  if (T.n == 0) return false;
-  const uint32_t *b = g.at<uint32_t>(T.bounds);
-  uint32_t lo = 0, hi = T.n;
-  if (T.jump) {
-    const uint32_t *jt = g.at<uint32_t>(T.jump);
-    lo = jt[addr >> 16];
-    hi = jt[(addr >> 16) + 1] + 1;
-  }
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (b[mid] <= addr) lo = mid; else hi = mid;
-  }
-  int32_t ei = g.at<int32_t>(T.longest)[lo];
+// Two lookups (src table, dst table) in lockstep so their dependent loads
+// overlap.  Per lookup: q.ti table (-1: none), q.addr, q.port.  Result:
+// ok, new address, has_new_port, new port.
+struct NatQ {
+  int32_t ti;
+  uint32_t addr;
+  uint16_t port;
+  bool ok, hp;
+  uint32_t na;
+  uint16_t np;
+};
+
+__device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port) {
+  const NatTab *tabs = g.at<NatTab>(g.im.nat_tab_recs);
   const NatEnt *ents = g.at<NatEnt>(g.im.nat_ents);
   const uint32_t *prs = g.at<uint32_t>(g.im.nat_prs);
-  // IpPortPrefixTrie::lookup: longest matching prefix first
-  while (ei >= 0) {
-    const NatEnt &E = ents[ei];
-    bool cov = false;
-    if (has_port) {
-      if (!E.is_pat) cov = true;
-      else
-        for (uint32_t k = 0; k < E.n_pr; k++) {
-          uint32_t pr = prs[E.first_pr + k];
-          if ((pr & 0xffff) <= port && port <= (pr >> 16)) { cov = true; break; }
-        }
+  const NatRange *ranges = g.at<NatRange>(g.im.nat_ranges);
+  NatTab T[2];
+  uint32_t e[2], lo[2], hi[2];
+  int32_t ei[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    q[k].ok = false; q[k].hp = false; q[k].na = 0; q[k].np = 0;
+    ei[k] = -1; e[k] = DPD_LEAF; lo[k] = 0; hi[k] = 0;
+    if (q[k].ti >= 0) {
+      T[k] = tabs[q[k].ti];
+      if (T[k].root) e[k] = g.at<uint32_t>(T[k].root)[q[k].addr >> (32 - T[k].s0)];
+      else hi[k] = T[k].n;
     }
-    if (cov || E.covers_all) break;
-    ei = E.parent;
   }
-  if (ei < 0) return false;
-  const NatEnt E = ents[ei];
-  const NatRange *R = g.at<NatRange>(g.im.nat_ranges) + E.first_range;
-  uint64_t ip_off = (uint64_t)(addr - E.net);
-  if (!E.is_pat) {
-    if (ip_off >= E.size) return false;
-    int sel = -1;  // last range with olo <= addr
-    uint32_t l = 0, h = E.n_ranges;
-    while (l < h) { uint32_t m = (l + h) >> 1; if (R[m].olo_ip <= addr) l = m + 1; else h = m; }
-    sel = (int)l - 1;
-    if (sel < 0 || addr > R[sel].ohi_ip) return false;
-    uint64_t o2 = ip_off - R[sel].offset;
-    uint64_t tl = (uint64_t)R[sel].thi_ip - R[sel].tlo_ip + 1;
-    if (o2 >= tl) return false;
-    na = R[sel].tlo_ip + (uint32_t)o2;
-    hp = false;
-    return true;
+  // multibit levels / small bounds search
+#pragma unroll
+  for (int l = 1; l <= 3; l++) {
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+      if (!(e[k] & DPD_LEAF))
+        e[k] = g.at<uint32_t>(T[k].blocks)[(e[k] << 8) | ((q[k].addr >> (32 - T[k].s0 - 8 * l)) & 0xff)];
   }
-  if (!has_port) return false;
-  int pk = -1;
-  for (uint32_t k = 0; k < E.n_pr; k++) {
-    uint32_t pr = prs[E.first_pr + k];
-    if ((pr & 0xffff) <= port && port <= (pr >> 16)) { pk = (int)k; break; }
+  for (int it = 0; it < 8; it++) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+      if (hi[k] - lo[k] > 1) {
+        uint32_t mid = (lo[k] + hi[k]) >> 1;
+        if (g.at<uint32_t>(T[k].bounds)[mid] <= q[k].addr) lo[k] = mid; else hi[k] = mid;
+        any = true;
+      }
+    if (!any) break;
   }
-  if (pk < 0) return false;
-  uint32_t pr = prs[E.first_pr + pk];
-  uint64_t plen = (uint64_t)(pr >> 16) - (pr & 0xffff) + 1;
-  uint64_t eo = ip_off * plen + (uint64_t)(port - (pr & 0xffff));
-  if (eo >= E.size) return false;
-  uint32_t l = 0, h = E.n_ranges;
-  while (l < h) {
-    uint32_t m = (l + h) >> 1;
-    bool le = R[m].olo_ip < addr || (R[m].olo_ip == addr && R[m].olo_port <= port);
-    if (le) l = m + 1; else h = m;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if (q[k].ti < 0 || T[k].n == 0) continue;
+    ei[k] = T[k].root ? (int32_t)(e[k] & ~DPD_LEAF) - 1 : g.at<int32_t>(T[k].longest)[lo[k]];
   }
-  int sel = (int)l - 1;
-  if (sel < 0) return false;
-  const NatRange RR = R[sel];
-  if (addr > RR.ohi_ip || (addr == RR.ohi_ip && port > RR.ohi_port)) return false;
-  uint64_t o2 = eo - RR.offset;
-  uint64_t tpl = (uint64_t)RR.thi_port - RR.tlo_port + 1;
-  uint64_t tip = (uint64_t)RR.thi_ip - RR.tlo_ip + 1;
-  if (o2 >= tip * tpl) return false;
-  na = RR.tlo_ip + (uint32_t)(o2 / tpl);
-  np = (uint16_t)(RR.tlo_port + (o2 % tpl));
-  if (np == 0) return false;
-  hp = true;
-  return true;
+  // IpPortPrefixTrie::lookup: longest matching prefix whose port set covers
+  NatEnt E[2];
+  bool fin[2] = {false, false};
+  for (int it = 0; it < 33; it++) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      if (ei[k] < 0 || fin[k]) continue;
+      E[k] = ents[ei[k]];
+      bool cov = false;
+      if (has_port) {
+        if (!E[k].is_pat) cov = true;
+        else
+          for (uint32_t j = 0; j < E[k].n_pr; j++) {
+            uint32_t pr = prs[E[k].first_pr + j];
+            if ((pr & 0xffff) <= q[k].port && q[k].port <= (pr >> 16)) { cov = true; break; }
+          }
+      }
+      if (cov || E[k].covers_all) fin[k] = true;
+      else ei[k] = E[k].parent;
+      any = true;
+    }
+    if (!any) break;
+  }
+  // range of the entry (DisjointRangesBTreeMap::lookup) and the mapping
+  uint32_t rl[2], rh[2];
+  uint64_t eo[2];
+  uint32_t prlo[2];
+  bool live[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    live[k] = ei[k] >= 0;
+    rl[k] = 0; rh[k] = 0; eo[k] = 0; prlo[k] = 0;
+    if (!live[k]) continue;
+    const uint32_t addr = q[k].addr;
+    const uint64_t ip_off = (uint64_t)(addr - E[k].net);
+    if (!E[k].is_pat) {
+      if (ip_off >= E[k].size) { live[k] = false; continue; }
+      eo[k] = ip_off;
+    } else {
+      if (!has_port) { live[k] = false; continue; }
+      int pk = -1;
+      for (uint32_t j = 0; j < E[k].n_pr; j++) {
+        uint32_t pr = prs[E[k].first_pr + j];
+        if ((pr & 0xffff) <= q[k].port && q[k].port <= (pr >> 16)) { pk = (int)j; break; }
+      }
+      if (pk < 0) { live[k] = false; continue; }
+      uint32_t pr = prs[E[k].first_pr + pk];
+      uint64_t plen = (uint64_t)(pr >> 16) - (pr & 0xffff) + 1;
+      eo[k] = ip_off * plen + (uint64_t)(q[k].port - (pr & 0xffff));
+      if (eo[k] >= E[k].size) { live[k] = false; continue; }
+    }
+    rh[k] = E[k].n_ranges;
+  }
+  for (int it = 0; it < 32; it++) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      if (!live[k] || rl[k] >= rh[k]) continue;
+      uint32_t m = (rl[k] + rh[k]) >> 1;
+      const NatRange &R = ranges[E[k].first_range + m];
+      bool le = E[k].is_pat ? (R.olo_ip < q[k].addr || (R.olo_ip == q[k].addr && R.olo_port <= q[k].port))
+                            : R.olo_ip <= q[k].addr;
+      if (le) rl[k] = m + 1; else rh[k] = m;
+      any = true;
+    }
+    if (!any) break;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if (!live[k]) continue;
+    int sel = (int)rl[k] - 1;
+    if (sel < 0) continue;
+    const NatRange R = ranges[E[k].first_range + sel];
+    const uint32_t addr = q[k].addr;
+    if (!E[k].is_pat) {
+      if (addr > R.ohi_ip) continue;
+      uint64_t o2 = eo[k] - R.offset;
+      uint64_t tl = (uint64_t)R.thi_ip - R.tlo_ip + 1;
+      if (o2 >= tl) continue;
+      q[k].na = R.tlo_ip + (uint32_t)o2;
+      q[k].ok = true;
+    } else {
+      if (addr > R.ohi_ip || (addr == R.ohi_ip && q[k].port > R.ohi_port)) continue;
+      uint64_t o2 = eo[k] - R.offset;
+      uint64_t tpl = (uint64_t)R.thi_port - R.tlo_port + 1;
+      uint64_t tip = (uint64_t)R.thi_ip - R.tlo_ip + 1;
+      if (o2 >= tip * tpl) continue;
+      uint16_t np = (uint16_t)(R.tlo_port + (o2 % tpl));
+      if (np == 0) continue;
+      q[k].na = R.tlo_ip + (uint32_t)(o2 / tpl);
+      q[k].np = np;
+      q[k].hp = true;
+      q[k].ok = true;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1051,24 +1139,27 @@ __device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, c
   const int32_t st = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].nat_src : -1;
   bool has_p = H.l4 == L4_TCP || H.l4 == L4_UDP;
   bool modified = false;
+  NatQ q[2];
+  q[0].ti = (H.net == 4 && (S.flags & DP_META_REQ_STATIC_NAT_SRC)) ? st : -1;
+  q[0].addr = S.v4src; q[0].port = has_p ? S.sport : 0;
+  q[1].ti = (H.net == 4 && (S.flags & DP_META_REQ_STATIC_NAT_DST)) ? VR.nat_dst : -1;
+  q[1].addr = S.v4dst; q[1].port = has_p ? S.dport : 0;
+  nat_find2(g, q, has_p);
   if (S.flags & DP_META_REQ_STATIC_NAT_SRC) {
     bool mod = false;
-    uint32_t na; bool hp; uint16_t np = 0;
-    if (H.net == 4 && nat_find(g, st, S.v4src, has_p, S.sport, na, hp, np)) {
-      if (!((na >> 28) == 0xe || na == 0xffffffffu)) {
-        if (na != S.v4src) { S.v4src = na; mod = true; }
-        if (has_p && hp && np != S.sport) { S.sport = np; mod = true; }
-      }
+    // source mapping: UnicastIpAddr::try_from rejects multicast / broadcast
+    if (q[0].ok && !((q[0].na >> 28) == 0xe || q[0].na == 0xffffffffu)) {
+      if (q[0].na != S.v4src) { S.v4src = q[0].na; mod = true; }
+      if (has_p && q[0].hp && q[0].np != S.sport) { S.sport = q[0].np; mod = true; }
     }
     if (mod) S.flags |= DP_META_NATTED_SRC;
     modified |= mod;
   }
   if (S.flags & DP_META_REQ_STATIC_NAT_DST) {
     bool mod = false;
-    uint32_t na; bool hp; uint16_t np = 0;
-    if (H.net == 4 && nat_find(g, VR.nat_dst, S.v4dst, has_p, S.dport, na, hp, np)) {
-      if (na != S.v4dst) { S.v4dst = na; mod = true; }
-      if (has_p && hp && np != S.dport) { S.dport = np; mod = true; }
+    if (q[1].ok) {
+      if (q[1].na != S.v4dst) { S.v4dst = q[1].na; mod = true; }
+      if (has_p && q[1].hp && q[1].np != S.dport) { S.dport = q[1].np; mod = true; }
     }
     if (mod) S.flags |= DP_META_NATTED_DST;
     modified |= mod;

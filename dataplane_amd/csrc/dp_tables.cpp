@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -325,10 +326,37 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
         bounds.push_back((uint64_t)bnd[k]);
         rows.push_back(add_row(cur));
       }
-      G.f[f].bounds = ib.put(bounds);
-      G.f[f].rows = ib.put(rows);
       G.f[f].n = (uint32_t)m;
       G.f[f].jump = 0;
+      if ((f >= 2 || fam == 4) && m > 16) {
+        // multibit table over the interval partition (v4 address: 16-8-8,
+        // port: 8-8; 8-8-8-8 for addresses when the table has many groups)
+        const int kbits = f >= 2 ? 16 : 32;
+        const int s0 = f >= 2 ? 8 : (groups.size() > 128 ? 8 : 16);
+        auto ivl = [&](uint64_t x) -> size_t {
+          return (size_t)(std::upper_bound(bnd.begin(), bnd.end(), (u128)x) - bnd.begin()) - 1;
+        };
+        std::vector<uint32_t> blocks;
+        std::function<uint32_t(uint64_t, int)> node = [&](uint64_t lo, int bits) -> uint32_t {
+          size_t i0 = ivl(lo), i1 = ivl(lo + ((1ull << bits) - 1));
+          if (i0 == i1) return DPD_LEAF | rows[i0];
+          uint32_t ch[256];
+          for (uint32_t c = 0; c < 256; c++) ch[c] = node(lo + ((uint64_t)c << (bits - 8)), bits - 8);
+          uint32_t bi = (uint32_t)(blocks.size() / 256);
+          blocks.insert(blocks.end(), ch, ch + 256);
+          return bi;
+        };
+        std::vector<uint32_t> root((size_t)1 << s0);
+        for (uint64_t b = 0; b < root.size(); b++) root[b] = node(b << (kbits - s0), kbits - s0);
+        G.f[f].root = ib.put(root);
+        if (blocks.empty()) blocks.push_back(0);
+        G.f[f].blocks = ib.put(blocks);
+        G.f[f].s0 = (uint8_t)s0;
+        G.f[f].kbits = (uint8_t)kbits;
+        continue;
+      }
+      G.f[f].bounds = ib.put(bounds);
+      G.f[f].rows = ib.put(rows);
       // bucket = top 16 bits of the key: v4 address >> 16, port itself,
       // v6 address hi64 >> 48
       G.f[f].shift = f >= 2 ? 0 : (fam == 4 ? 16 : 48);
@@ -742,20 +770,32 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
       longest.push_back(best < 0 ? -1 : (int32_t)(base + best));
     }
     NatTab t{};
-    t.bounds = ib.put(b32);
-    t.longest = ib.put(longest);
     t.n = (uint32_t)b32.size();
-    t.jump = 0;
     if (t.n > 16) {
-      std::vector<uint32_t> jump(65537);
-      size_t j = 0;
-      for (uint32_t b = 0; b < 65536; b++) {
-        uint64_t start = (uint64_t)b << 16;
-        while (j + 1 < b32.size() && b32[j + 1] <= start) j++;
-        jump[b] = (uint32_t)j;
-      }
-      jump[65536] = t.n - 1;
-      t.jump = ib.put(jump);
+      // multibit table over the address intervals: leaf = longest entry + 1
+      const int s0 = merged.size() > 128 ? 8 : 16;
+      auto ivl = [&](uint64_t x) -> size_t {
+        return (size_t)(std::upper_bound(b32.begin(), b32.end(), (uint32_t)x) - b32.begin()) - 1;
+      };
+      std::vector<uint32_t> blocks;
+      std::function<uint32_t(uint64_t, int)> node = [&](uint64_t lo, int bits) -> uint32_t {
+        size_t i0 = ivl(lo), i1 = ivl(lo + ((1ull << bits) - 1));
+        if (i0 == i1) return DPD_LEAF | (uint32_t)(longest[i0] + 1);
+        uint32_t ch[256];
+        for (uint32_t c = 0; c < 256; c++) ch[c] = node(lo + ((uint64_t)c << (bits - 8)), bits - 8);
+        uint32_t bi = (uint32_t)(blocks.size() / 256);
+        blocks.insert(blocks.end(), ch, ch + 256);
+        return bi;
+      };
+      std::vector<uint32_t> root((size_t)1 << s0);
+      for (uint64_t b = 0; b < root.size(); b++) root[b] = node(b << (32 - s0), 32 - s0);
+      if (blocks.empty()) blocks.push_back(0);
+      t.root = ib.put(root);
+      t.blocks = ib.put(blocks);
+      t.s0 = (uint8_t)s0;
+    } else {
+      t.bounds = ib.put(b32);
+      t.longest = ib.put(longest);
     }
     KV k = mt.first;
     k.v = (uint32_t)ntabs.size();
