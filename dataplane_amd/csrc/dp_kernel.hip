@@ -1369,95 +1369,168 @@ __device__ __forceinline__ void emit_stack(OW &w, const Frame &F, const Hdr &H, 
 }
 
 // Packet::serialize.  Returns the frame-relative output start.
-__device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S) {
-  if (S.encap) {
-    int inner = H.size;
-    int outer = 14 + (S.o_fam == 4 ? 20 : 40) + 16;
-    int start = S.pay_start - inner - outer;
-    if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
-    const int moved = move_exts(F, H, start + outer + ext_out_off(H));
-    OW w;
-    w.begin(F.g + start);
-    // outer Ethernet (added by Egress)
-    for (int i = 0; i < 6; i++) w.put(mac_b(S.odst, i));
-    for (int i = 0; i < 6; i++) w.put(mac_b(S.osrc, i));
-    w.put16(S.o_fam == 4 ? 0x0800 : 0x86dd);
-    if (S.o_fam == 4) {
-      // Ipv4Header::default() + src/dst/ttl/proto + payload len + checksum
-      uint16_t tot = (uint16_t)(20 + S.o_len);
-      uint64_t s = 0x4500u | S.o_tos;
-      s += tot; s += 0x4000; s += (64u << 8) | 17;
-      s += (S.o_src.w[0] >> 16) + (S.o_src.w[0] & 0xffff) + (S.o_dst.w[0] >> 16) + (S.o_dst.w[0] & 0xffff);
-      uint16_t ck = (uint16_t)~fold(s);
-      w.put(0x45); w.put(S.o_tos); w.put16(tot); w.put16(0); w.put16(0x4000);
-      w.put(64); w.put(17); w.put16(ck); w.put32(S.o_src.w[0]); w.put32(S.o_dst.w[0]);
+// Patch the header stack in place (layout unchanged): exactly the bytes
+// Headers::deparse would change -- rewritten fields, normalised reserved bits.
+__device__ __forceinline__ void patch_stack(const Frame &F, const Hdr &H, const State &S, uint16_t v4ck,
+                                            bool l4, uint16_t l4ck) {
+  uint8_t *q = F.g + H.hb;
+  if (S.eth_dirty) {
+    if (((uintptr_t)q & 1) == 0) {
+      for (int i = 0; i < 6; i += 2) *reinterpret_cast<uint16_t *>(q + i) = (uint16_t)(mac_b(S.edst, i) | (mac_b(S.edst, i + 1) << 8));
+      for (int i = 0; i < 6; i += 2) *reinterpret_cast<uint16_t *>(q + 6 + i) = (uint16_t)(mac_b(S.esrc, i) | (mac_b(S.esrc, i + 1) << 8));
     } else {
-      w.put(0x60 | (S.o_tos >> 4)); w.put((S.o_tos & 0xf) << 4); w.put(0); w.put(0);
-      w.put16(S.o_len); w.put(17); w.put(64);
-      for (int i = 0; i < 4; i++) w.put32(S.o_src.w[i]);
-      for (int i = 0; i < 4; i++) w.put32(S.o_dst.w[i]);
+      for (int i = 0; i < 6; i++) { q[i] = mac_b(S.edst, i); q[6 + i] = mac_b(S.esrc, i); }
     }
-    w.put16(S.o_sport); w.put16(4789); w.put16(S.o_len); w.put16(0);
-    w.put(0x08); w.put(0); w.put(0); w.put(0);
-    w.put((S.o_vni >> 16) & 0xff); w.put((S.o_vni >> 8) & 0xff); w.put(S.o_vni & 0xff); w.put(0);
-    emit_stack(w, F, H, S, H.net == 4, S.inner_v4_ck, S.inner_l4_ck, S.inner_l4_ck_val, moved);
-    w.finish(F, S.pay_start);
-    return start;
   }
-  // update_checksums over the current stack
-  bool v4 = H.net == 4;
-  uint16_t v4ck = v4 ? ipv4_csum(F, H, S) : 0;
-  bool l4 = H.net && H.l4 != L4_NONE && !H.vx;
-  uint16_t l4ck = l4 ? l4_csum(F, H, S) : 0;
-  int start = S.pay_start - H.size;
-  if (start == H.hb) {
-    // patch mode: layout unchanged
-    uint8_t *q = F.g + H.hb;
-    if (S.eth_dirty) {
-      if (((uintptr_t)q & 1) == 0) {
-        for (int i = 0; i < 6; i += 2) *reinterpret_cast<uint16_t *>(q + i) = (uint16_t)(mac_b(S.edst, i) | (mac_b(S.edst, i + 1) << 8));
-        for (int i = 0; i < 6; i += 2) *reinterpret_cast<uint16_t *>(q + 6 + i) = (uint16_t)(mac_b(S.esrc, i) | (mac_b(S.esrc, i + 1) << 8));
-      } else {
-        for (int i = 0; i < 6; i++) { q[i] = mac_b(S.edst, i); q[6 + i] = mac_b(S.esrc, i); }
-      }
-    }
-    if (H.net == 4) {
-      uint8_t *n = F.g + H.net_off;
-      uint8_t fl = F.b(H.net_off + 6);
-      if (fl & 0x80) st8(n + 6, fl & 0x7f);
-      st8(n + 8, S.ttl);
-      st16be(n + 10, v4ck);
-      st32be(n + 12, S.v4src);
-      st32be(n + 16, S.v4dst);
-    } else if (H.net == 6) {
-      st8(F.g + H.net_off + 7, S.ttl);
-    }
+  if (H.net == 4) {
+    uint8_t *n = F.g + H.net_off;
+    uint8_t fl = F.b(H.net_off + 6);
+    if (fl & 0x80) st8(n + 6, fl & 0x7f);
+    st8(n + 8, S.ttl);
+    st16be(n + 10, v4ck);
+    st32be(n + 12, S.v4src);
+    st32be(n + 16, S.v4dst);
+  } else if (H.net == 6) {
+    st8(F.g + H.net_off + 7, S.ttl);
+  }
 #pragma unroll
-    for (int e = 0; e < 3; e++) {
-      if (e >= H.next) break;
-      uint8_t *x = F.g + H.ext_off[e];
-      if (H.ext_kind[e] == HK_EXT_FRAG) { st8(x + 1, 0); st8(x + 3, F.b(H.ext_off[e] + 3) & 0xf9); }
-      if (H.ext_kind[e] == HK_EXT_AUTH) { st8(x + 2, 0); st8(x + 3, 0); }
+  for (int e = 0; e < 3; e++) {
+    if (e >= H.next) break;
+    uint8_t *x = F.g + H.ext_off[e];
+    if (H.ext_kind[e] == HK_EXT_FRAG) { st8(x + 1, 0); st8(x + 3, F.b(H.ext_off[e] + 3) & 0xf9); }
+    if (H.ext_kind[e] == HK_EXT_AUTH) { st8(x + 2, 0); st8(x + 3, 0); }
+  }
+  if (H.net && H.l4) {
+    uint8_t *l = F.g + H.l4_off;
+    if (H.l4 == L4_TCP || H.l4 == L4_UDP) { st16be(l, S.sport); st16be(l + 2, S.dport); }
+    if (H.l4 == L4_TCP) { uint8_t x = F.b(H.l4_off + 12); if (x & 0x0e) st8(l + 12, x & 0xf1); }
+    if (l4) {
+      if (H.l4 == L4_UDP) st16be(l + 6, l4ck);
+      else if (H.l4 == L4_TCP) st16be(l + 16, l4ck);
+      else st16be(l + 2, l4ck);
     }
-    if (H.net && H.l4) {
-      uint8_t *l = F.g + H.l4_off;
-      if (H.l4 == L4_TCP || H.l4 == L4_UDP) { st16be(l, S.sport); st16be(l + 2, S.dport); }
-      if (H.l4 == L4_TCP) { uint8_t x = F.b(H.l4_off + 12); if (x & 0x0e) st8(l + 12, x & 0xf1); }
-      if (l4) {
-        if (H.l4 == L4_UDP) st16be(l + 6, l4ck);
-        else if (H.l4 == L4_TCP) st16be(l + 16, l4ck);
-        else st16be(l + 2, l4ck);
+    if (H.vx) { uint8_t *v = F.g + H.vx_off; if (F.b(H.vx_off) != 0x08) st8(v, 0x08); }
+  }
+}
+
+// word i of an address without a dynamic register index (keeps it out of scratch)
+__device__ __forceinline__ uint32_t aw(const Addr16 &a, int i) {
+  return i == 0 ? a.w[0] : i == 1 ? a.w[1] : i == 2 ? a.w[2] : a.w[3];
+}
+
+// 16-bit word i of the VXLAN outer headers (Eth + IPv4/IPv6 + UDP + VXLAN)
+__device__ __forceinline__ uint32_t outer_word(const State &S, int i, uint32_t ck4) {
+  if (i < 3) return (uint32_t)(S.odst >> (32 - 16 * i)) & 0xffff;
+  if (i < 6) return (uint32_t)(S.osrc >> (32 - 16 * (i - 3))) & 0xffff;
+  if (i == 6) return S.o_fam == 4 ? 0x0800u : 0x86ddu;
+  int j = i - 7;
+  if (S.o_fam == 4) {
+    if (j < 10) {
+      switch (j) {
+        case 0: return 0x4500u | S.o_tos;
+        case 1: return (20u + S.o_len) & 0xffff;
+        case 2: return 0;
+        case 3: return 0x4000u;              // Ipv4Header::default(): DF
+        case 4: return (64u << 8) | 17u;
+        case 5: return ck4;
+        case 6: return S.o_src.w[0] >> 16;
+        case 7: return S.o_src.w[0] & 0xffff;
+        case 8: return S.o_dst.w[0] >> 16;
+        default: return S.o_dst.w[0] & 0xffff;
       }
-      if (H.vx) { uint8_t *v = F.g + H.vx_off; if (F.b(H.vx_off) != 0x08) st8(v, 0x08); }
     }
+    j -= 10;
+  } else {
+    if (j < 20) {
+      if (j == 0) return ((0x60u | (S.o_tos >> 4)) << 8) | ((S.o_tos & 0xfu) << 4);
+      if (j == 1) return 0;
+      if (j == 2) return S.o_len;
+      if (j == 3) return (17u << 8) | 64u;
+      int k = j - 4;
+      uint32_t w = k < 8 ? aw(S.o_src, k >> 1) : aw(S.o_dst, (k - 8) >> 1);
+      return (k & 1) ? (w & 0xffff) : (w >> 16);
+    }
+    j -= 20;
+  }
+  switch (j) {
+    case 0: return S.o_sport;
+    case 1: return 4789u;
+    case 2: return S.o_len;
+    case 3: return 0;                        // outer UDP checksum 0
+    case 4: return 0x0800u;                  // VXLAN flags: I
+    case 5: return 0;
+    case 6: return (S.o_vni >> 8) & 0xffff;
+    default: return (S.o_vni & 0xff) << 8;
+  }
+}
+
+// Write the outer headers at p (any alignment), in 4/2/1-byte stores.
+__device__ __forceinline__ void write_outer(uint8_t *p, const State &S) {
+  uint32_t ck4 = 0;
+  if (S.o_fam == 4) {
+    uint64_t s = 0x4500u | S.o_tos;
+    s += (uint16_t)(20 + S.o_len); s += 0x4000; s += (64u << 8) | 17;
+    s += (S.o_src.w[0] >> 16) + (S.o_src.w[0] & 0xffff) + (S.o_dst.w[0] >> 16) + (S.o_dst.w[0] & 0xffff);
+    ck4 = (uint16_t)~fold(s);
+  }
+  const int nw = S.o_fam == 4 ? 25 : 35;
+  const uintptr_t a = (uintptr_t)p;
+  if ((a & 3) == 0) {
+#pragma unroll 1
+    for (int i = 0; i + 1 < nw; i += 2)
+      *reinterpret_cast<uint32_t *>(p + 2 * i) = bswap16(outer_word(S, i, ck4)) | ((uint32_t)bswap16(outer_word(S, i + 1, ck4)) << 16);
+    if (nw & 1) *reinterpret_cast<uint16_t *>(p + 2 * (nw - 1)) = bswap16(outer_word(S, nw - 1, ck4));
+  } else if ((a & 1) == 0) {
+#pragma unroll 1
+    for (int i = 0; i < nw; i++) *reinterpret_cast<uint16_t *>(p + 2 * i) = bswap16(outer_word(S, i, ck4));
+  } else {
+#pragma unroll 1
+    for (int i = 0; i < nw; i++) { uint32_t w = outer_word(S, i, ck4); p[2 * i] = (uint8_t)(w >> 8); p[2 * i + 1] = (uint8_t)w; }
+  }
+}
+
+// Packet::serialize.  Returns the frame-relative output start.
+__device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S) {
+  const int inner_start = S.pay_start - H.size;
+  const int outer = S.encap ? 14 + (S.o_fam == 4 ? 20 : 40) + 16 : 0;
+  const int start = inner_start - outer;
+  // checksums: encap computed the inner ones (IpForwarder::vxlan_encap);
+  // otherwise update_checksums over the current stack
+  bool l4;
+  uint16_t v4ck, l4ck;
+  if (S.encap) {
+    v4ck = S.inner_v4_ck;
+    l4 = S.inner_l4_ck;
+    l4ck = S.inner_l4_ck_val;
+  } else {
+    v4ck = H.net == 4 ? ipv4_csum(F, H, S) : 0;
+    l4 = H.net && H.l4 != L4_NONE && !H.vx;
+    l4ck = l4 ? l4_csum(F, H, S) : 0;
+  }
+  if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
+  if (inner_start == H.hb) {
+    // the stack keeps its place: patch it (and prepend the outer headers)
+    patch_stack(F, H, S, v4ck, l4, l4ck);
+    if (S.encap) write_outer(F.g + start, S);
     return start;
   }
-  // rewrite mode (parse-limit quirk): re-emit the kept stack before the payload
-  if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
-  const int moved = move_exts(F, H, start + ext_out_off(H));
+  // the parse-limit quirk shrank the stack: re-emit it (after the outer headers)
+  const int moved = move_exts(F, H, start + outer + ext_out_off(H));
   OW w;
   w.begin(F.g + start);
-  emit_stack(w, F, H, S, v4, v4ck, l4, l4ck, moved);
+  if (S.encap) {
+    uint32_t c4 = 0;
+    if (S.o_fam == 4) {
+      uint64_t s = 0x4500u | S.o_tos;
+      s += (uint16_t)(20 + S.o_len); s += 0x4000; s += (64u << 8) | 17;
+      s += (S.o_src.w[0] >> 16) + (S.o_src.w[0] & 0xffff) + (S.o_dst.w[0] >> 16) + (S.o_dst.w[0] & 0xffff);
+      c4 = (uint16_t)~fold(s);
+    }
+    const int nw = S.o_fam == 4 ? 25 : 35;
+#pragma unroll 1
+    for (int i = 0; i < nw; i++) w.put16((uint16_t)outer_word(S, i, c4));
+  }
+  emit_stack(w, F, H, S, H.net == 4, v4ck, l4, l4ck, moved);
   w.finish(F, S.pay_start);
   return start;
 }
@@ -1560,7 +1633,12 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
 // ---------------------------------------------------------------------------
 // Kernel
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(TPB)
+#ifdef DP_WAVES
+#define DP_OCC __attribute__((amdgpu_waves_per_eu(DP_WAVES, DP_WAVES)))
+#else
+#define DP_OCC
+#endif
+__global__ void __launch_bounds__(TPB) DP_OCC
 dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__restrict__ buf,
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
                    dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ stats) {
