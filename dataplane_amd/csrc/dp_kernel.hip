@@ -50,8 +50,21 @@ __device__ unsigned long long g_stage_cycles[16];
 #define TS(k) do {} while (0)
 #define TS_FLUSH() do {} while (0)
 #endif
-constexpr int WIN = 128;          // header window bytes per packet (rest read from HBM)
-constexpr int SLAB = WIN + 4;     // 65 dwords: conflict-free byte reads
+// LDS per work-item: the header window slab + the hash-input scratch.
+// 160 B per work-item (WIN 96 + 4 + 60) lets 8 blocks of 128 share a CU's
+// 160 KiB: 4 waves per SIMD, matching the 128-VGPR budget of DP_WAVES 4.
+#ifndef DP_WIN
+#define DP_WIN 96
+#endif
+#ifndef DP_HS
+#define DP_HS 60
+#endif
+#ifndef DP_WAVES
+#define DP_WAVES 4
+#endif
+constexpr int WIN = DP_WIN;       // header window bytes per packet (rest read from HBM)
+constexpr int SLAB = WIN + 4;     // odd dword stride: conflict-free byte reads
+constexpr int HS = DP_HS;         // hash input scratch (packet_hash_* input <= 59 B)
 constexpr uint8_t DONE_NONE = 255;
 
 // ---------------------------------------------------------------------------
@@ -1232,143 +1245,6 @@ __device__ __forceinline__ void st32be(uint8_t *p, uint32_t v) {
   else { p[0] = v >> 24; p[1] = (v >> 16) & 0xff; p[2] = (v >> 8) & 0xff; p[3] = v & 0xff; }
 }
 
-// Byte-stream writer for rewrite mode: accumulates bytes and flushes
-// aligned dwords; the last dword merges the untouched payload bytes.
-struct OW {
-  uint8_t *p;       // next output address
-  uint32_t acc;
-  // keep the bytes in front of an unaligned start (headroom) intact
-  __device__ __forceinline__ void begin(uint8_t *q) {
-    p = q;
-    int sh = (int)((uintptr_t)q & 3);
-    acc = sh ? (*reinterpret_cast<const uint32_t *>(q - sh) & ((1u << (8 * sh)) - 1)) : 0;
-  }
-  __device__ __forceinline__ void put(uint8_t b) {
-    uintptr_t a = (uintptr_t)p;
-    int sh = (int)(a & 3);
-    if (sh == 0) acc = 0;
-    acc |= (uint32_t)b << (8 * sh);
-    if (sh == 3) *reinterpret_cast<uint32_t *>(p - 3) = acc;
-    p++;
-  }
-  __device__ __forceinline__ void put16(uint16_t v) { put(v >> 8); put(v & 0xff); }
-  __device__ __forceinline__ void put32(uint32_t v) { put(v >> 24); put((v >> 16) & 0xff); put((v >> 8) & 0xff); put(v & 0xff); }
-  // finish: the output ends where the payload starts; merge payload bytes
-  __device__ __forceinline__ void finish(const Frame &F, int pay_start) {
-    uintptr_t a = (uintptr_t)p;
-    int sh = (int)(a & 3);
-    if (sh == 0) return;
-    for (int k = sh, f = pay_start; k < 4; k++, f++) {
-      uint8_t b = f < F.len ? F.b(f) : p[k - sh];
-      acc |= (uint32_t)b << (8 * k);
-    }
-    *reinterpret_cast<uint32_t *>(p - sh) = acc;
-  }
-};
-
-// recorded extension header e: size and normalised bytes (Headers::deparse)
-__device__ __forceinline__ int ext_len(const Frame &F, const Hdr &H, int e) {
-  int eo = H.ext_off[e];
-  return H.ext_kind[e] == HK_EXT_RAW ? ((int)F.b(eo + 1) + 1) * 8
-       : H.ext_kind[e] == HK_EXT_FRAG ? 8 : ((int)F.b(eo + 1) + 2) * 4;
-}
-__device__ __forceinline__ int ext_bytes(const Frame &F, const Hdr &H) {
-  int t = 0;
-#pragma unroll
-  for (int e = 0; e < 3; e++) if (e < H.next) t += ext_len(F, H, e);
-  return t;
-}
-__device__ __forceinline__ uint8_t ext_byte(const Frame &F, const Hdr &H, int e, int eo, int i) {
-  uint8_t b = F.b(eo + i);
-  if (H.ext_kind[e] == HK_EXT_FRAG && i == 1) b = 0;
-  if (H.ext_kind[e] == HK_EXT_FRAG && i == 3) b &= 0xf9;
-  if (H.ext_kind[e] == HK_EXT_AUTH && (i == 2 || i == 3)) b = 0;
-  return b;
-}
-
-// The recorded extension headers are contiguous in the source and in the
-// output.  When the parse-limit quirk dropped headers behind them, their
-// output position d0 lies after their source; bytes beyond the LDS window
-// are read from the very buffer being rewritten, so before anything else is
-// written the block is moved back to front (memmove order) and the forward
-// writer re-reads the moved bytes.  Returns the bytes moved (0: not moved;
-// the sizes must be taken before the move, which may overwrite them).
-__device__ __forceinline__ int move_exts(const Frame &F, const Hdr &H, int d0) {
-  if (!H.next || d0 <= H.ext_off[0]) return 0;
-  const int eo0 = H.ext_off[0];
-  const int tot = ext_bytes(F, H);
-#pragma unroll
-  for (int e = 2; e >= 0; e--) {
-    if (e >= H.next) continue;
-    int eo = H.ext_off[e], d = d0 + (eo - eo0);
-    for (int i = ext_len(F, H, e) - 1; i >= 0; i--) F.g[d + i] = ext_byte(F, H, e, eo, i);
-  }
-  return tot;
-}
-__device__ __forceinline__ int ext_out_off(const Hdr &H) {  // within the emitted stack
-  return 14 + 4 * H.nvlan + (H.net == 4 ? H.net_hlen : 40);
-}
-
-// emit the inner header stack H (with current field values) via the writer
-__device__ __forceinline__ void emit_stack(OW &w, const Frame &F, const Hdr &H, const State &S, bool v4ck_given,
-                           uint16_t v4ck, bool l4ck_given, uint16_t l4ck, int moved) {
-  for (int i = 0; i < 6; i++) w.put(mac_b(S.edst, i));
-  for (int i = 0; i < 6; i++) w.put(mac_b(S.esrc, i));
-  w.put(F.b(H.hb + 12)); w.put(F.b(H.hb + 13));
-  for (int i = 0; i < 4 * H.nvlan; i++) w.put(F.b(H.hb + 14 + i));
-  if (!H.net) return;
-  int o = H.net_off;
-  if (H.net == 4) {
-    w.put(F.b(o)); w.put(F.b(o + 1)); w.put(F.b(o + 2)); w.put(F.b(o + 3));
-    w.put(F.b(o + 4)); w.put(F.b(o + 5)); w.put(F.b(o + 6) & 0x7f); w.put(F.b(o + 7));
-    w.put(S.ttl); w.put(F.b(o + 9));
-    if (v4ck_given) w.put16(v4ck); else { w.put(F.b(o + 10)); w.put(F.b(o + 11)); }
-    w.put32(S.v4src); w.put32(S.v4dst);
-    for (int i = 20; i < H.net_hlen; i++) w.put(F.b(o + i));
-  } else {
-    for (int i = 0; i < 7; i++) w.put(F.b(o + i));
-    w.put(S.ttl);
-    for (int i = 8; i < 40; i++) w.put(F.b(o + i));
-  }
-  if (H.next) {
-    if (moved) {
-      const int d0 = (int)(w.p - F.g);
-      for (int i = 0; i < moved; i++) w.put(F.g[d0 + i]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 3; e++) {
-        if (e >= H.next) break;
-        int eo = H.ext_off[e];
-        int n = ext_len(F, H, e);
-        for (int i = 0; i < n; i++) w.put(ext_byte(F, H, e, eo, i));
-      }
-    }
-  }
-  if (!H.l4) return;
-  int l = H.l4_off;
-  if (H.l4 == L4_TCP || H.l4 == L4_UDP) {
-    w.put16(S.sport); w.put16(S.dport);
-    if (H.l4 == L4_UDP) {
-      w.put(F.b(l + 4)); w.put(F.b(l + 5));
-      if (l4ck_given) w.put16(l4ck); else { w.put(F.b(l + 6)); w.put(F.b(l + 7)); }
-    } else {
-      for (int i = 4; i < 12; i++) w.put(F.b(l + i));
-      w.put(F.b(l + 12) & 0xf1); w.put(F.b(l + 13)); w.put(F.b(l + 14)); w.put(F.b(l + 15));
-      if (l4ck_given) w.put16(l4ck); else { w.put(F.b(l + 16)); w.put(F.b(l + 17)); }
-      for (int i = 18; i < H.l4_hlen; i++) w.put(F.b(l + i));
-    }
-  } else {
-    w.put(F.b(l)); w.put(F.b(l + 1));
-    if (l4ck_given) w.put16(l4ck); else { w.put(F.b(l + 2)); w.put(F.b(l + 3)); }
-    for (int i = 4; i < H.l4_hlen; i++) w.put(F.b(l + i));
-  }
-  if (H.vx) {
-    w.put(0x08); w.put(0); w.put(0); w.put(0);
-    w.put((H.vni >> 16) & 0xff); w.put((H.vni >> 8) & 0xff); w.put(H.vni & 0xff); w.put(0);
-  }
-}
-
-// Packet::serialize.  Returns the frame-relative output start.
 // Patch the header stack in place (layout unchanged): exactly the bytes
 // Headers::deparse would change -- rewritten fields, normalised reserved bits.
 __device__ __forceinline__ void patch_stack(const Frame &F, const Hdr &H, const State &S, uint16_t v4ck,
@@ -1489,6 +1365,14 @@ __device__ __forceinline__ void write_outer(uint8_t *p, const State &S) {
   }
 }
 
+// Move the recorded header stack [H.hb, H.hb + H.size) sh > 0 bytes later
+// (back to front: the source is read before any byte of it is overwritten;
+// bytes inside the LDS window come from the unmodified LDS copy).
+__device__ __forceinline__ void move_stack(const Frame &F, const Hdr &H, int sh) {
+#pragma unroll 1
+  for (int i = H.size - 1; i >= 0; i--) st8(F.g + H.hb + sh + i, F.b(H.hb + i));
+}
+
 // Packet::serialize.  Returns the frame-relative output start.
 __device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S) {
   const int inner_start = S.pay_start - H.size;
@@ -1508,30 +1392,23 @@ __device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S)
     l4ck = l4 ? l4_csum(F, H, S) : 0;
   }
   if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
-  if (inner_start == H.hb) {
-    // the stack keeps its place: patch it (and prepend the outer headers)
+  const int sh = inner_start - H.hb;  // > 0 when the parse-limit quirk dropped headers
+  if (sh == 0) {
     patch_stack(F, H, S, v4ck, l4, l4ck);
-    if (S.encap) write_outer(F.g + start, S);
-    return start;
+  } else {
+    // relocate the kept stack to end at the payload, then patch it there
+    // through a view whose offsets are shifted by sh (LDS reads still map
+    // to the original window bytes)
+    move_stack(F, H, sh);
+    Frame F2 = F;
+    F2.shift = F.shift - sh;
+    Hdr H2 = H;
+    H2.hb += sh; H2.net_off += sh; H2.l4_off += sh; H2.vx_off += sh;
+#pragma unroll
+    for (int e = 0; e < 3; e++) H2.ext_off[e] += sh;
+    patch_stack(F2, H2, S, v4ck, l4, l4ck);
   }
-  // the parse-limit quirk shrank the stack: re-emit it (after the outer headers)
-  const int moved = move_exts(F, H, start + outer + ext_out_off(H));
-  OW w;
-  w.begin(F.g + start);
-  if (S.encap) {
-    uint32_t c4 = 0;
-    if (S.o_fam == 4) {
-      uint64_t s = 0x4500u | S.o_tos;
-      s += (uint16_t)(20 + S.o_len); s += 0x4000; s += (64u << 8) | 17;
-      s += (S.o_src.w[0] >> 16) + (S.o_src.w[0] & 0xffff) + (S.o_dst.w[0] >> 16) + (S.o_dst.w[0] & 0xffff);
-      c4 = (uint16_t)~fold(s);
-    }
-    const int nw = S.o_fam == 4 ? 25 : 35;
-#pragma unroll 1
-    for (int i = 0; i < nw; i++) w.put16((uint16_t)outer_word(S, i, c4));
-  }
-  emit_stack(w, F, H, S, H.net == 4, v4ck, l4, l4ck, moved);
-  w.finish(F, S.pay_start);
+  if (S.encap) write_outer(F.g + start, S);
   return start;
 }
 
@@ -1633,29 +1510,29 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
 // ---------------------------------------------------------------------------
 // Kernel
 // ---------------------------------------------------------------------------
-#ifdef DP_WAVES
+// occupancy target: the compiler keeps VGPRs within 512 / DP_WAVES
 #define DP_OCC __attribute__((amdgpu_waves_per_eu(DP_WAVES, DP_WAVES)))
-#else
-#define DP_OCC
-#endif
 __global__ void __launch_bounds__(TPB) DP_OCC
 dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__restrict__ buf,
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
                    dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ stats) {
-  __shared__ __attribute__((aligned(16))) uint8_t slab_all[TPB * SLAB];
-  __shared__ uint8_t hash_all[TPB * 64];
-  __shared__ uint32_t hist[DP_DONE_COUNT + 1];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_all[TPB * (SLAB + HS)];
+  uint8_t *slab_all = lds_all;
+  uint8_t *hash_all = lds_all + TPB * SLAB;
   const int tid = threadIdx.x;
-  if (tid < DP_DONE_COUNT + 1) hist[tid] = 0;
   const uint32_t i = blockIdx.x * TPB + tid;
   uint8_t done_code = DONE_NONE;
   if (i < n) {
     Img g{img_base, im};
     const dp_pkt_in_t pin = in[i];
     dp_pkt_out_t o;
-    done_code = process_packet(g, (lds_u8 *)(slab_all + tid * SLAB), (lds_u8 *)(hash_all + tid * 64), buf, buf_bytes, pin, o);
+    done_code = process_packet(g, (lds_u8 *)(slab_all + tid * SLAB), (lds_u8 *)(hash_all + tid * HS), buf, buf_bytes, pin, o);
     out[i] = o;
   }
+  // DoneReason histogram in the (now free) slab memory, one atomic per reason
+  __syncthreads();
+  uint32_t *hist = reinterpret_cast<uint32_t *>(lds_all);
+  if (tid < DP_DONE_COUNT + 1) hist[tid] = 0;
   __syncthreads();
   if (i < n && done_code < DP_DONE_COUNT) atomicAdd(&hist[done_code], 1u);
   __syncthreads();

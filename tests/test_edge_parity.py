@@ -29,6 +29,29 @@ def test_edge_emu_matches_oracle(tables, seed):
     compare(o_ref, b_ref, o_dut, b_dut, inp, f"edge seed {seed}")
 
 
+@pytest.mark.parametrize("seed", [5, 6])
+def test_edge_small_window_matches_oracle(tables, seed):
+    """A 32-byte LDS header window: every header byte past it is read from
+    (and relocated within) the burst buffer."""
+    _, tp = tables
+    buf, inp = pack_burst(edge_frames(4000, seed))
+    b_ref, b_dut = buf.copy(), buf.copy()
+    o_ref = Oracle(tp).process(b_ref, inp, A.PKT_OUT)
+    o_dut = pyemu.process(tp, b_dut, inp, A.PKT_OUT, variant="w32")
+    compare(o_ref, b_ref, o_dut, b_dut, inp, f"edge w32 seed {seed}")
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5])
+def test_workload_small_window_matches_oracle(cfg):
+    from dataplane_amd.workload import Workload
+    w = Workload(cfg, 2000, seed=900 + cfg, n_routes_v4=2000, n_routes_v6=1000, n_acl=200,
+                 n_nat=32, tcp_percent=30)
+    b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
+    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+    o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT, variant="w32")
+    compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} w32")
+
+
 def test_edge_corpus_coverage(tables):
     """The corpus must reach (almost) every DoneReason the path can produce."""
     _, tp = tables
