@@ -38,6 +38,17 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def measured_traffic(cfg: int, n: int):
+    """HBM traffic per launch from the committed PMC passes (profiles/traffic.json,
+    written from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench),
+    scaled to this launch's packet count; None when no measurement exists."""
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))[f"C{cfg}"]
+    except (OSError, KeyError, ValueError):
+        return None, None
+    return int(t["bytes_per_pkt"] * n), t["source"]
+
+
 def cpu_baseline(w: Workload, sample: int, budget_s: float) -> dict:
     """The CPU oracle (C++ restatement of the reference pipeline) on this
     host's cores, DPDK-sized bursts of 64, on a bounded sample."""
@@ -156,10 +167,14 @@ def main() -> None:
     result = None
     if rank == 0:
         achieved = n * ALGO_BYTES[cfg] / (kernel_ms / 1e3) / 1e9
+        traffic, traffic_src = measured_traffic(cfg, n)
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                     "kernel": "dp_pipeline_kernel", "kernel_ms": round(kernel_ms, 4),
                     "bytes_per_pkt": ALGO_BYTES[cfg]}
+        if traffic is not None:
+            roofline["traffic_unit"] = "bytes per launch"
+            roofline["traffic_source"] = traffic_src
         result = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mpps", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
