@@ -90,6 +90,9 @@ def main() -> None:
     ap.add_argument("--routes-v6", type=int, default=0)
     ap.add_argument("--acl", type=int, default=0)
     ap.add_argument("--nat", type=int, default=0)
+    ap.add_argument("--layout", choices=["dpdk", "packed"], default="dpdk",
+                    help="burst buffer layout: DPDK mbuf data (128 B headroom, 64-byte aligned "
+                         "frames) or packed (96 B headroom, 16-byte aligned)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -108,7 +111,7 @@ def main() -> None:
     cfg = args.config
     t0 = time.perf_counter()
     w = Workload(cfg, args.packets, seed=shard_seed(args.seed, rank), n_routes_v4=args.routes_v4,
-                 n_routes_v6=args.routes_v6, n_acl=args.acl, n_nat=args.nat)
+                 n_routes_v6=args.routes_v6, n_acl=args.acl, n_nat=args.nat, layout=args.layout)
     log(rank, f"[bench] workload C{cfg}: {w.n} packets, built in {time.perf_counter() - t0:.1f}s")
     nf = GpuPathNf(local)
     t0 = time.perf_counter()
@@ -182,6 +185,7 @@ def main() -> None:
             "data": "synthetic (seeded, SURVEY.md §8d)",
             "config": {"workload": f"C{cfg}: " + CONFIG_NAMES[cfg], "packets_per_step_per_gpu": n,
                        "frame_bytes_per_step_per_gpu": w.frame_bytes, "seed": args.seed,
+                       "buffer_layout": args.layout,
                        "table_overrides": {k: v for k, v in dict(routes_v4=args.routes_v4,
                                            routes_v6=args.routes_v6, acl=args.acl,
                                            nat=args.nat).items() if v},

@@ -214,7 +214,7 @@ class WorkloadConfig(C.Structure):
     _fields_ = [("config", C.c_uint32), ("n_packets", C.c_uint32), ("seed", C.c_uint64),
                 ("n_routes_v4", C.c_uint32), ("n_routes_v6", C.c_uint32),
                 ("n_acl", C.c_uint32), ("n_nat", C.c_uint32), ("n_vni", C.c_uint32),
-                ("tcp_percent", C.c_uint32), ("pad", C.c_uint32)]
+                ("tcp_percent", C.c_uint32), ("layout", C.c_uint32)]
 
 
 def work_lib() -> C.CDLL:

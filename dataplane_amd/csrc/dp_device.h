@@ -169,13 +169,41 @@ struct FieldIdx {
   uint8_t pad;
 };
 
+// Candidate-list form of a group (mode DPD_GROUP_LIST): one field (`lfield`)
+// is indexed; its elementary interval maps to a run of CandRec -- the
+// group's rules whose `lfield` range covers the interval, in precedence
+// order, stored inline with every field and the rule's actions.  A lookup
+// reads the index, then verifies candidates in order until the first full
+// match: a few cache lines per packet instead of one bit-vector row per
+// field.  The table compiler chooses it when every list is short
+// (dp_tables.cpp build_classifier) and keeps the bit-vector form otherwise.
+// Index leaves (multibit DPD_LEAF entries, or rows[] of the bounds form)
+// hold a packed run: first record << DPD_RUN_BITS | count.
+#define DPD_GROUP_BV 0
+#define DPD_GROUP_LIST 1
+#define DPD_RUN_BITS 6
+#define DPD_RUN_MAX 63
+struct CandRec {       // 64 B, 64-byte aligned: one sector per candidate
+  uint64_t src_hi, src_lo;   // prefix network, key form (v4: hi 0, lo addr)
+  uint64_t dst_hi, dst_lo;
+  uint8_t slen, dlen;        // prefix lengths (v4: of 32, v6: of 128)
+  uint8_t proto_val, proto_mask;
+  uint16_t sp_lo, sp_hi, dp_lo, dp_hi;
+  uint32_t rule;             // global rule index (table's rule arrays)
+  uint32_t action, action2, aux, orig;
+};
+static_assert(sizeof(CandRec) == 64, "CandRec is one 64-byte sector");
+
 struct Group {
   uint32_t n_rules;
   uint32_t words;      // W = ceil(n_rules / 64)
   uint32_t sum_words;  // S = ceil(W / 64)
   uint32_t rule_base;  // index of rule 0 of this group in the table's rule arrays
-  uint64_t pool;       // offset of uint64_t rows[row][S + W]
-  uint64_t proto_rows; // offset of uint16_t[256]
+  uint32_t mode;       // DPD_GROUP_BV / DPD_GROUP_LIST
+  uint32_t lfield;     // LIST: the indexed field (0 src, 1 dst, 2 sport, 3 dport)
+  uint64_t recs;       // LIST: offset of CandRec[]
+  uint64_t pool;       // BV: offset of uint64_t rows[row][S + W]
+  uint64_t proto_rows; // BV: offset of uint16_t[256]
   FieldIdx f[4];
 };
 

@@ -66,6 +66,12 @@ constexpr int WIN = DP_WIN;       // header window bytes per packet (rest read f
 constexpr int SLAB = WIN + 4;     // odd dword stride: conflict-free byte reads
 constexpr int HS = DP_HS;         // hash input scratch (packet_hash_* input <= 59 B)
 constexpr uint8_t DONE_NONE = 255;
+// out-of-line cold paths (the emulator inlines freely)
+#ifdef DP_EMU
+#define DP_COLD
+#else
+#define DP_COLD __attribute__((noinline))
+#endif
 
 // ---------------------------------------------------------------------------
 // Image access
@@ -551,13 +557,53 @@ __device__ __forceinline__ uint32_t bucket_of(const FieldIdx &f, Key128 k) {
   return f.shift == 48 ? (uint32_t)(k.hi >> 48) : (uint32_t)(k.lo >> f.shift) & 0xffff;
 }
 
-// returns global rule index or -1.  The four field searches (elementary
-// interval containing the key) run in lockstep so their loads overlap.
-__device__ __forceinline__ int64_t classify(const Img &g, uint64_t group_recs, int32_t gi,
-                                            uint8_t proto, Key128 src, Key128 dst,
-                                            uint16_t sp, uint16_t dp) {
-  if (gi < 0) return -1;
-  const Group G = g.at<Group>(group_recs)[gi];
+// Elementary interval of one key in one field index -> its leaf value
+// (bit-vector row id, or packed candidate run).
+__device__ __forceinline__ uint32_t field_leaf(const Img &g, const FieldIdx &F, Key128 key) {
+  if (F.root) {
+    uint32_t k = (uint32_t)key.lo;
+    uint32_t e = g.at<uint32_t>(F.root)[k >> (F.kbits - F.s0)];
+#pragma unroll
+    for (int l = 1; l <= 3; l++) {
+      if (!(e & DPD_LEAF)) {
+        int rem = (int)F.kbits - (int)F.s0 - 8 * l;
+        e = g.at<uint32_t>(F.blocks)[(e << 8) | ((k >> rem) & 0xff)];
+      }
+    }
+    return e & ~DPD_LEAF;
+  }
+  uint32_t lo = 0, hi = F.n;
+  if (F.jump) {
+    const uint32_t *jt = g.at<uint32_t>(F.jump);
+    uint32_t t = bucket_of(F, key);
+    lo = jt[t];
+    hi = jt[t + 1] + 1;
+  }
+  const uint64_t *bd = g.at<uint64_t>(F.bounds);
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    uint64_t bh = bd[2 * (uint64_t)mid], bl = bd[2 * (uint64_t)mid + 1];
+    bool le = bh < key.hi || (bh == key.hi && bl <= key.lo);
+    if (le) lo = mid; else hi = mid;
+  }
+  return g.at<uint32_t>(F.rows)[lo];
+}
+
+// key inside the prefix (network a, length len) -- v4 keys use lo only
+__device__ __forceinline__ bool pfx_ok(Key128 k, uint64_t ahi, uint64_t alo, uint32_t len, bool v6) {
+  if (len == 0) return true;
+  if (!v6) return (((uint32_t)k.lo ^ (uint32_t)alo) >> (32 - len)) == 0;
+  if (len <= 64) return ((k.hi ^ ahi) >> (64 - len)) == 0;
+  if (k.hi != ahi) return false;
+  return len == 128 ? k.lo == alo : ((k.lo ^ alo) >> (128 - len)) == 0;
+}
+
+// Bit-vector group: global rule index of the first match, or -1.  Kept out
+// of line: its lockstep state is large and the candidate-list form is the
+// common one.
+__device__ DP_COLD int64_t classify_bv(const Img &g, const Group *Gp, uint8_t proto, Key128 src,
+                                       Key128 dst, uint16_t sp, uint16_t dp) {
+  const Group G = *Gp;
   Key128 key[4] = {src, dst, Key128{0, sp}, Key128{0, dp}};
   uint32_t lo[4], hi[4], e[4];
   // level 0 of every field: multibit root entry, or the jump-table range
@@ -616,17 +662,75 @@ __device__ __forceinline__ int64_t classify(const Img &g, uint64_t group_recs, i
   const uint64_t *p0 = pool + (uint64_t)r0 * stride, *p1 = pool + (uint64_t)r1 * stride;
   const uint64_t *p2 = pool + (uint64_t)r2 * stride, *p3 = pool + (uint64_t)r3 * stride;
   const uint64_t *p4 = pool + (uint64_t)r4 * stride;
-  for (uint32_t s = 0; s < G.sum_words; s++) {
+  int64_t ri = -1;
+  for (uint32_t s = 0; s < G.sum_words && ri < 0; s++) {
     uint64_t m = p0[s] & p1[s] & p2[s] & p3[s] & p4[s];
     while (m) {
       uint32_t w = s * 64 + (uint32_t)__ffsll((unsigned long long)m) - 1;
       uint32_t o = G.sum_words + w;
       uint64_t x = p0[o] & p1[o] & p2[o] & p3[o] & p4[o];
-      if (x) return (int64_t)G.rule_base + (int64_t)w * 64 + (__ffsll((unsigned long long)x) - 1);
+      if (x) { ri = (int64_t)G.rule_base + (int64_t)w * 64 + (__ffsll((unsigned long long)x) - 1); break; }
       m &= m - 1;
     }
   }
-  return -1;
+  return ri;
+}
+
+// Classification result: global rule index (-1: no match) and the rule's
+// action words (inline in the candidate record, else from the arrays).
+struct Hit {
+  int64_t rule;
+  uint32_t action, action2, aux, orig;
+};
+struct ClsArrays { uint64_t group_recs, action, action2, aux, orig; };
+#define CLS_ARRAYS(arr, t) ClsArrays{CLS(arr, t, group_recs), CLS(arr, t, action), CLS(arr, t, action2), CLS(arr, t, aux), CLS(arr, t, orig)}
+enum { W_ACTION = 1, W_ACTION2 = 2, W_AUX = 4, W_ORIG = 8 };
+
+// First match of (proto, src, dst, sport, dport) in group gi.
+//  - candidate-list groups: index of one field -> verify the inline
+//    candidates in precedence order;
+//  - bit-vector groups: the four field searches (elementary interval
+//    containing the key) run in lockstep so their loads overlap, then the
+//    rows are ANDed behind the summary level; first set bit wins.
+template <int WANT>
+__device__ __forceinline__ Hit classify(const Img &g, const ClsArrays &A, int32_t gi, bool v6,
+                                        uint8_t proto, Key128 src, Key128 dst, uint16_t sp, uint16_t dp) {
+  Hit h{-1, 0, 0, 0, 0};
+  if (gi < 0) return h;
+  const Group *Gp = g.at<Group>(A.group_recs) + gi;
+  if (Gp->mode == DPD_GROUP_LIST) {
+    const uint32_t f = Gp->lfield;
+    const FieldIdx F = Gp->f[f];
+    Key128 k = f == 0 ? src : f == 1 ? dst : Key128{0, f == 2 ? sp : dp};
+    const uint32_t run = field_leaf(g, F, k);
+    // a record is four 16-byte words: src, dst, (lens, proto, ports, rule),
+    // (action, action2, aux, orig)
+    const uint4 *R = g.at<uint4>(Gp->recs) + 4 * (uint64_t)(run >> DPD_RUN_BITS);
+    const uint32_t cnt = run & DPD_RUN_MAX;
+    for (uint32_t c = 0; c < cnt; c++) {
+      const uint4 w2 = R[4 * c + 2];
+      const uint32_t slen = w2.x & 0xff, dlen = (w2.x >> 8) & 0xff;
+      const uint32_t pval = (w2.x >> 16) & 0xff, pmask = w2.x >> 24;
+      if ((proto & pmask) != (pval & pmask)) continue;
+      if (sp < (w2.y & 0xffff) || sp > (w2.y >> 16) || dp < (w2.z & 0xffff) || dp > (w2.z >> 16)) continue;
+      const uint4 w0 = R[4 * c], w1 = R[4 * c + 1];
+      const uint64_t shi = ((uint64_t)w0.y << 32) | w0.x, slo = ((uint64_t)w0.w << 32) | w0.z;
+      const uint64_t dhi = ((uint64_t)w1.y << 32) | w1.x, dlo = ((uint64_t)w1.w << 32) | w1.z;
+      if (!pfx_ok(src, shi, slo, slen, v6) || !pfx_ok(dst, dhi, dlo, dlen, v6)) continue;
+      const uint4 w3 = R[4 * c + 3];
+      h.rule = w2.w; h.action = w3.x; h.action2 = w3.y; h.aux = w3.z; h.orig = w3.w;
+      return h;
+    }
+    return h;
+  }
+  const int64_t ri = classify_bv(g, Gp, proto, src, dst, sp, dp);
+  if (ri < 0) return h;
+  h.rule = ri;
+  if (WANT & W_ACTION) h.action = g.at<uint32_t>(A.action)[ri];
+  if (WANT & W_ACTION2) h.action2 = g.at<uint32_t>(A.action2)[ri];
+  if (WANT & W_AUX) h.aux = g.at<uint32_t>(A.aux)[ri];
+  if (WANT & W_ORIG) h.orig = g.at<uint32_t>(A.orig)[ri];
+  return h;
 }
 
 // ---------------------------------------------------------------------------
@@ -1097,15 +1201,16 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   int t = H.net == 4 ? 0 : 1;
   Key128 src = key_of(F, H, S, true), dst = key_of(F, H, S, false);
   const int32_t rg = g.at<VniRec>(g.im.vni_recs)[S.vni_idx].ffr[t];
-  int64_t ri = classify(g, CLS(ff_remote, t, group_recs), rg, proto, Key128{0, 0}, dst, 0, S.dport);
-  if (ri < 0) { done(S, DP_DONE_FILTERED); return; }
-  uint32_t dvni = g.at<uint32_t>(CLS(ff_remote, t, action))[ri];
-  uint32_t dnat = g.at<uint32_t>(CLS(ff_remote, t, action2))[ri];
-  int32_t pi = (int32_t)g.at<uint32_t>(CLS(ff_remote, t, aux))[ri];
+  const Hit rh = classify<W_ACTION | W_ACTION2 | W_AUX>(g, CLS_ARRAYS(ff_remote, t), rg, t, proto,
+                                                       Key128{0, 0}, dst, 0, S.dport);
+  if (rh.rule < 0) { done(S, DP_DONE_FILTERED); return; }
+  uint32_t dvni = rh.action;
+  uint32_t dnat = rh.action2;
+  int32_t pi = (int32_t)rh.aux;
   int32_t lg = g.at<PairRec>(g.im.pair_recs)[pi].ffl[t];
-  int64_t li = classify(g, CLS(ff_local, t, group_recs), lg, proto, src, Key128{0, 0}, S.sport, 0);
-  if (li < 0) { done(S, DP_DONE_FILTERED); return; }
-  uint32_t snat = g.at<uint32_t>(CLS(ff_local, t, action))[li];
+  const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, proto, src, Key128{0, 0}, S.sport, 0);
+  if (lh.rule < 0) { done(S, DP_DONE_FILTERED); return; }
+  uint32_t snat = lh.action;
   S.dst_vni = dvni;
   S.pair = pi;
   if (snat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
@@ -1120,12 +1225,12 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
   int t = H.net == 4 ? 0 : 1;
   const int32_t pi = pair_of(g, S);
   const int32_t ag = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].acl[t] : -1;
-  int64_t ri = classify(g, CLS(acl, t, group_recs), ag, proto, key_of(F, H, S, true),
-                        key_of(F, H, S, false), S.sport, S.dport);
+  const Hit ah = classify<W_ACTION | W_ORIG>(g, CLS_ARRAYS(acl, t), ag, t, proto, key_of(F, H, S, true),
+                                             key_of(F, H, S, false), S.sport, S.dport);
   uint32_t action;
-  if (ri >= 0) {
-    action = g.at<uint32_t>(CLS(acl, t, action))[ri];
-    S.acl_rule = g.at<uint32_t>(CLS(acl, t, orig))[ri];
+  if (ah.rule >= 0) {
+    action = ah.action;
+    S.acl_rule = ah.orig;
     S.acl = action == DP_ACL_DENY ? 2 : 1;
   } else {
     uint32_t v = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].acl_def : 0;

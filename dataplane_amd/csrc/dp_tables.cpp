@@ -16,8 +16,12 @@
 #include "dp_tables.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <cstddef>
 #include <functional>
+#include <map>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -34,8 +38,8 @@ struct ImgBuf {
     b.resize(o + (n ? n : align), 0);
     return o;
   }
-  template <class T> uint64_t put(const std::vector<T> &v) {
-    uint64_t o = alloc(sizeof(T) * v.size(), alignof(T) < 16 ? 16 : alignof(T));
+  template <class T> uint64_t put(const std::vector<T> &v, uint64_t align = 16) {
+    uint64_t o = alloc(sizeof(T) * v.size(), alignof(T) > align ? alignof(T) : align);
     if (!v.empty()) memcpy(b.data() + o, v.data(), sizeof(T) * v.size());
     return o;
   }
@@ -222,8 +226,90 @@ Iv prefix_iv(const dp_prefix_t &p, int fam) {
 
 // `gkv_out`: group keys -> group index; `order_out`: rules in global rule
 // index order (the order of the action arrays).
+// Elementary-interval index of one field: multibit table (v4 addresses,
+// ports; > 16 intervals) or sorted bounds (+ 16-bit jump table).  `leaf[k]`
+// (< 2^31) is the value of interval k: a bit-vector row id, or a packed
+// candidate run (DPD_GROUP_LIST).
+void build_field_index(ImgBuf &ib, FieldIdx &F, int f, int fam, size_t ngroups,
+                       const std::vector<u128> &bnd, const std::vector<uint32_t> &leaf) {
+  const size_t m = bnd.size();
+  F.n = (uint32_t)m;
+  F.jump = 0;
+  if ((f >= 2 || fam == 4) && m > 16) {
+    // multibit table over the interval partition (v4 address: 16-8-8,
+    // port: 8-8; 8-8-8-8 for addresses when the table has many groups)
+    const int kbits = f >= 2 ? 16 : 32;
+    const int s0 = f >= 2 ? 8 : (ngroups > 128 ? 8 : 16);
+    auto ivl = [&](uint64_t x) -> size_t {
+      return (size_t)(std::upper_bound(bnd.begin(), bnd.end(), (u128)x) - bnd.begin()) - 1;
+    };
+    std::vector<uint32_t> blocks;
+    std::function<uint32_t(uint64_t, int)> node = [&](uint64_t lo, int bits) -> uint32_t {
+      size_t i0 = ivl(lo), i1 = ivl(lo + ((1ull << bits) - 1));
+      if (i0 == i1) return DPD_LEAF | leaf[i0];
+      uint32_t ch[256];
+      for (uint32_t c = 0; c < 256; c++) ch[c] = node(lo + ((uint64_t)c << (bits - 8)), bits - 8);
+      uint32_t bi = (uint32_t)(blocks.size() / 256);
+      blocks.insert(blocks.end(), ch, ch + 256);
+      return bi;
+    };
+    std::vector<uint32_t> root((size_t)1 << s0);
+    for (uint64_t b = 0; b < root.size(); b++) root[b] = node(b << (kbits - s0), kbits - s0);
+    F.root = ib.put(root);
+    if (blocks.empty()) blocks.push_back(0);
+    F.blocks = ib.put(blocks);
+    F.s0 = (uint8_t)s0;
+    F.kbits = (uint8_t)kbits;
+    return;
+  }
+  std::vector<uint64_t> bounds;
+  for (size_t k = 0; k < m; k++) {
+    bounds.push_back((uint64_t)(bnd[k] >> 64));
+    bounds.push_back((uint64_t)bnd[k]);
+  }
+  F.bounds = ib.put(bounds);
+  F.rows = ib.put(leaf);
+  // bucket = top 16 bits of the key: v4 address >> 16, port itself,
+  // v6 address hi64 >> 48
+  F.shift = f >= 2 ? 0 : (fam == 4 ? 16 : 48);
+  if (m > 16) {
+    std::vector<uint32_t> jump(65537);
+    size_t j = 0;
+    for (uint32_t b = 0; b < 65536; b++) {
+      u128 start = f >= 2 ? (u128)b : (fam == 4 ? ((u128)b << 16) : ((u128)b << 112));
+      while (j + 1 < m && bnd[j + 1] <= start) j++;
+      jump[b] = (uint32_t)j;
+    }
+    jump[65536] = (uint32_t)(m - 1);
+    F.jump = ib.put(jump);
+  }
+}
+
+// Candidate-list limits: a group takes the list form when, for its best
+// field, no interval has more than kListMax candidates and the mean list
+// (over intervals) is at most kListMean; otherwise the bit-vector form.
+constexpr uint32_t kListMax = 24;
+constexpr double kListMean = 6.0;
+
+// Test knob: DPGPU_CLS_FORM=bv forces the bit-vector form, =list takes the
+// list form whenever the runs fit (<= DPD_RUN_MAX); unset/auto: limits above.
+// forms chosen by the most recent build on this thread (test introspection)
+thread_local uint32_t g_forms[2];
+
+int cls_form_override() {
+  const char *e = getenv("DPGPU_CLS_FORM");
+  if (!e) return 0;
+  if (!strcmp(e, "bv")) return 1;
+  if (!strcmp(e, "list")) return 2;
+  return 0;
+}
+
+// `gkv_out`: group keys -> group index; `order_out`: rules in global rule
+// index order (the order of the action arrays); `aux_patch`: image offsets
+// of CandRec::aux fields with their rule (filled in once PairRecs exist).
 Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam,
-                            std::vector<KV> *gkv_out, std::vector<const dp_rule_t *> *order_out) {
+                            std::vector<KV> *gkv_out, std::vector<const dp_rule_t *> *order_out,
+                            std::vector<std::pair<uint64_t, const dp_rule_t *>> *aux_patch = nullptr) {
   Classifier C{};
   // groups in first-appearance order, rules keep their match order
   std::vector<std::vector<uint32_t>> groups;
@@ -246,6 +332,8 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
   }
   std::vector<uint32_t> action, action2, orig;
   std::vector<Group> grecs;
+  std::vector<CandRec> recs;
+  std::vector<std::pair<size_t, const dp_rule_t *>> rec_rule;  // record index -> rule (aux patch)
   for (auto &gr : groups) {
     Group G{};
     uint32_t n = (uint32_t)gr.size();
@@ -259,6 +347,99 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
       action2.push_back(rules[ri].r.action2);
       orig.push_back(rules[ri].orig);
     }
+    // elementary intervals of the four fields, with the rules starting /
+    // ending at each bound
+    std::vector<u128> bnd[4];
+    std::vector<std::vector<uint32_t>> adds[4], dels[4];
+    uint32_t lmax[4];
+    double lmean[4];
+    for (int f = 0; f < 4; f++) {
+      u128 maxv = f >= 2 ? (u128)65535 : (fam == 4 ? (u128)0xffffffffu : ~(u128)0);
+      std::vector<Iv> iv(n);
+      for (uint32_t j = 0; j < n; j++) {
+        const dp_rule_t &r = rules[gr[j]].r;
+        if (f == 0) iv[j] = prefix_iv(r.src, fam);
+        else if (f == 1) iv[j] = prefix_iv(r.dst, fam);
+        else if (f == 2) iv[j] = Iv{r.sport_lo, r.sport_hi};
+        else iv[j] = Iv{r.dport_lo, r.dport_hi};
+      }
+      std::vector<u128> &b = bnd[f];
+      b.push_back(0);
+      for (auto &x : iv) {
+        if (x.lo > x.hi) continue;  // empty range: never matches
+        b.push_back(x.lo);
+        if (x.hi < maxv) b.push_back(x.hi + 1);
+      }
+      std::sort(b.begin(), b.end());
+      b.erase(std::unique(b.begin(), b.end()), b.end());
+      size_t m = b.size();
+      adds[f].assign(m + 1, {});
+      dels[f].assign(m + 1, {});
+      for (uint32_t j = 0; j < n; j++) {
+        if (iv[j].lo > iv[j].hi) continue;
+        size_t s = std::lower_bound(b.begin(), b.end(), iv[j].lo) - b.begin();
+        size_t e = iv[j].hi < maxv ? (size_t)(std::lower_bound(b.begin(), b.end(), iv[j].hi + 1) - b.begin()) : m;
+        adds[f][s].push_back(j);
+        dels[f][e].push_back(j);
+      }
+      int64_t cnt = 0;
+      uint64_t tot = 0;
+      lmax[f] = 0;
+      for (size_t k = 0; k < m; k++) {
+        cnt += (int64_t)adds[f][k].size() - (int64_t)dels[f][k].size();
+        lmax[f] = std::max(lmax[f], (uint32_t)cnt);
+        tot += (uint64_t)cnt;
+      }
+      lmean[f] = (double)tot / (double)m;
+    }
+    int lf = -1;
+    const int form = cls_form_override();
+    for (int f = 0; f < 4 && form != 1; f++) {
+      if (form == 2 ? lmax[f] > DPD_RUN_MAX : (lmax[f] > kListMax || lmean[f] > kListMean)) continue;
+      if (lf < 0 || lmax[f] < lmax[lf] || (lmax[f] == lmax[lf] && lmean[f] < lmean[lf])) lf = f;
+    }
+    if (lf >= 0) {
+      // candidate-list form: per interval of field lf, the covering rules in
+      // precedence order, stored inline (identical lists shared)
+      G.mode = DPD_GROUP_LIST;
+      G.lfield = (uint32_t)lf;
+      std::map<std::vector<uint32_t>, uint32_t> runs;
+      std::vector<uint32_t> leaf;
+      std::set<uint32_t> cur;
+      for (size_t k = 0; k < bnd[lf].size(); k++) {
+        for (uint32_t j : dels[lf][k]) cur.erase(j);
+        for (uint32_t j : adds[lf][k]) cur.insert(j);
+        std::vector<uint32_t> lst(cur.begin(), cur.end());
+        auto it = runs.find(lst);
+        if (it == runs.end()) {
+          uint32_t first = (uint32_t)recs.size();
+          for (uint32_t j : lst) {
+            const dp_rule_t &r = rules[gr[j]].r;
+            Iv si = prefix_iv(r.src, fam), di = prefix_iv(r.dst, fam);
+            CandRec c{};
+            c.src_hi = (uint64_t)(si.lo >> 64); c.src_lo = (uint64_t)si.lo;
+            c.dst_hi = (uint64_t)(di.lo >> 64); c.dst_lo = (uint64_t)di.lo;
+            c.slen = r.src.len; c.dlen = r.dst.len;
+            c.proto_val = r.proto_val; c.proto_mask = r.proto_mask;
+            c.sp_lo = r.sport_lo; c.sp_hi = r.sport_hi;
+            c.dp_lo = r.dport_lo; c.dp_hi = r.dport_hi;
+            c.rule = G.rule_base + j;
+            c.action = r.action; c.action2 = r.action2;
+            c.orig = rules[gr[j]].orig;
+            rec_rule.push_back({recs.size(), &r});
+            recs.push_back(c);
+          }
+          if (recs.size() >= (1u << (31 - DPD_RUN_BITS))) return Classifier{};  // unreachable sizes
+          it = runs.emplace(lst, (first << DPD_RUN_BITS) | (uint32_t)lst.size()).first;
+        }
+        leaf.push_back(it->second);
+      }
+      build_field_index(ib, G.f[lf], lf, fam, groups.size(), bnd[lf], leaf);
+      grecs.push_back(G);
+      g_forms[1]++;
+      continue;
+    }
+    G.mode = DPD_GROUP_BV;
     uint32_t W = G.words, S = G.sum_words;
     std::vector<uint64_t> pool;
     std::unordered_map<std::string, uint32_t> rowid;
@@ -287,95 +468,26 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
       }
       prow[p] = (uint16_t)add_row(bv);
     }
-    // four interval fields
+    // four interval fields: bit-vector row per elementary interval
     for (int f = 0; f < 4; f++) {
-      u128 maxv = f >= 2 ? (u128)65535 : (fam == 4 ? (u128)0xffffffffu : ~(u128)0);
-      std::vector<Iv> iv(n);
-      for (uint32_t j = 0; j < n; j++) {
-        const dp_rule_t &r = rules[gr[j]].r;
-        if (f == 0) iv[j] = prefix_iv(r.src, fam);
-        else if (f == 1) iv[j] = prefix_iv(r.dst, fam);
-        else if (f == 2) iv[j] = Iv{r.sport_lo, r.sport_hi};
-        else iv[j] = Iv{r.dport_lo, r.dport_hi};
-      }
-      std::vector<u128> bnd;
-      bnd.push_back(0);
-      for (auto &x : iv) {
-        if (x.lo > x.hi) continue;  // empty range: never matches
-        bnd.push_back(x.lo);
-        if (x.hi < maxv) bnd.push_back(x.hi + 1);
-      }
-      std::sort(bnd.begin(), bnd.end());
-      bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
-      size_t m = bnd.size();
-      std::vector<std::vector<uint32_t>> adds(m + 1), dels(m + 1);
-      for (uint32_t j = 0; j < n; j++) {
-        if (iv[j].lo > iv[j].hi) continue;
-        size_t s = std::lower_bound(bnd.begin(), bnd.end(), iv[j].lo) - bnd.begin();
-        size_t e = iv[j].hi < maxv ? (size_t)(std::lower_bound(bnd.begin(), bnd.end(), iv[j].hi + 1) - bnd.begin()) : m;
-        adds[s].push_back(j);
-        dels[e].push_back(j);
-      }
       std::vector<uint64_t> cur(W, 0);
-      std::vector<uint64_t> bounds;
       std::vector<uint32_t> rows;
-      for (size_t k = 0; k < m; k++) {
-        for (uint32_t j : dels[k]) cur[j >> 6] &= ~(1ull << (j & 63));
-        for (uint32_t j : adds[k]) cur[j >> 6] |= 1ull << (j & 63);
-        bounds.push_back((uint64_t)(bnd[k] >> 64));
-        bounds.push_back((uint64_t)bnd[k]);
+      for (size_t k = 0; k < bnd[f].size(); k++) {
+        for (uint32_t j : dels[f][k]) cur[j >> 6] &= ~(1ull << (j & 63));
+        for (uint32_t j : adds[f][k]) cur[j >> 6] |= 1ull << (j & 63);
         rows.push_back(add_row(cur));
       }
-      G.f[f].n = (uint32_t)m;
-      G.f[f].jump = 0;
-      if ((f >= 2 || fam == 4) && m > 16) {
-        // multibit table over the interval partition (v4 address: 16-8-8,
-        // port: 8-8; 8-8-8-8 for addresses when the table has many groups)
-        const int kbits = f >= 2 ? 16 : 32;
-        const int s0 = f >= 2 ? 8 : (groups.size() > 128 ? 8 : 16);
-        auto ivl = [&](uint64_t x) -> size_t {
-          return (size_t)(std::upper_bound(bnd.begin(), bnd.end(), (u128)x) - bnd.begin()) - 1;
-        };
-        std::vector<uint32_t> blocks;
-        std::function<uint32_t(uint64_t, int)> node = [&](uint64_t lo, int bits) -> uint32_t {
-          size_t i0 = ivl(lo), i1 = ivl(lo + ((1ull << bits) - 1));
-          if (i0 == i1) return DPD_LEAF | rows[i0];
-          uint32_t ch[256];
-          for (uint32_t c = 0; c < 256; c++) ch[c] = node(lo + ((uint64_t)c << (bits - 8)), bits - 8);
-          uint32_t bi = (uint32_t)(blocks.size() / 256);
-          blocks.insert(blocks.end(), ch, ch + 256);
-          return bi;
-        };
-        std::vector<uint32_t> root((size_t)1 << s0);
-        for (uint64_t b = 0; b < root.size(); b++) root[b] = node(b << (kbits - s0), kbits - s0);
-        G.f[f].root = ib.put(root);
-        if (blocks.empty()) blocks.push_back(0);
-        G.f[f].blocks = ib.put(blocks);
-        G.f[f].s0 = (uint8_t)s0;
-        G.f[f].kbits = (uint8_t)kbits;
-        continue;
-      }
-      G.f[f].bounds = ib.put(bounds);
-      G.f[f].rows = ib.put(rows);
-      // bucket = top 16 bits of the key: v4 address >> 16, port itself,
-      // v6 address hi64 >> 48
-      G.f[f].shift = f >= 2 ? 0 : (fam == 4 ? 16 : 48);
-      if (m > 16) {
-        std::vector<uint32_t> jump(65537);
-        size_t j = 0;
-        for (uint32_t b = 0; b < 65536; b++) {
-          u128 start = f >= 2 ? (u128)b : (fam == 4 ? ((u128)b << 16) : ((u128)b << 112));
-          while (j + 1 < m && bnd[j + 1] <= start) j++;
-          jump[b] = (uint32_t)j;
-        }
-        jump[65536] = (uint32_t)(m - 1);
-        G.f[f].jump = ib.put(jump);
-      }
+      build_field_index(ib, G.f[f], f, fam, groups.size(), bnd[f], rows);
     }
     G.proto_rows = ib.put(prow);
     G.pool = ib.put(pool);
     grecs.push_back(G);
+    g_forms[0]++;
   }
+  uint64_t recs_off = ib.put(recs, 64);
+  for (auto &G : grecs) G.recs = recs_off;
+  if (aux_patch)
+    for (auto &rr : rec_rule) aux_patch->push_back({recs_off + rr.first * sizeof(CandRec) + offsetof(CandRec, aux), rr.second});
   C.groups = build_hash(ib, gkv);
   if (gkv_out) *gkv_out = gkv;
   C.group_recs = ib.put(grecs);
@@ -413,6 +525,7 @@ int load_rules(const dp_rule_t *rs, uint32_t n, int fam, bool by_prio, int kind,
 }  // namespace
 
 int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
+  g_forms[0] = g_forms[1] = 0;
   if (!d || d->abi_version != DPGPU_ABI_VERSION) return DP_EINVAL;
   ImgBuf ib;
   ib.alloc(64);  // offset 0 is never a valid structure
@@ -644,10 +757,13 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
   std::vector<KV> gkv[6];
   std::vector<std::vector<CRule>> keep(6);
   std::vector<const dp_rule_t *> ffr_order[2];
+  std::vector<std::pair<uint64_t, const dp_rule_t *>> ffr_aux[2];
   for (int ti = 0; ti < 6; ti++) {
     auto &t = tabs[ti];
     if ((rc = load_rules(t.r, t.n, t.fam, t.prio, t.kind, keep[ti]))) return rc;
-    *t.dst = build_classifier(ib, keep[ti], t.fam, &gkv[ti], ti == 2 || ti == 3 ? &ffr_order[ti - 2] : nullptr);
+    bool ffr = ti == 2 || ti == 3;
+    *t.dst = build_classifier(ib, keep[ti], t.fam, &gkv[ti], ffr ? &ffr_order[ti - 2] : nullptr,
+                              ffr ? &ffr_aux[ti - 2] : nullptr);
   }
   auto gkey = [](uint32_t a, uint32_t b, uint32_t c) {
     return ((unsigned __int128)a << 64) | ((unsigned __int128)b << 32) | c;
@@ -861,6 +977,10 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     std::vector<uint32_t> aux;
     for (const dp_rule_t *r : ffr_order[t]) aux.push_back(pair_of(r->vni_a, r->action));
     im.ff_remote[t].aux = ib.put(aux);
+    for (auto &pa : ffr_aux[t]) {
+      uint32_t v = pair_of(pa.second->vni_a, pa.second->action);
+      memcpy(ib.b.data() + pa.first, &v, 4);
+    }
   }
   for (int ti : {0, 1, 4, 5})
     for (auto &e : gkv[ti]) if (e.k2 == 0) pair_of(e.k0, e.k1);
@@ -882,3 +1002,10 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
 }
 
 }  // namespace dpd
+
+// Test introspection: classifier groups built in bit-vector ([0]) and
+// candidate-list ([1]) form by the last image build on the calling thread.
+extern "C" void dpd_debug_classifier_forms(uint32_t out[2]) {
+  out[0] = dpd::g_forms[0];
+  out[1] = dpd::g_forms[1];
+}

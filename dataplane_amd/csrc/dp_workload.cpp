@@ -93,7 +93,9 @@ typedef struct dpw_config {
   uint32_t n_nat;         // /24 maps per direction
   uint32_t n_vni;         // source VPCs
   uint32_t tcp_percent;   // share of TCP among L4 (default 0: UDP only)
-  uint32_t pad;
+  uint32_t layout;        // 0: packed (DP_HEADROOM in front, 16-byte aligned slots);
+                          // 1: DPDK mbuf (RTE_PKTMBUF_HEADROOM = 128 in front of a
+                          //    64-byte aligned data start, slots 64-byte aligned)
 } dpw_config_t;
 
 struct dpw_workload {
@@ -442,11 +444,12 @@ int dpw_build(const dpw_config_t *c, dpw_workload_t **out) {
   }
   uint64_t off = 0;
   std::vector<uint32_t> offs(n);
+  const uint64_t hr = c->layout == 1 ? 128 : DP_HEADROOM, al = c->layout == 1 ? 64 : 16;
   for (uint32_t i = 0; i < n; i++) {
-    off += DP_HEADROOM;
+    off += hr;
     offs[i] = (uint32_t)off;
     off += flen[i];
-    off = (off + 15) & ~15ull;  // next slot 16-byte aligned
+    off = (off + al - 1) & ~(al - 1);  // next slot aligned
   }
   w.buf.assign(off + 64, 0);
   std::vector<uint32_t> acl_hit_pool;

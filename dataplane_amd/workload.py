@@ -28,11 +28,15 @@ CONFIG_NAMES = {
 class Workload:
     def __init__(self, config: int, n_packets: int, seed: int = 1, n_routes_v4: int = 0,
                  n_routes_v6: int = 0, n_acl: int = 0, n_nat: int = 0, n_vni: int = 0,
-                 tcp_percent: int = 0):
+                 tcp_percent: int = 0, layout: str = "packed"):
+        """layout "packed": DP_HEADROOM (96 B, the reference test buffer) in
+        front of 16-byte aligned frames; "dpdk": DPDK mbuf data layout,
+        RTE_PKTMBUF_HEADROOM (128 B) in front of 64-byte aligned frames."""
         self._lib = A.work_lib()
         cfg = A.WorkloadConfig(config=config, n_packets=n_packets, seed=seed,
                                n_routes_v4=n_routes_v4, n_routes_v6=n_routes_v6, n_acl=n_acl,
-                               n_nat=n_nat, n_vni=n_vni, tcp_percent=tcp_percent)
+                               n_nat=n_nat, n_vni=n_vni, tcp_percent=tcp_percent,
+                               layout={"packed": 0, "dpdk": 1}[layout])
         h = C.c_void_p()
         A.check(self._lib.dpw_build(C.byref(cfg), C.byref(h)), "dpw_build")
         self._h = h

@@ -32,3 +32,11 @@ def process(tables_ptr, buf: np.ndarray, inp: np.ndarray, out_dtype, variant: st
     if rc != 0:
         raise RuntimeError(f"emu rejected tables rc={rc}")
     return out
+
+
+def classifier_forms(variant: str = ""):
+    """(bit-vector groups, candidate-list groups) of the last image build on
+    this thread (dp_tables.cpp dpd_debug_classifier_forms)."""
+    out = (C.c_uint32 * 2)()
+    lib(variant).dpd_debug_classifier_forms(out)
+    return int(out[0]), int(out[1])

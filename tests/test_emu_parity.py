@@ -1,5 +1,6 @@
 """CPU: the GPU kernel's per-packet code, compiled for the host (tests/emu),
-against the oracle on seeded workloads of every config shape."""
+against the oracle on seeded workloads of every config shape, with the
+classifiers built in each form (bit-vector, candidate list, automatic)."""
 import pytest
 
 from dataplane_amd import _abi as A
@@ -10,11 +11,19 @@ import pyemu
 from helpers import compare
 
 
+@pytest.mark.parametrize("form", ["auto", "bv", "list"])
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
-def test_emu_matches_oracle(cfg):
+def test_emu_matches_oracle(cfg, form, monkeypatch):
+    monkeypatch.setenv("DPGPU_CLS_FORM", form)
     w = Workload(cfg, 3000, seed=100 + cfg, n_routes_v4=3000, n_routes_v6=1500, n_acl=400,
                  n_nat=48, tcp_percent=25)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
     o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
     o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT)
-    compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg}")
+    bv, lst = pyemu.classifier_forms()
+    if cfg != 1:  # C1 has no overlay tables
+        if form == "bv":
+            assert lst == 0 and bv > 0
+        elif form == "list":
+            assert lst > 0
+    compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} {form}")

@@ -24,8 +24,11 @@ def nf():
     n.close()
 
 
+@pytest.mark.parametrize("form", ["auto", "bv", "list"])
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
-def test_gpu_matches_oracle(nf, cfg):
+def test_gpu_matches_oracle(nf, cfg, form, monkeypatch):
+    """Classifiers built in each form (DPGPU_CLS_FORM, read at publish)."""
+    monkeypatch.setenv("DPGPU_CLS_FORM", form)
     w = Workload(cfg, 20000, seed=200 + cfg, n_routes_v4=20000, n_routes_v6=8000, n_acl=1000,
                  n_nat=64, tcp_percent=25)
     nf.publish(w.tables)
@@ -46,8 +49,10 @@ def edge():
 
 
 @pytest.mark.parametrize("seed", [11, 12, 13, 14, 15, 16])
-def test_gpu_edge_corpus(nf, edge, seed):
-    """Malformed / boundary frames and every table branch (tests/edgecase.py)."""
+def test_gpu_edge_corpus(nf, edge, seed, monkeypatch):
+    """Malformed / boundary frames and every table branch (tests/edgecase.py);
+    odd seeds with bit-vector classifiers, even seeds with candidate lists."""
+    monkeypatch.setenv("DPGPU_CLS_FORM", "bv" if seed % 2 else "list")
     _, tp = edge
     nf.publish(tp)
     buf, inp = pack_burst(edge_frames(20000, seed))
