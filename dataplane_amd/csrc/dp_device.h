@@ -30,6 +30,8 @@
 #endif
 
 #define DPD_MAX_INSTR 4
+// partial DoneReason histograms per context (kernel atomics spread over slots)
+#define DPD_STAT_SLOTS 256
 
 namespace dpd {
 

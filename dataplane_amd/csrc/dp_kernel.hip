@@ -60,7 +60,7 @@ __device__ unsigned long long g_stage_cycles[16];
 #define DP_HS 60
 #endif
 #ifndef DP_WAVES
-#define DP_WAVES 4
+#define DP_WAVES 3
 #endif
 constexpr int WIN = DP_WIN;       // header window bytes per packet (rest read from HBM)
 constexpr int SLAB = WIN + 4;     // odd dword stride: conflict-free byte reads
@@ -335,6 +335,19 @@ __device__ __forceinline__ bool parse(const Frame &F, int hb, Hdr &H) {
 // ---------------------------------------------------------------------------
 struct Addr16 { uint32_t w[4]; };  // network order bytes packed big-endian per word
 
+// VXLAN outer header values (IpForwarder::build_vxlan_headers)
+struct OuterHdr {
+  uint8_t fam, tos;      // outer IP family; dscp<<2|ecn
+  uint16_t sport, len;   // UDP source port; UDP length
+  uint32_t vni;
+  Addr16 src, dst;
+};
+// 16-bit words of Eth + outer IP + UDP + VXLAN
+__device__ __forceinline__ int outer_words(int fam) { return fam == 4 ? 25 : 35; }
+__device__ __forceinline__ uint32_t outer_ck4(const OuterHdr &S);
+__device__ __forceinline__ void hput16(LDS_AS uint8_t *o, int i, uint32_t v) { o[i] = (uint8_t)(v >> 8); o[i + 1] = (uint8_t)v; }
+__device__ __forceinline__ void hput32(LDS_AS uint8_t *o, int i, uint32_t v) { hput16(o, i, v >> 16); hput16(o, i + 2, v); }
+
 struct State {
   uint8_t done;
   uint32_t flags;
@@ -360,13 +373,9 @@ struct State {
   uint16_t sport, dport;
   // encap
   bool encap;
-  uint8_t o_fam;
-  Addr16 o_src, o_dst;
-  uint32_t o_vni;
-  uint16_t o_sport, o_len;
-  uint8_t o_tos;         // dscp<<2|ecn for the outer header
-  bool inner_l4_ck;      // inner L4 checksum recomputed at encap
-  uint16_t inner_v4_ck, inner_l4_ck_val;
+  uint8_t o_fam;         // outer IP family; the outer IP/UDP/VXLAN headers are
+                         // deparsed at encap into the lane's LDS scratch (F.hs)
+  bool inner_l4_ck;      // encap: the inner L4 checksum is recomputed
   bool o_eth;            // Egress added the outer Ethernet header
   uint64_t odst, osrc;   // outer Ethernet (encap)
   int pay_start;         // frame-relative payload start (inner after decap)
@@ -406,7 +415,16 @@ __device__ __forceinline__ Addr16 addr16(const Frame &F, int off) {
 
 // current destination address (after NAT) as a 16-byte key
 __device__ __forceinline__ void cur_dst(const Frame &F, const Hdr &H, const State &S, uint8_t &fam, Addr16 &a) {
-  if (S.encap) { fam = S.o_fam; a = S.o_dst; return; }
+  if (S.encap) {  // the outer destination, from the deparsed outer IP header
+    fam = S.o_fam;
+    const int o = S.o_fam == 4 ? 16 : 24;
+    for (int i = 0; i < 4; i++)
+      a.w[i] = (S.o_fam == 6 || i == 0)
+                   ? ((uint32_t)F.hs[o + 4 * i] << 24) | ((uint32_t)F.hs[o + 4 * i + 1] << 16) |
+                         ((uint32_t)F.hs[o + 4 * i + 2] << 8) | F.hs[o + 4 * i + 3]
+                   : 0u;
+    return;
+  }
   fam = (uint8_t)H.net;
   if (H.net == 4) { a.w[0] = S.v4dst; a.w[1] = a.w[2] = a.w[3] = 0; }
   else a = addr16(F, H.net_off + 24);
@@ -1055,13 +1073,13 @@ __device__ __forceinline__ void vxlan_encap(const Img &g, const Frame &F, const 
   if (dz == 0) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); S.eth_dirty = true; return; }
   S.edst = load_mac(in.mac);
   S.eth_dirty = true;
+  // inner checksums (IpForwarder::vxlan_encap): the IPv4 header checksum
+  // always, the full L4 checksum if REFR_CHKSUM; computed at serialize from
+  // the same (then unchanged) inner fields
   if (S.flags & DP_META_REFR_CHKSUM) {
-    if (H.net == 4) S.inner_v4_ck = ipv4_csum(F, H, S);
     S.inner_l4_ck = (H.l4 != L4_NONE) && !H.vx;
-    if (S.inner_l4_ck) S.inner_l4_ck_val = l4_csum(F, H, S);
     S.flags &= ~DP_META_REFR_CHKSUM;
   } else if (H.net == 4) {
-    S.inner_v4_ck = ipv4_csum(F, H, S);
     S.inner_l4_ck = false;
   } else {
     done(S, DP_DONE_INTERNAL_FAILURE);  // unreachable!() in the reference
@@ -1079,11 +1097,12 @@ __device__ __forceinline__ void vxlan_encap(const Img &g, const Frame &F, const 
     done(S, DP_DONE_VXLAN_ENCAP_FAILURE);
     return;
   }
+  OuterHdr ob;
   for (int i = 0; i < 4; i++) {
-    S.o_src.w[i] = ((uint32_t)fb.vtep_ip[4 * i] << 24) | ((uint32_t)fb.vtep_ip[4 * i + 1] << 16) | ((uint32_t)fb.vtep_ip[4 * i + 2] << 8) | fb.vtep_ip[4 * i + 3];
-    S.o_dst.w[i] = ((uint32_t)in.addr[4 * i] << 24) | ((uint32_t)in.addr[4 * i + 1] << 16) | ((uint32_t)in.addr[4 * i + 2] << 8) | in.addr[4 * i + 3];
+    ob.src.w[i] = ((uint32_t)fb.vtep_ip[4 * i] << 24) | ((uint32_t)fb.vtep_ip[4 * i + 1] << 16) | ((uint32_t)fb.vtep_ip[4 * i + 2] << 8) | fb.vtep_ip[4 * i + 3];
+    ob.dst.w[i] = ((uint32_t)in.addr[4 * i] << 24) | ((uint32_t)in.addr[4 * i + 1] << 16) | ((uint32_t)in.addr[4 * i + 2] << 8) | in.addr[4 * i + 3];
   }
-  if (S.o_fam == 4) { S.o_src.w[1] = S.o_src.w[2] = S.o_src.w[3] = 0; S.o_dst.w[1] = S.o_dst.w[2] = S.o_dst.w[3] = 0; }
+  if (S.o_fam == 4) { ob.src.w[1] = ob.src.w[2] = ob.src.w[3] = 0; ob.dst.w[1] = ob.dst.w[2] = ob.dst.w[3] = 0; }
   // headroom check of the prepend (Packet::vxlan_encap): inner headers go
   // right before the payload; we only fail if they would not fit at all.
   int inner_start = S.pay_start - H.size;
@@ -1099,10 +1118,39 @@ __device__ __forceinline__ void vxlan_encap(const Img &g, const Frame &F, const 
   }
   hash_ip_fields(F, H, S, hbuf);
   uint64_t x = rapid(hbuf.b, hbuf.n);
-  S.o_sport = (uint16_t)(x % 16384 + 49152);
-  S.o_len = (uint16_t)((F.len - S.pay_start) + H.size + 16);
-  S.o_tos = S.has_dscp ? (uint8_t)((S.dscp << 2) | S.ecn) : 0;
-  S.o_vni = in.vni;
+  ob.sport = (uint16_t)(x % 16384 + 49152);
+  ob.len = (uint16_t)((F.len - S.pay_start) + H.size + 16);
+  ob.tos = S.has_dscp ? (uint8_t)((S.dscp << 2) | S.ecn) : 0;
+  ob.vni = in.vni;
+  ob.fam = S.o_fam;
+  // deparse the outer IP/UDP/VXLAN now, over the dead hash input: none of it
+  // stays live in registers until serialize (Egress adds the outer Ethernet)
+  lds_u8 *o = F.hs;
+  int u;  // UDP header offset
+  if (ob.fam == 4) {
+    hput16(o, 0, 0x4500u | ob.tos);
+    hput16(o, 2, 20u + ob.len);
+    hput16(o, 4, 0);
+    hput16(o, 6, 0x4000u);                 // Ipv4Header::default(): DF
+    hput16(o, 8, (64u << 8) | 17u);
+    hput16(o, 10, outer_ck4(ob));
+    hput32(o, 12, ob.src.w[0]);
+    hput32(o, 16, ob.dst.w[0]);
+    u = 20;
+  } else {
+    hput32(o, 0, (0x60000000u | ((uint32_t)ob.tos << 20)));
+    hput16(o, 4, ob.len);
+    hput16(o, 6, (17u << 8) | 64u);
+#pragma unroll
+    for (int k = 0; k < 4; k++) { hput32(o, 8 + 4 * k, ob.src.w[k]); hput32(o, 24 + 4 * k, ob.dst.w[k]); }
+    u = 40;
+  }
+  hput16(o, u, ob.sport);
+  hput16(o, u + 2, 4789u);
+  hput16(o, u + 4, ob.len);
+  hput16(o, u + 6, 0);                     // outer UDP checksum 0
+  hput32(o, u + 8, 0x08000000u);           // VXLAN flags: I
+  hput32(o, u + 12, ob.vni << 8);
   S.encap = true;
   S.dst_vni = in.vni;
 }
@@ -1337,183 +1385,148 @@ __device__ __forceinline__ void stage_egress(const Img &g, const Frame &F, const
 // ---------------------------------------------------------------------------
 // Serialize
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void st8(uint8_t *p, uint8_t v) { *p = v; }
-__device__ __forceinline__ void st16be(uint8_t *p, uint16_t v) {
-  if (((uintptr_t)p & 1) == 0) *reinterpret_cast<uint16_t *>(p) = (uint16_t)((v >> 8) | (v << 8));
-  else { p[0] = v >> 8; p[1] = v & 0xff; }
-}
-__device__ __forceinline__ void st32be(uint8_t *p, uint32_t v) {
-  uint32_t s = __builtin_bswap32(v);
-  uintptr_t a = (uintptr_t)p;
-  if ((a & 3) == 0) *reinterpret_cast<uint32_t *>(p) = s;
-  else if ((a & 1) == 0) { *reinterpret_cast<uint16_t *>(p) = (uint16_t)s; *reinterpret_cast<uint16_t *>(p + 2) = (uint16_t)(s >> 16); }
-  else { p[0] = v >> 24; p[1] = (v >> 16) & 0xff; p[2] = (v >> 8) & 0xff; p[3] = v & 0xff; }
-}
-
-// Patch the header stack in place (layout unchanged): exactly the bytes
-// Headers::deparse would change -- rewritten fields, normalised reserved bits.
-__device__ __forceinline__ void patch_stack(const Frame &F, const Hdr &H, const State &S, uint16_t v4ck,
-                                            bool l4, uint16_t l4ck) {
-  uint8_t *q = F.g + H.hb;
-  if (S.eth_dirty) {
-    if (((uintptr_t)q & 1) == 0) {
-      for (int i = 0; i < 6; i += 2) *reinterpret_cast<uint16_t *>(q + i) = (uint16_t)(mac_b(S.edst, i) | (mac_b(S.edst, i + 1) << 8));
-      for (int i = 0; i < 6; i += 2) *reinterpret_cast<uint16_t *>(q + 6 + i) = (uint16_t)(mac_b(S.esrc, i) | (mac_b(S.esrc, i + 1) << 8));
-    } else {
-      for (int i = 0; i < 6; i++) { q[i] = mac_b(S.edst, i); q[6 + i] = mac_b(S.esrc, i); }
-    }
-  }
-  if (H.net == 4) {
-    uint8_t *n = F.g + H.net_off;
-    uint8_t fl = F.b(H.net_off + 6);
-    if (fl & 0x80) st8(n + 6, fl & 0x7f);
-    st8(n + 8, S.ttl);
-    st16be(n + 10, v4ck);
-    st32be(n + 12, S.v4src);
-    st32be(n + 16, S.v4dst);
-  } else if (H.net == 6) {
-    st8(F.g + H.net_off + 7, S.ttl);
-  }
-#pragma unroll
-  for (int e = 0; e < 3; e++) {
-    if (e >= H.next) break;
-    uint8_t *x = F.g + H.ext_off[e];
-    if (H.ext_kind[e] == HK_EXT_FRAG) { st8(x + 1, 0); st8(x + 3, F.b(H.ext_off[e] + 3) & 0xf9); }
-    if (H.ext_kind[e] == HK_EXT_AUTH) { st8(x + 2, 0); st8(x + 3, 0); }
-  }
-  if (H.net && H.l4) {
-    uint8_t *l = F.g + H.l4_off;
-    if (H.l4 == L4_TCP || H.l4 == L4_UDP) { st16be(l, S.sport); st16be(l + 2, S.dport); }
-    if (H.l4 == L4_TCP) { uint8_t x = F.b(H.l4_off + 12); if (x & 0x0e) st8(l + 12, x & 0xf1); }
-    if (l4) {
-      if (H.l4 == L4_UDP) st16be(l + 6, l4ck);
-      else if (H.l4 == L4_TCP) st16be(l + 16, l4ck);
-      else st16be(l + 2, l4ck);
-    }
-    if (H.vx) { uint8_t *v = F.g + H.vx_off; if (F.b(H.vx_off) != 0x08) st8(v, 0x08); }
-  }
-}
-
 // word i of an address without a dynamic register index (keeps it out of scratch)
 __device__ __forceinline__ uint32_t aw(const Addr16 &a, int i) {
   return i == 0 ? a.w[0] : i == 1 ? a.w[1] : i == 2 ? a.w[2] : a.w[3];
 }
 
-// 16-bit word i of the VXLAN outer headers (Eth + IPv4/IPv6 + UDP + VXLAN)
-__device__ __forceinline__ uint32_t outer_word(const State &S, int i, uint32_t ck4) {
-  if (i < 3) return (uint32_t)(S.odst >> (32 - 16 * i)) & 0xffff;
-  if (i < 6) return (uint32_t)(S.osrc >> (32 - 16 * (i - 3))) & 0xffff;
-  if (i == 6) return S.o_fam == 4 ? 0x0800u : 0x86ddu;
-  int j = i - 7;
-  if (S.o_fam == 4) {
-    if (j < 10) {
-      switch (j) {
-        case 0: return 0x4500u | S.o_tos;
-        case 1: return (20u + S.o_len) & 0xffff;
-        case 2: return 0;
-        case 3: return 0x4000u;              // Ipv4Header::default(): DF
-        case 4: return (64u << 8) | 17u;
-        case 5: return ck4;
-        case 6: return S.o_src.w[0] >> 16;
-        case 7: return S.o_src.w[0] & 0xffff;
-        case 8: return S.o_dst.w[0] >> 16;
-        default: return S.o_dst.w[0] & 0xffff;
-      }
-    }
-    j -= 10;
-  } else {
-    if (j < 20) {
-      if (j == 0) return ((0x60u | (S.o_tos >> 4)) << 8) | ((S.o_tos & 0xfu) << 4);
-      if (j == 1) return 0;
-      if (j == 2) return S.o_len;
-      if (j == 3) return (17u << 8) | 64u;
-      int k = j - 4;
-      uint32_t w = k < 8 ? aw(S.o_src, k >> 1) : aw(S.o_dst, (k - 8) >> 1);
-      return (k & 1) ? (w & 0xffff) : (w >> 16);
-    }
-    j -= 20;
-  }
-  switch (j) {
-    case 0: return S.o_sport;
-    case 1: return 4789u;
-    case 2: return S.o_len;
-    case 3: return 0;                        // outer UDP checksum 0
-    case 4: return 0x0800u;                  // VXLAN flags: I
-    case 5: return 0;
-    case 6: return (S.o_vni >> 8) & 0xffff;
-    default: return (S.o_vni & 0xff) << 8;
-  }
+// outer IPv4 header checksum (0 for an IPv6 outer header)
+__device__ __forceinline__ uint32_t outer_ck4(const OuterHdr &S) {
+  if (S.fam != 4) return 0;
+  uint64_t t = 0x4500u | S.tos;
+  t += (uint16_t)(20 + S.len); t += 0x4000; t += (64u << 8) | 17;
+  t += (S.src.w[0] >> 16) + (S.src.w[0] & 0xffff) + (S.dst.w[0] >> 16) + (S.dst.w[0] & 0xffff);
+  return (uint16_t)~fold(t);
 }
 
-// Write the outer headers at p (any alignment), in 4/2/1-byte stores.
-__device__ __forceinline__ void write_outer(uint8_t *p, const State &S) {
-  uint32_t ck4 = 0;
-  if (S.o_fam == 4) {
-    uint64_t s = 0x4500u | S.o_tos;
-    s += (uint16_t)(20 + S.o_len); s += 0x4000; s += (64u << 8) | 17;
-    s += (S.o_src.w[0] >> 16) + (S.o_src.w[0] & 0xffff) + (S.o_dst.w[0] >> 16) + (S.o_dst.w[0] & 0xffff);
-    ck4 = (uint16_t)~fold(s);
-  }
-  const int nw = S.o_fam == 4 ? 25 : 35;
-  const uintptr_t a = (uintptr_t)p;
-  if ((a & 3) == 0) {
-#pragma unroll 1
-    for (int i = 0; i + 1 < nw; i += 2)
-      *reinterpret_cast<uint32_t *>(p + 2 * i) = bswap16(outer_word(S, i, ck4)) | ((uint32_t)bswap16(outer_word(S, i + 1, ck4)) << 16);
-    if (nw & 1) *reinterpret_cast<uint16_t *>(p + 2 * (nw - 1)) = bswap16(outer_word(S, nw - 1, ck4));
-  } else if ((a & 1) == 0) {
-#pragma unroll 1
-    for (int i = 0; i < nw; i++) *reinterpret_cast<uint16_t *>(p + 2 * i) = bswap16(outer_word(S, i, ck4));
-  } else {
-#pragma unroll 1
-    for (int i = 0; i < nw; i++) { uint32_t w = outer_word(S, i, ck4); p[2 * i] = (uint8_t)(w >> 8); p[2 * i + 1] = (uint8_t)w; }
-  }
+// --- serializer ------------------------------------------------------------
+// Frame byte f lives at window position shift + f when 0 <= shift + f < WIN
+// (the LDS copy, written back by flush_window); any other byte is written
+// straight to the burst buffer.  Reads (F.b) see both.
+__device__ __forceinline__ void wput8(const Frame &F, int f, uint32_t v) {
+  const int o = F.shift + f;
+  if ((unsigned)o < (unsigned)WIN) F.lds[o] = (uint8_t)v;
+  else F.g[f] = (uint8_t)v;
+}
+__device__ __forceinline__ void wput16(const Frame &F, int f, uint32_t v) { wput8(F, f, v >> 8); wput8(F, f + 1, v); }
+__device__ __forceinline__ void wput32(const Frame &F, int f, uint32_t v) { wput16(F, f, v >> 16); wput16(F, f + 2, v); }
+__device__ __forceinline__ void wput_mac(const Frame &F, int f, uint64_t m) {
+  wput16(F, f, (uint32_t)(m >> 32)); wput32(F, f + 2, (uint32_t)m);
 }
 
-// Move the recorded header stack [H.hb, H.hb + H.size) sh > 0 bytes later
-// (back to front: the source is read before any byte of it is overwritten;
-// bytes inside the LDS window come from the unmodified LDS copy).
-__device__ __forceinline__ void move_stack(const Frame &F, const Hdr &H, int sh) {
+// Window positions [p, we) of one slab back to the burst buffer (gbase: the
+// 16-aligned address of window position 0; p 16-aligned).
+__device__ __forceinline__ void flush_range(uint8_t *gbase, const lds_u8 *slab, int p, int we) {
+  const lds_u32 *w = reinterpret_cast<const lds_u32 *>(slab);
 #pragma unroll 1
-  for (int i = H.size - 1; i >= 0; i--) st8(F.g + H.hb + sh + i, F.b(H.hb + i));
+  for (; p + 16 <= we; p += 16)
+    *reinterpret_cast<uint4 *>(gbase + p) = make_uint4(w[p >> 2], w[(p >> 2) + 1], w[(p >> 2) + 2], w[(p >> 2) + 3]);
+#pragma unroll 1
+  for (; p + 4 <= we; p += 4) *reinterpret_cast<uint32_t *>(gbase + p) = w[p >> 2];
+#pragma unroll 1
+  for (; p < we; p++) gbase[p] = slab[p];
 }
 
-// Packet::serialize.  Returns the frame-relative output start.
-__device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S) {
-  const int inner_start = S.pay_start - H.size;
+// The frame lies inside the burst buffer behind its headroom (else the
+// packet is InternalFailure and nothing of it is touched).
+__device__ __forceinline__ bool frame_ok(const dp_pkt_in_t &pin, uint64_t buf_bytes) {
+  return pin.off >= DP_HEADROOM && (((uint64_t)pin.off + pin.len + 15) & ~15ull) <= buf_bytes;
+}
+// 16-byte chunks of the header window (the frame's first WIN - shift bytes)
+__device__ __forceinline__ int window_chunks(const dp_pkt_in_t &pin) {
+  const int c = ((int)(pin.off & 15) + pin.len + 15) >> 4;
+  return c < WIN / 16 ? c : WIN / 16;
+}
+
+// Packet::serialize (net/src/packet/mod.rs:342-374): deparse the current
+// header stack in front of the payload (Headers::deparse), with
+// update_checksums (net/src/headers/mod.rs:894-929) -- or, for a VXLAN
+// encapsulation, the inner checksums of IpForwarder::vxlan_encap and the
+// outer Eth/IP/UDP/VXLAN headers.  Fields are patched into the LDS window
+// copy, checksums summed over the patched bytes, and the stack written back
+// in 16-byte chunks.  Returns the frame-relative output start.
+__device__ __forceinline__ int serialize(const Frame &F, const Hdr &H0, State &S, int &fl0, int &fl1) {
+  fl0 = fl1 = 0;
+  const int inner_start = S.pay_start - H0.size;
   const int outer = S.encap ? 14 + (S.o_fam == 4 ? 20 : 40) + 16 : 0;
   const int start = inner_start - outer;
-  // checksums: encap computed the inner ones (IpForwarder::vxlan_encap);
-  // otherwise update_checksums over the current stack
-  bool l4;
-  uint16_t v4ck, l4ck;
-  if (S.encap) {
-    v4ck = S.inner_v4_ck;
-    l4 = S.inner_l4_ck;
-    l4ck = S.inner_l4_ck_val;
-  } else {
-    v4ck = H.net == 4 ? ipv4_csum(F, H, S) : 0;
-    l4 = H.net && H.l4 != L4_NONE && !H.vx;
-    l4ck = l4 ? l4_csum(F, H, S) : 0;
-  }
   if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
-  const int sh = inner_start - H.hb;  // > 0 when the parse-limit quirk dropped headers
-  if (sh == 0) {
-    patch_stack(F, H, S, v4ck, l4, l4ck);
-  } else {
-    // relocate the kept stack to end at the payload, then patch it there
-    // through a view whose offsets are shifted by sh (LDS reads still map
-    // to the original window bytes)
-    move_stack(F, H, sh);
-    Frame F2 = F;
-    F2.shift = F.shift - sh;
-    Hdr H2 = H;
-    H2.hb += sh; H2.net_off += sh; H2.l4_off += sh; H2.vx_off += sh;
+  // the parse-limit quirk consumed headers it did not record: the kept
+  // stack moves sh bytes later to end at the payload (back to front)
+  const int sh = inner_start - H0.hb;
+  Hdr H = H0;
+  if (sh) {
+#pragma unroll 1
+    for (int i = H0.size - 1; i >= 0; i--) wput8(F, H0.hb + sh + i, F.b(H0.hb + i));
+    H.hb += sh; H.net_off += sh; H.l4_off += sh; H.vx_off += sh;
 #pragma unroll
-    for (int e = 0; e < 3; e++) H2.ext_off[e] += sh;
-    patch_stack(F2, H2, S, v4ck, l4, l4ck);
+    for (int e = 0; e < 3; e++) H.ext_off[e] += sh;
   }
-  if (S.encap) write_outer(F.g + start, S);
+  // deparse: rewritten fields and normalised reserved bits
+  if (S.eth_dirty) { wput_mac(F, H.hb, S.edst); wput_mac(F, H.hb + 6, S.esrc); }
+  if (H.net == 4) {
+    const int n = H.net_off;
+    wput8(F, n + 6, F.b(n + 6) & 0x7f);
+    wput8(F, n + 8, S.ttl);
+    wput16(F, n + 10, 0);
+    wput32(F, n + 12, S.v4src);
+    wput32(F, n + 16, S.v4dst);
+  } else if (H.net == 6) {
+    wput8(F, H.net_off + 7, S.ttl);
+  }
+#pragma unroll
+  for (int e = 0; e < 3; e++) {
+    if (e >= H.next) break;
+    const int x = H.ext_off[e];
+    if (H.ext_kind[e] == HK_EXT_FRAG) { wput8(F, x + 1, 0); wput8(F, x + 3, F.b(x + 3) & 0xf9); }
+    if (H.ext_kind[e] == HK_EXT_AUTH) { wput16(F, x + 2, 0); }
+  }
+  // L4 checksum: recomputed unless VXLAN (outer) or, for an encapsulated
+  // inner stack, REFR_CHKSUM was clear at encap
+  const bool l4 = H.net && H.l4 != L4_NONE && !H.vx && (!S.encap || S.inner_l4_ck);
+  const int l = H.l4_off;
+  int ck_off = -1;
+  if (H.net && H.l4) {
+    if (H.l4 == L4_TCP || H.l4 == L4_UDP) { wput16(F, l, S.sport); wput16(F, l + 2, S.dport); }
+    if (H.l4 == L4_TCP) wput8(F, l + 12, F.b(l + 12) & 0xf1);
+    if (l4) {
+      ck_off = H.l4 == L4_UDP ? l + 6 : H.l4 == L4_TCP ? l + 16 : l + 2;
+      wput16(F, ck_off, 0);
+    }
+    if (H.vx) wput8(F, H.vx_off, 0x08);
+  }
+  if (H.net == 4) wput16(F, H.net_off + 10, (uint16_t)~fold(sum_frame(F, H.net_off, H.net_off + H.net_hlen)));
+  if (ck_off >= 0) {
+    uint64_t t = sum_frame(F, l, F.len);
+    const uint32_t tl = (uint32_t)H.l4_hlen + (uint32_t)(F.len - S.pay_start);
+    if (H.l4 != L4_ICMP4) {  // pseudo header
+      if (H.net == 4) t += (S.v4src >> 16) + (S.v4src & 0xffff) + (S.v4dst >> 16) + (S.v4dst & 0xffff);
+      else t += sum_frame(F, H.net_off + 8, H.net_off + 40);
+      if (H.l4 == L4_UDP) t += 17u + F.be16(l + 4);
+      else t += (tl >> 16) + (tl & 0xffff) + (H.l4 == L4_TCP ? 6u : 58u);
+    }
+    uint16_t c = (uint16_t)~fold(t);
+    if (H.l4 == L4_UDP && c == 0) c = 0xffff;
+    wput16(F, ck_off, c);
+  }
+  if (S.encap) {  // outer Ethernet (Egress), then the outer IP/UDP/VXLAN deparsed at encap
+    wput_mac(F, start, S.odst);
+    wput_mac(F, start + 6, S.osrc);
+    wput16(F, start + 12, S.o_fam == 4 ? 0x0800u : 0x86ddu);
+    const int nb = 2 * (outer_words(S.o_fam) - 7);
+#pragma unroll 1
+    for (int i = 0; i < nb; i++) wput8(F, start + 14 + i, F.hs[i]);
+  }
+  // write-back range: window positions [fl0, fl1) covering [start, end of
+  // the stack), widened to whole 16-byte chunks inside [0, min(frame end,
+  // WIN)) -- this packet's own bytes, rewritten with the values read; bytes
+  // outside the window went straight to the buffer (wput8)
+  int p = F.shift + start;
+  p = (p < 0 ? 0 : p) & ~15;
+  const int lim = F.shift + F.len < WIN ? F.shift + F.len : WIN;
+  int we = (F.shift + H.hb + H.size + 15) & ~15;
+  if (we > lim) we = lim;
+  if (we > p) { fl0 = p; fl1 = we; }
   return start;
 }
 
@@ -1521,8 +1534,9 @@ __device__ __forceinline__ int serialize(const Frame &F, const Hdr &H, State &S)
 // Per-packet body
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, lds_u8 *hs, uint8_t *buf, uint64_t buf_bytes,
-                                  const dp_pkt_in_t &pin, dp_pkt_out_t &o) {
-  if (pin.off < DP_HEADROOM || (((uint64_t)pin.off + pin.len + 15) & ~15ull) > buf_bytes) {
+                                  const dp_pkt_in_t &pin, dp_pkt_out_t &o, int &fl0, int &fl1) {
+  fl0 = fl1 = 0;
+  if (!frame_ok(pin, buf_bytes)) {
     // layout contract violated: never touch memory outside the buffer
     o.off = pin.off; o.len = pin.len; o.done = DP_DONE_INTERNAL_FAILURE; o.acl = 0;
     o.meta_flags = 0; o.oif = 0; o.dst_vni = 0; o.src_vni = 0;
@@ -1536,17 +1550,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   F.g = buf + pin.off;
   F.shift = (int)(pin.off & 15);
   F.len = pin.len;
-  // stage the header window: 16-byte loads, stored as 4 dword LDS writes
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(buf + (pin.off & ~15u));
-    int nchunk = (F.shift + F.len + 15) >> 4;
-    if (nchunk > WIN / 16) nchunk = WIN / 16;
-    lds_u32 *dst = reinterpret_cast<lds_u32 *>(F.lds);
-    for (int c = 0; c < nchunk; c++) {
-      uint4 q = src[c];
-      dst[4 * c] = q.x; dst[4 * c + 1] = q.y; dst[4 * c + 2] = q.z; dst[4 * c + 3] = q.w;
-    }
-  }
+  // the header window is staged in `slab` by the caller (kernel / dpemu_run)
   o.off = pin.off; o.len = pin.len; o.acl = 0; o.oif = 0; o.dst_vni = 0; o.src_vni = 0;
   o.fib_entry = 0xffffffffu; o.acl_rule = 0xffffffffu;
   TS(0);
@@ -1564,7 +1568,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   S.eg_dmac = S.eg_smac = 0; S.fib = -1; S.vni_idx = -1; S.pair = -1;
   S.has_dscp = false; S.dscp = S.ecn = 0;
   S.fib_entry = 0xffffffffu; S.acl_rule = 0xffffffffu; S.acl = 0;
-  S.encap = false; S.o_eth = false; S.inner_l4_ck = false; S.inner_v4_ck = 0; S.inner_l4_ck_val = 0;
+  S.encap = false; S.o_eth = false; S.inner_l4_ck = false;
   S.ttl = 0; S.v4src = S.v4dst = 0;
   load_fields(F, H, S);
   TS(1);
@@ -1587,10 +1591,14 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   TS(6);
   stage_egress(g, F, H, S);
   TS(7);
+#ifdef DP_PROBE_NOSER
+  if (false) {
+#else
   if (S.done == DP_DONE_DELIVERED) {
+#endif
     if (!S.encap && icmp_is_error(F, H)) S.done = DP_DONE_UNHANDLED;
     else {
-      int st = serialize(F, H, S);
+      int st = serialize(F, H, S, fl0, fl1);
       S.flags &= ~DP_META_REFR_CHKSUM;
       if (S.done == DP_DONE_DELIVERED) {
         o.off = (uint32_t)((int)pin.off + st);
@@ -1617,31 +1625,110 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
 // ---------------------------------------------------------------------------
 // occupancy target: the compiler keeps VGPRs within 512 / DP_WAVES
 #define DP_OCC __attribute__((amdgpu_waves_per_eu(DP_WAVES, DP_WAVES)))
+
+// Wave-cooperative header-window staging and write-back.  M = the wave's
+// largest chunk count rounded up to a power of two; in round r lane L moves
+// chunk c of the wave's packet q, (q, c) = divmod(64 r + L, M): neighbouring
+// lanes move neighbouring 16-byte chunks of one frame, so a wave-instruction
+// touches 64 / M frames instead of 64.  Chunk c of packet q is window
+// position 16 c of q's slab and buf + base_q + 16 c.
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ int log2_up(int m) { return m <= 1 ? 0 : m <= 2 ? 1 : m <= 4 ? 2 : 3; }
+
+__device__ __forceinline__ void wave_load_windows(const uint8_t *buf, uint8_t *slab_wave, uint32_t base, int nch) {
+  const int lane = threadIdx.x & 63;
+  const int lg = log2_up(wave_max(nch));
+#pragma unroll 1
+  for (int r = 0; r < (1 << lg); r++) {
+    const int t = 64 * r + lane;
+    const int q = t >> lg, c = t & ((1 << lg) - 1);
+    const uint32_t qb = (uint32_t)__shfl((int)base, q);
+    const int qn = __shfl(nch, q);
+    if (c < qn) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(buf + qb + 16 * c);
+      lds_u32 *d = (lds_u32 *)(slab_wave + q * SLAB + 16 * c);
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_store_windows(uint8_t *buf, const uint8_t *slab_wave, uint32_t base, int c0, int c1) {
+  const int lane = threadIdx.x & 63;
+  const int lg = log2_up(wave_max(c1));
+#pragma unroll 1
+  for (int r = 0; r < (1 << lg); r++) {
+    const int t = 64 * r + lane;
+    const int q = t >> lg, c = t & ((1 << lg) - 1);
+    const uint32_t qb = (uint32_t)__shfl((int)base, q);
+    const int q0 = __shfl(c0, q), q1 = __shfl(c1, q);
+    if (c >= q0 && c < q1) {
+      const lds_u32 *w = (const lds_u32 *)(slab_wave + q * SLAB + 16 * c);
+      *reinterpret_cast<uint4 *>(buf + qb + 16 * c) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(TPB) DP_OCC
 dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__restrict__ buf,
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
-                   dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ stats) {
+                   dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ part) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_all[TPB * (SLAB + HS)];
   uint8_t *slab_all = lds_all;
   uint8_t *hash_all = lds_all + TPB * SLAB;
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  uint8_t *slab_wave = slab_all + (tid - lane) * SLAB;
+  lds_u8 *slab = (lds_u8 *)(slab_all + tid * SLAB);
   const uint32_t i = blockIdx.x * TPB + tid;
+  const bool live = i < n;
+  dp_pkt_in_t pin{};
+  if (live) pin = in[i];
+  const uint32_t base = pin.off & ~15u;
+  const int nch = live && frame_ok(pin, buf_bytes) ? window_chunks(pin) : 0;
+  wave_load_windows(buf, slab_wave, base, nch);
+  __syncthreads();
   uint8_t done_code = DONE_NONE;
-  if (i < n) {
+  int fl0 = 0, fl1 = 0;
+  if (live) {
     Img g{img_base, im};
-    const dp_pkt_in_t pin = in[i];
     dp_pkt_out_t o;
-    done_code = process_packet(g, (lds_u8 *)(slab_all + tid * SLAB), (lds_u8 *)(hash_all + tid * HS), buf, buf_bytes, pin, o);
+    done_code = process_packet(g, slab, (lds_u8 *)(hash_all + tid * HS), buf, buf_bytes, pin, o, fl0, fl1);
     out[i] = o;
   }
-  // DoneReason histogram in the (now free) slab memory, one atomic per reason
   __syncthreads();
-  uint32_t *hist = reinterpret_cast<uint32_t *>(lds_all);
-  if (tid < DP_DONE_COUNT + 1) hist[tid] = 0;
-  __syncthreads();
-  if (i < n && done_code < DP_DONE_COUNT) atomicAdd(&hist[done_code], 1u);
-  __syncthreads();
-  if (stats && tid < DP_DONE_COUNT && hist[tid]) atomicAdd(&stats[tid], (unsigned long long)hist[tid]);
+  // write-back: whole chunks by the wave, a partial tail by its owner
+  wave_store_windows(buf, slab_wave, base, fl0 >> 4, fl1 >> 4);
+  if (fl1 & 15) flush_range(buf + base, slab, fl1 & ~15, fl1);
+  // DoneReason histogram: per wave by ballot, one atomic per reason present
+  // into one of DPD_STAT_SLOTS partial histograms (dp_stats_reduce sums them)
+  if (part) {
+    unsigned long long pending = __ballot(live && done_code < DP_DONE_COUNT);
+    const int slot = (int)((blockIdx.x * (TPB / 64) + (tid >> 6)) & (DPD_STAT_SLOTS - 1));
+    while (pending) {
+      const int leader = __ffsll(pending) - 1;
+      const int r = __shfl((int)done_code, leader);
+      const unsigned long long m = __ballot(live && (int)done_code == r) & pending;
+      if (lane == leader) atomicAdd(&part[slot * DP_DONE_COUNT + r], (unsigned long long)__popcll(m));
+      pending &= ~m;
+    }
+  }
+}
+
+// Sum (and clear) the partial histograms into the caller's DoneReason counts.
+__global__ void __launch_bounds__(64) dp_stats_reduce(unsigned long long *__restrict__ part,
+                                                      unsigned long long *__restrict__ stats) {
+  const int r = threadIdx.x;
+  if (r >= DP_DONE_COUNT) return;
+  unsigned long long s = 0;
+  for (int k = 0; k < DPD_STAT_SLOTS; k++) {
+    s += part[k * DP_DONE_COUNT + r];
+    part[k * DP_DONE_COUNT + r] = 0;
+  }
+  if (s) atomicAdd(&stats[r], s);
 }
 #endif
 
@@ -1654,7 +1741,18 @@ extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uin
   static uint8_t slab[SLAB + 16];
   static uint8_t hs[64];
   Img g{img_base, *reinterpret_cast<const Image *>(image_struct)};
-  for (uint32_t i = 0; i < n; i++) process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i]);
+  for (uint32_t i = 0; i < n; i++) {
+    const int nch = frame_ok(in[i], buf_bytes) ? window_chunks(in[i]) : 0;
+    const uint4 *src = reinterpret_cast<const uint4 *>(buf + (in[i].off & ~15u));
+    for (int c = 0; c < nch; c++) {
+      const uint4 q = src[c];
+      uint32_t *d = reinterpret_cast<uint32_t *>(slab + 16 * c);
+      d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
+    }
+    int fl0, fl1;
+    process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1);
+    if (fl1 > fl0) flush_range(buf + (in[i].off & ~15u), slab, fl0, fl1);
+  }
 }
 #else
 // Launch wrapper used by the runtime (dp_runtime.cpp).
@@ -1670,12 +1768,16 @@ extern "C" int dp_debug_stage_cycles(unsigned long long *out16, int reset) {
 #endif
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
-                                   uint32_t n, uint64_t *stats, hipStream_t stream) {
+                                   uint32_t n, uint64_t *stats, uint64_t *stats_part, hipStream_t stream) {
   if (n == 0) return 0;
   Image im = *reinterpret_cast<const Image *>(image_struct);
   uint32_t blocks = (n + TPB - 1) / TPB;
+  unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
   hipLaunchKernelGGL(dp_pipeline_kernel, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                     buf_bytes, in, out, n, reinterpret_cast<unsigned long long *>(stats));
+                     buf_bytes, in, out, n, part);
+  if (stats)
+    hipLaunchKernelGGL(dp_stats_reduce, dim3(1), dim3(64), 0, stream, part,
+                       reinterpret_cast<unsigned long long *>(stats));
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 #endif

@@ -25,7 +25,7 @@
 
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
-                                   uint32_t n, uint64_t *stats, hipStream_t stream);
+                                   uint32_t n, uint64_t *stats, uint64_t *stats_part, hipStream_t stream);
 
 namespace {
 
@@ -82,6 +82,7 @@ struct dp_ctx {
   dp_pkt_in_t *d_in = nullptr;
   dp_pkt_out_t *d_out = nullptr;
   uint64_t *d_stats = nullptr;
+  uint64_t *d_part = nullptr;        // partial DoneReason histograms (kernel side)
   uint32_t cap_n = 0;
 };
 
@@ -104,6 +105,9 @@ int dp_ctx_create(int device_ordinal, dp_ctx_t **out) {
     return fail(DP_EIO, "hipStreamCreate", e);
   if ((e = hipMalloc(&c->d_stats, sizeof(uint64_t) * DP_DONE_COUNT)) != hipSuccess)
     return fail(DP_ENOMEM, "hipMalloc stats", e);
+  const size_t part_bytes = sizeof(uint64_t) * DP_DONE_COUNT * DPD_STAT_SLOTS;
+  if ((e = hipMalloc(&c->d_part, part_bytes)) != hipSuccess) return fail(DP_ENOMEM, "hipMalloc stats partials", e);
+  if ((e = hipMemset(c->d_part, 0, part_bytes)) != hipSuccess) return fail(DP_EIO, "clear stats partials", e);
   *out = c.release();
   return 0;
 }
@@ -117,6 +121,7 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->d_in) (void)hipFree(c->d_in);
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->d_part) (void)hipFree(c->d_part);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -175,7 +180,7 @@ int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
   auto img = current(c);
   if (!img) return fail(DP_ENOTABLES, "no tables published");
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  int rc = dpk_launch_pipeline(img->dev, &img->im, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, s);
+  int rc = dpk_launch_pipeline(img->dev, &img->im, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, c->d_part, s);
   if (rc) return fail(DP_EIO, "kernel launch failed", hipGetLastError());
   c->pinned = img;
   return 0;

@@ -16,6 +16,7 @@
 #define __launch_bounds__(x)
 #define __shared__
 struct uint4 { uint32_t x, y, z, w; };
+inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
 static inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
 static inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x); }
 static inline uint64_t __umul64hi(uint64_t a, uint64_t b) {
