@@ -216,6 +216,7 @@ struct Classifier {
   uint64_t action2;    // uint32_t[n_rules_total]
   uint64_t orig;       // uint32_t[n_rules_total] (index in the caller's array)
   uint64_t aux;        // uint32_t[n_rules_total]: flow-filter remote -> PairRec index
+  uint64_t recs;       // CandRec[] of the candidate-list groups (shared by all groups)
   uint32_t n_groups;
   uint32_t n_rules;
 };

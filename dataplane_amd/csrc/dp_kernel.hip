@@ -700,8 +700,10 @@ struct Hit {
   int64_t rule;
   uint32_t action, action2, aux, orig;
 };
-struct ClsArrays { uint64_t group_recs, action, action2, aux, orig; };
-#define CLS_ARRAYS(arr, t) ClsArrays{CLS(arr, t, group_recs), CLS(arr, t, action), CLS(arr, t, action2), CLS(arr, t, aux), CLS(arr, t, orig)}
+struct ClsArrays { uint64_t group_recs, action, action2, aux, orig, recs; };
+#define CLS_ARRAYS(arr, t) ClsArrays{CLS(arr, t, group_recs), CLS(arr, t, action), CLS(arr, t, action2), CLS(arr, t, aux), CLS(arr, t, orig), CLS(arr, t, recs)}
+// no hoisted index leaf (see hoist_walks)
+constexpr uint32_t NO_PRE = 0xffffffffu;
 enum { W_ACTION = 1, W_ACTION2 = 2, W_AUX = 4, W_ORIG = 8 };
 
 // First match of (proto, src, dst, sport, dport) in group gi.
@@ -710,20 +712,13 @@ enum { W_ACTION = 1, W_ACTION2 = 2, W_AUX = 4, W_ORIG = 8 };
 //  - bit-vector groups: the four field searches (elementary interval
 //    containing the key) run in lockstep so their loads overlap, then the
 //    rows are ANDed behind the summary level; first set bit wins.
-template <int WANT>
-__device__ __forceinline__ Hit classify(const Img &g, const ClsArrays &A, int32_t gi, bool v6,
-                                        uint8_t proto, Key128 src, Key128 dst, uint16_t sp, uint16_t dp) {
+__device__ __forceinline__ Hit verify_run(const Img &g, uint64_t recs, uint32_t run, bool v6, uint8_t proto,
+                                          Key128 src, Key128 dst, uint16_t sp, uint16_t dp) {
   Hit h{-1, 0, 0, 0, 0};
-  if (gi < 0) return h;
-  const Group *Gp = g.at<Group>(A.group_recs) + gi;
-  if (Gp->mode == DPD_GROUP_LIST) {
-    const uint32_t f = Gp->lfield;
-    const FieldIdx F = Gp->f[f];
-    Key128 k = f == 0 ? src : f == 1 ? dst : Key128{0, f == 2 ? sp : dp};
-    const uint32_t run = field_leaf(g, F, k);
+  {
     // a record is four 16-byte words: src, dst, (lens, proto, ports, rule),
     // (action, action2, aux, orig)
-    const uint4 *R = g.at<uint4>(Gp->recs) + 4 * (uint64_t)(run >> DPD_RUN_BITS);
+    const uint4 *R = g.at<uint4>(recs) + 4 * (uint64_t)(run >> DPD_RUN_BITS);
     const uint32_t cnt = run & DPD_RUN_MAX;
     for (uint32_t c = 0; c < cnt; c++) {
       const uint4 w2 = R[4 * c + 2];
@@ -739,7 +734,24 @@ __device__ __forceinline__ Hit classify(const Img &g, const ClsArrays &A, int32_
       h.rule = w2.w; h.action = w3.x; h.action2 = w3.y; h.aux = w3.z; h.orig = w3.w;
       return h;
     }
-    return h;
+  }
+  return h;
+}
+
+// `pre`: the group's list-index leaf when hoist_walks already walked it.
+template <int WANT>
+__device__ __forceinline__ Hit classify(const Img &g, const ClsArrays &A, int32_t gi, bool v6,
+                                        uint8_t proto, Key128 src, Key128 dst, uint16_t sp, uint16_t dp,
+                                        uint32_t pre = NO_PRE) {
+  Hit h{-1, 0, 0, 0, 0};
+  if (gi < 0) return h;
+  if (pre != NO_PRE) return verify_run(g, A.recs, pre, v6, proto, src, dst, sp, dp);
+  const Group *Gp = g.at<Group>(A.group_recs) + gi;
+  if (Gp->mode == DPD_GROUP_LIST) {
+    const uint32_t f = Gp->lfield;
+    const FieldIdx F = Gp->f[f];
+    Key128 k = f == 0 ? src : f == 1 ? dst : Key128{0, f == 2 ? sp : dp};
+    return verify_run(g, A.recs, field_leaf(g, F, k), v6, proto, src, dst, sp, dp);
   }
   const int64_t ri = classify_bv(g, Gp, proto, src, dst, sp, dp);
   if (ri < 0) return h;
@@ -766,7 +778,7 @@ struct NatQ {
   uint16_t np;
 };
 
-__device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port) {
+__device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port, const uint32_t pre[2]) {
   const NatTab *tabs = g.at<NatTab>(g.im.nat_tab_recs);
   const NatEnt *ents = g.at<NatEnt>(g.im.nat_ents);
   const uint32_t *prs = g.at<uint32_t>(g.im.nat_prs);
@@ -778,7 +790,10 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
   for (int k = 0; k < 2; k++) {
     q[k].ok = false; q[k].hp = false; q[k].na = 0; q[k].np = 0;
     ei[k] = -1; e[k] = DPD_LEAF; lo[k] = 0; hi[k] = 0;
-    if (q[k].ti >= 0) {
+    if (q[k].ti >= 0 && pre[k] != NO_PRE) {
+      e[k] = DPD_LEAF | pre[k];       // multibit walk done by hoist_walks
+      T[k].root = 1; T[k].n = 1;
+    } else if (q[k].ti >= 0) {
       T[k] = tabs[q[k].ti];
       if (T[k].root) e[k] = g.at<uint32_t>(T[k].root)[q[k].addr >> (32 - T[k].s0)];
       else hi[k] = T[k].n;
@@ -1241,7 +1256,72 @@ __device__ __forceinline__ Key128 key_of(const Frame &F, const Hdr &H, const Sta
   return k;
 }
 
-__device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, State &S) {
+// Hoisted index walks.  After the flow-filter remote verdict the next stages
+// -- flow-filter local, ACL, static NAT src and dst -- each start with a
+// multibit index walk that depends only on the VNI pair and the packet's
+// fields.  They run here in lockstep so their dependent loads overlap; the
+// stages continue from the leaves (NO_PRE: not hoisted -- v6, an absent
+// table, a bit-vector group or a bounds-form index; the stage walks itself).
+struct Pre { uint32_t ffl, acl, nsrc, ndst; };
+
+__device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_t pi, int32_t lg, Pre &P) {
+  P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
+  const PairRec PR = g.at<PairRec>(g.im.pair_recs)[pi];
+  const int32_t nat_dst = g.at<VniRec>(g.im.vni_recs)[S.vni_idx].nat_dst;
+  uint64_t root[4], blocks[4];
+  uint32_t key[4], e[4];
+  int rem0[4];
+  bool on[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) { on[k] = false; root[k] = blocks[k] = 0; key[k] = 0; rem0[k] = 0; e[k] = DPD_LEAF; }
+  // 0: flow-filter local (keys: src, -, sport, -); 1: ACL (src, dst, sport, dport)
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int32_t gi = k == 0 ? lg : PR.acl[0];
+    if (gi < 0) continue;
+    const Group *Gp = g.at<Group>(k == 0 ? g.im.ff_local[0].group_recs : g.im.acl[0].group_recs) + gi;
+    if (Gp->mode != DPD_GROUP_LIST) continue;
+    const uint32_t f = Gp->lfield;
+    const FieldIdx &FI = Gp->f[f];
+    const uint64_t r = FI.root;
+    if (!r) continue;
+    on[k] = true;
+    root[k] = r;
+    blocks[k] = FI.blocks;
+    rem0[k] = (int)FI.kbits - (int)FI.s0;
+    key[k] = f == 0 ? S.v4src : f == 1 ? (k == 0 ? 0u : S.v4dst) : f == 2 ? (uint32_t)S.sport : (k == 0 ? 0u : (uint32_t)S.dport);
+  }
+  // 2: NAT src table of the pair, 3: NAT dst table of the source VNI
+#pragma unroll
+  for (int k = 2; k < 4; k++) {
+    const int32_t ti = k == 2 ? PR.nat_src : nat_dst;
+    if (ti < 0) continue;
+    const NatTab &T = g.at<NatTab>(g.im.nat_tab_recs)[ti];
+    const uint64_t r = T.root;
+    if (!r || T.n == 0) continue;
+    on[k] = true;
+    root[k] = r;
+    blocks[k] = T.blocks;
+    rem0[k] = 32 - (int)T.s0;
+    key[k] = k == 2 ? S.v4src : S.v4dst;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (on[k]) e[k] = g.at<uint32_t>(root[k])[key[k] >> rem0[k]];
+#pragma unroll
+  for (int l = 1; l <= 3; l++) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (on[k] && !(e[k] & DPD_LEAF)) e[k] = g.at<uint32_t>(blocks[k])[(e[k] << 8) | ((key[k] >> (rem0[k] - 8 * l)) & 0xff)];
+  }
+  if (on[0]) P.ffl = e[0] & ~DPD_LEAF;
+  if (on[1]) P.acl = e[1] & ~DPD_LEAF;
+  if (on[2]) P.nsrc = e[2] & ~DPD_LEAF;
+  if (on[3]) P.ndst = e[3] & ~DPD_LEAF;
+}
+
+__device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, State &S, Pre &P) {
+  P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY) || S.dst_vni) return;
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
   if (!S.src_vni) { done(S, DP_DONE_UNROUTABLE); return; }
@@ -1256,7 +1336,8 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   uint32_t dnat = rh.action2;
   int32_t pi = (int32_t)rh.aux;
   int32_t lg = g.at<PairRec>(g.im.pair_recs)[pi].ffl[t];
-  const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, proto, src, Key128{0, 0}, S.sport, 0);
+  if (t == 0) hoist_walks(g, S, pi, lg, P);
+  const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, proto, src, Key128{0, 0}, S.sport, 0, P.ffl);
   if (lh.rule < 0) { done(S, DP_DONE_FILTERED); return; }
   uint32_t snat = lh.action;
   S.dst_vni = dvni;
@@ -1265,7 +1346,7 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   if (dnat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_DST;
 }
 
-__device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S) {
+__device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S, const Pre &P) {
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY)) return;
   if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
@@ -1274,7 +1355,7 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
   const int32_t pi = pair_of(g, S);
   const int32_t ag = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].acl[t] : -1;
   const Hit ah = classify<W_ACTION | W_ORIG>(g, CLS_ARRAYS(acl, t), ag, t, proto, key_of(F, H, S, true),
-                                             key_of(F, H, S, false), S.sport, S.dport);
+                                             key_of(F, H, S, false), S.sport, S.dport, t == 0 ? P.acl : NO_PRE);
   uint32_t action;
   if (ah.rule >= 0) {
     action = ah.action;
@@ -1293,7 +1374,7 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
   if (action == DP_ACL_DENY) done(S, DP_DONE_ACL_DROPPED);
 }
 
-__device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, const Hdr &H, State &S) {
+__device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, const Hdr &H, State &S, const Pre &P) {
   if (S.done != DONE_NONE) return;
   if (!(S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST))) return;
   if (S.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) return;
@@ -1310,7 +1391,8 @@ __device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, c
   q[0].addr = S.v4src; q[0].port = has_p ? S.sport : 0;
   q[1].ti = (H.net == 4 && (S.flags & DP_META_REQ_STATIC_NAT_DST)) ? VR.nat_dst : -1;
   q[1].addr = S.v4dst; q[1].port = has_p ? S.dport : 0;
-  nat_find2(g, q, has_p);
+  const uint32_t pre[2] = {P.nsrc, P.ndst};
+  nat_find2(g, q, has_p, pre);
   if (S.flags & DP_META_REQ_STATIC_NAT_SRC) {
     bool mod = false;
     // source mapping: UnicastIpAddr::try_from rejects multicast / broadcast
@@ -1581,11 +1663,12 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   TS(2);
   // IcmpErrorHandler: overlay ICMP errors need flow state (outside the slice)
   if (S.done == DONE_NONE && (S.flags & DP_META_IS_OVERLAY) && icmp_is_error(F, H)) done(S, DP_DONE_UNHANDLED);
-  stage_flow_filter(g, F, H, S);
+  Pre P;
+  stage_flow_filter(g, F, H, S, P);
   TS(3);
-  stage_acl(g, F, H, S);
+  stage_acl(g, F, H, S, P);
   TS(4);
-  stage_static_nat(g, F, H, S);
+  stage_static_nat(g, F, H, S, P);
   TS(5);
   stage_ipforward(g, F, H, S);  // IP-Forward-2
   TS(6);
@@ -1712,23 +1795,29 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__re
       const int leader = __ffsll(pending) - 1;
       const int r = __shfl((int)done_code, leader);
       const unsigned long long m = __ballot(live && (int)done_code == r) & pending;
-      if (lane == leader) atomicAdd(&part[slot * DP_DONE_COUNT + r], (unsigned long long)__popcll(m));
+      if (lane == leader) atomicAdd(&part[r * DPD_STAT_SLOTS + slot], (unsigned long long)__popcll(m));
       pending &= ~m;
     }
   }
 }
 
-// Sum (and clear) the partial histograms into the caller's DoneReason counts.
-__global__ void __launch_bounds__(64) dp_stats_reduce(unsigned long long *__restrict__ part,
-                                                      unsigned long long *__restrict__ stats) {
-  const int r = threadIdx.x;
-  if (r >= DP_DONE_COUNT) return;
-  unsigned long long s = 0;
-  for (int k = 0; k < DPD_STAT_SLOTS; k++) {
-    s += part[k * DP_DONE_COUNT + r];
-    part[k * DP_DONE_COUNT + r] = 0;
+// Sum (and clear) the partial histograms into the caller's DoneReason
+// counts: block r sums reason r's DPD_STAT_SLOTS partials.
+__global__ void __launch_bounds__(DPD_STAT_SLOTS) dp_stats_reduce(unsigned long long *__restrict__ part,
+                                                                  unsigned long long *__restrict__ stats) {
+  __shared__ unsigned long long wsum[DPD_STAT_SLOTS / 64];
+  const int r = blockIdx.x, k = threadIdx.x;
+  unsigned long long v = part[r * DPD_STAT_SLOTS + k];
+  if (v) part[r * DPD_STAT_SLOTS + k] = 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((k & 63) == 0) wsum[k >> 6] = v;
+  __syncthreads();
+  if (k == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < DPD_STAT_SLOTS / 64; w++) t += wsum[w];
+    if (t) atomicAdd(&stats[r], t);
   }
-  if (s) atomicAdd(&stats[r], s);
 }
 #endif
 
@@ -1776,7 +1865,7 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_st
   hipLaunchKernelGGL(dp_pipeline_kernel, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
                      buf_bytes, in, out, n, part);
   if (stats)
-    hipLaunchKernelGGL(dp_stats_reduce, dim3(1), dim3(64), 0, stream, part,
+    hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

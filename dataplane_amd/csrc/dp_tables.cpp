@@ -488,6 +488,7 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
   for (auto &G : grecs) G.recs = recs_off;
   if (aux_patch)
     for (auto &rr : rec_rule) aux_patch->push_back({recs_off + rr.first * sizeof(CandRec) + offsetof(CandRec, aux), rr.second});
+  C.recs = recs_off;
   C.groups = build_hash(ib, gkv);
   if (gkv_out) *gkv_out = gkv;
   C.group_recs = ib.put(grecs);
