@@ -1193,7 +1193,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
     return;
   }
   if (S.encap) { done(S, DP_DONE_INTERNAL_FAILURE); return; }  // routing an encapsulated packet again: unsupported
-  const FibRec fb = g.at<FibRec>(g.im.fibs)[fi];
+  const FibRec &fb = g.at<FibRec>(g.im.fibs)[fi];  // fields read where used (no struct copy)
   uint8_t fam; Addr16 dst;
   cur_dst(F, H, S, fam, dst);
   uint32_t nhi = lpm_lookup(g, fam == 4 ? fb.v4 : fb.v6, dst);
@@ -1214,7 +1214,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
     if (S.done != DONE_NONE) return;
   }
   for (uint32_t k = 0; k < E.n_instr; k++) {
-    const Instr in = ins[k];
+    const Instr &in = ins[k];
     switch (in.kind) {
       case DP_INSTR_DROP: done(S, DP_DONE_ROUTE_DROP); break;
       case DP_INSTR_LOCAL: {
@@ -1527,19 +1527,18 @@ __device__ __forceinline__ int window_chunks(const dp_pkt_in_t &pin) {
 // outer Eth/IP/UDP/VXLAN headers.  Fields are patched into the LDS window
 // copy, checksums summed over the patched bytes, and the stack written back
 // in 16-byte chunks.  Returns the frame-relative output start.
-__device__ __forceinline__ int serialize(const Frame &F, const Hdr &H0, State &S, int &fl0, int &fl1) {
+__device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &fl0, int &fl1) {
   fl0 = fl1 = 0;
-  const int inner_start = S.pay_start - H0.size;
+  const int inner_start = S.pay_start - H.size;
   const int outer = S.encap ? 14 + (S.o_fam == 4 ? 20 : 40) + 16 : 0;
   const int start = inner_start - outer;
   if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
   // the parse-limit quirk consumed headers it did not record: the kept
   // stack moves sh bytes later to end at the payload (back to front)
-  const int sh = inner_start - H0.hb;
-  Hdr H = H0;
+  const int sh = inner_start - H.hb;
   if (sh) {
 #pragma unroll 1
-    for (int i = H0.size - 1; i >= 0; i--) wput8(F, H0.hb + sh + i, F.b(H0.hb + i));
+    for (int i = H.size - 1; i >= 0; i--) wput8(F, H.hb + sh + i, F.b(H.hb + i));
     H.hb += sh; H.net_off += sh; H.l4_off += sh; H.vx_off += sh;
 #pragma unroll
     for (int e = 0; e < 3; e++) H.ext_off[e] += sh;

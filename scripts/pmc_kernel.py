@@ -1,0 +1,20 @@
+# Summarise rocprofv3 --pmc CSVs: per-dispatch mean of each counter for one
+# kernel (default dp_pipeline_kernel), over every pass directory given.
+import csv
+import sys
+from collections import defaultdict
+
+
+def summarise(dirs, kernel="dp_pipeline_kernel"):
+    vals = defaultdict(lambda: defaultdict(float))
+    for d in dirs:
+        for row in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+            if kernel not in row["Kernel_Name"]:
+                continue
+            vals[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in vals.items()}
+
+
+if __name__ == "__main__":
+    for k, v in sorted(summarise(sys.argv[1:]).items()):
+        print(f"{k:40s} {v:18.1f}")

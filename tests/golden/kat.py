@@ -365,9 +365,97 @@ def nat_cases() -> List[Case]:
     return cs
 
 
+def pat_case(name, ref, cfg, s, d, src, sport, dst, dport, want):
+    """check_packet_with_ports (nat/src/static_nat/test.rs:820-848): a TCP
+    packet, both static-NAT requirements set; `want` = (src, sport, dst, dport)."""
+    ws, wsp, wd, wdp = want
+    return Case(name, ref,
+                lambda: overlay_tables(src_vni=s, dst_vni=d, nat=cfg(),
+                                       nat_flags=(NAT_STATIC, NAT_STATIC)),
+                [Pkt(tcp_frame(src, dst, sport, dport, ttl=255), seeded_vni=s,
+                     expect=dict(done="Delivered", src=ws, dst=wd, sport=wsp, dport=wdp))])
+
+
+def pat_peering(left: List[N.Expose], right: List[N.Expose]):
+    """build_gwconfig_from_exposes (test.rs:787-818): VPC-1 (VNI 100) and
+    VPC-2 (VNI 200) peered with the given exposes."""
+    return N.nat_tables([N.Peering(100, 200, left, right), N.Peering(200, 100, right, left)])
+
+
+def pat_basic_config():
+    """test_config_with_port_ranges_basic (test.rs:850-869)."""
+    e1 = N.Expose(ips=[("1.1.0.0/16", (4001, 5000))], as_range=[("10.1.0.0/16", (8001, 9000))])
+    e2 = N.Expose(ips=[("10.2.0.0/16", (1, 5))], nat=False)
+    return pat_peering([e1], [e2])
+
+
+def pat_complex_config():
+    """test_config_with_port_ranges_complex (test.rs:914-990)."""
+    e1 = N.Expose(ips=[("1.1.1.0/24", (4001, 5000)), ("1.1.2.0/25", (4001, 5000)),
+                       ("1.1.3.0/25", (5001, 5500))],
+                  nots=[("1.1.1.64/26", (4001, 5000)), ("1.1.1.128/25", (4501, 5000))],
+                  as_range=[("10.1.0.0/30", (2001, 2300)), ("10.1.0.128/25", (2001, 3000)),
+                            ("10.1.1.0/25", (2501, 3000)), ("10.1.1.128/25", (3001, 4000)),
+                            ("10.1.2.3/32", (1, 37200))],
+                  not_as=[("10.1.1.128/25", (3456, 3755))])
+    e2 = N.Expose(ips=[("2.1.0.0/32", (1, 32768)), ("2.1.0.1/32", (1, 32768))],
+                  as_range=[("10.2.0.0/30", (1, 16384))])
+    return pat_peering([e1], [e2])
+
+
+def pat_default_config():
+    """test_config_with_port_ranges_with_default (test.rs:1152-1180); the
+    default expose (`set_default`) carries no NAT."""
+    e1 = N.Expose(ips=[("1.1.0.0/16", (4001, 5000))], as_range=[("10.1.0.0/16", (8001, 9000))])
+    e2 = N.Expose(ips=[("1.2.0.0/16", (2001, 3000))], as_range=[("10.2.0.0/16", (6001, 7000))])
+    e3 = N.Expose(ips=[], nat=False)
+    return pat_peering([e1], [e2, e3])
+
+
+def pat_doc_example_config():
+    """The worked example of PortAddrTranslationValue's doc comment
+    (nat/src/static_nat/setup/tables.rs:357-382): 1.0.0.0/24 ports
+    4001-5000 onto 2.0.0.0/25 ports 6001-7000 then 3.0.0.0/26 ports
+    8001-10000."""
+    e1 = N.Expose(ips=[("1.0.0.0/24", (4001, 5000))],
+                  as_range=[("2.0.0.0/25", (6001, 7000)), ("3.0.0.0/26", (8001, 10000))])
+    return pat_peering([e1], [N.Expose(ips=["9.0.0.0/8"], nat=False)])
+
+
+def pat_cases() -> List[Case]:
+    cs = []
+    vec = [  # (config, ref, forward (src, sport, dst, dport), expected translation)
+        (pat_basic_config, "nat/src/static_nat/test.rs:875-908",
+         ("1.1.2.3", 4024, "10.2.2.18", 1), ("10.1.2.3", 8024, "10.2.2.18", 1)),
+        (pat_complex_config, "nat/src/static_nat/test.rs:999-1033",
+         ("1.1.1.0", 4001, "10.2.0.0", 1), ("10.1.0.0", 2001, "2.1.0.0", 1)),
+        (pat_complex_config, "nat/src/static_nat/test.rs:1037-1071",
+         ("1.1.3.127", 5500, "10.2.0.3", 16384), ("10.1.2.3", 37200, "2.1.0.1", 32768)),
+        (pat_complex_config, "nat/src/static_nat/test.rs:1075-1109",
+         ("1.1.1.255", 4500, "10.2.0.1", 16384), ("10.1.0.254", 2800, "2.1.0.0", 32768)),
+        (pat_complex_config, "nat/src/static_nat/test.rs:1113-1147",
+         ("1.1.2.0", 4001, "10.2.0.2", 1), ("10.1.0.254", 2801, "2.1.0.1", 1)),
+        (pat_default_config, "nat/src/static_nat/test.rs:1184-1219",
+         ("1.1.2.3", 4024, "10.2.2.18", 7000), ("10.1.2.3", 8024, "1.2.2.18", 3000)),
+        (pat_default_config, "nat/src/static_nat/test.rs:1221-1255",
+         ("1.1.2.3", 4024, "123.123.123.123", 7000), ("10.1.2.3", 8024, "123.123.123.123", 7000)),
+        # the doc comment's (IP 3.0.0.7) answer; its "port 3" is the offset into
+        # 8001-10000, i.e. port 8003
+        (pat_doc_example_config, "nat/src/static_nat/setup/tables.rs:357-382",
+         ("1.0.0.142", 4003, "9.1.2.3", 80), ("3.0.0.7", 8003, "9.1.2.3", 80)),
+    ]
+    for k, (cfg, ref, (a, ap, b, bp), want) in enumerate(vec):
+        cs.append(pat_case(f"pat_{cfg.__name__}_{k}", ref, cfg, 100, 200, a, ap, b, bp, want))
+        if cfg is not pat_doc_example_config:   # reverse path restores the original
+            ws, wsp, wd, wdp = want
+            cs.append(pat_case(f"pat_{cfg.__name__}_{k}_reverse", ref, cfg, 200, 100, wd, wdp, ws,
+                               wsp, (b, bp, a, ap)))
+    return cs
+
+
 def all_cases() -> List[Case]:
     return acl_cases() + ff_cases() + lpm_cases() + ttl_cases() + vxlan_qos_cases() + \
-        parse_cases() + nat_cases()
+        parse_cases() + nat_cases() + pat_cases()
 
 
 # ------------------------------------------------------------------ checks
@@ -399,7 +487,8 @@ def check(pkt: Pkt, out, frame_out: Optional[bytes]) -> List[str]:
         bad.append(f"oif {int(out['oif'])} not in {e['oif_in']}")
     if "fib_entry_in" in e and int(out["fib_entry"]) not in e["fib_entry_in"]:
         bad.append(f"fib_entry {int(out['fib_entry'])} not in {e['fib_entry_in']}")
-    if frame_out is not None and any(k in e for k in ("ttl", "src", "dst", "outer_dscp")):
+    if frame_out is not None and any(k in e for k in ("ttl", "src", "dst", "outer_dscp",
+                                                      "sport", "dport")):
         o = l3_of(frame_out)
         ver = frame_out[o] >> 4
         if ver == 4:
@@ -411,6 +500,13 @@ def check(pkt: Pkt, out, frame_out: Optional[bytes]) -> List[str]:
             ttl = frame_out[o + 7]
             src = str(ipaddress.IPv6Address(frame_out[o + 8:o + 24]))
             dst = str(ipaddress.IPv6Address(frame_out[o + 24:o + 40]))
+        if ver == 4 and ("sport" in e or "dport" in e):
+            l4 = o + (frame_out[o] & 0xF) * 4
+            sp, dp = struct.unpack("!HH", frame_out[l4:l4 + 4])
+            if "sport" in e and sp != e["sport"]:
+                bad.append(f"sport {sp} != {e['sport']}")
+            if "dport" in e and dp != e["dport"]:
+                bad.append(f"dport {dp} != {e['dport']}")
         if "ttl" in e and ttl != e["ttl"]:
             bad.append(f"ttl {ttl} != {e['ttl']}")
         if "src" in e and src != e["src"]:

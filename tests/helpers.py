@@ -23,11 +23,13 @@ def compare(out_ref, buf_ref, out_dut, buf_dut, inp, label=""):
     # unobservable; e.g. Packet::vxlan_encap has already prepended the inner
     # headers when Egress then fails), so its slot is excluded.  Everything
     # else -- delivered frames, their headroom, gaps -- must match.
+    # A packet owns [off - DP_HEADROOM, off + len) whatever the buffer layout
+    # (packed: 96 B headroom; DPDK mbuf: 128 B in front of the frame).
     diff = buf_ref != buf_dut
     dropped = np.nonzero(out_ref["done"] != A.DONE["Delivered"])[0]
     if len(dropped):
         starts = inp["off"].astype(np.int64) - A.HEADROOM
-        ends = np.append(starts[1:], len(buf_ref))
+        ends = inp["off"].astype(np.int64) + inp["len"].astype(np.int64)
         for i in dropped:
             diff[starts[i]:ends[i]] = False
     if diff.any():

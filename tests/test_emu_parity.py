@@ -11,12 +11,13 @@ import pyemu
 from helpers import compare
 
 
-@pytest.mark.parametrize("form", ["auto", "bv", "list"])
+@pytest.mark.parametrize("form,layout", [("auto", "packed"), ("bv", "packed"), ("list", "packed"),
+                                         ("auto", "dpdk")])
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
-def test_emu_matches_oracle(cfg, form, monkeypatch):
+def test_emu_matches_oracle(cfg, form, layout, monkeypatch):
     monkeypatch.setenv("DPGPU_CLS_FORM", form)
     w = Workload(cfg, 3000, seed=100 + cfg, n_routes_v4=3000, n_routes_v6=1500, n_acl=400,
-                 n_nat=48, tcp_percent=25)
+                 n_nat=48, tcp_percent=25, layout=layout)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
     o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
     o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT)

@@ -24,13 +24,17 @@ def nf():
     n.close()
 
 
-@pytest.mark.parametrize("form", ["auto", "bv", "list"])
+CASES = [(f, "packed") for f in ("auto", "bv", "list")] + [("auto", "dpdk")]
+
+
+@pytest.mark.parametrize("form,layout", CASES)
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
-def test_gpu_matches_oracle(nf, cfg, form, monkeypatch):
-    """Classifiers built in each form (DPGPU_CLS_FORM, read at publish)."""
+def test_gpu_matches_oracle(nf, cfg, form, layout, monkeypatch):
+    """Classifiers built in each form (DPGPU_CLS_FORM, read at publish), in
+    the packed layout and in the DPDK mbuf layout bench.py times."""
     monkeypatch.setenv("DPGPU_CLS_FORM", form)
     w = Workload(cfg, 20000, seed=200 + cfg, n_routes_v4=20000, n_routes_v6=8000, n_acl=1000,
-                 n_nat=64, tcp_percent=25)
+                 n_nat=64, tcp_percent=25, layout=layout)
     nf.publish(w.tables)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
     o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
@@ -62,13 +66,14 @@ def test_gpu_edge_corpus(nf, edge, seed, monkeypatch):
     compare(o_ref, b_ref, o_dut, b_dut, inp, f"edge {seed}")
 
 
-@pytest.mark.parametrize("cfg", [2, 4, 5])
-def test_gpu_full_size(nf, cfg):
+@pytest.mark.parametrize("cfg,layout", [(2, "dpdk"), (2, "packed"), (3, "dpdk"), (4, "dpdk"),
+                                        (5, "dpdk")])
+def test_gpu_full_size(nf, cfg, layout):
     """BASELINE.json table sizes (1M v4 routes, 200k v6 on C5, 10k ACL rules
     per family, 256 NAT maps) at 1M packets, bit-exact against the oracle run
-    on all host cores."""
+    on all host cores; the DPDK mbuf layout is the one bench.py times."""
     import os
-    w = Workload(cfg, 1_000_000, seed=300 + cfg, tcp_percent=20)
+    w = Workload(cfg, 1_000_000, seed=300 + cfg, tcp_percent=20, layout=layout)
     nf.publish(w.tables)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
     o_ref = np.zeros(w.n, dtype=A.PKT_OUT)
