@@ -98,6 +98,23 @@ struct RouteNh {
   uint32_t first_entry, n_entries;
 };
 
+// Resolved next hop, one per RouteNh (the values of the LPM leaves).  A route
+// whose only FibEntry is a single Egress (or Drop) instruction is resolved in
+// place, so the leaf reaches the egress outcome in one dependent load; any
+// other route (ECMP, Local / decap, VXLAN encap, instruction lists) keeps the
+// RouteNh -> Entry -> Instr chain (DPD_NH_CHAIN).
+#define DPD_NH_CHAIN 0
+#define DPD_NH_EGRESS 1
+#define DPD_NH_DROP 2
+struct alignas(16) NhRec {  // 32 B
+  uint8_t kind, eg_code, if_code, has_oif;
+  uint32_t oif;
+  uint32_t entry;      // FibEntry index (EGRESS / DROP); CHAIN: first_entry
+  uint32_t n_entries;  // CHAIN
+  uint64_t eg_dmac, eg_smac;
+};
+static_assert(sizeof(NhRec) == 32, "NhRec is 32 B");
+
 // Interface record with Ingress's table-only checks pre-evaluated
 // (dataplane/src/packet_processor/ingress.rs:153-182)
 struct IfRec {         // 32 B
@@ -112,8 +129,22 @@ struct IfRec {         // 32 B
   uint64_t pad2;
 };
 
-// Per source VNI context (value of the VNI map)
-struct VniRec {        // 32 B
+// Multibit index descriptor (see FieldIdx / NatTab) copied into the context
+// record that leads to the index, so the hot path walks it without first
+// loading the Group / NatTab record (one dependent load less per lookup).
+struct Mbi {           // 24 B
+  uint64_t root;       // 0: not usable here (bit-vector group, bounds form, absent table)
+  uint64_t blocks;
+  uint8_t s0, kbits;   // root stride, key width (32 address / 16 port)
+  uint8_t field;       // classifier: the indexed field (0 src, 1 dst, 2 sport, 3 dport)
+  uint8_t pad;
+  uint32_t pad2;
+};
+
+// Per source VNI context.  The records are the open-addressing slots of the
+// VNI map themselves (key `vni`, 0 = empty: VNI 0 is invalid,
+// net/src/vxlan/vni.rs:76-82), so one dependent load finds the context.
+struct alignas(16) VniRec {  // 96 B
   uint32_t vni;
   uint32_t fib;        // FIB index of the VNI
   uint32_t vrf_id;
@@ -121,17 +152,28 @@ struct VniRec {        // 32 B
   int32_t nat_dst;     // NAT dst table of the VNI's PerVniTable, -1
   uint32_t pervni;     // a PerVniTable exists for the VNI
   uint32_t pad;
+  Mbi ffr4;            // index of the v4 remote group (candidate-list form)
+  Mbi ndst;            // index of the NAT dst table
+  uint64_t pad2[2];
 };
+static_assert(sizeof(VniRec) == 96, "VniRec is 96 B");
 
 // Per (src VNI, dst VNI) context: target of a flow-filter remote verdict
-struct PairRec {       // 32 B
+struct alignas(16) PairRec {  // 128 B
   int32_t ffl[2];      // flow-filter local group (src, dst, 0) v4 / v6
   int32_t acl[2];      // ACL group (src, dst, 0) v4 / v6
   uint32_t acl_def;    // default action + 1, 0 = none
   int32_t nat_src;     // NAT src table (src -> dst), -1
   int32_t dst_fib;     // FIB of the dst VNI, -1
   uint32_t dst_vni;
+  Mbi ffl4;            // index of the v4 local group (candidate-list form)
+  Mbi acl4;            // index of the v4 ACL group (candidate-list form)
+  Mbi nsrc;            // index of the NAT src table
+  uint64_t lpm4_direct;  // the dst FIB's v4 LPM (Lpm.direct / dbits), 0: none
+  uint32_t lpm4_dbits;
+  uint32_t pad;
 };
+static_assert(sizeof(PairRec) == 128, "PairRec is 128 B");
 
 struct Adj {           // adjacency slot (open addressing, keyed ifindex+ip)
   uint32_t ifindex;
@@ -231,14 +273,22 @@ struct NatRange {
   uint64_t offset;
 };
 
-struct NatEnt {
+// 64 B, one sector: the entry plus an inline copy of its range when it has
+// exactly one (the common case: the lookup then needs no range search).
+struct alignas(16) NatEnt {
   uint32_t net;              // prefix network (host order)
-  uint8_t len, is_pat, covers_all, pad;
+  uint8_t len, is_pat, covers_all, inl;  // inl: the range is inline (n_ranges == 1, offset < 2^32)
   int32_t parent;            // next shorter covering entry in this table, -1
   uint32_t first_pr, n_pr;   // uint32_t packed (lo | hi<<16)
   uint32_t first_range, n_ranges;
-  uint64_t size;
+  uint32_t size_lo, size_hi; // Nat: ip_len(); Pat: size()
+  uint32_t olo_ip, ohi_ip;   // inline range (NatRange fields)
+  uint16_t olo_port, ohi_port;
+  uint32_t tlo_ip, thi_ip;
+  uint16_t tlo_port, thi_port;
+  uint32_t offset;
 };
+static_assert(sizeof(NatEnt) == 64, "NatEnt is one 64-byte sector");
 
 struct NatTab {
   uint64_t bounds;           // uint32_t[n] interval starts (host order)
@@ -253,7 +303,9 @@ struct NatTab {
 struct Image {
   uint64_t bytes;
   int64_t genid;
-  HashMap vni_fib;           // vni -> VniRec index
+  uint64_t vni_slots;        // VniRec[vni_mask + 1], open addressing on hmix(vni, 0, 0)
+  uint32_t vni_mask;
+  uint32_t pad_vni;
   HashMap vrf_fib;           // vrf id -> fib index
   uint64_t fibs;             // FibRec[]
   uint32_t n_fibs;
@@ -261,6 +313,7 @@ struct Image {
   uint64_t pt_nodes;         // PtNode[]
   uint64_t pt_leaves;        // uint32_t[]
   uint64_t route_nhs;        // RouteNh[]
+  uint64_t nh_recs;          // NhRec[] (parallel to route_nhs)
   uint64_t entries;          // Entry[]
   uint64_t instrs;           // Instr[]
   HashMap ifaces;            // ifindex -> IfRec index
@@ -268,7 +321,6 @@ struct Image {
   uint64_t if_direct;        // IfRec[if_direct_n], indexed by ifindex (small ifindexes)
   uint32_t if_direct_n;
   uint32_t n_vni_recs;
-  uint64_t vni_recs;         // VniRec[] (values of vni_fib)
   HashMap pairs;             // (src vni, dst vni) -> PairRec index
   uint64_t pair_recs;        // PairRec[]
   AdjMap adjs;

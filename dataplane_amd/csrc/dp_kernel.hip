@@ -533,16 +533,14 @@ __device__ __forceinline__ uint32_t key6(uint64_t hi, uint64_t lo, int off) {
   return (uint32_t)(x >> 58);
 }
 
-__device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
-  const uint32_t *direct = g.at<uint32_t>(L.direct);
-  uint32_t idx;
-  if (L.width == 32) idx = a.w[0] >> (32 - L.dbits);
-  else idx = a.w[0] >> (32 - L.dbits);  // dbits <= 32
+__device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t direct_off, uint32_t dbits, const Addr16 &a) {
+  const uint32_t *direct = g.at<uint32_t>(direct_off);
+  const uint32_t idx = a.w[0] >> (32 - dbits);  // dbits <= 32 for both families
   uint32_t e = direct[idx];
   if (e & 0x80000000u) return e & 0x7fffffffu;
   const PtNode *nodes = g.at<PtNode>(g.im.pt_nodes);
   const uint32_t *leaves = g.at<uint32_t>(g.im.pt_leaves);
-  int off = (int)L.dbits;
+  int off = (int)dbits;
   uint32_t ni = e;
   const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1], klo = ((uint64_t)a.w[2] << 32) | a.w[3];
   for (int guard = 0; guard < 24; guard++) {
@@ -559,6 +557,20 @@ __device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const
     return leaves[nd.base0 + (uint32_t)__popcll(lv & m) - 1];
   }
   return g.im.drop_nh;  // unreachable for a well-formed image
+}
+__device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
+  return lpm_walk(g, L.direct, L.dbits, a);
+}
+
+// Multibit index walk from a context record's descriptor (Mbi): leaf value
+// (DPD_LEAF stripped) of `key` (an address, or a port with kbits 16).
+__device__ __forceinline__ uint32_t mbi_walk(const Img &g, const Mbi &m, uint32_t key) {
+  const int rem0 = (int)m.kbits - (int)m.s0;
+  uint32_t e = g.at<uint32_t>(m.root)[key >> rem0];
+#pragma unroll
+  for (int l = 1; l <= 3; l++)
+    if (!(e & DPD_LEAF)) e = g.at<uint32_t>(m.blocks)[(e << 8) | ((key >> (rem0 - 8 * l)) & 0xff)];
+  return e & ~DPD_LEAF;
 }
 
 // ---------------------------------------------------------------------------
@@ -715,23 +727,35 @@ enum { W_ACTION = 1, W_ACTION2 = 2, W_AUX = 4, W_ORIG = 8 };
 __device__ __forceinline__ Hit verify_run(const Img &g, uint64_t recs, uint32_t run, bool v6, uint8_t proto,
                                           Key128 src, Key128 dst, uint16_t sp, uint16_t dp) {
   Hit h{-1, 0, 0, 0, 0};
-  {
-    // a record is four 16-byte words: src, dst, (lens, proto, ports, rule),
-    // (action, action2, aux, orig)
-    const uint4 *R = g.at<uint4>(recs) + 4 * (uint64_t)(run >> DPD_RUN_BITS);
-    const uint32_t cnt = run & DPD_RUN_MAX;
-    for (uint32_t c = 0; c < cnt; c++) {
-      const uint4 w2 = R[4 * c + 2];
-      const uint32_t slen = w2.x & 0xff, dlen = (w2.x >> 8) & 0xff;
-      const uint32_t pval = (w2.x >> 16) & 0xff, pmask = w2.x >> 24;
-      if ((proto & pmask) != (pval & pmask)) continue;
-      if (sp < (w2.y & 0xffff) || sp > (w2.y >> 16) || dp < (w2.z & 0xffff) || dp > (w2.z >> 16)) continue;
-      const uint4 w0 = R[4 * c], w1 = R[4 * c + 1];
-      const uint64_t shi = ((uint64_t)w0.y << 32) | w0.x, slo = ((uint64_t)w0.w << 32) | w0.z;
-      const uint64_t dhi = ((uint64_t)w1.y << 32) | w1.x, dlo = ((uint64_t)w1.w << 32) | w1.z;
-      if (!pfx_ok(src, shi, slo, slen, v6) || !pfx_ok(dst, dhi, dlo, dlen, v6)) continue;
-      const uint4 w3 = R[4 * c + 3];
-      h.rule = w2.w; h.action = w3.x; h.action2 = w3.y; h.aux = w3.z; h.orig = w3.w;
+  // A record is four 16-byte words: src, dst, (lens, proto, ports, rule),
+  // (action, action2, aux, orig).  Every word of a candidate is requested at
+  // once (one dependent round trip per candidate instead of up to three; the
+  // words share one 64-byte sector, so only the first misses L1), and
+  // candidates are fetched two at a time so a run's round trips halve.
+  const uint4 *R = g.at<uint4>(recs) + 4 * (uint64_t)(run >> DPD_RUN_BITS);
+  const uint32_t cnt = run & DPD_RUN_MAX;
+  auto match = [&](const uint4 &w0, const uint4 &w1, const uint4 &w2) -> bool {
+    const uint32_t slen = w2.x & 0xff, dlen = (w2.x >> 8) & 0xff;
+    const uint32_t pval = (w2.x >> 16) & 0xff, pmask = w2.x >> 24;
+    if ((proto & pmask) != (pval & pmask)) return false;
+    if (sp < (w2.y & 0xffff) || sp > (w2.y >> 16) || dp < (w2.z & 0xffff) || dp > (w2.z >> 16)) return false;
+    const uint64_t shi = ((uint64_t)w0.y << 32) | w0.x, slo = ((uint64_t)w0.w << 32) | w0.z;
+    const uint64_t dhi = ((uint64_t)w1.y << 32) | w1.x, dlo = ((uint64_t)w1.w << 32) | w1.z;
+    return pfx_ok(src, shi, slo, slen, v6) && pfx_ok(dst, dhi, dlo, dlen, v6);
+  };
+#pragma unroll 1
+  for (uint32_t c = 0; c < cnt; c += 2) {
+    const uint4 *a = R + 4 * c;
+    const uint4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+    uint4 b0 = make_uint4(0, 0, 0, 0), b1 = b0, b2 = make_uint4(0, 0, 0, 0), b3 = b0;
+    const bool two = c + 1 < cnt;
+    if (two) { b0 = a[4]; b1 = a[5]; b2 = a[6]; b3 = a[7]; }
+    if (match(a0, a1, a2)) {
+      h.rule = a2.w; h.action = a3.x; h.action2 = a3.y; h.aux = a3.z; h.orig = a3.w;
+      return h;
+    }
+    if (two && match(b0, b1, b2)) {
+      h.rule = b2.w; h.action = b3.x; h.action2 = b3.y; h.aux = b3.z; h.orig = b3.w;
       return h;
     }
   }
@@ -859,8 +883,9 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
     if (!live[k]) continue;
     const uint32_t addr = q[k].addr;
     const uint64_t ip_off = (uint64_t)(addr - E[k].net);
+    const uint64_t esize = ((uint64_t)E[k].size_hi << 32) | E[k].size_lo;
     if (!E[k].is_pat) {
-      if (ip_off >= E[k].size) { live[k] = false; continue; }
+      if (ip_off >= esize) { live[k] = false; continue; }
       eo[k] = ip_off;
     } else {
       if (!has_port) { live[k] = false; continue; }
@@ -873,9 +898,16 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
       uint32_t pr = prs[E[k].first_pr + pk];
       uint64_t plen = (uint64_t)(pr >> 16) - (pr & 0xffff) + 1;
       eo[k] = ip_off * plen + (uint64_t)(q[k].port - (pr & 0xffff));
-      if (eo[k] >= E[k].size) { live[k] = false; continue; }
+      if (eo[k] >= esize) { live[k] = false; continue; }
     }
-    rh[k] = E[k].n_ranges;
+    if (E[k].inl) {
+      // the only range is inline in the entry: no search
+      const bool le = E[k].is_pat ? (E[k].olo_ip < addr || (E[k].olo_ip == addr && E[k].olo_port <= q[k].port))
+                                  : E[k].olo_ip <= addr;
+      rl[k] = rh[k] = le ? 1u : 0u;
+    } else {
+      rh[k] = E[k].n_ranges;
+    }
   }
   for (int it = 0; it < 32; it++) {
     bool any = false;
@@ -896,7 +928,14 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
     if (!live[k]) continue;
     int sel = (int)rl[k] - 1;
     if (sel < 0) continue;
-    const NatRange R = ranges[E[k].first_range + sel];
+    NatRange R;
+    if (E[k].inl) {
+      R.olo_ip = E[k].olo_ip; R.ohi_ip = E[k].ohi_ip; R.olo_port = E[k].olo_port; R.ohi_port = E[k].ohi_port;
+      R.tlo_ip = E[k].tlo_ip; R.thi_ip = E[k].thi_ip; R.tlo_port = E[k].tlo_port; R.thi_port = E[k].thi_port;
+      R.offset = E[k].offset;
+    } else {
+      R = ranges[E[k].first_range + sel];
+    }
     const uint32_t addr = q[k].addr;
     if (!E[k].is_pat) {
       if (addr > R.ohi_ip) continue;
@@ -997,10 +1036,25 @@ __device__ __forceinline__ void stage_ingress(const Img &g, const Frame &F, cons
 }
 
 // VNI -> VniRec (the VNI's FIB, VRF and per-VNI tables)
+// VNI map probe: the slots are the VniRecs themselves (vni 0 = empty)
+__device__ __forceinline__ int32_t find_vni(const Img &g, uint32_t vni) {
+  if (vni == 0) return -1;
+  const VniRec *slots = g.at<VniRec>(g.im.vni_slots);
+  const uint32_t mask = g.im.vni_mask;
+  uint32_t i = hmix(vni, 0, 0) & mask;
+  for (uint32_t probe = 0; probe <= mask; probe++) {
+    const uint32_t k = slots[i].vni;
+    if (k == vni) return (int32_t)i;
+    if (k == 0) return -1;
+    i = (i + 1) & mask;
+  }
+  return -1;
+}
+
 __device__ __forceinline__ bool enter_vni(const Img &g, State &S, uint32_t vni) {
-  uint32_t vi;
-  if (!hash_find(g, g.im.vni_fib, vni, 0, 0, vi)) return false;
-  const VniRec R = g.at<VniRec>(g.im.vni_recs)[vi];
+  const int32_t vi = find_vni(g, vni);
+  if (vi < 0) return false;
+  const VniRec R = g.at<VniRec>(g.im.vni_slots)[vi];
   S.src_vni = vni;
   S.has_vrf = true;
   S.vrf = R.vrf_id;
@@ -1175,13 +1229,19 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   bool had_vrf = S.has_vrf;
   uint32_t vrf0 = S.vrf;
   int32_t fi;
+  uint64_t d4 = 0;   // the dst FIB's v4 LPM, read from the pair context (no FibRec load)
+  uint32_t b4 = 0;
   if (S.dst_vni) {
     if (H.net == 0 && !S.encap) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
     int32_t pi = pair_of(g, S);
-    if (pi >= 0) fi = g.at<PairRec>(g.im.pair_recs)[pi].dst_fib;
-    else {
-      uint32_t vi;
-      fi = hash_find(g, g.im.vni_fib, S.dst_vni, 0, 0, vi) ? (int32_t)g.at<VniRec>(g.im.vni_recs)[vi].fib : -1;
+    if (pi >= 0) {
+      const PairRec &PR = g.at<PairRec>(g.im.pair_recs)[pi];
+      fi = PR.dst_fib;
+      d4 = PR.lpm4_direct;
+      b4 = PR.lpm4_dbits;
+    } else {
+      const int32_t vi = find_vni(g, S.dst_vni);
+      fi = vi >= 0 ? (int32_t)g.at<VniRec>(g.im.vni_slots)[vi].fib : -1;
     }
     if (fi < 0) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
   } else if (S.has_vrf) {
@@ -1196,15 +1256,30 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   const FibRec &fb = g.at<FibRec>(g.im.fibs)[fi];  // fields read where used (no struct copy)
   uint8_t fam; Addr16 dst;
   cur_dst(F, H, S, fam, dst);
-  uint32_t nhi = lpm_lookup(g, fam == 4 ? fb.v4 : fb.v6, dst);
-  const RouteNh nh = g.at<RouteNh>(g.im.route_nhs)[nhi];
+  const uint32_t nhi = (fam == 4 && d4) ? lpm_walk(g, d4, b4, dst) : lpm_lookup(g, fam == 4 ? fb.v4 : fb.v6, dst);
+  const NhRec nr = g.at<NhRec>(g.im.nh_recs)[nhi];
+  if (nr.kind != DPD_NH_CHAIN) {
+    // a single Egress / Drop instruction, resolved at publish (NhRec)
+    S.fib_entry = nr.entry;
+    decrement_ttl(S);
+    if (S.done != DONE_NONE) return;
+    if (nr.kind == DPD_NH_DROP) { done(S, DP_DONE_ROUTE_DROP); return; }
+    S.has_oif = nr.has_oif;
+    S.oif = nr.oif;
+    S.eg_code = nr.eg_code;
+    S.if_code = nr.if_code;
+    S.eg_dmac = nr.eg_dmac;
+    S.eg_smac = nr.eg_smac;
+    if (S.has_vrf == had_vrf && (!had_vrf || S.vrf == vrf0)) S.has_vrf = false;
+    return;
+  }
   uint32_t idx = 0;
-  if (nh.n_entries > 1) {
+  if (nr.n_entries > 1) {
     HBuf hbuf{F.hs, 0};
     hash_ip_fields(F, H, S, hbuf);
-    idx = (uint32_t)(rapid(hbuf.b, hbuf.n) % nh.n_entries);
+    idx = (uint32_t)(rapid(hbuf.b, hbuf.n) % nr.n_entries);
   }
-  uint32_t ei = nh.first_entry + idx;
+  uint32_t ei = nr.entry + idx;
   const Entry E = g.at<Entry>(g.im.entries)[ei];
   S.fib_entry = ei;
   const Instr *ins = g.at<Instr>(g.im.instrs) + E.first_instr;
@@ -1264,60 +1339,42 @@ __device__ __forceinline__ Key128 key_of(const Frame &F, const Hdr &H, const Sta
 // table, a bit-vector group or a bounds-form index; the stage walks itself).
 struct Pre { uint32_t ffl, acl, nsrc, ndst; };
 
-__device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_t pi, int32_t lg, Pre &P) {
+// Key of a classifier field for the v4 hoisted walks (f: 0 src, 1 dst, 2
+// sport, 3 dport); `local` = the flow-filter local table, whose dst / dport
+// keys are wildcards (0).
+__device__ __forceinline__ uint32_t mbi_key(const State &S, uint32_t f, bool local) {
+  return f == 0 ? S.v4src : f == 1 ? (local ? 0u : S.v4dst) : f == 2 ? (uint32_t)S.sport
+                                                                     : (local ? 0u : (uint32_t)S.dport);
+}
+
+__device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_t pi, Pre &P) {
   P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
-  const PairRec PR = g.at<PairRec>(g.im.pair_recs)[pi];
-  const int32_t nat_dst = g.at<VniRec>(g.im.vni_recs)[S.vni_idx].nat_dst;
-  uint64_t root[4], blocks[4];
+  // the index descriptors ride in the pair / VNI contexts (Mbi): the four
+  // walks start right after the pair context arrives
+  const PairRec &PR = g.at<PairRec>(g.im.pair_recs)[pi];
+  const VniRec &VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
+  Mbi m[4] = {PR.ffl4, PR.acl4, PR.nsrc, VR.ndst};
   uint32_t key[4], e[4];
   int rem0[4];
-  bool on[4];
+  key[0] = mbi_key(S, m[0].field, true);
+  key[1] = mbi_key(S, m[1].field, false);
+  key[2] = S.v4src;
+  key[3] = S.v4dst;
 #pragma unroll
-  for (int k = 0; k < 4; k++) { on[k] = false; root[k] = blocks[k] = 0; key[k] = 0; rem0[k] = 0; e[k] = DPD_LEAF; }
-  // 0: flow-filter local (keys: src, -, sport, -); 1: ACL (src, dst, sport, dport)
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    const int32_t gi = k == 0 ? lg : PR.acl[0];
-    if (gi < 0) continue;
-    const Group *Gp = g.at<Group>(k == 0 ? g.im.ff_local[0].group_recs : g.im.acl[0].group_recs) + gi;
-    if (Gp->mode != DPD_GROUP_LIST) continue;
-    const uint32_t f = Gp->lfield;
-    const FieldIdx &FI = Gp->f[f];
-    const uint64_t r = FI.root;
-    if (!r) continue;
-    on[k] = true;
-    root[k] = r;
-    blocks[k] = FI.blocks;
-    rem0[k] = (int)FI.kbits - (int)FI.s0;
-    key[k] = f == 0 ? S.v4src : f == 1 ? (k == 0 ? 0u : S.v4dst) : f == 2 ? (uint32_t)S.sport : (k == 0 ? 0u : (uint32_t)S.dport);
+  for (int k = 0; k < 4; k++) {
+    rem0[k] = (int)m[k].kbits - (int)m[k].s0;
+    e[k] = m[k].root ? g.at<uint32_t>(m[k].root)[key[k] >> rem0[k]] : DPD_LEAF;
   }
-  // 2: NAT src table of the pair, 3: NAT dst table of the source VNI
-#pragma unroll
-  for (int k = 2; k < 4; k++) {
-    const int32_t ti = k == 2 ? PR.nat_src : nat_dst;
-    if (ti < 0) continue;
-    const NatTab &T = g.at<NatTab>(g.im.nat_tab_recs)[ti];
-    const uint64_t r = T.root;
-    if (!r || T.n == 0) continue;
-    on[k] = true;
-    root[k] = r;
-    blocks[k] = T.blocks;
-    rem0[k] = 32 - (int)T.s0;
-    key[k] = k == 2 ? S.v4src : S.v4dst;
-  }
-#pragma unroll
-  for (int k = 0; k < 4; k++)
-    if (on[k]) e[k] = g.at<uint32_t>(root[k])[key[k] >> rem0[k]];
 #pragma unroll
   for (int l = 1; l <= 3; l++) {
 #pragma unroll
     for (int k = 0; k < 4; k++)
-      if (on[k] && !(e[k] & DPD_LEAF)) e[k] = g.at<uint32_t>(blocks[k])[(e[k] << 8) | ((key[k] >> (rem0[k] - 8 * l)) & 0xff)];
+      if (!(e[k] & DPD_LEAF)) e[k] = g.at<uint32_t>(m[k].blocks)[(e[k] << 8) | ((key[k] >> (rem0[k] - 8 * l)) & 0xff)];
   }
-  if (on[0]) P.ffl = e[0] & ~DPD_LEAF;
-  if (on[1]) P.acl = e[1] & ~DPD_LEAF;
-  if (on[2]) P.nsrc = e[2] & ~DPD_LEAF;
-  if (on[3]) P.ndst = e[3] & ~DPD_LEAF;
+  if (m[0].root) P.ffl = e[0] & ~DPD_LEAF;
+  if (m[1].root) P.acl = e[1] & ~DPD_LEAF;
+  if (m[2].root) P.nsrc = e[2] & ~DPD_LEAF;
+  if (m[3].root) P.ndst = e[3] & ~DPD_LEAF;
 }
 
 __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, State &S, Pre &P) {
@@ -1328,15 +1385,20 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   uint8_t proto = net_proto(F, H);
   int t = H.net == 4 ? 0 : 1;
   Key128 src = key_of(F, H, S, true), dst = key_of(F, H, S, false);
-  const int32_t rg = g.at<VniRec>(g.im.vni_recs)[S.vni_idx].ffr[t];
+  const VniRec &VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
+  const int32_t rg = VR.ffr[t];
+  // v4 candidate-list group: walk its index straight from the VNI context
+  const uint32_t pre = (t == 0 && VR.ffr4.root) ? mbi_walk(g, VR.ffr4, mbi_key(S, VR.ffr4.field, false) *
+                                                                          (VR.ffr4.field & 1))
+                                                : NO_PRE;
   const Hit rh = classify<W_ACTION | W_ACTION2 | W_AUX>(g, CLS_ARRAYS(ff_remote, t), rg, t, proto,
-                                                       Key128{0, 0}, dst, 0, S.dport);
+                                                       Key128{0, 0}, dst, 0, S.dport, pre);
   if (rh.rule < 0) { done(S, DP_DONE_FILTERED); return; }
   uint32_t dvni = rh.action;
   uint32_t dnat = rh.action2;
   int32_t pi = (int32_t)rh.aux;
   int32_t lg = g.at<PairRec>(g.im.pair_recs)[pi].ffl[t];
-  if (t == 0) hoist_walks(g, S, pi, lg, P);
+  if (t == 0) hoist_walks(g, S, pi, P);
   const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, proto, src, Key128{0, 0}, S.sport, 0, P.ffl);
   if (lh.rule < 0) { done(S, DP_DONE_FILTERED); return; }
   uint32_t snat = lh.action;
@@ -1379,7 +1441,7 @@ __device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, c
   if (!(S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST))) return;
   if (S.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) return;
   if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
-  const VniRec VR = g.at<VniRec>(g.im.vni_recs)[S.vni_idx];
+  const VniRec VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
   if (!VR.pervni) { done(S, DP_DONE_UNROUTABLE); return; }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
   const int32_t pi = pair_of(g, S);

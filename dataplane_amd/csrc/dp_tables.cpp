@@ -676,6 +676,31 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
   im.route_nhs = ib.put(nhs);
   im.entries = ib.put(entries);
   im.instrs = ib.put(instrs);
+  // resolved next hops (one per RouteNh): a single FibEntry holding a single
+  // Egress / Drop instruction is resolved in place
+  std::vector<NhRec> nhrecs;
+  for (const RouteNh &n : nhs) {
+    NhRec r{};
+    r.kind = DPD_NH_CHAIN;
+    r.entry = n.first_entry;
+    r.n_entries = n.n_entries;
+    if (n.n_entries == 1 && entries[n.first_entry].n_instr == 1) {
+      const Instr &x = instrs[entries[n.first_entry].first_instr];
+      if (x.kind == DP_INSTR_EGRESS) {
+        r.kind = DPD_NH_EGRESS;
+        r.eg_code = x.eg_code;
+        r.if_code = x.if_code;
+        r.has_oif = (x.flags & DP_INSTR_HAS_IFINDEX) ? 1 : 0;
+        r.oif = x.ifindex;
+        r.eg_dmac = x.eg_dmac;
+        r.eg_smac = x.eg_smac;
+      } else if (x.kind == DP_INSTR_DROP) {
+        r.kind = DPD_NH_DROP;
+      }
+    }
+    nhrecs.push_back(r);
+  }
+  im.nh_recs = ib.put(nhrecs);
 
   // --- interfaces / adjacencies
   std::vector<IfRec> ifs;
@@ -819,7 +844,8 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
       ne.net = be32(e->prefix.addr);
       ne.len = e->prefix.len;
       ne.is_pat = e->is_pat ? 1 : 0;
-      ne.size = e->size;
+      ne.size_lo = (uint32_t)e->size;
+      ne.size_hi = (uint32_t)(e->size >> 32);
       ne.first_pr = (uint32_t)nprs.size();
       ne.n_pr = e->n_port_ranges;
       uint64_t tot = 0;
@@ -846,6 +872,13 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
       });
       ne.first_range = (uint32_t)nranges.size();
       ne.n_ranges = (uint32_t)rs.size();
+      if (rs.size() == 1 && rs[0].offset <= 0xffffffffull) {
+        const NatRange &x = rs[0];
+        ne.inl = 1;
+        ne.olo_ip = x.olo_ip; ne.ohi_ip = x.ohi_ip; ne.olo_port = x.olo_port; ne.ohi_port = x.ohi_port;
+        ne.tlo_ip = x.tlo_ip; ne.thi_ip = x.thi_ip; ne.tlo_port = x.tlo_port; ne.thi_port = x.thi_port;
+        ne.offset = (uint32_t)x.offset;
+      }
       nranges.insert(nranges.end(), rs.begin(), rs.end());
       ne.parent = -1;
       nents.push_back(ne);
@@ -931,6 +964,23 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     auto it = ntmap.find(gkey(kind, sv, dv));
     return it == ntmap.end() ? -1 : it->second;
   };
+  // multibit index descriptors for the context records (Mbi)
+  auto cls_mbi = [&](const Classifier &C, int32_t gi) {
+    Mbi m{};
+    if (gi < 0) return m;
+    Group G;
+    memcpy(&G, ib.b.data() + C.group_recs + (uint64_t)gi * sizeof(Group), sizeof(Group));
+    if (G.mode != DPD_GROUP_LIST || !G.f[G.lfield].root) return m;
+    const FieldIdx &F = G.f[G.lfield];
+    m.root = F.root; m.blocks = F.blocks; m.s0 = F.s0; m.kbits = F.kbits; m.field = (uint8_t)G.lfield;
+    return m;
+  };
+  auto nat_mbi = [&](int32_t ti) {
+    Mbi m{};
+    if (ti < 0 || !ntabs[ti].root || ntabs[ti].n == 0) return m;
+    m.root = ntabs[ti].root; m.blocks = ntabs[ti].blocks; m.s0 = ntabs[ti].s0; m.kbits = 32;
+    return m;
+  };
   std::vector<VniRec> vrecs;
   std::vector<KV> vnikv2;
   for (uint32_t vni : vni_order) {
@@ -942,12 +992,27 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     r.ffr[1] = group_of(3, vni, 0);
     r.nat_dst = nat_tab(0, vni, 0);
     r.pervni = has_pervni.count(vni) ? 1 : 0;
+    r.ffr4 = cls_mbi(im.ff_remote[0], r.ffr[0]);
+    r.ndst = nat_mbi(r.nat_dst);
     vnikv2.push_back(KV{vni, 0, 0, (uint32_t)vrecs.size()});
     vrecs.push_back(r);
   }
-  im.vni_fib = build_hash(ib, vnikv2);
-  im.vni_recs = ib.put(vrecs);
-  im.n_vni_recs = (uint32_t)vrecs.size();
+  {
+    // the records are the slots of the VNI map (key vni, 0 = empty)
+    uint32_t cap = 2;
+    while (cap < 2 * std::max<size_t>(1, vrecs.size())) cap <<= 1;
+    std::vector<VniRec> slots(cap);
+    memset(slots.data(), 0, sizeof(VniRec) * cap);
+    for (auto &r : vrecs) {
+      if (r.vni == 0) return DP_EINVAL;
+      uint32_t i = hmix(r.vni, 0, 0) & (cap - 1);
+      while (slots[i].vni != 0) i = (i + 1) & (cap - 1);
+      slots[i] = r;
+    }
+    im.vni_slots = ib.put(slots);
+    im.vni_mask = cap - 1;
+    im.n_vni_recs = (uint32_t)vrecs.size();
+  }
   std::unordered_map<uint64_t, uint32_t> pidx;
   std::vector<PairRec> prs;
   std::vector<KV> pkv;
@@ -968,6 +1033,10 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     auto f = vni2fib.find(dv);
     r.dst_fib = f == vni2fib.end() ? -1 : (int32_t)f->second;
     r.dst_vni = dv;
+    r.ffl4 = cls_mbi(im.ff_local[0], r.ffl[0]);
+    r.acl4 = cls_mbi(im.acl[0], r.acl[0]);
+    r.nsrc = nat_mbi(r.nat_src);
+    if (r.dst_fib >= 0) { r.lpm4_direct = fibs[r.dst_fib].v4.direct; r.lpm4_dbits = fibs[r.dst_fib].v4.dbits; }
     uint32_t id = (uint32_t)prs.size();
     pidx[k] = id;
     pkv.push_back(KV{sv, dv, 0, id});
