@@ -237,6 +237,18 @@ struct CandRec {       // 64 B, 64-byte aligned: one sector per candidate
   uint32_t action, action2, aux, orig;
 };
 static_assert(sizeof(CandRec) == 64, "CandRec is one 64-byte sector");
+// v4 candidate (32 B, two per sector): the predicates plus the three action
+// words a v4 lookup reads.  act0 = action; act1 = action2 (flow-filter
+// remote) or the caller's rule index (ACL, flow-filter local); act2 = the
+// PairRec index (flow-filter remote) or the global rule index.
+struct alignas(16) CandRec4 {
+  uint32_t src, dst;                   // prefix networks
+  uint8_t slen, dlen, proto_val, proto_mask;
+  uint16_t sp_lo, sp_hi;
+  uint16_t dp_lo, dp_hi;
+  uint32_t act0, act1, act2;
+};
+static_assert(sizeof(CandRec4) == 32, "CandRec4 is 32 B");
 
 struct Group {
   uint32_t n_rules;
@@ -258,7 +270,8 @@ struct Classifier {
   uint64_t action2;    // uint32_t[n_rules_total]
   uint64_t orig;       // uint32_t[n_rules_total] (index in the caller's array)
   uint64_t aux;        // uint32_t[n_rules_total]: flow-filter remote -> PairRec index
-  uint64_t recs;       // CandRec[] of the candidate-list groups (shared by all groups)
+  uint64_t recs;       // candidate records of the list groups (shared by all groups):
+                       // CandRec4[] in a v4 classifier, CandRec[] in a v6 one
   uint32_t n_groups;
   uint32_t n_rules;
 };

@@ -727,13 +727,44 @@ enum { W_ACTION = 1, W_ACTION2 = 2, W_AUX = 4, W_ORIG = 8 };
 __device__ __forceinline__ Hit verify_run(const Img &g, uint64_t recs, uint32_t run, bool v6, uint8_t proto,
                                           Key128 src, Key128 dst, uint16_t sp, uint16_t dp) {
   Hit h{-1, 0, 0, 0, 0};
-  // A record is four 16-byte words: src, dst, (lens, proto, ports, rule),
-  // (action, action2, aux, orig).  Every word of a candidate is requested at
-  // once (one dependent round trip per candidate instead of up to three; the
-  // words share one 64-byte sector, so only the first misses L1), and
-  // candidates are fetched two at a time so a run's round trips halve.
-  const uint4 *R = g.at<uint4>(recs) + 4 * (uint64_t)(run >> DPD_RUN_BITS);
-  const uint32_t cnt = run & DPD_RUN_MAX;
+  const uint32_t first = run >> DPD_RUN_BITS, cnt = run & DPD_RUN_MAX;
+  if (!v6) {
+    // v4: 32-byte records (CandRec4), two candidates per round trip -- their
+    // four 16-byte words are requested together (one or two sectors)
+    const uint4 *R = g.at<uint4>(recs) + 2 * (uint64_t)first;
+    const uint32_t s = (uint32_t)src.lo, d = (uint32_t)dst.lo;
+    auto match4 = [&](const uint4 &w0, const uint4 &w1) -> bool {
+      const uint32_t slen = w0.z & 0xff, dlen = (w0.z >> 8) & 0xff;
+      const uint32_t pval = (w0.z >> 16) & 0xff, pmask = w0.z >> 24;
+      if ((proto & pmask) != (pval & pmask)) return false;
+      if (sp < (w0.w & 0xffff) || sp > (w0.w >> 16) || dp < (w1.x & 0xffff) || dp > (w1.x >> 16)) return false;
+      if (slen && ((s ^ w0.x) >> (32 - slen))) return false;
+      if (dlen && ((d ^ w0.y) >> (32 - dlen))) return false;
+      return true;
+    };
+#pragma unroll 1
+    for (uint32_t c = 0; c < cnt; c += 2) {
+      // named registers, not an array: a dynamically indexed array would live in scratch
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      const uint4 *q = R + 2 * c;
+      const uint4 a0 = q[0], a1 = q[1];
+      const uint4 b0 = c + 1 < cnt ? q[2] : z, b1 = c + 1 < cnt ? q[3] : z;
+      uint4 hit = z;
+      bool found = true;
+      if (match4(a0, a1)) hit = a1;
+      else if (c + 1 < cnt && match4(b0, b1)) hit = b1;
+      else found = false;
+      if (found) {
+        h.rule = hit.w; h.action = hit.y; h.action2 = hit.z; h.orig = hit.z; h.aux = hit.w;
+        return h;
+      }
+    }
+    return h;
+  }
+  // v6: four 16-byte words per record: src, dst, (lens, proto, ports, rule),
+  // (action, action2, aux, orig); every word of a candidate is requested at
+  // once and candidates come two per round trip
+  const uint4 *R = g.at<uint4>(recs) + 4 * (uint64_t)first;
   auto match = [&](const uint4 &w0, const uint4 &w1, const uint4 &w2) -> bool {
     const uint32_t slen = w2.x & 0xff, dlen = (w2.x >> 8) & 0xff;
     const uint32_t pval = (w2.x >> 16) & 0xff, pmask = w2.x >> 24;

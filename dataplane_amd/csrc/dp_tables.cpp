@@ -307,7 +307,9 @@ int cls_form_override() {
 // `gkv_out`: group keys -> group index; `order_out`: rules in global rule
 // index order (the order of the action arrays); `aux_patch`: image offsets
 // of CandRec::aux fields with their rule (filled in once PairRecs exist).
-Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam,
+// `kind`: 0 ACL, 1 flow-filter remote, 2 flow-filter local (which action
+// words a v4 candidate record carries, CandRec4).
+Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam, int kind,
                             std::vector<KV> *gkv_out, std::vector<const dp_rule_t *> *order_out,
                             std::vector<std::pair<uint64_t, const dp_rule_t *>> *aux_patch = nullptr) {
   Classifier C{};
@@ -484,10 +486,28 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
     grecs.push_back(G);
     g_forms[0]++;
   }
-  uint64_t recs_off = ib.put(recs, 64);
+  uint64_t recs_off;
+  if (fam == 4) {
+    std::vector<CandRec4> r4;
+    for (const CandRec &c : recs) {
+      CandRec4 x{};
+      x.src = (uint32_t)c.src_lo; x.dst = (uint32_t)c.dst_lo;
+      x.slen = c.slen; x.dlen = c.dlen; x.proto_val = c.proto_val; x.proto_mask = c.proto_mask;
+      x.sp_lo = c.sp_lo; x.sp_hi = c.sp_hi; x.dp_lo = c.dp_lo; x.dp_hi = c.dp_hi;
+      x.act0 = c.action;
+      x.act1 = kind == 1 ? c.action2 : c.orig;
+      x.act2 = kind == 1 ? c.aux : c.rule;
+      r4.push_back(x);
+    }
+    recs_off = ib.put(r4, 64);
+    if (aux_patch)
+      for (auto &rr : rec_rule) aux_patch->push_back({recs_off + rr.first * sizeof(CandRec4) + offsetof(CandRec4, act2), rr.second});
+  } else {
+    recs_off = ib.put(recs, 64);
+    if (aux_patch)
+      for (auto &rr : rec_rule) aux_patch->push_back({recs_off + rr.first * sizeof(CandRec) + offsetof(CandRec, aux), rr.second});
+  }
   for (auto &G : grecs) G.recs = recs_off;
-  if (aux_patch)
-    for (auto &rr : rec_rule) aux_patch->push_back({recs_off + rr.first * sizeof(CandRec) + offsetof(CandRec, aux), rr.second});
   C.recs = recs_off;
   C.groups = build_hash(ib, gkv);
   if (gkv_out) *gkv_out = gkv;
@@ -788,7 +808,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     auto &t = tabs[ti];
     if ((rc = load_rules(t.r, t.n, t.fam, t.prio, t.kind, keep[ti]))) return rc;
     bool ffr = ti == 2 || ti == 3;
-    *t.dst = build_classifier(ib, keep[ti], t.fam, &gkv[ti], ffr ? &ffr_order[ti - 2] : nullptr,
+    *t.dst = build_classifier(ib, keep[ti], t.fam, t.kind, &gkv[ti], ffr ? &ffr_order[ti - 2] : nullptr,
                               ffr ? &ffr_aux[ti - 2] : nullptr);
   }
   auto gkey = [](uint32_t a, uint32_t b, uint32_t c) {
