@@ -167,7 +167,8 @@ STRUCTS = dict(dp_ipaddr_t=IpAddr, dp_prefix_t=Prefix, dp_fib_t=Fib, dp_vni_fib_
 # every symbol include/dpgpu.h declares
 GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_publish",
                "dp_tables_genid", "dp_process_burst", "dp_process_burst_device",
-               "dp_ctx_synchronize", "dp_tables_device_bytes", "dp_last_error"]
+               "dp_process_burst_sharded", "dp_ctx_synchronize", "dp_tables_device_bytes",
+               "dp_last_error"]
 
 _VP = C.c_void_p
 _U8P = C.POINTER(C.c_uint8)
@@ -197,6 +198,8 @@ def gpu_lib() -> C.CDLL:
         lib.dp_process_burst.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, C.c_uint32, _VP]
         lib.dp_process_burst_device.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, C.c_uint32,
                                                 _VP, _VP]
+        lib.dp_process_burst_sharded.argtypes = [C.POINTER(_VP), C.c_uint32, _VP, C.c_uint64,
+                                                 _VP, _VP, C.c_uint32, _VP]
         lib.dp_ctx_synchronize.argtypes = [_VP]
         lib.dp_tables_device_bytes.argtypes = [_VP]
         lib.dp_tables_device_bytes.restype = C.c_uint64

@@ -1947,6 +1947,26 @@ extern "C" int dp_debug_stage_cycles(unsigned long long *out16, int reset) {
   return 0;
 }
 #endif
+// Whole-burst failure: every packet InternalFailure (dpgpu.h conventions).
+__global__ void __launch_bounds__(256) dp_mark_failed(const dp_pkt_in_t *__restrict__ in,
+                                                      dp_pkt_out_t *__restrict__ out, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  dp_pkt_out_t o{};
+  o.off = in[i].off;
+  o.len = in[i].len;
+  o.done = DP_DONE_INTERNAL_FAILURE;
+  o.fib_entry = 0xffffffffu;
+  o.acl_rule = 0xffffffffu;
+  out[i] = o;
+}
+
+extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, hipStream_t stream) {
+  if (n == 0 || !in || !out) return 0;
+  hipLaunchKernelGGL(dp_mark_failed, dim3((n + 255) / 256), dim3(256), 0, stream, in, out, n);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    uint32_t n, uint64_t *stats, uint64_t *stats_part, hipStream_t stream) {

@@ -6,19 +6,25 @@
 // Table publication mirrors the reference's lock-free reader handles
 // (left-right for FIB / NAT, ArcSwap Slot for flow-filter / ACL,
 // SURVEY.md §1): dp_tables_publish compiles and uploads a new image, then
-// swaps one per-device shared pointer under a mutex.  Each burst pins the
-// image it launched with (a shared_ptr held by the context until its next
-// burst), so the previous image is released only after every context has
-// moved on; hipFree synchronises, so no kernel still reads freed memory.
+// swaps one per-device shared pointer under a mutex.  Every burst keeps a
+// reference to the image it launched with until a completion event of that
+// burst has fired (polled without blocking at the context's next burst), so
+// an old image is released only after the last burst reading it has ended.
+// A released image's memory goes to a per-device graveyard and is freed by
+// the publishing (mgmt) thread -- hipFree synchronises the device, so it never
+// runs on a worker's burst path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/dpgpu.h"
 #include "dp_tables.h"
@@ -26,6 +32,7 @@
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    uint32_t n, uint64_t *stats, uint64_t *stats_part, hipStream_t stream);
+extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, hipStream_t stream);
 
 namespace {
 
@@ -40,18 +47,52 @@ int fail(int rc, const char *what, hipError_t e = hipSuccess) {
   return rc;
 }
 
+struct DeviceTables;
+DeviceTables &dev_tables(int device);
+
+// Device memory of retired images, freed by the publishing thread.
+struct Graveyard {
+  std::mutex mu;
+  std::vector<uint8_t *> dead;
+};
+std::mutex g_grave_mu;
+std::map<int, std::unique_ptr<Graveyard>> g_grave;
+
+Graveyard &graveyard(int device) {
+  std::lock_guard<std::mutex> lk(g_grave_mu);
+  auto &p = g_grave[device];
+  if (!p) p.reset(new Graveyard());
+  return *p;
+}
+
+void bury(int device, uint8_t *p) {
+  Graveyard &gy = graveyard(device);
+  std::lock_guard<std::mutex> lk(gy.mu);
+  gy.dead.push_back(p);
+}
+
+// hipFree the retired images of `device` (publish / destroy only).
+void drain_graveyard(int device) {
+  std::vector<uint8_t *> dead;
+  {
+    Graveyard &gy = graveyard(device);
+    std::lock_guard<std::mutex> lk(gy.mu);
+    dead.swap(gy.dead);
+  }
+  if (dead.empty()) return;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(device);
+  for (uint8_t *p : dead) (void)hipFree(p);
+  (void)hipSetDevice(prev);
+}
+
 struct DevImage {
   int device = 0;
   uint8_t *dev = nullptr;
   dpd::Image im{};
   ~DevImage() {
-    if (dev) {
-      int prev = 0;
-      (void)hipGetDevice(&prev);
-      (void)hipSetDevice(device);
-      (void)hipFree(dev);
-      (void)hipSetDevice(prev);
-    }
+    if (dev) bury(device, dev);  // freed later, off the burst path
   }
 };
 
@@ -70,21 +111,80 @@ DeviceTables &dev_tables(int device) {
   return *p;
 }
 
+// One launched burst: the image it reads and its completion event.
+struct InFlight {
+  std::shared_ptr<DevImage> img;
+  hipEvent_t done = nullptr;
+};
+
+// DoneReason partial histograms: a small ring of buffers, one per launch.
+// A slot is reused only after the launch that used it (kernel + reduce) has
+// completed: the new launch's stream waits on the slot's event, so bursts on
+// different streams never share partial counters.
+constexpr int kPartSlots = 4;
+struct PartSlot {
+  uint64_t *part = nullptr;
+  hipEvent_t used = nullptr;
+  bool armed = false;
+};
+
 }  // namespace
 
 struct dp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  std::shared_ptr<DevImage> pinned;  // image used by the last burst
+  std::deque<InFlight> inflight;     // bursts not yet known complete
+  std::vector<hipEvent_t> spare;     // recycled completion events
+  PartSlot parts[kPartSlots];
+  int next_part = 0;
   // host-path staging
   uint8_t *d_buf = nullptr;
   uint64_t d_buf_cap = 0;
   dp_pkt_in_t *d_in = nullptr;
   dp_pkt_out_t *d_out = nullptr;
   uint64_t *d_stats = nullptr;
-  uint64_t *d_part = nullptr;        // partial DoneReason histograms (kernel side)
   uint32_t cap_n = 0;
 };
+
+namespace {
+
+// Drop the image references of bursts that have completed (non-blocking).
+void reap(dp_ctx *c) {
+  while (!c->inflight.empty()) {
+    InFlight &f = c->inflight.front();
+    if (f.done && hipEventQuery(f.done) == hipErrorNotReady) break;
+    if (f.done) c->spare.push_back(f.done);
+    c->inflight.pop_front();
+  }
+}
+
+hipEvent_t take_event(dp_ctx *c) {
+  if (!c->spare.empty()) {
+    hipEvent_t e = c->spare.back();
+    c->spare.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Every packet of a failed burst is InternalFailure (dpgpu.h conventions,
+// SURVEY.md §5 failure detection); host arrays.
+void mark_failed_host(const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n) {
+  if (!out) return;
+  for (uint32_t i = 0; i < n; i++) {
+    dp_pkt_out_t o{};
+    o.off = in ? in[i].off : 0;
+    o.len = in ? in[i].len : 0;
+    o.done = DP_DONE_INTERNAL_FAILURE;
+    o.fib_entry = 0xffffffffu;
+    o.acl_rule = 0xffffffffu;
+    out[i] = o;
+  }
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -106,8 +206,12 @@ int dp_ctx_create(int device_ordinal, dp_ctx_t **out) {
   if ((e = hipMalloc(&c->d_stats, sizeof(uint64_t) * DP_DONE_COUNT)) != hipSuccess)
     return fail(DP_ENOMEM, "hipMalloc stats", e);
   const size_t part_bytes = sizeof(uint64_t) * DP_DONE_COUNT * DPD_STAT_SLOTS;
-  if ((e = hipMalloc(&c->d_part, part_bytes)) != hipSuccess) return fail(DP_ENOMEM, "hipMalloc stats partials", e);
-  if ((e = hipMemset(c->d_part, 0, part_bytes)) != hipSuccess) return fail(DP_EIO, "clear stats partials", e);
+  for (auto &ps : c->parts) {
+    if ((e = hipMalloc(&ps.part, part_bytes)) != hipSuccess) return fail(DP_ENOMEM, "hipMalloc stats partials", e);
+    if ((e = hipMemset(ps.part, 0, part_bytes)) != hipSuccess) return fail(DP_EIO, "clear stats partials", e);
+    if ((e = hipEventCreateWithFlags(&ps.used, hipEventDisableTiming)) != hipSuccess)
+      return fail(DP_EIO, "hipEventCreate", e);
+  }
   *out = c.release();
   return 0;
 }
@@ -116,14 +220,26 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (!c) return DP_EINVAL;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  c->pinned.reset();
+  for (auto &f : c->inflight) {
+    if (f.done) {
+      (void)hipEventSynchronize(f.done);
+      (void)hipEventDestroy(f.done);
+    }
+  }
+  c->inflight.clear();
+  for (hipEvent_t e : c->spare) (void)hipEventDestroy(e);
+  for (auto &ps : c->parts) {
+    if (ps.used) { (void)hipEventSynchronize(ps.used); (void)hipEventDestroy(ps.used); }
+    if (ps.part) (void)hipFree(ps.part);
+  }
   if (c->d_buf) (void)hipFree(c->d_buf);
   if (c->d_in) (void)hipFree(c->d_in);
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_stats) (void)hipFree(c->d_stats);
-  if (c->d_part) (void)hipFree(c->d_part);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  const int dev = c->device;
   delete c;
+  drain_graveyard(dev);
   return 0;
 }
 
@@ -133,6 +249,7 @@ int dp_tables_publish(dp_ctx_t *c, const dp_tables_desc_t *tables) {
   int rc = dpd::build_image(tables, bi);
   if (rc) return fail(rc, "table compile rejected the descriptors");
   (void)hipSetDevice(c->device);
+  drain_graveyard(c->device);  // images no burst reads any more
   auto img = std::make_shared<DevImage>();
   img->device = c->device;
   hipError_t e = hipMalloc(&img->dev, bi.bytes.size());
@@ -147,7 +264,7 @@ int dp_tables_publish(dp_ctx_t *c, const dp_tables_desc_t *tables) {
     old = dt.cur;
     dt.cur = img;
   }
-  // `old` is freed here only if no context still pins it
+  // `old` is retired here only if no in-flight burst still references it
   return 0;
 }
 
@@ -176,13 +293,38 @@ int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
                             uint64_t *dev_stats, void *stream) {
   if (!c) return fail(DP_EINVAL, "null ctx");
   if (n == 0) return 0;
-  if (!dev_buf || !dev_in || !dev_out || ((uintptr_t)dev_buf & 15)) return fail(DP_EINVAL, "bad burst buffers");
-  auto img = current(c);
-  if (!img) return fail(DP_ENOTABLES, "no tables published");
+  if (!dev_in || !dev_out) return fail(DP_EINVAL, "null burst descriptors");
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  int rc = dpk_launch_pipeline(img->dev, &img->im, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, c->d_part, s);
-  if (rc) return fail(DP_EIO, "kernel launch failed", hipGetLastError());
-  c->pinned = img;
+  reap(c);
+  auto img = current(c);
+  if (!dev_buf || ((uintptr_t)dev_buf & 15) || !img) {
+    // whole-burst failure: every packet InternalFailure
+    (void)dpk_mark_failed(dev_in, dev_out, n, s);
+    return !img ? fail(DP_ENOTABLES, "no tables published") : fail(DP_EINVAL, "bad burst buffer");
+  }
+  uint64_t *part = nullptr;
+  PartSlot *ps = nullptr;
+  if (dev_stats) {
+    ps = &c->parts[c->next_part];
+    c->next_part = (c->next_part + 1) % kPartSlots;
+    if (ps->armed && hipStreamWaitEvent(s, ps->used, 0) != hipSuccess) return fail(DP_EIO, "stream wait");
+    part = ps->part;
+  }
+  int rc = dpk_launch_pipeline(img->dev, &img->im, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, part, s);
+  if (rc) {
+    hipError_t e = hipGetLastError();
+    (void)dpk_mark_failed(dev_in, dev_out, n, s);
+    return fail(DP_EIO, "kernel launch failed", e);
+  }
+  if (ps) {
+    (void)hipEventRecord(ps->used, s);
+    ps->armed = true;
+  }
+  InFlight f;
+  f.img = img;
+  f.done = take_event(c);
+  if (f.done) (void)hipEventRecord(f.done, s);
+  c->inflight.push_back(std::move(f));
   return 0;
 }
 
@@ -190,46 +332,164 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
                      dp_pkt_out_t *out, uint32_t n, uint64_t *stats) {
   if (!c) return fail(DP_EINVAL, "null ctx");
   if (n == 0) return 0;
-  if (!buf || !in || !out) return fail(DP_EINVAL, "null burst buffers");
+  if (!buf || !in || !out) {
+    mark_failed_host(in, out, n);
+    return fail(DP_EINVAL, "null burst buffers");
+  }
   for (uint32_t i = 0; i < n; i++)
-    if (in[i].off < DP_HEADROOM || (uint64_t)in[i].off + in[i].len > buf_bytes)
+    if (in[i].off < DP_HEADROOM || (uint64_t)in[i].off + in[i].len > buf_bytes) {
+      mark_failed_host(in, out, n);
       return fail(DP_EINVAL, "frame outside the burst buffer / headroom");
+    }
   (void)hipSetDevice(c->device);
   hipError_t e;
+  auto bail = [&](int rc, const char *what, hipError_t err) {
+    mark_failed_host(in, out, n);
+    return fail(rc, what, err);
+  };
   uint64_t need = ((buf_bytes + 15) & ~15ull) + 16;
   if (need > c->d_buf_cap) {
-    if (c->d_buf) (void)hipFree(c->d_buf);
+    if (c->d_buf) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->d_buf); }
     c->d_buf = nullptr;
-    if ((e = hipMalloc(&c->d_buf, need)) != hipSuccess) { c->d_buf_cap = 0; return fail(DP_ENOMEM, "hipMalloc burst", e); }
+    if ((e = hipMalloc(&c->d_buf, need)) != hipSuccess) { c->d_buf_cap = 0; return bail(DP_ENOMEM, "hipMalloc burst", e); }
     c->d_buf_cap = need;
   }
   if (n > c->cap_n) {
+    (void)hipStreamSynchronize(c->stream);
     if (c->d_in) (void)hipFree(c->d_in);
     if (c->d_out) (void)hipFree(c->d_out);
     c->d_in = nullptr; c->d_out = nullptr; c->cap_n = 0;
-    if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess) return fail(DP_ENOMEM, "hipMalloc in", e);
-    if ((e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess) return fail(DP_ENOMEM, "hipMalloc out", e);
+    if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess) return bail(DP_ENOMEM, "hipMalloc in", e);
+    if ((e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess) return bail(DP_ENOMEM, "hipMalloc out", e);
     c->cap_n = n;
   }
   hipStream_t s = c->stream;
-  if ((e = hipMemcpyAsync(c->d_buf, buf, buf_bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return fail(DP_EIO, "H2D burst", e);
-  if ((e = hipMemcpyAsync(c->d_in, in, sizeof(dp_pkt_in_t) * n, hipMemcpyHostToDevice, s)) != hipSuccess) return fail(DP_EIO, "H2D meta", e);
-  if (stats && (e = hipMemsetAsync(c->d_stats, 0, sizeof(uint64_t) * DP_DONE_COUNT, s)) != hipSuccess) return fail(DP_EIO, "memset stats", e);
+  if ((e = hipMemcpyAsync(c->d_buf, buf, buf_bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D burst", e);
+  if ((e = hipMemcpyAsync(c->d_in, in, sizeof(dp_pkt_in_t) * n, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D meta", e);
+  if (stats && (e = hipMemsetAsync(c->d_stats, 0, sizeof(uint64_t) * DP_DONE_COUNT, s)) != hipSuccess) return bail(DP_EIO, "memset stats", e);
   int rc = dp_process_burst_device(c, c->d_buf, need, c->d_in, c->d_out, n, stats ? c->d_stats : nullptr, s);
-  if (rc) return rc;
-  if ((e = hipMemcpyAsync(buf, c->d_buf, buf_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(DP_EIO, "D2H burst", e);
-  if ((e = hipMemcpyAsync(out, c->d_out, sizeof(dp_pkt_out_t) * n, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(DP_EIO, "D2H meta", e);
+  if (rc) {
+    (void)hipMemcpyAsync(out, c->d_out, sizeof(dp_pkt_out_t) * n, hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    mark_failed_host(in, out, n);
+    return rc;
+  }
+  if ((e = hipMemcpyAsync(buf, c->d_buf, buf_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H burst", e);
+  if ((e = hipMemcpyAsync(out, c->d_out, sizeof(dp_pkt_out_t) * n, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H meta", e);
   uint64_t hstats[DP_DONE_COUNT];
-  if (stats && (e = hipMemcpyAsync(hstats, c->d_stats, sizeof(hstats), hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(DP_EIO, "D2H stats", e);
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(DP_EIO, "stream sync", e);
+  if (stats && (e = hipMemcpyAsync(hstats, c->d_stats, sizeof(hstats), hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H stats", e);
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return bail(DP_EIO, "stream sync", e);
   if (stats) for (int k = 0; k < DP_DONE_COUNT; k++) stats[k] += hstats[k];
+  return 0;
+}
+
+int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf, uint64_t buf_bytes,
+                             const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, uint64_t *stats) {
+  if (!ctxs || n_ctx == 0) { mark_failed_host(in, out, n); return fail(DP_EINVAL, "no contexts"); }
+  if (n == 0) return 0;
+  if (!buf || !in || !out) { mark_failed_host(in, out, n); return fail(DP_EINVAL, "null burst buffers"); }
+  // packets in buffer order, each owning [off - DP_HEADROOM, off + len): the
+  // shards' byte spans are then disjoint and can be copied back concurrently
+  for (uint32_t i = 0; i < n; i++) {
+    const bool inside = in[i].off >= DP_HEADROOM && (uint64_t)in[i].off + in[i].len <= buf_bytes;
+    const bool ordered = i == 0 || in[i].off - DP_HEADROOM >= (uint64_t)in[i - 1].off + in[i - 1].len;
+    if (!inside || !ordered) {
+      mark_failed_host(in, out, n);
+      return fail(DP_EINVAL, "sharded bursts need in-order, non-overlapping packet slots");
+    }
+  }
+  for (uint32_t k = 0; k < n_ctx; k++)
+    if (!ctxs[k]) { mark_failed_host(in, out, n); return fail(DP_EINVAL, "null context"); }
+  struct Shard {
+    uint32_t first, cnt;
+    uint64_t lo, hi;               // byte span in `buf`
+    std::vector<dp_pkt_in_t> rin;  // in-records rebased to the span
+    uint64_t st[DP_DONE_COUNT];
+  };
+  std::vector<Shard> sh(n_ctx);
+  int rc = 0;
+  for (uint32_t k = 0; k < n_ctx; k++) {
+    Shard &S = sh[k];
+    S.first = (uint32_t)((uint64_t)n * k / n_ctx);
+    S.cnt = (uint32_t)((uint64_t)n * (k + 1) / n_ctx) - S.first;
+    if (!S.cnt) continue;
+    // 64-byte aligned start, never below the previous packet's end: the
+    // spans are disjoint, so the concurrent copies back never overlap
+    const uint64_t prev_end = S.first ? (uint64_t)in[S.first - 1].off + in[S.first - 1].len : 0;
+    S.lo = std::max<uint64_t>(prev_end, (in[S.first].off - DP_HEADROOM) & ~63ull);
+    const dp_pkt_in_t &last = in[S.first + S.cnt - 1];
+    S.hi = std::min<uint64_t>(buf_bytes, (uint64_t)last.off + last.len);
+    S.rin.assign(in + S.first, in + S.first + S.cnt);
+    for (auto &r : S.rin) r.off -= (uint32_t)S.lo;
+  }
+  // stage and launch every shard on its own device, then collect
+  std::vector<int> launched(n_ctx, 0);
+  for (uint32_t k = 0; k < n_ctx && !rc; k++) {
+    Shard &S = sh[k];
+    if (!S.cnt) continue;
+    dp_ctx *c = ctxs[k];
+    (void)hipSetDevice(c->device);
+    const uint64_t bytes = S.hi - S.lo;
+    const uint64_t need = ((bytes + 15) & ~15ull) + 16;
+    hipError_t e = hipSuccess;
+    if (need > c->d_buf_cap) {
+      if (c->d_buf) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->d_buf); }
+      c->d_buf = nullptr;
+      c->d_buf_cap = 0;
+      if ((e = hipMalloc(&c->d_buf, need)) != hipSuccess) { rc = fail(DP_ENOMEM, "hipMalloc shard", e); break; }
+      c->d_buf_cap = need;
+    }
+    if (S.cnt > c->cap_n) {
+      (void)hipStreamSynchronize(c->stream);
+      if (c->d_in) (void)hipFree(c->d_in);
+      if (c->d_out) (void)hipFree(c->d_out);
+      c->d_in = nullptr; c->d_out = nullptr; c->cap_n = 0;
+      if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * S.cnt)) != hipSuccess ||
+          (e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * S.cnt)) != hipSuccess) {
+        rc = fail(DP_ENOMEM, "hipMalloc shard records", e);
+        break;
+      }
+      c->cap_n = S.cnt;
+    }
+    hipStream_t s = c->stream;
+    if ((e = hipMemcpyAsync(c->d_buf, buf + S.lo, bytes, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->d_in, S.rin.data(), sizeof(dp_pkt_in_t) * S.cnt, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (stats && (e = hipMemsetAsync(c->d_stats, 0, sizeof(uint64_t) * DP_DONE_COUNT, s)) != hipSuccess)) {
+      rc = fail(DP_EIO, "H2D shard", e);
+      break;
+    }
+    if ((rc = dp_process_burst_device(c, c->d_buf, need, c->d_in, c->d_out, S.cnt, stats ? c->d_stats : nullptr, s)))
+      break;
+    if ((e = hipMemcpyAsync(buf + S.lo, c->d_buf, bytes, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(out + S.first, c->d_out, sizeof(dp_pkt_out_t) * S.cnt, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (stats && (e = hipMemcpyAsync(S.st, c->d_stats, sizeof(S.st), hipMemcpyDeviceToHost, s)) != hipSuccess)) {
+      rc = fail(DP_EIO, "D2H shard", e);
+      break;
+    }
+    launched[k] = 1;
+  }
+  for (uint32_t k = 0; k < n_ctx; k++) {
+    if (!launched[k]) continue;
+    (void)hipSetDevice(ctxs[k]->device);
+    hipError_t e = hipStreamSynchronize(ctxs[k]->stream);
+    if (e != hipSuccess && !rc) rc = fail(DP_EIO, "shard stream sync", e);
+  }
+  if (rc) { mark_failed_host(in, out, n); return rc; }
+  for (uint32_t k = 0; k < n_ctx; k++) {
+    Shard &S = sh[k];
+    for (uint32_t i = 0; i < S.cnt; i++) out[S.first + i].off += (uint32_t)S.lo;
+    if (stats && S.cnt)
+      for (int r = 0; r < DP_DONE_COUNT; r++) stats[r] += S.st[r];
+  }
   return 0;
 }
 
 int dp_ctx_synchronize(dp_ctx_t *c) {
   if (!c) return DP_EINVAL;
   hipError_t e = hipStreamSynchronize(c->stream);
-  return e == hipSuccess ? 0 : fail(DP_EIO, "stream sync", e);
+  if (e != hipSuccess) return fail(DP_EIO, "stream sync", e);
+  reap(c);
+  return 0;
 }
 
 }  // extern "C"

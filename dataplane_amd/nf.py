@@ -119,6 +119,21 @@ class GpuPathNf:
                                                  n, dev_stats, stream),
                 "dp_process_burst_device", self.lib)
 
+    @staticmethod
+    def process_sharded(nfs: List["GpuPathNf"], buf: np.ndarray, inp: np.ndarray,
+                        stats: Optional[np.ndarray] = None) -> np.ndarray:
+        """Host-origin burst split over several contexts / GPUs
+        (dp_process_burst_sharded): contiguous shards of whole packets, one
+        per context, copied and processed concurrently."""
+        out = np.zeros(len(inp), dtype=A.PKT_OUT)
+        ctxs = (C.c_void_p * len(nfs))(*[nf.ctx for nf in nfs])
+        lib = nfs[0].lib
+        sp = stats.ctypes.data if stats is not None else None
+        A.check(lib.dp_process_burst_sharded(ctxs, len(nfs), buf.ctypes.data, buf.nbytes,
+                                             inp.ctypes.data, out.ctypes.data, len(inp), sp),
+                "dp_process_burst_sharded", lib)
+        return out
+
     def synchronize(self) -> None:
         A.check(self.lib.dp_ctx_synchronize(self.ctx), "dp_ctx_synchronize", self.lib)
 

@@ -405,7 +405,9 @@ int64_t dp_tables_genid(const dp_ctx_t *ctx);
  * memory holding every frame at in[i].off with DP_HEADROOM bytes in front.
  * Frames are rewritten in place; out[i] tells where each serialized frame
  * now starts.  Synchronous.  `stats` (may be NULL) receives DP_DONE_COUNT
- * counters (PacketStatsNF, pipeline/src/sample_nfs.rs:225-273). */
+ * counters (PacketStatsNF, pipeline/src/sample_nfs.rs:225-273).  On any
+ * error (layout violation, HIP failure) every out[i] is
+ * DP_DONE_INTERNAL_FAILURE and the negative status is returned. */
 int dp_process_burst(dp_ctx_t *ctx, uint8_t *buf, uint64_t buf_bytes,
                      const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
                      uint64_t *stats);
@@ -415,11 +417,31 @@ int dp_process_burst(dp_ctx_t *ctx, uint8_t *buf, uint64_t buf_bytes,
  * `dev_buf` must be 16-byte aligned and `buf_bytes` must cover every frame
  * end rounded up to 16 bytes (frames are staged with 16-byte loads); a
  * packet violating the layout contract is marked DP_DONE_INTERNAL_FAILURE
- * without touching memory.  `dev_stats` (may be NULL) is accumulated into
- * (DP_DONE_COUNT u64). */
+ * without touching memory, and a burst that cannot run at all (no tables,
+ * misaligned buffer, launch failure) has every dev_out[i] marked
+ * DP_DONE_INTERNAL_FAILURE on `stream` besides the negative status.
+ * `dev_stats` (may be NULL) is accumulated into (DP_DONE_COUNT u64).
+ * Bursts of one context may run concurrently on different streams. */
 int dp_process_burst_device(dp_ctx_t *ctx, uint8_t *dev_buf, uint64_t buf_bytes,
                             const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out,
                             uint32_t n, uint64_t *dev_stats, void *stream);
+
+/* Multi-GPU, host-origin burst: `ctxs` holds one
+ * context per device (created by the caller, e.g. one per GPU of the node).
+ * The burst -- laid out as for dp_process_burst, with packets in buffer
+ * order and non-overlapping slots [off - DP_HEADROOM, off + len) -- is split
+ * into n_ctx contiguous shards of whole packets (shard k: packets
+ * [k n / n_ctx, (k+1) n / n_ctx)); each shard's byte span is copied to its
+ * device with its own hipMemcpyAsync (every GPU has its own PCIe link, no
+ * collective), processed there, and copied back.  Packets are independent,
+ * so the result equals dp_process_burst on one device bit for bit
+ * (tests/test_shard.py).  The analogue of the reference's per-worker fan-out
+ * (dataplane/src/drivers/kernel/fanout.rs:49-73, worker.rs:175).
+ * Synchronous; `stats` (may be NULL) receives the summed DoneReason counts.
+ * A whole-burst failure marks every packet DP_DONE_INTERNAL_FAILURE. */
+int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf,
+                             uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
+                             uint32_t n, uint64_t *stats);
 
 /* Wait for the context's stream. */
 int dp_ctx_synchronize(dp_ctx_t *ctx);

@@ -156,3 +156,66 @@ def test_gpu_golden_vectors(nf, name):
     b = z["buf_in"].copy()
     out = nf.process_arrays(b, z["inp"])
     compare(z["out"], z["buf_out"], out, b, z["inp"], f"golden {name} gpu")
+
+
+@pytest.mark.parametrize("layout", ["packed", "dpdk"])
+def test_gpu_sharded_matches_single(nf, layout):
+    """dp_process_burst_sharded over three contexts (one per GPU when the
+    box has them, else three streams of GPU 0) equals the oracle bit for bit,
+    with the DoneReason counts summed."""
+    import torch
+    ndev = torch.cuda.device_count()
+    w = Workload(2, 30001, seed=91, n_routes_v4=20000, n_acl=800, n_nat=32, tcp_percent=25,
+                 layout=layout)
+    nfs = [GpuPathNf(k % ndev) for k in range(3)]
+    try:
+        for x in nfs:
+            x.publish(w.tables)
+        b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
+        o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+        stats = np.zeros(A.DONE_COUNT, dtype=np.uint64)
+        o_dut = GpuPathNf.process_sharded(nfs, b_dut, w.inp, stats)
+        compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"sharded {layout}")
+        assert int(stats.sum()) == w.n
+        assert int(stats[A.DONE["Delivered"]]) == hist(o_ref).get("Delivered", 0)
+    finally:
+        for x in nfs:
+            x.close()
+
+
+def test_gpu_whole_burst_failure_marks_internal_failure(nf):
+    """A burst that cannot run marks every packet InternalFailure besides the
+    negative status (dpgpu.h conventions): host path with a frame outside the
+    buffer, sharded path with overlapping slots, device path with a
+    misaligned buffer."""
+    import ctypes as C
+    import torch
+    w = Workload(1, 256, seed=3)
+    nf.publish(w.tables)
+    lib = A.gpu_lib()
+    bad = w.inp.copy()
+    bad["off"][7] = w.buf.nbytes + 64
+    out = np.zeros(len(bad), dtype=A.PKT_OUT)
+    out["done"] = A.DONE["Delivered"]
+    b = w.fresh_buf()
+    rc = lib.dp_process_burst(nf.ctx, b.ctypes.data, b.nbytes, bad.ctypes.data, out.ctypes.data,
+                              len(bad), None)
+    assert rc < 0 and np.all(out["done"] == A.DONE["InternalFailure"])
+    ovl = w.inp.copy()
+    ovl["off"][5] = ovl["off"][4] + 8
+    out[:] = 0
+    out["done"] = A.DONE["Delivered"]
+    ctxs = (C.c_void_p * 1)(nf.ctx)
+    rc = lib.dp_process_burst_sharded(ctxs, 1, b.ctypes.data, b.nbytes, ovl.ctypes.data,
+                                      out.ctypes.data, len(ovl), None)
+    assert rc < 0 and np.all(out["done"] == A.DONE["InternalFailure"])
+    dev = torch.device("cuda", 0)
+    db = torch.from_numpy(w.fresh_buf()).to(dev)
+    di = torch.from_numpy(w.inp.view(np.uint8)).to(dev)
+    do = torch.full((w.n * A.PKT_OUT.itemsize,), 0x1f, dtype=torch.uint8, device=dev)
+    rc = lib.dp_process_burst_device(nf.ctx, db.data_ptr() + 1, db.numel() - 1, di.data_ptr(),
+                                     do.data_ptr(), w.n, None, None)
+    nf.synchronize()
+    o = do.cpu().numpy().view(A.PKT_OUT)
+    assert rc < 0 and np.all(o["done"] == A.DONE["InternalFailure"])
+    assert np.array_equal(o["off"], w.inp["off"])
