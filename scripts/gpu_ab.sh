@@ -1,14 +1,11 @@
-# A/B of library variants on C1/C2/C4 bench lines: LIBS="default lib/libdpgpu_w3.so"
+# Library A/B: bench each config in $CFGS with each library in $LIBS
+# (names under dataplane_amd/lib, "dpgpu" = the product build).
 set -o pipefail
 mkdir -p gpurun_out/ab
-export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/ab/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -30 gpurun_out/ab/pytest.log; exit 1; }
-echo PYTEST_OK
-for lib in ${LIBS:-default}; do
-  for c in ${CFGS:-2 1 4}; do
-    tag=$(basename $lib .so)_c$c
-    if [ "$lib" = default ]; then unset DPGPU_LIB; else export DPGPU_LIB=$PWD/dataplane_amd/$lib; fi
-    timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 5 --no-cpu --no-host > gpurun_out/ab/$tag.json 2> gpurun_out/ab/$tag.err || { echo BENCH_FAIL $tag; tail -5 gpurun_out/ab/$tag.err; exit 1; }
-    python -c "import json;d=json.load(open('gpurun_out/ab/$tag.json'));print('$tag', d['value'], d['roofline']['kernel_ms'])"
+for c in ${CFGS:-2 1}; do
+  for lib in ${LIBS:-dpgpu}; do
+    L=dataplane_amd/lib/lib$lib.so
+    DPGPU_LIB=$PWD/$L timeout -k 10 120 python bench.py --config $c --no-cpu --no-host > gpurun_out/ab/c${c}_$lib.json 2> gpurun_out/ab/c${c}_$lib.err || { echo FAIL $c $lib; tail -3 gpurun_out/ab/c${c}_$lib.err; exit 1; }
+    python -c "import json;d=json.load(open('gpurun_out/ab/c${c}_$lib.json'));print('C$c $lib', d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])"
   done
 done

@@ -136,6 +136,7 @@ def edge_tables() -> TablesBuilder:
     t.add_route(d, "10.135.0.0/16", t.add_nh([[TB.encap(2000, "100.65.0.8", "02:00:00:00:88:08")]]))
     t.add_route(d, "10.136.0.0/16", enc(2000, "100.65.0.9", oif=10, a="192.0.2.99"))
     t.add_route(d, "::/0", enc(2000, "100.65.0.2"))
+    t.add_route(d, "10.140.0.0/16", enc(2000, "100.65.0.10"))  # VPC 1010's NATed dsts
     t.add_route(d, "2001:db8:100::/48", eg(10, "2001:db8::1"))
     for vni in (2001, 2002, 2003, 2004, 2005):
         t.add_route(vpc[vni], "0.0.0.0/0", enc(vni, "100.65.0.2" if vni != 2001 else "2001:db8:9::2"))
@@ -211,6 +212,77 @@ def edge_tables() -> TablesBuilder:
                          1023, 1, 65535)]),
     ])
     t.add_nat_table(0, 1001, 0, [])
+    # ---- VPCs 1010 / 1011 take the kernel's fast overlay path (one peer
+    # only, and enough rules / NAT prefixes for multibit indexes)
+    vpc[1010] = t.add_fib(110, vtep_ip=VTEP4, vtep_mac=M1, vnis=[1010])
+    vpc[1011] = t.add_fib(111, vnis=[1011])
+    t.add_route(vpc[1010], "0.0.0.0/0", nh_drop)
+    t.add_route(vpc[1011], "0.0.0.0/0", nh_drop)
+    for v in (1010, 1011):
+        for k in range(24):
+            t.add_ff_remote(v, f"172.40.{k}.0/24", 2000, NAT_STATIC if k % 3 else NAT_NONE,
+                            proto=6 if k % 5 == 0 else None,
+                            dports=(80, 90) if k % 7 == 0 else (0, 65535))
+        t.add_ff_remote(v, "10.128.0.0/12", 2000)
+        t.add_ff_remote(v, "172.32.0.0/16", 2000, NAT_STATIC)
+        t.add_ff_remote(v, "::/0", 2000)
+        for k in range(20):
+            t.add_ff_local(v, 2000, f"10.20.{k}.0/24", NAT_STATIC if k % 4 != 3 else NAT_NONE,
+                           proto=17 if k % 6 == 0 else None,
+                           sports=(1000, 2000) if k % 5 == 0 else (0, 65535))
+    t.add_ff_remote(1010, "0.0.0.0/0", 2000)          # 1011: no default (misses filtered)
+    t.add_ff_local(1010, 2000, "10.0.0.0/16", NAT_STATIC)
+    t.add_ff_local(1010, 2000, "0.0.0.0/0", NAT_NONE)
+    t.add_ff_local(1010, 2000, "::/0", NAT_NONE)
+    for k in range(24):
+        # every rule names a destination (a /16 parent for k == 0): the
+        # per-interval candidate lists stay short, so the group takes the
+        # candidate-list form with a multibit dst index
+        kw = {"dst": "172.40.0.0/16" if k == 0 else
+              f"172.40.{k}.0/24" if k % 2 else f"172.40.{k}.128/25"}
+        if k % 3 == 0:
+            kw["src"] = f"10.20.{k}.0/24"
+        if k % 5 == 0:
+            kw["proto"] = 6 if k % 10 == 0 else 17
+        if k % 7 == 0:
+            kw["dports"] = (53, 53)
+        if k % 11 == 0:
+            kw["sports"] = (1000, 1999)
+        t.add_acl(1010, 2000, DENY if k % 3 == 1 else ALLOW, **kw)
+    t.add_acl(1010, 2000, ALLOW, dst="172.40.0.0/19")  # after the specific rules
+    t.add_acl_default(1010, 2000, DENY)               # 1011: no ACL at all
+    src_ents, dst_ents = [], []
+    for k in range(18):
+        if k == 4:
+            src_ents.append(dict(prefix=f"10.20.{k}.0/24", pat=True, port_ranges=[(1000, 1999)],
+                                 size=256 * 1000, ranges=[rng(f"10.20.{k}.0", f"10.20.{k}.255",
+                                                              "172.51.0.0", "172.51.3.255", 0,
+                                                              1000, 1999, 2000, 2249)]))
+        elif k == 5:
+            src_ents.append(dict(prefix=f"10.20.{k}.0/24", size=256,
+                                 ranges=[rng(f"10.20.{k}.0", f"10.20.{k}.255", "224.0.7.0",
+                                             "224.0.7.255")]))
+        elif k == 6:
+            src_ents.append(dict(prefix=f"10.20.{k}.0/24", size=256, ranges=[
+                rng(f"10.20.{k}.0", f"10.20.{k}.99", "172.52.0.0", "172.52.0.99", 0),
+                rng(f"10.20.{k}.100", f"10.20.{k}.255", "172.53.0.0", "172.53.0.155", 100)]))
+        else:
+            src_ents.append(dict(prefix=f"10.20.{k}.0/24", size=256,
+                                 ranges=[rng(f"10.20.{k}.0", f"10.20.{k}.255", f"172.50.{k}.0",
+                                             f"172.50.{k}.255")]))
+    src_ents.append(dict(prefix="10.20.0.0/16", size=65536, ranges=[
+        rng("10.20.0.0", "10.20.255.255", "172.54.0.0", "172.54.255.255")]))
+    for k in range(18):
+        if k == 2:
+            dst_ents.append(dict(prefix=f"172.40.{k}.0/24", pat=True, port_ranges=[(80, 90)], size=256 * 11,
+                                 ranges=[rng(f"172.40.{k}.0", f"172.40.{k}.255", "10.140.2.1",
+                                             "10.140.2.1", 0, 80, 90, 9000, 11815)]))
+        else:
+            dst_ents.append(dict(prefix=f"172.40.{k}.0/24", size=256,
+                                 ranges=[rng(f"172.40.{k}.0", f"172.40.{k}.255", f"10.140.{k}.0",
+                                             f"10.140.{k}.255")]))
+    t.add_nat_table(1, 1010, 2000, src_ents)
+    t.add_nat_table(0, 1010, 0, dst_ents)
     return t
 
 
@@ -231,11 +303,24 @@ OVERLAY_V4_DST = ["172.32.0.9", "172.32.1.7", "172.32.2.5", "172.32.3.5", "172.3
                   "172.33.4.4", "10.128.5.3", "10.128.7.1", "10.128.0.1", "10.129.0.5",
                   "10.129.1.5", "10.130.0.7", "10.131.0.1", "10.132.0.2", "10.133.0.1",
                   "10.134.0.1", "10.135.0.1", "10.136.0.1", "10.144.0.1", "10.145.0.1",
-                  "10.146.0.1", "10.147.0.1", "10.148.0.1", "10.200.0.1", "192.168.1.1"]
+                  "10.146.0.1", "10.147.0.1", "10.148.0.1", "10.200.0.1", "192.168.1.1",
+                  "172.40.0.9", "172.40.2.5", "172.40.3.9", "172.40.5.1", "172.40.7.1",
+                  "172.40.14.2", "172.40.21.7", "172.40.30.1", "10.140.9.9", "172.40.2.130",
+                  "172.40.40.1"]
 OVERLAY_V4_SRC = ["10.0.0.5", "10.0.1.200", "10.0.2.3", "10.0.3.9", "10.0.3.100", "10.0.77.7",
-                  "10.0.200.1", "10.1.2.3", "10.5.0.1", "10.9.9.9"]
+                  "10.0.200.1", "10.1.2.3", "10.5.0.1", "10.9.9.9", "10.20.1.5", "10.20.4.9",
+                  "10.20.5.5", "10.20.6.120", "10.20.6.7", "10.20.12.2", "10.20.18.2", "10.20.30.1",
+                  "10.20.4.77", "10.20.5.200", "10.20.4.1"]
 OVERLAY_V6_DST = ["2001:db8:100:5::1", "2001:db8:100:6::1", "2001:db8:1ff::1", "2001:db8:9999::1"]
 OVERLAY_V6_SRC = ["2001:db8:aa::1", "2001:db8:bb::2"]
+FAST_V4_SRC = ["10.20.1.5", "10.20.2.9", "10.20.3.3", "10.20.4.9", "10.20.4.77", "10.20.5.5",
+               "10.20.5.200", "10.20.6.7", "10.20.6.120", "10.20.12.2", "10.20.17.1",
+               "10.20.18.2", "10.20.30.1", "10.0.7.7", "10.9.9.9"]
+FAST_V4_DST = ["172.40.0.9", "172.40.1.1", "172.40.2.5", "172.40.2.130", "172.40.3.9",
+               "172.40.4.4", "172.40.5.1", "172.40.7.1", "172.40.14.2", "172.40.17.3",
+               "172.40.21.7", "172.40.30.1", "172.40.40.1", "10.140.9.9", "172.32.3.3",
+               "10.129.0.5", "192.168.1.1"]
+FAST_PORTS = [53, 79, 80, 85, 90, 91, 443, 999, 1000, 1500, 1999, 2000, 2001, 8080]
 PORTS = [1, 7, 8, 53, 80, 85, 99, 100, 443, 999, 1000, 1500, 1999, 2000, 2001, 4789, 8080,
          65535]
 
@@ -324,7 +409,7 @@ def _ip6_packet(r, src, dst):
 
 def _vxlan_frame(r, inner_frame):
     """Outer IPv4/UDP/VXLAN to the local VTEP carrying ``inner_frame``."""
-    vni = _pick(r, [1000, 1000, 1001, 1002, 2000, 999, 0])
+    vni = _pick(r, [1000, 1000, 1001, 1002, 2000, 999, 0, 1010, 1010, 1011])
     flags = 0x08 if r.random() < 0.9 else _pick(r, [0x00, 0x0C, 0x88])
     r1 = b"\0\0\0" if r.random() < 0.95 else b"\0\x01\0"
     vx = P.vxlan(vni, flags, r1, 0 if r.random() < 0.95 else 1)
@@ -388,7 +473,8 @@ def edge_frames(n: int, seed: int):
             f = _vxlan_frame(r, _inner_frame(r))
         elif kind < 0.95:                            # seeded overlay (post-decap inner frame)
             f = _inner_frame(r)
-            flags, svni = A.IN_SEEDED_OVERLAY, _pick(r, [1000, 1000, 1000, 1001, 1002, 2000, 999])
+            flags, svni = A.IN_SEEDED_OVERLAY, _pick(r, [1000, 1000, 1000, 1001, 1002, 2000, 999,
+                                                         1010, 1010, 1010, 1011])
         else:                                        # non-IP / garbage
             f = P.l2(M1, PEER, _pick(r, [0x0806, 0x88cc, 0x8100])) + bytes(r.randrange(0, 60))
         f = bytearray(f)
@@ -397,6 +483,23 @@ def edge_frames(n: int, seed: int):
         if r.random() < 0.15:                        # Ethernet padding / trailing bytes
             f += bytes(r.randrange(1, 20))
         out.append((bytes(f[:65535]), iif, flags, svni))
+    # VPCs 1010 / 1011 (the fast overlay path): every NAT / PAT / ACL corner,
+    # enumerated rather than left to the draw above
+    for _ in range(600):
+        src = _pick(r, FAST_V4_SRC)
+        dst = _pick(r, FAST_V4_DST)
+        proto = _pick(r, [6, 6, 17, 17, 1])
+        pay = _payload(r)
+        if proto == 1:
+            body = _l4_v4(r, 1, src, dst, pay)
+        else:
+            sp, dp = _pick(r, FAST_PORTS), _pick(r, FAST_PORTS)
+            body = (P.tcp(sp, dp, pay, P.pseudo4(src, dst, 6, 20 + len(pay))) if proto == 6 else
+                    P.udp(sp, dp, pay, P.pseudo4(src, dst, 17, 8 + len(pay))))
+        ip = P.ipv4(src, dst, proto, len(body), ttl=_pick(r, [64, 64, 64, 1]),
+                    ident=r.randrange(65536))
+        f = P.l2("02:00:00:00:aa:01", "02:00:00:00:bb:01", 0x0800) + ip + body
+        out.append((f, 1, A.IN_SEEDED_OVERLAY, _pick(r, [1010, 1010, 1010, 1011])))
     return out
 
 
