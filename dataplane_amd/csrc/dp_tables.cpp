@@ -16,6 +16,7 @@
 #include "dp_tables.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <cstddef>
@@ -291,18 +292,14 @@ void build_field_index(ImgBuf &ib, FieldIdx &F, int f, int fam, size_t ngroups,
 constexpr uint32_t kListMax = 24;
 constexpr double kListMean = 6.0;
 
-// Test knob: DPGPU_CLS_FORM=bv forces the bit-vector form, =list takes the
-// list form whenever the runs fit (<= DPD_RUN_MAX); unset/auto: limits above.
+// Classifier form override for the parity tests (dpd_debug_set_classifier_form):
+// 1 forces the bit-vector form, 2 takes the list form whenever the runs fit
+// (<= DPD_RUN_MAX); 0 (the default): the limits above.
 // forms chosen by the most recent build on this thread (test introspection)
 thread_local uint32_t g_forms[2];
+std::atomic<int> g_cls_form{0};
 
-int cls_form_override() {
-  const char *e = getenv("DPGPU_CLS_FORM");
-  if (!e) return 0;
-  if (!strcmp(e, "bv")) return 1;
-  if (!strcmp(e, "list")) return 2;
-  return 0;
-}
+int cls_form_override() { return g_cls_form.load(std::memory_order_relaxed); }
 
 // `gkv_out`: group keys -> group index; `order_out`: rules in global rule
 // index order (the order of the action arrays); `aux_patch`: image offsets
@@ -1095,6 +1092,12 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
 
 // Test introspection: classifier groups built in bit-vector ([0]) and
 // candidate-list ([1]) form by the last image build on the calling thread.
+// Test hook: classifier form for later image builds in this process (0 auto,
+// 1 bit-vector, 2 candidate list).  Not part of the product ABI (dpgpu.h).
+extern "C" void dpd_debug_set_classifier_form(int form) {
+  dpd::g_cls_form.store(form >= 0 && form <= 2 ? form : 0, std::memory_order_relaxed);
+}
+
 extern "C" void dpd_debug_classifier_forms(uint32_t out[2]) {
   out[0] = dpd::g_forms[0];
   out[1] = dpd::g_forms[1];

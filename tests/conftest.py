@@ -13,3 +13,21 @@ if EMU not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
+
+
+CLS_FORMS = {"auto": 0, "bv": 1, "list": 2}
+
+
+@pytest.fixture
+def cls_form():
+    """cls_form(lib, "bv" | "list" | "auto"): classifier form for the image
+    builds of `lib` (dpd_debug_set_classifier_form); reset after the test."""
+    used = []
+
+    def set_form(lib, form):
+        lib.dpd_debug_set_classifier_form(CLS_FORMS[form])
+        used.append(lib)
+
+    yield set_form
+    for lib in used:
+        lib.dpd_debug_set_classifier_form(0)

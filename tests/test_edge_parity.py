@@ -20,8 +20,8 @@ def tables():
 
 @pytest.mark.parametrize("form", ["auto", "bv", "list"])
 @pytest.mark.parametrize("seed", [1, 2, 3, 4])
-def test_edge_emu_matches_oracle(tables, seed, form, monkeypatch):
-    monkeypatch.setenv("DPGPU_CLS_FORM", form)
+def test_edge_emu_matches_oracle(tables, seed, form, cls_form):
+    cls_form(pyemu.lib(), form)
     _, tp = tables
     frames = edge_frames(4000, seed)
     buf, inp = pack_burst(frames)

@@ -14,8 +14,8 @@ from helpers import compare
 @pytest.mark.parametrize("form,layout", [("auto", "packed"), ("bv", "packed"), ("list", "packed"),
                                          ("auto", "dpdk")])
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
-def test_emu_matches_oracle(cfg, form, layout, monkeypatch):
-    monkeypatch.setenv("DPGPU_CLS_FORM", form)
+def test_emu_matches_oracle(cfg, form, layout, cls_form):
+    cls_form(pyemu.lib(), form)
     w = Workload(cfg, 3000, seed=100 + cfg, n_routes_v4=3000, n_routes_v6=1500, n_acl=400,
                  n_nat=48, tcp_percent=25, layout=layout)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()

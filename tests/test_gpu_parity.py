@@ -29,10 +29,10 @@ CASES = [(f, "packed") for f in ("auto", "bv", "list")] + [("auto", "dpdk")]
 
 @pytest.mark.parametrize("form,layout", CASES)
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
-def test_gpu_matches_oracle(nf, cfg, form, layout, monkeypatch):
-    """Classifiers built in each form (DPGPU_CLS_FORM, read at publish), in
+def test_gpu_matches_oracle(nf, cfg, form, layout, cls_form):
+    """Classifiers built in each form (dpd_debug_set_classifier_form, read at publish), in
     the packed layout and in the DPDK mbuf layout bench.py times."""
-    monkeypatch.setenv("DPGPU_CLS_FORM", form)
+    cls_form(A.gpu_lib(), form)
     w = Workload(cfg, 20000, seed=200 + cfg, n_routes_v4=20000, n_routes_v6=8000, n_acl=1000,
                  n_nat=64, tcp_percent=25, layout=layout)
     nf.publish(w.tables)
@@ -53,10 +53,10 @@ def edge():
 
 
 @pytest.mark.parametrize("seed", [11, 12, 13, 14, 15, 16])
-def test_gpu_edge_corpus(nf, edge, seed, monkeypatch):
+def test_gpu_edge_corpus(nf, edge, seed, cls_form):
     """Malformed / boundary frames and every table branch (tests/edgecase.py);
     odd seeds with bit-vector classifiers, even seeds with candidate lists."""
-    monkeypatch.setenv("DPGPU_CLS_FORM", "bv" if seed % 2 else "list")
+    cls_form(A.gpu_lib(), "bv" if seed % 2 else "list")
     _, tp = edge
     nf.publish(tp)
     buf, inp = pack_burst(edge_frames(20000, seed))
