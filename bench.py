@@ -49,28 +49,90 @@ def measured_traffic(cfg: int, n: int):
     return int(t["bytes_per_pkt"] * n), t["source"]
 
 
-def cpu_baseline(w: Workload, sample: int, budget_s: float) -> dict:
-    """The CPU oracle (C++ restatement of the reference pipeline) on this
-    host's cores, DPDK-sized bursts of 64, on a bounded sample."""
-    from oracle.pyoracle import Oracle  # test-infrastructure checker, timed as the baseline
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    o = Oracle(w.tables)
-    n = min(sample, w.n)
-    inp = w.inp[:n].copy()
-    out = np.zeros(n, dtype=A.PKT_OUT)
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: one per CPU this process may run
+    on, capped at the GPU box's per-GPU CPU share (16; the box's nproc shows
+    the whole machine)."""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _time_cpu(run, n: int, budget_s: float, max_reps: int) -> tuple:
+    """Repeat run() (which returns its own seconds for n packets) until the
+    budget is spent; (Mpps, reps, seconds)."""
     done, t_total, reps = 0, 0.0, 0
-    while t_total < budget_s and reps < 50:
-        buf = w.fresh_buf()
-        t0 = time.perf_counter()
-        o.process_parallel(buf, inp, out, threads=threads, burst=64)
-        t_total += time.perf_counter() - t0
+    while t_total < budget_s and reps < max_reps:
+        t_total += run()
         done += n
         reps += 1
+    return done / t_total / 1e6, reps, t_total
+
+
+def cpu_baseline(w: Workload, sample: int, budget_s: float) -> dict:
+    """Two CPU legs on this host, DPDK-sized bursts of 64, bounded samples:
+      - "port" (the reported value): the oracle (oracle/), the C++
+        restatement of the reference pipeline (linear-scan classifiers,
+        binary-trie LPM, like the reference's own reference implementations),
+        on cpu_threads() threads and on 1;
+      - "compiled": the kernel's per-packet body built for the host
+        (tests/emu, -O3) over the same compiled table image (Poptrie LPM,
+        candidate-list classifiers), on the same thread counts."""
+    from oracle.pyoracle import Oracle  # test-infrastructure checker, timed as the baseline
+    sys.path.insert(0, os.path.join(ROOT, "tests", "emu"))
+    import pyemu  # test infrastructure (host build of the kernel body)
+    threads = cpu_threads()
+    o = Oracle(w.tables)
+
+    def oracle_run(m, th):
+        inp, out = w.inp[:m].copy(), np.zeros(m, dtype=A.PKT_OUT)
+
+        def run():
+            buf = w.fresh_buf()
+            t0 = time.perf_counter()
+            o.process_parallel(buf, inp, out, threads=th, burst=64)
+            return time.perf_counter() - t0
+        return run
+    n = min(sample, w.n)
+    n1 = max(64, n // 8)
+    port_n, reps, t_port = _time_cpu(oracle_run(n, threads), n, budget_s, 50)
+    port_1, _, _ = _time_cpu(oracle_run(n1, 1), n1, budget_s / 4, 3)
     o.close()
-    return {"value": round(done / t_total / 1e6, 4), "unit": "Mpps", "cores": threads,
-            "kind": "port",
-            "sample": f"{reps} x {n} packets of the same workload, bursts of 64, "
-                      f"C++ restatement of the reference pipeline (oracle/), {t_total:.1f} s"}
+
+    emu = pyemu.ParallelEmu(w.tables)
+    ebuf = pyemu.aligned_copy(w.buf)
+
+    def emu_run(m, th):
+        inp, out = w.inp[:m].copy(), np.zeros(m, dtype=A.PKT_OUT)
+
+        def run():
+            ebuf[:w.buf.nbytes] = w.buf
+            t0 = time.perf_counter()
+            emu.run(ebuf, w.buf.nbytes, inp, out, threads=th, burst=64)
+            return time.perf_counter() - t0
+        return run
+    ne = min(w.n, 8 * n)
+    emu_n, ereps, t_emu = _time_cpu(emu_run(ne, threads), ne, budget_s / 2, 20)
+    emu_1, _, _ = _time_cpu(emu_run(ne // 8, 1), ne // 8, budget_s / 4, 3)
+    emu.close()
+    return {"value": round(port_n, 4), "unit": "Mpps", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "value_1_thread": round(port_1, 4),
+            "sample": f"{reps} x {n} packets of the same workload, bursts of 64, C++ restatement "
+                      f"of the reference pipeline (oracle/), {t_port:.1f} s on {threads} threads "
+                      f"(the box's per-GPU CPU share); value_1_thread over {n1} packets",
+            "compiled": {"value": round(emu_n, 3), "unit": "Mpps", "cores": threads,
+                         "value_1_thread": round(emu_1, 3),
+                         "what": "the kernel's per-packet body compiled for the host (tests/emu, "
+                                 "-O3) over the same table image (Poptrie LPM, candidate lists)",
+                         "sample": f"{ereps} x {ne} packets, {t_emu:.1f} s"}}
 
 
 def main() -> None:
@@ -144,19 +206,39 @@ def main() -> None:
         step(k)
     torch.cuda.synchronize(dev)
     dstats.zero_()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    # one event per step boundary, on the launch stream: per-step durations
+    # (median) besides the whole timed region
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    ev0.record(stream)
+    evs[0].record(stream)
     for k in range(args.steps):
         step(args.warmup + k)
-    ev1.record(stream)
+        evs[k + 1].record(stream)
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t_start
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    step_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
+    kernel_ms = evs[0].elapsed_time(evs[-1]) / args.steps
+
+    # roofline timing of dp_pipeline_kernel alone (no histogram, so no
+    # dp_stats_reduce launch): one event pair per launch, re-using the
+    # processed buffers' pristine copies
+    for k in range(nbuf):
+        bufs[k, :w.buf.nbytes].copy_(pristine)
+    torch.cuda.synchronize(dev)
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    for k in range(args.steps):
+        kev[k][0].record(stream)
+        nf.process_device(bufs[args.warmup + k].data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n,
+                          None, sptr)
+        kev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    launch_ms = sorted(a.elapsed_time(b) for a, b in kev)
+    pipe_ms_median = launch_ms[len(launch_ms) // 2]
+    pipe_ms_mean = sum(launch_ms) / len(launch_ms)
 
     elapsed, hist = reduce_over_ranks(elapsed, dstats.cpu().numpy(), dev)
 
@@ -169,11 +251,15 @@ def main() -> None:
 
     result = None
     if rank == 0:
-        achieved = n * ALGO_BYTES[cfg] / (kernel_ms / 1e3) / 1e9
+        achieved = n * ALGO_BYTES[cfg] / (pipe_ms_mean / 1e3) / 1e9
         traffic, traffic_src = measured_traffic(cfg, n)
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "kernel": "dp_pipeline_kernel", "kernel_ms": round(kernel_ms, 4),
+                    "kernel": "dp_pipeline_kernel", "kernel_ms": round(pipe_ms_mean, 4),
+                    "kernel_ms_median": round(pipe_ms_median, 4),
+                    "kernel_timing": f"HIP events around each of {args.steps} launches on the "
+                                     "launch stream (achieved uses the mean, as rocprof's "
+                                     "AverageNs)",
                     "bytes_per_pkt": ALGO_BYTES[cfg]}
         if traffic is not None:
             roofline["traffic_unit"] = "bytes per launch"
@@ -190,22 +276,38 @@ def main() -> None:
                                            routes_v6=args.routes_v6, acl=args.acl,
                                            nat=args.nat).items() if v},
                        "parallelism": f"dp{world} (independent shards)"},
+            "step_ms_median": round(sorted(step_ms)[len(step_ms) // 2], 4),
+            "step_ms_events_mean": round(kernel_ms, 4),
+            "mpps_median_step": round(world * n / (sorted(step_ms)[len(step_ms) // 2] / 1e3) / 1e6, 3),
             "roofline": roofline,
             "done_histogram": {A.DONE_NAMES[i]: int(c) for i, c in enumerate(hist) if c},
         }
         if world == 1 and not args.no_host:
-            # host-origin rate: pinned host buffers, H2D + kernel + D2H per burst
-            pinned = torch.empty(w.buf.nbytes, dtype=torch.uint8).pin_memory()
-            pnp = pinned.numpy()
-            reps, t_host = 3, 0.0
-            for _ in range(reps + 1):
+            # host-origin rate (dp_process_burst): pinned host burst buffer and
+            # records, chunked H2D / kernel / D2H overlapped on several streams
+            def pinned(nbytes):
+                return torch.empty(nbytes, dtype=torch.uint8).pin_memory().numpy()
+            pnp = pinned(w.buf.nbytes)
+            pin_in = pinned(w.inp.nbytes).view(A.PKT_IN)
+            pin_in[:] = w.inp
+            pin_out = pinned(n * A.PKT_OUT.itemsize).view(A.PKT_OUT)
+            reps, t_host = 5, []
+            for r in range(reps + 1):
                 pnp[:] = w.buf
                 t0 = time.perf_counter()
-                nf.process_arrays(pnp, w.inp)
-                dt = time.perf_counter() - t0
-                if _ > 0:
-                    t_host += dt
-            result["host_inclusive_mpps"] = round(reps * n / t_host / 1e6, 3)
+                nf.process_arrays(pnp, pin_in, out=pin_out)
+                if r > 0:
+                    t_host.append(time.perf_counter() - t0)
+            th = sorted(t_host)[len(t_host) // 2]
+            pcie_bytes = 2 * w.buf.nbytes + n * (A.PKT_IN.itemsize + A.PKT_OUT.itemsize)
+            result["host_inclusive_mpps"] = round(n / th / 1e6, 3)
+            result["host_inclusive"] = {
+                "mpps_median": round(n / th / 1e6, 3), "runs": reps,
+                "pcie_bytes_per_burst": pcie_bytes,
+                "pcie_gbs": round(pcie_bytes / th / 1e9, 2),
+                "what": "dp_process_burst on pinned host buffers: the burst's slot spans "
+                        "(headroom + frame) and records H2D, kernel, D2H, in chunks of 64K+ "
+                        "packets on 3 streams"}
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(w, args.cpu_sample, args.cpu_budget)
         print(json.dumps(result), flush=True)

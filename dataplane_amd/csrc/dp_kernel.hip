@@ -1919,8 +1919,8 @@ __global__ void __launch_bounds__(DPD_STAT_SLOTS) dp_stats_reduce(unsigned long 
 // Host emulation entry (tests/emu only): runs the per-packet body serially.
 extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
                           uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n) {
-  static uint8_t slab[SLAB + 16];
-  static uint8_t hs[64];
+  thread_local uint8_t slab[SLAB + 16];
+  thread_local uint8_t hs[64];
   Img g{img_base, *reinterpret_cast<const Image *>(image_struct)};
   for (uint32_t i = 0; i < n; i++) {
     const int nch = frame_ok(in[i], buf_bytes) ? window_chunks(in[i]) : 0;

@@ -122,6 +122,13 @@ struct InFlight {
 // completed: the new launch's stream waits on the slot's event, so bursts on
 // different streams never share partial counters.
 constexpr int kPartSlots = 4;
+
+// Host-origin bursts are moved in chunks of at least kHostChunk packets on
+// kHostStreams streams, so one chunk's device-to-host copy, the next one's
+// kernel and the one after's host-to-device copy overlap (PCIe is full
+// duplex).
+constexpr uint32_t kHostChunk = 65536;
+constexpr int kHostStreams = 3;
 struct PartSlot {
   uint64_t *part = nullptr;
   hipEvent_t used = nullptr;
@@ -144,6 +151,9 @@ struct dp_ctx {
   dp_pkt_out_t *d_out = nullptr;
   uint64_t *d_stats = nullptr;
   uint32_t cap_n = 0;
+  hipStream_t hs[kHostStreams] = {};   // host-path copy/compute streams
+  hipEvent_t hev[kHostStreams + 1] = {};
+  bool host_streams = false;
 };
 
 namespace {
@@ -236,6 +246,8 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->d_in) (void)hipFree(c->d_in);
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_stats) (void)hipFree(c->d_stats);
+  for (auto &h : c->hs) if (h) { (void)hipStreamSynchronize(h); (void)hipStreamDestroy(h); }
+  for (auto &e : c->hev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   const int dev = c->device;
   delete c;
@@ -364,18 +376,74 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     c->cap_n = n;
   }
   hipStream_t s = c->stream;
-  if ((e = hipMemcpyAsync(c->d_buf, buf, buf_bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D burst", e);
-  if ((e = hipMemcpyAsync(c->d_in, in, sizeof(dp_pkt_in_t) * n, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D meta", e);
-  if (stats && (e = hipMemsetAsync(c->d_stats, 0, sizeof(uint64_t) * DP_DONE_COUNT, s)) != hipSuccess) return bail(DP_EIO, "memset stats", e);
-  int rc = dp_process_burst_device(c, c->d_buf, need, c->d_in, c->d_out, n, stats ? c->d_stats : nullptr, s);
-  if (rc) {
-    (void)hipMemcpyAsync(out, c->d_out, sizeof(dp_pkt_out_t) * n, hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-    mark_failed_host(in, out, n);
-    return rc;
+  // packets in buffer order with disjoint slots: chunked, overlapped copies
+  // of each chunk's own byte span; anything else: one whole-buffer copy
+  bool ordered = true;
+  for (uint32_t i = 1; i < n && ordered; i++)
+    ordered = in[i].off - DP_HEADROOM >= (uint64_t)in[i - 1].off + in[i - 1].len;
+  const uint32_t nch = ordered ? std::max<uint32_t>(1, std::min<uint32_t>(n / kHostChunk, 256)) : 1;
+  if (nch > 1 && !c->host_streams) {
+    for (int k = 0; k < kHostStreams; k++)
+      if ((e = hipStreamCreateWithFlags(&c->hs[k], hipStreamNonBlocking)) != hipSuccess)
+        return bail(DP_EIO, "hipStreamCreate (host path)", e);
+    for (auto &ev : c->hev)
+      if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess)
+        return bail(DP_EIO, "hipEventCreate (host path)", e);
+    c->host_streams = true;
   }
-  if ((e = hipMemcpyAsync(buf, c->d_buf, buf_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H burst", e);
-  if ((e = hipMemcpyAsync(out, c->d_out, sizeof(dp_pkt_out_t) * n, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H meta", e);
+  if (stats && (e = hipMemsetAsync(c->d_stats, 0, sizeof(uint64_t) * DP_DONE_COUNT, s)) != hipSuccess)
+    return bail(DP_EIO, "memset stats", e);
+  if (nch == 1) {
+    if ((e = hipMemcpyAsync(c->d_buf, buf, buf_bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D burst", e);
+    if ((e = hipMemcpyAsync(c->d_in, in, sizeof(dp_pkt_in_t) * n, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D meta", e);
+    int rc = dp_process_burst_device(c, c->d_buf, need, c->d_in, c->d_out, n, stats ? c->d_stats : nullptr, s);
+    if (rc) {
+      (void)hipStreamSynchronize(s);
+      mark_failed_host(in, out, n);
+      return rc;
+    }
+    if ((e = hipMemcpyAsync(buf, c->d_buf, buf_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H burst", e);
+    if ((e = hipMemcpyAsync(out, c->d_out, sizeof(dp_pkt_out_t) * n, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H meta", e);
+  } else {
+    // every host stream starts after the context stream's prior work (and
+    // the stats clear); the context stream then waits for all of them
+    if ((e = hipEventRecord(c->hev[kHostStreams], s)) != hipSuccess) return bail(DP_EIO, "event record", e);
+    for (int k = 0; k < kHostStreams; k++)
+      if ((e = hipStreamWaitEvent(c->hs[k], c->hev[kHostStreams], 0)) != hipSuccess) return bail(DP_EIO, "stream wait", e);
+    int rc = 0;
+    for (uint32_t k = 0; k < nch && !rc; k++) {
+      const uint32_t first = (uint32_t)((uint64_t)n * k / nch);
+      const uint32_t cnt = (uint32_t)((uint64_t)n * (k + 1) / nch) - first;
+      // byte span [lo, hi) of the chunk: from its first packet's headroom (16-aligned, never
+      // below the previous packet's end) to its last frame's end -- disjoint across chunks
+      const uint64_t prev_end = first ? (uint64_t)in[first - 1].off + in[first - 1].len : 0;
+      const uint64_t lo = std::max<uint64_t>(prev_end, (in[first].off - DP_HEADROOM) & ~15ull);
+      const uint64_t hi = (uint64_t)in[first + cnt - 1].off + in[first + cnt - 1].len;
+      hipStream_t hs = c->hs[k % kHostStreams];
+      if ((e = hipMemcpyAsync(c->d_buf + lo, buf + lo, hi - lo, hipMemcpyHostToDevice, hs)) != hipSuccess ||
+          (e = hipMemcpyAsync(c->d_in + first, in + first, sizeof(dp_pkt_in_t) * cnt, hipMemcpyHostToDevice, hs)) != hipSuccess) {
+        rc = fail(DP_EIO, "H2D chunk", e);
+        break;
+      }
+      if ((rc = dp_process_burst_device(c, c->d_buf, need, c->d_in + first, c->d_out + first, cnt,
+                                        stats ? c->d_stats : nullptr, hs)))
+        break;
+      if ((e = hipMemcpyAsync(buf + lo, c->d_buf + lo, hi - lo, hipMemcpyDeviceToHost, hs)) != hipSuccess ||
+          (e = hipMemcpyAsync(out + first, c->d_out + first, sizeof(dp_pkt_out_t) * cnt, hipMemcpyDeviceToHost, hs)) != hipSuccess) {
+        rc = fail(DP_EIO, "D2H chunk", e);
+        break;
+      }
+    }
+    for (int k = 0; k < kHostStreams; k++) {
+      (void)hipEventRecord(c->hev[k], c->hs[k]);
+      (void)hipStreamWaitEvent(s, c->hev[k], 0);
+    }
+    if (rc) {
+      (void)hipStreamSynchronize(s);
+      mark_failed_host(in, out, n);
+      return rc;
+    }
+  }
   uint64_t hstats[DP_DONE_COUNT];
   if (stats && (e = hipMemcpyAsync(hstats, c->d_stats, sizeof(hstats), hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H stats", e);
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return bail(DP_EIO, "stream sync", e);

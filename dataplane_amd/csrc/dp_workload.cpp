@@ -322,6 +322,11 @@ int dpw_build(const dpw_config_t *c, dpw_workload_t **out) {
   // src VPC k (VNI 1000+k) peers with the dst VPC (VNI 2000).
   // private space of VPC k: 10.(16k..16k+15).0.0/12-ish; NAT publics 172.16/12
   std::vector<uint32_t> src_nat_priv, src_nat_pub, dst_nat_pub, dst_nat_priv;
+  // every 4th source-NAT map is PAT (ports kPatPortLo..65535)
+  const uint16_t kPatPortLo = 1024;
+  auto is_pat = [](uint32_t k) { return (k & 3) == 3; };
+  // per v4 ACL rule: the NAT /24 its src / dst prefix was built over (0: none)
+  std::vector<std::array<uint32_t, 2>> acl_anchor;
   if (overlay) {
     for (uint32_t k = 0; k < n_nat; k++) {
       src_nat_priv.push_back(0x0a000000u | ((k % 240u) << 16) | ((k / 240u) << 8));   // 10.x.y.0/24
@@ -342,8 +347,11 @@ int dpw_build(const dpw_config_t *c, dpw_workload_t **out) {
         r.action2 = DP_NAT_STATIC;
         w.ffr4.push_back(r);
       }
+      // the peer's routed space 10/8 (not a wildcard: other destinations miss
+      // the remote stage and are Filtered)
       dp_rule_t d = wildcard_rule(4);
-      d.vni_a = svni; d.priority = (0 + 1) << 1; d.action = kDstVni; d.action2 = DP_NAT_NONE;
+      d.vni_a = svni; d.dst = pfx4(0x0a000000u, 8); d.priority = (8 + 1) << 1;
+      d.action = kDstVni; d.action2 = DP_NAT_NONE;
       w.ffr4.push_back(d);
       dp_rule_t d6 = wildcard_rule(6);
       d6.vni_a = svni; d6.priority = (0 + 1) << 1; d6.action = kDstVni; d6.action2 = DP_NAT_NONE;
@@ -353,12 +361,15 @@ int dpw_build(const dpw_config_t *c, dpw_workload_t **out) {
         dp_rule_t r = wildcard_rule(4);
         r.vni_a = svni; r.vni_b = kDstVni;
         r.src = pfx4(src_nat_priv[k], 24);
+        if (is_pat(k)) { r.sport_lo = kPatPortLo; r.sport_hi = 65535; }
         r.priority = ((24 + 1) << 1);
         r.action = DP_NAT_STATIC;
         w.ffl4.push_back(r);
       }
+      // own routed space 10/8 (sources outside it miss the local stage)
       dp_rule_t l = wildcard_rule(4);
-      l.vni_a = svni; l.vni_b = kDstVni; l.priority = 2; l.action = DP_NAT_NONE;
+      l.vni_a = svni; l.vni_b = kDstVni; l.src = pfx4(0x0a000000u, 8); l.priority = (8 + 1) << 1;
+      l.action = DP_NAT_NONE;
       w.ffl4.push_back(l);
       dp_rule_t l6 = wildcard_rule(6);
       l6.vni_a = svni; l6.vni_b = kDstVni; l6.priority = 2; l6.action = DP_NAT_NONE;
@@ -370,12 +381,26 @@ int dpw_build(const dpw_config_t *c, dpw_workload_t **out) {
         e.prefix = pfx4(src_nat_priv[k], 24);
         e.first_range = (uint32_t)w.nat_ranges.size();
         e.n_ranges = 1;
-        e.size = 256;
         dp_nat_range_t rg{};
         put32(rg.orig_lo_ip, src_nat_priv[k]); put32(rg.orig_hi_ip, src_nat_priv[k] | 0xff);
         rg.orig_hi_port = 65535;
         put32(rg.tgt_lo_ip, src_nat_pub[k]); put32(rg.tgt_hi_ip, src_nat_pub[k] | 0xff);
         rg.tgt_hi_port = 65535;
+        if (is_pat(k)) {
+          // PAT (NatTableValue::Pat): 256 addresses x ports 1024..65535 onto
+          // 252 addresses x ports 0..65535 -- equal sizes (256 * 64512 =
+          // 252 * 65536), one range, offset 0; a mapped port 0 is rejected
+          e.is_pat = 1;
+          e.first_port_range = (uint32_t)w.nat_prs.size();
+          e.n_port_ranges = 1;
+          w.nat_prs.push_back(dp_port_range_t{kPatPortLo, 65535});
+          e.size = 256ull * (65536 - kPatPortLo);
+          rg.orig_lo_port = kPatPortLo;
+          put32(rg.tgt_hi_ip, src_nat_pub[k] + 251);
+          rg.tgt_lo_port = 0;
+        } else {
+          e.size = 256;
+        }
         w.nat_ranges.push_back(rg);
         w.nat_ents.push_back(e);
         st.n_entries++;
@@ -413,8 +438,27 @@ int dpw_build(const dpw_config_t *c, dpw_workload_t **out) {
         int sl, dl;
         if (fam == 4) {
           sl = 16 + (int)R.below(13); dl = 16 + (int)R.below(13);
-          r.src = pfx4(0x0a000000u | (R.u32() & 0x00ffffffu), sl);
-          r.dst = pfx4(0x0a000000u | (R.u32() & 0x00ffffffu), dl);
+          uint32_t sa = 0x0a000000u | (R.u32() & 0x00ffffffu), da = 0x0a000000u | (R.u32() & 0x00ffffffu);
+          uint32_t sanc = 0, danc = 0;
+          // half of the rules sit over one of the VPC's source-NAT /24s and
+          // half over a destination-NAT public /24 (anchored: a packet steered
+          // to the rule keeps an address inside that /24, so steering toward
+          // ACL rules keeps the NAT share)
+          if (n_nat && R.below(2) == 0) {
+            uint32_t kk = s + n_vni * R.below(std::max<uint32_t>(1, (n_nat - s + n_vni - 1) / n_vni));
+            if (kk >= n_nat) kk = s;
+            sanc = src_nat_priv[kk];
+            sl = 20 + (int)R.below(9);
+            sa = sanc | (R.u32() & 0xff);
+          }
+          if (n_nat && R.below(2) == 0) {
+            danc = dst_nat_pub[R.below(n_nat)];
+            dl = 22 + (int)R.below(7);
+            da = danc | (R.u32() & 0xff);
+          }
+          r.src = pfx4(sa, sl);
+          r.dst = pfx4(da, dl);
+          acl_anchor.push_back({sanc, danc});
         } else {
           uint8_t a[16] = {0x20, 0x01, 0x0d, 0xb8}, b[16] = {0x20, 0x01, 0x0d, 0xb8};
           for (int i = 4; i < 16; i++) { a[i] = (uint8_t)R.u32(); b[i] = (uint8_t)R.u32(); }
@@ -485,6 +529,7 @@ int dpw_build(const dpw_config_t *c, dpw_workload_t **out) {
     uint8_t *l4;
     uint16_t l4len;
     uint32_t sip = 0, dip = 0;
+    int steer_dp = -1;  // destination port inside the steered ACL rule's range
     uint8_t s6[16], d6[16];
     if (!is6) {
       if (overlay) {
@@ -513,9 +558,22 @@ int dpw_build(const dpw_config_t *c, dpw_workload_t **out) {
             uint32_t dn = (uint32_t)ar.dst.addr[0] << 24 | (uint32_t)ar.dst.addr[1] << 16 | (uint32_t)ar.dst.addr[2] << 8 | ar.dst.addr[3];
             sip = sn | (R.u32() & (ar.src.len >= 32 ? 0 : (0xffffffffu >> ar.src.len)));
             dip = dn | (R.u32() & (ar.dst.len >= 32 ? 0 : (0xffffffffu >> ar.dst.len)));
+            // anchored prefixes: stay inside the NAT /24 (which holds the prefix
+            // when it is longer than /24, else is inside it)
+            const uint32_t sanc = acl_anchor[rk][0], danc = acl_anchor[rk][1];
+            if (sanc && ar.src.len <= 24) sip = sanc | (1 + R.below(254));
+            if (danc && ar.dst.len <= 24) dip = danc | (1 + R.below(254));
             if (ar.proto_mask) tcp = ar.proto_val == 6;
+            steer_dp = (int)ar.dport_lo + (int)R.below((uint32_t)ar.dport_hi - ar.dport_lo + 1);
+            if (steer_dp < 1024) steer_dp = -1;  // wildcard: keep the random port
           }
         }
+        // flow-filter misses: 3% toward a destination no peering exposes
+        // (remote stage miss), 2% from a source outside the VPC's space
+        // (local stage miss) -- both Filtered
+        const uint32_t u = R.below(100);
+        if (u < 3) dip = 0xc0a80000u | (R.u32() & 0xffffu);        // 192.168/16
+        else if (u < 5) sip = 0x647f0000u | (R.u32() & 0xffffu);   // 100.127/16
       } else {
         sip = 0x0a000000u | (R.u32() & 0x00ffffffu);
         const dp_route_t &rr = w.routes[R.below(n_v4)];
@@ -545,6 +603,7 @@ int dpw_build(const dpw_config_t *c, dpw_workload_t **out) {
     // payload
     for (int k = 0; k < l4len; k++) l4[k] = (uint8_t)R.u32();
     uint16_t sp = (uint16_t)(1024 + R.below(64512)), dp = (uint16_t)(1024 + R.below(64512));
+    if (steer_dp >= 0) dp = (uint16_t)steer_dp;
     if (tcp && l4len < 20) tcp = false;  // 64B frames stay UDP
     if (!is6) ip[9] = tcp ? 6 : 17; else ip[6] = tcp ? 6 : 17;
     if (!is6) { put16(ip + 10, 0); put16(ip + 10, csum_fold(sum_bytes(ip, 20))); }

@@ -103,9 +103,11 @@ class GpuPathNf:
         return iter(burst)
 
     def process_arrays(self, buf: np.ndarray, inp: np.ndarray,
-                       stats: Optional[np.ndarray] = None) -> np.ndarray:
+                       stats: Optional[np.ndarray] = None,
+                       out: Optional[np.ndarray] = None) -> np.ndarray:
         """Host-origin burst, in place (dp_process_burst)."""
-        out = np.zeros(len(inp), dtype=A.PKT_OUT)
+        if out is None:
+            out = np.zeros(len(inp), dtype=A.PKT_OUT)
         sp = stats.ctypes.data if stats is not None else None
         A.check(self.lib.dp_process_burst(self.ctx, buf.ctypes.data, buf.nbytes, inp.ctypes.data,
                                           out.ctypes.data, len(inp), sp),

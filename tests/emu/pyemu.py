@@ -40,3 +40,43 @@ def classifier_forms(variant: str = ""):
     out = (C.c_uint32 * 2)()
     lib(variant).dpd_debug_classifier_forms(out)
     return int(out[0]), int(out[1])
+
+
+def aligned_copy(buf: np.ndarray) -> np.ndarray:
+    """16-byte aligned copy of a burst buffer with 16 bytes of slack."""
+    raw = np.zeros(buf.nbytes + 48, dtype=np.uint8)
+    off = (-raw.ctypes.data) & 15
+    a = raw[off:off + buf.nbytes + 16]
+    a[:buf.nbytes] = buf
+    return a
+
+
+class ParallelEmu:
+    """The kernel body over one compiled image on host threads (bench.py's
+    compiled CPU leg); libdpemu_fast.so is the -O3 build."""
+
+    def __init__(self, tables_ptr):
+        p = os.path.join(HERE, "build", "libdpemu_fast.so")
+        if not os.path.exists(p):
+            subprocess.run(["make", "-s", "-C", HERE, "build/libdpemu_fast.so"], check=True)
+        self.l = l = C.CDLL(p)
+        V = C.c_void_p
+        l.dpemu_ctx_create.argtypes = [V]
+        l.dpemu_ctx_create.restype = V
+        l.dpemu_ctx_free.argtypes = [V]
+        l.dpemu_run_parallel.argtypes = [V, V, C.c_uint64, V, V, C.c_uint32, C.c_uint32, C.c_uint32]
+        self.h = l.dpemu_ctx_create(C.cast(tables_ptr, C.c_void_p))
+        if not self.h:
+            raise RuntimeError("emu rejected tables")
+
+    def run(self, buf: np.ndarray, buf_bytes: int, inp: np.ndarray, out: np.ndarray, threads: int,
+            burst: int = 64):
+        rc = self.l.dpemu_run_parallel(self.h, buf.ctypes.data, buf_bytes, inp.ctypes.data,
+                                       out.ctypes.data, len(inp), burst, threads)
+        if rc != 0:
+            raise RuntimeError(f"emu run rc={rc}")
+
+    def close(self):
+        if self.h:
+            self.l.dpemu_ctx_free(self.h)
+            self.h = None
