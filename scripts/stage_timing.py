@@ -32,7 +32,7 @@ def main():
     a = ap.parse_args()
     torch.cuda.init()
     dev = torch.device("cuda", 0)
-    w = Workload(a.config, a.packets, seed=1, n_acl=a.acl, n_nat=a.nat)
+    w = Workload(a.config, a.packets, seed=1, n_acl=a.acl, n_nat=a.nat, layout="dpdk")
     nf = GpuPathNf(0)
     nf.publish(w.tables)
     lib = A.gpu_lib()
