@@ -136,6 +136,17 @@ __device__ __forceinline__ uint64_t load_mac(const uint8_t *p) {
 }
 __device__ __forceinline__ uint8_t mac_b(uint64_t m, int i) { return (uint8_t)(m >> (40 - 8 * i)); }
 
+// Frame byte f lives at window position shift + f when 0 <= shift + f < WIN
+// (the LDS copy, written back by flush_window); any other byte is written
+// straight to the burst buffer.  Reads (F.b) see both.
+__device__ __forceinline__ void wput8(const Frame &F, int f, uint32_t v) {
+  const int o = F.shift + f;
+  if ((unsigned)o < (unsigned)WIN) F.lds[o] = (uint8_t)v;
+  else F.g[f] = (uint8_t)v;
+}
+__device__ __forceinline__ void wput16(const Frame &F, int f, uint32_t v) { wput8(F, f, v >> 8); wput8(F, f + 1, v); }
+__device__ __forceinline__ void wput32(const Frame &F, int f, uint32_t v) { wput16(F, f, v >> 16); wput16(F, f + 2, v); }
+
 // ---------------------------------------------------------------------------
 // Parsed header stack (offsets are frame-relative)
 // ---------------------------------------------------------------------------
@@ -256,6 +267,172 @@ __device__ __forceinline__ int kind_of_proto(uint8_t p, bool v6) {
   return HK_NONE;
 }
 
+// ---------------------------------------------------------------------------
+// ICMP error messages (cold paths: only such packets reach them)
+// ---------------------------------------------------------------------------
+// Error message types as the reference sees them: etherparse's decoded
+// type/code pairs mapped through net/src/icmp4/mod.rs:406-465 and
+// net/src/icmp6/mod.rs:396-459 (a Redirect with a non-unicast gateway and a
+// Packet Too Big below MTU 1280 are Unknown), error classes
+// icmp4/mod.rs:555-563, icmp6/mod.rs:577-585.
+__device__ __forceinline__ bool icmp_err_at(const Frame &F, int o, bool v6) {
+  const uint8_t t = F.b(o), c = F.b(o + 1);
+  if (!v6) {
+    if (t == 3) return c <= 15;
+    if (t == 5) {
+      if (c > 3) return false;
+      const uint32_t gw = F.be32(o + 4);
+      return !((gw >> 28) == 0xe || gw == 0xffffffffu);
+    }
+    if (t == 11) return c <= 1;
+    if (t == 12) return c <= 2;
+    return false;
+  }
+  if (t == 1) return c <= 6;
+  if (t == 2) return c == 0 && F.be32(o + 4) >= 1280;
+  if (t == 3) return c <= 1;
+  if (t == 4) return c <= 10;
+  return false;
+}
+
+// Embedded headers of an ICMP error message (EmbeddedHeaders,
+// net/src/headers/embedded.rs:43-48): frame offsets of the IP header, the
+// kept extension headers and the (possibly truncated) transport header.
+struct Emb {
+  int off, net, net_hlen;
+  int next, ext_len;
+  int ext_off[3];
+  uint8_t ext_kind[3];
+  int tk;            // L4_* (L4_NONE: none)
+  bool full;         // a full transport header (else a partial one: every remaining byte)
+  int t_off, t_len;
+  int consumed, rec;  // bytes consumed / written back by the deparse
+};
+
+// TruncatedTcp / TruncatedUdp / TruncatedIcmp4 / TruncatedIcmp6::parse
+// (tcp/truncated.rs:193-214, udp/truncated.rs, icmp4/truncated.rs:200-221):
+// the full header, else -- on a length shortfall only -- a partial header of
+// every remaining byte (TCP/UDP: >= 4 bytes and non-zero ports; ICMP: >= 2).
+// Returns the length (0: no transport), `full` tells which.
+__device__ __forceinline__ int trunc_transport(const Frame &F, int pos, int k, bool &full) {
+  const int rem = F.len - pos;
+  uint32_t aux = 0;
+  full = false;
+  if (k == HK_TCP) {
+    bool short_ = rem < 20;
+    if (!short_) {
+      const int doff = F.b(pos + 12) >> 4;
+      if (doff < 5) return 0;
+      short_ = rem < doff * 4;
+    }
+    if (!short_) { full = true; return try_parse(F, HK_TCP, pos, aux); }
+  } else if (k == HK_UDP) {
+    if (rem >= 8) { full = true; return try_parse(F, HK_UDP, pos, aux); }
+  } else {
+    const int n = try_parse(F, k, pos, aux);
+    if (n) { full = true; return n; }
+    return rem >= 2 ? rem : 0;
+  }
+  if (rem < 4 || F.be16(pos) == 0 || F.be16(pos + 2) == 0) return 0;
+  return rem;
+}
+
+// EmbeddedHeaders::parse_with (embedded.rs:289-397) at `pos`: the IP header
+// (else no embedded headers: false), then the embedded-payload dispatch of
+// ipv4/mod.rs:320-331, ipv6/mod.rs:266-287, ipv6/ext_parse.rs:46-69,
+// ip_auth/v4.rs:67-87, with the main loop's parse-then-record order (an
+// extension header past MAX_NET_EXTENSIONS ends the loop after its successor
+// was consumed).
+__device__ DP_COLD bool emb_parse(const Frame &F, int pos, bool v6, Emb &E) {
+  uint32_t aux = 0;
+  E.off = pos; E.net = v6 ? 6 : 4; E.next = 0; E.ext_len = 0; E.tk = L4_NONE; E.full = false;
+  E.t_off = E.t_len = 0;
+  E.net_hlen = try_parse(F, v6 ? HK_V6 : HK_V4, pos, aux);
+  if (!E.net_hlen) return false;
+  uint8_t nh = v6 ? F.b(pos + 6) : F.b(pos + 9);
+  int p = pos + E.net_hlen;
+  int prior = 0;  // 0 IP, 1 extension header, 2 transport
+  int prior_off = 0, prior_len = 0, prior_kind = 0;
+  bool prior_full = false;
+  for (int guard = 0; guard < 8; guard++) {
+    int next = -1, nlen = 0, nkind = 0, noff = p;
+    bool nfull = false;
+    if (prior != 2) {
+      int k = HK_NONE;
+      switch (nh) {
+        case 6: k = HK_TCP; break;
+        case 17: k = HK_UDP; break;
+        case 1: k = v6 ? HK_NONE : HK_ICMP4; break;
+        case 58: k = v6 ? HK_ICMP6 : HK_NONE; break;
+        case 51: k = HK_EXT_AUTH; break;
+        case 0: case 43: case 60: k = v6 ? HK_EXT_RAW : HK_NONE; break;
+        case 44: k = v6 ? HK_EXT_FRAG : HK_NONE; break;
+      }
+      if (k == HK_TCP || k == HK_UDP || k == HK_ICMP4 || k == HK_ICMP6) {
+        nlen = trunc_transport(F, p, k, nfull);
+        next = nlen ? 2 : -1;
+      } else if (k != HK_NONE) {
+        nlen = try_parse(F, k, p, aux);
+        next = nlen ? 1 : -1;
+      }
+      nkind = k;
+      if (next >= 0) p += nlen;
+    }
+    bool brk = false;
+    if (prior == 1) {
+      if (E.next < 3) {
+        E.ext_off[E.next] = prior_off; E.ext_kind[E.next] = (uint8_t)prior_kind;
+        E.ext_len += prior_len;
+        E.next++;
+      } else {
+        brk = true;
+      }
+    } else if (prior == 2) {
+      E.tk = prior_kind == HK_TCP ? L4_TCP : prior_kind == HK_UDP ? L4_UDP
+                                                                   : prior_kind == HK_ICMP4 ? L4_ICMP4 : L4_ICMP6;
+      E.full = prior_full; E.t_off = prior_off; E.t_len = prior_len;
+    }
+    if (brk || next < 0) break;
+    prior = next; prior_off = noff; prior_len = nlen; prior_kind = nkind; prior_full = nfull;
+    if (next == 1) nh = F.b(noff);
+  }
+  E.consumed = p - pos;
+  E.rec = E.net_hlen + E.ext_len + E.t_len;
+  return true;
+}
+
+// The bytes Icmpv4Header / Icmpv6Header::to_bytes write back for an error
+// message: only the fields its type defines survive (v4 DestUnreachable code
+// 4: the next-hop MTU; Redirect: the gateway; ParameterProblem code 0: the
+// pointer byte; v6 PacketTooBig: the MTU; ParameterProblem: the pointer);
+// unused bytes -- RFC 4884's length among them -- are zero.
+__device__ __forceinline__ void icmp_norm_at(const Frame &F, int o, bool v6) {
+  if (!icmp_err_at(F, o, v6)) return;
+  const uint8_t t = F.b(o), c = F.b(o + 1);
+  if (!v6) {
+    if (t == 3) { wput16(F, o + 4, 0); if (c != 4) wput16(F, o + 6, 0); }
+    if (t == 11) wput32(F, o + 4, 0);
+    if (t == 12) { wput8(F, o + 5, 0); wput16(F, o + 6, 0); if (c != 0) wput8(F, o + 4, 0); }
+  } else if (t == 1 || t == 3) {
+    wput32(F, o + 4, 0);
+  }
+}
+// An ICMP error message's embedded headers as the deparse writes them back
+// (EmbeddedHeaders::deparse): the embedded IPv4 reserved flag bit, extension-header reserved fields, a full
+// embedded TCP header's reserved bits and a full embedded ICMP header.
+// Applied to the frame right after the parse: every later reader (checksum
+// validation, serialize) sees the bytes the reference's structures hold.
+__device__ DP_COLD void emb_normalize(const Frame &F, const Emb &E) {
+  if (E.net == 4) wput8(F, E.off + 6, F.b(E.off + 6) & 0x7f);
+  for (int e = 0; e < E.next; e++) {
+    const int x = E.ext_off[e];
+    if (E.ext_kind[e] == HK_EXT_FRAG) { wput8(F, x + 1, 0); wput8(F, x + 3, F.b(x + 3) & 0xf9); }
+    if (E.ext_kind[e] == HK_EXT_AUTH) wput16(F, x + 2, 0);
+  }
+  if (E.full && E.tk == L4_TCP) wput8(F, E.t_off + 12, F.b(E.t_off + 12) & 0xf1);
+  if (E.full && (E.tk == L4_ICMP4 || E.tk == L4_ICMP6)) icmp_norm_at(F, E.t_off, E.tk == L4_ICMP6);
+}
+
 // Headers::parse (net/src/headers/mod.rs:474-578) incl. the MAX_VLANS /
 // MAX_NET_EXTENSIONS quirk.  Returns false if the Ethernet header is invalid.
 __device__ __forceinline__ bool parse(const Frame &F, int hb, Hdr &H) {
@@ -320,13 +497,27 @@ __device__ __forceinline__ bool parse(const Frame &F, int hb, Hdr &H) {
     if (brk || !nlen) break;
     cur = nk; cur_pos = npos; cur_len = nlen; cur_aux = naux;
   }
+  // an ICMP error message's payload: its embedded packet fragment
+  // (Icmp4::parse_payload, icmp4/mod.rs:626-646, and the ICMPv6 twin)
+  int emb_rec = 0;
+  if ((H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) && pos == H.l4_off + H.l4_hlen &&
+      icmp_err_at(F, H.l4_off, H.l4 == L4_ICMP6)) {
+    // the header as Icmpv4Header / Icmpv6Header write it back
+    icmp_norm_at(F, H.l4_off, H.l4 == L4_ICMP6);
+    Emb E;
+    if (emb_parse(F, pos, H.l4 == L4_ICMP6, E)) {
+      emb_normalize(F, E);
+      pos += E.consumed;
+      emb_rec = E.rec;
+    }
+  }
   H.consumed = pos - hb;
   int sz2 = 14 + 4 * H.nvlan;
   if (H.net) {
     sz2 += H.net_hlen + H.ext_len;
     if (H.l4) { sz2 += H.l4_hlen; if (H.vx) sz2 += 8; }
   }
-  H.size = sz2;
+  H.size = sz2 + emb_rec;
   return true;
 }
 
@@ -428,12 +619,6 @@ __device__ __forceinline__ void cur_dst(const Frame &F, const Hdr &H, const Stat
   fam = (uint8_t)H.net;
   if (H.net == 4) { a.w[0] = S.v4dst; a.w[1] = a.w[2] = a.w[3] = 0; }
   else a = addr16(F, H.net_off + 24);
-}
-
-__device__ __forceinline__ bool icmp_is_error(const Frame &F, const Hdr &H) {
-  if (H.l4 == L4_ICMP4) { uint8_t t = F.b(H.l4_off); return t == 3 || t == 5 || t == 11 || t == 12; }
-  if (H.l4 == L4_ICMP6) { uint8_t t = F.b(H.l4_off); return t >= 1 && t <= 4; }
-  return false;
 }
 
 // ---------------------------------------------------------------------------
@@ -1038,6 +1223,62 @@ __device__ __forceinline__ uint32_t sum_frame(const Frame &F, int a, int e) {
   return (wa & 1) ? le : bswap16(le);
 }
 
+// An ICMP error message carries embedded headers when its parse consumed
+// bytes past the ICMP header (nothing else follows an ICMP header).
+__device__ __forceinline__ bool has_emb(const Hdr &H) {
+  return (H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) && H.hb + H.consumed > H.l4_off + H.l4_hlen;
+}
+// Sum (not complemented) of the ICMP checksum input of an error message with
+// embedded headers: the ICMP header (checksum word excluded), then
+// get_payload_for_checksum (icmp_any/checksum.rs:226-259) -- the embedded IP
+// header, the embedded transport header and the payload, WITHOUT the
+// embedded extension headers (as the reference computes it) -- and for
+// ICMPv6 the pseudo header over that length (Icmpv6Type::calc_checksum).
+__device__ DP_COLD uint32_t icmp_err_sum(const Frame &F, const Hdr &H, const Emb &E, int pay_start) {
+  const int l = H.l4_off;
+  uint64_t t = sum_frame(F, l, l + 2) + sum_frame(F, l + 4, l + H.l4_hlen);  // checksum word out
+  t += sum_frame(F, E.off, E.off + E.net_hlen);
+  t += sum_frame(F, E.t_off, E.t_off + E.t_len);
+  t += sum_frame(F, pay_start, F.len);
+  if (H.l4 == L4_ICMP6) {
+    const uint32_t tl = (uint32_t)(H.l4_hlen + E.net_hlen + E.t_len + (F.len - pay_start));
+    t += sum_frame(F, H.net_off + 8, H.net_off + 40);
+    t += (tl >> 16) + (tl & 0xffff) + 58u;
+  }
+  return fold(t);
+}
+// IPv4 header checksum of the embedded header as it stands (checksum word out)
+__device__ __forceinline__ uint16_t emb_ipv4_ck(const Frame &F, const Emb &E) {
+  const uint64_t t = sum_frame(F, E.off, E.off + 10) + sum_frame(F, E.off + 12, E.off + E.net_hlen);
+  return (uint16_t)~fold(t);
+}
+
+// IcmpErrorHandler with an empty flow table (nat/src/icmp_handler/nf.rs:61-120):
+// IcmpErrorPacket::new needs an embedded IP header and transport
+// (net/src/packet/icmp_err.rs:37-53; else IcmpErrorIncomplete), then
+// src_vpcd (Unroutable), valid ICMP and embedded IPv4 checksums
+// (validate_checksums, :71-87; InvalidChecksum) and a flow key -- ports, or
+// an ICMP query identifier (net/src/flows/flow_key.rs:635-660;
+// IcmpErrorIncomplete).  No flow exists, so the packet goes on.
+__device__ DP_COLD uint8_t icmp_error_check(const Frame &F, const Hdr &H, const State &S) {
+  Emb E;
+  const bool v6 = H.l4 == L4_ICMP6;
+  if (!has_emb(H) || !emb_parse(F, H.l4_off + H.l4_hlen, v6, E) || E.tk == L4_NONE)
+    return DP_DONE_ICMP_ERROR_INCOMPLETE;
+  if (!S.src_vni) return DP_DONE_UNROUTABLE;
+  if ((uint16_t)~icmp_err_sum(F, H, E, S.pay_start) != F.be16(H.l4_off + 2)) return DP_DONE_INVALID_CHECKSUM;
+  if (E.net == 4 && emb_ipv4_ck(F, E) != F.be16(E.off + 10)) return DP_DONE_INVALID_CHECKSUM;
+  if (E.tk == L4_ICMP4 || E.tk == L4_ICMP6) {
+    // identifier: a query message (v4 echo / timestamp, v6 echo); a full
+    // header only for the decoded types (code 0), a partial one with >= 6 bytes
+    const uint8_t t = F.b(E.t_off), c = F.b(E.t_off + 1);
+    const bool q = E.tk == L4_ICMP6 ? (t == 128 || t == 129) : (t == 0 || t == 8 || t == 13 || t == 14);
+    const bool id = E.full ? (q && c == 0) : (q && E.t_len >= 6);
+    if (!id) return DP_DONE_ICMP_ERROR_INCOMPLETE;
+  }
+  return DONE_NONE;
+}
+
 // ---------------------------------------------------------------------------
 // Stages
 // ---------------------------------------------------------------------------
@@ -1467,10 +1708,31 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
   if (action == DP_ACL_DENY) done(S, DP_DONE_ACL_DROPPED);
 }
 
+// The embedded packet of an ICMP error message, translated back by static
+// NAT (nat/src/static_nat/nf.rs:111-155, nat/src/icmp_handler/
+// icmp_error_msg.rs nat_translate_icmp_inner_src/dst): its destination
+// through the source table (find_src_mapping), its source through the
+// destination table (find_dst_mapping), with the ports of a TCP / UDP
+// header (full or partial).  q[0]: inner destination, q[1]: inner source.
+// Returns false without an embedded IPv4 header.
+__device__ DP_COLD bool nat_icmp_inner(const Img &g, const Frame &F, const Hdr &H, int32_t st, int32_t dt, NatQ q[2],
+                                       Emb &E) {
+  if (!emb_parse(F, H.l4_off + H.l4_hlen, H.l4 == L4_ICMP6, E) || E.net != 4) return false;
+  const bool hp = E.tk == L4_TCP || E.tk == L4_UDP;
+  q[0].ti = st; q[0].addr = F.be32(E.off + 16); q[0].port = hp ? F.be16(E.t_off + 2) : 0;
+  q[1].ti = dt; q[1].addr = F.be32(E.off + 12); q[1].port = hp ? F.be16(E.t_off) : 0;
+  const uint32_t pre[2] = {NO_PRE, NO_PRE};
+  nat_find2(g, q, hp, pre);
+  return true;
+}
+
 __device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, const Hdr &H, State &S, const Pre &P) {
   if (S.done != DONE_NONE) return;
   if (!(S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST))) return;
-  if (S.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) return;
+  // an ICMP error message with an embedded packet is translated even when
+  // already marked NATed (nf.rs:350-362)
+  const bool ie = has_emb(H) && icmp_err_at(F, H.l4_off, H.l4 == L4_ICMP6);
+  if ((S.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) && !ie) return;
   if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
   const VniRec VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
   if (!VR.pervni) { done(S, DP_DONE_UNROUTABLE); return; }
@@ -1486,21 +1748,40 @@ __device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, c
   q[1].addr = S.v4dst; q[1].port = has_p ? S.dport : 0;
   const uint32_t pre[2] = {P.nsrc, P.ndst};
   nat_find2(g, q, has_p, pre);
-  if (S.flags & DP_META_REQ_STATIC_NAT_SRC) {
+  NatQ qi[2];
+  Emb E;
+  const bool inner = ie && nat_icmp_inner(g, F, H, st, VR.nat_dst, qi, E);
+  const bool inner_p = inner && (E.tk == L4_TCP || E.tk == L4_UDP);
+  if ((S.flags & DP_META_REQ_STATIC_NAT_SRC) && !(S.flags & DP_META_NATTED_SRC)) {
     bool mod = false;
     // source mapping: UnicastIpAddr::try_from rejects multicast / broadcast
     if (q[0].ok && !((q[0].na >> 28) == 0xe || q[0].na == 0xffffffffu)) {
       if (q[0].na != S.v4src) { S.v4src = q[0].na; mod = true; }
       if (has_p && q[0].hp && q[0].np != S.sport) { S.sport = q[0].np; mod = true; }
     }
+    // the embedded destination (find_src_mapping: unicast only); a mapping
+    // found counts as a modification (Ok(true))
+    if (inner && qi[0].ok && !((qi[0].na >> 28) == 0xe || qi[0].na == 0xffffffffu)) {
+      wput32(F, E.off + 16, qi[0].na);
+      if (inner_p && qi[0].hp) wput16(F, E.t_off + 2, qi[0].np);
+      mod = true;
+    }
     if (mod) S.flags |= DP_META_NATTED_SRC;
     modified |= mod;
   }
-  if (S.flags & DP_META_REQ_STATIC_NAT_DST) {
+  if ((S.flags & DP_META_REQ_STATIC_NAT_DST) && !(S.flags & DP_META_NATTED_DST)) {
     bool mod = false;
     if (q[1].ok) {
       if (q[1].na != S.v4dst) { S.v4dst = q[1].na; mod = true; }
       if (has_p && q[1].hp && q[1].np != S.dport) { S.dport = q[1].np; mod = true; }
+    }
+    // the embedded source (find_dst_mapping): a non-unicast target is
+    // NotUnicast -> NatFailure
+    if (inner && qi[1].ok) {
+      if ((qi[1].na >> 28) == 0xe || qi[1].na == 0xffffffffu) { done(S, DP_DONE_NAT_FAILURE); return; }
+      wput32(F, E.off + 12, qi[1].na);
+      if (inner_p && qi[1].hp) wput16(F, E.t_off, qi[1].np);
+      mod = true;
     }
     if (mod) S.flags |= DP_META_NATTED_DST;
     modified |= mod;
@@ -1575,16 +1856,6 @@ __device__ __forceinline__ uint32_t outer_ck4(const OuterHdr &S) {
 }
 
 // --- serializer ------------------------------------------------------------
-// Frame byte f lives at window position shift + f when 0 <= shift + f < WIN
-// (the LDS copy, written back by flush_window); any other byte is written
-// straight to the burst buffer.  Reads (F.b) see both.
-__device__ __forceinline__ void wput8(const Frame &F, int f, uint32_t v) {
-  const int o = F.shift + f;
-  if ((unsigned)o < (unsigned)WIN) F.lds[o] = (uint8_t)v;
-  else F.g[f] = (uint8_t)v;
-}
-__device__ __forceinline__ void wput16(const Frame &F, int f, uint32_t v) { wput8(F, f, v >> 8); wput8(F, f + 1, v); }
-__device__ __forceinline__ void wput32(const Frame &F, int f, uint32_t v) { wput16(F, f, v >> 16); wput16(F, f + 2, v); }
 __device__ __forceinline__ void wput_mac(const Frame &F, int f, uint64_t m) {
   wput16(F, f, (uint32_t)(m >> 32)); wput32(F, f + 2, (uint32_t)m);
 }
@@ -1626,6 +1897,9 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
   const int outer = S.encap ? 14 + (S.o_fam == 4 ? 20 : 40) + 16 : 0;
   const int start = inner_start - outer;
   if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
+  // an ICMP error message's embedded headers, located before any move
+  Emb E;
+  const bool emb = has_emb(H) && emb_parse(F, H.l4_off + H.l4_hlen, H.l4 == L4_ICMP6, E);
   // the parse-limit quirk consumed headers it did not record: the kept
   // stack moves sh bytes later to end at the payload (back to front)
   const int sh = inner_start - H.hb;
@@ -1635,6 +1909,10 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
     H.hb += sh; H.net_off += sh; H.l4_off += sh; H.vx_off += sh;
 #pragma unroll
     for (int e = 0; e < 3; e++) H.ext_off[e] += sh;
+    if (emb) {
+      E.off += sh; E.t_off += sh;
+      for (int e = 0; e < E.next; e++) E.ext_off[e] += sh;
+    }
   }
   // deparse: rewritten fields and normalised reserved bits
   if (S.eth_dirty) { wput_mac(F, H.hb, S.edst); wput_mac(F, H.hb + 6, S.esrc); }
@@ -1670,7 +1948,13 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
     if (H.vx) wput8(F, H.vx_off, 0x08);
   }
   if (H.net == 4) wput16(F, H.net_off + 10, (uint16_t)~fold(sum_frame(F, H.net_off, H.net_off + H.net_hlen)));
-  if (ck_off >= 0) {
+  if (ck_off >= 0 && emb) {
+    // update_checksums with embedded headers (net/src/headers/mod.rs:906-928):
+    // the embedded IPv4 header first (part of the ICMP payload; its transport
+    // checksum stays), then the ICMP checksum over get_payload_for_checksum
+    if (E.net == 4) wput16(F, E.off + 10, emb_ipv4_ck(F, E));
+    wput16(F, ck_off, (uint16_t)~icmp_err_sum(F, H, E, S.pay_start));
+  } else if (ck_off >= 0) {
     uint64_t t = sum_frame(F, l, F.len);
     const uint32_t tl = (uint32_t)H.l4_hlen + (uint32_t)(F.len - S.pay_start);
     if (H.l4 != L4_ICMP4) {  // pseudo header
@@ -1753,8 +2037,12 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
     stage_ipforward(g, F, H, S);  // IP-Forward-1
   }
   TS(2);
-  // IcmpErrorHandler: overlay ICMP errors need flow state (outside the slice)
-  if (S.done == DONE_NONE && (S.flags & DP_META_IS_OVERLAY) && icmp_is_error(F, H)) done(S, DP_DONE_UNHANDLED);
+  // IcmpErrorHandler (nat/src/icmp_handler/nf.rs:184-194): overlay ICMP error messages
+  if (S.done == DONE_NONE && (S.flags & DP_META_IS_OVERLAY) && (H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) &&
+      icmp_err_at(F, H.l4_off, H.l4 == L4_ICMP6)) {
+    const uint8_t r = icmp_error_check(F, H, S);
+    if (r != DONE_NONE) done(S, r);
+  }
   Pre P;
   stage_flow_filter(g, F, H, S, P);
   TS(3);
@@ -1771,14 +2059,11 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
 #else
   if (S.done == DP_DONE_DELIVERED) {
 #endif
-    if (!S.encap && icmp_is_error(F, H)) S.done = DP_DONE_UNHANDLED;
-    else {
-      int st = serialize(F, H, S, fl0, fl1);
-      S.flags &= ~DP_META_REFR_CHKSUM;
-      if (S.done == DP_DONE_DELIVERED) {
-        o.off = (uint32_t)((int)pin.off + st);
-        o.len = (uint16_t)(F.len - st);
-      }
+    int st = serialize(F, H, S, fl0, fl1);
+    S.flags &= ~DP_META_REFR_CHKSUM;
+    if (S.done == DP_DONE_DELIVERED) {
+      o.off = (uint32_t)((int)pin.off + st);
+      o.len = (uint16_t)(F.len - st);
     }
   }
   o.done = S.done;

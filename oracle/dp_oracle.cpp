@@ -192,6 +192,36 @@ struct Icmp {  // type, code, checksum, rest (4 or 16 bytes)
   int hlen;
 };
 
+// EmbeddedHeaders (net/src/headers/embedded.rs:43-48): the IP packet fragment
+// an ICMP error message carries -- IP header, <= MAX_NET_EXTENSIONS extension
+// headers, and a possibly truncated transport header (TruncatedTcp/Udp/
+// Icmp4/Icmp6: a full header, or a partial one that keeps every remaining
+// byte, tcp/truncated.rs:67-103, udp/truncated.rs:67-103, icmp4/truncated.rs).
+struct Emb {
+  bool present = false;
+  int net = 0;  // 4 / 6
+  Ipv4 v4{};
+  Ipv6 v6{};
+  std::vector<Ext> ext;
+  int tk = L4_NONE;  // transport kind (L4_*), L4_NONE: none
+  bool full = false;
+  Tcp tcp{};
+  Udp udp{};
+  Icmp icmp{};
+  std::vector<uint8_t> part;  // partial transport header bytes (deparsed as they are)
+  int net_size() const { return net == 4 ? v4.hlen() : net == 6 ? 40 : 0; }
+  int transport_size() const {
+    if (tk == L4_NONE) return 0;
+    if (!full) return (int)part.size();
+    return tk == L4_TCP ? tcp.hlen() : tk == L4_UDP ? 8 : icmp.hlen;
+  }
+  int size() const {  // EmbeddedHeaders::size (embedded.rs:402-414)
+    int s = net_size() + transport_size();
+    if (net) for (auto &e : ext) s += (int)e.bytes.size();
+    return s;
+  }
+};
+
 struct Headers {
   bool has_eth = false;
   Eth eth{};
@@ -206,6 +236,7 @@ struct Headers {
   Icmp icmp{};
   bool has_vxlan = false;
   uint32_t vni = 0;
+  Emb emb;  // Headers::embedded_ip (ICMP error messages only)
 
   int size() const {
     int s = has_eth ? 14 : 0;
@@ -217,6 +248,7 @@ struct Headers {
     if (net && l4 == L4_UDP) s += 8;
     if (net && (l4 == L4_ICMP4 || l4 == L4_ICMP6)) s += icmp.hlen;
     if (net && l4 != L4_NONE && has_vxlan) s += 8;
+    if (emb.present) s += emb.size();
     return s;
   }
 };
@@ -427,6 +459,170 @@ bool parse_icmp(Reader &r, Icmp &ic, bool v6) {
   return true;
 }
 
+// --- ICMP types as the reference sees them ---------------------------------
+// etherparse 0.21 decodes the type/code pair (Icmpv4Type / Icmpv6Type); a
+// pair it does not know is Unknown.  The reference maps that onto its own
+// enums (net/src/icmp4/mod.rs:406-465, net/src/icmp6/mod.rs:396-459), which
+// also turn a Redirect with a non-unicast gateway and a Packet Too Big with
+// an MTU below 1280 into Unknown.  Error messages: icmp4/mod.rs:555-563,
+// icmp6/mod.rs:577-585.
+bool icmp4_error(const uint8_t *q) {
+  const uint8_t t = q[0], c = q[1];
+  switch (t) {
+    case 3: return c <= 15;   // DestUnreachable (16 codes)
+    case 5: {                 // Redirect (4 codes), gateway UnicastIpv4Addr
+      if (c > 3) return false;
+      const bool bcast = q[4] == 255 && q[5] == 255 && q[6] == 255 && q[7] == 255;
+      return !((q[4] & 0xf0) == 0xe0 || bcast);
+    }
+    case 11: return c <= 1;   // TimeExceeded
+    case 12: return c <= 2;   // ParameterProblem
+    default: return false;
+  }
+}
+bool icmp6_error(const uint8_t *q) {
+  const uint8_t t = q[0], c = q[1];
+  switch (t) {
+    case 1: return c <= 6;                      // DestUnreachable
+    case 2: return c == 0 && be32(q + 4) >= 1280;  // PacketTooBig (Icmp6PacketTooBig::new)
+    case 3: return c <= 1;                      // TimeExceeded
+    case 4: return c <= 10;                     // ParameterProblem
+    default: return false;
+  }
+}
+// The 8 (v4 timestamp: 20) header bytes Icmpv4Header / Icmpv6Header write
+// back (to_bytes): an error message keeps only the fields its type defines
+// (v4 DestUnreachable: the next-hop MTU of code 4; Redirect: the gateway;
+// ParameterProblem code 0: the pointer byte; v6 PacketTooBig: the MTU,
+// ParameterProblem: the pointer), the unused bytes -- RFC 4884's length
+// among them -- are written as zero.  Other types are written back as parsed.
+void icmp_norm(const uint8_t *q, int hlen, bool v6, uint8_t *o) {
+  memcpy(o, q, hlen);
+  if (!v6 && icmp4_error(q)) {
+    if (q[0] == 3) { o[4] = o[5] = 0; if (q[1] != 4) o[6] = o[7] = 0; }
+    if (q[0] == 11) o[4] = o[5] = o[6] = o[7] = 0;
+    if (q[0] == 12) { o[5] = o[6] = o[7] = 0; if (q[1] != 0) o[4] = 0; }
+  }
+  if (v6 && icmp6_error(q)) {
+    if (q[0] == 1 || q[0] == 3) o[4] = o[5] = o[6] = o[7] = 0;
+  }
+}
+// Icmp4::identifier / Icmp6::identifier of a full header: decoded echo and
+// timestamp messages (code 0) carry one (icmp4/mod.rs:565-576)
+bool icmp_full_identifier(const Icmp &ic, bool v6, uint16_t &id) {
+  const uint8_t t = ic.raw[0], c = ic.raw[1];
+  const bool q = v6 ? ((t == 128 || t == 129) && c == 0)
+                    : ((t == 0 || t == 8 || t == 13 || t == 14) && c == 0);
+  if (!q) return false;
+  id = be16(ic.raw + 4);
+  return true;
+}
+
+// TruncatedTcp::parse (tcp/truncated.rs:193-214): the full header if
+// Tcp::parse succeeds; a Length error (fewer bytes than the header) gives a
+// partial header of every remaining byte (>= 4, non-zero ports); any other
+// error (data offset < 5, zero port) fails.
+bool parse_trunc_tcp(Reader &r, Emb &e) {
+  const size_t n = r.remaining();
+  const uint8_t *q = r.cur();
+  bool len_err = n < 20;
+  if (!len_err) {
+    const int doff = q[12] >> 4;
+    if (doff < 5) return false;
+    len_err = n < (size_t)doff * 4;
+  }
+  if (!len_err) {
+    if (!parse_tcp(r, e.tcp)) return false;  // zero ports
+    e.tk = L4_TCP; e.full = true;
+    return true;
+  }
+  if (n < 4 || be16(q) == 0 || be16(q + 2) == 0) return false;
+  e.tk = L4_TCP; e.full = false;
+  e.part.assign(q, q + n);
+  r.pos += n;
+  return true;
+}
+// TruncatedUdp::parse (udp/truncated.rs): full >= 8 bytes, else partial (>= 4)
+bool parse_trunc_udp(Reader &r, Emb &e) {
+  const size_t n = r.remaining();
+  const uint8_t *q = r.cur();
+  if (n >= 8) {
+    if (!parse_udp(r, e.udp)) return false;
+    e.tk = L4_UDP; e.full = true;
+    return true;
+  }
+  if (n < 4 || be16(q) == 0 || be16(q + 2) == 0) return false;
+  e.tk = L4_UDP; e.full = false;
+  e.part.assign(q, q + n);
+  r.pos += n;
+  return true;
+}
+// TruncatedIcmp4 / TruncatedIcmp6::parse (icmp4/truncated.rs:200-221): the
+// full header (8 bytes, v4 timestamp 20), else a partial one (>= 2 bytes)
+bool parse_trunc_icmp(Reader &r, Emb &e, bool v6) {
+  const size_t n = r.remaining();
+  const uint8_t *q = r.cur();
+  e.tk = v6 ? L4_ICMP6 : L4_ICMP4;
+  if (parse_icmp(r, e.icmp, v6)) { e.full = true; return true; }
+  if (n < 2) { e.tk = L4_NONE; return false; }
+  e.full = false;
+  e.part.assign(q, q + n);
+  r.pos += n;
+  return true;
+}
+
+// EmbeddedHeaders::parse_with (net/src/headers/embedded.rs:289-397): the IP
+// header, then Ipv4::parse_embedded_payload / Ipv6::parse_embedded_payload
+// (ipv4/mod.rs:320-331, ipv6/mod.rs:266-287, ipv6/ext_parse.rs:46-69,
+// ip_auth/v4.rs:67-87) with the MAX_NET_EXTENSIONS quirk of the main loop.
+// Returns the consumed bytes, or -1 when the IP header does not parse (no
+// embedded headers at all, icmp4/mod.rs:626-646).
+int parse_embedded(const uint8_t *p, size_t len, bool v6, Emb &e) {
+  Reader r{p, len, 0};
+  e = Emb{};
+  if (!v6) { if (!parse_ipv4(r, e.v4)) return -1; e.net = 4; }
+  else { if (!parse_ipv6(r, e.v6)) return -1; e.net = 6; }
+  e.present = true;
+  // the loop of embedded.rs:318-390: parse the header after `prior`
+  // (consuming it), then record `prior` -- an extension header past the limit
+  // breaks the loop after its successor was consumed
+  enum { P_IP, P_EXT, P_TR };
+  int prior = P_IP;
+  Ext pext{};
+  uint8_t nh = v6 ? e.v6.nh : e.v4.proto;
+  Emb tr;  // a parsed transport, recorded when it becomes `prior`
+  for (;;) {
+    int next = -1;
+    Ext x{};
+    if (prior != P_TR) {
+      bool ok = false;
+      switch (nh) {
+        case 6: ok = parse_trunc_tcp(r, tr); next = P_TR; break;
+        case 17: ok = parse_trunc_udp(r, tr); next = P_TR; break;
+        case 1: if (!v6) { ok = parse_trunc_icmp(r, tr, false); next = P_TR; } break;
+        case 58: if (v6) { ok = parse_trunc_icmp(r, tr, true); next = P_TR; } break;
+        case 51: ok = parse_ext_auth(r, x); next = P_EXT; break;
+        case 0: case 43: case 60: if (v6) { ok = parse_ext_raw(r, x); next = P_EXT; } break;
+        case 44: if (v6) { ok = parse_ext_frag(r, x); next = P_EXT; } break;
+        default: break;
+      }
+      if (!ok) next = -1;
+    }
+    bool brk = false;
+    if (prior == P_EXT) {
+      if (e.ext.size() < 3) e.ext.push_back(pext);
+      else brk = true;
+    } else if (prior == P_TR) {
+      e.tk = tr.tk; e.full = tr.full; e.tcp = tr.tcp; e.udp = tr.udp; e.icmp = tr.icmp;
+      e.part = tr.part;
+    }
+    if (brk || next < 0) break;
+    prior = next;
+    if (next == P_EXT) { pext = x; nh = x.nh; }
+  }
+  return (int)r.pos;
+}
+
 // Vxlan::parse (net/src/vxlan/mod.rs:91-122)
 bool parse_vxlan(Reader &r, uint32_t &vni) {
   if (r.remaining() < 8) return false;
@@ -440,22 +636,10 @@ bool parse_vxlan(Reader &r, uint32_t &vni) {
   return true;
 }
 
-bool icmp_is_error(const Headers &h) {
-  if (h.l4 == L4_ICMP4) {
-    uint8_t t = h.icmp.raw[0];
-    return t == 3 || t == 5 || t == 11 || t == 12;
-  }
-  if (h.l4 == L4_ICMP6) {
-    uint8_t t = h.icmp.raw[0];
-    return t >= 1 && t <= 4;
-  }
-  return false;
-}
-
 // Headers::parse loop, including its MAX_VLANS / MAX_NET_EXTENSIONS quirk:
 // the header after the limit is still consumed but not recorded.
 // Returns consumed bytes, or -1 on Eth failure.
-enum HKind { H_ETH, H_VLAN, H_V4, H_V6, H_EXT, H_TCP, H_UDP, H_ICMP4, H_ICMP6, H_VXLAN };
+enum HKind { H_ETH, H_VLAN, H_V4, H_V6, H_EXT, H_TCP, H_UDP, H_ICMP4, H_ICMP6, H_VXLAN, H_EMB };
 struct HeaderVal {
   int kind;
   Vlan vlan;
@@ -466,6 +650,7 @@ struct HeaderVal {
   Udp udp;
   Icmp icmp;
   uint32_t vni;
+  Emb emb;
 };
 
 bool parse_by_ethertype(uint16_t et, Reader &r, HeaderVal &out) {
@@ -513,6 +698,18 @@ bool parse_next_ctx(const HeaderVal &prior, Reader &r, HeaderVal &out, bool v6ct
       }
       return parse_by_proto(nh, true, false, r, out);  // ext_parse.rs dispatch
     }
+    case H_ICMP4:
+    case H_ICMP6: {
+      // Icmp4/Icmp6::parse_payload (icmp4/mod.rs:626-646): an error message's
+      // embedded packet fragment
+      const bool v6 = prior.kind == H_ICMP6;
+      if (!(v6 ? icmp6_error(prior.icmp.raw) : icmp4_error(prior.icmp.raw))) return false;
+      const int c = parse_embedded(r.cur(), r.remaining(), v6, out.emb);
+      if (c < 0) return false;
+      out.kind = H_EMB;
+      r.pos += (size_t)c;
+      return true;
+    }
     case H_UDP:
       // Udp::parse_payload: VXLAN only on dport 4789 (net/src/udp/mod.rs:152-166)
       if (prior.udp.dport == 4789) {
@@ -521,9 +718,7 @@ bool parse_next_ctx(const HeaderVal &prior, Reader &r, HeaderVal &out, bool v6ct
       }
       return false;
     default:
-      // TCP / VXLAN: no further parse.  ICMP errors would parse an embedded
-      // packet; ICMP error messages are outside this slice (handled by the
-      // caller, see DESIGN.md "scope").
+      // TCP / VXLAN / embedded headers: no further parse
       return false;
   }
 }
@@ -552,6 +747,7 @@ int parse_headers(const uint8_t *p, size_t len, Headers &h) {
       case H_ICMP4: h.l4 = L4_ICMP4; h.icmp = prior.icmp; break;
       case H_ICMP6: h.l4 = L4_ICMP6; h.icmp = prior.icmp; break;
       case H_VXLAN: h.has_vxlan = true; h.vni = prior.vni; break;
+      case H_EMB: h.emb = prior.emb; break;
       case H_VLAN:
         if (h.vlans.size() < 4) h.vlans.push_back(prior.vlan); else brk = true;
         break;
@@ -623,6 +819,64 @@ int deparse_tcp(const Tcp &t, uint8_t *q) {
   return t.hlen();
 }
 
+int deparse_icmp(const Icmp &ic, bool v6, uint8_t *q) {
+  icmp_norm(ic.raw, ic.hlen, v6, q);
+  return ic.hlen;
+}
+// EmbeddedHeaders::deparse pieces (embedded.rs:416-461): the IP header, the
+// extension headers, the transport header (a partial one as parsed)
+int deparse_emb_ip(const Emb &e, uint8_t *q) {
+  return e.net == 4 ? deparse_ipv4(e.v4, q) : deparse_ipv6(e.v6, q);
+}
+int deparse_emb_transport(const Emb &e, uint8_t *q) {
+  if (e.tk == L4_NONE) return 0;
+  if (!e.full) { memcpy(q, e.part.data(), e.part.size()); return (int)e.part.size(); }
+  switch (e.tk) {
+    case L4_TCP: return deparse_tcp(e.tcp, q);
+    case L4_UDP:
+      put16(q, e.udp.sport); put16(q + 2, e.udp.dport); put16(q + 4, e.udp.len); put16(q + 6, e.udp.csum);
+      return 8;
+    default: return deparse_icmp(e.icmp, e.tk == L4_ICMP6, q);
+  }
+}
+int deparse_emb(const Emb &e, uint8_t *q) {
+  int o = deparse_emb_ip(e, q);
+  for (auto &x : e.ext) { memcpy(q + o, x.bytes.data(), x.bytes.size()); o += (int)x.bytes.size(); }
+  return o + deparse_emb_transport(e, q + o);
+}
+// icmp_any/checksum.rs:226-259 get_payload_for_checksum: the embedded IP
+// header, the embedded transport header, then the payload -- the embedded
+// extension headers are not part of it (as in the reference)
+std::vector<uint8_t> icmp_checksum_payload(const Emb &e, const uint8_t *pay, size_t plen) {
+  std::vector<uint8_t> v(e.net_size() + e.transport_size() + plen);
+  int o = deparse_emb_ip(e, v.data());
+  o += deparse_emb_transport(e, v.data() + o);
+  if (plen) memcpy(v.data() + o, pay, plen);
+  return v;
+}
+// Icmpv4Type::calc_checksum / Icmpv6Type::calc_checksum over the header as
+// written back and `pay` (v6: pseudo header of the outer IPv6 addresses)
+uint16_t icmp_checksum(const Headers &h, const uint8_t *pay, size_t plen) {
+  const bool v6 = h.l4 == L4_ICMP6;
+  uint8_t hb[20];
+  icmp_norm(h.icmp.raw, h.icmp.hlen, v6, hb);
+  hb[2] = hb[3] = 0;
+  Sum16 s;
+  if (v6) {
+    uint32_t tl = (uint32_t)h.icmp.hlen + (uint32_t)plen;
+    s.add_slice(h.v6.src, 16); s.add_slice(h.v6.dst, 16);
+    s.add_u16((uint16_t)(tl >> 16)); s.add_u16((uint16_t)tl); s.add2(0, 0); s.add2(0, 58);
+  }
+  s.add_slice(hb, h.icmp.hlen);
+  s.add_slice(pay, plen);
+  return s.ones_complement();
+}
+bool icmp_is_error_msg(const Headers &h) {
+  if (h.l4 == L4_ICMP4) return icmp4_error(h.icmp.raw);
+  if (h.l4 == L4_ICMP6) return icmp6_error(h.icmp.raw);
+  return false;
+}
+
 int deparse_headers(const Headers &h, uint8_t *q) {
   int o = 0;
   if (h.has_eth) {
@@ -652,8 +906,7 @@ int deparse_headers(const Headers &h, uint8_t *q) {
       o += 8;
       break;
     default:
-      memcpy(q + o, h.icmp.raw, h.icmp.hlen);
-      o += h.icmp.hlen;
+      o += deparse_icmp(h.icmp, h.l4 == L4_ICMP6, q + o);
       break;
   }
   if (h.has_vxlan) {
@@ -663,6 +916,7 @@ int deparse_headers(const Headers &h, uint8_t *q) {
     q[o + 7] = 0;
     o += 8;
   }
+  if (h.emb.present) o += deparse_emb(h.emb, q + o);
   return o;
 }
 
@@ -671,6 +925,9 @@ void update_checksums(Headers &h, const uint8_t *pay, size_t plen) {
   if (h.net == 0) return;
   if (h.net == 4) h.v4.csum = ipv4_checksum(h.v4);
   if (h.has_vxlan) return;
+  // the embedded IPv4 header first: it is part of the ICMP payload
+  // (headers/mod.rs:906-919; its transport checksum is left as is)
+  if (h.emb.present && h.emb.net == 4) h.emb.v4.csum = ipv4_checksum(h.emb.v4);
   Sum16 s;
   switch (h.l4) {
     case L4_NONE: return;
@@ -701,26 +958,16 @@ void update_checksums(Headers &h, const uint8_t *pay, size_t plen) {
       h.tcp.csum = s.ones_complement();
       return;
     }
-    case L4_ICMP4: {
-      if (h.net != 4) return;  // debug!("illegal") in the reference
-      Icmp c = h.icmp;
-      c.raw[2] = c.raw[3] = 0;
-      s.add_slice(c.raw, c.hlen);
-      s.add_slice(pay, plen);
-      uint16_t v = s.ones_complement();
-      put16(h.icmp.raw + 2, v);
-      return;
-    }
+    case L4_ICMP4:
     case L4_ICMP6: {
-      if (h.net != 6) return;
-      uint32_t tl = (uint32_t)h.icmp.hlen + (uint32_t)plen;
-      s.add_slice(h.v6.src, 16); s.add_slice(h.v6.dst, 16);
-      s.add_u16((uint16_t)(tl >> 16)); s.add_u16((uint16_t)tl); s.add2(0, 0); s.add2(0, 58);
-      Icmp c = h.icmp;
-      c.raw[2] = c.raw[3] = 0;
-      s.add_slice(c.raw, c.hlen);
-      s.add_slice(pay, plen);
-      put16(h.icmp.raw + 2, s.ones_complement());
+      if (h.net != (h.l4 == L4_ICMP4 ? 4 : 6)) return;  // debug!("illegal") in the reference
+      // an error message with an embedded packet: get_payload_for_checksum
+      if (icmp_is_error_msg(h) && h.emb.present) {
+        std::vector<uint8_t> v = icmp_checksum_payload(h.emb, pay, plen);
+        put16(h.icmp.raw + 2, icmp_checksum(h, v.data(), v.size()));
+      } else {
+        put16(h.icmp.raw + 2, icmp_checksum(h, pay, plen));
+      }
       return;
     }
   }
@@ -1241,12 +1488,36 @@ void stage_acl(const dpo_tables &T, Packet &p) {
   if (action == DP_ACL_DENY) p.done(DP_DONE_ACL_DROPPED);
 }
 
-// StaticNat (nat/src/static_nat/nf.rs:158-368)
+// Embedded transport ports (EmbeddedTransport::source / destination,
+// embedded.rs:545-601): TCP / UDP only, full or partial headers alike.
+bool emb_port(const Emb &e, bool src, uint16_t &port) {
+  if (e.tk != L4_TCP && e.tk != L4_UDP) return false;
+  if (!e.full) port = be16(e.part.data() + (src ? 0 : 2));
+  else if (e.tk == L4_TCP) port = src ? e.tcp.sport : e.tcp.dport;
+  else port = src ? e.udp.sport : e.udp.dport;
+  return true;
+}
+// set_source / set_destination of the embedded transport.  The reference
+// also calls update_checksum on it, but discards the incremental result
+// (icmp_error_msg.rs translate_inner_tcp_udp_*, embedded.rs:612-647, the
+// default Checksum::increment_update_checksum returns, never stores): the
+// embedded transport checksum stays as it was.
+void emb_set_port(Emb &e, bool src, uint16_t port) {
+  if (!e.full) put16(e.part.data() + (src ? 0 : 2), port);
+  else if (e.tk == L4_TCP) (src ? e.tcp.sport : e.tcp.dport) = port;
+  else (src ? e.udp.sport : e.udp.dport) = port;
+}
+
+// StaticNat (nat/src/static_nat/nf.rs:158-368), with the embedded packet of
+// an ICMP error message translated back (nf.rs:111-155,
+// nat/src/icmp_handler/icmp_error_msg.rs: nat_translate_icmp_inner_src/dst)
 void stage_static_nat(const dpo_tables &T, Packet &p) {
   if (p.is_done()) return;
   uint32_t need = DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST;
   if (!(p.m.flags & need)) return;
-  if (p.m.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) return;  // no ICMP errors here
+  const bool icmp_err = icmp_is_error_msg(p.h) && p.h.emb.present;
+  // an ICMP error message is NATed even when already marked NATed (nf.rs:350-362)
+  if ((p.m.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) && !icmp_err) return;
   if (!p.m.src_vni || !p.m.dst_vni) { p.done(DP_DONE_UNROUTABLE); return; }
   auto dt = T.nat_dst.find(p.m.src_vni);
   bool has_src_tables = false;
@@ -1257,9 +1528,10 @@ void stage_static_nat(const dpo_tables &T, Packet &p) {
   bool has_sp = p.h.l4 == L4_TCP || p.h.l4 == L4_UDP;
   uint16_t *psp = p.h.l4 == L4_TCP ? &p.h.tcp.sport : &p.h.udp.sport;
   uint16_t *pdp = p.h.l4 == L4_TCP ? &p.h.tcp.dport : &p.h.udp.dport;
+  Emb &e = p.h.emb;
+  auto st = T.nat_src.find({p.m.src_vni, p.m.dst_vni});
   if ((p.m.flags & DP_META_REQ_STATIC_NAT_SRC) && !(p.m.flags & DP_META_NATTED_SRC)) {
     bool mod = false;
-    auto st = T.nat_src.find({p.m.src_vni, p.m.dst_vni});
     if (st != T.nat_src.end() && p.h.net == 4) {
       uint32_t na; bool hp; uint16_t np;
       if (nat_find_mapping(st->second, p.h.v4.src, has_sp, has_sp ? *psp : 0, na, hp, np)) {
@@ -1269,6 +1541,18 @@ void stage_static_nat(const dpo_tables &T, Packet &p) {
           if (na != be32(p.h.v4.src)) { put32(p.h.v4.src, na); mod = true; }
           if (has_sp && hp && np != *psp) { *psp = np; mod = true; }
         }
+      }
+    }
+    // the embedded packet's destination: find_src_mapping (nf.rs:134-155)
+    if (icmp_err && st != T.nat_src.end() && e.net == 4) {
+      uint16_t port = 0;
+      const bool hp_in = emb_port(e, false, port);
+      uint32_t na; bool hp; uint16_t np;
+      if (nat_find_mapping(st->second, e.v4.dst, hp_in, port, na, hp, np) &&
+          !((na >> 28) == 0xe || na == 0xffffffffu)) {
+        put32(e.v4.dst, na);
+        if (hp_in && hp) emb_set_port(e, false, np);
+        mod = true;  // Ok(true) whenever a mapping exists
       }
     }
     if (mod) p.m.flags |= DP_META_NATTED_SRC;
@@ -1283,10 +1567,55 @@ void stage_static_nat(const dpo_tables &T, Packet &p) {
         if (has_sp && hp && np != *pdp) { *pdp = np; mod = true; }
       }
     }
+    // the embedded packet's source: find_dst_mapping (nf.rs:111-132); a
+    // non-unicast target is NotUnicast -> NatFailure (icmp_error_msg.rs)
+    if (icmp_err && dt != T.nat_dst.end() && e.net == 4) {
+      uint16_t port = 0;
+      const bool hp_in = emb_port(e, true, port);
+      uint32_t na; bool hp; uint16_t np;
+      if (nat_find_mapping(dt->second, e.v4.src, hp_in, port, na, hp, np)) {
+        if ((na >> 28) == 0xe || na == 0xffffffffu) { p.done(DP_DONE_NAT_FAILURE); return; }
+        put32(e.v4.src, na);
+        if (hp_in && hp) emb_set_port(e, true, np);
+        mod = true;
+      }
+    }
     if (mod) p.m.flags |= DP_META_NATTED_DST;
     modified |= mod;
   }
   if (modified) p.m.flags |= DP_META_REFR_CHKSUM;
+}
+
+// IcmpErrorHandler (nat/src/icmp_handler/nf.rs:61-194) with an empty flow
+// table: an overlay ICMP error message must carry an embedded IP header and
+// transport (IcmpErrorPacket::new, net/src/packet/icmp_err.rs:37-53), valid
+// ICMP and embedded IPv4 checksums (validate_checksums, :71-87) and a flow
+// key (embedded ports, or an ICMP query identifier: flow_key.rs:635-660);
+// then no flow is found and the packet goes on (nf.rs:113-120).
+void stage_icmp_error(const dpo_tables &T, Packet &p) {
+  if (p.is_done() || !p.overlay() || !icmp_is_error_msg(p.h)) return;
+  const Emb &e = p.h.emb;
+  if (!e.present || e.tk == L4_NONE) { p.done(DP_DONE_ICMP_ERROR_INCOMPLETE); return; }
+  if (!p.m.src_vni) { p.done(DP_DONE_UNROUTABLE); return; }
+  std::vector<uint8_t> v = icmp_checksum_payload(e, p.buf + p.pay_start, p.pay_end - p.pay_start);
+  if (icmp_checksum(p.h, v.data(), v.size()) != be16(p.h.icmp.raw + 2)) {
+    p.done(DP_DONE_INVALID_CHECKSUM);
+    return;
+  }
+  if (e.net == 4 && ipv4_checksum(e.v4) != e.v4.csum) { p.done(DP_DONE_INVALID_CHECKSUM); return; }
+  if (e.tk == L4_ICMP4 || e.tk == L4_ICMP6) {
+    const bool v6 = e.tk == L4_ICMP6;
+    bool has_id;
+    uint16_t id;
+    if (e.full) has_id = icmp_full_identifier(e.icmp, v6, id);
+    else {
+      // TruncatedIcmp4Header / TruncatedIcmp6Header::identifier: query type, >= 6 bytes
+      const uint8_t t = e.part[0];
+      const bool q = v6 ? (t == 128 || t == 129) : (t == 0 || t == 8 || t == 13 || t == 14);
+      has_id = q && e.part.size() >= 6;
+    }
+    if (!has_id) { p.done(DP_DONE_ICMP_ERROR_INCOMPLETE); return; }  // EmbeddedMissingIcmpId
+  }
 }
 
 bool adj_lookup(const dpo_tables &T, const Ip &ip, uint32_t oif, uint8_t mac[6]) {
@@ -1377,9 +1706,7 @@ void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pk
     stage_ingress(T, p, in.iif);
     stage_ipforward(T, p);  // IP-Forward-1
   }
-  // IcmpErrorHandler (nat/src/icmp_handler/nf.rs:184-194): overlay ICMP
-  // error messages need the stateful handler -- outside this slice.
-  if (!p.is_done() && p.overlay() && icmp_is_error(p.h)) p.done(DP_DONE_UNHANDLED);
+  stage_icmp_error(T, p);
   // FlowLookup: identity with an empty flow table
   stage_flow_filter(T, p);
   stage_acl(T, p);
@@ -1389,12 +1716,7 @@ void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pk
     p.done(DP_DONE_INTERNAL_FAILURE);
   stage_ipforward(T, p);  // IP-Forward-2
   stage_egress(T, p);
-  if (p.m.done == DP_DONE_DELIVERED) {
-    // Underlay ICMP error messages carry embedded headers whose checksums the
-    // reference refreshes too: outside this slice.
-    if (icmp_is_error(p.h)) p.done_force(DP_DONE_UNHANDLED);
-    else serialize(p);
-  }
+  if (p.m.done == DP_DONE_DELIVERED) serialize(p);
   out.done = p.m.done < 0 ? (uint8_t)DP_DONE_NONE : (uint8_t)p.m.done;
   out.meta_flags = p.m.flags;
   out.oif = p.m.has_oif ? p.m.oif : 0;

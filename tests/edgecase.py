@@ -18,6 +18,7 @@ seeded overlay packets from known and unknown VNIs.
 from __future__ import annotations
 
 import random
+import struct
 
 import numpy as np
 
@@ -329,7 +330,126 @@ def _ports(r):
     return _pick(r, PORTS) if r.random() < 0.7 else r.randrange(1, 65536)
 
 
+# --- ICMP error messages carrying an embedded packet fragment --------------
+# (net/src/headers/embedded.rs; nat/src/icmp_handler).  The fragment is the
+# packet the error answers: usually the reverse of the outer addresses (so the
+# overlay NAT translates it back), with a full or truncated transport header.
+
+def _emb_transport(r, v6, isrc, idst):
+    """(next header, transport bytes) of an embedded packet, maybe truncated."""
+    kind = _pick(r, ["udp", "udp", "tcp", "tcp", "echo", "icmp", "other"])
+    pay = bytes(r.randrange(256) for _ in range(_pick(r, [0, 0, 4, 12, 30])))
+    ps = (P.pseudo6 if v6 else P.pseudo4)
+    sp, dp = _pick(r, [53, 80, 443, 1234, 2000, 8080]), _pick(r, [53, 80, 443, 999, 2001, 5678])
+    if kind == "udp":
+        nh, t = 17, P.udp(sp, dp, pay, ps(isrc, idst, 17, 8 + len(pay)))
+    elif kind == "tcp":
+        opts = b"" if r.random() < 0.8 else bytes([1] * 4)
+        nh, t = 6, P.tcp(sp, dp, pay, ps(isrc, idst, 6, 20 + len(opts) + len(pay)), options=opts,
+                         reserved=r.choice([0, 0, 0, 0xE]))
+    elif kind == "echo":
+        typ = _pick(r, [128, 129]) if v6 else _pick(r, [8, 0, 13])
+        rest = struct.pack("!HH", r.randrange(65536), r.randrange(65536))
+        if typ == 13:
+            rest += bytes(12)
+        code = 0 if r.random() < 0.85 else 1
+        nh = 58 if v6 else 1
+        t = (P.icmp6(typ, code, rest, pay, isrc, idst) if v6 else P.icmp4(typ, code, rest, pay))
+    elif kind == "icmp":
+        nh = 58 if v6 else 1
+        t = (P.icmp6(1, 4, bytes(4), pay, isrc, idst) if v6 else P.icmp4(3, 3, bytes(4), pay))
+    else:
+        nh, t = 47, bytes(r.randrange(256) for _ in range(12))
+    cut = _pick(r, [None, None, None, None, 8, 6, 4, 3, 1])
+    return nh, (t if cut is None else t[:cut])
+
+
+def _emb_packet(r, v6, isrc, idst):
+    """An embedded IP packet fragment: (bytes, byte ranges of its extension headers)."""
+    nh, body = _emb_transport(r, v6, isrc, idst)
+    exts = []
+    if v6:
+        for _ in range(_pick(r, [0, 0, 0, 1, 2, 3, 4])):
+            kind = _pick(r, [0, 43, 60, 44, 51])
+            if kind == 44:
+                e = P.ext_frag(nh, ident=r.randrange(1 << 32), reserved=r.randrange(2) * 0x11)
+            elif kind == 51:
+                e = P.ext_auth(nh, payload_len=1, reserved=r.randrange(2) * 0x1234)
+            else:
+                e = P.ext_raw(nh, hdr_len=_pick(r, [0, 1]), fill=r.randrange(256))
+            exts.insert(0, e)
+            nh = kind
+        ip = P.ipv6(isrc, idst, nh, sum(map(len, exts)) + len(body) + 40, hop=_pick(r, [1, 63]))
+    else:
+        if r.random() < 0.1:  # IPv4 AH in front of the transport
+            exts.insert(0, P.ext_auth(nh, payload_len=1))
+            nh = 51
+        evil = r.random() < 0.1
+        ip = P.ipv4(isrc, idst, nh, sum(map(len, exts)) + len(body) + r.randrange(0, 100),
+                    ttl=_pick(r, [1, 63]), evil=evil, ident=r.randrange(65536),
+                    options=b"" if r.random() < 0.9 else bytes([1] * 4))
+        if r.random() < 0.08:  # a bad embedded IPv4 checksum
+            ip = ip[:10] + bytes([ip[10] ^ 0x5a]) + ip[11:]
+        if r.random() < 0.05:  # not an IPv4 header at all
+            ip = bytes([0x7e]) + ip[1:]
+    ext_ranges, o = [], len(ip)
+    for e in exts:
+        ext_ranges.append((o, o + len(e)))
+        o += len(e)
+    return ip + b"".join(exts) + body, ext_ranges
+
+
+def _icmp_err(r, v6, src, dst):
+    """An ICMP error message (the L4 body of the outer packet src -> dst)."""
+    if r.random() < 0.7:  # answers a packet dst -> src, as a reply would
+        isrc, idst = dst, src
+    else:
+        isrc = _pick(r, OVERLAY_V6_DST if v6 else OVERLAY_V4_DST)
+        idst = _pick(r, OVERLAY_V6_SRC if v6 else OVERLAY_V4_SRC)
+    emb, ext_ranges = _emb_packet(r, v6, isrc, idst)
+    if v6:
+        typ = _pick(r, [1, 1, 2, 3, 4])
+        code = {1: _pick(r, [0, 3, 4, 6, 7]), 2: 0, 3: _pick(r, [0, 1, 2]),
+                4: _pick(r, [0, 1, 10, 11])}[typ]
+        rest = (struct.pack("!I", _pick(r, [1280, 1500, 1000])) if typ == 2 else
+                struct.pack("!I", r.randrange(40)) if typ == 4 else
+                bytes(4) if r.random() < 0.8 else b"\x00\x09\x00\x01")
+    else:
+        typ = _pick(r, [3, 3, 3, 11, 11, 12, 5])
+        code = {3: _pick(r, [0, 1, 3, 4, 13, 15, 16]), 11: _pick(r, [0, 1, 2]),
+                12: _pick(r, [0, 1, 2, 3]), 5: _pick(r, [0, 1, 3, 4])}[typ]
+        if typ == 5:
+            rest = P.ip4(_pick(r, ["192.0.2.1", "224.0.0.5", "10.0.0.1"]))
+        elif typ == 3 and code == 4:
+            rest = struct.pack("!HH", 0, _pick(r, [1400, 0, 576]))
+        elif typ == 12 and code == 0:
+            rest = bytes([r.randrange(28), 0, 0, 0])
+        else:
+            rest = bytes(4)
+        if r.random() < 0.2:  # RFC 4884 length / junk in the unused bytes
+            rest = bytes([rest[0], r.randrange(1, 40)]) + rest[2:]
+    pad = b"" if r.random() < 0.8 else bytes(r.randrange(1, 12))
+    hdr = bytes([typ, code, 0, 0]) + rest
+    # checksum as the reference validates it: header + embedded IP and
+    # transport + rest, the embedded extension headers left out (icmp_any/
+    # checksum.rs get_payload_for_checksum); sometimes left wrong on purpose
+    covered = bytearray(emb + pad)
+    for a, b in reversed(ext_ranges):
+        del covered[a:b]
+    msg = hdr + bytes(covered)
+    if v6:
+        ps = P.ip6(src) + P.ip6(dst) + struct.pack("!IxxxB", len(msg), 58)
+        c = P.csum_fold(P.sum16(ps) + P.sum16(msg))
+    else:
+        c = P.csum_fold(P.sum16(msg))
+    if r.random() < 0.1:
+        c ^= 0x0101
+    return hdr[:2] + struct.pack("!H", c) + hdr[4:] + emb + pad
+
+
 def _l4_v4(r, proto, src, dst, payload):
+    if proto == 1 and r.random() < 0.5:
+        return _icmp_err(r, False, src, dst)
     sp, dp = _ports(r), _ports(r)
     if proto == 6:
         opts = b"" if r.random() < 0.7 else bytes([1] * (4 * r.randrange(1, 4)))
@@ -345,6 +465,8 @@ def _l4_v4(r, proto, src, dst, payload):
 
 
 def _l4_v6(r, nh, src, dst, payload):
+    if nh == 58 and r.random() < 0.5:
+        return _icmp_err(r, True, src, dst)
     sp, dp = _ports(r), _ports(r)
     if nh == 6:
         return P.tcp(sp, dp, payload, P.pseudo6(src, dst, 6, 20 + len(payload)))

@@ -453,9 +453,79 @@ def pat_cases() -> List[Case]:
     return cs
 
 
+# ------------------------------------------------------- ICMP error messages
+
+def icmp4_err_frame(osrc, odst, isrc, idst, inner_proto=6, p1=1234, p2=5678, typ=3, code=0,
+                    rest=b"\0\0\0\0", bad_icmp_ck=False, inner=True, inner_ttl=4, ttl=8):
+    """build_test_icmp4_destination_unreachable_packet (net/src/packet/
+    test_utils.rs:314-400): Eth / IPv4 (ttl 8) / ICMP Destination Unreachable
+    (Network) / embedded IPv4 (ttl 4) / full TCP, UDP or ICMP echo header;
+    every checksum valid unless asked otherwise."""
+    if not inner:
+        emb = b""
+    else:
+        if inner_proto == 6:
+            t = P.tcp(p1, p2, b"", P.pseudo4(isrc, idst, 6, 20))
+        elif inner_proto == 17:
+            t = P.udp(p1, p2, b"", P.pseudo4(isrc, idst, 17, 8))
+        elif inner_proto == 1:
+            t = P.icmp4(8, 0, struct.pack("!HH", p1, p2))
+        elif inner_proto == -1:          # an ICMP error inside: no identifier
+            t, inner_proto = P.icmp4(3, 1, b"\0\0\0\0"), 1
+        else:                            # a protocol with no embedded transport parser
+            t = b""
+        emb = P.ipv4(isrc, idst, inner_proto, len(t), ttl=inner_ttl) + t
+    body = P.icmp4(typ, code, rest, emb)
+    if bad_icmp_ck:
+        body = body[:2] + bytes([body[2] ^ 0xFF]) + body[3:]
+    return P.eth(IF_MAC, PEER_MAC, 0x0800) + P.ipv4(osrc, odst, 1, len(body), ttl=ttl) + body
+
+
+def icmp_error_cases() -> List[Case]:
+    """ICMP error messages: the IcmpErrorHandler with an empty flow table
+    (nat/src/icmp_handler/nf.rs:61-120), static NAT of the embedded packet
+    (nat/src/static_nat/nf.rs:111-155) and the checksum refresh at serialize
+    (net/src/headers/mod.rs:894-928)."""
+    ov = lambda **kw: overlay_tables(**kw)  # noqa: E731
+    h = "nat/src/icmp_handler/nf.rs"
+    return [
+        # test_nat_icmp_error_msg_static_44: (10.0.0.1 -> 2.1.0.1) back to
+        # (5.5.0.1 -> 1.1.0.1), its embedded (2.1.0.1 -> 10.0.0.1) back to
+        # (1.1.0.1 -> 5.5.0.1)
+        Case("icmp_error_static_nat_44", "nat/src/static_nat/test.rs:333-374",
+             lambda: overlay_tables(src_vni=200, dst_vni=100, nat=dst_nat_static_44_config(),
+                                    nat_flags=(NAT_STATIC, NAT_STATIC)),
+             [Pkt(icmp4_err_frame("10.0.0.1", "2.1.0.1", "2.1.0.1", "10.0.0.1"), seeded_vni=200,
+                  expect=dict(done="Delivered", src="5.5.0.1", dst="1.1.0.1",
+                              inner_src="1.1.0.1", inner_dst="5.5.0.1"))]),
+        Case("icmp_error_no_flow_passes", f"{h}:113-120", ov, [
+            Pkt(icmp4_err_frame("10.1.0.1", "10.2.0.1", "10.2.0.1", "10.1.0.1", 17), seeded_vni=100,
+                expect=dict(done="Delivered", src="10.1.0.1", inner_src="10.2.0.1",
+                            inner_dst="10.1.0.1")),
+            Pkt(icmp4_err_frame("10.1.0.1", "10.2.0.1", "10.2.0.1", "10.1.0.1", 1), seeded_vni=100,
+                expect=dict(done="Delivered"))]),
+        Case("icmp_error_bad_checksum", f"{h}:77-88 (net/src/packet/icmp_err.rs:71-87)", ov, [
+            Pkt(icmp4_err_frame("10.1.0.1", "10.2.0.1", "10.2.0.1", "10.1.0.1", bad_icmp_ck=True),
+                seeded_vni=100, expect=dict(done="InvalidChecksum"))]),
+        Case("icmp_error_incomplete", f"{h}:61-66,102-108 (net/src/packet/icmp_err.rs:178-228,"
+             " net/src/flows/flow_key.rs:653-657)", ov, [
+            Pkt(icmp4_err_frame("10.1.0.1", "10.2.0.1", "", "", inner=False), seeded_vni=100,
+                expect=dict(done="IcmpErrorIncomplete")),
+            Pkt(icmp4_err_frame("10.1.0.1", "10.2.0.1", "10.2.0.1", "10.1.0.1", 47), seeded_vni=100,
+                expect=dict(done="IcmpErrorIncomplete")),
+            Pkt(icmp4_err_frame("10.1.0.1", "10.2.0.1", "10.2.0.1", "10.1.0.1", -1), seeded_vni=100,
+                expect=dict(done="IcmpErrorIncomplete"))]),
+        # underlay: not the handler's business (overlay only); delivered with
+        # its checksums refreshed (TTL -1)
+        Case("icmp_error_underlay_delivered", f"{h}:184-194", ov, [
+            Pkt(icmp4_err_frame("192.0.2.9", "203.0.113.5", "203.0.113.5", "192.0.2.9", ttl=64),
+                expect=dict(done="Delivered", ttl=63, inner_src="203.0.113.5"))]),
+    ]
+
+
 def all_cases() -> List[Case]:
     return acl_cases() + ff_cases() + lpm_cases() + ttl_cases() + vxlan_qos_cases() + \
-        parse_cases() + nat_cases() + pat_cases()
+        parse_cases() + nat_cases() + pat_cases() + icmp_error_cases()
 
 
 # ------------------------------------------------------------------ checks
@@ -487,6 +557,16 @@ def check(pkt: Pkt, out, frame_out: Optional[bytes]) -> List[str]:
         bad.append(f"oif {int(out['oif'])} not in {e['oif_in']}")
     if "fib_entry_in" in e and int(out["fib_entry"]) not in e["fib_entry_in"]:
         bad.append(f"fib_entry {int(out['fib_entry'])} not in {e['fib_entry_in']}")
+    if frame_out is not None and ("inner_src" in e or "inner_dst" in e):
+        # the embedded IPv4 header of an ICMPv4 error message
+        o = l3_of(frame_out)
+        eo = o + (frame_out[o] & 0xF) * 4 + 8
+        isrc = str(ipaddress.IPv4Address(frame_out[eo + 12:eo + 16]))
+        idst = str(ipaddress.IPv4Address(frame_out[eo + 16:eo + 20]))
+        if "inner_src" in e and isrc != e["inner_src"]:
+            bad.append(f"inner src {isrc} != {e['inner_src']}")
+        if "inner_dst" in e and idst != e["inner_dst"]:
+            bad.append(f"inner dst {idst} != {e['inner_dst']}")
     if frame_out is not None and any(k in e for k in ("ttl", "src", "dst", "outer_dscp",
                                                       "sport", "dport")):
         o = l3_of(frame_out)
@@ -582,5 +662,15 @@ def checksum_errors(frame: bytes) -> List[str]:
         elif proto == 6 and len(frame) >= l4o + 20:
             if P.csum_fold(P.sum16(pseudo(len(frame) - l4o)) + P.sum16(frame[l4o:])) != 0:
                 bad.append("tcp checksum")
+        elif proto == 1 and ver == 4 and len(frame) >= l4o + 8:
+            # ICMPv4 over the whole message; an error message's embedded IPv4
+            # header is refreshed too (net/src/headers/mod.rs:906-919)
+            if P.csum_fold(P.sum16(frame[l4o:])) != 0:
+                bad.append("icmp checksum")
+            eo = l4o + 8
+            if frame[l4o] in (3, 11, 12) and len(frame) >= eo + 20 and frame[eo] >> 4 == 4:
+                ehl = (frame[eo] & 0xF) * 4
+                if P.csum_fold(P.sum16(frame[eo:eo + ehl])) != 0:
+                    bad.append("embedded ipv4 header checksum")
         return bad
     return bad
