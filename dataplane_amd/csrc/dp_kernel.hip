@@ -169,6 +169,7 @@ struct Hdr {
   uint32_t vni;
   int consumed;     // bytes consumed from hb
   int size;         // deparse size of the kept stack
+  uint32_t emb;     // ICMP error message's embedded headers (emb_pack), 0: none
 };
 
 // try to parse one header of kind `k` at frame offset `pos`; returns its
@@ -343,7 +344,7 @@ __device__ __forceinline__ int trunc_transport(const Frame &F, int pos, int k, b
 // ip_auth/v4.rs:67-87, with the main loop's parse-then-record order (an
 // extension header past MAX_NET_EXTENSIONS ends the loop after its successor
 // was consumed).
-__device__ DP_COLD bool emb_parse(const Frame &F, int pos, bool v6, Emb &E) {
+__device__ __forceinline__ bool emb_parse(const Frame &F, int pos, bool v6, Emb &E) {
   uint32_t aux = 0;
   E.off = pos; E.net = v6 ? 6 : 4; E.next = 0; E.ext_len = 0; E.tk = L4_NONE; E.full = false;
   E.t_off = E.t_len = 0;
@@ -422,7 +423,7 @@ __device__ __forceinline__ void icmp_norm_at(const Frame &F, int o, bool v6) {
 // embedded TCP header's reserved bits and a full embedded ICMP header.
 // Applied to the frame right after the parse: every later reader (checksum
 // validation, serialize) sees the bytes the reference's structures hold.
-__device__ DP_COLD void emb_normalize(const Frame &F, const Emb &E) {
+__device__ __forceinline__ void emb_normalize(const Frame &F, const Emb &E) {
   if (E.net == 4) wput8(F, E.off + 6, F.b(E.off + 6) & 0x7f);
   for (int e = 0; e < E.next; e++) {
     const int x = E.ext_off[e];
@@ -433,11 +434,38 @@ __device__ DP_COLD void emb_normalize(const Frame &F, const Emb &E) {
   if (E.full && (E.tk == L4_ICMP4 || E.tk == L4_ICMP6)) icmp_norm_at(F, E.t_off, E.tk == L4_ICMP6);
 }
 
+// What the later stages need of the embedded headers, in one word of the
+// parsed header stack: present, IP version and header length, the bytes of
+// the kept extension headers (left out of the ICMP checksum), the transport
+// kind and whether it is a full header.  Offsets follow from the ICMP
+// header's, so they stay right when the serializer moves the stack.
+__device__ __forceinline__ uint32_t emb_pack(const Emb &E) {
+  return 1u | ((uint32_t)(E.net_hlen >> 2) << 4) | ((uint32_t)E.tk << 10) | ((uint32_t)E.full << 14) |
+         ((uint32_t)(E.net == 6) << 15) | ((uint32_t)E.ext_len << 16);
+}
+struct EmbV { int off, net, net_hlen, t_off, t_len, tk; bool full; };
+__device__ __forceinline__ EmbV emb_view(const Frame &F, const Hdr &H) {
+  EmbV e;
+  e.off = H.l4_off + H.l4_hlen;
+  e.net = (H.emb >> 15) & 1 ? 6 : 4;
+  e.net_hlen = (int)((H.emb >> 4) & 15) << 2;
+  e.tk = (int)((H.emb >> 10) & 7);
+  e.full = (H.emb >> 14) & 1;
+  e.t_off = e.off + e.net_hlen + (int)(H.emb >> 16);
+  if (e.tk == L4_NONE) e.t_len = 0;
+  else if (!e.full) e.t_len = F.len - e.t_off;  // a partial header: every remaining byte
+  else if (e.tk == L4_TCP) e.t_len = (F.b(e.t_off + 12) >> 4) * 4;
+  else if (e.tk == L4_UDP) e.t_len = 8;
+  else e.t_len = (e.tk == L4_ICMP4 && (F.b(e.t_off) == 13 || F.b(e.t_off) == 14) && F.b(e.t_off + 1) == 0) ? 20 : 8;
+  return e;
+}
+
 // Headers::parse (net/src/headers/mod.rs:474-578) incl. the MAX_VLANS /
 // MAX_NET_EXTENSIONS quirk.  Returns false if the Ethernet header is invalid.
 __device__ __forceinline__ bool parse(const Frame &F, int hb, Hdr &H) {
   H.hb = hb; H.nvlan = 0; H.net = 0; H.next = 0; H.ext_len = 0; H.l4 = L4_NONE;
   H.vx = false; H.vni = 0; H.net_off = H.net_hlen = 0; H.l4_off = H.l4_hlen = 0; H.vx_off = 0;
+  H.emb = 0;
   int rem = F.len - hb;
   if (rem < 14) return false;
   uint8_t d0 = 0, s0 = F.b(hb + 6), dz = 0, sz = 0;
@@ -509,6 +537,7 @@ __device__ __forceinline__ bool parse(const Frame &F, int hb, Hdr &H) {
       emb_normalize(F, E);
       pos += E.consumed;
       emb_rec = E.rec;
+      H.emb = emb_pack(E);
     }
   }
   H.consumed = pos - hb;
@@ -1223,18 +1252,15 @@ __device__ __forceinline__ uint32_t sum_frame(const Frame &F, int a, int e) {
   return (wa & 1) ? le : bswap16(le);
 }
 
-// An ICMP error message carries embedded headers when its parse consumed
-// bytes past the ICMP header (nothing else follows an ICMP header).
-__device__ __forceinline__ bool has_emb(const Hdr &H) {
-  return (H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) && H.hb + H.consumed > H.l4_off + H.l4_hlen;
-}
+// An ICMP error message whose embedded IP header parsed.
+__device__ __forceinline__ bool has_emb(const Hdr &H) { return H.emb != 0; }
 // Sum (not complemented) of the ICMP checksum input of an error message with
 // embedded headers: the ICMP header (checksum word excluded), then
 // get_payload_for_checksum (icmp_any/checksum.rs:226-259) -- the embedded IP
 // header, the embedded transport header and the payload, WITHOUT the
 // embedded extension headers (as the reference computes it) -- and for
 // ICMPv6 the pseudo header over that length (Icmpv6Type::calc_checksum).
-__device__ DP_COLD uint32_t icmp_err_sum(const Frame &F, const Hdr &H, const Emb &E, int pay_start) {
+__device__ __forceinline__ uint32_t icmp_err_sum(const Frame &F, const Hdr &H, const EmbV &E, int pay_start) {
   const int l = H.l4_off;
   uint64_t t = sum_frame(F, l, l + 2) + sum_frame(F, l + 4, l + H.l4_hlen);  // checksum word out
   t += sum_frame(F, E.off, E.off + E.net_hlen);
@@ -1248,7 +1274,7 @@ __device__ DP_COLD uint32_t icmp_err_sum(const Frame &F, const Hdr &H, const Emb
   return fold(t);
 }
 // IPv4 header checksum of the embedded header as it stands (checksum word out)
-__device__ __forceinline__ uint16_t emb_ipv4_ck(const Frame &F, const Emb &E) {
+__device__ __forceinline__ uint16_t emb_ipv4_ck(const Frame &F, const EmbV &E) {
   const uint64_t t = sum_frame(F, E.off, E.off + 10) + sum_frame(F, E.off + 12, E.off + E.net_hlen);
   return (uint16_t)~fold(t);
 }
@@ -1260,11 +1286,10 @@ __device__ __forceinline__ uint16_t emb_ipv4_ck(const Frame &F, const Emb &E) {
 // (validate_checksums, :71-87; InvalidChecksum) and a flow key -- ports, or
 // an ICMP query identifier (net/src/flows/flow_key.rs:635-660;
 // IcmpErrorIncomplete).  No flow exists, so the packet goes on.
-__device__ DP_COLD uint8_t icmp_error_check(const Frame &F, const Hdr &H, const State &S) {
-  Emb E;
-  const bool v6 = H.l4 == L4_ICMP6;
-  if (!has_emb(H) || !emb_parse(F, H.l4_off + H.l4_hlen, v6, E) || E.tk == L4_NONE)
-    return DP_DONE_ICMP_ERROR_INCOMPLETE;
+__device__ __forceinline__ uint8_t icmp_error_check(const Frame &F, const Hdr &H, const State &S) {
+  if (!has_emb(H)) return DP_DONE_ICMP_ERROR_INCOMPLETE;
+  const EmbV E = emb_view(F, H);
+  if (E.tk == L4_NONE) return DP_DONE_ICMP_ERROR_INCOMPLETE;
   if (!S.src_vni) return DP_DONE_UNROUTABLE;
   if ((uint16_t)~icmp_err_sum(F, H, E, S.pay_start) != F.be16(H.l4_off + 2)) return DP_DONE_INVALID_CHECKSUM;
   if (E.net == 4 && emb_ipv4_ck(F, E) != F.be16(E.off + 10)) return DP_DONE_INVALID_CHECKSUM;
@@ -1715,9 +1740,10 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
 // destination table (find_dst_mapping), with the ports of a TCP / UDP
 // header (full or partial).  q[0]: inner destination, q[1]: inner source.
 // Returns false without an embedded IPv4 header.
-__device__ DP_COLD bool nat_icmp_inner(const Img &g, const Frame &F, const Hdr &H, int32_t st, int32_t dt, NatQ q[2],
-                                       Emb &E) {
-  if (!emb_parse(F, H.l4_off + H.l4_hlen, H.l4 == L4_ICMP6, E) || E.net != 4) return false;
+__device__ __forceinline__ bool nat_icmp_inner(const Img &g, const Frame &F, const Hdr &H, int32_t st, int32_t dt, NatQ q[2],
+                                               EmbV &E) {
+  E = emb_view(F, H);
+  if (E.net != 4) return false;
   const bool hp = E.tk == L4_TCP || E.tk == L4_UDP;
   q[0].ti = st; q[0].addr = F.be32(E.off + 16); q[0].port = hp ? F.be16(E.t_off + 2) : 0;
   q[1].ti = dt; q[1].addr = F.be32(E.off + 12); q[1].port = hp ? F.be16(E.t_off) : 0;
@@ -1749,7 +1775,7 @@ __device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, c
   const uint32_t pre[2] = {P.nsrc, P.ndst};
   nat_find2(g, q, has_p, pre);
   NatQ qi[2];
-  Emb E;
+  EmbV E;
   const bool inner = ie && nat_icmp_inner(g, F, H, st, VR.nat_dst, qi, E);
   const bool inner_p = inner && (E.tk == L4_TCP || E.tk == L4_UDP);
   if ((S.flags & DP_META_REQ_STATIC_NAT_SRC) && !(S.flags & DP_META_NATTED_SRC)) {
@@ -1897,9 +1923,6 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
   const int outer = S.encap ? 14 + (S.o_fam == 4 ? 20 : 40) + 16 : 0;
   const int start = inner_start - outer;
   if (start < -(int)DP_HEADROOM) { S.done = DP_DONE_NO_HEAD_ROOM; return 0; }
-  // an ICMP error message's embedded headers, located before any move
-  Emb E;
-  const bool emb = has_emb(H) && emb_parse(F, H.l4_off + H.l4_hlen, H.l4 == L4_ICMP6, E);
   // the parse-limit quirk consumed headers it did not record: the kept
   // stack moves sh bytes later to end at the payload (back to front)
   const int sh = inner_start - H.hb;
@@ -1909,10 +1932,6 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
     H.hb += sh; H.net_off += sh; H.l4_off += sh; H.vx_off += sh;
 #pragma unroll
     for (int e = 0; e < 3; e++) H.ext_off[e] += sh;
-    if (emb) {
-      E.off += sh; E.t_off += sh;
-      for (int e = 0; e < E.next; e++) E.ext_off[e] += sh;
-    }
   }
   // deparse: rewritten fields and normalised reserved bits
   if (S.eth_dirty) { wput_mac(F, H.hb, S.edst); wput_mac(F, H.hb + 6, S.esrc); }
@@ -1948,7 +1967,8 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
     if (H.vx) wput8(F, H.vx_off, 0x08);
   }
   if (H.net == 4) wput16(F, H.net_off + 10, (uint16_t)~fold(sum_frame(F, H.net_off, H.net_off + H.net_hlen)));
-  if (ck_off >= 0 && emb) {
+  if (ck_off >= 0 && has_emb(H)) {
+    const EmbV E = emb_view(F, H);
     // update_checksums with embedded headers (net/src/headers/mod.rs:906-928):
     // the embedded IPv4 header first (part of the ICMP payload; its transport
     // checksum stays), then the ICMP checksum over get_payload_for_checksum

@@ -1944,4 +1944,20 @@ int dpo_nat_lookup(const dpo_tables_t *t, uint32_t kind, uint32_t src_vni, uint3
 
 uint64_t dpo_hash_bytes(const uint8_t *p, uint32_t len) { return rapid(p, len); }
 
+// Packet::new then Packet::serialize of a frame with no stage in between
+// (the driver's tx of a packet built from an output frame, worker.rs:577):
+// `out` receives the frame the reference would transmit.  Returns its
+// length, or -1 if the frame does not parse (or exceeds `cap`).
+int dpo_reserialize(const uint8_t *frame, uint32_t len, uint8_t *out, uint32_t cap) {
+  Headers h;
+  int c = parse_headers(frame, len, h);
+  if (c < 0) return -1;
+  update_checksums(h, frame + c, len - (uint32_t)c);
+  const int hs = h.size();
+  if ((uint32_t)hs + (len - (uint32_t)c) > cap) return -1;
+  deparse_headers(h, out);
+  memcpy(out + hs, frame + c, len - (uint32_t)c);
+  return hs + (int)(len - (uint32_t)c);
+}
+
 }  // extern "C"

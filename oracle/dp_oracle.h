@@ -66,6 +66,9 @@ int dpo_nat_lookup(const dpo_tables_t *t, uint32_t kind, uint32_t src_vni,
                    uint16_t port, uint8_t *new_addr4, uint16_t *new_port);
 /* rapidhash-style 64-bit hash restatement (parity unpinned). */
 uint64_t dpo_hash_bytes(const uint8_t *p, uint32_t len);
+/* Packet::new + Packet::serialize of one frame (tx of a packet rebuilt from
+ * an output frame); returns the transmitted length or -1. */
+int dpo_reserialize(const uint8_t *frame, uint32_t len, uint8_t *out, uint32_t cap);
 
 #ifdef __cplusplus
 }

@@ -40,6 +40,8 @@ def lib() -> C.CDLL:
         l.dpo_checksum_ipv4_header.restype = C.c_uint16
         l.dpo_hash_bytes.argtypes = [V, C.c_uint32]
         l.dpo_hash_bytes.restype = C.c_uint64
+        l.dpo_reserialize.argtypes = [V, C.c_uint32, V, C.c_uint32]
+        l.dpo_reserialize.restype = C.c_int
         _lib = l
     return _lib
 
@@ -77,3 +79,10 @@ class Oracle:
             self.close()
         except Exception:
             pass
+
+
+def reserialize(frame: bytes) -> bytes | None:
+    """Packet::new + Packet::serialize of one frame (None: does not parse)."""
+    out = (C.c_uint8 * (len(frame) + 256))()
+    n = lib().dpo_reserialize(frame, len(frame), out, len(out))
+    return None if n < 0 else bytes(out[:n])
