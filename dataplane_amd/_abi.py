@@ -168,7 +168,11 @@ STRUCTS = dict(dp_ipaddr_t=IpAddr, dp_prefix_t=Prefix, dp_fib_t=Fib, dp_vni_fib_
 GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_publish",
                "dp_tables_genid", "dp_process_burst", "dp_process_burst_device",
                "dp_process_burst_sharded", "dp_ctx_synchronize", "dp_tables_device_bytes",
-               "dp_last_error"]
+               "dp_last_error", "dp_ctx_set_option"]
+
+# dp_ctx_set_option (include/dpgpu.h)
+OPT_HOST_PATH = 1
+HOST_AUTO, HOST_COPY, HOST_ZERO_COPY = 0, 1, 2
 
 _VP = C.c_void_p
 _U8P = C.POINTER(C.c_uint8)
@@ -204,6 +208,7 @@ def gpu_lib() -> C.CDLL:
         lib.dp_tables_device_bytes.argtypes = [_VP]
         lib.dp_tables_device_bytes.restype = C.c_uint64
         lib.dp_last_error.restype = C.c_char_p
+        lib.dp_ctx_set_option.argtypes = [_VP, C.c_int, C.c_int64]
         if lib.dp_abi_version() != ABI_VERSION:
             raise RuntimeError("libdpgpu.so ABI version mismatch")
         _gpu = lib

@@ -29,7 +29,10 @@ namespace {
 
 using namespace dpd;
 
-constexpr int TPB = 128;
+#ifndef DP_TPB
+#define DP_TPB 128
+#endif
+constexpr int TPB = DP_TPB;  // work-items (packets) per workgroup
 // LDS pointers carry their address space explicitly so every access is a
 // ds_read/ds_write (a generic pointer would turn them into flat loads)
 #ifdef DP_EMU

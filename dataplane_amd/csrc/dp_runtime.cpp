@@ -154,6 +154,7 @@ struct dp_ctx {
   hipStream_t hs[kHostStreams] = {};   // host-path copy/compute streams
   hipEvent_t hev[kHostStreams + 1] = {};
   bool host_streams = false;
+  int host_path = DP_HOST_AUTO;        // dp_ctx_set_option(DP_OPT_HOST_PATH)
 };
 
 namespace {
@@ -340,6 +341,29 @@ int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
   return 0;
 }
 
+// The device-visible address of pinned, device-mapped host memory (the
+// caller's hipHostMalloc'd / registered buffers), nullptr for anything else.
+static void *mapped_ptr(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+  const char *base = static_cast<const char *>(a.hostPointer ? a.hostPointer : p);
+  return static_cast<char *>(a.devicePointer) + (static_cast<const char *>(p) - base);
+}
+
+int dp_ctx_set_option(dp_ctx_t *c, int option, int64_t value) {
+  if (!c) return fail(DP_EINVAL, "null ctx");
+  if (option == DP_OPT_HOST_PATH) {
+    if (value < DP_HOST_AUTO || value > DP_HOST_ZERO_COPY) return fail(DP_EINVAL, "bad host path mode");
+    c->host_path = (int)value;
+    return 0;
+  }
+  return fail(DP_EINVAL, "unknown option");
+}
+
 int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt_in_t *in,
                      dp_pkt_out_t *out, uint32_t n, uint64_t *stats) {
   if (!c) return fail(DP_EINVAL, "null ctx");
@@ -359,6 +383,33 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     mark_failed_host(in, out, n);
     return fail(rc, what, err);
   };
+  // Zero-copy: when the burst buffer and both record arrays are pinned,
+  // device-mapped host memory, the kernel reads the frames and records over
+  // PCIe and writes the rewritten header spans and out records back in place
+  // -- only the bytes the path touches cross the link (window chunks in, the
+  // rewritten span and the 32-byte record out), no staging copies.
+  if (c->host_path != DP_HOST_COPY) {
+    uint64_t end = 0;
+    for (uint32_t i = 0; i < n; i++) end = std::max<uint64_t>(end, ((uint64_t)in[i].off + in[i].len + 15) & ~15ull);
+    uint8_t *db = static_cast<uint8_t *>(mapped_ptr(buf));
+    const dp_pkt_in_t *din = static_cast<const dp_pkt_in_t *>(mapped_ptr(in));
+    dp_pkt_out_t *dout = static_cast<dp_pkt_out_t *>(mapped_ptr(out));
+    const bool zc = db && din && dout && !((uintptr_t)db & 15) && end <= buf_bytes;
+    if (zc) {
+      hipStream_t s = c->stream;
+      if (stats && (e = hipMemsetAsync(c->d_stats, 0, sizeof(uint64_t) * DP_DONE_COUNT, s)) != hipSuccess)
+        return bail(DP_EIO, "memset stats", e);
+      int rc = dp_process_burst_device(c, db, buf_bytes, din, dout, n, stats ? c->d_stats : nullptr, s);
+      uint64_t hstats[DP_DONE_COUNT];
+      if (!rc && stats && (e = hipMemcpyAsync(hstats, c->d_stats, sizeof(hstats), hipMemcpyDeviceToHost, s)) != hipSuccess)
+        rc = fail(DP_EIO, "D2H stats", e);
+      if ((e = hipStreamSynchronize(s)) != hipSuccess && !rc) rc = fail(DP_EIO, "stream sync", e);
+      if (rc) { mark_failed_host(in, out, n); return rc; }
+      if (stats) for (int k = 0; k < DP_DONE_COUNT; k++) stats[k] += hstats[k];
+      return 0;
+    }
+    if (c->host_path == DP_HOST_ZERO_COPY) return bail(DP_EINVAL, "zero-copy needs pinned, mapped, 16-byte aligned buffers", hipSuccess);
+  }
   uint64_t need = ((buf_bytes + 15) & ~15ull) + 16;
   if (need > c->d_buf_cap) {
     if (c->d_buf) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->d_buf); }

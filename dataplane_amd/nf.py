@@ -102,6 +102,11 @@ class GpuPathNf:
                 p.frame = bytes(buf[r["off"]:r["off"] + r["len"]])
         return iter(burst)
 
+    def set_host_path(self, mode: int) -> None:
+        """dp_ctx_set_option(DP_OPT_HOST_PATH): A.HOST_AUTO / HOST_COPY / HOST_ZERO_COPY."""
+        A.check(self.lib.dp_ctx_set_option(self.ctx, A.OPT_HOST_PATH, mode), "dp_ctx_set_option",
+                self.lib)
+
     def process_arrays(self, buf: np.ndarray, inp: np.ndarray,
                        stats: Optional[np.ndarray] = None,
                        out: Optional[np.ndarray] = None) -> np.ndarray:

@@ -446,6 +446,25 @@ int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf
 /* Wait for the context's stream. */
 int dp_ctx_synchronize(dp_ctx_t *ctx);
 
+/* Context options (dp_ctx_set_option). */
+enum dp_ctx_option {
+    /* How dp_process_burst moves a host-origin burst:
+     *   DP_HOST_AUTO      zero-copy when `buf`, `in` and `out` are all pinned,
+     *                     device-mapped host memory (hipHostMalloc /
+     *                     hipHostRegister) and `buf` is 16-byte aligned with
+     *                     every frame end rounded up to 16 inside buf_bytes;
+     *                     otherwise staged copies (default);
+     *   DP_HOST_COPY      staged copies: each chunk's slot span and records
+     *                     H2D, kernel, D2H, chunks overlapped on 3 streams;
+     *   DP_HOST_ZERO_COPY zero-copy only: the kernel reads the frames and
+     *                     records over PCIe and writes the rewritten header
+     *                     spans and records back in place; a burst that does
+     *                     not qualify fails with DP_EINVAL. */
+    DP_OPT_HOST_PATH = 1
+};
+enum dp_host_path { DP_HOST_AUTO = 0, DP_HOST_COPY = 1, DP_HOST_ZERO_COPY = 2 };
+int dp_ctx_set_option(dp_ctx_t *ctx, int option, int64_t value);
+
 /* Introspection: bytes of the device table image and its parts (for
  * DESIGN.md / bench), and the last HIP error string. */
 uint64_t dp_tables_device_bytes(const dp_ctx_t *ctx);

@@ -112,6 +112,47 @@ def test_gpu_device_path_and_determinism(nf):
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("mode", ["copy", "zero_copy", "auto"])
+def test_gpu_host_paths_pinned(nf, mode):
+    """dp_process_burst on pinned host buffers in each host-path mode
+    (dp_ctx_set_option): chunked staging copies, and the kernel working on
+    the mapped host frames directly.  Same bytes and records either way."""
+    import torch
+    m = {"copy": A.HOST_COPY, "zero_copy": A.HOST_ZERO_COPY, "auto": A.HOST_AUTO}[mode]
+    w = Workload(2, 150000, seed=91, n_routes_v4=50000, n_acl=2000, n_nat=64, tcp_percent=30,
+                 layout="dpdk")
+    nf.publish(w.tables)
+    b_ref = w.fresh_buf()
+    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+
+    def pinned(nbytes):
+        return torch.empty(nbytes, dtype=torch.uint8).pin_memory().numpy()
+    pb = pinned(w.buf.nbytes)
+    pb[:] = w.fresh_buf()
+    pi = pinned(w.inp.nbytes).view(A.PKT_IN)
+    pi[:] = w.inp
+    po = pinned(w.n * A.PKT_OUT.itemsize).view(A.PKT_OUT)
+    nf.set_host_path(m)
+    try:
+        o = nf.process_arrays(pb, pi, out=po)
+    finally:
+        nf.set_host_path(A.HOST_AUTO)
+    compare(o_ref, b_ref, o, pb, w.inp, f"host path {mode}")
+
+
+def test_gpu_zero_copy_rejects_pageable(nf):
+    """Forcing zero copy on pageable (unmapped) buffers fails with an error
+    instead of falling back silently."""
+    w = Workload(1, 1024, seed=3)
+    nf.publish(w.tables)
+    nf.set_host_path(A.HOST_ZERO_COPY)
+    try:
+        with pytest.raises(RuntimeError):
+            nf.process_arrays(w.fresh_buf(), w.inp)
+    finally:
+        nf.set_host_path(A.HOST_AUTO)
+
+
 def test_gpu_republish_and_empty(nf, edge):
     """A burst after dp_tables_publish sees the new generation; n == 0 is a
     no-op; offsets outside the buffer contract are InternalFailure and touch
