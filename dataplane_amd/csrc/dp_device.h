@@ -59,6 +59,9 @@ struct Lpm {
   uint64_t direct;     // offset of uint32_t[1 << dbits]; bit31 = leaf(nh) else node idx
   uint32_t dbits;      // direct-pointing bits (16..24)
   uint32_t width;      // 32 or 128
+  uint64_t blocks;     // != 0: DIR-24-8 -- a non-leaf direct entry is the index of a
+                       // uint16_t[256] block of next hops for the last 8 bits (v4 with a
+                       // 24-bit direct table); 0: Poptrie nodes below the direct table
 };
 
 struct FibRec {
@@ -169,9 +172,10 @@ struct alignas(16) PairRec {  // 128 B
   Mbi ffl4;            // index of the v4 local group (candidate-list form)
   Mbi acl4;            // index of the v4 ACL group (candidate-list form)
   Mbi nsrc;            // index of the NAT src table
-  uint64_t lpm4_direct;  // the dst FIB's v4 LPM (Lpm.direct / dbits), 0: none
+  uint64_t lpm4_direct;  // the dst FIB's v4 LPM (Lpm.direct / dbits / blocks), 0: none
   uint32_t lpm4_dbits;
   uint32_t pad;
+  uint64_t lpm4_blocks;
 };
 static_assert(sizeof(PairRec) == 128, "PairRec is 128 B");
 

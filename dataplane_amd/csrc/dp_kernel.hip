@@ -42,6 +42,17 @@ constexpr int TPB = DP_TPB;  // work-items (packets) per workgroup
 #endif
 typedef LDS_AS uint8_t lds_u8;
 typedef LDS_AS uint32_t lds_u32;
+// Dependent-load round trips per packet and stage (host emulation only,
+// -DDP_TRIPS; scripts/trips.py): the chain-length model of the kernel.
+#if defined(DP_EMU) && defined(DP_TRIPS)
+thread_local uint16_t dp_trip[8];
+thread_local int dp_trip_st;
+#define TRIP_ST(x) (dp_trip_st = (x))
+#define TRIP() (dp_trip[dp_trip_st]++)
+#else
+#define TRIP_ST(x) ((void)0)
+#define TRIP() ((void)0)
+#endif
 // Optional per-stage wave timing (build with -DDP_TIMING; scripts/stage_timing.py)
 #if defined(DP_TIMING) && !defined(DP_EMU)
 __device__ unsigned long long g_stage_cycles[16];
@@ -94,6 +105,7 @@ __device__ __forceinline__ bool hash_find(const Img &g, const HashMap &m, uint32
   uint32_t key2 = k2 | 0x80000000u;
   uint32_t i = hmix(k0, k1, k2) & m.mask;
   for (uint32_t probe = 0; probe <= m.mask; probe++) {
+    TRIP();
     HashSlot e = s[i];
     if (!(e.k2 & 0x80000000u)) return false;
     if (e.k0 == k0 && e.k1 == k1 && e.k2 == key2) { val = e.val; return true; }
@@ -112,11 +124,20 @@ struct Frame {
   uint8_t *g;       // frame start in HBM
   int shift;        // frame start & 15
   int len;
+  // The whole frame is inside the window (shift + len <= WIN): every read is
+  // an LDS read.  process_packet is inlined twice, with this a compile-time
+  // true and false; a wave whose frames all fit runs the first copy, which
+  // has none of the per-byte window tests and HBM fallbacks.
+  bool inwin;
   // The LDS read is unconditional (clamped index) so the compiler keeps it a
   // ds_read and never fuses the two loads into one generic (flat) load
   // through a select of pointers; the HBM read stays behind a branch.
   __device__ __forceinline__ uint8_t b(int f) const {
     int o = shift + f;
+#ifdef DP_EMU
+    if (inwin && (o < 0 || o >= WIN)) __builtin_trap();
+#endif
+    if (inwin) return lds[o];
     uint8_t v = lds[o < WIN ? o : 0];
     if (o >= WIN) v = g[f];
     return v;
@@ -750,11 +771,15 @@ __device__ __forceinline__ uint32_t key6(uint64_t hi, uint64_t lo, int off) {
   return (uint32_t)(x >> 58);
 }
 
-__device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t direct_off, uint32_t dbits, const Addr16 &a) {
+__device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t direct_off, uint32_t dbits, uint64_t blocks,
+                                             const Addr16 &a) {
   const uint32_t *direct = g.at<uint32_t>(direct_off);
   const uint32_t idx = a.w[0] >> (32 - dbits);  // dbits <= 32 for both families
   uint32_t e = direct[idx];
+  TRIP();
   if (e & 0x80000000u) return e & 0x7fffffffu;
+  TRIP();
+  if (blocks) return g.at<uint16_t>(blocks)[(e << 8) | (a.w[0] & 0xff)];  // DIR-24-8 (v4)
   const PtNode *nodes = g.at<PtNode>(g.im.pt_nodes);
   const uint32_t *leaves = g.at<uint32_t>(g.im.pt_leaves);
   int off = (int)dbits;
@@ -762,6 +787,7 @@ __device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t direct_off, 
   const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1], klo = ((uint64_t)a.w[2] << 32) | a.w[3];
   for (int guard = 0; guard < 24; guard++) {
     const PtNode &nd = nodes[ni];
+    TRIP();
     uint64_t vec = nd.vec, lv = nd.leafvec;
     uint32_t v = key6(khi, klo, off);
     uint64_t bit = 1ull << v;
@@ -776,7 +802,7 @@ __device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t direct_off, 
   return g.im.drop_nh;  // unreachable for a well-formed image
 }
 __device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
-  return lpm_walk(g, L.direct, L.dbits, a);
+  return lpm_walk(g, L.direct, L.dbits, L.blocks, a);
 }
 
 // Multibit index walk from a context record's descriptor (Mbi): leaf value
@@ -784,9 +810,10 @@ __device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const
 __device__ __forceinline__ uint32_t mbi_walk(const Img &g, const Mbi &m, uint32_t key) {
   const int rem0 = (int)m.kbits - (int)m.s0;
   uint32_t e = g.at<uint32_t>(m.root)[key >> rem0];
+  TRIP();
 #pragma unroll
   for (int l = 1; l <= 3; l++)
-    if (!(e & DPD_LEAF)) e = g.at<uint32_t>(m.blocks)[(e << 8) | ((key >> (rem0 - 8 * l)) & 0xff)];
+    if (!(e & DPD_LEAF) && (TRIP(), true)) e = g.at<uint32_t>(m.blocks)[(e << 8) | ((key >> (rem0 - 8 * l)) & 0xff)];
   return e & ~DPD_LEAF;
 }
 
@@ -810,9 +837,11 @@ __device__ __forceinline__ uint32_t field_leaf(const Img &g, const FieldIdx &F, 
   if (F.root) {
     uint32_t k = (uint32_t)key.lo;
     uint32_t e = g.at<uint32_t>(F.root)[k >> (F.kbits - F.s0)];
+    TRIP();
 #pragma unroll
     for (int l = 1; l <= 3; l++) {
       if (!(e & DPD_LEAF)) {
+        TRIP();
         int rem = (int)F.kbits - (int)F.s0 - 8 * l;
         e = g.at<uint32_t>(F.blocks)[(e << 8) | ((k >> rem) & 0xff)];
       }
@@ -828,6 +857,7 @@ __device__ __forceinline__ uint32_t field_leaf(const Img &g, const FieldIdx &F, 
   }
   const uint64_t *bd = g.at<uint64_t>(F.bounds);
   while (hi - lo > 1) {
+    TRIP();
     uint32_t mid = (lo + hi) >> 1;
     uint64_t bh = bd[2 * (uint64_t)mid], bl = bd[2 * (uint64_t)mid + 1];
     bool le = bh < key.hi || (bh == key.hi && bl <= key.lo);
@@ -961,6 +991,7 @@ __device__ __forceinline__ Hit verify_run(const Img &g, uint64_t recs, uint32_t 
     };
 #pragma unroll 1
     for (uint32_t c = 0; c < cnt; c += 2) {
+      TRIP();
       // named registers, not an array: a dynamically indexed array would live in scratch
       const uint4 z = make_uint4(0, 0, 0, 0);
       const uint4 *q = R + 2 * c;
@@ -993,6 +1024,7 @@ __device__ __forceinline__ Hit verify_run(const Img &g, uint64_t recs, uint32_t 
   };
 #pragma unroll 1
   for (uint32_t c = 0; c < cnt; c += 2) {
+    TRIP();
     const uint4 *a = R + 4 * c;
     const uint4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
     uint4 b0 = make_uint4(0, 0, 0, 0), b1 = b0, b2 = make_uint4(0, 0, 0, 0), b3 = b0;
@@ -1066,14 +1098,17 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
       e[k] = DPD_LEAF | pre[k];       // multibit walk done by hoist_walks
       T[k].root = 1; T[k].n = 1;
     } else if (q[k].ti >= 0) {
+      TRIP();
       T[k] = tabs[q[k].ti];
       if (T[k].root) e[k] = g.at<uint32_t>(T[k].root)[q[k].addr >> (32 - T[k].s0)];
       else hi[k] = T[k].n;
     }
   }
   // multibit levels / small bounds search
+  if ((!(e[0] & DPD_LEAF) && q[0].ti >= 0) || (!(e[1] & DPD_LEAF) && q[1].ti >= 0)) TRIP();
 #pragma unroll
   for (int l = 1; l <= 3; l++) {
+    if (!(e[0] & DPD_LEAF) || !(e[1] & DPD_LEAF)) TRIP();
 #pragma unroll
     for (int k = 0; k < 2; k++)
       if (!(e[k] & DPD_LEAF))
@@ -1089,6 +1124,7 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
         any = true;
       }
     if (!any) break;
+    TRIP();
   }
 #pragma unroll
   for (int k = 0; k < 2; k++) {
@@ -1100,6 +1136,7 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
   bool fin[2] = {false, false};
   for (int it = 0; it < 33; it++) {
     bool any = false;
+    if ((ei[0] >= 0 && !fin[0]) || (ei[1] >= 0 && !fin[1])) TRIP();
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       if (ei[k] < 0 || fin[k]) continue;
@@ -1129,6 +1166,7 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
     live[k] = ei[k] >= 0;
     rl[k] = 0; rh[k] = 0; eo[k] = 0; prlo[k] = 0;
     if (!live[k]) continue;
+    if (E[k].is_pat) TRIP();
     const uint32_t addr = q[k].addr;
     const uint64_t ip_off = (uint64_t)(addr - E[k].net);
     const uint64_t esize = ((uint64_t)E[k].size_hi << 32) | E[k].size_lo;
@@ -1162,6 +1200,7 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       if (!live[k] || rl[k] >= rh[k]) continue;
+      if (k == 0 || !(live[0] && rl[0] < rh[0])) TRIP();
       uint32_t m = (rl[k] + rh[k]) >> 1;
       const NatRange &R = ranges[E[k].first_range + m];
       bool le = E[k].is_pat ? (R.olo_ip < q[k].addr || (R.olo_ip == q[k].addr && R.olo_port <= q[k].port))
@@ -1182,6 +1221,7 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
       R.tlo_ip = E[k].tlo_ip; R.thi_ip = E[k].thi_ip; R.tlo_port = E[k].tlo_port; R.thi_port = E[k].thi_port;
       R.offset = E[k].offset;
     } else {
+      TRIP();
       R = ranges[E[k].first_range + sel];
     }
     const uint32_t addr = q[k].addr;
@@ -1229,7 +1269,7 @@ __device__ __forceinline__ uint32_t sum_frame(const Frame &F, int a, int e) {
   const uint8_t *gbase = F.g - F.shift;  // 16-aligned HBM address of window pos 0
   for (int d = d0; d < d1; d += 4) {
     uint32_t w;
-    if (d + 4 <= WIN) w = *reinterpret_cast<const lds_u32 *>(F.lds + d);
+    if (F.inwin || d + 4 <= WIN) w = *reinterpret_cast<const lds_u32 *>(F.lds + d);
     else {
       // whole 16-byte chunks from HBM when possible
       if ((d & 15) == 0 && d + 16 <= d1) {
@@ -1343,6 +1383,7 @@ __device__ __forceinline__ int32_t find_vni(const Img &g, uint32_t vni) {
   const uint32_t mask = g.im.vni_mask;
   uint32_t i = hmix(vni, 0, 0) & mask;
   for (uint32_t probe = 0; probe <= mask; probe++) {
+    TRIP();
     const uint32_t k = slots[i].vni;
     if (k == vni) return (int32_t)i;
     if (k == 0) return -1;
@@ -1529,7 +1570,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   bool had_vrf = S.has_vrf;
   uint32_t vrf0 = S.vrf;
   int32_t fi;
-  uint64_t d4 = 0;   // the dst FIB's v4 LPM, read from the pair context (no FibRec load)
+  uint64_t d4 = 0, k4 = 0;   // the dst FIB's v4 LPM, read from the pair context (no FibRec load)
   uint32_t b4 = 0;
   if (S.dst_vni) {
     if (H.net == 0 && !S.encap) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
@@ -1539,6 +1580,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
       fi = PR.dst_fib;
       d4 = PR.lpm4_direct;
       b4 = PR.lpm4_dbits;
+      k4 = PR.lpm4_blocks;
     } else {
       const int32_t vi = find_vni(g, S.dst_vni);
       fi = vi >= 0 ? (int32_t)g.at<VniRec>(g.im.vni_slots)[vi].fib : -1;
@@ -1556,7 +1598,8 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   const FibRec &fb = g.at<FibRec>(g.im.fibs)[fi];  // fields read where used (no struct copy)
   uint8_t fam; Addr16 dst;
   cur_dst(F, H, S, fam, dst);
-  const uint32_t nhi = (fam == 4 && d4) ? lpm_walk(g, d4, b4, dst) : lpm_lookup(g, fam == 4 ? fb.v4 : fb.v6, dst);
+  const uint32_t nhi = (fam == 4 && d4) ? lpm_walk(g, d4, b4, k4, dst) : lpm_lookup(g, fam == 4 ? fb.v4 : fb.v6, dst);
+  TRIP();
   const NhRec nr = g.at<NhRec>(g.im.nh_recs)[nhi];
   if (nr.kind != DPD_NH_CHAIN) {
     // a single Egress / Drop instruction, resolved at publish (NhRec)
@@ -1580,6 +1623,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
     idx = (uint32_t)(rapid(hbuf.b, hbuf.n) % nr.n_entries);
   }
   uint32_t ei = nr.entry + idx;
+  TRIP();
   const Entry E = g.at<Entry>(g.im.entries)[ei];
   S.fib_entry = ei;
   const Instr *ins = g.at<Instr>(g.im.instrs) + E.first_instr;
@@ -1665,8 +1709,10 @@ __device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_
     rem0[k] = (int)m[k].kbits - (int)m[k].s0;
     e[k] = m[k].root ? g.at<uint32_t>(m[k].root)[key[k] >> rem0[k]] : DPD_LEAF;
   }
+  TRIP();
 #pragma unroll
   for (int l = 1; l <= 3; l++) {
+    if (!(e[0] & e[1] & e[2] & e[3] & DPD_LEAF)) TRIP();
 #pragma unroll
     for (int k = 0; k < 4; k++)
       if (!(e[k] & DPD_LEAF)) e[k] = g.at<uint32_t>(m[k].blocks)[(e[k] << 8) | ((key[k] >> (rem0[k] - 8 * l)) & 0xff)];
@@ -1697,6 +1743,8 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   uint32_t dvni = rh.action;
   uint32_t dnat = rh.action2;
   int32_t pi = (int32_t)rh.aux;
+  TRIP_ST(3);
+  TRIP();
   int32_t lg = g.at<PairRec>(g.im.pair_recs)[pi].ffl[t];
   if (t == 0) hoist_walks(g, S, pi, P);
   const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, proto, src, Key128{0, 0}, S.sport, 0, P.ffl);
@@ -2015,7 +2063,7 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
 // Per-packet body
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, lds_u8 *hs, uint8_t *buf, uint64_t buf_bytes,
-                                  const dp_pkt_in_t &pin, dp_pkt_out_t &o, int &fl0, int &fl1) {
+                                  const dp_pkt_in_t &pin, dp_pkt_out_t &o, int &fl0, int &fl1, bool inwin) {
   fl0 = fl1 = 0;
   if (!frame_ok(pin, buf_bytes)) {
     // layout contract violated: never touch memory outside the buffer
@@ -2031,6 +2079,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   F.g = buf + pin.off;
   F.shift = (int)(pin.off & 15);
   F.len = pin.len;
+  F.inwin = inwin;
   // the header window is staged in `slab` by the caller (kernel / dpemu_run)
   o.off = pin.off; o.len = pin.len; o.acl = 0; o.oif = 0; o.dst_vni = 0; o.src_vni = 0;
   o.fib_entry = 0xffffffffu; o.acl_rule = 0xffffffffu;
@@ -2053,6 +2102,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   S.ttl = 0; S.v4src = S.v4dst = 0;
   load_fields(F, H, S);
   TS(1);
+  TRIP_ST(1);
   if (pin.flags & DP_IN_SEEDED_OVERLAY) {
     if (!enter_vni(g, S, pin.src_vni)) done(S, DP_DONE_UNROUTABLE);
   } else {
@@ -2067,14 +2117,29 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
     if (r != DONE_NONE) done(S, r);
   }
   Pre P;
+  TRIP_ST(2);
+#ifndef DP_PROBE_NOFF
   stage_flow_filter(g, F, H, S, P);
+#else
+  P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
+#endif
   TS(3);
+  TRIP_ST(4);
+#ifndef DP_PROBE_NOACL
   stage_acl(g, F, H, S, P);
+#endif
   TS(4);
+  TRIP_ST(5);
+#ifndef DP_PROBE_NONAT
   stage_static_nat(g, F, H, S, P);
+#endif
   TS(5);
+  TRIP_ST(6);
+#ifndef DP_PROBE_NOIPF2
   stage_ipforward(g, F, H, S);  // IP-Forward-2
+#endif
   TS(6);
+  TRIP_ST(7);
   stage_egress(g, F, H, S);
   TS(7);
 #ifdef DP_PROBE_NOSER
@@ -2173,13 +2238,17 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__re
   const uint32_t base = pin.off & ~15u;
   const int nch = live && frame_ok(pin, buf_bytes) ? window_chunks(pin) : 0;
   wave_load_windows(buf, slab_wave, base, nch);
+  // wave-uniform: every live frame of the wave lies inside its window
+  const bool all_fit = __ballot(live && (pin.off & 15) + pin.len > (uint32_t)WIN) == 0;
   __syncthreads();
   uint8_t done_code = DONE_NONE;
   int fl0 = 0, fl1 = 0;
   if (live) {
     Img g{img_base, im};
     dp_pkt_out_t o;
-    done_code = process_packet(g, slab, (lds_u8 *)(hash_all + tid * HS), buf, buf_bytes, pin, o, fl0, fl1);
+    lds_u8 *hs = (lds_u8 *)(hash_all + tid * HS);
+    if (all_fit) done_code = process_packet(g, slab, hs, buf, buf_bytes, pin, o, fl0, fl1, true);
+    else done_code = process_packet(g, slab, hs, buf, buf_bytes, pin, o, fl0, fl1, false);
     out[i] = o;
   }
   __syncthreads();
@@ -2224,6 +2293,9 @@ __global__ void __launch_bounds__(DPD_STAT_SLOTS) dp_stats_reduce(unsigned long 
 }  // namespace
 
 #ifdef DP_EMU
+#ifdef DP_TRIPS
+static uint16_t *dp_trip_out;  // per packet x 8 stages (dpemu_trips_out)
+#endif
 // Host emulation entry (tests/emu only): runs the per-packet body serially.
 extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
                           uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n) {
@@ -2231,6 +2303,10 @@ extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uin
   thread_local uint8_t hs[64];
   Img g{img_base, *reinterpret_cast<const Image *>(image_struct)};
   for (uint32_t i = 0; i < n; i++) {
+#ifdef DP_TRIPS
+    for (int k = 0; k < 8; k++) dp_trip[k] = 0;
+    dp_trip_st = 0;
+#endif
     const int nch = frame_ok(in[i], buf_bytes) ? window_chunks(in[i]) : 0;
     const uint4 *src = reinterpret_cast<const uint4 *>(buf + (in[i].off & ~15u));
     for (int c = 0; c < nch; c++) {
@@ -2239,10 +2315,19 @@ extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uin
       d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
     }
     int fl0, fl1;
-    process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1);
+    const bool fit = (in[i].off & 15) + in[i].len <= (uint32_t)WIN;
+    if (fit) process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, true);
+    else process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, false);
     if (fl1 > fl0) flush_range(buf + (in[i].off & ~15u), slab, fl0, fl1);
+#ifdef DP_TRIPS
+    if (dp_trip_out)
+      for (int k = 0; k < 8; k++) dp_trip_out[8 * (uint64_t)i + k] = dp_trip[k];
+#endif
   }
 }
+#ifdef DP_TRIPS
+extern "C" void dpemu_trips_out(uint16_t *p) { dp_trip_out = p; }
+#endif
 #else
 // Launch wrapper used by the runtime (dp_runtime.cpp).
 #if defined(DP_TIMING)

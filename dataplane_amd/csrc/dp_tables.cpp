@@ -188,6 +188,45 @@ Lpm build_lpm(ImgBuf &ib, PtBuilder &pb, std::vector<PRoute> &routes, int width,
     std::fill(dval.begin() + s0, dval.begin() + s0 + cnt, p->nh);
   }
   for (size_t s = 0; s < dval.size(); s++) direct[s] = 0x80000000u | dval[s];
+  Lpm L{};
+  // v4 with a 24-bit direct table: DIR-24-8, one uint16_t[256] block of
+  // next hops per /24 that holds longer routes -- a lookup is at most two
+  // dependent loads (a Poptrie node walk below the direct table is up to
+  // three: node, node, leaf).  Needs every next hop to fit in 16 bits.
+  uint32_t max_nh = 0;
+  for (auto &r : uniq) max_nh = std::max(max_nh, r.nh);
+#ifdef DP_NO_DIR248
+  max_nh = 0xffffu;
+#endif
+  if (width == 32 && dbits == 24 && max_nh < 0xffffu) {
+    std::vector<uint16_t> blocks;
+    size_t i = 0;
+    while (i < uniq.size()) {
+      if (uniq[i].len <= 24) { i++; continue; }
+      const uint32_t s = kbits(uniq[i].key, 0, 24);
+      std::vector<const PRoute *> sub;
+      size_t j = i;
+      while (j < uniq.size() && kbits(uniq[j].key, 0, 24) == s) {
+        if (uniq[j].len > 24) sub.push_back(&uniq[j]);
+        j++;
+      }
+      std::stable_sort(sub.begin(), sub.end(), [](const PRoute *a, const PRoute *b) { return a->len < b->len; });
+      const size_t base = blocks.size();
+      blocks.resize(base + 256, (uint16_t)dval[s]);
+      for (auto *p : sub) {
+        const uint32_t v0 = kbits(p->key, 24, 8) & ~((1u << (32 - p->len)) - 1);
+        std::fill(blocks.begin() + base + v0, blocks.begin() + base + v0 + (1u << (32 - p->len)), (uint16_t)p->nh);
+      }
+      direct[s] = (uint32_t)(base >> 8);
+      i = j;
+    }
+    if (blocks.empty()) blocks.resize(256, 0);
+    L.blocks = ib.put(blocks);
+    L.direct = ib.put(direct);
+    L.dbits = dbits;
+    L.width = (uint32_t)width;
+    return L;
+  }
   // long routes: one node per direct slot
   size_t i = 0;
   while (i < uniq.size()) {
@@ -205,7 +244,6 @@ Lpm build_lpm(ImgBuf &ib, PtBuilder &pb, std::vector<PRoute> &routes, int width,
     direct[s] = idx;
     i = j;
   }
-  Lpm L{};
   L.direct = ib.put(direct);
   L.dbits = dbits;
   L.width = (uint32_t)width;
@@ -1053,7 +1091,8 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     r.ffl4 = cls_mbi(im.ff_local[0], r.ffl[0]);
     r.acl4 = cls_mbi(im.acl[0], r.acl[0]);
     r.nsrc = nat_mbi(r.nat_src);
-    if (r.dst_fib >= 0) { r.lpm4_direct = fibs[r.dst_fib].v4.direct; r.lpm4_dbits = fibs[r.dst_fib].v4.dbits; }
+    if (r.dst_fib >= 0) { r.lpm4_direct = fibs[r.dst_fib].v4.direct; r.lpm4_dbits = fibs[r.dst_fib].v4.dbits;
+                          r.lpm4_blocks = fibs[r.dst_fib].v4.blocks; }
     uint32_t id = (uint32_t)prs.size();
     pidx[k] = id;
     pkv.push_back(KV{sv, dv, 0, id});

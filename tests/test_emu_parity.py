@@ -28,3 +28,15 @@ def test_emu_matches_oracle(cfg, form, layout, cls_form):
         elif form == "list":
             assert lst > 0
     compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} {form}")
+
+
+@pytest.mark.parametrize("cfg", [2, 4, 5])
+def test_emu_dir24_8(cfg):
+    """More than 64Ki v4 routes: the 24-bit direct table with DIR-24-8 blocks
+    for the /25-/32 routes, on the overlay (pair context) and underlay FIBs."""
+    w = Workload(cfg, 20000, seed=400 + cfg, n_routes_v4=120000, n_routes_v6=4000, n_acl=400,
+                 n_nat=48, tcp_percent=25, layout="dpdk")
+    b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
+    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+    o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT)
+    compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} dir24-8")
