@@ -124,8 +124,9 @@ struct Frame {
   uint8_t *g;       // frame start in HBM
   int shift;        // frame start & 15
   int len;
-  // The whole frame is inside the window (shift + len <= WIN): every read is
-  // an LDS read.  process_packet is inlined twice, with this a compile-time
+  // The whole frame is inside the window (shift + len <= WIN) at an even
+  // window position: every read is an LDS read, and the 16-bit fields (all at
+  // even frame offsets) are single 16-bit LDS accesses.  process_packet is inlined twice, with this a compile-time
   // true and false; a wave whose frames all fit runs the first copy, which
   // has none of the per-byte window tests and HBM fallbacks.
   bool inwin;
@@ -142,8 +143,18 @@ struct Frame {
     if (o >= WIN) v = g[f];
     return v;
   }
-  __device__ __forceinline__ uint16_t be16(int f) const { return (uint16_t)((b(f) << 8) | b(f + 1)); }
+  __device__ __forceinline__ uint16_t be16(int f) const {
+#ifdef DP_EMU
+    if (inwin && (f & 1)) __builtin_trap();
+#endif
+    if (inwin) {
+      const uint32_t x = *reinterpret_cast<const LDS_AS uint16_t *>(lds + shift + f);
+      return (uint16_t)((x << 8) | (x >> 8));
+    }
+    return (uint16_t)((b(f) << 8) | b(f + 1));
+  }
   __device__ __forceinline__ uint32_t be32(int f) const {
+    if (inwin) return ((uint32_t)be16(f) << 16) | be16(f + 2);
     return ((uint32_t)b(f) << 24) | ((uint32_t)b(f + 1) << 16) | ((uint32_t)b(f + 2) << 8) | b(f + 3);
   }
 };
@@ -163,12 +174,31 @@ __device__ __forceinline__ uint8_t mac_b(uint64_t m, int i) { return (uint8_t)(m
 // Frame byte f lives at window position shift + f when 0 <= shift + f < WIN
 // (the LDS copy, written back by flush_window); any other byte is written
 // straight to the burst buffer.  Reads (F.b) see both.
-__device__ __forceinline__ void wput8(const Frame &F, int f, uint32_t v) {
+// wput8_any: any byte of the slot (an encap prepend may start before the
+// frame); wput8: a byte of the frame itself (0 <= f < len), an LDS store
+// with no test when the whole frame is in the window.
+__device__ __forceinline__ void wput8_any(const Frame &F, int f, uint32_t v) {
   const int o = F.shift + f;
   if ((unsigned)o < (unsigned)WIN) F.lds[o] = (uint8_t)v;
   else F.g[f] = (uint8_t)v;
 }
-__device__ __forceinline__ void wput16(const Frame &F, int f, uint32_t v) { wput8(F, f, v >> 8); wput8(F, f + 1, v); }
+__device__ __forceinline__ void wput8(const Frame &F, int f, uint32_t v) {
+#ifdef DP_EMU
+  if (F.inwin && (f < 0 || f >= F.len)) __builtin_trap();
+#endif
+  if (F.inwin) F.lds[F.shift + f] = (uint8_t)v;
+  else wput8_any(F, f, v);
+}
+__device__ __forceinline__ void wput16(const Frame &F, int f, uint32_t v) {
+  if (F.inwin) {
+#ifdef DP_EMU
+    if (f < 0 || f + 2 > F.len || (f & 1)) __builtin_trap();
+#endif
+    *reinterpret_cast<LDS_AS uint16_t *>(F.lds + F.shift + f) = (uint16_t)(((v & 0xff) << 8) | ((v >> 8) & 0xff));
+    return;
+  }
+  wput8(F, f, v >> 8); wput8(F, f + 1, v);
+}
 __device__ __forceinline__ void wput32(const Frame &F, int f, uint32_t v) { wput16(F, f, v >> 16); wput16(F, f + 2, v); }
 
 // ---------------------------------------------------------------------------
@@ -2039,12 +2069,16 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
     wput16(F, ck_off, c);
   }
   if (S.encap) {  // outer Ethernet (Egress), then the outer IP/UDP/VXLAN deparsed at encap
-    wput_mac(F, start, S.odst);
-    wput_mac(F, start + 6, S.osrc);
-    wput16(F, start + 12, S.o_fam == 4 ? 0x0800u : 0x86ddu);
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      wput8_any(F, start + i, mac_b(S.odst, i));
+      wput8_any(F, start + 6 + i, mac_b(S.osrc, i));
+    }
+    wput8_any(F, start + 12, S.o_fam == 4 ? 0x08u : 0x86u);
+    wput8_any(F, start + 13, S.o_fam == 4 ? 0x00u : 0xddu);
     const int nb = 2 * (outer_words(S.o_fam) - 7);
 #pragma unroll 1
-    for (int i = 0; i < nb; i++) wput8(F, start + 14 + i, F.hs[i]);
+    for (int i = 0; i < nb; i++) wput8_any(F, start + 14 + i, F.hs[i]);
   }
   // write-back range: window positions [fl0, fl1) covering [start, end of
   // the stack), widened to whole 16-byte chunks inside [0, min(frame end,
@@ -2239,7 +2273,7 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__re
   const int nch = live && frame_ok(pin, buf_bytes) ? window_chunks(pin) : 0;
   wave_load_windows(buf, slab_wave, base, nch);
   // wave-uniform: every live frame of the wave lies inside its window
-  const bool all_fit = __ballot(live && (pin.off & 15) + pin.len > (uint32_t)WIN) == 0;
+  const bool all_fit = __ballot(live && ((pin.off & 15) + pin.len > (uint32_t)WIN || (pin.off & 1))) == 0;
   __syncthreads();
   uint8_t done_code = DONE_NONE;
   int fl0 = 0, fl1 = 0;
@@ -2315,7 +2349,7 @@ extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uin
       d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
     }
     int fl0, fl1;
-    const bool fit = (in[i].off & 15) + in[i].len <= (uint32_t)WIN;
+    const bool fit = (in[i].off & 15) + in[i].len <= (uint32_t)WIN && !(in[i].off & 1);
     if (fit) process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, true);
     else process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, false);
     if (fl1 > fl0) flush_range(buf + (in[i].off & ~15u), slab, fl0, fl1);

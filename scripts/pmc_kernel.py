@@ -1,6 +1,7 @@
 # Summarise rocprofv3 --pmc CSVs: per-dispatch mean of each counter for one
 # kernel (default dp_pipeline_kernel), over every pass directory given.
 import csv
+import glob
 import sys
 from collections import defaultdict
 
@@ -8,7 +9,8 @@ from collections import defaultdict
 def summarise(dirs, kernel="dp_pipeline_kernel"):
     vals = defaultdict(lambda: defaultdict(float))
     for d in dirs:
-        for row in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+        files = glob.glob(f"{d}/**/run_counter_collection.csv", recursive=True)
+        for row in (r for f in files for r in csv.DictReader(open(f))):
             if kernel not in row["Kernel_Name"]:
                 continue
             vals[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
