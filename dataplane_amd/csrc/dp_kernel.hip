@@ -73,6 +73,9 @@ __device__ unsigned long long g_stage_cycles[16];
 #ifndef DP_HS
 #define DP_HS 60
 #endif
+#ifndef DP_CAND4
+#define DP_CAND4 2  // v4 classifier candidates fetched per round trip (2 or 4; 4 measured slower)
+#endif
 #ifndef DP_WAVES
 #define DP_WAVES 3
 #endif
@@ -792,12 +795,11 @@ __device__ __forceinline__ void hash_ip_fields(const Frame &F, const Hdr &H, con
 // ---------------------------------------------------------------------------
 // 6 bits of the key at [off, off+6), zero-padded past the address width
 // (v4 keys carry zeros in w[1..3]); the key is held as two u64 halves.
+// bits [off, off + 6) of the 128-bit key (hi:lo), zero past bit 127 -- selects, no branches
 __device__ __forceinline__ uint32_t key6(uint64_t hi, uint64_t lo, int off) {
-  uint64_t x;
-  if (off == 0) x = hi;
-  else if (off < 64) x = (hi << off) | (lo >> (64 - off));
-  else if (off < 128) x = lo << (off - 64);
-  else x = 0;
+  const int o = off & 63;
+  uint64_t x = off < 64 ? (hi << o) | ((lo >> 1) >> (63 - o)) : lo << o;
+  if (off >= 128) x = 0;
   return (uint32_t)(x >> 58);
 }
 
@@ -1006,8 +1008,8 @@ __device__ __forceinline__ Hit verify_run(const Img &g, uint64_t recs, uint32_t 
   Hit h{-1, 0, 0, 0, 0};
   const uint32_t first = run >> DPD_RUN_BITS, cnt = run & DPD_RUN_MAX;
   if (!v6) {
-    // v4: 32-byte records (CandRec4), two candidates per round trip -- their
-    // four 16-byte words are requested together (one or two sectors)
+    // v4: 32-byte records (CandRec4), DP_CAND4 candidates per round trip --
+    // their 16-byte words are requested together
     const uint4 *R = g.at<uint4>(recs) + 2 * (uint64_t)first;
     const uint32_t s = (uint32_t)src.lo, d = (uint32_t)dst.lo;
     auto match4 = [&](const uint4 &w0, const uint4 &w1) -> bool {
@@ -1020,17 +1022,25 @@ __device__ __forceinline__ Hit verify_run(const Img &g, uint64_t recs, uint32_t 
       return true;
     };
 #pragma unroll 1
-    for (uint32_t c = 0; c < cnt; c += 2) {
+    for (uint32_t c = 0; c < cnt; c += DP_CAND4) {
       TRIP();
       // named registers, not an array: a dynamically indexed array would live in scratch
       const uint4 z = make_uint4(0, 0, 0, 0);
       const uint4 *q = R + 2 * c;
       const uint4 a0 = q[0], a1 = q[1];
       const uint4 b0 = c + 1 < cnt ? q[2] : z, b1 = c + 1 < cnt ? q[3] : z;
+#if DP_CAND4 == 4
+      const uint4 c0 = c + 2 < cnt ? q[4] : z, c1 = c + 2 < cnt ? q[5] : z;
+      const uint4 d0 = c + 3 < cnt ? q[6] : z, d1 = c + 3 < cnt ? q[7] : z;
+#endif
       uint4 hit = z;
       bool found = true;
       if (match4(a0, a1)) hit = a1;
       else if (c + 1 < cnt && match4(b0, b1)) hit = b1;
+#if DP_CAND4 == 4
+      else if (c + 2 < cnt && match4(c0, c1)) hit = c1;
+      else if (c + 3 < cnt && match4(d0, d1)) hit = d1;
+#endif
       else found = false;
       if (found) {
         h.rule = hit.w; h.action = hit.y; h.action2 = hit.z; h.orig = hit.z; h.aux = hit.w;
@@ -1268,9 +1278,13 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
       uint64_t tpl = (uint64_t)R.thi_port - R.tlo_port + 1;
       uint64_t tip = (uint64_t)R.thi_ip - R.tlo_ip + 1;
       if (o2 >= tip * tpl) continue;
-      uint16_t np = (uint16_t)(R.tlo_port + (o2 % tpl));
+      // o2 / tpl, o2 % tpl (tpl <= 65536): 32-bit division unless o2 needs more
+      uint64_t dq;
+      if (!(o2 >> 32)) dq = (uint32_t)o2 / (uint32_t)tpl;
+      else dq = o2 / tpl;
+      uint16_t np = (uint16_t)(R.tlo_port + (o2 - dq * tpl));
       if (np == 0) continue;
-      q[k].na = R.tlo_ip + (uint32_t)(o2 / tpl);
+      q[k].na = R.tlo_ip + (uint32_t)dq;
       q[k].np = np;
       q[k].hp = true;
       q[k].ok = true;
@@ -1281,9 +1295,14 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
 // ---------------------------------------------------------------------------
 // One's complement sums
 // ---------------------------------------------------------------------------
+// one's complement fold of a 64-bit sum to 16 bits (fixed steps, no loop:
+// <= 2^33 after the first, <= 0x2fffe, <= 0x10001, <= 0xffff)
 __device__ __forceinline__ uint32_t fold(uint64_t s) {
-  while (s >> 16) s = (s & 0xffff) + (s >> 16);
-  return (uint32_t)s;
+  s = (s & 0xffffffffull) + (s >> 32);
+  uint32_t v = (uint32_t)(s & 0xffff) + (uint32_t)(s >> 16);
+  v = (v & 0xffff) + (v >> 16);
+  v = (v & 0xffff) + (v >> 16);
+  return v;
 }
 __device__ __forceinline__ uint16_t bswap16(uint32_t v) { return (uint16_t)(((v & 0xff) << 8) | ((v >> 8) & 0xff)); }
 
