@@ -517,6 +517,51 @@ __device__ __forceinline__ EmbV emb_view(const Frame &F, const Hdr &H) {
   return e;
 }
 
+// The generic loop's result for the dominant shapes -- Ethernet + IPv4 /
+// IPv6 without extension headers + UDP (not to the VXLAN port) / TCP --
+// computed straight-line; false: not such a frame, run the loop.
+__device__ __forceinline__ bool parse_fast(const Frame &F, int hb, Hdr &H) {
+  const int pos = hb + 14;
+  const int rem = F.len - pos;
+  const uint16_t et = F.be16(hb + 12);
+  int nhl, proto;
+  if (et == 0x0800) {
+    if (rem < 20) return false;
+    const uint8_t v = F.b(pos);
+    nhl = (v & 0xf) * 4;
+    if ((v >> 4) != 4 || nhl < 20 || rem < nhl || F.be16(pos + 2) < nhl) return false;
+    const uint32_t src = F.be32(pos + 12);
+    if ((src >> 28) == 0xe || src == 0xffffffffu) return false;
+    proto = F.b(pos + 9);
+  } else if (et == 0x86dd) {
+    if (rem < 40 || (F.b(pos) >> 4) != 6 || F.b(pos + 8) == 0xff) return false;
+    nhl = 40;
+    proto = F.b(pos + 6);
+  } else {
+    return false;
+  }
+  const int lp = pos + nhl, lrem = F.len - lp;
+  int lhl;
+  if (proto == 17) {
+    if (lrem < 8 || F.be16(lp) == 0 || F.be16(lp + 2) == 0 || F.be16(lp + 2) == 4789) return false;
+    lhl = 8;
+    H.l4 = L4_UDP;
+  } else if (proto == 6) {
+    if (lrem < 20) return false;
+    lhl = (F.b(lp + 12) >> 4) * 4;
+    if (lhl < 20 || lrem < lhl || F.be16(lp) == 0 || F.be16(lp + 2) == 0) return false;
+    H.l4 = L4_TCP;
+  } else {
+    return false;
+  }
+  H.net = et == 0x0800 ? 4 : 6;
+  H.net_off = pos; H.net_hlen = nhl;
+  H.l4_off = lp; H.l4_hlen = lhl;
+  H.consumed = lp + lhl - hb;
+  H.size = 14 + nhl + lhl;
+  return true;
+}
+
 // Headers::parse (net/src/headers/mod.rs:474-578) incl. the MAX_VLANS /
 // MAX_NET_EXTENSIONS quirk.  Returns false if the Ethernet header is invalid.
 __device__ __forceinline__ bool parse(const Frame &F, int hb, Hdr &H) {
@@ -529,6 +574,8 @@ __device__ __forceinline__ bool parse(const Frame &F, int hb, Hdr &H) {
   for (int i = 0; i < 6; i++) { uint8_t x = F.b(hb + i); dz |= x; if (i == 0) d0 = x; sz |= F.b(hb + 6 + i); }
   (void)d0;
   if (dz == 0 || sz == 0 || (s0 & 1)) return false;
+  if (parse_fast(F, hb, H)) return true;
+  H.l4 = L4_NONE;
   int pos = hb + 14;
   bool v6ctx = false;
   uint32_t aux = 0;
