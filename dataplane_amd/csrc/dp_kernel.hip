@@ -95,7 +95,7 @@ constexpr uint8_t DONE_NONE = 255;
 // ---------------------------------------------------------------------------
 struct Img {
   const uint8_t *base;
-  Image im;
+  const Image &im;  // in HBM on the device (read where used), host memory in the emulator
   template <class T> __device__ __forceinline__ const T *at(uint64_t off) const {
     return reinterpret_cast<const T *>(base + off);
   }
@@ -1971,10 +1971,18 @@ __device__ __forceinline__ bool adj_find(const Img &g, uint32_t oif, uint8_t fam
     const Adj &e = s[h];
     if (!e.used) return false;
     if (e.ifindex == oif && e.fam == fam) {
+      // fully unrolled: a constant index keeps `a` in registers (a dynamic
+      // a.w[i >> 2] would put it in scratch memory)
       bool eq = true;
-      int n = fam == 4 ? 4 : 16;
-      for (int i = 0; i < n; i++) eq &= e.addr[i] == (uint8_t)(a.w[i >> 2] >> (24 - 8 * (i & 3)));
-      if (eq) { for (int i = 0; i < 6; i++) mac[i] = e.mac[i]; return true; }
+      const int n = fam == 4 ? 4 : 16;
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        if (i < n) eq &= e.addr[i] == (uint8_t)(a.w[i >> 2] >> (24 - 8 * (i & 3)));
+      if (eq) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) mac[i] = e.mac[i];
+        return true;
+      }
     }
     h = (h + 1) & m.mask;
   }
@@ -2321,7 +2329,7 @@ __device__ __forceinline__ void wave_store_windows(uint8_t *buf, const uint8_t *
 }
 
 __global__ void __launch_bounds__(TPB) DP_OCC
-dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__restrict__ buf,
+dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict__ im, uint8_t *__restrict__ buf,
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
                    dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ part) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_all[TPB * (SLAB + HS)];
@@ -2344,7 +2352,7 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, Image im, uint8_t *__re
   uint8_t done_code = DONE_NONE;
   int fl0 = 0, fl1 = 0;
   if (live) {
-    Img g{img_base, im};
+    Img g{img_base, *im};
     dp_pkt_out_t o;
     lds_u8 *hs = (lds_u8 *)(hash_all + tid * HS);
     if (all_fit) done_code = process_packet(g, slab, hs, buf, buf_bytes, pin, o, fl0, fl1, true);
@@ -2460,11 +2468,11 @@ extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
+extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    uint32_t n, uint64_t *stats, uint64_t *stats_part, hipStream_t stream) {
   if (n == 0) return 0;
-  Image im = *reinterpret_cast<const Image *>(image_struct);
+  const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
   hipLaunchKernelGGL(dp_pipeline_kernel, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,

@@ -29,7 +29,7 @@
 #include "../../include/dpgpu.h"
 #include "dp_tables.h"
 
-extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
+extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    uint32_t n, uint64_t *stats, uint64_t *stats_part, hipStream_t stream);
 extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, hipStream_t stream);
@@ -91,6 +91,7 @@ struct DevImage {
   int device = 0;
   uint8_t *dev = nullptr;
   dpd::Image im{};
+  uint64_t im_off = 0;  // the Image descriptor, uploaded after the table bytes
   ~DevImage() {
     if (dev) bury(device, dev);  // freed later, off the burst path
   }
@@ -265,6 +266,11 @@ int dp_tables_publish(dp_ctx_t *c, const dp_tables_desc_t *tables) {
   drain_graveyard(c->device);  // images no burst reads any more
   auto img = std::make_shared<DevImage>();
   img->device = c->device;
+  // the kernel reads the Image descriptor from HBM (scalar loads where used)
+  // instead of taking it by value: 100+ kernel-argument SGPRs would spill
+  img->im_off = (bi.bytes.size() + 63) & ~(uint64_t)63;
+  bi.bytes.resize(img->im_off + sizeof(dpd::Image));
+  memcpy(bi.bytes.data() + img->im_off, &bi.im, sizeof(dpd::Image));
   hipError_t e = hipMalloc(&img->dev, bi.bytes.size());
   if (e != hipSuccess) return fail(DP_ENOMEM, "hipMalloc table image", e);
   if ((e = hipMemcpy(img->dev, bi.bytes.data(), bi.bytes.size(), hipMemcpyHostToDevice)) != hipSuccess)
@@ -323,7 +329,7 @@ int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
     if (ps->armed && hipStreamWaitEvent(s, ps->used, 0) != hipSuccess) return fail(DP_EIO, "stream wait");
     part = ps->part;
   }
-  int rc = dpk_launch_pipeline(img->dev, &img->im, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, part, s);
+  int rc = dpk_launch_pipeline(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, part, s);
   if (rc) {
     hipError_t e = hipGetLastError();
     (void)dpk_mark_failed(dev_in, dev_out, n, s);
