@@ -26,7 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from dataplane_amd import GpuPathNf, _abi as A  # noqa: E402
-from dataplane_amd.shard import reduce_over_ranks, shard_seed  # noqa: E402
+from dataplane_amd.shard import reduce_over_ranks, shard_seed, timed_scatter_gather  # noqa: E402
 from dataplane_amd.workload import ALGO_BYTES, CONFIG_NAMES, Workload  # noqa: E402
 
 METRIC = "Mpps device-resident (64B IPv4, 1M-route LPM + 10k ACL + NAT) at 1/2/4/8 GPU"
@@ -147,6 +147,8 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--no-rccl", action="store_true",
+                    help="N > 1: skip the resident-burst scatter / process / gather measurement")
     # ablation knobs (0 = the config's default table sizes)
     ap.add_argument("--routes-v4", type=int, default=0)
     ap.add_argument("--routes-v6", type=int, default=0)
@@ -164,7 +166,9 @@ def main() -> None:
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        import datetime
+        # a hung collective ends the run in minutes, not the 10-minute default
+        dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=180))
 
     def barrier():
         if world > 1:
@@ -242,6 +246,25 @@ def main() -> None:
 
     elapsed, hist = reduce_over_ranks(elapsed, dstats.cpu().numpy(), dev)
 
+    # N > 1, after the timed region: the path for a burst resident on one GPU
+    # (rank 0's shard scattered over all ranks with RCCL point-to-point sends,
+    # processed, gathered back), reported beside -- never inside -- `value`
+    rccl = None
+    if world > 1 and not args.no_rccl:
+        del bufs
+        w0 = w if rank == 0 else Workload(cfg, args.packets, seed=shard_seed(args.seed, 0),
+                                          n_routes_v4=args.routes_v4, n_routes_v6=args.routes_v6,
+                                          n_acl=args.acl, n_nat=args.nat, layout=args.layout)
+
+        def process_shard(span, rin, cnt):
+            o = torch.empty(max(1, cnt) * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+            if cnt:
+                nf.process_device(span.data_ptr(), span.numel(), rin.data_ptr(), o.data_ptr(), cnt,
+                                  None, sptr)
+            return o
+        rccl = timed_scatter_gather(w0.inp, w0.fresh_buf, process_shard, rank, world, dev,
+                                    A.PKT_IN.itemsize, A.PKT_OUT.itemsize)
+
     ms_per_step = elapsed * 1e3 / args.steps
     total_pkts = world * n * args.steps
     value = total_pkts / elapsed / 1e6
@@ -282,6 +305,8 @@ def main() -> None:
             "roofline": roofline,
             "done_histogram": {A.DONE_NAMES[i]: int(c) for i, c in enumerate(hist) if c},
         }
+        if rccl:
+            result["resident_burst_scatter_gather"] = rccl
         if world == 1 and not args.no_host:
             # host-origin rate (dp_process_burst): pinned host burst buffer and
             # records, chunked H2D / kernel / D2H overlapped on several streams

@@ -53,6 +53,13 @@ thread_local int dp_trip_st;
 #define TRIP_ST(x) ((void)0)
 #define TRIP() ((void)0)
 #endif
+// Wave-level loop iterations on the GPU (diagnostic build -DDP_TIMING -DDP_GPU_TRIPS):
+// the first active lane of the wave counts one iteration into g_stage_cycles[k]
+#if defined(DP_TIMING) && defined(DP_GPU_TRIPS) && !defined(DP_EMU)
+#define GTRIP(k) do { if ((int)threadIdx.x % 64 == __ffsll((long long)__ballot(1)) - 1) atomicAdd(&g_stage_cycles[k], 1ull); } while (0)
+#else
+#define GTRIP(k) ((void)0)
+#endif
 // Optional per-stage wave timing (build with -DDP_TIMING; scripts/stage_timing.py)
 #if defined(DP_TIMING) && !defined(DP_EMU)
 __device__ unsigned long long g_stage_cycles[16];
@@ -1051,7 +1058,7 @@ enum { W_ACTION = 1, W_ACTION2 = 2, W_AUX = 4, W_ORIG = 8 };
 //    containing the key) run in lockstep so their loads overlap, then the
 //    rows are ANDed behind the summary level; first set bit wins.
 __device__ __forceinline__ Hit verify_run(const Img &g, uint64_t recs, uint32_t run, bool v6, uint8_t proto,
-                                          Key128 src, Key128 dst, uint16_t sp, uint16_t dp) {
+                                          Key128 src, Key128 dst, uint16_t sp, uint16_t dp, bool acl = false) {
   Hit h{-1, 0, 0, 0, 0};
   const uint32_t first = run >> DPD_RUN_BITS, cnt = run & DPD_RUN_MAX;
   if (!v6) {
@@ -1071,6 +1078,7 @@ __device__ __forceinline__ Hit verify_run(const Img &g, uint64_t recs, uint32_t 
 #pragma unroll 1
     for (uint32_t c = 0; c < cnt; c += DP_CAND4) {
       TRIP();
+      if (acl) GTRIP(14); else GTRIP(13);
       // named registers, not an array: a dynamically indexed array would live in scratch
       const uint4 z = make_uint4(0, 0, 0, 0);
       const uint4 *q = R + 2 * c;
@@ -1136,13 +1144,14 @@ __device__ __forceinline__ Hit classify(const Img &g, const ClsArrays &A, int32_
                                         uint32_t pre = NO_PRE) {
   Hit h{-1, 0, 0, 0, 0};
   if (gi < 0) return h;
-  if (pre != NO_PRE) return verify_run(g, A.recs, pre, v6, proto, src, dst, sp, dp);
+  if (pre != NO_PRE) { GTRIP(15); return verify_run(g, A.recs, pre, v6, proto, src, dst, sp, dp, (WANT & W_ORIG) != 0); }
   const Group *Gp = g.at<Group>(A.group_recs) + gi;
   if (Gp->mode == DPD_GROUP_LIST) {
     const uint32_t f = Gp->lfield;
     const FieldIdx F = Gp->f[f];
     Key128 k = f == 0 ? src : f == 1 ? dst : Key128{0, f == 2 ? sp : dp};
-    return verify_run(g, A.recs, field_leaf(g, F, k), v6, proto, src, dst, sp, dp);
+    GTRIP(12);
+    return verify_run(g, A.recs, field_leaf(g, F, k), v6, proto, src, dst, sp, dp, (WANT & W_ORIG) != 0);
   }
   const int64_t ri = classify_bv(g, Gp, proto, src, dst, sp, dp);
   if (ri < 0) return h;

@@ -193,3 +193,64 @@ def rebase_gathered(out: np.ndarray, shards: Sequence[Shard]) -> np.ndarray:
             o = out["off"][s.first:s.first + s.cnt].astype(np.int64) + s.lo
             out["off"][s.first:s.first + s.cnt] = o.astype(np.uint32)
     return out
+
+
+def timed_scatter_gather(inp: np.ndarray, fresh_buf, process, rank: int, world: int, device,
+                         pkt_in_size: int, pkt_out_size: int, reps: int = 3, root: int = 0) -> dict:
+    """Cost of the resident-burst path on its own: the root's burst (`inp`,
+    `fresh_buf()` -> its bytes) scattered to every rank, each shard processed
+    there (`process(span, rin, cnt) -> out-records tensor`), spans and records
+    gathered back.  Barrier-bracketed wall time of each phase, median over
+    `reps` (after one untimed round); bytes are what crosses the links (the
+    root's own shard is a local copy).  Returns the figures on the root."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        dist.barrier()
+
+    buf_np = fresh_buf() if rank == root else None
+    buf_bytes = int(buf_np.nbytes) if rank == root else 0
+    nb = torch.tensor([buf_bytes], dtype=torch.int64, device=device)
+    dist.broadcast(nb, root)
+    shards = split_burst(inp, int(nb.item()), world)
+    buf = torch.from_numpy(buf_np).to(device) if rank == root else None
+    inp_u8 = torch.from_numpy(inp.view(np.uint8).copy()).to(device) if rank == root else None
+    out_all = (torch.empty(len(inp) * pkt_out_size, dtype=torch.uint8, device=device)
+               if rank == root else None)
+    times = []
+    for r in range(reps + 1):
+        sync()
+        t0 = time.perf_counter()
+        span, rin = scatter_burst(buf, inp_u8, shards, pkt_in_size, rank, world, device, root)
+        sync()
+        t1 = time.perf_counter()
+        s = shards[rank]
+        out = process(span, rin, s.cnt)
+        sync()
+        t2 = time.perf_counter()
+        gather_burst(span, out, buf, out_all, shards, pkt_out_size, rank, world, root)
+        sync()
+        t3 = time.perf_counter()
+        if r:
+            times.append((t1 - t0, t2 - t1, t3 - t2))
+    if rank != root:
+        return {}
+    med = [sorted(t[i] for t in times)[len(times) // 2] for i in range(3)]
+    peers = [s for k, s in enumerate(shards) if k != root and s.cnt]
+    sc_bytes = sum((s.hi - s.lo) + s.cnt * pkt_in_size for s in peers)
+    ga_bytes = sum((s.hi - s.lo) + s.cnt * pkt_out_size for s in peers)
+    return {"packets": int(len(inp)), "ranks": world,
+            "scatter_ms": round(med[0] * 1e3, 3), "process_ms": round(med[1] * 1e3, 3),
+            "gather_ms": round(med[2] * 1e3, 3),
+            "scatter_bytes": int(sc_bytes), "gather_bytes": int(ga_bytes),
+            "scatter_gbs": round(sc_bytes / med[0] / 1e9, 2) if med[0] else None,
+            "gather_gbs": round(ga_bytes / med[2] / 1e9, 2) if med[2] else None,
+            "mpps_end_to_end": round(len(inp) / sum(med) / 1e6, 2),
+            "what": "a burst resident on the root GPU: grouped point-to-point sends of each "
+                    "rank's byte span and records (RCCL over xGMI), per-rank processing, "
+                    "gather back; barrier-bracketed phases, median of the timed rounds"}

@@ -56,7 +56,12 @@ def main():
     res = {k: round(float(cyc[i]) / tot, 4) for i, k in enumerate(STAGES)}
     waves = a.reps * ((w.n + 63) // 64)
     res["cycles_per_wave"] = round(tot / waves, 1)
-    print(json.dumps({"config": a.config, "acl": a.acl, "nat": a.nat, "stages": res}))
+    # -DDP_GPU_TRIPS builds: wave-level loop iterations per wave
+    trips = {k: round(float(cyc[i]) / waves, 3) for i, k in
+             [(12, "indexed_verify_calls"), (13, "ff_verify_iters"), (14, "acl_verify_iters"),
+              (15, "hoisted_verify_calls")]}
+    print(json.dumps({"config": a.config, "acl": a.acl, "nat": a.nat, "stages": res,
+                      "wave_trips": trips}))
 
 
 if __name__ == "__main__":

@@ -94,3 +94,49 @@ def test_split_rejects_overlapping_slots():
     inp["len"] = [60, 60]
     with pytest.raises(ValueError):
         SH.split_burst(inp, 4096, 2)
+
+
+def _timed_rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dataplane_amd import _abi as A
+    from dataplane_amd import shard as SH
+    from dataplane_amd.workload import Workload
+    from oracle.pyoracle import Oracle
+    w = Workload(2, 2000, seed=9, n_routes_v4=2000, n_acl=100, n_nat=8, layout="dpdk")
+    orc = Oracle(w.tables)
+
+    def process(span, rin, cnt):
+        out = np.zeros(max(1, cnt), dtype=A.PKT_OUT)
+        if cnt:
+            out = orc.process(span.numpy(), rin.numpy()[:cnt * A.PKT_IN.itemsize].view(A.PKT_IN),
+                              A.PKT_OUT)
+        return torch.from_numpy(out.view(np.uint8).copy())
+    res = SH.timed_scatter_gather(w.inp, w.fresh_buf, process, rank, world, torch.device("cpu"),
+                                  A.PKT_IN.itemsize, A.PKT_OUT.itemsize, reps=2)
+    q.put((rank, res))
+    orc.close()
+    dist.destroy_process_group()
+
+
+def test_timed_scatter_gather_reports_on_root():
+    """bench.py's N > 1 resident-burst measurement (scatter, per-rank
+    processing, gather) runs to completion on every rank and reports the
+    phases and link bytes on the root."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_timed_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    r0, r1 = res[0], res[1]
+    assert r1 == {}
+    assert r0["ranks"] == 2 and r0["packets"] == 2000
+    assert r0["scatter_bytes"] > 1000 * 64 and r0["gather_bytes"] > 1000 * 64
+    assert r0["scatter_ms"] >= 0 and r0["gather_ms"] >= 0 and r0["process_ms"] > 0
