@@ -2081,7 +2081,55 @@ __device__ __forceinline__ int window_chunks(const dp_pkt_in_t &pin) {
 // outer Eth/IP/UDP/VXLAN headers.  Fields are patched into the LDS window
 // copy, checksums summed over the patched bytes, and the stack written back
 // in 16-byte chunks.  Returns the frame-relative output start.
+// The common shape -- the whole frame in the LDS window, no encap / VXLAN /
+// extension headers / ICMP error / parse-limit relocation, IPv4 or IPv6 with
+// UDP or TCP -- straight-line: the same bytes as the general serialize below,
+// with the IPv4 header checksum summed from the field values instead of a
+// pass over the patched header.
+__device__ __forceinline__ int serialize_fast(const Frame &F, const Hdr &H, const State &S, int &fl0, int &fl1) {
+  const int n = H.net_off, l = H.l4_off;
+  if (S.eth_dirty) { wput_mac(F, H.hb, S.edst); wput_mac(F, H.hb + 6, S.esrc); }
+  uint64_t t;
+  if (H.net == 4) {
+    const uint32_t w3 = F.be16(n + 6) & 0x7fffu;                 // reserved flag bit not kept
+    const uint32_t w4 = ((uint32_t)S.ttl << 8) | F.b(n + 9);
+    const uint32_t a = (S.v4src >> 16) + (S.v4src & 0xffff) + (S.v4dst >> 16) + (S.v4dst & 0xffff);
+    uint64_t s = (uint64_t)F.be16(n) + F.be16(n + 2) + F.be16(n + 4) + w3 + w4 + a;
+    for (int i = 20; i < H.net_hlen; i += 2) s += F.be16(n + i);  // options
+    wput16(F, n + 6, w3);
+    wput16(F, n + 8, w4);
+    wput16(F, n + 10, (uint16_t)~fold(s));
+    wput32(F, n + 12, S.v4src);
+    wput32(F, n + 16, S.v4dst);
+    t = a;
+  } else {
+    wput8(F, n + 7, S.ttl);
+    t = sum_frame(F, n + 8, n + 40);
+  }
+  wput16(F, l, S.sport);
+  wput16(F, l + 2, S.dport);
+  const bool udp = H.l4 == L4_UDP;
+  if (!udp) wput8(F, l + 12, F.b(l + 12) & 0xf1);
+  const int ck_off = udp ? l + 6 : l + 16;
+  wput16(F, ck_off, 0);
+  t += sum_frame(F, l, F.len);
+  const uint32_t tl = (uint32_t)H.l4_hlen + (uint32_t)(F.len - S.pay_start);
+  t += udp ? 17u + F.be16(l + 4) : (tl >> 16) + (tl & 0xffff) + 6u;
+  uint16_t c = (uint16_t)~fold(t);
+  if (udp && c == 0) c = 0xffff;
+  wput16(F, ck_off, c);
+  const int p = (F.shift + H.hb) & ~15;
+  int we = (F.shift + H.hb + H.size + 15) & ~15;
+  if (we > F.shift + F.len) we = F.shift + F.len;
+  fl0 = fl1 = 0;
+  if (we > p) { fl0 = p; fl1 = we; }
+  return H.hb;
+}
+
 __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &fl0, int &fl1) {
+  if (F.inwin && !S.encap && !H.vx && H.next == 0 && !has_emb(H) && S.pay_start - H.size == H.hb &&
+      (H.net == 4 || H.net == 6) && (H.l4 == L4_UDP || H.l4 == L4_TCP))
+    return serialize_fast(F, H, S, fl0, fl1);
   fl0 = fl1 = 0;
   const int inner_start = S.pay_start - H.size;
   const int outer = S.encap ? 14 + (S.o_fam == 4 ? 20 : 40) + 16 : 0;
