@@ -48,6 +48,22 @@ PKT_OUT = np.dtype([("off", "<u4"), ("len", "<u2"), ("done", "u1"), ("acl", "u1"
                     ("src_vni", "<u4"), ("fib_entry", "<u4"), ("acl_rule", "<u4")])
 assert PKT_IN.itemsize == 16 and PKT_OUT.itemsize == 32
 
+# Flow table (include/dpgpu.h "Flow table")
+FLOW_TCP, FLOW_UDP, FLOW_ICMP_QUERY, FLOW_ICMP_OTHER = 1, 2, 3, 4
+FLOW_ACTIVE, FLOW_CANCELLED, FLOW_EXPIRED, FLOW_DETACHED = 0, 1, 2, 3
+FLOW_INITIATOR, FLOW_REQ_STATIC_NAT_SRC, FLOW_REQ_STATIC_NAT_DST = 1, 2, 4
+FLOW_NONE = (1 << 64) - 1
+FLOW_INSERTED, FLOW_REPLACED, EFLOWCAP = 0, 1, -28
+ACL_SCOPE_FLOW, ACL_SCOPE_PACKET = 0, 1
+FLOW_KEY = np.dtype([("src_vni", "<u4"), ("family", "u1"), ("kind", "u1"), ("pad", "<u2"),
+                     ("sport", "<u2"), ("dport", "<u2"), ("src", "u1", 16), ("dst", "u1", 16)])
+FLOW = np.dtype([("key", FLOW_KEY), ("dst_vni", "<u4"), ("flags", "<u4"), ("pad", "<u4"),
+                 ("genid", "<i8"), ("expires_at", "<u8")], align=True)
+FLOW_INFO = np.dtype([("ref", "<u8"), ("status", "<u4"), ("flags", "<u4"), ("dst_vni", "<u4"),
+                      ("pad", "<u4"), ("genid", "<i8"), ("expires_at", "<u8"),
+                      ("related", "<u8")])
+assert FLOW_KEY.itemsize == 44 and FLOW.itemsize == 72 and FLOW_INFO.itemsize == 48
+
 
 class IpAddr(C.Structure):
     _fields_ = [("family", C.c_uint8), ("pad", C.c_uint8 * 3), ("addr", C.c_uint8 * 16)]
@@ -168,7 +184,12 @@ STRUCTS = dict(dp_ipaddr_t=IpAddr, dp_prefix_t=Prefix, dp_fib_t=Fib, dp_vni_fib_
 GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_publish",
                "dp_tables_genid", "dp_process_burst", "dp_process_burst_device",
                "dp_process_burst_sharded", "dp_ctx_synchronize", "dp_tables_device_bytes",
-               "dp_last_error", "dp_ctx_set_option"]
+               "dp_last_error", "dp_ctx_set_option", "dp_flow_table_create",
+               "dp_flow_table_destroy", "dp_flow_table_set_capacity", "dp_flow_insert",
+               "dp_flow_insert_pair", "dp_flow_lookup", "dp_flow_get", "dp_flow_remove",
+               "dp_flow_invalidate", "dp_flow_set_status", "dp_flow_sweep", "dp_flow_count",
+               "dp_ctx_attach_flow_table", "dp_process_burst_device_ex"]
+NP_STRUCTS = dict(dp_flow_key_t=FLOW_KEY, dp_flow_t=FLOW, dp_flow_info_t=FLOW_INFO)
 
 # dp_ctx_set_option (include/dpgpu.h)
 OPT_HOST_PATH = 1
@@ -209,6 +230,21 @@ def gpu_lib() -> C.CDLL:
         lib.dp_tables_device_bytes.restype = C.c_uint64
         lib.dp_last_error.restype = C.c_char_p
         lib.dp_ctx_set_option.argtypes = [_VP, C.c_int, C.c_int64]
+        lib.dp_flow_table_create.argtypes = [C.c_int, C.c_uint64, C.POINTER(_VP)]
+        lib.dp_flow_table_destroy.argtypes = [_VP]
+        lib.dp_flow_table_set_capacity.argtypes = [_VP, C.c_uint64]
+        lib.dp_flow_insert.argtypes = [_VP, _VP, C.c_uint32, _VP, _VP]
+        lib.dp_flow_insert_pair.argtypes = [_VP, _VP, _VP, _VP, _VP]
+        lib.dp_flow_lookup.argtypes = [_VP, _VP, C.c_uint32, _VP]
+        lib.dp_flow_get.argtypes = [_VP, _VP, C.c_uint32, _VP]
+        lib.dp_flow_remove.argtypes = [_VP, _VP, C.c_uint32, _VP]
+        lib.dp_flow_invalidate.argtypes = [_VP, _VP, C.c_uint32]
+        lib.dp_flow_set_status.argtypes = [_VP, C.c_uint64, C.c_uint32]
+        lib.dp_flow_sweep.argtypes = [_VP, C.c_uint64, _VP]
+        lib.dp_flow_count.argtypes = [_VP, _VP, _VP]
+        lib.dp_ctx_attach_flow_table.argtypes = [_VP, _VP]
+        lib.dp_process_burst_device_ex.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, C.c_uint32,
+                                                   _VP, _VP, _VP]
         if lib.dp_abi_version() != ABI_VERSION:
             raise RuntimeError("libdpgpu.so ABI version mismatch")
         _gpu = lib

@@ -1,0 +1,48 @@
+// SPDX-License-Identifier: Apache-2.0
+//
+// Host-side state of a device flow table (include/dpgpu.h "Flow table"),
+// shared by the flow-table API (dp_flows.hip) and the burst runtime
+// (dp_runtime.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+
+#include "dp_flow.h"
+
+// A device buffer grown on demand and kept (hipFree synchronises the device,
+// so it never runs on a call that bursts may overlap).
+struct FlowScratch {
+  void *p = nullptr;
+  size_t cap = 0;
+  void *get(size_t bytes) {
+    if (bytes <= cap) return p;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    cap = bytes;
+    return p;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct dp_flow_table {
+  int device = 0;
+  dpf::FlowSlot *slots = nullptr;  // HBM
+  uint64_t nslots = 0;
+  uint32_t mask = 0;
+  uint64_t capacity = 0;           // FlowTable::set_capacity
+  uint64_t len = 0;                // FULL slots (FlowTable::len)
+  hipStream_t stream = nullptr;    // management kernels
+  std::mutex mu;                   // one management call at a time
+  FlowScratch scr[4];              // management-call buffers
+};
+
+// Error reporting of the library (dp_last_error), defined in dp_runtime.cpp.
+int dpr_fail(int rc, const char *what, hipError_t e = hipSuccess);

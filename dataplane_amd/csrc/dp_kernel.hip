@@ -24,6 +24,7 @@
 
 #include "../../include/dpgpu.h"
 #include "dp_device.h"
+#include "dp_flow.h"
 
 namespace {
 
@@ -1453,6 +1454,152 @@ __device__ __forceinline__ uint8_t icmp_error_check(const Frame &F, const Hdr &H
 }
 
 // ---------------------------------------------------------------------------
+// Flow table (the flows variant of the kernel only; dp_flow.h)
+// ---------------------------------------------------------------------------
+// The flow FlowLookup attached to the packet (PacketMeta.flow_info), as it
+// stood when the burst started, and the flow-table effects the packet has;
+// they are applied by the kernel after the per-packet body, wave-aggregated.
+struct FlowPk {
+  uint32_t slot;       // kNoSlot: none
+  uint32_t state;      // its slot state word (the ref's tag)
+  uint32_t canon;      // the pair's canonical slot: min(slot, live related)
+  uint32_t related;    // the related flow's slot if it is in the table, else kNoSlot
+  uint32_t dst_vni, fflags;
+  int64_t genid;
+  bool active;         // FlowStatus::Active
+  uint32_t ev0, ev1;   // pair invalidations: flow-filter, ACL deny (kNoSlot: none)
+  uint32_t ev_mark;    // mark of ev1 (ACL deny at packet idx: idx + 1)
+  bool sens;           // ACL allowed it as the reply of a flow-scope-allowed flow
+  uint32_t def_acl, s_flags, s_oif, s_fib;
+};
+
+__device__ __forceinline__ uint4 ld4(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
+__device__ __forceinline__ uint32_t le32_at(const Frame &F, int f) {
+  return (uint32_t)F.b(f) | ((uint32_t)F.b(f + 1) << 8) | ((uint32_t)F.b(f + 2) << 16) |
+         ((uint32_t)F.b(f + 3) << 24);
+}
+__device__ __forceinline__ uint32_t be16_bytes(const Frame &F, int f) {
+  return ((uint32_t)F.b(f) << 8) | F.b(f + 1);
+}
+
+// FlowTable::lookup (flow-entry/src/flow_table/table.rs:267-275): linear
+// probing from the key's hash; one 128-byte line per slot, its first 48
+// bytes (state + key) fetched in one round trip.
+__device__ __forceinline__ uint32_t flow_probe(const dpf::FlowCtx &fc, const dpf::FKey &k, uint32_t &state) {
+  uint32_t i = dpf::fkey_hash(k) & fc.mask;
+#pragma unroll 1
+  for (uint32_t p = 0; p <= fc.mask; p++) {
+    const dpf::FlowSlot *s = fc.slots + i;
+    const uint4 a = ld4(&s->state), b = ld4(&s->src[0]), c = ld4(&s->dst[0]);
+    const uint32_t st = a.x & 3u;
+    if (st == dpf::FS_EMPTY) return dpf::kNoSlot;
+    if (st == dpf::FS_FULL && a.y == k.w[0] && a.z == k.w[1] && a.w == k.w[2] && b.x == k.w[3] &&
+        b.y == k.w[4] && b.z == k.w[5] && b.w == k.w[6] && c.x == k.w[7] && c.y == k.w[8] &&
+        c.z == k.w[9] && c.w == k.w[10]) {
+      state = a.x;
+      return i;
+    }
+    i = (i + 1) & fc.mask;
+  }
+  return dpf::kNoSlot;
+}
+
+// FlowKey::try_from(&Packet) (net/src/flows/flow_key.rs:589-621).  false: no
+// key, or an ICMP error message's key (IcmpProtoKey::ErrorMsgData), which no
+// stored flow has.
+__device__ __forceinline__ bool packet_fkey(const Frame &F, const Hdr &H, const State &S, dpf::FKey &k) {
+  if (H.net == 0) return false;
+  uint32_t kind, ports = 0;
+  if (H.l4 == L4_TCP || H.l4 == L4_UDP) {
+    kind = H.l4 == L4_TCP ? DP_FLOW_TCP : DP_FLOW_UDP;
+    ports = ((uint32_t)S.sport << 16) | S.dport;
+  } else if (H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) {
+    // IcmpProtoKey::new_icmp_v4/v6 (flow_key.rs:318-338): Echo Request / Reply
+    const bool v6 = H.l4 == L4_ICMP6;
+    const uint8_t t = F.b(H.l4_off), c = F.b(H.l4_off + 1);
+    if (c == 0 && (v6 ? (t == 128 || t == 129) : (t == 0 || t == 8))) {
+      kind = DP_FLOW_ICMP_QUERY;
+      ports = be16_bytes(F, H.l4_off + 4) << 16;
+    } else if (icmp_err_at(F, H.l4_off, v6)) {
+      return false;
+    } else {
+      kind = DP_FLOW_ICMP_OTHER;
+    }
+  } else {
+    return false;
+  }
+  k.w[0] = S.src_vni;
+  k.w[1] = (H.net == 4 ? 4u : 6u) | (kind << 8);
+  k.w[2] = ports;
+  if (H.net == 4) {
+    k.w[3] = __builtin_bswap32(S.v4src);
+    k.w[7] = __builtin_bswap32(S.v4dst);
+    k.w[4] = k.w[5] = k.w[6] = k.w[8] = k.w[9] = k.w[10] = 0;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      k.w[3 + j] = le32_at(F, H.net_off + 8 + 4 * j);
+      k.w[7 + j] = le32_at(F, H.net_off + 24 + 4 * j);
+    }
+  }
+  return true;
+}
+
+// Attach a found flow: its FlowInfo fields and whether its related flow is
+// still in the table (a Weak that upgrades), as the burst starts.
+__device__ __forceinline__ void flow_attach(const dpf::FlowCtx &fc, uint32_t slot, uint32_t state, FlowPk &fp) {
+  const dpf::FlowSlot *s = fc.slots + slot;
+  const uint4 v = ld4(&s->status), w = ld4(&s->related_tag);
+  fp.slot = slot;
+  fp.state = state;
+  fp.active = v.x == DP_FLOW_ACTIVE;
+  fp.fflags = v.y;
+  fp.dst_vni = v.z;
+  fp.genid = (int64_t)(((uint64_t)w.w << 32) | w.z);
+  fp.related = dpf::kNoSlot;
+  fp.canon = slot;
+  if (v.w <= fc.mask && fc.slots[v.w].state == w.x) {
+    fp.related = v.w;
+    fp.canon = slot < v.w ? slot : v.w;
+  }
+}
+
+// IcmpErrorHandler with a flow table (nat/src/icmp_handler/nf.rs:102-152):
+// the embedded packet's flow key, reversed, from the error's source VPC
+// (embedded_flowkey flow_key.rs:635-660, FlowKey::reverse :567-576).  A flow
+// found inactive filters the error; an active one sets the destination VPC
+// and -- with no masquerade / port-forwarding state to translate with --
+// filters it too.  Runs after icmp_error_check accepted the message.
+__device__ __forceinline__ void icmp_error_flow(const dpf::FlowCtx &fc, const Frame &F, const Hdr &H, State &S) {
+  const EmbV E = emb_view(F, H);
+  dpf::FKey k;
+  uint32_t kind, ports;
+  if (E.tk == L4_TCP || E.tk == L4_UDP) {
+    kind = E.tk == L4_TCP ? DP_FLOW_TCP : DP_FLOW_UDP;
+    ports = (be16_bytes(F, E.t_off + 2) << 16) | be16_bytes(F, E.t_off);
+  } else {
+    kind = DP_FLOW_ICMP_QUERY;
+    ports = be16_bytes(F, E.t_off + 4) << 16;
+  }
+  k.w[0] = S.src_vni;
+  k.w[1] = (uint32_t)E.net | (kind << 8);
+  k.w[2] = ports;
+  const int so = E.net == 4 ? 12 : 8, dof = E.net == 4 ? 16 : 24;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const bool w = E.net == 6 || j == 0;
+    k.w[3 + j] = w ? le32_at(F, E.off + dof + 4 * j) : 0u;
+    k.w[7 + j] = w ? le32_at(F, E.off + so + 4 * j) : 0u;
+  }
+  uint32_t st;
+  const uint32_t sl = flow_probe(fc, k, st);
+  if (sl == dpf::kNoSlot) return;  // no flow: let it through (nf.rs:114-121)
+  const uint4 v = ld4(&fc.slots[sl].status);
+  if (v.x == DP_FLOW_ACTIVE) S.dst_vni = v.z;  // nf.rs:139-140
+  done(S, DP_DONE_FILTERED);                   // inactive (:126-130) / no NAT state (:143-152)
+}
+
+// ---------------------------------------------------------------------------
 // Stages
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool find_iface(const Img &g, uint32_t ifx, IfRec &out) {
@@ -1828,9 +1975,27 @@ __device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_
   if (m[3].root) P.ndst = e[3] & ~DPD_LEAF;
 }
 
-__device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, State &S, Pre &P) {
+// FlowFilter (flow-filter/src/lib.rs:75-246).  FL: with a flow table -- an
+// attached flow that is active and not outdated bypasses the tables
+// (dst_vpcd_from_valid_flow / tag_for_bypass, lib.rs:122-131,213-231,327-349);
+// a miss invalidates the attached flow pair, and so does a hit for a flow of
+// another generation (should_invalidate_flow, :258-294: without masquerade /
+// port-forwarding state an outdated flow is either misrouted or no longer
+// needed).  Flows carry no such state, so revalidation (flow_revalidation_data,
+// :296-325) is the plain lookup.
+template <bool FL>
+__device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, State &S, Pre &P,
+                                                  FlowPk &fp, const dpf::FlowCtx *fc) {
   P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY) || S.dst_vni) return;
+  if constexpr (FL) {
+    if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid) {
+      S.dst_vni = fp.dst_vni;
+      if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_SRC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
+      if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_DST) S.flags |= DP_META_REQ_STATIC_NAT_DST;
+      return;
+    }
+  }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
   if (!S.src_vni) { done(S, DP_DONE_UNROUTABLE); return; }
   uint8_t proto = net_proto(F, H);
@@ -1844,7 +2009,11 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
                                                 : NO_PRE;
   const Hit rh = classify<W_ACTION | W_ACTION2 | W_AUX>(g, CLS_ARRAYS(ff_remote, t), rg, t, proto,
                                                        Key128{0, 0}, dst, 0, S.dport, pre);
-  if (rh.rule < 0) { done(S, DP_DONE_FILTERED); return; }
+  if (rh.rule < 0) {
+    if constexpr (FL) if (fp.slot != dpf::kNoSlot) fp.ev0 = fp.canon;
+    done(S, DP_DONE_FILTERED);
+    return;
+  }
   uint32_t dvni = rh.action;
   uint32_t dnat = rh.action2;
   int32_t pi = (int32_t)rh.aux;
@@ -1853,15 +2022,32 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   int32_t lg = g.at<PairRec>(g.im.pair_recs)[pi].ffl[t];
   if (t == 0) hoist_walks(g, S, pi, P);
   const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, proto, src, Key128{0, 0}, S.sport, 0, P.ffl);
-  if (lh.rule < 0) { done(S, DP_DONE_FILTERED); return; }
+  if (lh.rule < 0) {
+    if constexpr (FL) if (fp.slot != dpf::kNoSlot) fp.ev0 = fp.canon;
+    done(S, DP_DONE_FILTERED);
+    return;
+  }
   uint32_t snat = lh.action;
   S.dst_vni = dvni;
   S.pair = pi;
   if (snat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
   if (dnat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_DST;
+  if constexpr (FL) if (fp.slot != dpf::kNoSlot && fp.genid != fc->genid) fp.ev0 = fp.canon;
 }
 
-__device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S, const Pre &P) {
+// AclFilter (acl-filter/src/lib.rs:51-138).  The classifier action word
+// carries the verdict (low byte) and the rule's AclScope (dp_tables.cpp).
+// FL: a direct miss with a valid attached flow (active, not outdated:
+// packet_has_valid_flow :71-94) whose related flow is in the table looks up
+// the related flow's key between the swapped VPCs (reverse_summary
+// :205-217); a Flow-scope Allow there admits the packet (:110-128).  That
+// verdict rests on the flow still being valid when the packet reaches the
+// ACL -- an invalidation by the flow filter (any packet of the burst) or by
+// an earlier packet's deny turns it into the peering default
+// (dp_flow_fixup).  A deny invalidates the packet's flow pair.
+template <bool FL>
+__device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S, const Pre &P,
+                                          FlowPk &fp, const dpf::FlowCtx *fc, uint32_t idx) {
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY)) return;
   if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
@@ -1873,20 +2059,55 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
                                              key_of(F, H, S, false), S.sport, S.dport, t == 0 ? P.acl : NO_PRE);
   uint32_t action;
   if (ah.rule >= 0) {
-    action = ah.action;
+    action = ah.action & 0xffu;
     S.acl_rule = ah.orig;
     S.acl = action == DP_ACL_DENY ? 2 : 1;
   } else {
     uint32_t v = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].acl_def : 0;
-    if (v) {
-      action = v - 1;
-      S.acl = action == DP_ACL_DENY ? 4 : 3;
-    } else {
-      action = DP_ACL_ALLOW;
-      S.acl = 5;
+    const uint8_t def = v ? ((v - 1) == DP_ACL_DENY ? 4 : 3) : 5;
+    action = v ? v - 1 : DP_ACL_ALLOW;
+    S.acl = def;
+    if constexpr (FL) {
+      if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid && fp.related != dpf::kNoSlot) {
+        const dpf::FlowSlot *r = fc->slots + fp.related;
+        const uint4 a = ld4(&r->state), b = ld4(&r->src[0]), c = ld4(&r->dst[0]);
+        const uint32_t fam = a.z & 0xffu, kind = a.z >> 8;
+        const bool ports = kind == DP_FLOW_TCP || kind == DP_FLOW_UDP;
+        const uint8_t rproto = kind == DP_FLOW_TCP ? 6 : kind == DP_FLOW_UDP ? 17 : fam == 4 ? 1 : 58;
+        const int rt = fam == 4 ? 0 : 1;
+        uint32_t rpi;
+        const int32_t rg = hash_find(g, g.im.pairs, S.dst_vni, S.src_vni, 0, rpi)
+                               ? g.at<PairRec>(g.im.pair_recs)[rpi].acl[rt] : -1;
+        Key128 ks, kd;
+        if (fam == 4) {
+          ks = Key128{0, __builtin_bswap32(b.x)};
+          kd = Key128{0, __builtin_bswap32(c.x)};
+        } else {
+          ks = Key128{((uint64_t)__builtin_bswap32(b.x) << 32) | __builtin_bswap32(b.y),
+                      ((uint64_t)__builtin_bswap32(b.z) << 32) | __builtin_bswap32(b.w)};
+          kd = Key128{((uint64_t)__builtin_bswap32(c.x) << 32) | __builtin_bswap32(c.y),
+                      ((uint64_t)__builtin_bswap32(c.z) << 32) | __builtin_bswap32(c.w)};
+        }
+        const Hit rh = classify<W_ACTION | W_ORIG>(g, CLS_ARRAYS(acl, rt), rg, rt, rproto, ks, kd,
+                                                   ports ? (uint16_t)(a.w >> 16) : 0,
+                                                   ports ? (uint16_t)a.w : 0);
+        if (rh.rule >= 0 && rh.action == (DP_ACL_ALLOW | (DP_ACL_SCOPE_FLOW << 8))) {
+          action = DP_ACL_ALLOW;
+          S.acl = 6;
+          S.acl_rule = rh.orig;
+          fp.sens = true;
+          fp.def_acl = def;
+          fp.s_flags = S.flags;
+          fp.s_oif = S.has_oif ? S.oif : 0;
+          fp.s_fib = S.fib_entry;
+        }
+      }
     }
   }
-  if (action == DP_ACL_DENY) done(S, DP_DONE_ACL_DROPPED);
+  if (action == DP_ACL_DENY) {
+    if constexpr (FL) if (fp.slot != dpf::kNoSlot) { fp.ev1 = fp.canon; fp.ev_mark = idx + 1; }
+    done(S, DP_DONE_ACL_DROPPED);
+  }
 }
 
 // The embedded packet of an ICMP error message, translated back by static
@@ -2227,9 +2448,17 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
 // ---------------------------------------------------------------------------
 // Per-packet body
 // ---------------------------------------------------------------------------
+// FL: the flows variant -- FlowLookup on fc's table and the flow-aware
+// branches; fp receives the packet's flow and its flow-table effects.
+template <bool FL>
 __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, lds_u8 *hs, uint8_t *buf, uint64_t buf_bytes,
-                                  const dp_pkt_in_t &pin, dp_pkt_out_t &o, int &fl0, int &fl1, bool inwin) {
+                                  const dp_pkt_in_t &pin, dp_pkt_out_t &o, int &fl0, int &fl1, bool inwin,
+                                  const dpf::FlowCtx *fc, FlowPk &fp, uint32_t idx) {
   fl0 = fl1 = 0;
+  if constexpr (FL) {
+    fp.slot = fp.ev0 = fp.ev1 = dpf::kNoSlot;
+    fp.sens = false;
+  }
   if (!frame_ok(pin, buf_bytes)) {
     // layout contract violated: never touch memory outside the buffer
     o.off = pin.off; o.len = pin.len; o.done = DP_DONE_INTERNAL_FAILURE; o.acl = 0;
@@ -2280,18 +2509,29 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
       icmp_err_at(F, H.l4_off, H.l4 == L4_ICMP6)) {
     const uint8_t r = icmp_error_check(F, H, S);
     if (r != DONE_NONE) done(S, r);
+    else if constexpr (FL) icmp_error_flow(*fc, F, H, S);
+  }
+  // FlowLookup (flow-entry/src/flow_table/nf_lookup.rs:34-55); identity
+  // without a flow table
+  if constexpr (FL) {
+    dpf::FKey k;
+    uint32_t st;
+    if (S.done == DONE_NONE && (S.flags & DP_META_IS_OVERLAY) && !S.dst_vni && packet_fkey(F, H, S, k)) {
+      const uint32_t sl = flow_probe(*fc, k, st);
+      if (sl != dpf::kNoSlot) flow_attach(*fc, sl, st, fp);
+    }
   }
   Pre P;
   TRIP_ST(2);
 #ifndef DP_PROBE_NOFF
-  stage_flow_filter(g, F, H, S, P);
+  stage_flow_filter<FL>(g, F, H, S, P, fp, fc);
 #else
   P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
 #endif
   TS(3);
   TRIP_ST(4);
 #ifndef DP_PROBE_NOACL
-  stage_acl(g, F, H, S, P);
+  stage_acl<FL>(g, F, H, S, P, fp, fc, idx);
 #endif
   TS(4);
   TRIP_ST(5);
@@ -2385,10 +2625,47 @@ __device__ __forceinline__ void wave_store_windows(uint8_t *buf, const uint8_t *
   }
 }
 
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// The flow-table effects of a wave's packets (FL only), wave-aggregated:
+// flow refs, invalidation marks and events, flow-dependent ACL verdicts.
+__device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, uint32_t i, const FlowPk &fp) {
+  const int lane = threadIdx.x & 63;
+  const bool has = live && fp.slot != dpf::kNoSlot;
+  if (live && fc.refs) fc.refs[i] = has ? dpf::make_ref(fp.slot, fp.state) : ~0ull;
+  const bool e0 = has && fp.ev0 != dpf::kNoSlot, e1 = has && fp.ev1 != dpf::kNoSlot;
+  if (e0) atomicMin(&fc.slots[fp.ev0].mark, 0u);
+  if (e1) atomicMin(&fc.slots[fp.ev1].mark, fp.ev_mark);
+  const uint64_t m0 = __ballot(e0), m1 = __ballot(e1);
+  if (m0 | m1) {
+    const int leader = __ffsll((long long)(m0 | m1)) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&fc.events[0], (uint32_t)(__popcll(m0) + __popcll(m1)));
+    base = (uint32_t)__shfl((int)base, leader);
+    if (e0) fc.events[1 + base + __popcll(m0 & lanes_below(lane))] = fp.ev0;
+    if (e1) fc.events[1 + base + __popcll(m0) + __popcll(m1 & lanes_below(lane))] = fp.ev1;
+  }
+  const bool sv = has && fp.sens;
+  const uint64_t ms = __ballot(sv);
+  if (ms) {
+    const int leader = __ffsll((long long)ms) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&fc.sens[0], (uint32_t)__popcll(ms));
+    base = (uint32_t)__shfl((int)base, leader);
+    if (sv) {
+      dpf::SensRec *R = reinterpret_cast<dpf::SensRec *>(fc.sens + 8) + base + __popcll(ms & lanes_below(lane));
+      *R = dpf::SensRec{i, fp.canon, fp.s_flags, fp.s_oif, fp.s_fib, fp.def_acl, {0, 0}};
+    }
+  }
+}
+
+// FL: the flows variant (a flow table is attached to the context).
+template <bool FL>
 __global__ void __launch_bounds__(TPB) DP_OCC
 dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict__ im, uint8_t *__restrict__ buf,
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
-                   dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ part) {
+                   dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ part,
+                   dpf::FlowCtx fc) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_all[TPB * (SLAB + HS)];
   uint8_t *slab_all = lds_all;
   uint8_t *hash_all = lds_all + TPB * SLAB;
@@ -2408,14 +2685,17 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   __syncthreads();
   uint8_t done_code = DONE_NONE;
   int fl0 = 0, fl1 = 0;
+  FlowPk fp;
+  fp.slot = dpf::kNoSlot;
   if (live) {
     Img g{img_base, *im};
     dp_pkt_out_t o;
     lds_u8 *hs = (lds_u8 *)(hash_all + tid * HS);
-    if (all_fit) done_code = process_packet(g, slab, hs, buf, buf_bytes, pin, o, fl0, fl1, true);
-    else done_code = process_packet(g, slab, hs, buf, buf_bytes, pin, o, fl0, fl1, false);
+    if (all_fit) done_code = process_packet<FL>(g, slab, hs, buf, buf_bytes, pin, o, fl0, fl1, true, &fc, fp, i);
+    else done_code = process_packet<FL>(g, slab, hs, buf, buf_bytes, pin, o, fl0, fl1, false, &fc, fp, i);
     out[i] = o;
   }
+  if constexpr (FL) flow_effects(fc, live, i, fp);
   __syncthreads();
   // write-back: whole chunks by the wave, a partial tail by its owner
   wave_store_windows(buf, slab_wave, base, fl0 >> 4, fl1 >> 4);
@@ -2432,6 +2712,55 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
       if (lane == leader) atomicAdd(&part[r * DPD_STAT_SLOTS + slot], (unsigned long long)__popcll(m));
       pending &= ~m;
     }
+  }
+}
+
+// After the burst's pipeline kernel (flows variant), on its stream.
+// dp_flow_fixup: a verdict "allowed as the reply of a flow-scope-allowed
+// flow" stands only if the flow pair was still valid when the packet reached
+// the ACL: not invalidated by the flow filter (mark 0: the flow filter runs
+// over the whole burst before any ACL) nor by the deny of an earlier packet
+// (mark idx + 1).  Otherwise the peering default applies; a default Deny
+// drops the packet at the ACL with its metadata as it stood there.
+__global__ void __launch_bounds__(256) dp_flow_fixup(dpf::FlowCtx fc, const dp_pkt_in_t *__restrict__ in,
+                                                     dp_pkt_out_t *__restrict__ out,
+                                                     unsigned long long *__restrict__ stats) {
+  const uint32_t cnt = fc.sens[0];
+  const dpf::SensRec *recs = reinterpret_cast<const dpf::SensRec *>(fc.sens + 8);
+  for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < cnt; r += gridDim.x * 256) {
+    const dpf::SensRec R = recs[r];
+    if (fc.slots[R.canon].mark > R.idx) continue;  // still valid at its ACL
+    dp_pkt_out_t o = out[R.idx];
+    o.acl = (uint8_t)R.def_acl;
+    o.acl_rule = 0xffffffffu;
+    if (R.def_acl == 4) {
+      if (stats && o.done < DP_DONE_COUNT) {
+        atomicAdd(&stats[o.done], ~0ull);  // -1
+        atomicAdd(&stats[DP_DONE_ACL_DROPPED], 1ull);
+      }
+      o.done = DP_DONE_ACL_DROPPED;
+      o.off = in[R.idx].off;
+      o.len = in[R.idx].len;
+      o.meta_flags = R.meta_flags;
+      o.oif = R.oif;
+      o.fib_entry = R.fib_entry;
+    }
+    out[R.idx] = o;
+  }
+}
+
+// dp_flow_apply: the burst's invalidations (FlowInfo::invalidate_pair,
+// net/src/flows/flow_info.rs:435-455) become the flows' status; the marks
+// return to idle.
+__global__ void __launch_bounds__(256) dp_flow_apply(dpf::FlowCtx fc) {
+  const uint32_t cnt = fc.events[0];
+  for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < cnt; r += gridDim.x * 256) {
+    const uint32_t c = fc.events[1 + r];
+    dpf::FlowSlot &s = fc.slots[c];
+    s.status = DP_FLOW_CANCELLED;
+    s.mark = dpf::kIdleMark;
+    const uint32_t rel = s.related;
+    if (rel <= fc.mask && fc.slots[rel].state == s.related_tag) fc.slots[rel].status = DP_FLOW_CANCELLED;
   }
 }
 
@@ -2481,8 +2810,9 @@ extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uin
     }
     int fl0, fl1;
     const bool fit = (in[i].off & 15) + in[i].len <= (uint32_t)WIN && !(in[i].off & 1);
-    if (fit) process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, true);
-    else process_packet(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, false);
+    FlowPk fp;
+    if (fit) process_packet<false>(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, true, nullptr, fp, i);
+    else process_packet<false>(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, false, nullptr, fp, i);
     if (fl1 > fl0) flush_range(buf + (in[i].off & ~15u), slab, fl0, fl1);
 #ifdef DP_TRIPS
     if (dp_trip_out)
@@ -2532,11 +2862,37 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_de
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
-  hipLaunchKernelGGL(dp_pipeline_kernel, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                     buf_bytes, in, out, n, part);
+  hipLaunchKernelGGL(dp_pipeline_kernel<false>, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
+                     buf_bytes, in, out, n, part, dpf::FlowCtx{});
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// The flows variant: counters cleared, the pipeline, the histogram, then the
+// flow fix-up and the invalidations, in stream order.  `fc` points at host
+// memory holding the launch's FlowCtx (device pointers inside).
+extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
+                                         uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
+                                         uint32_t n, uint64_t *stats, uint64_t *stats_part,
+                                         const void *fc_host, hipStream_t stream) {
+  if (n == 0) return 0;
+  const dpf::FlowCtx fc = *reinterpret_cast<const dpf::FlowCtx *>(fc_host);
+  if (hipMemsetAsync(fc.events, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
+  if (hipMemsetAsync(fc.sens, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
+  const Image *im = reinterpret_cast<const Image *>(image_dev);
+  uint32_t blocks = (n + TPB - 1) / TPB;
+  unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
+  hipLaunchKernelGGL(dp_pipeline_kernel<true>, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
+                     buf_bytes, in, out, n, part, fc);
+  if (stats)
+    hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
+                       reinterpret_cast<unsigned long long *>(stats));
+  const uint32_t fb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(dp_flow_fixup, dim3(fb), dim3(256), 0, stream, fc, in, out,
+                     reinterpret_cast<unsigned long long *>(stats));
+  hipLaunchKernelGGL(dp_flow_apply, dim3(fb), dim3(256), 0, stream, fc);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 #endif

@@ -27,12 +27,17 @@
 #include <vector>
 
 #include "../../include/dpgpu.h"
+#include "dp_flows_rt.h"
 #include "dp_tables.h"
 
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    uint32_t n, uint64_t *stats, uint64_t *stats_part, hipStream_t stream);
 extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, hipStream_t stream);
+extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
+                                         uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
+                                         uint32_t n, uint64_t *stats, uint64_t *stats_part,
+                                         const void *fc_host, hipStream_t stream);
 
 namespace {
 
@@ -46,6 +51,12 @@ int fail(int rc, const char *what, hipError_t e = hipSuccess) {
   }
   return rc;
 }
+
+}  // namespace
+
+int dpr_fail(int rc, const char *what, hipError_t e) { return fail(rc, what, e); }
+
+namespace {
 
 struct DeviceTables;
 DeviceTables &dev_tables(int device);
@@ -156,6 +167,13 @@ struct dp_ctx {
   hipEvent_t hev[kHostStreams + 1] = {};
   bool host_streams = false;
   int host_path = DP_HOST_AUTO;        // dp_ctx_set_option(DP_OPT_HOST_PATH)
+  // flow table (dp_ctx_attach_flow_table) and the per-launch flow scratch:
+  // invalidation events and flow-dependent ACL verdicts; a launch waits for
+  // the previous flows launch before reusing it
+  dp_flow_table *ft = nullptr;
+  FlowScratch fl_ev, fl_sens;
+  hipEvent_t fl_used = nullptr;
+  bool fl_armed = false;
 };
 
 namespace {
@@ -248,6 +266,9 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->d_in) (void)hipFree(c->d_in);
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_stats) (void)hipFree(c->d_stats);
+  c->fl_ev.release();
+  c->fl_sens.release();
+  if (c->fl_used) (void)hipEventDestroy(c->fl_used);
   for (auto &h : c->hs) if (h) { (void)hipStreamSynchronize(h); (void)hipStreamDestroy(h); }
   for (auto &e : c->hev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -307,9 +328,9 @@ static std::shared_ptr<DevImage> current(dp_ctx_t *c) {
   return dt.cur;
 }
 
-int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
-                            const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out, uint32_t n,
-                            uint64_t *dev_stats, void *stream) {
+static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const dp_pkt_in_t *dev_in,
+                        dp_pkt_out_t *dev_out, uint32_t n, uint64_t *dev_stats, uint64_t *dev_flow_refs,
+                        void *stream) {
   if (!c) return fail(DP_EINVAL, "null ctx");
   if (n == 0) return 0;
   if (!dev_in || !dev_out) return fail(DP_EINVAL, "null burst descriptors");
@@ -329,7 +350,36 @@ int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
     if (ps->armed && hipStreamWaitEvent(s, ps->used, 0) != hipSuccess) return fail(DP_EIO, "stream wait");
     part = ps->part;
   }
-  int rc = dpk_launch_pipeline(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, part, s);
+  int rc;
+  if (c->ft) {
+    // the flows variant: FlowLookup on the attached table and the flow-aware
+    // stages, with this launch's event / verdict scratch
+    if (c->fl_armed && hipStreamWaitEvent(s, c->fl_used, 0) != hipSuccess) return fail(DP_EIO, "stream wait");
+    dpf::FlowCtx fc{};
+    fc.slots = c->ft->slots;
+    fc.mask = c->ft->mask;
+    fc.n = n;
+    fc.events = static_cast<uint32_t *>(c->fl_ev.get(sizeof(uint32_t) * (1 + 2 * (uint64_t)n)));
+    fc.sens = static_cast<uint32_t *>(c->fl_sens.get(sizeof(uint32_t) * 8 + sizeof(dpf::SensRec) * (uint64_t)n));
+    fc.refs = reinterpret_cast<unsigned long long *>(dev_flow_refs);
+    fc.genid = img->im.genid;
+    if (!fc.events || !fc.sens) {
+      (void)dpk_mark_failed(dev_in, dev_out, n, s);
+      return fail(DP_ENOMEM, "flow burst scratch");
+    }
+    rc = dpk_launch_pipeline_flows(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out, n,
+                                   dev_stats, part, &fc, s);
+    if (!rc) {
+      if (!c->fl_used && hipEventCreateWithFlags(&c->fl_used, hipEventDisableTiming) != hipSuccess)
+        return fail(DP_EIO, "hipEventCreate");
+      (void)hipEventRecord(c->fl_used, s);
+      c->fl_armed = true;
+    }
+  } else {
+    if (dev_flow_refs) (void)hipMemsetAsync(dev_flow_refs, 0xff, sizeof(uint64_t) * n, s);  // DP_FLOW_NONE
+    rc = dpk_launch_pipeline(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats,
+                             part, s);
+  }
   if (rc) {
     hipError_t e = hipGetLastError();
     (void)dpk_mark_failed(dev_in, dev_out, n, s);
@@ -344,6 +394,27 @@ int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
   f.done = take_event(c);
   if (f.done) (void)hipEventRecord(f.done, s);
   c->inflight.push_back(std::move(f));
+  return 0;
+}
+
+int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
+                            const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out, uint32_t n,
+                            uint64_t *dev_stats, void *stream) {
+  return launch_burst(c, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, nullptr, stream);
+}
+
+int dp_process_burst_device_ex(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
+                               const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out, uint32_t n,
+                               uint64_t *dev_stats, uint64_t *dev_flow_refs, void *stream) {
+  return launch_burst(c, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, dev_flow_refs, stream);
+}
+
+int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
+  if (!c) return fail(DP_EINVAL, "null ctx");
+  if (ft && ft->device != c->device) return fail(DP_EINVAL, "flow table on another device");
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->ft = ft;
   return 0;
 }
 
@@ -438,7 +509,9 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
   bool ordered = true;
   for (uint32_t i = 1; i < n && ordered; i++)
     ordered = in[i].off - DP_HEADROOM >= (uint64_t)in[i - 1].off + in[i - 1].len;
-  const uint32_t nch = ordered ? std::max<uint32_t>(1, std::min<uint32_t>(n / kHostChunk, 256)) : 1;
+  // with a flow table the burst stays one launch: its packets share flow state
+  // in the reference's burst order
+  const uint32_t nch = ordered && !c->ft ? std::max<uint32_t>(1, std::min<uint32_t>(n / kHostChunk, 256)) : 1;
   if (nch > 1 && !c->host_streams) {
     for (int k = 0; k < kHostStreams; k++)
       if ((e = hipStreamCreateWithFlags(&c->hs[k], hipStreamNonBlocking)) != hipSuccess)
@@ -523,8 +596,12 @@ int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf
       return fail(DP_EINVAL, "sharded bursts need in-order, non-overlapping packet slots");
     }
   }
-  for (uint32_t k = 0; k < n_ctx; k++)
+  for (uint32_t k = 0; k < n_ctx; k++) {
     if (!ctxs[k]) { mark_failed_host(in, out, n); return fail(DP_EINVAL, "null context"); }
+    // one flow table per device cannot give the shards the reference's
+    // shared Arc<FlowTable> (flows shard by 5-tuple hash)
+    if (ctxs[k]->ft) { mark_failed_host(in, out, n); return fail(DP_ENOTSUP, "sharded bursts with a flow table"); }
+  }
   struct Shard {
     uint32_t first, cnt;
     uint64_t lo, hi;               // byte span in `buf`

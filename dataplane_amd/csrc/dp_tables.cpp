@@ -561,7 +561,8 @@ int load_rules(const dp_rule_t *rs, uint32_t n, int fam, bool by_prio, int kind,
     const dp_rule_t &r = rs[i];
     if (!valid_prefix(r.src) || !valid_prefix(r.dst)) return DP_EINVAL;
     if (r.src.family != fam || r.dst.family != fam) return DP_EINVAL;
-    if (kind == 0 && r.gate != 0) return DP_EINVAL;                      // ACL
+    if (kind == 0 && (r.gate != 0 || r.action > DP_ACL_DENY || r.action2 > DP_ACL_SCOPE_PACKET))
+      return DP_EINVAL;                                                   // ACL
     if (kind == 1) {                                                      // FF remote
       if (r.src.len != 0 || r.sport_lo != 0 || r.sport_hi != 65535 || r.gate != 0) return DP_EINVAL;
       if (r.action2 == DP_NAT_MASQUERADE || r.action2 == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
@@ -571,6 +572,9 @@ int load_rules(const dp_rule_t *rs, uint32_t n, int fam, bool by_prio, int kind,
       if (r.action == DP_NAT_MASQUERADE || r.action == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
     }
     out.push_back(CRule{r, i});
+    // ACL: the verdict and its AclScope travel in one action word (both
+    // classifier forms carry `action` to the lookup)
+    if (kind == 0) out.back().r.action = r.action | (r.action2 << 8);
   }
   if (by_prio)
     std::stable_sort(out.begin(), out.end(),

@@ -119,6 +119,21 @@ class GpuPathNf:
                 "dp_process_burst", self.lib)
         return out
 
+    def attach_flows(self, flow_table) -> None:
+        """FlowLookup::new(name, flow_table) (flow-entry/src/flow_table/nf_lookup.rs:24-32):
+        this context's pipeline consults `flow_table` (a dataplane_amd.flows.FlowTable);
+        None detaches it (an empty flow table)."""
+        A.check(self.lib.dp_ctx_attach_flow_table(self.ctx, flow_table.h if flow_table else None),
+                "dp_ctx_attach_flow_table", self.lib)
+
+    def process_device_ex(self, dev_buf: int, buf_bytes: int, dev_in: int, dev_out: int, n: int,
+                          dev_stats: Optional[int] = None, dev_flow_refs: Optional[int] = None,
+                          stream: Optional[int] = None) -> None:
+        """dp_process_burst_device_ex: also each packet's attached flow (a ref)."""
+        A.check(self.lib.dp_process_burst_device_ex(self.ctx, dev_buf, buf_bytes, dev_in, dev_out,
+                                                    n, dev_stats, dev_flow_refs, stream),
+                "dp_process_burst_device_ex", self.lib)
+
     def process_device(self, dev_buf: int, buf_bytes: int, dev_in: int, dev_out: int, n: int,
                        dev_stats: Optional[int] = None, stream: Optional[int] = None) -> None:
         """Device-resident burst (dp_process_burst_device): raw device pointers."""

@@ -168,9 +168,12 @@ class TablesBuilder:
         r.dst = mk_prefix(dst) if dst else wildcard(family)
         return r
 
-    def add_acl(self, src_vni: int, dst_vni: int, action: int, family: int = 4, **kw) -> None:
-        """ACL rules are matched in insertion order (first match)."""
-        self.acl[family].append(self.rule(family, vni_a=src_vni, vni_b=dst_vni, action=action, **kw))
+    def add_acl(self, src_vni: int, dst_vni: int, action: int, family: int = 4,
+                scope: int = A.ACL_SCOPE_FLOW, **kw) -> None:
+        """ACL rules are matched in insertion order (first match); `scope` is
+        AclScope (Flow by default, config/src/external/overlay/acl.rs:137-141)."""
+        self.acl[family].append(self.rule(family, vni_a=src_vni, vni_b=dst_vni, action=action,
+                                          action2=scope, **kw))
 
     def add_acl_default(self, src_vni: int, dst_vni: int, action: int) -> None:
         self.acl_defaults.append(A.AclDefault(src_vni, dst_vni, action))

@@ -142,7 +142,8 @@ typedef struct dp_pkt_out {
     uint8_t done;        /* enum dp_done_reason */
     uint8_t acl;         /* 0: ACL not consulted, 1: allow (rule), 2: deny (rule),
                             3: allow (peering default), 4: deny (peering default),
-                            5: allow (no ACL for peering) */
+                            5: allow (no ACL for peering), 6: allow (reply of a
+                            flow a Flow-scope rule allowed; acl_rule = that rule) */
     uint32_t meta_flags; /* enum dp_meta_flag */
     uint32_t oif;        /* PacketMeta.oif (0 if None) */
     uint32_t dst_vni;    /* PacketMeta.dst_vpcd VNI (0 if None) */
@@ -283,10 +284,15 @@ typedef struct dp_rule {
     dp_prefix_t dst;
     uint32_t action;        /* ACL: 0 Allow / 1 Deny.  FF remote: dst VNI.
                                FF local: enum dp_nat_mode (source NAT mode). */
-    uint32_t action2;       /* FF remote: enum dp_nat_mode (destination NAT) */
+    uint32_t action2;       /* FF remote: enum dp_nat_mode (destination NAT).
+                               ACL: enum dp_acl_scope */
 } dp_rule_t;
 
 enum dp_acl_action { DP_ACL_ALLOW = 0, DP_ACL_DENY = 1 };
+/* AclScope (config/src/external/overlay/acl.rs:137-141; Flow is the default):
+ * a Flow-scope Allow also admits replies of a flow it allowed
+ * (acl-filter/src/lib.rs:110-128). */
+enum dp_acl_scope { DP_ACL_SCOPE_FLOW = 0, DP_ACL_SCOPE_PACKET = 1 };
 /* NatRequirement (flow-filter/src/lib.rs NatMode = Option<NatRequirement>). */
 enum dp_nat_mode { DP_NAT_NONE = 0, DP_NAT_STATIC = 1, DP_NAT_MASQUERADE = 2,
                    DP_NAT_PORT_FORWARDING = 3 };
@@ -464,6 +470,134 @@ enum dp_ctx_option {
 };
 enum dp_host_path { DP_HOST_AUTO = 0, DP_HOST_COPY = 1, DP_HOST_ZERO_COPY = 2 };
 int dp_ctx_set_option(dp_ctx_t *ctx, int option, int64_t value);
+
+/* ------------------------------------------------------------------------ */
+/* Flow table: FlowTable                              */
+/* (flow-entry/src/flow_table/table.rs:24-330) resident in HBM, consulted by */
+/* the FlowLookup stage (nf_lookup.rs:34-55) and by the flow-aware branches  */
+/* of IcmpErrorHandler (nat/src/icmp_handler/nf.rs:102-180), FlowFilter      */
+/* (flow-filter/src/lib.rs:115-349) and AclFilter (acl-filter/src/lib.rs:    */
+/* 62-138) for every context it is attached to.                              */
+/*                                                                           */
+/* Flows carry no masquerade / port-forwarding state (that is §8f rank 3):   */
+/* FlowInfoLocked.nat_state and .port_fw_state are always None, and every    */
+/* flow has a destination VPC.                                               */
+/*                                                                           */
+/* Burst semantics are the reference pipeline's: FlowLookup, the flow-filter */
+/* bypass decision and IcmpErrorHandler see flow states as they were when    */
+/* the burst started; flows invalidated by the flow-filter (a miss, or an    */
+/* outdated flow) are seen invalid by every AclFilter of the burst, and a    */
+/* packet denied by the ACL invalidates its flows for the packets after it   */
+/* (the pipeline runs FlowFilter over the whole burst, then the later stages */
+/* packet by packet: flow-filter/src/lib.rs:352-363).                        */
+/* ------------------------------------------------------------------------ */
+typedef struct dp_flow_table dp_flow_table_t;
+
+/* IpProtoKey variant (net/src/flows/flow_key.rs:360-365).  ICMP error keys
+ * (IcmpProtoKey::ErrorMsgData) are never stored: no creator of flows makes
+ * them, so dp_flow_insert rejects them and lookups of such keys miss. */
+enum dp_flow_kind {
+    DP_FLOW_TCP = 1,          /* sport / dport */
+    DP_FLOW_UDP = 2,          /* sport / dport */
+    DP_FLOW_ICMP_QUERY = 3,   /* IcmpProtoKey::QueryMsgData: sport = identifier, dport = 0 */
+    DP_FLOW_ICMP_OTHER = 4    /* IcmpProtoKey::Unsupported: ports 0 */
+};
+/* FlowStatus (net/src/flows/flow_info.rs:37-49). */
+enum dp_flow_status { DP_FLOW_ACTIVE = 0, DP_FLOW_CANCELLED = 1, DP_FLOW_EXPIRED = 2,
+                      DP_FLOW_DETACHED = 3 };
+/* FlowInfoFlags (flow_info.rs:142-149). */
+enum dp_flow_flag { DP_FLOW_INITIATOR = 1u << 0, DP_FLOW_REQ_STATIC_NAT_SRC = 1u << 1,
+                    DP_FLOW_REQ_STATIC_NAT_DST = 1u << 2 };
+
+/* FlowKey (flow_key.rs:457-463): src_vpcd (0 = None), addresses of one
+ * family (v4 in src[0..4] / dst[0..4], the rest zero), protocol key. */
+typedef struct dp_flow_key {
+    uint32_t src_vni;
+    uint8_t family;           /* 4 or 6 */
+    uint8_t kind;             /* enum dp_flow_kind */
+    uint16_t pad;
+    uint16_t sport, dport;
+    uint8_t src[16];
+    uint8_t dst[16];
+} dp_flow_key_t;
+
+/* A FlowInfo to insert (flow_info.rs:189-199). */
+typedef struct dp_flow {
+    dp_flow_key_t key;
+    uint32_t dst_vni;         /* FlowInfoLocked.dst_vpcd (required, != 0) */
+    uint32_t flags;           /* enum dp_flow_flag */
+    uint32_t pad;
+    int64_t genid;            /* FlowInfo.genid */
+    uint64_t expires_at;      /* FlowInfo.expires_at, on the caller's clock */
+} dp_flow_t;
+
+/* A flow as stored.  `ref` names one stored FlowInfo (slot + fill tag); a
+ * flow replaced or removed from the table no longer matches its ref. */
+typedef struct dp_flow_info {
+    uint64_t ref;             /* DP_FLOW_NONE: not found */
+    uint32_t status;          /* enum dp_flow_status */
+    uint32_t flags;
+    uint32_t dst_vni;
+    uint32_t pad;
+    int64_t genid;
+    uint64_t expires_at;
+    uint64_t related;         /* ref of the related flow (FlowInfo.related), DP_FLOW_NONE */
+} dp_flow_info_t;
+#define DP_FLOW_NONE UINT64_MAX
+
+/* dp_flow_insert per-flow results */
+#define DP_FLOW_INSERTED 0
+#define DP_FLOW_REPLACED 1    /* an existing flow of that key became Detached */
+#define DP_EFLOWCAP (-28)     /* FlowTableError::CapacityExceeded (ENOSPC) */
+
+/* `slots`: a power of two; the table holds at most slots / 2 flows.  The
+ * capacity (FlowTable::set_capacity) defaults to FlowTable::DEFAULT_CAPACITY
+ * (10M, table.rs:65) clamped to slots / 2. */
+int dp_flow_table_create(int device_ordinal, uint64_t slots, dp_flow_table_t **out);
+int dp_flow_table_destroy(dp_flow_table_t *ft);
+int dp_flow_table_set_capacity(dp_flow_table_t *ft, uint64_t capacity);
+
+/* FlowTable::insert for each flow in order (table.rs:134-260): the flow
+ * becomes Active; an existing flow of the same key is Detached and replaced;
+ * at capacity a new flow is refused (DP_EFLOWCAP).  `refs` / `results` may
+ * be NULL.  Synchronous. */
+int dp_flow_insert(dp_flow_table_t *ft, const dp_flow_t *flows, uint32_t n, uint64_t *refs,
+                   int32_t *results);
+/* FlowInfo::related_pair (flow_info.rs:290-339) then insert of both: exactly
+ * one flow must have DP_FLOW_INITIATOR and the keys must differ.  The second
+ * is admitted at capacity if the first is in the table and Active
+ * (table.rs:221-233).  refs[2] / results[2] may be NULL. */
+int dp_flow_insert_pair(dp_flow_table_t *ft, const dp_flow_t *a, const dp_flow_t *b,
+                        uint64_t *refs, int32_t *results);
+/* FlowTable::lookup (table.rs:267-275). */
+int dp_flow_lookup(dp_flow_table_t *ft, const dp_flow_key_t *keys, uint32_t n,
+                   dp_flow_info_t *out);
+/* Current state of stored flows by ref (status etc.; ref DP_FLOW_NONE in
+ * `out` when the ref no longer names a stored flow). */
+int dp_flow_get(dp_flow_table_t *ft, const uint64_t *refs, uint32_t n, dp_flow_info_t *out);
+/* FlowTable::remove (table.rs:282-295): the flow becomes Detached. */
+int dp_flow_remove(dp_flow_table_t *ft, const dp_flow_key_t *keys, uint32_t n,
+                   uint32_t *n_removed);
+/* FlowInfo::invalidate_pair (flow_info.rs:435-455) / update_status. */
+int dp_flow_invalidate(dp_flow_table_t *ft, const uint64_t *refs, uint32_t n);
+int dp_flow_set_status(dp_flow_table_t *ft, uint64_t ref, uint32_t status);
+/* The flow timers (FlowTable::start_timer, table.rs:160-213) up to `now`:
+ * an Active flow with expires_at <= now becomes Expired and leaves the table;
+ * a Cancelled or Expired flow leaves the table; a Detached one stays. */
+int dp_flow_sweep(dp_flow_table_t *ft, uint64_t now, uint64_t *n_removed);
+/* FlowTable::len / active_len (table.rs:297-317). */
+int dp_flow_count(dp_flow_table_t *ft, uint64_t *len, uint64_t *active);
+/* FlowLookup::new(name, Arc<FlowTable>) for this context's pipeline (and the
+ * IcmpErrorHandler's table); NULL detaches (an empty flow table).  The table
+ * must live on the context's device and outlive the attachment. */
+int dp_ctx_attach_flow_table(dp_ctx_t *ctx, dp_flow_table_t *ft);
+
+/* dp_process_burst_device plus, when `dev_flow_refs` is not NULL, the flow
+ * FlowLookup attached to each packet (PacketMeta.flow_info) as a ref
+ * (DP_FLOW_NONE: none). */
+int dp_process_burst_device_ex(dp_ctx_t *ctx, uint8_t *dev_buf, uint64_t buf_bytes,
+                               const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out, uint32_t n,
+                               uint64_t *dev_stats, uint64_t *dev_flow_refs, void *stream);
 
 /* Introspection: bytes of the device table image and its parts (for
  * DESIGN.md / bench), and the last HIP error string. */

@@ -276,6 +276,7 @@ struct Packet {
   uint64_t pay_start, pay_end;  // payload is buf[pay_start, pay_end)
   uint64_t room_start;          // first byte this packet may write
   Meta m;
+  int64_t flow = -1;            // PacketMeta.flow_info (a flow of the oracle's table)
   void done(int r) { if (m.done < 0) m.done = r; }
   void done_force(int r) { m.done = r; }
   bool is_done() const { return m.done >= 0; }
@@ -1053,6 +1054,51 @@ struct dpo_tables {
 };
 
 namespace {
+// FlowKey (net/src/flows/flow_key.rs:457-463) as a comparable value.  Its Hash
+// covers (src_vpcd, src_ip, src_port, dst_ip, dst_port) and its Eq the whole
+// key; the TCP/UDP port Eq is symmetric (flow_key.rs:57-60, 123-127) but a
+// port-swapped key hashes elsewhere, so a lookup matches the key exactly.
+struct FKey {
+  uint32_t vni = 0;
+  uint8_t fam = 0, kind = 0;
+  uint16_t sp = 0, dp = 0;
+  uint8_t src[16] = {0}, dst[16] = {0};
+  bool operator==(const FKey &o) const {
+    return vni == o.vni && fam == o.fam && kind == o.kind && sp == o.sp && dp == o.dp &&
+           memcmp(src, o.src, 16) == 0 && memcmp(dst, o.dst, 16) == 0;
+  }
+};
+struct FKeyHash {
+  size_t operator()(const FKey &k) const {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void *p, size_t n) {
+      for (size_t i = 0; i < n; i++) { h ^= ((const uint8_t *)p)[i]; h *= 1099511628211ull; }
+    };
+    mix(&k.vni, 4); mix(&k.fam, 1); mix(&k.kind, 1); mix(&k.sp, 2); mix(&k.dp, 2);
+    mix(k.src, 16); mix(k.dst, 16);
+    return (size_t)h;
+  }
+};
+// FlowInfo (net/src/flows/flow_info.rs:189-199) without masquerade / port-
+// forwarding state; `related` is the Weak of related_pair, alive while the
+// related flow is in the table.
+struct OFlow {
+  dp_flow_t d{};
+  FKey key;
+  uint32_t status = DP_FLOW_DETACHED;
+  int64_t related = -1;
+  bool in_table = false;
+};
+}  // namespace
+
+// FlowTable (flow-entry/src/flow_table/table.rs:24-330)
+struct dpo_flows {
+  std::vector<OFlow> f;                                 // every FlowInfo ever made (ref = index)
+  std::unordered_map<FKey, uint64_t, FKeyHash> map;     // the table
+  uint64_t capacity = 10000000;                         // FlowTable::DEFAULT_CAPACITY
+};
+
+namespace {
 
 // ---------------------------------------------------------------------------
 // Classifier: first match over rules in match order
@@ -1421,11 +1467,92 @@ void stage_ipforward(const dpo_tables &T, Packet &p) {
   if (p.m.has_vrf == had_vrf && (!had_vrf || p.m.vrf == vrf0)) p.m.has_vrf = false;
 }
 
-// FlowFilter (flow-filter/src/lib.rs:75-246, context/tables.rs:800-915)
-void stage_flow_filter(const dpo_tables &T, Packet &p) {
+// --- flow table ----------------------------------------------------------
+void flow_invalidate(dpo_flows *FL, int64_t r) {  // FlowInfo::invalidate (flow_info.rs:435-442)
+  if (FL && r >= 0) FL->f[r].status = DP_FLOW_CANCELLED;
+}
+bool flow_alive(const dpo_flows *FL, int64_t r) { return r >= 0 && FL->f[r].in_table; }
+void flow_invalidate_pair(dpo_flows *FL, int64_t r) {  // invalidate_pair (flow_info.rs:449-455)
+  if (!FL || r < 0) return;
+  flow_invalidate(FL, r);
+  if (flow_alive(FL, FL->f[r].related)) flow_invalidate(FL, FL->f[r].related);
+}
+int64_t flow_find(const dpo_flows *FL, const FKey &k) {  // FlowTable::lookup (table.rs:267-275)
+  auto it = FL->map.find(k);
+  return it == FL->map.end() ? -1 : (int64_t)it->second;
+}
+void key_addrs(FKey &k, int fam, const uint8_t *src, const uint8_t *dst) {
+  k.fam = (uint8_t)fam;
+  memcpy(k.src, src, fam == 4 ? 4 : 16);
+  memcpy(k.dst, dst, fam == 4 ? 4 : 16);
+}
+// FlowKey::try_from(&Packet) (flow_key.rs:589-621).  false: no key, or an
+// ICMP error key (IcmpProtoKey::ErrorMsgData), which no flow ever has.
+bool packet_flow_key(const Packet &p, FKey &k) {
+  if (p.h.net == 0) return false;
+  k = FKey{};
+  k.vni = p.m.src_vni;
+  if (p.h.net == 4) key_addrs(k, 4, p.h.v4.src, p.h.v4.dst);
+  else key_addrs(k, 6, p.h.v6.src, p.h.v6.dst);
+  switch (p.h.l4) {
+    case L4_TCP: k.kind = DP_FLOW_TCP; k.sp = p.h.tcp.sport; k.dp = p.h.tcp.dport; return true;
+    case L4_UDP: k.kind = DP_FLOW_UDP; k.sp = p.h.udp.sport; k.dp = p.h.udp.dport; return true;
+    case L4_ICMP4:
+    case L4_ICMP6: {
+      // IcmpProtoKey::new_icmp_v4/v6 (flow_key.rs:318-338): Echo Request /
+      // Reply (etherparse decodes them with code 0) carry their identifier
+      const bool v6 = p.h.l4 == L4_ICMP6;
+      const uint8_t t = p.h.icmp.raw[0], c = p.h.icmp.raw[1];
+      const bool echo = c == 0 && (v6 ? (t == 128 || t == 129) : (t == 0 || t == 8));
+      if (echo) { k.kind = DP_FLOW_ICMP_QUERY; k.sp = be16(p.h.icmp.raw + 4); return true; }
+      if (icmp_is_error_msg(p.h)) return false;
+      k.kind = DP_FLOW_ICMP_OTHER;
+      return true;
+    }
+    default: return false;
+  }
+}
+// FlowLookup::process (flow-entry/src/flow_table/nf_lookup.rs:34-55)
+void stage_flow_lookup(const dpo_flows *FL, Packet &p) {
+  if (!FL || p.is_done() || !p.overlay() || p.m.dst_vni) return;
+  FKey k;
+  if (packet_flow_key(p, k)) p.flow = flow_find(FL, k);
+}
+// FlowSummary::from_meta (flow-filter/src/lib.rs:380-398): every stored flow
+// has a destination VPC and neither masquerade nor port-forwarding state.
+struct FlowSummary {
+  bool present = false;
+  int64_t genid = 0;
+  uint32_t dst_vni = 0;
+};
+
+// FlowFilter (flow-filter/src/lib.rs:75-246, context/tables.rs:800-915), in
+// the reference's burst phases: classify + lookup (A, B) for every packet of
+// the burst, then apply_route (C) for every packet.
+struct FfWork {
+  bool lookup = false;
+  FlowSummary fs;
+  int64_t ri = -1, li = -1;  // remote / local rule (-1: miss)
+};
+void ff_classify(const dpo_tables &T, const dpo_flows *FL, Packet &p, FfWork &w) {
+  w = FfWork{};
   if (p.is_done() || !p.overlay() || p.m.dst_vni) return;
+  if (FL && p.flow >= 0) {
+    const OFlow &f = FL->f[p.flow];
+    w.fs = FlowSummary{true, f.d.genid, f.d.dst_vni};
+    // dst_vpcd_from_valid_flow (lib.rs:327-349) -> tag_for_bypass (:213-231)
+    if (f.status == DP_FLOW_ACTIVE && f.d.genid >= T.genid) {
+      p.m.dst_vni = f.d.dst_vni;
+      if (f.d.flags & DP_FLOW_REQ_STATIC_NAT_SRC) p.m.flags |= DP_META_REQ_STATIC_NAT_SRC;
+      if (f.d.flags & DP_FLOW_REQ_STATIC_NAT_DST) p.m.flags |= DP_META_REQ_STATIC_NAT_DST;
+      return;
+    }
+    // flow_revalidation_data (:296-325): without masquerade / port-forwarding
+    // state it is (None, Ungated) -- the regular lookup below
+  }
   if (p.h.net == 0) { p.done(DP_DONE_NOT_IP); return; }
   if (!p.m.src_vni) { p.done(DP_DONE_UNROUTABLE); return; }
+  w.lookup = true;
   uint8_t proto = p.h.net == 4 ? p.h.v4.proto : p.h.v6.nh;
   uint16_t sp = 0, dpp = 0;
   if (p.h.l4 == L4_TCP) { sp = p.h.tcp.sport; dpp = p.h.tcp.dport; }
@@ -1435,16 +1562,23 @@ void stage_flow_filter(const dpo_tables &T, Packet &p) {
   const auto &rem = p.h.net == 4 ? T.ffr4 : T.ffr6;
   const auto &loc = p.h.net == 4 ? T.ffl4 : T.ffl6;
   static const uint8_t zero16[16] = {0};
-  // RemoteKey has no source fields (flow-filter/src/context/tables.rs:192-207)
   Key k{proto, p.m.src_vni, 0 /* GateVni: dst_vpcd None */, 0, zero16, dst, 0, dpp};
-  int64_t ri = classify(rem, k, p.h.net);
-  if (ri < 0) { p.done(DP_DONE_FILTERED); return; }  // DestinationMiss
-  const dp_rule_t &rv = rem[ri].r;
-  // LocalKey has no destination fields (tables.rs:211-229)
-  Key k2{proto, p.m.src_vni, rv.action, 0 /* SourceGate::Ungated */, src, zero16, sp, 0};
-  int64_t li = classify(loc, k2, p.h.net);
-  if (li < 0) { p.done(DP_DONE_FILTERED); return; }  // SourceMiss
-  uint32_t src_nat = loc[li].r.action, dst_nat = rv.action2;
+  w.ri = classify(rem, k, p.h.net);
+  if (w.ri < 0) return;  // DestinationMiss
+  Key k2{proto, p.m.src_vni, rem[w.ri].r.action, 0 /* SourceGate::Ungated */, src, zero16, sp, 0};
+  w.li = classify(loc, k2, p.h.net);
+}
+void ff_apply(const dpo_tables &T, dpo_flows *FL, Packet &p, const FfWork &w) {
+  if (!w.lookup) return;
+  if (w.ri < 0 || w.li < 0) {  // DestinationMiss / SourceMiss (lib.rs:174-185)
+    flow_invalidate_pair(FL, p.flow);
+    p.done(DP_DONE_FILTERED);
+    return;
+  }
+  const auto &rem = p.h.net == 4 ? T.ffr4 : T.ffr6;
+  const auto &loc = p.h.net == 4 ? T.ffl4 : T.ffl6;
+  const dp_rule_t &rv = rem[w.ri].r;
+  uint32_t src_nat = loc[w.li].r.action, dst_nat = rv.action2;
   p.m.dst_vni = rv.action;
   // set_nat_requirements (flow-filter/src/lib.rs:233-246)
   auto apply = [&](uint32_t mode, uint32_t stat_flag) {
@@ -1454,10 +1588,14 @@ void stage_flow_filter(const dpo_tables &T, Packet &p) {
   };
   apply(src_nat, DP_META_REQ_STATIC_NAT_SRC);
   apply(dst_nat, DP_META_REQ_STATIC_NAT_DST);
+  // should_invalidate_flow (lib.rs:258-294): a flow of another generation is
+  // outdated -- a different destination, or (no masquerade / port-forwarding
+  // requirement) no longer needed
+  if (w.fs.present && w.fs.genid != T.genid) flow_invalidate_pair(FL, p.flow);
 }
 
 // AclFilter (acl-filter/src/lib.rs:51-152)
-void stage_acl(const dpo_tables &T, Packet &p) {
+void stage_acl(const dpo_tables &T, dpo_flows *FL, Packet &p) {
   if (p.is_done() || !p.overlay()) return;
   if (!p.m.src_vni || !p.m.dst_vni) { p.done(DP_DONE_UNROUTABLE); return; }
   if (p.h.net == 0) { p.done(DP_DONE_NOT_IP); return; }
@@ -1470,11 +1608,33 @@ void stage_acl(const dpo_tables &T, Packet &p) {
   const auto &tab = p.h.net == 4 ? T.acl4 : T.acl6;
   Key k{proto, p.m.src_vni, p.m.dst_vni, 0, src, dst, sp, dpp};
   int64_t ri = classify(tab, k, p.h.net);
+  // packet_has_valid_flow (acl-filter/src/lib.rs:71-94)
+  const bool valid_flow = FL && p.flow >= 0 && FL->f[p.flow].status == DP_FLOW_ACTIVE &&
+                          FL->f[p.flow].d.genid >= T.genid;
+  int64_t rr = -1;
+  const std::vector<Rule> *rtab = nullptr;
+  if (ri < 0 && valid_flow && flow_alive(FL, FL->f[p.flow].related)) {
+    // reverse_summary (lib.rs:205-217): the related flow's key between the
+    // swapped VPCs; a Flow-scope Allow admits the reply (lib.rs:110-128)
+    const FKey &rk = FL->f[FL->f[p.flow].related].key;
+    const uint8_t rproto = rk.kind == DP_FLOW_TCP ? 6 : rk.kind == DP_FLOW_UDP ? 17 : rk.fam == 4 ? 1 : 58;
+    const bool rports = rk.kind == DP_FLOW_TCP || rk.kind == DP_FLOW_UDP;
+    rtab = rk.fam == 4 ? &T.acl4 : &T.acl6;
+    Key rkey{rproto, p.m.dst_vni, p.m.src_vni, 0, rk.src, rk.dst, (uint16_t)(rports ? rk.sp : 0),
+             (uint16_t)(rports ? rk.dp : 0)};
+    rr = classify(*rtab, rkey, rk.fam);
+    if (rr >= 0 && !((*rtab)[rr].r.action == DP_ACL_ALLOW && (*rtab)[rr].r.action2 == DP_ACL_SCOPE_FLOW))
+      rr = -1;
+  }
   uint32_t action;
   if (ri >= 0) {
     action = tab[ri].r.action;
     p.m.acl_rule = tab[ri].orig_index;
     p.m.acl = action == DP_ACL_DENY ? 2 : 1;
+  } else if (rr >= 0) {
+    action = DP_ACL_ALLOW;
+    p.m.acl_rule = (*rtab)[rr].orig_index;
+    p.m.acl = 6;
   } else {
     auto it = T.acl_default.find({p.m.src_vni, p.m.dst_vni});
     if (it != T.acl_default.end()) {
@@ -1485,7 +1645,10 @@ void stage_acl(const dpo_tables &T, Packet &p) {
       p.m.acl = 5;
     }
   }
-  if (action == DP_ACL_DENY) p.done(DP_DONE_ACL_DROPPED);
+  if (action == DP_ACL_DENY) {
+    flow_invalidate_pair(FL, p.flow);
+    p.done(DP_DONE_ACL_DROPPED);
+  }
 }
 
 // Embedded transport ports (EmbeddedTransport::source / destination,
@@ -1592,7 +1755,7 @@ void stage_static_nat(const dpo_tables &T, Packet &p) {
 // ICMP and embedded IPv4 checksums (validate_checksums, :71-87) and a flow
 // key (embedded ports, or an ICMP query identifier: flow_key.rs:635-660);
 // then no flow is found and the packet goes on (nf.rs:113-120).
-void stage_icmp_error(const dpo_tables &T, Packet &p) {
+void stage_icmp_error(const dpo_tables &T, const dpo_flows *FL, Packet &p) {
   if (p.is_done() || !p.overlay() || !icmp_is_error_msg(p.h)) return;
   const Emb &e = p.h.emb;
   if (!e.present || e.tk == L4_NONE) { p.done(DP_DONE_ICMP_ERROR_INCOMPLETE); return; }
@@ -1616,6 +1779,28 @@ void stage_icmp_error(const dpo_tables &T, Packet &p) {
     }
     if (!has_id) { p.done(DP_DONE_ICMP_ERROR_INCOMPLETE); return; }  // EmbeddedMissingIcmpId
   }
+  if (!FL) return;
+  // the embedded packet's flow key, reversed, from the error's source VPC
+  // (embedded_flowkey flow_key.rs:635-660, FlowKey::reverse :569-576)
+  FKey k;
+  k.vni = p.m.src_vni;
+  if (e.net == 4) key_addrs(k, 4, e.v4.dst, e.v4.src);
+  else key_addrs(k, 6, e.v6.dst, e.v6.src);
+  if (e.tk == L4_TCP || e.tk == L4_UDP) {
+    k.kind = e.tk == L4_TCP ? DP_FLOW_TCP : DP_FLOW_UDP;
+    emb_port(e, false, k.sp);
+    emb_port(e, true, k.dp);
+  } else {
+    k.kind = DP_FLOW_ICMP_QUERY;
+    k.sp = e.full ? be16(e.icmp.raw + 4) : be16(e.part.data() + 4);
+  }
+  const int64_t r = flow_find(FL, k);
+  if (r < 0) return;  // no flow: let the packet through (nf.rs:114-121)
+  const OFlow &f = FL->f[r];
+  if (f.status != DP_FLOW_ACTIVE) { p.done(DP_DONE_FILTERED); return; }  // nf.rs:126-130
+  p.m.dst_vni = f.d.dst_vni;  // nf.rs:139-140
+  // no masquerade / port-forwarding state to translate with (nf.rs:143-152)
+  p.done(DP_DONE_FILTERED);
 }
 
 bool adj_lookup(const dpo_tables &T, const Ip &ip, uint32_t oif, uint8_t mac[6]) {
@@ -1674,8 +1859,10 @@ void serialize(Packet &p) {
   p.pay_start -= (uint64_t)need;
 }
 
-void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pkt_out_t &out) {
-  Packet p;
+// The stages before FlowFilter (Packet::new .. FlowLookup); false when the
+// frame is rejected (out is final then).
+bool process_pre(const dpo_tables &T, const dpo_flows *FL, uint8_t *buf, const dp_pkt_in_t &in,
+                 dp_pkt_out_t &out, Packet &p) {
   p.buf = buf;
   p.room_start = in.off >= DP_HEADROOM ? in.off - DP_HEADROOM : 0;
   out.off = in.off;
@@ -1687,7 +1874,7 @@ void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pk
   if (c < 0) {  // Packet::new fails: frame rejected by the driver (worker.rs:409-421)
     out.done = DP_DONE_NOT_ETHERNET;
     out.meta_flags = 0;
-    return;
+    return false;
   }
   p.pay_start = in.off + (uint64_t)c;
   p.pay_end = in.off + (uint64_t)in.len;
@@ -1706,10 +1893,14 @@ void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pk
     stage_ingress(T, p, in.iif);
     stage_ipforward(T, p);  // IP-Forward-1
   }
-  stage_icmp_error(T, p);
-  // FlowLookup: identity with an empty flow table
-  stage_flow_filter(T, p);
-  stage_acl(T, p);
+  stage_icmp_error(T, FL, p);
+  stage_flow_lookup(FL, p);  // identity with no (or an empty) flow table
+  return true;
+}
+
+// The stages after FlowFilter (AclFilter .. Egress) and serialize.
+void process_post(const dpo_tables &T, dpo_flows *FL, Packet &p, dp_pkt_out_t &out) {
+  stage_acl(T, FL, p);
   stage_static_nat(T, p);
   // PortForwarder / Masquerade: identity (no REQ_* flags from static-only tables)
   if (!p.is_done() && (p.m.flags & (DP_META_REQ_MASQUERADE | DP_META_REQ_PORT_FORWARDING)))
@@ -1729,6 +1920,98 @@ void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pk
     out.off = (uint32_t)p.pay_start;
     out.len = (uint16_t)(p.pay_end - p.pay_start);
   }
+}
+
+// Without a flow table the stages of different packets share no state, so the
+// burst is processed packet by packet.
+void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pkt_out_t &out) {
+  Packet p;
+  if (!process_pre(T, nullptr, buf, in, out, p)) return;
+  FfWork w;
+  ff_classify(T, nullptr, p, w);
+  ff_apply(T, nullptr, p, w);
+  process_post(T, nullptr, p, out);
+}
+
+// With a flow table, in the reference's burst order: the lazy stages up to
+// FlowLookup packet by packet, FlowFilter over the materialised burst (all
+// classifications, then all route applications: flow-filter/src/lib.rs:75-111,
+// 352-363), then the lazy stages after it packet by packet.
+void process_burst_flows(const dpo_tables &T, dpo_flows *FL, uint8_t *buf, const dp_pkt_in_t *in,
+                         dp_pkt_out_t *out, uint32_t n, uint64_t *flow_refs) {
+  std::vector<Packet> P(n);
+  std::vector<char> live(n);
+  std::vector<FfWork> W(n);
+  for (uint32_t i = 0; i < n; i++) live[i] = process_pre(T, FL, buf, in[i], out[i], P[i]);
+  for (uint32_t i = 0; i < n; i++) if (live[i]) ff_classify(T, FL, P[i], W[i]);
+  for (uint32_t i = 0; i < n; i++) if (live[i]) ff_apply(T, FL, P[i], W[i]);
+  for (uint32_t i = 0; i < n; i++) {
+    if (live[i]) process_post(T, FL, P[i], out[i]);
+    if (flow_refs) flow_refs[i] = live[i] && P[i].flow >= 0 ? (uint64_t)P[i].flow : DP_FLOW_NONE;
+  }
+}
+
+FKey fkey_of(const dp_flow_key_t &x) {
+  FKey k;
+  k.vni = x.src_vni; k.kind = x.kind; k.sp = x.sport; k.dp = x.dport;
+  key_addrs(k, x.family == 4 ? 4 : 6, x.src, x.dst);
+  if (x.family != 4 && x.family != 6) k.fam = x.family;
+  return k;
+}
+// What a FlowInfo can hold here (dpgpu.h dp_flow_t).
+int flow_check(const dp_flow_t &f) {
+  const dp_flow_key_t &x = f.key;
+  if (x.family != 4 && x.family != 6) return DP_EINVAL;
+  if (x.kind < DP_FLOW_TCP || x.kind > DP_FLOW_ICMP_OTHER) return DP_EINVAL;
+  if ((x.kind == DP_FLOW_TCP || x.kind == DP_FLOW_UDP) && (x.sport == 0 || x.dport == 0))
+    return DP_EINVAL;  // TcpPort / UdpPort are non-zero
+  if (x.kind == DP_FLOW_ICMP_QUERY && x.dport) return DP_EINVAL;
+  if (x.kind == DP_FLOW_ICMP_OTHER && (x.sport || x.dport)) return DP_EINVAL;
+  if (x.src_vni >= (1u << 24) || f.dst_vni == 0 || f.dst_vni >= (1u << 24)) return DP_EINVAL;
+  if (f.flags & ~7u) return DP_EINVAL;
+  return 0;
+}
+// FlowTable::insert_common (table.rs:215-260).  `partner`: the related flow
+// of a pair (the capacity exception for the second half, :221-233).
+int32_t flow_insert_one(dpo_flows *FL, const dp_flow_t &d, int64_t partner, int64_t &ref) {
+  ref = -1;
+  if (FL->map.size() >= FL->capacity &&
+      !(partner >= 0 && FL->f[partner].status == DP_FLOW_ACTIVE))
+    return DP_EFLOWCAP;
+  OFlow nf;
+  nf.d = d;
+  nf.key = fkey_of(d.key);
+  nf.status = DP_FLOW_ACTIVE;
+  nf.in_table = true;
+  ref = (int64_t)FL->f.size();
+  int32_t res = DP_FLOW_INSERTED;
+  auto it = FL->map.find(nf.key);
+  if (it != FL->map.end()) {
+    OFlow &old = FL->f[it->second];
+    const bool was_expired = old.status == DP_FLOW_EXPIRED;
+    old.status = DP_FLOW_DETACHED;
+    old.in_table = false;
+    it->second = (uint64_t)ref;
+    if (!was_expired) res = DP_FLOW_REPLACED;
+  } else {
+    FL->map.emplace(nf.key, (uint64_t)ref);
+  }
+  FL->f.push_back(nf);
+  return res;
+}
+void flow_info_of(const dpo_flows *FL, int64_t r, dp_flow_info_t &o) {
+  memset(&o, 0, sizeof(o));
+  o.ref = DP_FLOW_NONE;
+  o.related = DP_FLOW_NONE;
+  if (r < 0 || !FL->f[r].in_table) return;
+  const OFlow &f = FL->f[r];
+  o.ref = (uint64_t)r;
+  o.status = f.status;
+  o.flags = f.d.flags;
+  o.dst_vni = f.d.dst_vni;
+  o.genid = f.d.genid;
+  o.expires_at = f.d.expires_at;
+  if (flow_alive(FL, f.related)) o.related = (uint64_t)f.related;
 }
 
 bool valid_prefix(const dp_prefix_t &p) {
@@ -1829,7 +2112,7 @@ int dpo_tables_build(const dp_tables_desc_t *d, dpo_tables_t **out) {
     }
   for (auto *v : {&T->acl4, &T->acl6})
     for (auto &r : *v)
-      if (r.r.gate != 0) return DP_EINVAL;
+      if (r.r.gate != 0 || r.r.action > DP_ACL_DENY || r.r.action2 > DP_ACL_SCOPE_PACKET) return DP_EINVAL;
   for (uint32_t i = 0; i < d->n_acl_defaults; i++)
     T->acl_default[{d->acl_defaults[i].src_vni, d->acl_defaults[i].dst_vni}] = d->acl_defaults[i].action;
   for (uint32_t i = 0; i < d->n_nat_tables; i++) {
@@ -1892,6 +2175,132 @@ int dpo_process_parallel(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes
     });
   }
   for (auto &x : th) x.join();
+  return 0;
+}
+
+int dpo_process_burst_flows(const dpo_tables_t *t, dpo_flows_t *fl, uint8_t *buf, uint64_t buf_bytes,
+                            const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, uint64_t *stats,
+                            uint64_t *flow_refs) {
+  if (!t || (!buf && n)) return DP_EINVAL;
+  for (uint32_t i = 0; i < n; i++)
+    if (in[i].off < DP_HEADROOM || (uint64_t)in[i].off + in[i].len > buf_bytes) return DP_EINVAL;
+  if (!fl) {
+    for (uint32_t i = 0; i < n; i++) {
+      process_one(*t, buf, in[i], out[i]);
+      if (flow_refs) flow_refs[i] = DP_FLOW_NONE;
+    }
+  } else {
+    process_burst_flows(*t, fl, buf, in, out, n, flow_refs);
+  }
+  if (stats)
+    for (uint32_t i = 0; i < n; i++) if (out[i].done < DP_DONE_COUNT) stats[out[i].done]++;
+  return 0;
+}
+
+int dpo_flows_create(dpo_flows_t **out) {
+  if (!out) return DP_EINVAL;
+  *out = new dpo_flows();
+  return 0;
+}
+void dpo_flows_free(dpo_flows_t *fl) { delete fl; }
+int dpo_flows_set_capacity(dpo_flows_t *fl, uint64_t capacity) {
+  if (!fl) return DP_EINVAL;
+  fl->capacity = capacity;
+  return 0;
+}
+int dpo_flow_insert(dpo_flows_t *fl, const dp_flow_t *flows, uint32_t n, uint64_t *refs,
+                    int32_t *results) {
+  if (!fl || (!flows && n)) return DP_EINVAL;
+  for (uint32_t i = 0; i < n; i++) if (int rc = flow_check(flows[i])) return rc;
+  for (uint32_t i = 0; i < n; i++) {
+    int64_t r;
+    const int32_t res = flow_insert_one(fl, flows[i], -1, r);
+    if (refs) refs[i] = r < 0 ? DP_FLOW_NONE : (uint64_t)r;
+    if (results) results[i] = res;
+  }
+  return 0;
+}
+// FlowInfo::related_pair (flow_info.rs:290-339), then both inserts
+int dpo_flow_insert_pair(dpo_flows_t *fl, const dp_flow_t *a, const dp_flow_t *b, uint64_t *refs,
+                         int32_t *results) {
+  if (!fl || !a || !b) return DP_EINVAL;
+  if (int rc = flow_check(*a)) return rc;
+  if (int rc = flow_check(*b)) return rc;
+  if (fkey_of(a->key) == fkey_of(b->key)) return DP_EINVAL;
+  if (((a->flags ^ b->flags) & DP_FLOW_INITIATOR) == 0) return DP_EINVAL;
+  int64_t ra, rb;
+  const int32_t res_a = flow_insert_one(fl, *a, -1, ra);
+  const int32_t res_b = flow_insert_one(fl, *b, ra, rb);
+  if (ra >= 0 && rb >= 0) { fl->f[ra].related = rb; fl->f[rb].related = ra; }
+  if (refs) {
+    refs[0] = ra < 0 ? DP_FLOW_NONE : (uint64_t)ra;
+    refs[1] = rb < 0 ? DP_FLOW_NONE : (uint64_t)rb;
+  }
+  if (results) { results[0] = res_a; results[1] = res_b; }
+  return 0;
+}
+int dpo_flow_lookup(dpo_flows_t *fl, const dp_flow_key_t *keys, uint32_t n, dp_flow_info_t *out) {
+  if (!fl || ((!keys || !out) && n)) return DP_EINVAL;
+  for (uint32_t i = 0; i < n; i++) flow_info_of(fl, flow_find(fl, fkey_of(keys[i])), out[i]);
+  return 0;
+}
+int dpo_flow_get(dpo_flows_t *fl, const uint64_t *refs, uint32_t n, dp_flow_info_t *out) {
+  if (!fl || ((!refs || !out) && n)) return DP_EINVAL;
+  for (uint32_t i = 0; i < n; i++)
+    flow_info_of(fl, refs[i] < fl->f.size() ? (int64_t)refs[i] : -1, out[i]);
+  return 0;
+}
+int dpo_flow_remove(dpo_flows_t *fl, const dp_flow_key_t *keys, uint32_t n, uint32_t *n_removed) {
+  if (!fl || (!keys && n)) return DP_EINVAL;
+  uint32_t c = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    auto it = fl->map.find(fkey_of(keys[i]));
+    if (it == fl->map.end()) continue;
+    OFlow &f = fl->f[it->second];
+    f.status = DP_FLOW_DETACHED;
+    f.in_table = false;
+    fl->map.erase(it);
+    c++;
+  }
+  if (n_removed) *n_removed = c;
+  return 0;
+}
+int dpo_flow_invalidate(dpo_flows_t *fl, const uint64_t *refs, uint32_t n) {
+  if (!fl || (!refs && n)) return DP_EINVAL;
+  for (uint32_t i = 0; i < n; i++)
+    if (refs[i] < fl->f.size() && fl->f[refs[i]].in_table) flow_invalidate_pair(fl, (int64_t)refs[i]);
+  return 0;
+}
+int dpo_flow_set_status(dpo_flows_t *fl, uint64_t ref, uint32_t status) {
+  if (!fl || status > DP_FLOW_DETACHED) return DP_EINVAL;
+  if (ref >= fl->f.size() || !fl->f[ref].in_table) return DP_EINVAL;
+  fl->f[ref].status = status;
+  return 0;
+}
+// The flow timers up to `now` (table.rs:160-213)
+int dpo_flow_sweep(dpo_flows_t *fl, uint64_t now, uint64_t *n_removed) {
+  if (!fl) return DP_EINVAL;
+  uint64_t c = 0;
+  for (auto it = fl->map.begin(); it != fl->map.end();) {
+    OFlow &f = fl->f[it->second];
+    bool gone = false;
+    if (f.status == DP_FLOW_ACTIVE) {
+      if (f.d.expires_at <= now) { f.status = DP_FLOW_EXPIRED; gone = true; }
+    } else if (f.status == DP_FLOW_CANCELLED || f.status == DP_FLOW_EXPIRED) {
+      gone = true;
+    }
+    if (gone) { f.in_table = false; it = fl->map.erase(it); c++; }
+    else ++it;
+  }
+  if (n_removed) *n_removed = c;
+  return 0;
+}
+int dpo_flow_count(dpo_flows_t *fl, uint64_t *len, uint64_t *active) {
+  if (!fl) return DP_EINVAL;
+  uint64_t a = 0;
+  for (auto &kv : fl->map) a += fl->f[kv.second].status == DP_FLOW_ACTIVE;
+  if (len) *len = fl->map.size();
+  if (active) *active = a;
   return 0;
 }
 

@@ -49,6 +49,30 @@ int dpo_process_parallel(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes
                          const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
                          uint32_t burst, uint32_t threads);
 
+/* Flow table (flow-entry/src/flow_table/table.rs) with the dp_flow_* semantics
+ * of include/dpgpu.h; refs are indices of the FlowInfos the table made. */
+typedef struct dpo_flows dpo_flows_t;
+int dpo_flows_create(dpo_flows_t **out);
+void dpo_flows_free(dpo_flows_t *fl);
+int dpo_flows_set_capacity(dpo_flows_t *fl, uint64_t capacity);
+int dpo_flow_insert(dpo_flows_t *fl, const dp_flow_t *flows, uint32_t n, uint64_t *refs,
+                    int32_t *results);
+int dpo_flow_insert_pair(dpo_flows_t *fl, const dp_flow_t *a, const dp_flow_t *b, uint64_t *refs,
+                         int32_t *results);
+int dpo_flow_lookup(dpo_flows_t *fl, const dp_flow_key_t *keys, uint32_t n, dp_flow_info_t *out);
+int dpo_flow_get(dpo_flows_t *fl, const uint64_t *refs, uint32_t n, dp_flow_info_t *out);
+int dpo_flow_remove(dpo_flows_t *fl, const dp_flow_key_t *keys, uint32_t n, uint32_t *n_removed);
+int dpo_flow_invalidate(dpo_flows_t *fl, const uint64_t *refs, uint32_t n);
+int dpo_flow_set_status(dpo_flows_t *fl, uint64_t ref, uint32_t status);
+int dpo_flow_sweep(dpo_flows_t *fl, uint64_t now, uint64_t *n_removed);
+int dpo_flow_count(dpo_flows_t *fl, uint64_t *len, uint64_t *active);
+/* One burst through the pipeline with FlowLookup on `fl` (NULL: an empty
+ * flow table), in the reference's burst order; flow_refs (may be NULL)
+ * receives each packet's PacketMeta.flow_info (DP_FLOW_NONE: none). */
+int dpo_process_burst_flows(const dpo_tables_t *t, dpo_flows_t *fl, uint8_t *buf,
+                            uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
+                            uint32_t n, uint64_t *stats, uint64_t *flow_refs);
+
 /* Primitive restatements exposed for unit tests. */
 uint16_t dpo_checksum_ipv4_header(const uint8_t *hdr, uint32_t hlen);
 /* LPM of one address in one FIB: returns route nh index or -1. */

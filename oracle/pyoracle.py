@@ -42,6 +42,19 @@ def lib() -> C.CDLL:
         l.dpo_hash_bytes.restype = C.c_uint64
         l.dpo_reserialize.argtypes = [V, C.c_uint32, V, C.c_uint32]
         l.dpo_reserialize.restype = C.c_int
+        l.dpo_process_burst_flows.argtypes = [V, V, V, C.c_uint64, V, V, C.c_uint32, V, V]
+        l.dpo_flows_create.argtypes = [C.POINTER(V)]
+        l.dpo_flows_free.argtypes = [V]
+        l.dpo_flows_set_capacity.argtypes = [V, C.c_uint64]
+        l.dpo_flow_insert.argtypes = [V, V, C.c_uint32, V, V]
+        l.dpo_flow_insert_pair.argtypes = [V, V, V, V, V]
+        l.dpo_flow_lookup.argtypes = [V, V, C.c_uint32, V]
+        l.dpo_flow_get.argtypes = [V, V, C.c_uint32, V]
+        l.dpo_flow_remove.argtypes = [V, V, C.c_uint32, V]
+        l.dpo_flow_invalidate.argtypes = [V, V, C.c_uint32]
+        l.dpo_flow_set_status.argtypes = [V, C.c_uint64, C.c_uint32]
+        l.dpo_flow_sweep.argtypes = [V, C.c_uint64, V]
+        l.dpo_flow_count.argtypes = [V, V, V]
         _lib = l
     return _lib
 
@@ -62,6 +75,20 @@ class Oracle:
         if rc != 0:
             raise RuntimeError(f"oracle process failed rc={rc}")
         return (out, st) if stats else out
+
+    def process_flows(self, buf: np.ndarray, inp: np.ndarray, out_dtype, flows, stats=False):
+        """One burst with FlowLookup on `flows` (an OracleFlows, or None for an
+        empty flow table): (out, flow_refs[, stats])."""
+        out = np.zeros(len(inp), dtype=out_dtype)
+        refs = np.zeros(len(inp), dtype=np.uint64)
+        st = np.zeros(34, dtype=np.uint64)
+        rc = lib().dpo_process_burst_flows(self.h, flows.h if flows is not None else None,
+                                           buf.ctypes.data, buf.nbytes, inp.ctypes.data,
+                                           out.ctypes.data, len(inp), st.ctypes.data,
+                                           refs.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"oracle process failed rc={rc}")
+        return (out, refs, st) if stats else (out, refs)
 
     def process_parallel(self, buf, inp, out, threads: int, burst: int = 64):
         rc = lib().dpo_process_parallel(self.h, buf.ctypes.data, buf.nbytes, inp.ctypes.data,
@@ -86,3 +113,88 @@ def reserialize(frame: bytes) -> bytes | None:
     out = (C.c_uint8 * (len(frame) + 256))()
     n = lib().dpo_reserialize(frame, len(frame), out, len(out))
     return None if n < 0 else bytes(out[:n])
+
+
+class OracleFlows:
+    """The oracle's FlowTable with the interface of dataplane_amd.flows.FlowTable."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        lib().dpo_flows_create(C.byref(h))
+        self.h = h
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"oracle {what} rc={rc}")
+
+    def set_capacity(self, capacity: int) -> None:
+        self._chk(lib().dpo_flows_set_capacity(self.h, capacity), "set_capacity")
+
+    def insert(self, flows):
+        from dataplane_amd import _abi as A
+        flows = np.ascontiguousarray(np.atleast_1d(flows), dtype=A.FLOW)
+        refs = np.zeros(len(flows), np.uint64)
+        res = np.zeros(len(flows), np.int32)
+        self._chk(lib().dpo_flow_insert(self.h, flows.ctypes.data, len(flows), refs.ctypes.data,
+                                        res.ctypes.data), "insert")
+        return refs, res
+
+    def insert_pair(self, a, b):
+        from dataplane_amd import _abi as A
+        a = np.ascontiguousarray(a, dtype=A.FLOW)
+        b = np.ascontiguousarray(b, dtype=A.FLOW)
+        refs = np.zeros(2, np.uint64)
+        res = np.zeros(2, np.int32)
+        self._chk(lib().dpo_flow_insert_pair(self.h, a.ctypes.data, b.ctypes.data,
+                                             refs.ctypes.data, res.ctypes.data), "insert_pair")
+        return refs, res
+
+    def lookup(self, keys):
+        from dataplane_amd import _abi as A
+        keys = np.ascontiguousarray(np.atleast_1d(keys), dtype=A.FLOW_KEY)
+        out = np.zeros(len(keys), A.FLOW_INFO)
+        self._chk(lib().dpo_flow_lookup(self.h, keys.ctypes.data, len(keys), out.ctypes.data),
+                  "lookup")
+        return out
+
+    def get(self, refs):
+        from dataplane_amd import _abi as A
+        refs = np.ascontiguousarray(refs, dtype=np.uint64)
+        out = np.zeros(len(refs), A.FLOW_INFO)
+        self._chk(lib().dpo_flow_get(self.h, refs.ctypes.data, len(refs), out.ctypes.data), "get")
+        return out
+
+    def remove(self, keys) -> int:
+        from dataplane_amd import _abi as A
+        keys = np.ascontiguousarray(np.atleast_1d(keys), dtype=A.FLOW_KEY)
+        n = C.c_uint32()
+        self._chk(lib().dpo_flow_remove(self.h, keys.ctypes.data, len(keys), C.byref(n)), "remove")
+        return n.value
+
+    def invalidate(self, refs) -> None:
+        refs = np.ascontiguousarray(refs, dtype=np.uint64)
+        self._chk(lib().dpo_flow_invalidate(self.h, refs.ctypes.data, len(refs)), "invalidate")
+
+    def set_status(self, ref: int, status: int) -> None:
+        self._chk(lib().dpo_flow_set_status(self.h, int(ref), status), "set_status")
+
+    def sweep(self, now: int) -> int:
+        n = C.c_uint64()
+        self._chk(lib().dpo_flow_sweep(self.h, now, C.byref(n)), "sweep")
+        return n.value
+
+    def count(self):
+        ln, act = C.c_uint64(), C.c_uint64()
+        self._chk(lib().dpo_flow_count(self.h, C.byref(ln), C.byref(act)), "count")
+        return ln.value, act.value
+
+    def close(self):
+        if self.h:
+            lib().dpo_flows_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

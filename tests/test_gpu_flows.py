@@ -1,0 +1,139 @@
+"""GPU: the flow table (dp_flow_*) and the flows variant of the pipeline
+through the C ABI, against the oracle's restatement of the reference
+(FlowTable, FlowLookup, the flow-aware FlowFilter / AclFilter /
+IcmpErrorHandler branches, the burst order).  Bit-exact."""
+import numpy as np
+import pytest
+
+from dataplane_amd import GpuPathNf, _abi as A
+from dataplane_amd.flows import FlowTable
+from dataplane_amd.workload import Workload
+from oracle.pyoracle import Oracle, OracleFlows
+
+from edgecase import pack_burst
+from flowgen import frames_of, install, scenario
+from golden.flowkat import all_cases, run_case
+from helpers import compare
+from test_flows import table_semantics
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def nf():
+    import torch
+    torch.cuda.init()
+    n = GpuPathNf(0)
+    yield n
+    n.attach_flows(None)
+    n.close()
+
+
+def run_device(nf, buf, inp, stats=False):
+    """One device-resident burst with flow refs out: (out, refs[, stats]);
+    `buf` is rewritten in place."""
+    import torch
+    dev = torch.device("cuda", 0)
+    db = torch.from_numpy(buf).to(dev)
+    di = torch.from_numpy(inp.view(np.uint8).copy()).to(dev)
+    do = torch.zeros(len(inp) * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+    dr = torch.zeros(len(inp), dtype=torch.int64, device=dev)
+    st = torch.zeros(A.DONE_COUNT, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    nf.process_device_ex(db.data_ptr(), db.numel(), di.data_ptr(), do.data_ptr(), len(inp),
+                         st.data_ptr(), dr.data_ptr())
+    nf.synchronize()
+    buf[:] = db.cpu().numpy()
+    out = do.cpu().numpy().view(A.PKT_OUT)
+    refs = dr.cpu().numpy().view(np.uint64)
+    return (out, refs, st.cpu().numpy().view(np.uint64)) if stats else (out, refs)
+
+
+class GpuBackend:
+    def __init__(self, nf):
+        self.nf = nf
+
+    def table(self):
+        return FlowTable(0, 1 << 12)
+
+    def process(self, tb, buf, inp, ft):
+        self.nf.publish(tb.build())
+        self.nf.attach_flows(ft)
+        try:
+            return run_device(self.nf, buf, inp)
+        finally:
+            self.nf.attach_flows(None)
+
+
+def test_gpu_flow_table_semantics():
+    table_semantics(FlowTable(0, 1 << 10))
+
+
+def test_gpu_flow_known_answers(nf):
+    errs = []
+    for case in all_cases():
+        errs += run_case(case, GpuBackend(nf))
+    assert not errs, "\n".join(errs)
+
+
+def _ref_map(a, b):
+    """Translate refs of table `a` to refs of table `b` by insertion order."""
+    return {x: y for x, y in zip(a, b) if x != A.FLOW_NONE}
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gpu_flows_random_bursts(nf, seed):
+    """Seeded scenarios (tests/flowgen.py) over a C2-shaped workload: two
+    bursts in a row, then the flow timers; outputs, serialized bytes, flow
+    refs and every flow's state equal the oracle's."""
+    w = Workload(2, 6000, seed=seed, n_routes_v4=3000, n_acl=400, n_nat=24, tcp_percent=30)
+    ora = Oracle(w.tables)
+    frames = frames_of(w)
+    ob = w.fresh_buf()
+    o0 = ora.process(ob, w.inp, A.PKT_OUT)
+    items, burst = scenario(frames, o0["dst_vni"], genid=1, seed=seed, n_flows=600,
+                            vnis=sorted(set(int(v) for v in o0["dst_vni"] if v)))
+    oft, gft = OracleFlows(), FlowTable(0, 1 << 13)
+    orefs, grefs = install(oft, items), install(gft, items)
+    g2o = _ref_map(grefs, orefs)
+    nf.publish(w.tables)
+    nf.attach_flows(gft)
+    try:
+        for rnd in range(2):
+            buf, inp = pack_burst([(f, 1, A.IN_SEEDED_OVERLAY, v) for f, v in burst])
+            obuf, gbuf = buf.copy(), buf.copy()
+            oout, oref, ost = ora.process_flows(obuf, inp, A.PKT_OUT, oft, stats=True)
+            gout, gref, gst = run_device(nf, gbuf, inp, stats=True)
+            compare(oout, obuf, gout, gbuf, inp, f"flows seed {seed} burst {rnd}")
+            mapped = np.array([g2o.get(int(r), A.FLOW_NONE) if int(r) != A.FLOW_NONE else A.FLOW_NONE
+                               for r in gref], dtype=np.uint64)
+            assert np.array_equal(mapped, oref), f"flow refs differ ({np.count_nonzero(mapped != oref)})"
+            assert np.array_equal(gst, ost), "DoneReason histogram"
+            assert int((oout["acl"] == 6).sum()) > 0, "no packet took the flow-scope reply path"
+            gi, oi = gft.get(grefs), oft.get(orefs)
+            for j in range(len(grefs)):
+                gone_g, gone_o = gi[j]["ref"] == A.FLOW_NONE, oi[j]["ref"] == A.FLOW_NONE
+                assert gone_g == gone_o, f"flow {j} presence"
+                if not gone_g:
+                    assert gi[j]["status"] == oi[j]["status"], f"flow {j} status (burst {rnd})"
+        assert gft.count() == oft.count()
+        assert gft.sweep(1 << 62) == oft.sweep(1 << 62)
+        assert gft.count() == oft.count()
+    finally:
+        nf.attach_flows(None)
+
+
+def test_gpu_flows_empty_table_matches_no_table(nf):
+    """An attached empty flow table changes nothing."""
+    w = Workload(2, 4096, seed=5, n_routes_v4=2000, n_acl=300, n_nat=16)
+    ft = FlowTable(0, 1 << 8)
+    nf.publish(w.tables)
+    b0, b1 = w.fresh_buf(), w.fresh_buf()
+    out0 = nf.process_arrays(b0, w.inp)
+    nf.attach_flows(ft)
+    try:
+        out1, refs = run_device(nf, b1, w.inp)
+    finally:
+        nf.attach_flows(None)
+    compare(out0, b0, out1, b1, w.inp, "empty flow table")
+    assert (refs == np.uint64(A.FLOW_NONE)).all()
