@@ -65,7 +65,8 @@ class GpuBackend:
             self.nf.attach_flows(None)
 
 
-def test_gpu_flow_table_semantics():
+def test_gpu_flow_table_semantics(nf):
+    # (nf: torch's HIP runtime initialises before libdpgpu's claims the device)
     table_semantics(FlowTable(0, 1 << 10))
 
 
