@@ -135,6 +135,84 @@ def cpu_baseline(w: Workload, sample: int, budget_s: float) -> dict:
                          "sample": f"{ereps} x {ne} packets, {t_emu:.1f} s"}}
 
 
+def flows_leg(nf, w, dev, stream, steps: int) -> dict:
+    """The same burst with a flow table attached:
+    every other packet belongs to an established flow pair (Active, current
+    generation, its destination the packet's own flow-filter verdict), so it
+    bypasses the flow-filter tables; the pipeline runs its flows variant
+    (FlowLookup on every overlay packet, the flow-aware stages, the fix-up
+    and invalidation kernels).  Reported beside `value`, never inside it."""
+    from dataplane_amd.flows import FlowTable
+    n = w.n
+    bb = (w.buf.nbytes + 255) & ~255
+    pristine = torch.from_numpy(w.buf).to(dev)
+    b = torch.empty(bb, dtype=torch.uint8, device=dev)
+    dinp = torch.from_numpy(w.inp.view(np.uint8)).to(dev)
+    dout = torch.empty(n * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+    sptr = stream.cuda_stream
+    # each packet's flow-filter verdict, from one run without flows
+    b[:w.buf.nbytes].copy_(pristine)
+    nf.process_device(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None, sptr)
+    torch.cuda.synchronize(dev)
+    out = dout.cpu().numpy().view(A.PKT_OUT)
+    # request keys of the even packets that have a verdict (Eth / IPv4 / UDP|TCP frames)
+    off = w.inp["off"].astype(np.int64)
+    sel = np.nonzero((np.arange(n) % 2 == 0) & (out["dst_vni"] != 0) & (w.inp["src_vni"] != 0))[0]
+    o = off[sel]
+    proto = w.buf[o + 23]
+    keep = (w.buf[o + 12] == 8) & (w.buf[o + 13] == 0) & (w.buf[o + 14] == 0x45) & \
+           ((proto == 6) | (proto == 17))
+    sel, o, proto = sel[keep], o[keep], proto[keep]
+    fl = np.zeros(len(sel), A.FLOW)
+    k = fl["key"]
+    k["src_vni"] = w.inp["src_vni"][sel]
+    k["family"] = 4
+    k["kind"] = np.where(proto == 6, A.FLOW_TCP, A.FLOW_UDP)
+    k["sport"] = (w.buf[o + 34].astype(np.uint16) << 8) | w.buf[o + 35]
+    k["dport"] = (w.buf[o + 36].astype(np.uint16) << 8) | w.buf[o + 37]
+    for j in range(4):
+        k["src"][:, j] = w.buf[o + 26 + j]
+        k["dst"][:, j] = w.buf[o + 30 + j]
+    fl["key"] = k
+    fl["dst_vni"] = out["dst_vni"][sel]
+    fl["flags"] = A.FLOW_INITIATOR
+    fl["genid"] = nf.data.genid
+    fl["expires_at"] = (1 << 63) - 1
+    kb = np.ascontiguousarray(fl["key"]).view(np.uint8).reshape(len(fl), -1)
+    _, first = np.unique(kb, axis=0, return_index=True)
+    fl = fl[np.sort(first)]
+    slots = 1 << max(12, int(np.ceil(np.log2(max(1, 4 * len(fl))))))
+    ft = FlowTable(0, slots)
+    ft.set_capacity(len(fl))
+    t0 = time.perf_counter()
+    _, res = ft.insert(fl)
+    t_ins = time.perf_counter() - t0
+    nf.attach_flows(ft)
+    refs = torch.empty(n, dtype=torch.int64, device=dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps + 2)]
+    for k2 in range(steps + 2):
+        b[:w.buf.nbytes].copy_(pristine)
+        ev[k2][0].record(stream)
+        nf.process_device_ex(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None,
+                             refs.data_ptr(), sptr)
+        ev[k2][1].record(stream)
+    torch.cuda.synchronize(dev)
+    ms = sorted(a.elapsed_time(c) for a, c in ev[2:])
+    hit = int((refs.cpu().numpy().view(np.uint64) != np.uint64(A.FLOW_NONE)).sum())
+    nf.attach_flows(None)
+    ln, act = ft.count()
+    ft.close()
+    med = ms[len(ms) // 2]
+    return {"mpps_median": round(n / (med / 1e3) / 1e6, 3), "launch_ms_median": round(med, 4),
+            "flows": int((res == A.FLOW_INSERTED).sum()), "table_slots": slots,
+            "insert_s": round(t_ins, 3), "packets_with_flow": hit, "flows_active_after": int(act),
+            "what": "the same burst with a flow table attached: every other packet's flow pair "
+                    "established (Active, current generation), FlowLookup on every overlay "
+                    "packet, flow-filter bypass, flows-variant kernel + fix-up + invalidation "
+                    "kernels per launch (median of %d launches)" % steps}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,6 +225,7 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--no-flows", action="store_true", help="skip the flow-table leg")
     ap.add_argument("--no-rccl", action="store_true",
                     help="N > 1: skip the resident-burst scatter / process / gather measurement")
     # ablation knobs (0 = the config's default table sizes)
@@ -307,6 +386,8 @@ def main() -> None:
         }
         if rccl:
             result["resident_burst_scatter_gather"] = rccl
+        if world == 1 and not args.no_flows:
+            result["flow_table"] = flows_leg(nf, w, dev, stream, args.steps)
         if world == 1 and not args.no_host:
             # host-origin rate (dp_process_burst): pinned host burst buffer and
             # records, chunked H2D / kernel / D2H overlapped on several streams

@@ -11,9 +11,11 @@
  *   AclFilter -> StaticNat -> PortForwarder -> Masquerade -> IP-Forward-2 -> Egress
  *
  * followed by Packet::serialize (net/src/packet/mod.rs:363-374).  One call of
- * dp_process_burst*() runs that whole block for a burst, on the GPU, with the
- * stateless-slice preconditions of SURVEY.md §8a A7 (empty flow table, no
- * masquerade / port-forwarding exposes: those stages are identity).
+ * dp_process_burst*() runs that whole block for a burst, on the GPU.  The
+ * FlowTable FlowLookup and IcmpErrorHandler consult is a device flow table
+ * attached to the context (dp_ctx_attach_flow_table; none attached = an
+ * empty table).  Masquerade / port-forwarding exposes are
+ * refused at publish: PortForwarder and Masquerade are identity.
  *
  * A Rust `GpuPathNf: NetworkFunction` materialises the burst
  * exactly like FlowFilter::process does (flow-filter/src/lib.rs:357-362),
