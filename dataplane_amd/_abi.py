@@ -188,8 +188,19 @@ GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_p
                "dp_flow_table_destroy", "dp_flow_table_set_capacity", "dp_flow_insert",
                "dp_flow_insert_pair", "dp_flow_lookup", "dp_flow_get", "dp_flow_remove",
                "dp_flow_invalidate", "dp_flow_set_status", "dp_flow_sweep", "dp_flow_count",
-               "dp_ctx_attach_flow_table", "dp_process_burst_device_ex"]
+               "dp_ctx_attach_flow_table", "dp_process_burst_device_ex", "dp_mbuf_burst_in",
+               "dp_mbuf_burst_out", "dp_process_mbufs"]
 NP_STRUCTS = dict(dp_flow_key_t=FLOW_KEY, dp_flow_t=FLOW, dp_flow_info_t=FLOW_INFO)
+
+
+class MbufLayout(C.Structure):
+    """dp_mbuf_layout_t: byte offsets of the rte_mbuf fields the DPDK glue uses."""
+    _fields_ = [("buf_addr", C.c_uint16), ("data_off", C.c_uint16), ("nb_segs", C.c_uint16),
+                ("port", C.c_uint16), ("pkt_len", C.c_uint16), ("data_len", C.c_uint16),
+                ("buf_len", C.c_uint16), ("pad", C.c_uint16)]
+
+
+MBUF_LAYOUT_DPDK = MbufLayout(0, 16, 20, 22, 36, 40, 54, 0)  # DP_MBUF_LAYOUT_DPDK
 
 # dp_ctx_set_option (include/dpgpu.h)
 OPT_HOST_PATH = 1
@@ -245,6 +256,11 @@ def gpu_lib() -> C.CDLL:
         lib.dp_ctx_attach_flow_table.argtypes = [_VP, _VP]
         lib.dp_process_burst_device_ex.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, C.c_uint32,
                                                    _VP, _VP, _VP]
+        lib.dp_mbuf_burst_in.argtypes = [_VP, C.c_uint64, _VP, C.c_uint32, C.POINTER(MbufLayout),
+                                         _VP, C.c_uint32, _VP]
+        lib.dp_mbuf_burst_out.argtypes = [_VP, C.c_uint32, C.POINTER(MbufLayout), _VP, _VP]
+        lib.dp_process_mbufs.argtypes = [_VP, _VP, C.c_uint64, _VP, C.c_uint32,
+                                         C.POINTER(MbufLayout), _VP, C.c_uint32, _VP, _VP]
         if lib.dp_abi_version() != ABI_VERSION:
             raise RuntimeError("libdpgpu.so ABI version mismatch")
         _gpu = lib

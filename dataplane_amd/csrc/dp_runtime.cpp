@@ -171,6 +171,10 @@ struct dp_ctx {
   // invalidation events and flow-dependent ACL verdicts; a launch waits for
   // the previous flows launch before reusing it
   dp_flow_table *ft = nullptr;
+  // dp_process_mbufs: pinned, device-mapped burst records
+  dp_pkt_in_t *mb_in = nullptr;
+  dp_pkt_out_t *mb_out = nullptr;
+  uint32_t mb_cap = 0;
   FlowScratch fl_ev, fl_sens;
   hipEvent_t fl_used = nullptr;
   bool fl_armed = false;
@@ -268,6 +272,8 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   c->fl_ev.release();
   c->fl_sens.release();
+  if (c->mb_in) (void)hipHostFree(c->mb_in);
+  if (c->mb_out) (void)hipHostFree(c->mb_out);
   if (c->fl_used) (void)hipEventDestroy(c->fl_used);
   for (auto &h : c->hs) if (h) { (void)hipStreamSynchronize(h); (void)hipStreamDestroy(h); }
   for (auto &e : c->hev) if (e) (void)hipEventDestroy(e);
@@ -692,6 +698,57 @@ int dp_ctx_synchronize(dp_ctx_t *c) {
   if (e != hipSuccess) return fail(DP_EIO, "stream sync", e);
   reap(c);
   return 0;
+}
+
+// DPDK rx burst -> path -> tx-ready mbufs (include/dpgpu.h "DPDK rx / tx
+// burst glue"): the frames stay in their mempool memory, the kernel works on
+// them over PCIe (the zero-copy host path), only the records are the
+// context's own pinned arrays.
+int dp_process_mbufs(dp_ctx_t *c, const void *pool_base, uint64_t pool_bytes, void *const *mbufs, uint32_t n,
+                     const dp_mbuf_layout_t *layout, const uint32_t *port_ifindex, uint32_t n_ports,
+                     dp_pkt_out_t *out, uint64_t *stats) {
+  if (!c) return fail(DP_EINVAL, "null ctx");
+  if (n == 0) return 0;
+  if (!out || !mbufs || !layout || !pool_base) {
+    mark_failed_host(nullptr, out, n);
+    return fail(DP_EINVAL, "null argument");
+  }
+  (void)hipSetDevice(c->device);
+  if (n > c->mb_cap) {
+    if (c->mb_in) (void)hipHostFree(c->mb_in);
+    if (c->mb_out) (void)hipHostFree(c->mb_out);
+    c->mb_in = nullptr;
+    c->mb_out = nullptr;
+    c->mb_cap = 0;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&c->mb_in), sizeof(dp_pkt_in_t) * n, hipHostMallocMapped);
+    if (e == hipSuccess)
+      e = hipHostMalloc(reinterpret_cast<void **>(&c->mb_out), sizeof(dp_pkt_out_t) * n, hipHostMallocMapped);
+    if (e != hipSuccess) {
+      mark_failed_host(nullptr, out, n);
+      return fail(DP_ENOMEM, "pinned mbuf burst records", e);
+    }
+    c->mb_cap = n;
+  }
+  std::vector<dp_pkt_in_t> rin(n);
+  int rc = dp_mbuf_burst_in(pool_base, pool_bytes, mbufs, n, layout, port_ifindex, n_ports, rin.data());
+  if (rc) { mark_failed_host(nullptr, out, n); return fail(rc, "mbuf burst records"); }
+  // an mbuf outside the layout contract is InternalFailure on its own; the
+  // others run as one burst
+  std::vector<uint32_t> idx;
+  idx.reserve(n);
+  for (uint32_t i = 0; i < n; i++)
+    if (rin[i].off >= DP_HEADROOM) { c->mb_in[idx.size()] = rin[i]; idx.push_back(i); }
+  mark_failed_host(rin.data(), out, n);
+  const int mode = c->host_path;
+  c->host_path = DP_HOST_ZERO_COPY;
+  rc = idx.empty() ? 0 : dp_process_burst(c, const_cast<uint8_t *>(static_cast<const uint8_t *>(pool_base)),
+                                          pool_bytes, c->mb_in, c->mb_out, (uint32_t)idx.size(), stats);
+  c->host_path = mode;
+  if (rc) return rc;  // every out[i] InternalFailure
+  for (size_t j = 0; j < idx.size(); j++) out[idx[j]] = c->mb_out[j];
+  if (stats) stats[DP_DONE_INTERNAL_FAILURE] += n - idx.size();
+  rc = dp_mbuf_burst_out(mbufs, n, layout, rin.data(), out);
+  return rc ? fail(rc, "mbuf burst results") : 0;
 }
 
 }  // extern "C"

@@ -683,6 +683,7 @@ extern "C" uint32_t dpw_sizeof(const char *name) {
       {"dp_tables_desc_t", sizeof(dp_tables_desc_t)}, {"dp_pkt_in_t", sizeof(dp_pkt_in_t)},
       {"dp_pkt_out_t", sizeof(dp_pkt_out_t)}, {"dp_flow_key_t", sizeof(dp_flow_key_t)},
       {"dp_flow_t", sizeof(dp_flow_t)}, {"dp_flow_info_t", sizeof(dp_flow_info_t)},
+      {"dp_mbuf_layout_t", sizeof(dp_mbuf_layout_t)},
   };
   for (auto &e : tab)
     if (strcmp(e.n, name) == 0) return e.s;

@@ -134,6 +134,23 @@ class GpuPathNf:
                                                     n, dev_stats, dev_flow_refs, stream),
                 "dp_process_burst_device_ex", self.lib)
 
+    def process_mbufs(self, pool_base: int, pool_bytes: int, mbufs: np.ndarray,
+                      port_ifindex: Optional[np.ndarray] = None,
+                      stats: Optional[np.ndarray] = None, layout=None) -> np.ndarray:
+        """An rx burst of rte_mbufs (addresses in `mbufs`) through the path in
+        their pinned, device-mapped mempool region (dp_process_mbufs): the
+        delivered mbufs hold their serialized frames, ready for tx."""
+        mbufs = np.ascontiguousarray(mbufs, dtype=np.uint64)
+        out = np.zeros(len(mbufs), dtype=A.PKT_OUT)
+        pif = None if port_ifindex is None else np.ascontiguousarray(port_ifindex, dtype=np.uint32)
+        A.check(self.lib.dp_process_mbufs(self.ctx, pool_base, pool_bytes, mbufs.ctypes.data,
+                                          len(mbufs), C.byref(layout or A.MBUF_LAYOUT_DPDK),
+                                          pif.ctypes.data if pif is not None else None,
+                                          len(pif) if pif is not None else 0, out.ctypes.data,
+                                          stats.ctypes.data if stats is not None else None),
+                "dp_process_mbufs", self.lib)
+        return out
+
     def process_device(self, dev_buf: int, buf_bytes: int, dev_in: int, dev_out: int, n: int,
                        dev_stats: Optional[int] = None, stream: Optional[int] = None) -> None:
         """Device-resident burst (dp_process_burst_device): raw device pointers."""

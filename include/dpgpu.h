@@ -601,6 +601,58 @@ int dp_process_burst_device_ex(dp_ctx_t *ctx, uint8_t *dev_buf, uint64_t buf_byt
                                const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out, uint32_t n,
                                uint64_t *dev_stats, uint64_t *dev_flow_refs, void *stream);
 
+/* ------------------------------------------------------------------------ */
+/* DPDK rx / tx burst glue: an rx burst of rte_mbufs  */
+/* (RxQueue::receive, dpdk/src/queue/rx.rs:178-201) runs through the path in */
+/* place in its mempool memory, and every delivered mbuf is left holding its */
+/* serialized frame, ready for TxQueue::transmit (dpdk/src/queue/tx.rs:      */
+/* 144-160).  The mempool region must be pinned and device-mapped            */
+/* (hipHostRegister of the hugepage memzone): the kernel reads and rewrites  */
+/* the frames over PCIe, no staging copies (the zero-copy host path).        */
+/* Mbuf::raw_data (dpdk/src/mem.rs:502-522): the frame is the first segment, */
+/* buf_addr + data_off, data_len bytes.                                      */
+/* ------------------------------------------------------------------------ */
+
+/* Byte offsets of the rte_mbuf fields this glue reads and writes; the
+ * default is the rte_mbuf_core.h layout of the reference's DPDK (v26.03,
+ * npins/sources.json: githedgehog/dpdk@fa7e361) on 64-bit targets. */
+typedef struct dp_mbuf_layout {
+    uint16_t buf_addr;    /* void *   */
+    uint16_t data_off;    /* uint16_t */
+    uint16_t nb_segs;     /* uint16_t */
+    uint16_t port;        /* uint16_t */
+    uint16_t pkt_len;     /* uint32_t */
+    uint16_t data_len;    /* uint16_t */
+    uint16_t buf_len;     /* uint16_t */
+    uint16_t pad;
+} dp_mbuf_layout_t;
+#define DP_MBUF_LAYOUT_DPDK {0, 16, 20, 22, 36, 40, 54, 0}
+
+/* Burst records for an rx burst: in[i].off = the frame's offset from
+ * `pool_base`, .len = data_len, .iif = port_ifindex[port] (the driver's
+ * PacketMeta.iif; `port_ifindex` NULL: the port number).  An mbuf whose frame
+ * lies outside [pool_base, pool_base + pool_bytes), beyond 4 GiB of it, or
+ * with less than DP_HEADROOM bytes of headroom, gets a record the pipeline
+ * marks InternalFailure.  Host only (no device call). */
+int dp_mbuf_burst_in(const void *pool_base, uint64_t pool_bytes, void *const *mbufs, uint32_t n,
+                     const dp_mbuf_layout_t *layout, const uint32_t *port_ifindex,
+                     uint32_t n_ports, dp_pkt_in_t *in);
+/* Apply a burst's results to its mbufs: a Delivered mbuf's data_off,
+ * data_len and pkt_len describe its serialized frame (prepend / trim of the
+ * headroom, dpdk/src/mem.rs:547-590); other mbufs are left as received (the
+ * caller frees them).  Host only. */
+int dp_mbuf_burst_out(void *const *mbufs, uint32_t n, const dp_mbuf_layout_t *layout,
+                      const dp_pkt_in_t *in, const dp_pkt_out_t *out);
+/* dp_mbuf_burst_in, the pipeline over the mapped mempool region (zero copy),
+ * dp_mbuf_burst_out.  `out` (host memory) receives every packet's result;
+ * the caller transmits the Delivered mbufs on their out[i].oif and frees the
+ * others.  Synchronous.  A pool that is not device-mapped fails with
+ * DP_EINVAL (every out[i] InternalFailure). */
+int dp_process_mbufs(dp_ctx_t *ctx, const void *pool_base, uint64_t pool_bytes,
+                     void *const *mbufs, uint32_t n, const dp_mbuf_layout_t *layout,
+                     const uint32_t *port_ifindex, uint32_t n_ports, dp_pkt_out_t *out,
+                     uint64_t *stats);
+
 /* Introspection: bytes of the device table image and its parts (for
  * DESIGN.md / bench), and the last HIP error string. */
 uint64_t dp_tables_device_bytes(const dp_ctx_t *ctx);
