@@ -57,7 +57,7 @@ struct FlowCtx {
   FlowSlot *slots;
   uint32_t mask;        // slots - 1
   uint32_t n;           // packets of the burst
-  // invalidation events: [0] count, then canonical slots (<= 2 per packet)
+  // invalidation events: [0] count, then the invalidated flows' slots (<= 2 per packet)
   uint32_t *events;
   // ACL decisions that rest on a flow's validity (acl = 6): [0] count, then
   // SensRec records
@@ -71,12 +71,13 @@ struct FlowCtx {
 // peering default instead (dp_flow_fixup), with the meta as it was at the ACL.
 struct SensRec {
   uint32_t idx;         // packet index
-  uint32_t canon;       // canonical slot of its flow pair
+  uint32_t slot;        // its flow
   uint32_t meta_flags;  // at the ACL
   uint32_t oif;         // at the ACL (0: None)
   uint32_t fib_entry;   // at the ACL
   uint32_t def_acl;     // the default verdict: out.acl code 3 / 4 / 5
-  uint32_t pad[2];
+  uint32_t related;     // the flow's related slot and its state when paired
+  uint32_t related_tag;
 };
 
 __host__ __device__ inline uint64_t make_ref(uint32_t slot, uint32_t state) {

@@ -1462,12 +1462,12 @@ __device__ __forceinline__ uint8_t icmp_error_check(const Frame &F, const Hdr &H
 struct FlowPk {
   uint32_t slot;       // kNoSlot: none
   uint32_t state;      // its slot state word (the ref's tag)
-  uint32_t canon;      // the pair's canonical slot: min(slot, live related)
-  uint32_t related;    // the related flow's slot if it is in the table, else kNoSlot
+  uint32_t related;    // the related flow's slot (kNoSlot: none) and its state when
+  uint32_t related_tag;  // the pair was made: alive while that slot still holds it
   uint32_t dst_vni, fflags;
   int64_t genid;
   bool active;         // FlowStatus::Active
-  uint32_t ev0, ev1;   // pair invalidations: flow-filter, ACL deny (kNoSlot: none)
+  uint32_t ev0, ev1;   // pair invalidations (the flow's slot): flow-filter, ACL deny (kNoSlot: none)
   uint32_t ev_mark;    // mark of ev1 (ACL deny at packet idx: idx + 1)
   bool sens;           // ACL allowed it as the reply of a flow-scope-allowed flow
   uint32_t def_acl, s_flags, s_oif, s_fib;
@@ -1483,14 +1483,19 @@ __device__ __forceinline__ uint32_t be16_bytes(const Frame &F, int f) {
 }
 
 // FlowTable::lookup (flow-entry/src/flow_table/table.rs:267-275): linear
-// probing from the key's hash; one 128-byte line per slot, its first 48
-// bytes (state + key) fetched in one round trip.
-__device__ __forceinline__ uint32_t flow_probe(const dpf::FlowCtx &fc, const dpf::FKey &k, uint32_t &state) {
+// probing from the key's hash; one 128-byte line per slot, whose state, key
+// and FlowInfo words (the first 80 bytes) are fetched in one round trip.
+// v / w: the found slot's words 48..63 (status, flags, dst_vni, related) and
+// 64..79 (related_tag, mark, genid).
+__device__ __forceinline__ uint32_t flow_probe(const dpf::FlowCtx &fc, const dpf::FKey &k, uint32_t &state,
+                                               uint4 &v, uint4 &w) {
   uint32_t i = dpf::fkey_hash(k) & fc.mask;
 #pragma unroll 1
   for (uint32_t p = 0; p <= fc.mask; p++) {
     const dpf::FlowSlot *s = fc.slots + i;
     const uint4 a = ld4(&s->state), b = ld4(&s->src[0]), c = ld4(&s->dst[0]);
+    v = ld4(&s->status);
+    w = ld4(&s->related_tag);
     const uint32_t st = a.x & 3u;
     if (st == dpf::FS_EMPTY) return dpf::kNoSlot;
     if (st == dpf::FS_FULL && a.y == k.w[0] && a.z == k.w[1] && a.w == k.w[2] && b.x == k.w[3] &&
@@ -1545,23 +1550,17 @@ __device__ __forceinline__ bool packet_fkey(const Frame &F, const Hdr &H, const 
   return true;
 }
 
-// Attach a found flow: its FlowInfo fields and whether its related flow is
-// still in the table (a Weak that upgrades), as the burst starts.
-__device__ __forceinline__ void flow_attach(const dpf::FlowCtx &fc, uint32_t slot, uint32_t state, FlowPk &fp) {
-  const dpf::FlowSlot *s = fc.slots + slot;
-  const uint4 v = ld4(&s->status), w = ld4(&s->related_tag);
+// Attach a found flow (PacketMeta.flow_info): its FlowInfo as the burst started.
+__device__ __forceinline__ void flow_attach(uint32_t slot, uint32_t state, const uint4 &v, const uint4 &w,
+                                            FlowPk &fp) {
   fp.slot = slot;
   fp.state = state;
   fp.active = v.x == DP_FLOW_ACTIVE;
   fp.fflags = v.y;
   fp.dst_vni = v.z;
+  fp.related = v.w;
+  fp.related_tag = w.x;
   fp.genid = (int64_t)(((uint64_t)w.w << 32) | w.z);
-  fp.related = dpf::kNoSlot;
-  fp.canon = slot;
-  if (v.w <= fc.mask && fc.slots[v.w].state == w.x) {
-    fp.related = v.w;
-    fp.canon = slot < v.w ? slot : v.w;
-  }
 }
 
 // IcmpErrorHandler with a flow table (nat/src/icmp_handler/nf.rs:102-152):
@@ -1592,9 +1591,9 @@ __device__ __forceinline__ void icmp_error_flow(const dpf::FlowCtx &fc, const Fr
     k.w[7 + j] = w ? le32_at(F, E.off + so + 4 * j) : 0u;
   }
   uint32_t st;
-  const uint32_t sl = flow_probe(fc, k, st);
+  uint4 v, w;
+  const uint32_t sl = flow_probe(fc, k, st, v, w);
   if (sl == dpf::kNoSlot) return;  // no flow: let it through (nf.rs:114-121)
-  const uint4 v = ld4(&fc.slots[sl].status);
   if (v.x == DP_FLOW_ACTIVE) S.dst_vni = v.z;  // nf.rs:139-140
   done(S, DP_DONE_FILTERED);                   // inactive (:126-130) / no NAT state (:143-152)
 }
@@ -2010,7 +2009,7 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   const Hit rh = classify<W_ACTION | W_ACTION2 | W_AUX>(g, CLS_ARRAYS(ff_remote, t), rg, t, proto,
                                                        Key128{0, 0}, dst, 0, S.dport, pre);
   if (rh.rule < 0) {
-    if constexpr (FL) if (fp.slot != dpf::kNoSlot) fp.ev0 = fp.canon;
+    if constexpr (FL) if (fp.slot != dpf::kNoSlot) fp.ev0 = fp.slot;
     done(S, DP_DONE_FILTERED);
     return;
   }
@@ -2023,7 +2022,7 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   if (t == 0) hoist_walks(g, S, pi, P);
   const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, proto, src, Key128{0, 0}, S.sport, 0, P.ffl);
   if (lh.rule < 0) {
-    if constexpr (FL) if (fp.slot != dpf::kNoSlot) fp.ev0 = fp.canon;
+    if constexpr (FL) if (fp.slot != dpf::kNoSlot) fp.ev0 = fp.slot;
     done(S, DP_DONE_FILTERED);
     return;
   }
@@ -2032,7 +2031,7 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   S.pair = pi;
   if (snat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
   if (dnat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_DST;
-  if constexpr (FL) if (fp.slot != dpf::kNoSlot && fp.genid != fc->genid) fp.ev0 = fp.canon;
+  if constexpr (FL) if (fp.slot != dpf::kNoSlot && fp.genid != fc->genid) fp.ev0 = fp.slot;
 }
 
 // AclFilter (acl-filter/src/lib.rs:51-138).  The classifier action word
@@ -2068,9 +2067,10 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
     action = v ? v - 1 : DP_ACL_ALLOW;
     S.acl = def;
     if constexpr (FL) {
-      if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid && fp.related != dpf::kNoSlot) {
+      if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid && fp.related <= fc->mask) {
         const dpf::FlowSlot *r = fc->slots + fp.related;
         const uint4 a = ld4(&r->state), b = ld4(&r->src[0]), c = ld4(&r->dst[0]);
+        if (a.x == fp.related_tag) {  // the related flow is still in the table (Weak::upgrade)
         const uint32_t fam = a.z & 0xffu, kind = a.z >> 8;
         const bool ports = kind == DP_FLOW_TCP || kind == DP_FLOW_UDP;
         const uint8_t rproto = kind == DP_FLOW_TCP ? 6 : kind == DP_FLOW_UDP ? 17 : fam == 4 ? 1 : 58;
@@ -2101,11 +2101,12 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
           fp.s_oif = S.has_oif ? S.oif : 0;
           fp.s_fib = S.fib_entry;
         }
+        }
       }
     }
   }
   if (action == DP_ACL_DENY) {
-    if constexpr (FL) if (fp.slot != dpf::kNoSlot) { fp.ev1 = fp.canon; fp.ev_mark = idx + 1; }
+    if constexpr (FL) if (fp.slot != dpf::kNoSlot) { fp.ev1 = fp.slot; fp.ev_mark = idx + 1; }
     done(S, DP_DONE_ACL_DROPPED);
   }
 }
@@ -2517,8 +2518,9 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
     dpf::FKey k;
     uint32_t st;
     if (S.done == DONE_NONE && (S.flags & DP_META_IS_OVERLAY) && !S.dst_vni && packet_fkey(F, H, S, k)) {
-      const uint32_t sl = flow_probe(*fc, k, st);
-      if (sl != dpf::kNoSlot) flow_attach(*fc, sl, st, fp);
+      uint4 v, w;
+      const uint32_t sl = flow_probe(*fc, k, st, v, w);
+      if (sl != dpf::kNoSlot) flow_attach(sl, st, v, w, fp);
     }
   }
   Pre P;
@@ -2654,7 +2656,7 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
     base = (uint32_t)__shfl((int)base, leader);
     if (sv) {
       dpf::SensRec *R = reinterpret_cast<dpf::SensRec *>(fc.sens + 8) + base + __popcll(ms & lanes_below(lane));
-      *R = dpf::SensRec{i, fp.canon, fp.s_flags, fp.s_oif, fp.s_fib, fp.def_acl, {0, 0}};
+      *R = dpf::SensRec{i, fp.slot, fp.s_flags, fp.s_oif, fp.s_fib, fp.def_acl, fp.related, fp.related_tag};
     }
   }
 }
@@ -2729,7 +2731,10 @@ __global__ void __launch_bounds__(256) dp_flow_fixup(dpf::FlowCtx fc, const dp_p
   const dpf::SensRec *recs = reinterpret_cast<const dpf::SensRec *>(fc.sens + 8);
   for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < cnt; r += gridDim.x * 256) {
     const dpf::SensRec R = recs[r];
-    if (fc.slots[R.canon].mark > R.idx) continue;  // still valid at its ACL
+    // the pair is invalid if either flow was invalidated (invalidate_pair
+    // marks the flow it was called on; the related flow only while alive)
+    const bool rel = R.related <= fc.mask && fc.slots[R.related].state == R.related_tag;
+    if (fc.slots[R.slot].mark > R.idx && (!rel || fc.slots[R.related].mark > R.idx)) continue;  // still valid
     dp_pkt_out_t o = out[R.idx];
     o.acl = (uint8_t)R.def_acl;
     o.acl_rule = 0xffffffffu;
