@@ -142,7 +142,7 @@ def flows_leg(nf, w, dev, stream, steps: int) -> dict:
     bypasses the flow-filter tables; the pipeline runs its flows variant
     (FlowLookup on every overlay packet, the flow-aware stages, the fix-up
     and invalidation kernels).  Reported beside `value`, never inside it."""
-    from dataplane_amd.flows import FlowTable
+    from dataplane_amd.flows import FlowTable, burst_request_flows
     n = w.n
     bb = (w.buf.nbytes + 255) & ~255
     pristine = torch.from_numpy(w.buf).to(dev)
@@ -155,32 +155,8 @@ def flows_leg(nf, w, dev, stream, steps: int) -> dict:
     nf.process_device(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None, sptr)
     torch.cuda.synchronize(dev)
     out = dout.cpu().numpy().view(A.PKT_OUT)
-    # request keys of the even packets that have a verdict (Eth / IPv4 / UDP|TCP frames)
-    off = w.inp["off"].astype(np.int64)
-    sel = np.nonzero((np.arange(n) % 2 == 0) & (out["dst_vni"] != 0) & (w.inp["src_vni"] != 0))[0]
-    o = off[sel]
-    proto = w.buf[o + 23]
-    keep = (w.buf[o + 12] == 8) & (w.buf[o + 13] == 0) & (w.buf[o + 14] == 0x45) & \
-           ((proto == 6) | (proto == 17))
-    sel, o, proto = sel[keep], o[keep], proto[keep]
-    fl = np.zeros(len(sel), A.FLOW)
-    k = fl["key"]
-    k["src_vni"] = w.inp["src_vni"][sel]
-    k["family"] = 4
-    k["kind"] = np.where(proto == 6, A.FLOW_TCP, A.FLOW_UDP)
-    k["sport"] = (w.buf[o + 34].astype(np.uint16) << 8) | w.buf[o + 35]
-    k["dport"] = (w.buf[o + 36].astype(np.uint16) << 8) | w.buf[o + 37]
-    for j in range(4):
-        k["src"][:, j] = w.buf[o + 26 + j]
-        k["dst"][:, j] = w.buf[o + 30 + j]
-    fl["key"] = k
-    fl["dst_vni"] = out["dst_vni"][sel]
-    fl["flags"] = A.FLOW_INITIATOR
-    fl["genid"] = nf.data.genid
-    fl["expires_at"] = (1 << 63) - 1
-    kb = np.ascontiguousarray(fl["key"]).view(np.uint8).reshape(len(fl), -1)
-    _, first = np.unique(kb, axis=0, return_index=True)
-    fl = fl[np.sort(first)]
+    # the even packets' request flows (Eth / IPv4 / UDP|TCP frames with a verdict)
+    fl = burst_request_flows(w.buf, w.inp, np.arange(0, n, 2), out["dst_vni"], nf.data.genid)
     slots = 1 << max(12, int(np.ceil(np.log2(max(1, 4 * len(fl))))))
     ft = FlowTable(0, slots)
     ft.set_capacity(len(fl))

@@ -145,6 +145,39 @@ class FlowTable:
             pass
 
 
+def burst_request_flows(buf: np.ndarray, inp: np.ndarray, sel: np.ndarray, dst_vni: np.ndarray,
+                        genid: int, flags: int = A.FLOW_INITIATOR) -> np.ndarray:
+    """Flows (one per distinct key) for the packets `sel` of a burst of
+    untagged Eth / IPv4 (no options) / TCP|UDP frames seeded with their
+    source VNI: FlowKey::try_from of each packet, its destination VPC
+    `dst_vni[i]`, `genid`, never expiring.  Vectorised; other frames are
+    skipped."""
+    off = inp["off"].astype(np.int64)
+    sel = np.asarray(sel)
+    o = off[sel]
+    proto = buf[o + 23]
+    keep = (buf[o + 12] == 8) & (buf[o + 13] == 0) & (buf[o + 14] == 0x45) & \
+           ((proto == 6) | (proto == 17)) & (inp["src_vni"][sel] != 0) & (dst_vni[sel] != 0)
+    sel, o, proto = sel[keep], o[keep], proto[keep]
+    fl = np.zeros(len(sel), A.FLOW)
+    k = fl["key"]
+    k["src_vni"] = inp["src_vni"][sel]
+    k["family"] = 4
+    k["kind"] = np.where(proto == 6, A.FLOW_TCP, A.FLOW_UDP)
+    k["sport"] = (buf[o + 34].astype(np.uint16) << 8) | buf[o + 35]
+    k["dport"] = (buf[o + 36].astype(np.uint16) << 8) | buf[o + 37]
+    for j in range(4):
+        k["src"][:, j] = buf[o + 26 + j]
+        k["dst"][:, j] = buf[o + 30 + j]
+    fl["dst_vni"] = dst_vni[sel]
+    fl["flags"] = flags
+    fl["genid"] = genid
+    fl["expires_at"] = NEVER
+    kb = np.ascontiguousarray(fl["key"]).view(np.uint8).reshape(len(fl), -1)
+    _, first = np.unique(kb, axis=0, return_index=True)
+    return fl[np.sort(first)]
+
+
 def key_records(keys: Sequence[np.ndarray]) -> np.ndarray:
     out = np.zeros(len(keys), A.FLOW_KEY)
     for i, k in enumerate(keys):

@@ -118,3 +118,17 @@ def test_flow_insert_rejects_invalid():
         ft.insert_pair(a, make_flow(reverse_key(k4(0), 200), 100))
     with pytest.raises(RuntimeError):              # identical keys
         ft.insert_pair(make_flow(k4(0), 200, A.FLOW_INITIATOR), a)
+
+
+def test_burst_request_flows_match_packet_keys():
+    """The vectorised flow builder (bench, full-size tests) makes exactly
+    FlowKey::try_from of each frame (tests/flowgen.frame_key)."""
+    from dataplane_amd.flows import burst_request_flows
+    from dataplane_amd.workload import Workload
+    from flowgen import frame_key, frames_of
+    w = Workload(2, 3000, seed=4, n_routes_v4=1000, n_acl=100, n_nat=8, tcp_percent=30)
+    dst = np.full(w.n, 7, np.uint32)
+    fl = burst_request_flows(w.buf, w.inp, np.arange(w.n), dst, genid=3)
+    want = {frame_key(f, v).tobytes() for f, v in frames_of(w) if v}
+    got = {np.ascontiguousarray(k).tobytes() for k in fl["key"]}
+    assert got == want and (fl["dst_vni"] == 7).all() and (fl["genid"] == 3).all()

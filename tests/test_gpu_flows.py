@@ -138,3 +138,38 @@ def test_gpu_flows_empty_table_matches_no_table(nf):
         nf.attach_flows(None)
     compare(out0, b0, out1, b1, w.inp, "empty flow table")
     assert (refs == np.uint64(A.FLOW_NONE)).all()
+
+
+def test_gpu_flows_full_size(nf):
+    """BASELINE.json's C2 tables (1M routes, 10k ACL rules, NAT) with a
+    flow table of ~250k established flows over a 500k-packet burst: every
+    output, byte, flow ref and flow state equals the oracle's."""
+    from dataplane_amd.flows import burst_request_flows
+    w = Workload(2, 500_000, seed=9)
+    ora = Oracle(w.tables)
+    nf.publish(w.tables)
+    o0 = nf.process_arrays(w.fresh_buf(), w.inp)   # each packet's flow-filter verdict
+    fl = burst_request_flows(w.buf, w.inp, np.arange(0, w.n, 2), o0["dst_vni"], genid=1)
+    # a tenth of them from another generation, a tenth towards another VPC
+    fl["genid"][::10] = 0
+    fl["dst_vni"][5::10] = np.roll(fl["dst_vni"], 1)[5::10]
+    oft, gft = OracleFlows(), FlowTable(0, 1 << 20)
+    oref, ores = oft.insert(fl)
+    gref, gres = gft.insert(fl)
+    assert np.array_equal(ores, gres) and (gres == A.FLOW_INSERTED).all()
+    g2o = _ref_map(gref, oref)
+    nf.attach_flows(gft)
+    try:
+        obuf, gbuf = w.fresh_buf(), w.fresh_buf()
+        oout, orf = ora.process_flows(obuf, w.inp, A.PKT_OUT, oft)
+        gout, grf = run_device(nf, gbuf, w.inp)
+    finally:
+        nf.attach_flows(None)
+    compare(oout, obuf, gout, gbuf, w.inp, "flows full size")
+    mapped = np.array([g2o.get(int(r), A.FLOW_NONE) if int(r) != A.FLOW_NONE else A.FLOW_NONE
+                       for r in grf], dtype=np.uint64)
+    assert np.array_equal(mapped, orf)
+    assert int((orf != np.uint64(A.FLOW_NONE)).sum()) >= len(fl)
+    gi, oi = gft.get(gref), oft.get(oref)
+    assert np.array_equal(gi["status"], oi["status"])
+    assert gft.count() == oft.count()
