@@ -1849,7 +1849,15 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   const FibRec &fb = g.at<FibRec>(g.im.fibs)[fi];  // fields read where used (no struct copy)
   uint8_t fam; Addr16 dst;
   cur_dst(F, H, S, fam, dst);
-  const uint32_t nhi = (fam == 4 && d4) ? lpm_walk(g, d4, b4, k4, dst) : lpm_lookup(g, fam == 4 ? fb.v4 : fb.v6, dst);
+  // one walk for every lane: v4 and v6 lanes of a wave issue their direct-table
+  // loads together (two call sites would run one after the other)
+  if (!(fam == 4 && d4)) {
+    const Lpm &L = fam == 4 ? fb.v4 : fb.v6;
+    d4 = L.direct;
+    b4 = L.dbits;
+    k4 = L.blocks;
+  }
+  const uint32_t nhi = lpm_walk(g, d4, b4, k4, dst);
   TRIP();
   const NhRec nr = g.at<NhRec>(g.im.nh_recs)[nhi];
   if (nr.kind != DPD_NH_CHAIN) {

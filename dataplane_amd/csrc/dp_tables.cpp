@@ -710,9 +710,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     memcpy(fr.vtep_ip, s.vtep_ip.addr, s.vtep_ip.family == 6 ? 16 : 4);
     uint32_t d4 = r4[f].size() > 65536 ? 24 : 16;
     fr.v4 = build_lpm(ib, pb, r4[f], 32, d4);
-    // a large v6 FIB gets a 24-bit direct table too: two fewer Poptrie levels
-    // (dependent loads) for the common /48s
-    fr.v6 = build_lpm(ib, pb, r6[f], 128, r6[f].size() > 65536 ? 24 : 16);
+    fr.v6 = build_lpm(ib, pb, r6[f], 128, 16);
     fibs.push_back(fr);
     vrfkv.push_back(KV{s.vrf_id, 0, 0, f});
   }

@@ -41,13 +41,3 @@ def test_emu_dir24_8(cfg):
     o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT)
     compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} dir24-8")
 
-
-def test_emu_v6_direct24():
-    """More than 64Ki v6 routes: the v6 LPM starts from a 24-bit direct table
-    (Poptrie below it)."""
-    w = Workload(5, 20000, seed=450, n_routes_v4=3000, n_routes_v6=80000, n_acl=400,
-                 n_nat=48, tcp_percent=25, layout="dpdk")
-    b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
-    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
-    o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT)
-    compare(o_ref, b_ref, o_dut, b_dut, w.inp, "C5 v6 direct-24")
