@@ -1373,29 +1373,34 @@ __device__ __forceinline__ uint32_t sum_frame(const Frame &F, int a, int e) {
   int d0 = wa & ~3, d1 = (we + 3) & ~3;
   uint64_t s = 0;
   const uint8_t *gbase = F.g - F.shift;  // 16-aligned HBM address of window pos 0
-  for (int d = d0; d < d1; d += 4) {
-    uint32_t w;
-    if (F.inwin || d + 4 <= WIN) w = *reinterpret_cast<const lds_u32 *>(F.lds + d);
-    else {
-      // whole 16-byte chunks from HBM when possible
-      if ((d & 15) == 0 && d + 16 <= d1) {
-        uint4 q = *reinterpret_cast<const uint4 *>(gbase + d);
-        uint32_t ws[4] = {q.x, q.y, q.z, q.w};
-        for (int k = 0; k < 4; k++) {
-          uint32_t x = ws[k];
-          int dd = d + 4 * k;
-          if (dd < wa) x &= 0xffffffffu << (8 * (wa - dd));
-          if (dd + 4 > we) x &= 0xffffffffu >> (8 * (dd + 4 - we));
-          s += x;
-        }
-        d += 12;
-        continue;
-      }
-      w = *reinterpret_cast<const uint32_t *>(gbase + d);
+  auto masked = [&](uint32_t x, int dd) -> uint32_t {
+    if (dd < wa) x &= 0xffffffffu << (8 * (wa - dd));
+    if (dd + 4 > we) x &= 0xffffffffu >> (8 * (dd + 4 - we));
+    return x;
+  };
+  int d = d0;
+  while (d < d1) {
+    if (F.inwin || d + 4 <= WIN) {
+      s += masked(*reinterpret_cast<const lds_u32 *>(F.lds + d), d);
+      d += 4;
+    } else if ((d & 15) == 0 && d + 64 <= d1) {
+      // beyond the window: 64 bytes per round trip (four 16-byte loads
+      // issued together), not one load waited on per iteration
+      const uint4 *q = reinterpret_cast<const uint4 *>(gbase + d);
+      const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+      s += (uint64_t)masked(q0.x, d) + masked(q0.y, d + 4) + masked(q0.z, d + 8) + masked(q0.w, d + 12);
+      s += (uint64_t)masked(q1.x, d + 16) + masked(q1.y, d + 20) + masked(q1.z, d + 24) + masked(q1.w, d + 28);
+      s += (uint64_t)masked(q2.x, d + 32) + masked(q2.y, d + 36) + masked(q2.z, d + 40) + masked(q2.w, d + 44);
+      s += (uint64_t)masked(q3.x, d + 48) + masked(q3.y, d + 52) + masked(q3.z, d + 56) + masked(q3.w, d + 60);
+      d += 64;
+    } else if ((d & 15) == 0 && d + 16 <= d1) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(gbase + d);
+      s += (uint64_t)masked(q.x, d) + masked(q.y, d + 4) + masked(q.z, d + 8) + masked(q.w, d + 12);
+      d += 16;
+    } else {
+      s += masked(*reinterpret_cast<const uint32_t *>(gbase + d), d);
+      d += 4;
     }
-    if (d < wa) w &= 0xffffffffu << (8 * (wa - d));
-    if (d + 4 > we) w &= 0xffffffffu >> (8 * (d + 4 - we));
-    s += w;
   }
   uint32_t le = fold(s);  // sum of little-endian words at even absolute offsets
   return (wa & 1) ? le : bswap16(le);
