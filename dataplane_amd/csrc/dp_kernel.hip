@@ -1383,9 +1383,21 @@ __device__ __forceinline__ uint32_t sum_frame(const Frame &F, int a, int e) {
     if (F.inwin || d + 4 <= WIN) {
       s += masked(*reinterpret_cast<const lds_u32 *>(F.lds + d), d);
       d += 4;
-    } else if ((d & 15) == 0 && d + 64 <= d1) {
-      // beyond the window: 64 bytes per round trip (four 16-byte loads
+    } else if ((d & 15) == 0 && d + 128 <= d1) {
+      // beyond the window: 128 bytes per round trip (eight 16-byte loads
       // issued together), not one load waited on per iteration
+      const uint4 *q = reinterpret_cast<const uint4 *>(gbase + d);
+      const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6], q7 = q[7];
+      s += (uint64_t)masked(q0.x, d) + masked(q0.y, d + 4) + masked(q0.z, d + 8) + masked(q0.w, d + 12);
+      s += (uint64_t)masked(q1.x, d + 16) + masked(q1.y, d + 20) + masked(q1.z, d + 24) + masked(q1.w, d + 28);
+      s += (uint64_t)masked(q2.x, d + 32) + masked(q2.y, d + 36) + masked(q2.z, d + 40) + masked(q2.w, d + 44);
+      s += (uint64_t)masked(q3.x, d + 48) + masked(q3.y, d + 52) + masked(q3.z, d + 56) + masked(q3.w, d + 60);
+      s += (uint64_t)masked(q4.x, d + 64) + masked(q4.y, d + 68) + masked(q4.z, d + 72) + masked(q4.w, d + 76);
+      s += (uint64_t)masked(q5.x, d + 80) + masked(q5.y, d + 84) + masked(q5.z, d + 88) + masked(q5.w, d + 92);
+      s += (uint64_t)masked(q6.x, d + 96) + masked(q6.y, d + 100) + masked(q6.z, d + 104) + masked(q6.w, d + 108);
+      s += (uint64_t)masked(q7.x, d + 112) + masked(q7.y, d + 116) + masked(q7.z, d + 120) + masked(q7.w, d + 124);
+      d += 128;
+    } else if ((d & 15) == 0 && d + 64 <= d1) {
       const uint4 *q = reinterpret_cast<const uint4 *>(gbase + d);
       const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
       s += (uint64_t)masked(q0.x, d) + masked(q0.y, d + 4) + masked(q0.z, d + 8) + masked(q0.w, d + 12);
