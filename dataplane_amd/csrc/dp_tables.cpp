@@ -327,8 +327,14 @@ void build_field_index(ImgBuf &ib, FieldIdx &F, int f, int fam, size_t ngroups,
 // Candidate-list limits: a group takes the list form when, for its best
 // field, no interval has more than kListMax candidates and the mean list
 // (over intervals) is at most kListMean; otherwise the bit-vector form.
-constexpr uint32_t kListMax = 24;
-constexpr double kListMean = 6.0;
+#ifndef DP_LIST_MAX
+#define DP_LIST_MAX 24
+#endif
+#ifndef DP_LIST_MEAN
+#define DP_LIST_MEAN 6.0
+#endif
+constexpr uint32_t kListMax = DP_LIST_MAX;
+constexpr double kListMean = DP_LIST_MEAN;
 
 // Classifier form override for the parity tests (dpd_debug_set_classifier_form):
 // 1 forces the bit-vector form, 2 takes the list form whenever the runs fit
