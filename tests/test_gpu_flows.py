@@ -82,18 +82,22 @@ def _ref_map(a, b):
     return {x: y for x, y in zip(a, b) if x != A.FLOW_NONE}
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_gpu_flows_random_bursts(nf, seed):
-    """Seeded scenarios (tests/flowgen.py) over a C2-shaped workload: two
-    bursts in a row, then the flow timers; outputs, serialized bytes, flow
-    refs and every flow's state equal the oracle's."""
-    w = Workload(2, 6000, seed=seed, n_routes_v4=3000, n_acl=400, n_nat=24, tcp_percent=30)
+@pytest.mark.parametrize("cfg,seed", [(2, 1), (2, 2), (5, 3)])
+def test_gpu_flows_random_bursts(nf, cfg, seed):
+    """Seeded scenarios (tests/flowgen.py) over a C2-shaped workload, and a
+    C5-shaped one (v4 / v6 mix: v6 flow keys, v6 ACL reply path): two bursts
+    in a row, then the flow timers; outputs, serialized bytes, flow refs and
+    every flow's state equal the oracle's."""
+    w = Workload(cfg, 6000, seed=seed, n_routes_v4=3000, n_routes_v6=2000 if cfg == 5 else 0,
+                 n_acl=400, n_nat=24, tcp_percent=30)
     ora = Oracle(w.tables)
     frames = frames_of(w)
     ob = w.fresh_buf()
     o0 = ora.process(ob, w.inp, A.PKT_OUT)
     items, burst = scenario(frames, o0["dst_vni"], genid=1, seed=seed, n_flows=600,
                             vnis=sorted(set(int(v) for v in o0["dst_vni"] if v)))
+    if cfg == 5:
+        assert sum(int(it[1]["key"]["family"]) == 6 for it in items) > 50
     oft, gft = OracleFlows(), FlowTable(0, 1 << 13)
     orefs, grefs = install(oft, items), install(gft, items)
     g2o = _ref_map(grefs, orefs)
@@ -105,7 +109,7 @@ def test_gpu_flows_random_bursts(nf, seed):
             obuf, gbuf = buf.copy(), buf.copy()
             oout, oref, ost = ora.process_flows(obuf, inp, A.PKT_OUT, oft, stats=True)
             gout, gref, gst = run_device(nf, gbuf, inp, stats=True)
-            compare(oout, obuf, gout, gbuf, inp, f"flows seed {seed} burst {rnd}")
+            compare(oout, obuf, gout, gbuf, inp, f"flows C{cfg} seed {seed} burst {rnd}")
             mapped = np.array([g2o.get(int(r), A.FLOW_NONE) if int(r) != A.FLOW_NONE else A.FLOW_NONE
                                for r in gref], dtype=np.uint64)
             assert np.array_equal(mapped, oref), f"flow refs differ ({np.count_nonzero(mapped != oref)})"
