@@ -177,3 +177,32 @@ def test_gpu_flows_full_size(nf):
     gi, oi = gft.get(gref), oft.get(oref)
     assert np.array_equal(gi["status"], oi["status"])
     assert gft.count() == oft.count()
+
+
+def test_gpu_flows_host_origin(nf):
+    """With a flow table attached, the host-origin entry (dp_process_burst:
+    the burst is one launch, never chunked, since flow-filter invalidations
+    must reach every later packet of the burst) matches the oracle on a burst
+    larger than the host path's chunk; the sharded entry refuses flow tables."""
+    from dataplane_amd.flows import burst_request_flows
+    w = Workload(2, 150_000, seed=11, n_routes_v4=5000, n_acl=500, n_nat=24, tcp_percent=30)
+    ora = Oracle(w.tables)
+    nf.publish(w.tables)
+    o0 = nf.process_arrays(w.fresh_buf(), w.inp)
+    fl = burst_request_flows(w.buf, w.inp, np.arange(0, w.n, 3), o0["dst_vni"], genid=1)
+    fl["genid"][::7] = 0
+    oft, gft = OracleFlows(), FlowTable(0, 1 << 18)
+    oref, _ = oft.insert(fl)
+    gref, _ = gft.insert(fl)
+    nf.attach_flows(gft)
+    try:
+        obuf, hbuf = w.fresh_buf(), w.fresh_buf()
+        oout, _ = ora.process_flows(obuf, w.inp, A.PKT_OUT, oft)
+        hout = nf.process_arrays(hbuf, w.inp)
+        with pytest.raises(RuntimeError):
+            GpuPathNf.process_sharded([nf], w.fresh_buf(), w.inp)
+    finally:
+        nf.attach_flows(None)
+    compare(oout, obuf, hout, hbuf, w.inp, "flows host-origin")
+    assert np.array_equal(gft.get(gref)["status"], oft.get(oref)["status"])
+    assert gft.count() == oft.count()
