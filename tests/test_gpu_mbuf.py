@@ -66,3 +66,56 @@ def test_gpu_mbuf_pool_must_be_mapped(nf):
     nf.publish(w.tables)
     with pytest.raises(RuntimeError):
         nf.process_mbufs(pool.base, pool.mem.nbytes, mbufs)
+
+
+def test_gpu_mbuf_burst_with_flows(nf):
+    """C4 through the DPDK glue with a flow table attached: FlowLookup runs on
+    the decapsulated overlay packets (flows keyed by the inner 5-tuple and the
+    VXLAN VNI, half of them from a stale generation, a quarter towards an
+    unknown VPC); outputs, frames and flow states equal the oracle's."""
+    from dataplane_amd.flows import FlowTable, make_flow
+    from oracle.pyoracle import OracleFlows
+    from flowgen import frame_key
+    w = Workload(4, 3000, seed=8, n_routes_v4=2000, n_acl=200, n_nat=16)
+    frames = [f for f, _ in frames_of(w)]
+    ports = w.inp["iif"]
+    buf, inp = pack_burst([(f, int(p), 0, 0) for f, p in zip(frames, ports)])
+    ora = Oracle(w.tables)
+    o0 = ora.process(buf.copy(), inp, A.PKT_OUT)
+    genid = int(w.tables.contents.genid)
+    vnis = sorted(set(int(v) for v in o0["dst_vni"] if v))
+    fls, seen = [], set()
+    for i in range(0, len(frames), 2):
+        f = frames[i]
+        if len(f) < 84 or f[12:14] != b"\x08\x00" or f[23] != 17 or f[36:38] != b"\x12\xb5":
+            continue
+        k = frame_key(f[50:], int.from_bytes(f[46:49], "big"))
+        if k is None or not o0[i]["dst_vni"] or k.tobytes() in seen:
+            continue
+        seen.add(k.tobytes())
+        d = int(o0[i]["dst_vni"])
+        if len(fls) % 4 == 2:            # a flow towards a VPC the tables do not know
+            d = max(vnis) + 17
+        fls.append(make_flow(k, d, A.FLOW_INITIATOR, genid=genid - (len(fls) & 1)))
+    assert len(fls) > 300
+    fl = np.array(fls, dtype=A.FLOW)
+    oft, gft = OracleFlows(), FlowTable(0, 1 << 13)
+    oref, _ = oft.insert(fl)
+    gref, _ = gft.insert(fl)
+    oout, _ = ora.process_flows(buf, inp, A.PKT_OUT, oft)
+    pool = FakeMempool(pinned(FakeMempool.bytes_for(len(frames) + 1)))
+    mbufs = pool.load(frames, ports)
+    nf.publish(w.tables)
+    nf.attach_flows(gft)
+    try:
+        out = nf.process_mbufs(pool.base, pool.mem.nbytes, mbufs)
+    finally:
+        nf.attach_flows(None)
+    for k in ("done", "acl", "meta_flags", "oif", "dst_vni", "src_vni", "fib_entry", "acl_rule"):
+        bad = np.nonzero(out[k] != oout[k])[0]
+        assert len(bad) == 0, f"{k} differs at {bad[:5]}"
+    for i in np.nonzero(oout["done"] == A.DONE["Delivered"])[0]:
+        o, ln = int(oout[i]["off"]), int(oout[i]["len"])
+        assert pool.frame(int(i)) == buf[o:o + ln].tobytes(), f"packet {i} frame"
+    assert np.array_equal(gft.get(gref)["status"], oft.get(oref)["status"])
+    assert gft.count() == oft.count()
