@@ -57,7 +57,11 @@ struct FlowCtx {
   FlowSlot *slots;
   uint32_t mask;        // slots - 1
   uint32_t n;           // packets of the burst
-  // invalidation events: [0] count, then the invalidated flows' slots (<= 2 per packet)
+  uint32_t max_probe;   // probe bound (dp_flow_table::max_probe)
+  uint32_t pad;
+  // invalidation events: [0] count, then (slot, state word) of each
+  // invalidated flow (<= 2 per packet); the state word is the fill the event
+  // is about, so an event never touches a later fill of the slot
   uint32_t *events;
   // ACL decisions that rest on a flow's validity (acl = 6): [0] count, then
   // SensRec records

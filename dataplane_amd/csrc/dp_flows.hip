@@ -27,9 +27,12 @@ namespace {
 
 constexpr uint32_t kTB = 256;
 
-__device__ __forceinline__ uint32_t probe(const FlowSlot *slots, uint32_t mask, const FKey &k, uint32_t &state) {
+// FlowTable::lookup by key: linear probing from the key's home slot, at most
+// max_probe + 1 slots (no stored flow sits further from its home)
+__device__ __forceinline__ uint32_t probe(const FlowSlot *slots, uint32_t mask, uint32_t max_probe, const FKey &k,
+                                          uint32_t &state) {
   uint32_t i = dpf::fkey_hash(k) & mask;
-  for (uint32_t p = 0; p <= mask; p++) {
+  for (uint32_t p = 0; p <= max_probe; p++) {
     const FlowSlot &s = slots[i];
     const uint32_t st = __hip_atomic_load(&s.state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     if ((st & 3u) == dpf::FS_EMPTY) return dpf::kNoSlot;
@@ -63,12 +66,12 @@ __device__ void fill_info(const FlowSlot *slots, uint32_t mask, uint32_t sl, dp_
     o.related = dpf::make_ref(s.related, s.related_tag);
 }
 
-__global__ void __launch_bounds__(kTB) fl_find_k(const FlowSlot *slots, uint32_t mask, const FKey *keys, uint32_t n,
-                                                uint32_t *slot_out) {
+__global__ void __launch_bounds__(kTB) fl_find_k(const FlowSlot *slots, uint32_t mask, uint32_t max_probe,
+                                                const FKey *keys, uint32_t n, uint32_t *slot_out) {
   const uint32_t i = blockIdx.x * kTB + threadIdx.x;
   if (i >= n) return;
   uint32_t st;
-  slot_out[i] = probe(slots, mask, keys[i], st);
+  slot_out[i] = probe(slots, mask, max_probe, keys[i], st);
 }
 
 struct InsRec {
@@ -81,9 +84,10 @@ struct InsRec {
 
 // Fill one slot per record: the replaced flow's slot, or the first EMPTY /
 // TOMB slot of the key's probe sequence (claimed by CAS).  The new FlowInfo
-// is Active (table.rs:235-240), with no related flow yet.
+// is Active (table.rs:235-240), with no related flow yet.  A new slot's
+// displacement from the key's home raises the table's probe bound (*meta).
 __global__ void __launch_bounds__(kTB) fl_insert_k(FlowSlot *slots, uint32_t mask, const InsRec *recs, uint32_t n,
-                                                  uint64_t *refs) {
+                                                  uint64_t *refs, uint32_t *meta) {
   const uint32_t i = blockIdx.x * kTB + threadIdx.x;
   if (i >= n) return;
   const InsRec r = recs[i];
@@ -99,6 +103,7 @@ __global__ void __launch_bounds__(kTB) fl_insert_k(FlowSlot *slots, uint32_t mas
       if ((st == dpf::FS_EMPTY || st == dpf::FS_TOMB) &&
           atomicCAS(&slots[p].state, old, (old & ~3u) | dpf::FS_BUSY) == old) {
         sl = p;
+        atomicMax(meta, (p - (dpf::fkey_hash(r.k) & mask)) & mask);
         break;
       }
       if (st == dpf::FS_FULL || st == dpf::FS_BUSY) p = (p + 1) & mask;
@@ -132,12 +137,12 @@ __global__ void fl_link_k(FlowSlot *slots, uint32_t mask, uint64_t a, uint64_t b
   slots[sb].related_tag = slots[sa].state;
 }
 
-__global__ void __launch_bounds__(kTB) fl_lookup_k(const FlowSlot *slots, uint32_t mask, const FKey *keys, uint32_t n,
-                                                  dp_flow_info_t *out) {
+__global__ void __launch_bounds__(kTB) fl_lookup_k(const FlowSlot *slots, uint32_t mask, uint32_t max_probe,
+                                                  const FKey *keys, uint32_t n, dp_flow_info_t *out) {
   const uint32_t i = blockIdx.x * kTB + threadIdx.x;
   if (i >= n) return;
   uint32_t st;
-  const uint32_t sl = probe(slots, mask, keys[i], st);
+  const uint32_t sl = probe(slots, mask, max_probe, keys[i], st);
   dp_flow_info_t o{};
   o.ref = DP_FLOW_NONE;
   o.related = DP_FLOW_NONE;
@@ -157,15 +162,27 @@ __global__ void __launch_bounds__(kTB) fl_get_k(const FlowSlot *slots, uint32_t 
 }
 
 // FlowTable::remove (table.rs:282-295): Detached, out of the table
-__global__ void __launch_bounds__(kTB) fl_remove_k(FlowSlot *slots, uint32_t mask, const FKey *keys, uint32_t n,
-                                                  uint32_t *count) {
+__global__ void __launch_bounds__(kTB) fl_remove_k(FlowSlot *slots, uint32_t mask, uint32_t max_probe,
+                                                  const FKey *keys, uint32_t n, uint32_t *count) {
   const uint32_t i = blockIdx.x * kTB + threadIdx.x;
   if (i >= n) return;
   uint32_t st;
-  const uint32_t sl = probe(slots, mask, keys[i], st);
+  const uint32_t sl = probe(slots, mask, max_probe, keys[i], st);
   if (sl == dpf::kNoSlot) return;
   slots[sl].status = DP_FLOW_DETACHED;
-  if (atomicCAS(&slots[sl].state, st, (st & ~3u) | dpf::FS_TOMB) == st) atomicAdd(count, 1u);
+  if (atomicCAS(&slots[sl].state, st, (st & ~3u) | dpf::FS_TOMB) != st) return;
+  atomicAdd(count, 1u);
+  // the new tombstone ends a cluster: it and the tombstones before it
+  // become EMPTY (as fl_reclaim_k; a missed reclaim only costs probe length)
+  if ((__hip_atomic_load(&slots[(sl + 1) & mask].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) & 3u) !=
+      dpf::FS_EMPTY)
+    return;
+  uint32_t j = sl;
+  for (uint32_t k = 0; k < mask; k++, j = (j - 1) & mask) {
+    const uint32_t o = __hip_atomic_load(&slots[j].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if ((o & 3u) != dpf::FS_TOMB) break;
+    atomicCAS(&slots[j].state, o, (o & ~3u) | dpf::FS_EMPTY);
+  }
 }
 
 // FlowInfo::invalidate_pair (flow_info.rs:449-455)
@@ -199,6 +216,41 @@ __global__ void __launch_bounds__(kTB) fl_sweep_k(FlowSlot *slots, uint64_t nslo
     }
     if (gone && atomicCAS(&s.state, st, (st & ~3u) | dpf::FS_TOMB) == st) atomicAdd(count, 1ull);
   }
+}
+
+// Tombstone reclamation after removals: a run of TOMB slots that ends at an
+// EMPTY slot becomes EMPTY (a probe passing through the run would stop at
+// that EMPTY slot anyway, so every lookup's outcome is unchanged).  Each
+// EMPTY slot's thread walks back over its own run; runs are disjoint.  Stored
+// flows never move, so refs and related links stay valid; the fill tag is
+// kept, so the next fill of a reclaimed slot still gets a new tag.
+__global__ void __launch_bounds__(kTB) fl_reclaim_k(FlowSlot *slots, uint64_t nslots, unsigned long long *count) {
+  const uint32_t mask = (uint32_t)(nslots - 1);
+  for (uint64_t i = blockIdx.x * (uint64_t)kTB + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * kTB) {
+    if ((slots[i].state & 3u) != dpf::FS_EMPTY) continue;
+    uint32_t j = ((uint32_t)i - 1) & mask;
+    unsigned long long c = 0;
+    for (uint32_t k = 0; k < mask && j != (uint32_t)i; k++, j = (j - 1) & mask) {
+      const uint32_t st = slots[j].state;
+      if ((st & 3u) != dpf::FS_TOMB) break;
+      slots[j].state = (st & ~3u) | dpf::FS_EMPTY;
+      c++;
+    }
+    if (c) atomicAdd(count, c);
+  }
+}
+
+// Slot census for dpf_debug_table_stats: FULL, TOMB, EMPTY
+__global__ void __launch_bounds__(kTB) fl_census_k(const FlowSlot *slots, uint64_t nslots, unsigned long long *out) {
+  unsigned long long c[3] = {0, 0, 0};
+  for (uint64_t i = blockIdx.x * (uint64_t)kTB + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * kTB) {
+    const uint32_t st = slots[i].state & 3u;
+    c[0] += st == dpf::FS_FULL;
+    c[1] += st == dpf::FS_TOMB;
+    c[2] += st == dpf::FS_EMPTY;
+  }
+  for (int k = 0; k < 3; k++)
+    if (c[k]) atomicAdd(&out[k], c[k]);
 }
 
 __global__ void __launch_bounds__(kTB) fl_count_k(const FlowSlot *slots, uint64_t nslots, unsigned long long *out) {
@@ -256,6 +308,8 @@ int run(dp_flow_table *ft, const char *what, F f) {
   int prev = 0;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(ft->device);
+  // after every flows burst launched before this call (dp_flows_rt.h)
+  if (ft->burst_armed) (void)hipStreamWaitEvent(ft->stream, ft->last_burst, 0);
   int rc = f(ft->stream);
   hipError_t e = hipStreamSynchronize(ft->stream);
   if (!rc && e != hipSuccess) rc = dpr_fail(DP_EIO, what, e);
@@ -288,7 +342,8 @@ int insert_batch(dp_flow_table *ft, const dp_flow_t *flows, uint32_t n, const in
     FKey *dk = upload(s_keys, keys.data(), n, st);
     uint32_t *ds = static_cast<uint32_t *>(s_slots.get(sizeof(uint32_t) * n));
     if (!dk || !ds) return dpr_fail(DP_ENOMEM, "flow scratch");
-    hipLaunchKernelGGL(fl_find_k, dim3(blocks_for(n)), dim3(kTB), 0, st, ft->slots, ft->mask, dk, n, ds);
+    hipLaunchKernelGGL(fl_find_k, dim3(blocks_for(n)), dim3(kTB), 0, st, ft->slots, ft->mask, ft->max_probe, dk, n,
+                       ds);
     if (hipMemcpyAsync(found.data(), ds, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st) != hipSuccess)
       return dpr_fail(DP_EIO, "flow probe copy");
     return 0;
@@ -320,20 +375,29 @@ int insert_batch(dp_flow_table *ft, const dp_flow_t *flows, uint32_t n, const in
     which.push_back(i);
   }
   std::vector<uint64_t> got(recs.size());
+  uint32_t maxp = ft->max_probe;
   if (!recs.empty()) {
     rc = run(ft, "flow insert", [&](hipStream_t st) {
       InsRec *dr = upload(s_recs, recs.data(), recs.size(), st);
       uint64_t *df = static_cast<uint64_t *>(s_refs.get(sizeof(uint64_t) * recs.size()));
       if (!dr || !df) return dpr_fail(DP_ENOMEM, "flow scratch");
       hipLaunchKernelGGL(fl_insert_k, dim3(blocks_for(recs.size())), dim3(kTB), 0, st, ft->slots, ft->mask, dr,
-                         (uint32_t)recs.size(), df);
-      if (hipMemcpyAsync(got.data(), df, sizeof(uint64_t) * recs.size(), hipMemcpyDeviceToHost, st) != hipSuccess)
+                         (uint32_t)recs.size(), df, ft->d_meta);
+      if (hipMemcpyAsync(got.data(), df, sizeof(uint64_t) * recs.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipMemcpyAsync(&maxp, ft->d_meta, sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess)
         return dpr_fail(DP_EIO, "flow insert copy");
       return 0;
     });
     if (rc) return rc;
   }
-  ft->len = len;
+  // the probe bound covers every slot filled, whatever happens below
+  ft->max_probe = maxp;
+  // a flow that found no slot was never stored: the count takes only the
+  // stored ones, then the whole batch reports the failure
+  uint64_t lost = 0;
+  for (size_t j = 0; j < recs.size(); j++)
+    if (got[j] == ~0ull && recs[j].slot == dpf::kNoSlot) lost++;
+  ft->len = len - lost;
   for (uint32_t i = 0; i < n; i++) {
     if (refs) refs[i] = DP_FLOW_NONE;
     if (results) results[i] = res[i];
@@ -365,12 +429,17 @@ int dp_flow_table_create(int device_ordinal, uint64_t slots, dp_flow_table_t **o
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(device_ordinal);
   e = hipStreamCreateWithFlags(&ft->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ft->last_burst, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(&ft->slots, slots * sizeof(FlowSlot));
+  if (e == hipSuccess) e = hipMalloc(&ft->d_meta, sizeof(uint32_t) * 4);
+  if (e == hipSuccess) e = hipMemset(ft->d_meta, 0, sizeof(uint32_t) * 4);
   // every slot EMPTY with tag 0; marks idle
   if (e == hipSuccess) e = hipMemset(ft->slots, 0, slots * sizeof(FlowSlot));
   (void)hipSetDevice(prev);
   if (e != hipSuccess) {
     if (ft->slots) (void)hipFree(ft->slots);
+    if (ft->d_meta) (void)hipFree(ft->d_meta);
+    if (ft->last_burst) (void)hipEventDestroy(ft->last_burst);
     if (ft->stream) (void)hipStreamDestroy(ft->stream);
     delete ft;
     return dpr_fail(DP_ENOMEM, "flow table allocation", e);
@@ -382,11 +451,36 @@ int dp_flow_table_create(int device_ordinal, uint64_t slots, dp_flow_table_t **o
 int dp_flow_table_destroy(dp_flow_table_t *ft) {
   if (!ft) return DP_EINVAL;
   (void)hipSetDevice(ft->device);
+  if (ft->burst_armed) (void)hipEventSynchronize(ft->last_burst);
   (void)hipStreamSynchronize(ft->stream);
   (void)hipFree(ft->slots);
+  (void)hipFree(ft->d_meta);
   for (auto &x : ft->scr) x.release();
+  (void)hipEventDestroy(ft->last_burst);
   (void)hipStreamDestroy(ft->stream);
   delete ft;
+  return 0;
+}
+
+// Test hook (not part of dpgpu.h): out[0..3] = FULL, TOMB and EMPTY slots,
+// and the table's probe bound (max_probe).
+int dpf_debug_table_stats(dp_flow_table_t *ft, uint64_t *out) {
+  if (!ft || !out) return dpr_fail(DP_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(ft->mu);
+  Scratch &sc = ft->scr[0];
+  unsigned long long c[3] = {0, 0, 0};
+  int rc = run(ft, "flow census", [&](hipStream_t st) {
+    unsigned long long *dc = static_cast<unsigned long long *>(sc.get(sizeof(c)));
+    if (!dc) return dpr_fail(DP_ENOMEM, "flow scratch");
+    if (hipMemsetAsync(dc, 0, sizeof(c), st) != hipSuccess) return dpr_fail(DP_EIO, "memset");
+    const uint32_t b = blocks_for(ft->nslots) < 4096 ? blocks_for(ft->nslots) : 4096;
+    hipLaunchKernelGGL(fl_census_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, dc);
+    if (hipMemcpyAsync(c, dc, sizeof(c), hipMemcpyDeviceToHost, st) != hipSuccess)
+      return dpr_fail(DP_EIO, "flow census copy");
+    return 0;
+  });
+  if (rc) return rc;
+  out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = ft->max_probe;
   return 0;
 }
 
@@ -457,7 +551,8 @@ int dp_flow_lookup(dp_flow_table_t *ft, const dp_flow_key_t *keys, uint32_t n, d
     FKey *dk = upload(sk, k.data(), n, st);
     dp_flow_info_t *d = static_cast<dp_flow_info_t *>(so.get(sizeof(dp_flow_info_t) * n));
     if (!dk || !d) return dpr_fail(DP_ENOMEM, "flow scratch");
-    hipLaunchKernelGGL(fl_lookup_k, dim3(blocks_for(n)), dim3(kTB), 0, st, ft->slots, ft->mask, dk, n, d);
+    hipLaunchKernelGGL(fl_lookup_k, dim3(blocks_for(n)), dim3(kTB), 0, st, ft->slots, ft->mask, ft->max_probe, dk,
+                       n, d);
     if (hipMemcpyAsync(out, d, sizeof(dp_flow_info_t) * n, hipMemcpyDeviceToHost, st) != hipSuccess)
       return dpr_fail(DP_EIO, "flow lookup copy");
     return 0;
@@ -492,7 +587,9 @@ int dp_flow_remove(dp_flow_table_t *ft, const dp_flow_key_t *keys, uint32_t n, u
     uint32_t *dc = static_cast<uint32_t *>(sc.get(sizeof(uint32_t)));
     if (!dk || !dc) return dpr_fail(DP_ENOMEM, "flow scratch");
     if (hipMemsetAsync(dc, 0, sizeof(uint32_t), st) != hipSuccess) return dpr_fail(DP_EIO, "memset");
-    if (n) hipLaunchKernelGGL(fl_remove_k, dim3(blocks_for(n)), dim3(kTB), 0, st, ft->slots, ft->mask, dk, n, dc);
+    if (n)
+      hipLaunchKernelGGL(fl_remove_k, dim3(blocks_for(n)), dim3(kTB), 0, st, ft->slots, ft->mask, ft->max_probe,
+                         dk, n, dc);
     if (hipMemcpyAsync(&cnt, dc, sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess)
       return dpr_fail(DP_EIO, "flow remove copy");
     return 0;
@@ -539,13 +636,15 @@ int dp_flow_sweep(dp_flow_table_t *ft, uint64_t now, uint64_t *n_removed) {
   Scratch &sc = ft->scr[0];
   unsigned long long cnt = 0;
   int rc = run(ft, "flow sweep", [&](hipStream_t st) {
-    unsigned long long *dc = static_cast<unsigned long long *>(sc.get(sizeof(cnt)));
+    unsigned long long *dc = static_cast<unsigned long long *>(sc.get(2 * sizeof(cnt)));
     if (!dc) return dpr_fail(DP_ENOMEM, "flow scratch");
-    if (hipMemsetAsync(dc, 0, sizeof(cnt), st) != hipSuccess) return dpr_fail(DP_EIO, "memset");
+    if (hipMemsetAsync(dc, 0, 2 * sizeof(cnt), st) != hipSuccess) return dpr_fail(DP_EIO, "memset");
     const uint32_t b = blocks_for(ft->nslots) < 4096 ? blocks_for(ft->nslots) : 4096;
     hipLaunchKernelGGL(fl_sweep_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, now, dc);
     if (hipMemcpyAsync(&cnt, dc, sizeof(cnt), hipMemcpyDeviceToHost, st) != hipSuccess)
       return dpr_fail(DP_EIO, "flow sweep copy");
+    // the tombstones the timers left, wherever they end a cluster
+    hipLaunchKernelGGL(fl_reclaim_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, dc + 1);
     return 0;
   });
   if (rc) return rc;

@@ -39,8 +39,20 @@ struct dp_flow_table {
   uint32_t mask = 0;
   uint64_t capacity = 0;           // FlowTable::set_capacity
   uint64_t len = 0;                // FULL slots (FlowTable::len)
+  uint32_t max_probe = 0;          // largest displacement of any flow ever stored: a lookup
+                                   // probes at most max_probe + 1 slots, however many
+                                   // tombstones removals have left
+  uint32_t *d_meta = nullptr;      // device word: the inserts' atomicMax of their displacement
   hipStream_t stream = nullptr;    // management kernels
-  std::mutex mu;                   // one management call at a time
+  // One order for everything that touches the table: management calls and the
+  // flows bursts of every attached context.  A management call holds `mu` for
+  // its whole (synchronous) run and first waits for `last_burst`; a flows
+  // launch takes `mu`, waits for `last_burst` too (bursts of contexts sharing
+  // the table never overlap: their burst-local invalidation marks live in the
+  // shared slots) and records `last_burst` after its kernels.
+  std::mutex mu;
+  hipEvent_t last_burst = nullptr;
+  bool burst_armed = false;
   FlowScratch scr[4];              // management-call buffers
 };
 

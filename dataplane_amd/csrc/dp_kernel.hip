@@ -91,8 +91,10 @@ constexpr int WIN = DP_WIN;       // header window bytes per packet (rest read f
 constexpr int SLAB = WIN + 4;     // odd dword stride: conflict-free byte reads
 constexpr int HS = DP_HS;         // hash input scratch (packet_hash_* input <= 59 B)
 constexpr uint8_t DONE_NONE = 255;
-// out-of-line cold paths (the emulator inlines freely)
-#ifdef DP_EMU
+// out-of-line cold paths (the emulator inlines freely, except its
+// DP_EMU_OUTLINE build, which keeps every function out of line so the CPU
+// suite runs the call shape of the device code: tests/emu libdpemu_outline.so)
+#if defined(DP_EMU) && !defined(DP_EMU_OUTLINE)
 #define DP_COLD
 #else
 #define DP_COLD __attribute__((noinline))
@@ -101,12 +103,15 @@ constexpr uint8_t DONE_NONE = 255;
 // ---------------------------------------------------------------------------
 // Image access
 // ---------------------------------------------------------------------------
-struct Img {
+struct ImgBase {
   const uint8_t *base;
-  const Image &im;  // in HBM on the device (read where used), host memory in the emulator
   template <class T> __device__ __forceinline__ const T *at(uint64_t off) const {
     return reinterpret_cast<const T *>(base + off);
   }
+};
+struct Img : ImgBase {
+  const Image &im;  // in HBM on the device (read where used), host memory in the emulator
+  __device__ __forceinline__ Img(const uint8_t *b, const Image &i) : ImgBase{b}, im(i) {}
 };
 
 __device__ __forceinline__ bool hash_find(const Img &g, const HashMap &m, uint32_t k0,
@@ -964,9 +969,12 @@ __device__ __forceinline__ bool pfx_ok(Key128 k, uint64_t ahi, uint64_t alo, uin
 
 // Bit-vector group: global rule index of the first match, or -1.  Kept out
 // of line: its lockstep state is large and the candidate-list form is the
-// common one.
-__device__ DP_COLD int64_t classify_bv(const Img &g, const Group *Gp, uint8_t proto, Key128 src,
+// common one.  Every argument is a value or a pointer into the table image
+// (global memory): nothing of the caller's private frame or LDS crosses the
+// call (DESIGN.md "Out-of-line device functions").
+__device__ DP_COLD int64_t classify_bv(const uint8_t *base, const Group *Gp, uint8_t proto, Key128 src,
                                        Key128 dst, uint16_t sp, uint16_t dp) {
+  const ImgBase g{base};
   const Group G = *Gp;
   Key128 key[4] = {src, dst, Key128{0, sp}, Key128{0, dp}};
   uint32_t lo[4], hi[4], e[4];
@@ -1154,7 +1162,7 @@ __device__ __forceinline__ Hit classify(const Img &g, const ClsArrays &A, int32_
     GTRIP(12);
     return verify_run(g, A.recs, field_leaf(g, F, k), v6, proto, src, dst, sp, dp, (WANT & W_ORIG) != 0);
   }
-  const int64_t ri = classify_bv(g, Gp, proto, src, dst, sp, dp);
+  const int64_t ri = classify_bv(g.base, Gp, proto, src, dst, sp, dp);
   if (ri < 0) return h;
   h.rule = ri;
   if (WANT & W_ACTION) h.action = g.at<uint32_t>(A.action)[ri];
@@ -1508,7 +1516,7 @@ __device__ __forceinline__ uint32_t flow_probe(const dpf::FlowCtx &fc, const dpf
                                                uint4 &v, uint4 &w) {
   uint32_t i = dpf::fkey_hash(k) & fc.mask;
 #pragma unroll 1
-  for (uint32_t p = 0; p <= fc.mask; p++) {
+  for (uint32_t p = 0; p <= fc.max_probe; p++) {
     const dpf::FlowSlot *s = fc.slots + i;
     const uint4 a = ld4(&s->state), b = ld4(&s->src[0]), c = ld4(&s->dst[0]);
     v = ld4(&s->status);
@@ -2669,8 +2677,17 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(&fc.events[0], (uint32_t)(__popcll(m0) + __popcll(m1)));
     base = (uint32_t)__shfl((int)base, leader);
-    if (e0) fc.events[1 + base + __popcll(m0 & lanes_below(lane))] = fp.ev0;
-    if (e1) fc.events[1 + base + __popcll(m0) + __popcll(m1 & lanes_below(lane))] = fp.ev1;
+    // (slot, state word) pairs: the fill of the packet's flow (ev0 / ev1 are fp.slot)
+    if (e0) {
+      const uint32_t k = base + __popcll(m0 & lanes_below(lane));
+      fc.events[1 + 2 * k] = fp.ev0;
+      fc.events[2 + 2 * k] = fp.state;
+    }
+    if (e1) {
+      const uint32_t k = base + __popcll(m0) + __popcll(m1 & lanes_below(lane));
+      fc.events[1 + 2 * k] = fp.ev1;
+      fc.events[2 + 2 * k] = fp.state;
+    }
   }
   const bool sv = has && fp.sens;
   const uint64_t ms = __ballot(sv);
@@ -2785,8 +2802,12 @@ __global__ void __launch_bounds__(256) dp_flow_fixup(dpf::FlowCtx fc, const dp_p
 __global__ void __launch_bounds__(256) dp_flow_apply(dpf::FlowCtx fc) {
   const uint32_t cnt = fc.events[0];
   for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < cnt; r += gridDim.x * 256) {
-    const uint32_t c = fc.events[1 + r];
+    const uint32_t c = fc.events[1 + 2 * r], tag = fc.events[2 + 2 * r];
     dpf::FlowSlot &s = fc.slots[c];
+    // the fill the event is about (a slot is never refilled while a burst
+    // runs -- dp_flow_table's order -- but an event must not be able to
+    // cancel an unrelated later flow)
+    if (s.state != tag) continue;
     s.status = DP_FLOW_CANCELLED;
     s.mark = dpf::kIdleMark;
     const uint32_t rel = s.related;

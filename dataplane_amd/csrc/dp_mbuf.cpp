@@ -49,8 +49,11 @@ int dp_mbuf_burst_in(const void *pool_base, uint64_t pool_bytes, void *const *mb
     const uint16_t port = rd<uint16_t>(m, layout->port);
     const uintptr_t frame = buf + doff;
     // the headroom in front of the frame belongs to the packet (DP_HEADROOM
-    // contract): it must lie in the pool region, as must the frame
-    if (buf < base || doff < DP_HEADROOM || frame + dlen > base + pool_bytes || frame - base > UINT32_MAX) {
+    // contract): it must lie in the pool region, as must the frame rounded
+    // up to 16 bytes (the kernel stages frames with 16-byte loads): a frame
+    // at the very end of the pool fails alone, not the whole burst
+    if (buf < base || doff < DP_HEADROOM || frame - base > UINT32_MAX ||
+        ((frame - base + dlen + 15) & ~(uintptr_t)15) > pool_bytes) {
       in[i] = bad_record();
       continue;
     }

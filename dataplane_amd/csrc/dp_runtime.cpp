@@ -359,13 +359,20 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
   int rc;
   if (c->ft) {
     // the flows variant: FlowLookup on the attached table and the flow-aware
-    // stages, with this launch's event / verdict scratch
+    // stages, with this launch's event / verdict scratch; in the table's one
+    // order (dp_flows_rt.h): after every earlier management call and every
+    // earlier flows burst of any context attached to the table
+    dp_flow_table *ft = c->ft;
+    std::lock_guard<std::mutex> lk(ft->mu);
     if (c->fl_armed && hipStreamWaitEvent(s, c->fl_used, 0) != hipSuccess) return fail(DP_EIO, "stream wait");
+    if (ft->burst_armed && hipStreamWaitEvent(s, ft->last_burst, 0) != hipSuccess)
+      return fail(DP_EIO, "stream wait (flow table)");
     dpf::FlowCtx fc{};
-    fc.slots = c->ft->slots;
-    fc.mask = c->ft->mask;
+    fc.slots = ft->slots;
+    fc.mask = ft->mask;
+    fc.max_probe = ft->max_probe;
     fc.n = n;
-    fc.events = static_cast<uint32_t *>(c->fl_ev.get(sizeof(uint32_t) * (1 + 2 * (uint64_t)n)));
+    fc.events = static_cast<uint32_t *>(c->fl_ev.get(sizeof(uint32_t) * (1 + 4 * (uint64_t)n)));
     fc.sens = static_cast<uint32_t *>(c->fl_sens.get(sizeof(uint32_t) * 8 + sizeof(dpf::SensRec) * (uint64_t)n));
     fc.refs = reinterpret_cast<unsigned long long *>(dev_flow_refs);
     fc.genid = img->im.genid;
@@ -380,6 +387,7 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
         return fail(DP_EIO, "hipEventCreate");
       (void)hipEventRecord(c->fl_used, s);
       c->fl_armed = true;
+      if (hipEventRecord(ft->last_burst, s) == hipSuccess) ft->burst_armed = true;
     }
   } else {
     if (dev_flow_refs) (void)hipMemsetAsync(dev_flow_refs, 0xff, sizeof(uint64_t) * n, s);  // DP_FLOW_NONE

@@ -133,6 +133,14 @@ class FlowTable:
                 self.lib)
         return ln.value, act.value
 
+    def debug_stats(self) -> dict:
+        """Slot census (test hook dpf_debug_table_stats, not part of dpgpu.h):
+        FULL / TOMB / EMPTY slots and the lookup probe bound."""
+        out = (C.c_uint64 * 4)()
+        self.lib.dpf_debug_table_stats.argtypes = [C.c_void_p, C.c_void_p]
+        A.check(self.lib.dpf_debug_table_stats(self.h, out), "dpf_debug_table_stats", self.lib)
+        return dict(full=out[0], tomb=out[1], empty=out[2], max_probe=out[3])
+
     def close(self) -> None:
         if self.h:
             self.lib.dp_flow_table_destroy(self.h)

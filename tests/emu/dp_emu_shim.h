@@ -12,7 +12,13 @@
 #define __host__
 #endif
 #define __global__
+#ifdef DP_EMU_OUTLINE
+// every device function out of line (built with -fno-inline): the call
+// shape of DP_COLD functions on the GPU, arguments by reference included
+#define __forceinline__ __attribute__((noinline))
+#else
 #define __forceinline__ inline
+#endif
 #define __launch_bounds__(x)
 #define __shared__
 struct uint4 { uint32_t x, y, z, w; };

@@ -10,7 +10,8 @@ _libs = {}
 
 
 def lib(variant: str = ""):
-    """variant "" = the product window; "w32" = a 32-byte header window."""
+    """variant "" = the product window; "w32" = a 32-byte header window;
+    "outline" = every device function out of line (DP_EMU_OUTLINE)."""
     if variant not in _libs:
         p = os.environ.get("DPEMU_LIB") if not variant else None
         if not p:

@@ -73,3 +73,31 @@ def test_edge_corpus_coverage(tables):
                  "REQ_STATIC_NAT_DST", "IS_L2_BCAST"):
         assert np.any(f & A.META[flag]), flag
     assert set(np.unique(out["acl"])) >= {0, 1, 2, 3, 4, 5}
+
+
+@pytest.mark.parametrize("form", ["bv", "list"])
+def test_edge_outline_matches_oracle(tables, form, cls_form):
+    """Every device function kept out of line (tests/emu libdpemu_outline.so:
+    -fno-inline, DP_COLD honoured): the by-reference call shape of the GPU's
+    noinline functions (classify_bv) runs under the CPU suite too."""
+    cls_form(pyemu.lib("outline"), form)
+    _, tp = tables
+    buf, inp = pack_burst(edge_frames(3000, 7))
+    b_ref, b_dut = buf.copy(), buf.copy()
+    o_ref = Oracle(tp).process(b_ref, inp, A.PKT_OUT)
+    o_dut = pyemu.process(tp, b_dut, inp, A.PKT_OUT, variant="outline")
+    if form == "bv":
+        assert pyemu.classifier_forms("outline")[0] > 0
+    compare(o_ref, b_ref, o_dut, b_dut, inp, f"edge outline {form}")
+
+
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_workload_outline_matches_oracle(cfg, cls_form):
+    from dataplane_amd.workload import Workload
+    cls_form(pyemu.lib("outline"), "bv")
+    w = Workload(cfg, 2000, seed=950 + cfg, n_routes_v4=2000, n_routes_v6=1000, n_acl=200,
+                 n_nat=32, tcp_percent=30)
+    b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
+    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+    o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT, variant="outline")
+    compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} outline")

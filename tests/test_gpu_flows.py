@@ -206,3 +206,92 @@ def test_gpu_flows_host_origin(nf):
     compare(oout, obuf, hout, hbuf, w.inp, "flows host-origin")
     assert np.array_equal(gft.get(gref)["status"], oft.get(oref)["status"])
     assert gft.count() == oft.count()
+
+
+def test_gpu_flows_two_contexts_one_table(nf):
+    """Two worker contexts attached to one flow table (one
+    table per device, every worker's context attached) run flows bursts on
+    their own streams, launched back to back: the table orders them (the
+    burst-local invalidation marks live in the shared slots), so outputs and
+    flow states equal the oracle's two bursts run one after the other."""
+    import torch
+    w = Workload(2, 8000, seed=21, n_routes_v4=3000, n_acl=400, n_nat=24, tcp_percent=30)
+    ora = Oracle(w.tables)
+    frames = frames_of(w)
+    o0 = ora.process(w.fresh_buf(), w.inp, A.PKT_OUT)
+    items, burst = scenario(frames, o0["dst_vni"], genid=1, seed=21, n_flows=700,
+                            vnis=sorted(set(int(v) for v in o0["dst_vni"] if v)))
+    oft, gft = OracleFlows(), FlowTable(0, 1 << 13)
+    orefs, grefs = install(oft, items), install(gft, items)
+    half = len(burst) // 2
+    bursts = [pack_burst([(f, 1, A.IN_SEEDED_OVERLAY, v) for f, v in part])
+              for part in (burst[:half], burst[half:])]
+    nf2 = GpuPathNf(0)
+    dev = torch.device("cuda", 0)
+    try:
+        for x in (nf, nf2):
+            x.publish(w.tables)
+            x.attach_flows(gft)
+        streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        dbufs, dins, douts = [], [], []
+        for buf, inp in bursts:
+            dbufs.append(torch.from_numpy(buf.copy()).to(dev))
+            dins.append(torch.from_numpy(inp.view(np.uint8).copy()).to(dev))
+            douts.append(torch.zeros(len(inp) * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev))
+        torch.cuda.synchronize(dev)
+        for k, x in enumerate((nf, nf2)):
+            x.process_device_ex(dbufs[k].data_ptr(), dbufs[k].numel(), dins[k].data_ptr(),
+                                douts[k].data_ptr(), len(bursts[k][1]), None, None,
+                                streams[k].cuda_stream)
+        torch.cuda.synchronize(dev)
+        for k, (buf, inp) in enumerate(bursts):
+            obuf = buf.copy()
+            oout, _ = ora.process_flows(obuf, inp, A.PKT_OUT, oft)
+            gbuf = dbufs[k].cpu().numpy()
+            gout = douts[k].cpu().numpy().view(A.PKT_OUT)
+            compare(oout, obuf, gout, gbuf, inp, f"two contexts, burst {k}")
+        gi, oi = gft.get(grefs), oft.get(orefs)
+        assert np.array_equal(gi["ref"] == A.FLOW_NONE, oi["ref"] == A.FLOW_NONE)
+        live = gi["ref"] != A.FLOW_NONE
+        assert np.array_equal(gi["status"][live], oi["status"][live])
+    finally:
+        for x in (nf, nf2):
+            x.attach_flows(None)
+        nf2.close()
+
+
+def test_gpu_flow_table_churn(nf):
+    """Insert / timer-sweep cycles (tombstones): removals leave no
+    unbounded tombstone build-up -- runs of tombstones that end a cluster are
+    reclaimed, lookups probe at most max_probe + 1 slots -- and every lookup
+    stays right: live flows are found, expired ones are not."""
+    from dataplane_amd.flows import flow_key, make_flow
+    rng = np.random.default_rng(5)
+    slots = 1 << 12
+    gft = FlowTable(0, slots)
+    prev = None
+    try:
+        for cyc in range(1, 41):
+            fl = np.zeros(1400, A.FLOW)
+            for i in range(len(fl)):
+                a = rng.integers(1, 2**31, size=2)
+                fl[i] = make_flow(flow_key(7, int(a[0]), int(a[1]), A.FLOW_UDP,
+                                           int(rng.integers(1, 65535)), int(rng.integers(1, 65535))),
+                                  dst_vni=9, genid=1, expires_at=cyc + (i % 2))
+            refs, res = gft.insert(fl)
+            assert (res == A.FLOW_INSERTED).all()
+            removed = gft.sweep(cyc)                  # this cycle's even flows, last cycle's odd ones
+            st = gft.debug_stats()
+            assert st["full"] == gft.count()[0]
+            assert st["max_probe"] <= 64, st
+            assert st["empty"] >= slots // 4, st      # without reclamation: 0 by cycle 18
+            found = gft.lookup(fl["key"])
+            live = (np.arange(len(fl)) % 2) == 1
+            assert (found["ref"][live] != A.FLOW_NONE).all()
+            assert (found["ref"][~live] == A.FLOW_NONE).all()
+            if prev is not None:
+                assert (gft.lookup(prev["key"])["ref"] == A.FLOW_NONE).all()
+                assert removed == len(fl) // 2 + len(prev) // 2
+            prev = fl
+    finally:
+        gft.close()

@@ -62,3 +62,23 @@ def test_mbuf_burst_results():
     assert (pool.field(1, "data_off"), pool.field(1, "data_len"), pool.field(1, "pkt_len")) == (HEADROOM - 50, 110, 110)
     assert (pool.field(2, "data_off"), pool.field(2, "data_len")) == (HEADROOM, 60)
     assert (pool.field(3, "data_off"), pool.field(3, "data_len")) == (HEADROOM, 64)
+
+
+def test_mbuf_frame_at_pool_tail_fails_alone():
+    """A frame whose end lies inside the pool but whose end rounded up to 16
+    bytes (the kernel's 16-byte staging) does not fit gets its own failure record;
+    the other mbufs keep theirs (no whole-burst DP_EINVAL later)."""
+    lib = A.gpu_lib()
+    pool = FakeMempool(np.zeros(FakeMempool.bytes_for(2), np.uint8))
+    mbufs = pool.load([b"\x01" * 60, b"\x02" * 61], ports=[0, 0])
+    full = burst_in(pool, mbufs)
+    end = int(full[1]["off"]) + 61                    # the last frame's exact end
+    assert end % 16 != 0
+    inp = np.zeros(2, A.PKT_IN)
+    assert lib.dp_mbuf_burst_in(pool.base, end, mbufs.ctypes.data, 2, C.byref(A.MBUF_LAYOUT_DPDK),
+                                None, 0, inp.ctypes.data) == 0
+    assert inp[0]["off"] == full[0]["off"] and inp[0]["len"] == 60
+    assert inp[1]["off"] == 0 and inp[1]["len"] == 0
+    assert lib.dp_mbuf_burst_in(pool.base, (end + 15) & ~15, mbufs.ctypes.data, 2,
+                                C.byref(A.MBUF_LAYOUT_DPDK), None, 0, inp.ctypes.data) == 0
+    assert inp[1]["off"] == full[1]["off"]
