@@ -269,6 +269,7 @@ def test_gpu_flow_table_churn(nf):
     rng = np.random.default_rng(5)
     slots = 1 << 12
     gft = FlowTable(0, slots)
+    gft.set_capacity(3000)           # above the 2100 flows a cycle holds before its sweep
     prev = None
     try:
         for cyc in range(1, 41):
