@@ -149,14 +149,16 @@ def flows_leg(nf, w, dev, stream, steps: int) -> dict:
     b = torch.empty(bb, dtype=torch.uint8, device=dev)
     dinp = torch.from_numpy(w.inp.view(np.uint8)).to(dev)
     dout = torch.empty(n * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+    dmeta = torch.empty(n * A.PKT_META.itemsize, dtype=torch.uint8, device=dev)
     sptr = stream.cuda_stream
     # each packet's flow-filter verdict, from one run without flows
     b[:w.buf.nbytes].copy_(pristine)
-    nf.process_device(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None, sptr)
+    nf.process_device(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None, sptr,
+                      dev_meta=dmeta.data_ptr())
     torch.cuda.synchronize(dev)
-    out = dout.cpu().numpy().view(A.PKT_OUT)
+    meta = dmeta.cpu().numpy().view(A.PKT_META)
     # the even packets' request flows (Eth / IPv4 / UDP|TCP frames with a verdict)
-    fl = burst_request_flows(w.buf, w.inp, np.arange(0, n, 2), out["dst_vni"], nf.data.genid)
+    fl = burst_request_flows(w.buf, w.inp, np.arange(0, n, 2), meta["dst_vni"], nf.data.genid)
     slots = 1 << max(12, int(np.ceil(np.log2(max(1, 4 * len(fl))))))
     ft = FlowTable(0, slots)
     ft.set_capacity(len(fl))
@@ -164,18 +166,18 @@ def flows_leg(nf, w, dev, stream, steps: int) -> dict:
     _, res = ft.insert(fl)
     t_ins = time.perf_counter() - t0
     nf.attach_flows(ft)
-    refs = torch.empty(n, dtype=torch.int64, device=dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps + 2)]
     for k2 in range(steps + 2):
         b[:w.buf.nbytes].copy_(pristine)
         ev[k2][0].record(stream)
-        nf.process_device_ex(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None,
-                             refs.data_ptr(), sptr)
+        nf.process_device(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None, sptr,
+                          dev_meta=dmeta.data_ptr())
         ev[k2][1].record(stream)
     torch.cuda.synchronize(dev)
     ms = sorted(a.elapsed_time(c) for a, c in ev[2:])
-    hit = int((refs.cpu().numpy().view(np.uint64) != np.uint64(A.FLOW_NONE)).sum())
+    refs = dmeta.cpu().numpy().view(A.PKT_META)["flow_ref"]
+    hit = int((refs != np.uint64(A.FLOW_NONE)).sum())
     nf.attach_flows(None)
     ln, act = ft.count()
     ft.close()
@@ -186,7 +188,8 @@ def flows_leg(nf, w, dev, stream, steps: int) -> dict:
             "what": "the same burst with a flow table attached: every other packet's flow pair "
                     "established (Active, current generation), FlowLookup on every overlay "
                     "packet, flow-filter bypass, flows-variant kernel + fix-up + invalidation "
-                    "kernels per launch (median of %d launches)" % steps}
+                    "kernels per launch, dp_pkt_meta_t (flow refs) written "
+                    "(median of %d launches)" % steps}
 
 
 def main() -> None:
@@ -298,6 +301,21 @@ def main() -> None:
     launch_ms = sorted(a.elapsed_time(b) for a, b in kev)
     pipe_ms_median = launch_ms[len(launch_ms) // 2]
     pipe_ms_mean = sum(launch_ms) / len(launch_ms)
+    # the same launches also writing the optional dp_pkt_meta_t array (the
+    # rest of PacketMeta: VNIs, FIB entry, ACL rule, VRF, next hop, DSCP)
+    dmeta = torch.empty(n * A.PKT_META.itemsize, dtype=torch.uint8, device=dev)
+    for k in range(nbuf):
+        bufs[k, :w.buf.nbytes].copy_(pristine)
+    torch.cuda.synchronize(dev)
+    for k in range(args.steps):
+        kev[k][0].record(stream)
+        nf.process_device(bufs[args.warmup + k].data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n,
+                          None, sptr, dev_meta=dmeta.data_ptr())
+        kev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    meta_ms = sorted(a.elapsed_time(b) for a, b in kev)
+    meta_ms_median = meta_ms[len(meta_ms) // 2]
+    del dmeta
 
     elapsed, hist = reduce_over_ranks(elapsed, dstats.cpu().numpy(), dev)
 
@@ -359,6 +377,10 @@ def main() -> None:
             "step_ms_events_mean": round(kernel_ms, 4),
             "mpps_median_step": round(world * n / (sorted(step_ms)[len(step_ms) // 2] / 1e3) / 1e6, 3),
             "roofline": roofline,
+            "with_meta": {"kernel_ms_median": round(meta_ms_median, 4),
+                          "mpps_median": round(n / (meta_ms_median / 1e3) / 1e6, 3),
+                          "what": "the same launches also writing dp_pkt_meta_t (48 B per "
+                                  "packet: the rest of PacketMeta) beside dp_pkt_out_t"},
             "done_histogram": {A.DONE_NAMES[i]: int(c) for i, c in enumerate(hist) if c},
         }
         if rccl:
@@ -380,7 +402,7 @@ def main() -> None:
                 for r in range(reps + 1):
                     pnp[:] = w.buf
                     t0 = time.perf_counter()
-                    nf.process_arrays(pnp, pin_in, out=pin_out)
+                    nf.process_arrays(pnp, pin_in, out=pin_out, with_meta=False)
                     if r > 0:
                         t_host.append(time.perf_counter() - t0)
                 return sorted(t_host)[len(t_host) // 2]

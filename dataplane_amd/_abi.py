@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 HEADROOM = 96
 
 # DoneReason (net/src/packet/meta.rs:84-119)
@@ -43,10 +43,48 @@ IN_SEEDED_OVERLAY = 1
 
 PKT_IN = np.dtype([("off", "<u4"), ("len", "<u2"), ("flags", "<u2"), ("iif", "<u4"),
                    ("src_vni", "<u4")])
+# dp_pkt_out_t: what the driver needs to transmit or drop a packet (always written)
 PKT_OUT = np.dtype([("off", "<u4"), ("len", "<u2"), ("done", "u1"), ("acl", "u1"),
-                    ("meta_flags", "<u4"), ("oif", "<u4"), ("dst_vni", "<u4"),
-                    ("src_vni", "<u4"), ("fib_entry", "<u4"), ("acl_rule", "<u4")])
-assert PKT_IN.itemsize == 16 and PKT_OUT.itemsize == 32
+                    ("oif", "<u4"), ("meta_flags", "<u2"), ("pad", "<u2")])
+# dp_pkt_meta_t: the rest of PacketMeta (optional array)
+PKT_META = np.dtype([("dst_vni", "<u4"), ("src_vni", "<u4"), ("fib_entry", "<u4"),
+                     ("acl_rule", "<u4"), ("vrf", "<u4"), ("pm_flags", "u1"), ("dscp", "u1"),
+                     ("ecn", "u1"), ("nh_family", "u1"), ("nh_addr", "u1", 16),
+                     ("flow_ref", "<u8")])
+assert PKT_IN.itemsize == 16 and PKT_OUT.itemsize == 16 and PKT_META.itemsize == 48
+# one packet's whole result (test / host convenience): dp_pkt_out_t then dp_pkt_meta_t
+PKT_RES = np.dtype(PKT_OUT.descr + PKT_META.descr)
+assert PKT_RES.itemsize == 64
+PM_HAS_VRF, PM_HAS_NH, PM_HAS_DSCP = 1, 2, 4
+
+
+def join_results(out: np.ndarray, meta: np.ndarray) -> np.ndarray:
+    """PKT_RES records from a dp_pkt_out_t array and a dp_pkt_meta_t array."""
+    res = np.zeros(len(out), dtype=PKT_RES)
+    for f in PKT_OUT.names:
+        res[f] = out[f]
+    for f in PKT_META.names:
+        res[f] = meta[f]
+    return res
+
+
+def nh_text(r) -> str:
+    """A PKT_RES / PKT_META record's next-hop address as text (nh_family 4 / 6)."""
+    import ipaddress
+    b = bytes(np.asarray(r["nh_addr"], dtype=np.uint8))
+    return str(ipaddress.IPv4Address(b[:4]) if int(r["nh_family"]) == 4
+               else ipaddress.IPv6Address(b))
+
+
+def split_results(res: np.ndarray):
+    """(dp_pkt_out_t array, dp_pkt_meta_t array) of PKT_RES records."""
+    out = np.zeros(len(res), dtype=PKT_OUT)
+    meta = np.zeros(len(res), dtype=PKT_META)
+    for f in PKT_OUT.names:
+        out[f] = res[f]
+    for f in PKT_META.names:
+        meta[f] = res[f]
+    return out, meta
 
 # Flow table (include/dpgpu.h "Flow table")
 FLOW_TCP, FLOW_UDP, FLOW_ICMP_QUERY, FLOW_ICMP_OTHER = 1, 2, 3, 4
@@ -188,8 +226,8 @@ GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_p
                "dp_flow_table_destroy", "dp_flow_table_set_capacity", "dp_flow_insert",
                "dp_flow_insert_pair", "dp_flow_lookup", "dp_flow_get", "dp_flow_remove",
                "dp_flow_invalidate", "dp_flow_set_status", "dp_flow_sweep", "dp_flow_count",
-               "dp_ctx_attach_flow_table", "dp_process_burst_device_ex", "dp_mbuf_burst_in",
-               "dp_mbuf_burst_out", "dp_process_mbufs"]
+               "dp_ctx_attach_flow_table", "dp_mbuf_burst_in", "dp_mbuf_burst_out",
+               "dp_process_mbufs"]
 NP_STRUCTS = dict(dp_flow_key_t=FLOW_KEY, dp_flow_t=FLOW, dp_flow_info_t=FLOW_INFO)
 
 
@@ -231,11 +269,11 @@ def gpu_lib() -> C.CDLL:
         lib.dp_tables_publish.argtypes = [_VP, C.POINTER(TablesDesc)]
         lib.dp_tables_genid.argtypes = [_VP]
         lib.dp_tables_genid.restype = C.c_int64
-        lib.dp_process_burst.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, C.c_uint32, _VP]
-        lib.dp_process_burst_device.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, C.c_uint32,
-                                                _VP, _VP]
+        lib.dp_process_burst.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, _VP, C.c_uint32, _VP]
+        lib.dp_process_burst_device.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, _VP,
+                                                C.c_uint32, _VP, _VP]
         lib.dp_process_burst_sharded.argtypes = [C.POINTER(_VP), C.c_uint32, _VP, C.c_uint64,
-                                                 _VP, _VP, C.c_uint32, _VP]
+                                                 _VP, _VP, _VP, C.c_uint32, _VP]
         lib.dp_ctx_synchronize.argtypes = [_VP]
         lib.dp_tables_device_bytes.argtypes = [_VP]
         lib.dp_tables_device_bytes.restype = C.c_uint64
@@ -254,13 +292,11 @@ def gpu_lib() -> C.CDLL:
         lib.dp_flow_sweep.argtypes = [_VP, C.c_uint64, _VP]
         lib.dp_flow_count.argtypes = [_VP, _VP, _VP]
         lib.dp_ctx_attach_flow_table.argtypes = [_VP, _VP]
-        lib.dp_process_burst_device_ex.argtypes = [_VP, _VP, C.c_uint64, _VP, _VP, C.c_uint32,
-                                                   _VP, _VP, _VP]
         lib.dp_mbuf_burst_in.argtypes = [_VP, C.c_uint64, _VP, C.c_uint32, C.POINTER(MbufLayout),
                                          _VP, C.c_uint32, _VP]
         lib.dp_mbuf_burst_out.argtypes = [_VP, C.c_uint32, C.POINTER(MbufLayout), _VP, _VP]
         lib.dp_process_mbufs.argtypes = [_VP, _VP, C.c_uint64, _VP, C.c_uint32,
-                                         C.POINTER(MbufLayout), _VP, C.c_uint32, _VP, _VP]
+                                         C.POINTER(MbufLayout), _VP, C.c_uint32, _VP, _VP, _VP]
         if lib.dp_abi_version() != ABI_VERSION:
             raise RuntimeError("libdpgpu.so ABI version mismatch")
         _gpu = lib

@@ -135,14 +135,15 @@ struct IfRec {         // 32 B
 // Multibit index descriptor (see FieldIdx / NatTab) copied into the context
 // record that leads to the index, so the hot path walks it without first
 // loading the Group / NatTab record (one dependent load less per lookup).
-struct Mbi {           // 24 B
-  uint64_t root;       // 0: not usable here (bit-vector group, bounds form, absent table)
-  uint64_t blocks;
+struct Mbi {           // 16 B (image offsets < 4 GiB: dp_tables.cpp refuses larger images)
+  uint32_t root;       // 0: not usable here (bit-vector group, bounds form, absent table)
+  uint32_t blocks;
   uint8_t s0, kbits;   // root stride, key width (32 address / 16 port)
   uint8_t field;       // classifier: the indexed field (0 src, 1 dst, 2 sport, 3 dport)
   uint8_t pad;
   uint32_t pad2;
 };
+static_assert(sizeof(Mbi) == 16, "Mbi is 16 B");
 
 // Per source VNI context.  The records are the open-addressing slots of the
 // VNI map themselves (key `vni`, 0 = empty: VNI 0 is invalid,
@@ -157,7 +158,7 @@ struct alignas(16) VniRec {  // 96 B
   uint32_t pad;
   Mbi ffr4;            // index of the v4 remote group (candidate-list form)
   Mbi ndst;            // index of the NAT dst table
-  uint64_t pad2[2];
+  uint64_t pad2[4];
 };
 static_assert(sizeof(VniRec) == 96, "VniRec is 96 B");
 
@@ -171,11 +172,13 @@ struct alignas(16) PairRec {  // 128 B
   uint32_t dst_vni;
   Mbi ffl4;            // index of the v4 local group (candidate-list form)
   Mbi acl4;            // index of the v4 ACL group (candidate-list form)
+  Mbi acl4b;           // the ACL group's second list index (Group.lfield2), root 0: none
   Mbi nsrc;            // index of the NAT src table
   uint64_t lpm4_direct;  // the dst FIB's v4 LPM (Lpm.direct / dbits / blocks), 0: none
   uint32_t lpm4_dbits;
   uint32_t pad;
   uint64_t lpm4_blocks;
+  uint64_t pad2;
 };
 static_assert(sizeof(PairRec) == 128, "PairRec is 128 B");
 
@@ -229,6 +232,7 @@ struct FieldIdx {
 // hold a packed run: first record << DPD_RUN_BITS | count.
 #define DPD_GROUP_BV 0
 #define DPD_GROUP_LIST 1
+#define DPD_NO_FIELD 0xffu
 #define DPD_RUN_BITS 6
 #define DPD_RUN_MAX 63
 struct CandRec {       // 64 B, 64-byte aligned: one sector per candidate
@@ -261,6 +265,10 @@ struct Group {
   uint32_t rule_base;  // index of rule 0 of this group in the table's rule arrays
   uint32_t mode;       // DPD_GROUP_BV / DPD_GROUP_LIST
   uint32_t lfield;     // LIST: the indexed field (0 src, 1 dst, 2 sport, 3 dport)
+  uint32_t lfield2;    // LIST: a second indexed field (DPD_NO_FIELD: none); its runs hold
+                       // the same candidates for the other field's intervals, so a lookup
+                       // may verify whichever of the two runs is shorter
+  uint32_t pad_l;
   uint64_t recs;       // LIST: offset of CandRec[]
   uint64_t pool;       // BV: offset of uint64_t rows[row][S + W]
   uint64_t proto_rows; // BV: offset of uint16_t[256]

@@ -66,7 +66,6 @@ struct FlowCtx {
   // ACL decisions that rest on a flow's validity (acl = 6): [0] count, then
   // SensRec records
   uint32_t *sens;
-  unsigned long long *refs;  // per packet PacketMeta.flow_info ref, nullable
   int64_t genid;        // the burst's PipelineData genid
 };
 
@@ -82,6 +81,10 @@ struct SensRec {
   uint32_t def_acl;     // the default verdict: out.acl code 3 / 4 / 5
   uint32_t related;     // the flow's related slot and its state when paired
   uint32_t related_tag;
+  uint32_t dst_vni;     // PacketMeta at the ACL: dst_vpcd, vrf (bit 31: Some), the nh_addr source
+  uint32_t vrf;
+  uint32_t nh_ref;
+  uint32_t pad;
 };
 
 __host__ __device__ inline uint64_t make_ref(uint32_t slot, uint32_t state) {

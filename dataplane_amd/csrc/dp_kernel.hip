@@ -702,6 +702,8 @@ struct State {
   uint8_t dscp, ecn;
   uint32_t fib_entry, acl_rule;
   uint8_t acl;
+  uint32_t nh_ref;       // PacketMeta.nh_addr source: the last Egress instruction executed
+                         // (NH_NONE; bit 31: the single instruction of FibEntry `low bits`)
   // current header field values
   uint64_t edst, esrc;   // current Ethernet dst / src (48-bit, byte 0 on top)
   bool eth_dirty;
@@ -719,6 +721,8 @@ struct State {
 };
 
 __device__ __forceinline__ void done(State &S, uint8_t r) { if (S.done == DONE_NONE) S.done = r; }
+constexpr uint32_t NH_NONE = 0xffffffffu;
+constexpr uint32_t NH_ENTRY = 0x80000000u;
 
 __device__ __forceinline__ void load_fields(const Frame &F, const Hdr &H, State &S) {
   S.edst = mac_at(F, H.hb);
@@ -1496,6 +1500,7 @@ struct FlowPk {
   uint32_t ev_mark;    // mark of ev1 (ACL deny at packet idx: idx + 1)
   bool sens;           // ACL allowed it as the reply of a flow-scope-allowed flow
   uint32_t def_acl, s_flags, s_oif, s_fib;
+  uint32_t s_dvni, s_vrf, s_nh;  // dst_vni, vrf (bit 31: Some) and nh_ref at the ACL
 };
 
 __device__ __forceinline__ uint4 ld4(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
@@ -1891,6 +1896,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
     decrement_ttl(S);
     if (S.done != DONE_NONE) return;
     if (nr.kind == DPD_NH_DROP) { done(S, DP_DONE_ROUTE_DROP); return; }
+    S.nh_ref = NH_ENTRY | nr.entry;  // the entry's one Egress instruction
     S.has_oif = nr.has_oif;
     S.oif = nr.oif;
     S.eg_code = nr.eg_code;
@@ -1937,6 +1943,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
       }
       case DP_INSTR_ENCAP_VXLAN: vxlan_encap(g, F, H, S, in, fb); break;
       case DP_INSTR_EGRESS:
+        S.nh_ref = E.first_instr + k;
         S.has_oif = in.flags & DP_INSTR_HAS_IFINDEX;
         S.oif = in.ifindex;
         S.eg_code = in.eg_code;
@@ -1967,6 +1974,14 @@ __device__ __forceinline__ Key128 key_of(const Frame &F, const Hdr &H, const Sta
 // table, a bit-vector group or a bounds-form index; the stage walks itself).
 struct Pre { uint32_t ffl, acl, nsrc, ndst; };
 
+// The shorter of two candidate runs of one ACL group (the run of the packet's
+// interval in the group's first and second list index): either holds every
+// rule that can match, in precedence order.
+__device__ __forceinline__ uint32_t shorter_run(uint32_t a, uint32_t b) {
+  if (b == NO_PRE) return a;
+  return (b & DPD_RUN_MAX) < (a & DPD_RUN_MAX) ? b : a;
+}
+
 // Key of a classifier field for the v4 hoisted walks (f: 0 src, 1 dst, 2
 // sport, 3 dport); `local` = the flow-filter local table, whose dst / dport
 // keys are wildcards (0).
@@ -1981,28 +1996,30 @@ __device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_
   // walks start right after the pair context arrives
   const PairRec &PR = g.at<PairRec>(g.im.pair_recs)[pi];
   const VniRec &VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
-  Mbi m[4] = {PR.ffl4, PR.acl4, PR.nsrc, VR.ndst};
-  uint32_t key[4], e[4];
-  int rem0[4];
+  constexpr int NW = 5;
+  Mbi m[NW] = {PR.ffl4, PR.acl4, PR.nsrc, VR.ndst, PR.acl4b};
+  uint32_t key[NW], e[NW];
+  int rem0[NW];
   key[0] = mbi_key(S, m[0].field, true);
   key[1] = mbi_key(S, m[1].field, false);
   key[2] = S.v4src;
   key[3] = S.v4dst;
+  key[4] = mbi_key(S, m[4].field, false);
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < NW; k++) {
     rem0[k] = (int)m[k].kbits - (int)m[k].s0;
     e[k] = m[k].root ? g.at<uint32_t>(m[k].root)[key[k] >> rem0[k]] : DPD_LEAF;
   }
   TRIP();
 #pragma unroll
   for (int l = 1; l <= 3; l++) {
-    if (!(e[0] & e[1] & e[2] & e[3] & DPD_LEAF)) TRIP();
+    if (!(e[0] & e[1] & e[2] & e[3] & e[4] & DPD_LEAF)) TRIP();
 #pragma unroll
-    for (int k = 0; k < 4; k++)
+    for (int k = 0; k < NW; k++)
       if (!(e[k] & DPD_LEAF)) e[k] = g.at<uint32_t>(m[k].blocks)[(e[k] << 8) | ((key[k] >> (rem0[k] - 8 * l)) & 0xff)];
   }
   if (m[0].root) P.ffl = e[0] & ~DPD_LEAF;
-  if (m[1].root) P.acl = e[1] & ~DPD_LEAF;
+  if (m[1].root) P.acl = shorter_run(e[1] & ~DPD_LEAF, m[4].root ? e[4] & ~DPD_LEAF : NO_PRE);
   if (m[2].root) P.nsrc = e[2] & ~DPD_LEAF;
   if (m[3].root) P.ndst = e[3] & ~DPD_LEAF;
 }
@@ -2133,6 +2150,9 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
           fp.s_flags = S.flags;
           fp.s_oif = S.has_oif ? S.oif : 0;
           fp.s_fib = S.fib_entry;
+          fp.s_dvni = S.dst_vni;
+          fp.s_vrf = S.has_vrf ? (0x80000000u | S.vrf) : 0u;
+          fp.s_nh = S.nh_ref;
         }
         }
       }
@@ -2480,14 +2500,57 @@ __device__ __forceinline__ int serialize(const Frame &F, Hdr &H, State &S, int &
 }
 
 // ---------------------------------------------------------------------------
+// Burst records
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ dp_pkt_out_t out_record(uint32_t off, uint16_t len, uint8_t done) {
+  dp_pkt_out_t o;
+  o.off = off; o.len = len; o.done = done; o.acl = 0; o.oif = 0; o.meta_flags = 0; o.pad = 0;
+  return o;
+}
+// PacketMeta of a packet no stage annotated
+__device__ __forceinline__ dp_pkt_meta_t meta_none() {
+  dp_pkt_meta_t m;
+  m.dst_vni = m.src_vni = 0;
+  m.fib_entry = m.acl_rule = 0xffffffffu;
+  m.vrf = 0; m.pm_flags = 0; m.dscp = m.ecn = 0; m.nh_family = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) m.nh_addr[i] = 0;
+  m.flow_ref = ~0ull;
+  return m;
+}
+// PacketMeta.nh_addr: the address of the last Egress instruction executed
+// (packet_exec_instruction_egress, ipforward.rs:308-327: None without one)
+__device__ __forceinline__ void meta_nh(const Img &g, uint32_t nh_ref, dp_pkt_meta_t &m) {
+  if (nh_ref == NH_NONE) return;
+  const uint32_t ii = (nh_ref & NH_ENTRY) ? g.at<Entry>(g.im.entries)[nh_ref & ~NH_ENTRY].first_instr : nh_ref;
+  const Instr &in = g.at<Instr>(g.im.instrs)[ii];
+  if (!(in.flags & DP_INSTR_HAS_ADDR)) return;
+  m.pm_flags |= DP_PM_HAS_NH;
+  m.nh_family = in.fam;
+#pragma unroll
+  for (int i = 0; i < 16; i++) m.nh_addr[i] = in.addr[i];
+}
+__device__ __forceinline__ dp_pkt_meta_t meta_of(const Img &g, const State &S) {
+  dp_pkt_meta_t m = meta_none();
+  m.dst_vni = S.dst_vni;
+  m.src_vni = S.src_vni;
+  m.fib_entry = S.fib_entry;
+  m.acl_rule = S.acl_rule;
+  if (S.has_vrf) { m.pm_flags |= DP_PM_HAS_VRF; m.vrf = S.vrf; }
+  if (S.has_dscp) { m.pm_flags |= DP_PM_HAS_DSCP; m.dscp = S.dscp; m.ecn = S.ecn; }
+  meta_nh(g, S.nh_ref, m);
+  return m;
+}
+
+// ---------------------------------------------------------------------------
 // Per-packet body
 // ---------------------------------------------------------------------------
 // FL: the flows variant -- FlowLookup on fc's table and the flow-aware
 // branches; fp receives the packet's flow and its flow-table effects.
 template <bool FL>
 __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, lds_u8 *hs, uint8_t *buf, uint64_t buf_bytes,
-                                  const dp_pkt_in_t &pin, dp_pkt_out_t &o, int &fl0, int &fl1, bool inwin,
-                                  const dpf::FlowCtx *fc, FlowPk &fp, uint32_t idx) {
+                                  const dp_pkt_in_t &pin, dp_pkt_out_t &o, dp_pkt_meta_t *pm, int &fl0, int &fl1,
+                                  bool inwin, const dpf::FlowCtx *fc, FlowPk &fp, uint32_t idx) {
   fl0 = fl1 = 0;
   if constexpr (FL) {
     fp.slot = fp.ev0 = fp.ev1 = dpf::kNoSlot;
@@ -2495,9 +2558,8 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   }
   if (!frame_ok(pin, buf_bytes)) {
     // layout contract violated: never touch memory outside the buffer
-    o.off = pin.off; o.len = pin.len; o.done = DP_DONE_INTERNAL_FAILURE; o.acl = 0;
-    o.meta_flags = 0; o.oif = 0; o.dst_vni = 0; o.src_vni = 0;
-    o.fib_entry = 0xffffffffu; o.acl_rule = 0xffffffffu;
+    o = out_record(pin.off, pin.len, DP_DONE_INTERNAL_FAILURE);
+    if (pm) *pm = meta_none();
     return o.done;
   }
   TS_DECL
@@ -2509,15 +2571,14 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   F.len = pin.len;
   F.inwin = inwin;
   // the header window is staged in `slab` by the caller (kernel / dpemu_run)
-  o.off = pin.off; o.len = pin.len; o.acl = 0; o.oif = 0; o.dst_vni = 0; o.src_vni = 0;
-  o.fib_entry = 0xffffffffu; o.acl_rule = 0xffffffffu;
   TS(0);
   Hdr H;
   if (!parse(F, 0, H)) {
-    o.done = DP_DONE_NOT_ETHERNET;
-    o.meta_flags = 0;
+    o = out_record(pin.off, pin.len, DP_DONE_NOT_ETHERNET);
+    if (pm) *pm = meta_none();
     return o.done;
   }
+  o.off = pin.off; o.len = pin.len;
   State S;
   S.done = DONE_NONE;
   S.flags = DP_META_INITIALIZED | DP_META_KEEP;
@@ -2525,7 +2586,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   S.has_oif = false; S.oif = 0; S.eg_code = DP_DONE_ROUTE_FAILURE; S.if_code = 255;
   S.eg_dmac = S.eg_smac = 0; S.fib = -1; S.vni_idx = -1; S.pair = -1;
   S.has_dscp = false; S.dscp = S.ecn = 0;
-  S.fib_entry = 0xffffffffu; S.acl_rule = 0xffffffffu; S.acl = 0;
+  S.fib_entry = 0xffffffffu; S.acl_rule = 0xffffffffu; S.acl = 0; S.nh_ref = NH_NONE;
   S.encap = false; S.o_eth = false; S.inner_l4_ck = false;
   S.ttl = 0; S.v4src = S.v4dst = 0;
   load_fields(F, H, S);
@@ -2595,13 +2656,15 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
     }
   }
   o.done = S.done;
-  o.meta_flags = S.flags;
+  o.meta_flags = (uint16_t)S.flags;
   o.oif = S.has_oif ? S.oif : 0;
-  o.dst_vni = S.dst_vni;
-  o.src_vni = S.src_vni;
-  o.fib_entry = S.fib_entry;
-  o.acl_rule = S.acl_rule;
   o.acl = S.acl;
+  o.pad = 0;
+  if (pm) {
+    dp_pkt_meta_t m = meta_of(g, S);
+    if constexpr (FL) if (fp.slot != dpf::kNoSlot) m.flow_ref = dpf::make_ref(fp.slot, fp.state);
+    *pm = m;
+  }
   TS(8);
   TS_FLUSH();
   return o.done;
@@ -2667,7 +2730,6 @@ __device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull
 __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, uint32_t i, const FlowPk &fp) {
   const int lane = threadIdx.x & 63;
   const bool has = live && fp.slot != dpf::kNoSlot;
-  if (live && fc.refs) fc.refs[i] = has ? dpf::make_ref(fp.slot, fp.state) : ~0ull;
   const bool e0 = has && fp.ev0 != dpf::kNoSlot, e1 = has && fp.ev1 != dpf::kNoSlot;
   if (e0) atomicMin(&fc.slots[fp.ev0].mark, 0u);
   if (e1) atomicMin(&fc.slots[fp.ev1].mark, fp.ev_mark);
@@ -2698,7 +2760,8 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
     base = (uint32_t)__shfl((int)base, leader);
     if (sv) {
       dpf::SensRec *R = reinterpret_cast<dpf::SensRec *>(fc.sens + 8) + base + __popcll(ms & lanes_below(lane));
-      *R = dpf::SensRec{i, fp.slot, fp.s_flags, fp.s_oif, fp.s_fib, fp.def_acl, fp.related, fp.related_tag};
+      *R = dpf::SensRec{i, fp.slot, fp.s_flags, fp.s_oif, fp.s_fib, fp.def_acl, fp.related, fp.related_tag,
+                        fp.s_dvni, fp.s_vrf, fp.s_nh, 0};
     }
   }
 }
@@ -2708,8 +2771,8 @@ template <bool FL>
 __global__ void __launch_bounds__(TPB) DP_OCC
 dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict__ im, uint8_t *__restrict__ buf,
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
-                   dp_pkt_out_t *__restrict__ out, uint32_t n, unsigned long long *__restrict__ part,
-                   dpf::FlowCtx fc) {
+                   dp_pkt_out_t *__restrict__ out, dp_pkt_meta_t *__restrict__ meta, uint32_t n,
+                   unsigned long long *__restrict__ part, dpf::FlowCtx fc) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_all[TPB * (SLAB + HS)];
   uint8_t *slab_all = lds_all;
   uint8_t *hash_all = lds_all + TPB * SLAB;
@@ -2735,8 +2798,9 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
     Img g{img_base, *im};
     dp_pkt_out_t o;
     lds_u8 *hs = (lds_u8 *)(hash_all + tid * HS);
-    if (all_fit) done_code = process_packet<FL>(g, slab, hs, buf, buf_bytes, pin, o, fl0, fl1, true, &fc, fp, i);
-    else done_code = process_packet<FL>(g, slab, hs, buf, buf_bytes, pin, o, fl0, fl1, false, &fc, fp, i);
+    dp_pkt_meta_t *pm = meta ? meta + i : nullptr;
+    if (all_fit) done_code = process_packet<FL>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, true, &fc, fp, i);
+    else done_code = process_packet<FL>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, false, &fc, fp, i);
     out[i] = o;
   }
   if constexpr (FL) flow_effects(fc, live, i, fp);
@@ -2766,8 +2830,11 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
 // over the whole burst before any ACL) nor by the deny of an earlier packet
 // (mark idx + 1).  Otherwise the peering default applies; a default Deny
 // drops the packet at the ACL with its metadata as it stood there.
-__global__ void __launch_bounds__(256) dp_flow_fixup(dpf::FlowCtx fc, const dp_pkt_in_t *__restrict__ in,
+__global__ void __launch_bounds__(256) dp_flow_fixup(const uint8_t *__restrict__ img_base,
+                                                     const Image *__restrict__ im, dpf::FlowCtx fc,
+                                                     const dp_pkt_in_t *__restrict__ in,
                                                      dp_pkt_out_t *__restrict__ out,
+                                                     dp_pkt_meta_t *__restrict__ meta,
                                                      unsigned long long *__restrict__ stats) {
   const uint32_t cnt = fc.sens[0];
   const dpf::SensRec *recs = reinterpret_cast<const dpf::SensRec *>(fc.sens + 8);
@@ -2779,7 +2846,7 @@ __global__ void __launch_bounds__(256) dp_flow_fixup(dpf::FlowCtx fc, const dp_p
     if (fc.slots[R.slot].mark > R.idx && (!rel || fc.slots[R.related].mark > R.idx)) continue;  // still valid
     dp_pkt_out_t o = out[R.idx];
     o.acl = (uint8_t)R.def_acl;
-    o.acl_rule = 0xffffffffu;
+    if (meta) meta[R.idx].acl_rule = 0xffffffffu;
     if (R.def_acl == 4) {
       if (stats && o.done < DP_DONE_COUNT) {
         atomicAdd(&stats[o.done], ~0ull);  // -1
@@ -2788,9 +2855,21 @@ __global__ void __launch_bounds__(256) dp_flow_fixup(dpf::FlowCtx fc, const dp_p
       o.done = DP_DONE_ACL_DROPPED;
       o.off = in[R.idx].off;
       o.len = in[R.idx].len;
-      o.meta_flags = R.meta_flags;
+      o.meta_flags = (uint16_t)R.meta_flags;
       o.oif = R.oif;
-      o.fib_entry = R.fib_entry;
+      if (meta) {
+        // PacketMeta as it stood at the ACL
+        dp_pkt_meta_t m = meta[R.idx];
+        m.fib_entry = R.fib_entry;
+        m.dst_vni = R.dst_vni;
+        m.pm_flags &= (uint8_t)~(DP_PM_HAS_VRF | DP_PM_HAS_NH);
+        m.vrf = 0; m.nh_family = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) m.nh_addr[k] = 0;
+        if (R.vrf) { m.pm_flags |= DP_PM_HAS_VRF; m.vrf = R.vrf & 0x7fffffffu; }
+        meta_nh(Img{img_base, *im}, R.nh_ref, m);
+        meta[R.idx] = m;
+      }
     }
     out[R.idx] = o;
   }
@@ -2843,7 +2922,8 @@ static uint16_t *dp_trip_out;  // per packet x 8 stages (dpemu_trips_out)
 #endif
 // Host emulation entry (tests/emu only): runs the per-packet body serially.
 extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
-                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n) {
+                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta,
+                          uint32_t n) {
   thread_local uint8_t slab[SLAB + 16];
   thread_local uint8_t hs[64];
   Img g{img_base, *reinterpret_cast<const Image *>(image_struct)};
@@ -2862,8 +2942,9 @@ extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uin
     int fl0, fl1;
     const bool fit = (in[i].off & 15) + in[i].len <= (uint32_t)WIN && !(in[i].off & 1);
     FlowPk fp;
-    if (fit) process_packet<false>(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, true, nullptr, fp, i);
-    else process_packet<false>(g, slab, hs, buf, buf_bytes, in[i], out[i], fl0, fl1, false, nullptr, fp, i);
+    dp_pkt_meta_t *pm = meta ? meta + i : nullptr;
+    if (fit) process_packet<false>(g, slab, hs, buf, buf_bytes, in[i], out[i], pm, fl0, fl1, true, nullptr, fp, i);
+    else process_packet<false>(g, slab, hs, buf, buf_bytes, in[i], out[i], pm, fl0, fl1, false, nullptr, fp, i);
     if (fl1 > fl0) flush_range(buf + (in[i].off & ~15u), slab, fl0, fl1);
 #ifdef DP_TRIPS
     if (dp_trip_out)
@@ -2888,33 +2969,31 @@ extern "C" int dp_debug_stage_cycles(unsigned long long *out16, int reset) {
 #endif
 // Whole-burst failure: every packet InternalFailure (dpgpu.h conventions).
 __global__ void __launch_bounds__(256) dp_mark_failed(const dp_pkt_in_t *__restrict__ in,
-                                                      dp_pkt_out_t *__restrict__ out, uint32_t n) {
+                                                      dp_pkt_out_t *__restrict__ out,
+                                                      dp_pkt_meta_t *__restrict__ meta, uint32_t n) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  dp_pkt_out_t o{};
-  o.off = in[i].off;
-  o.len = in[i].len;
-  o.done = DP_DONE_INTERNAL_FAILURE;
-  o.fib_entry = 0xffffffffu;
-  o.acl_rule = 0xffffffffu;
-  out[i] = o;
+  out[i] = out_record(in[i].off, in[i].len, DP_DONE_INTERNAL_FAILURE);
+  if (meta) meta[i] = meta_none();
 }
 
-extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, hipStream_t stream) {
+extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
+                               hipStream_t stream) {
   if (n == 0 || !in || !out) return 0;
-  hipLaunchKernelGGL(dp_mark_failed, dim3((n + 255) / 256), dim3(256), 0, stream, in, out, n);
+  hipLaunchKernelGGL(dp_mark_failed, dim3((n + 255) / 256), dim3(256), 0, stream, in, out, meta, n);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
-                                   uint32_t n, uint64_t *stats, uint64_t *stats_part, hipStream_t stream) {
+                                   dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
+                                   hipStream_t stream) {
   if (n == 0) return 0;
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
   hipLaunchKernelGGL(dp_pipeline_kernel<false>, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                     buf_bytes, in, out, n, part, dpf::FlowCtx{});
+                     buf_bytes, in, out, meta, n, part, dpf::FlowCtx{});
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));
@@ -2926,7 +3005,7 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_de
 // memory holding the launch's FlowCtx (device pointers inside).
 extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
-                                         uint32_t n, uint64_t *stats, uint64_t *stats_part,
+                                         dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
                                          const void *fc_host, hipStream_t stream) {
   if (n == 0) return 0;
   const dpf::FlowCtx fc = *reinterpret_cast<const dpf::FlowCtx *>(fc_host);
@@ -2936,12 +3015,12 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
   hipLaunchKernelGGL(dp_pipeline_kernel<true>, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                     buf_bytes, in, out, n, part, fc);
+                     buf_bytes, in, out, meta, n, part, fc);
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));
   const uint32_t fb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
-  hipLaunchKernelGGL(dp_flow_fixup, dim3(fb), dim3(256), 0, stream, fc, in, out,
+  hipLaunchKernelGGL(dp_flow_fixup, dim3(fb), dim3(256), 0, stream, img_base, im, fc, in, out, meta,
                      reinterpret_cast<unsigned long long *>(stats));
   hipLaunchKernelGGL(dp_flow_apply, dim3(fb), dim3(256), 0, stream, fc);
   return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -32,11 +32,13 @@
 
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
-                                   uint32_t n, uint64_t *stats, uint64_t *stats_part, hipStream_t stream);
-extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, hipStream_t stream);
+                                   dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
+                                   hipStream_t stream);
+extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
+                               hipStream_t stream);
 extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
-                                         uint32_t n, uint64_t *stats, uint64_t *stats_part,
+                                         dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
                                          const void *fc_host, hipStream_t stream);
 
 namespace {
@@ -161,6 +163,7 @@ struct dp_ctx {
   uint64_t d_buf_cap = 0;
   dp_pkt_in_t *d_in = nullptr;
   dp_pkt_out_t *d_out = nullptr;
+  dp_pkt_meta_t *d_meta = nullptr;
   uint64_t *d_stats = nullptr;
   uint32_t cap_n = 0;
   hipStream_t hs[kHostStreams] = {};   // host-path copy/compute streams
@@ -174,6 +177,7 @@ struct dp_ctx {
   // dp_process_mbufs: pinned, device-mapped burst records
   dp_pkt_in_t *mb_in = nullptr;
   dp_pkt_out_t *mb_out = nullptr;
+  dp_pkt_meta_t *mb_meta = nullptr;
   uint32_t mb_cap = 0;
   FlowScratch fl_ev, fl_sens;
   hipEvent_t fl_used = nullptr;
@@ -205,16 +209,21 @@ hipEvent_t take_event(dp_ctx *c) {
 
 // Every packet of a failed burst is InternalFailure (dpgpu.h conventions,
 // SURVEY.md §5 failure detection); host arrays.
-void mark_failed_host(const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n) {
-  if (!out) return;
+void mark_failed_host(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n) {
   for (uint32_t i = 0; i < n; i++) {
-    dp_pkt_out_t o{};
-    o.off = in ? in[i].off : 0;
-    o.len = in ? in[i].len : 0;
-    o.done = DP_DONE_INTERNAL_FAILURE;
-    o.fib_entry = 0xffffffffu;
-    o.acl_rule = 0xffffffffu;
-    out[i] = o;
+    if (out) {
+      dp_pkt_out_t o{};
+      o.off = in ? in[i].off : 0;
+      o.len = in ? in[i].len : 0;
+      o.done = DP_DONE_INTERNAL_FAILURE;
+      out[i] = o;
+    }
+    if (meta) {
+      dp_pkt_meta_t m{};
+      m.fib_entry = m.acl_rule = 0xffffffffu;
+      m.flow_ref = DP_FLOW_NONE;
+      meta[i] = m;
+    }
   }
 }
 
@@ -269,11 +278,13 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->d_buf) (void)hipFree(c->d_buf);
   if (c->d_in) (void)hipFree(c->d_in);
   if (c->d_out) (void)hipFree(c->d_out);
+  if (c->d_meta) (void)hipFree(c->d_meta);
   if (c->d_stats) (void)hipFree(c->d_stats);
   c->fl_ev.release();
   c->fl_sens.release();
   if (c->mb_in) (void)hipHostFree(c->mb_in);
   if (c->mb_out) (void)hipHostFree(c->mb_out);
+  if (c->mb_meta) (void)hipHostFree(c->mb_meta);
   if (c->fl_used) (void)hipEventDestroy(c->fl_used);
   for (auto &h : c->hs) if (h) { (void)hipStreamSynchronize(h); (void)hipStreamDestroy(h); }
   for (auto &e : c->hev) if (e) (void)hipEventDestroy(e);
@@ -335,7 +346,7 @@ static std::shared_ptr<DevImage> current(dp_ctx_t *c) {
 }
 
 static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const dp_pkt_in_t *dev_in,
-                        dp_pkt_out_t *dev_out, uint32_t n, uint64_t *dev_stats, uint64_t *dev_flow_refs,
+                        dp_pkt_out_t *dev_out, dp_pkt_meta_t *dev_meta, uint32_t n, uint64_t *dev_stats,
                         void *stream) {
   if (!c) return fail(DP_EINVAL, "null ctx");
   if (n == 0) return 0;
@@ -345,7 +356,7 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
   auto img = current(c);
   if (!dev_buf || ((uintptr_t)dev_buf & 15) || !img) {
     // whole-burst failure: every packet InternalFailure
-    (void)dpk_mark_failed(dev_in, dev_out, n, s);
+    (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
     return !img ? fail(DP_ENOTABLES, "no tables published") : fail(DP_EINVAL, "bad burst buffer");
   }
   uint64_t *part = nullptr;
@@ -374,14 +385,13 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.n = n;
     fc.events = static_cast<uint32_t *>(c->fl_ev.get(sizeof(uint32_t) * (1 + 4 * (uint64_t)n)));
     fc.sens = static_cast<uint32_t *>(c->fl_sens.get(sizeof(uint32_t) * 8 + sizeof(dpf::SensRec) * (uint64_t)n));
-    fc.refs = reinterpret_cast<unsigned long long *>(dev_flow_refs);
     fc.genid = img->im.genid;
     if (!fc.events || !fc.sens) {
-      (void)dpk_mark_failed(dev_in, dev_out, n, s);
+      (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
       return fail(DP_ENOMEM, "flow burst scratch");
     }
-    rc = dpk_launch_pipeline_flows(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out, n,
-                                   dev_stats, part, &fc, s);
+    rc = dpk_launch_pipeline_flows(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out,
+                                   dev_meta, n, dev_stats, part, &fc, s);
     if (!rc) {
       if (!c->fl_used && hipEventCreateWithFlags(&c->fl_used, hipEventDisableTiming) != hipSuccess)
         return fail(DP_EIO, "hipEventCreate");
@@ -390,13 +400,12 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
       if (hipEventRecord(ft->last_burst, s) == hipSuccess) ft->burst_armed = true;
     }
   } else {
-    if (dev_flow_refs) (void)hipMemsetAsync(dev_flow_refs, 0xff, sizeof(uint64_t) * n, s);  // DP_FLOW_NONE
-    rc = dpk_launch_pipeline(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats,
-                             part, s);
+    rc = dpk_launch_pipeline(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out, dev_meta, n,
+                             dev_stats, part, s);
   }
   if (rc) {
     hipError_t e = hipGetLastError();
-    (void)dpk_mark_failed(dev_in, dev_out, n, s);
+    (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
     return fail(DP_EIO, "kernel launch failed", e);
   }
   if (ps) {
@@ -412,15 +421,9 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
 }
 
 int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
-                            const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out, uint32_t n,
-                            uint64_t *dev_stats, void *stream) {
-  return launch_burst(c, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, nullptr, stream);
-}
-
-int dp_process_burst_device_ex(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
-                               const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out, uint32_t n,
-                               uint64_t *dev_stats, uint64_t *dev_flow_refs, void *stream) {
-  return launch_burst(c, dev_buf, buf_bytes, dev_in, dev_out, n, dev_stats, dev_flow_refs, stream);
+                            const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out, dp_pkt_meta_t *dev_meta,
+                            uint32_t n, uint64_t *dev_stats, void *stream) {
+  return launch_burst(c, dev_buf, buf_bytes, dev_in, dev_out, dev_meta, n, dev_stats, stream);
 }
 
 int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
@@ -456,46 +459,47 @@ int dp_ctx_set_option(dp_ctx_t *c, int option, int64_t value) {
 }
 
 int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt_in_t *in,
-                     dp_pkt_out_t *out, uint32_t n, uint64_t *stats) {
+                     dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats) {
   if (!c) return fail(DP_EINVAL, "null ctx");
   if (n == 0) return 0;
   if (!buf || !in || !out) {
-    mark_failed_host(in, out, n);
+    mark_failed_host(in, out, meta, n);
     return fail(DP_EINVAL, "null burst buffers");
   }
   for (uint32_t i = 0; i < n; i++)
     if (in[i].off < DP_HEADROOM || (uint64_t)in[i].off + in[i].len > buf_bytes) {
-      mark_failed_host(in, out, n);
+      mark_failed_host(in, out, meta, n);
       return fail(DP_EINVAL, "frame outside the burst buffer / headroom");
     }
   (void)hipSetDevice(c->device);
   hipError_t e;
   auto bail = [&](int rc, const char *what, hipError_t err) {
-    mark_failed_host(in, out, n);
+    mark_failed_host(in, out, meta, n);
     return fail(rc, what, err);
   };
-  // Zero-copy: when the burst buffer and both record arrays are pinned,
+  // Zero-copy: when the burst buffer and the record arrays are pinned,
   // device-mapped host memory, the kernel reads the frames and records over
-  // PCIe and writes the rewritten header spans and out records back in place
-  // -- only the bytes the path touches cross the link (window chunks in, the
-  // rewritten span and the 32-byte record out), no staging copies.
+  // PCIe and writes the rewritten header spans and records back in place --
+  // only the bytes the path touches cross the link (window chunks in, the
+  // rewritten span and the 16-byte record out), no staging copies.
   if (c->host_path != DP_HOST_COPY) {
     uint64_t end = 0;
     for (uint32_t i = 0; i < n; i++) end = std::max<uint64_t>(end, ((uint64_t)in[i].off + in[i].len + 15) & ~15ull);
     uint8_t *db = static_cast<uint8_t *>(mapped_ptr(buf));
     const dp_pkt_in_t *din = static_cast<const dp_pkt_in_t *>(mapped_ptr(in));
     dp_pkt_out_t *dout = static_cast<dp_pkt_out_t *>(mapped_ptr(out));
-    const bool zc = db && din && dout && !((uintptr_t)db & 15) && end <= buf_bytes;
+    dp_pkt_meta_t *dmeta = meta ? static_cast<dp_pkt_meta_t *>(mapped_ptr(meta)) : nullptr;
+    const bool zc = db && din && dout && (!meta || dmeta) && !((uintptr_t)db & 15) && end <= buf_bytes;
     if (zc) {
       hipStream_t s = c->stream;
       if (stats && (e = hipMemsetAsync(c->d_stats, 0, sizeof(uint64_t) * DP_DONE_COUNT, s)) != hipSuccess)
         return bail(DP_EIO, "memset stats", e);
-      int rc = dp_process_burst_device(c, db, buf_bytes, din, dout, n, stats ? c->d_stats : nullptr, s);
+      int rc = dp_process_burst_device(c, db, buf_bytes, din, dout, dmeta, n, stats ? c->d_stats : nullptr, s);
       uint64_t hstats[DP_DONE_COUNT];
       if (!rc && stats && (e = hipMemcpyAsync(hstats, c->d_stats, sizeof(hstats), hipMemcpyDeviceToHost, s)) != hipSuccess)
         rc = fail(DP_EIO, "D2H stats", e);
       if ((e = hipStreamSynchronize(s)) != hipSuccess && !rc) rc = fail(DP_EIO, "stream sync", e);
-      if (rc) { mark_failed_host(in, out, n); return rc; }
+      if (rc) { mark_failed_host(in, out, meta, n); return rc; }
       if (stats) for (int k = 0; k < DP_DONE_COUNT; k++) stats[k] += hstats[k];
       return 0;
     }
@@ -512,11 +516,14 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     (void)hipStreamSynchronize(c->stream);
     if (c->d_in) (void)hipFree(c->d_in);
     if (c->d_out) (void)hipFree(c->d_out);
-    c->d_in = nullptr; c->d_out = nullptr; c->cap_n = 0;
+    if (c->d_meta) (void)hipFree(c->d_meta);
+    c->d_in = nullptr; c->d_out = nullptr; c->d_meta = nullptr; c->cap_n = 0;
     if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess) return bail(DP_ENOMEM, "hipMalloc in", e);
     if ((e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess) return bail(DP_ENOMEM, "hipMalloc out", e);
+    if ((e = hipMalloc(&c->d_meta, sizeof(dp_pkt_meta_t) * n)) != hipSuccess) return bail(DP_ENOMEM, "hipMalloc meta", e);
     c->cap_n = n;
   }
+  dp_pkt_meta_t *dm = meta ? c->d_meta : nullptr;
   hipStream_t s = c->stream;
   // packets in buffer order with disjoint slots: chunked, overlapped copies
   // of each chunk's own byte span; anything else: one whole-buffer copy
@@ -539,15 +546,17 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     return bail(DP_EIO, "memset stats", e);
   if (nch == 1) {
     if ((e = hipMemcpyAsync(c->d_buf, buf, buf_bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D burst", e);
-    if ((e = hipMemcpyAsync(c->d_in, in, sizeof(dp_pkt_in_t) * n, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D meta", e);
-    int rc = dp_process_burst_device(c, c->d_buf, need, c->d_in, c->d_out, n, stats ? c->d_stats : nullptr, s);
+    if ((e = hipMemcpyAsync(c->d_in, in, sizeof(dp_pkt_in_t) * n, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D records", e);
+    int rc = dp_process_burst_device(c, c->d_buf, need, c->d_in, c->d_out, dm, n, stats ? c->d_stats : nullptr, s);
     if (rc) {
       (void)hipStreamSynchronize(s);
-      mark_failed_host(in, out, n);
+      mark_failed_host(in, out, meta, n);
       return rc;
     }
     if ((e = hipMemcpyAsync(buf, c->d_buf, buf_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H burst", e);
-    if ((e = hipMemcpyAsync(out, c->d_out, sizeof(dp_pkt_out_t) * n, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H meta", e);
+    if ((e = hipMemcpyAsync(out, c->d_out, sizeof(dp_pkt_out_t) * n, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H records", e);
+    if (meta && (e = hipMemcpyAsync(meta, dm, sizeof(dp_pkt_meta_t) * n, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return bail(DP_EIO, "D2H meta", e);
   } else {
     // every host stream starts after the context stream's prior work (and
     // the stats clear); the context stream then waits for all of them
@@ -569,11 +578,12 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
         rc = fail(DP_EIO, "H2D chunk", e);
         break;
       }
-      if ((rc = dp_process_burst_device(c, c->d_buf, need, c->d_in + first, c->d_out + first, cnt,
-                                        stats ? c->d_stats : nullptr, hs)))
+      if ((rc = dp_process_burst_device(c, c->d_buf, need, c->d_in + first, c->d_out + first, dm ? dm + first : nullptr,
+                                        cnt, stats ? c->d_stats : nullptr, hs)))
         break;
       if ((e = hipMemcpyAsync(buf + lo, c->d_buf + lo, hi - lo, hipMemcpyDeviceToHost, hs)) != hipSuccess ||
-          (e = hipMemcpyAsync(out + first, c->d_out + first, sizeof(dp_pkt_out_t) * cnt, hipMemcpyDeviceToHost, hs)) != hipSuccess) {
+          (e = hipMemcpyAsync(out + first, c->d_out + first, sizeof(dp_pkt_out_t) * cnt, hipMemcpyDeviceToHost, hs)) != hipSuccess ||
+          (meta && (e = hipMemcpyAsync(meta + first, dm + first, sizeof(dp_pkt_meta_t) * cnt, hipMemcpyDeviceToHost, hs)) != hipSuccess)) {
         rc = fail(DP_EIO, "D2H chunk", e);
         break;
       }
@@ -584,7 +594,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     }
     if (rc) {
       (void)hipStreamSynchronize(s);
-      mark_failed_host(in, out, n);
+      mark_failed_host(in, out, meta, n);
       return rc;
     }
   }
@@ -596,25 +606,26 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
 }
 
 int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf, uint64_t buf_bytes,
-                             const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, uint64_t *stats) {
-  if (!ctxs || n_ctx == 0) { mark_failed_host(in, out, n); return fail(DP_EINVAL, "no contexts"); }
+                             const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
+                             uint64_t *stats) {
+  if (!ctxs || n_ctx == 0) { mark_failed_host(in, out, meta, n); return fail(DP_EINVAL, "no contexts"); }
   if (n == 0) return 0;
-  if (!buf || !in || !out) { mark_failed_host(in, out, n); return fail(DP_EINVAL, "null burst buffers"); }
+  if (!buf || !in || !out) { mark_failed_host(in, out, meta, n); return fail(DP_EINVAL, "null burst buffers"); }
   // packets in buffer order, each owning [off - DP_HEADROOM, off + len): the
   // shards' byte spans are then disjoint and can be copied back concurrently
   for (uint32_t i = 0; i < n; i++) {
     const bool inside = in[i].off >= DP_HEADROOM && (uint64_t)in[i].off + in[i].len <= buf_bytes;
     const bool ordered = i == 0 || in[i].off - DP_HEADROOM >= (uint64_t)in[i - 1].off + in[i - 1].len;
     if (!inside || !ordered) {
-      mark_failed_host(in, out, n);
+      mark_failed_host(in, out, meta, n);
       return fail(DP_EINVAL, "sharded bursts need in-order, non-overlapping packet slots");
     }
   }
   for (uint32_t k = 0; k < n_ctx; k++) {
-    if (!ctxs[k]) { mark_failed_host(in, out, n); return fail(DP_EINVAL, "null context"); }
+    if (!ctxs[k]) { mark_failed_host(in, out, meta, n); return fail(DP_EINVAL, "null context"); }
     // one flow table per device cannot give the shards the reference's
     // shared Arc<FlowTable> (flows shard by 5-tuple hash)
-    if (ctxs[k]->ft) { mark_failed_host(in, out, n); return fail(DP_ENOTSUP, "sharded bursts with a flow table"); }
+    if (ctxs[k]->ft) { mark_failed_host(in, out, meta, n); return fail(DP_ENOTSUP, "sharded bursts with a flow table"); }
   }
   struct Shard {
     uint32_t first, cnt;
@@ -659,25 +670,29 @@ int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf
       (void)hipStreamSynchronize(c->stream);
       if (c->d_in) (void)hipFree(c->d_in);
       if (c->d_out) (void)hipFree(c->d_out);
-      c->d_in = nullptr; c->d_out = nullptr; c->cap_n = 0;
+      if (c->d_meta) (void)hipFree(c->d_meta);
+      c->d_in = nullptr; c->d_out = nullptr; c->d_meta = nullptr; c->cap_n = 0;
       if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * S.cnt)) != hipSuccess ||
-          (e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * S.cnt)) != hipSuccess) {
+          (e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * S.cnt)) != hipSuccess ||
+          (e = hipMalloc(&c->d_meta, sizeof(dp_pkt_meta_t) * S.cnt)) != hipSuccess) {
         rc = fail(DP_ENOMEM, "hipMalloc shard records", e);
         break;
       }
       c->cap_n = S.cnt;
     }
     hipStream_t s = c->stream;
+    dp_pkt_meta_t *dm = meta ? c->d_meta : nullptr;
     if ((e = hipMemcpyAsync(c->d_buf, buf + S.lo, bytes, hipMemcpyHostToDevice, s)) != hipSuccess ||
         (e = hipMemcpyAsync(c->d_in, S.rin.data(), sizeof(dp_pkt_in_t) * S.cnt, hipMemcpyHostToDevice, s)) != hipSuccess ||
         (stats && (e = hipMemsetAsync(c->d_stats, 0, sizeof(uint64_t) * DP_DONE_COUNT, s)) != hipSuccess)) {
       rc = fail(DP_EIO, "H2D shard", e);
       break;
     }
-    if ((rc = dp_process_burst_device(c, c->d_buf, need, c->d_in, c->d_out, S.cnt, stats ? c->d_stats : nullptr, s)))
+    if ((rc = dp_process_burst_device(c, c->d_buf, need, c->d_in, c->d_out, dm, S.cnt, stats ? c->d_stats : nullptr, s)))
       break;
     if ((e = hipMemcpyAsync(buf + S.lo, c->d_buf, bytes, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipMemcpyAsync(out + S.first, c->d_out, sizeof(dp_pkt_out_t) * S.cnt, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (meta && (e = hipMemcpyAsync(meta + S.first, dm, sizeof(dp_pkt_meta_t) * S.cnt, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
         (stats && (e = hipMemcpyAsync(S.st, c->d_stats, sizeof(S.st), hipMemcpyDeviceToHost, s)) != hipSuccess)) {
       rc = fail(DP_EIO, "D2H shard", e);
       break;
@@ -690,7 +705,7 @@ int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf
     hipError_t e = hipStreamSynchronize(ctxs[k]->stream);
     if (e != hipSuccess && !rc) rc = fail(DP_EIO, "shard stream sync", e);
   }
-  if (rc) { mark_failed_host(in, out, n); return rc; }
+  if (rc) { mark_failed_host(in, out, meta, n); return rc; }
   for (uint32_t k = 0; k < n_ctx; k++) {
     Shard &S = sh[k];
     for (uint32_t i = 0; i < S.cnt; i++) out[S.first + i].off += (uint32_t)S.lo;
@@ -714,46 +729,54 @@ int dp_ctx_synchronize(dp_ctx_t *c) {
 // context's own pinned arrays.
 int dp_process_mbufs(dp_ctx_t *c, const void *pool_base, uint64_t pool_bytes, void *const *mbufs, uint32_t n,
                      const dp_mbuf_layout_t *layout, const uint32_t *port_ifindex, uint32_t n_ports,
-                     dp_pkt_out_t *out, uint64_t *stats) {
+                     dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint64_t *stats) {
   if (!c) return fail(DP_EINVAL, "null ctx");
   if (n == 0) return 0;
   if (!out || !mbufs || !layout || !pool_base) {
-    mark_failed_host(nullptr, out, n);
+    mark_failed_host(nullptr, out, meta, n);
     return fail(DP_EINVAL, "null argument");
   }
   (void)hipSetDevice(c->device);
   if (n > c->mb_cap) {
     if (c->mb_in) (void)hipHostFree(c->mb_in);
     if (c->mb_out) (void)hipHostFree(c->mb_out);
+    if (c->mb_meta) (void)hipHostFree(c->mb_meta);
     c->mb_in = nullptr;
     c->mb_out = nullptr;
+    c->mb_meta = nullptr;
     c->mb_cap = 0;
     hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&c->mb_in), sizeof(dp_pkt_in_t) * n, hipHostMallocMapped);
     if (e == hipSuccess)
       e = hipHostMalloc(reinterpret_cast<void **>(&c->mb_out), sizeof(dp_pkt_out_t) * n, hipHostMallocMapped);
+    if (e == hipSuccess)
+      e = hipHostMalloc(reinterpret_cast<void **>(&c->mb_meta), sizeof(dp_pkt_meta_t) * n, hipHostMallocMapped);
     if (e != hipSuccess) {
-      mark_failed_host(nullptr, out, n);
+      mark_failed_host(nullptr, out, meta, n);
       return fail(DP_ENOMEM, "pinned mbuf burst records", e);
     }
     c->mb_cap = n;
   }
   std::vector<dp_pkt_in_t> rin(n);
   int rc = dp_mbuf_burst_in(pool_base, pool_bytes, mbufs, n, layout, port_ifindex, n_ports, rin.data());
-  if (rc) { mark_failed_host(nullptr, out, n); return fail(rc, "mbuf burst records"); }
+  if (rc) { mark_failed_host(nullptr, out, meta, n); return fail(rc, "mbuf burst records"); }
   // an mbuf outside the layout contract is InternalFailure on its own; the
   // others run as one burst
   std::vector<uint32_t> idx;
   idx.reserve(n);
   for (uint32_t i = 0; i < n; i++)
     if (rin[i].off >= DP_HEADROOM) { c->mb_in[idx.size()] = rin[i]; idx.push_back(i); }
-  mark_failed_host(rin.data(), out, n);
+  mark_failed_host(rin.data(), out, meta, n);
   const int mode = c->host_path;
   c->host_path = DP_HOST_ZERO_COPY;
   rc = idx.empty() ? 0 : dp_process_burst(c, const_cast<uint8_t *>(static_cast<const uint8_t *>(pool_base)),
-                                          pool_bytes, c->mb_in, c->mb_out, (uint32_t)idx.size(), stats);
+                                          pool_bytes, c->mb_in, c->mb_out, meta ? c->mb_meta : nullptr,
+                                          (uint32_t)idx.size(), stats);
   c->host_path = mode;
   if (rc) return rc;  // every out[i] InternalFailure
-  for (size_t j = 0; j < idx.size(); j++) out[idx[j]] = c->mb_out[j];
+  for (size_t j = 0; j < idx.size(); j++) {
+    out[idx[j]] = c->mb_out[j];
+    if (meta) meta[idx[j]] = c->mb_meta[j];
+  }
   if (stats) stats[DP_DONE_INTERNAL_FAILURE] += n - idx.size();
   rc = dp_mbuf_burst_out(mbufs, n, layout, rin.data(), out);
   return rc ? fail(rc, "mbuf burst results") : 0;

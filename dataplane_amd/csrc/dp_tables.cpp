@@ -23,6 +23,7 @@
 #include <functional>
 #include <map>
 #include <set>
+#include <cstdio>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -341,6 +342,7 @@ constexpr double kListMean = DP_LIST_MEAN;
 // (<= DPD_RUN_MAX); 0 (the default): the limits above.
 // forms chosen by the most recent build on this thread (test introspection)
 thread_local uint32_t g_forms[2];
+thread_local std::string g_group_stats;  // per-group list statistics (dpd_debug_group_stats)
 std::atomic<int> g_cls_form{0};
 
 int cls_form_override() { return g_cls_form.load(std::memory_order_relaxed); }
@@ -435,6 +437,12 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
       }
       lmean[f] = (double)tot / (double)m;
     }
+    {
+      char line[256];
+      snprintf(line, sizeof line, "kind %d fam %d rules %u lmax %u %u %u %u lmean %.2f %.2f %.2f %.2f\n", kind, fam, n,
+               lmax[0], lmax[1], lmax[2], lmax[3], lmean[0], lmean[1], lmean[2], lmean[3]);
+      g_group_stats += line;
+    }
     int lf = -1;
     const int form = cls_form_override();
     for (int f = 0; f < 4 && form != 1; f++) {
@@ -446,12 +454,14 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
       // precedence order, stored inline (identical lists shared)
       G.mode = DPD_GROUP_LIST;
       G.lfield = (uint32_t)lf;
+      G.lfield2 = DPD_NO_FIELD;
       std::map<std::vector<uint32_t>, uint32_t> runs;
-      std::vector<uint32_t> leaf;
+      // runs of field `fi`'s intervals -> index leaves
+      auto list_leaves = [&](int fi, std::vector<uint32_t> &leaf) -> bool {
       std::set<uint32_t> cur;
-      for (size_t k = 0; k < bnd[lf].size(); k++) {
-        for (uint32_t j : dels[lf][k]) cur.erase(j);
-        for (uint32_t j : adds[lf][k]) cur.insert(j);
+      for (size_t k = 0; k < bnd[fi].size(); k++) {
+        for (uint32_t j : dels[fi][k]) cur.erase(j);
+        for (uint32_t j : adds[fi][k]) cur.insert(j);
         std::vector<uint32_t> lst(cur.begin(), cur.end());
         auto it = runs.find(lst);
         if (it == runs.end()) {
@@ -472,12 +482,30 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
             rec_rule.push_back({recs.size(), &r});
             recs.push_back(c);
           }
-          if (recs.size() >= (1u << (31 - DPD_RUN_BITS))) return Classifier{};  // unreachable sizes
+          if (recs.size() >= (1u << (31 - DPD_RUN_BITS))) return false;  // unreachable sizes
           it = runs.emplace(lst, (first << DPD_RUN_BITS) | (uint32_t)lst.size()).first;
         }
         leaf.push_back(it->second);
       }
+      return true;
+      };
+      std::vector<uint32_t> leaf;
+      if (!list_leaves(lf, leaf)) return Classifier{};
       build_field_index(ib, G.f[lf], lf, fam, groups.size(), bnd[lf], leaf);
+      // v4 ACL groups: a second list index over another field whose runs fit
+      // (the lookup verifies the shorter of the two runs a packet selects:
+      // both hold every rule that can match it, in precedence order)
+      int lf2 = -1;
+      if (kind == 0 && fam == 4 && form != 2)
+        for (int f = 0; f < 4; f++)
+          if (f != lf && lmax[f] <= DPD_RUN_MAX && bnd[f].size() > 16 && (lf2 < 0 || lmean[f] < lmean[lf2]))
+            lf2 = f;
+      if (lf2 >= 0) {
+        std::vector<uint32_t> leaf2;
+        if (!list_leaves(lf2, leaf2)) return Classifier{};
+        build_field_index(ib, G.f[lf2], lf2, fam, groups.size(), bnd[lf2], leaf2);
+        G.lfield2 = (uint32_t)lf2;
+      }
       grecs.push_back(G);
       g_forms[1]++;
       continue;
@@ -592,6 +620,7 @@ int load_rules(const dp_rule_t *rs, uint32_t n, int fam, bool by_prio, int kind,
 
 int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
   g_forms[0] = g_forms[1] = 0;
+  g_group_stats.clear();
   if (!d || d->abi_version != DPGPU_ABI_VERSION) return DP_EINVAL;
   ImgBuf ib;
   ib.alloc(64);  // offset 0 is never a valid structure
@@ -1037,13 +1066,27 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     memcpy(&G, ib.b.data() + C.group_recs + (uint64_t)gi * sizeof(Group), sizeof(Group));
     if (G.mode != DPD_GROUP_LIST || !G.f[G.lfield].root) return m;
     const FieldIdx &F = G.f[G.lfield];
-    m.root = F.root; m.blocks = F.blocks; m.s0 = F.s0; m.kbits = F.kbits; m.field = (uint8_t)G.lfield;
+    m.root = (uint32_t)F.root; m.blocks = (uint32_t)F.blocks; m.s0 = F.s0; m.kbits = F.kbits;
+    m.field = (uint8_t)G.lfield;
+    return m;
+  };
+  // the second list index of a v4 ACL group (Group.lfield2)
+  auto cls_mbi2 = [&](const Classifier &C, int32_t gi) {
+    Mbi m{};
+    if (gi < 0) return m;
+    Group G;
+    memcpy(&G, ib.b.data() + C.group_recs + (uint64_t)gi * sizeof(Group), sizeof(Group));
+    if (G.mode != DPD_GROUP_LIST || !G.f[G.lfield].root || G.lfield2 == DPD_NO_FIELD || !G.f[G.lfield2].root)
+      return m;
+    const FieldIdx &F = G.f[G.lfield2];
+    m.root = (uint32_t)F.root; m.blocks = (uint32_t)F.blocks; m.s0 = F.s0; m.kbits = F.kbits;
+    m.field = (uint8_t)G.lfield2;
     return m;
   };
   auto nat_mbi = [&](int32_t ti) {
     Mbi m{};
     if (ti < 0 || !ntabs[ti].root || ntabs[ti].n == 0) return m;
-    m.root = ntabs[ti].root; m.blocks = ntabs[ti].blocks; m.s0 = ntabs[ti].s0; m.kbits = 32;
+    m.root = (uint32_t)ntabs[ti].root; m.blocks = (uint32_t)ntabs[ti].blocks; m.s0 = ntabs[ti].s0; m.kbits = 32;
     return m;
   };
   std::vector<VniRec> vrecs;
@@ -1100,6 +1143,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
     r.dst_vni = dv;
     r.ffl4 = cls_mbi(im.ff_local[0], r.ffl[0]);
     r.acl4 = cls_mbi(im.acl[0], r.acl[0]);
+    r.acl4b = cls_mbi2(im.acl[0], r.acl[0]);
     r.nsrc = nat_mbi(r.nat_src);
     if (r.dst_fib >= 0) { r.lpm4_direct = fibs[r.dst_fib].v4.direct; r.lpm4_dbits = fibs[r.dst_fib].v4.dbits;
                           r.lpm4_blocks = fibs[r.dst_fib].v4.blocks; }
@@ -1131,6 +1175,8 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
 
   ib.alloc(64);
   im.bytes = ib.b.size();
+  // context records carry 32-bit image offsets (Mbi)
+  if (im.bytes >= (1ull << 32)) return DP_ENOMEM;
   out.bytes.swap(ib.b);
   out.im = im;
   out.pt_nodes = pb.nodes.size();
@@ -1146,6 +1192,8 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
 extern "C" void dpd_debug_set_classifier_form(int form) {
   dpd::g_cls_form.store(form >= 0 && form <= 2 ? form : 0, std::memory_order_relaxed);
 }
+
+extern "C" const char *dpd_debug_group_stats(void) { return dpd::g_group_stats.c_str(); }
 
 extern "C" void dpd_debug_classifier_forms(uint32_t out[2]) {
   out[0] = dpd::g_forms[0];

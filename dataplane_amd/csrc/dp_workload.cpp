@@ -681,7 +681,8 @@ extern "C" uint32_t dpw_sizeof(const char *name) {
       {"dp_nat_table_t", sizeof(dp_nat_table_t)}, {"dp_nat_entry_t", sizeof(dp_nat_entry_t)},
       {"dp_port_range_t", sizeof(dp_port_range_t)}, {"dp_nat_range_t", sizeof(dp_nat_range_t)},
       {"dp_tables_desc_t", sizeof(dp_tables_desc_t)}, {"dp_pkt_in_t", sizeof(dp_pkt_in_t)},
-      {"dp_pkt_out_t", sizeof(dp_pkt_out_t)}, {"dp_flow_key_t", sizeof(dp_flow_key_t)},
+      {"dp_pkt_out_t", sizeof(dp_pkt_out_t)}, {"dp_pkt_meta_t", sizeof(dp_pkt_meta_t)},
+      {"dp_flow_key_t", sizeof(dp_flow_key_t)},
       {"dp_flow_t", sizeof(dp_flow_t)}, {"dp_flow_info_t", sizeof(dp_flow_info_t)},
       {"dp_mbuf_layout_t", sizeof(dp_mbuf_layout_t)},
   };

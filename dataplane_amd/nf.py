@@ -45,6 +45,11 @@ class Packet:
     dst_vni: Optional[int] = None
     fib_entry: Optional[int] = None
     acl_rule: Optional[int] = None
+    vrf: Optional[int] = None           # PacketMeta.vrf
+    nh_addr: Optional[str] = None       # PacketMeta.nh_addr (next-hop IP, text form)
+    dscp: Optional[int] = None          # PacketMeta.dscp / .ecn (set by the path when known)
+    ecn: Optional[int] = None
+    flow_ref: int = 0                   # the packet's attached flow (meta.flow_info), 0 = none
 
     def is_done(self) -> bool:
         return self.done is not None
@@ -98,6 +103,12 @@ class GpuPathNf:
             p.dst_vni = int(r["dst_vni"]) or None
             p.fib_entry = None if r["fib_entry"] == 0xFFFFFFFF else int(r["fib_entry"])
             p.acl_rule = None if r["acl_rule"] == 0xFFFFFFFF else int(r["acl_rule"])
+            pm = int(r["pm_flags"])
+            p.vrf = int(r["vrf"]) if pm & A.PM_HAS_VRF else None
+            p.nh_addr = A.nh_text(r) if pm & A.PM_HAS_NH else None
+            p.dscp = int(r["dscp"]) if pm & A.PM_HAS_DSCP else None
+            p.ecn = int(r["ecn"]) if pm & A.PM_HAS_DSCP else None
+            p.flow_ref = int(r["flow_ref"])
             if d == A.DONE["Delivered"]:
                 p.frame = bytes(buf[r["off"]:r["off"] + r["len"]])
         return iter(burst)
@@ -109,15 +120,22 @@ class GpuPathNf:
 
     def process_arrays(self, buf: np.ndarray, inp: np.ndarray,
                        stats: Optional[np.ndarray] = None,
-                       out: Optional[np.ndarray] = None) -> np.ndarray:
-        """Host-origin burst, in place (dp_process_burst)."""
+                       out: Optional[np.ndarray] = None,
+                       meta: Optional[np.ndarray] = None, with_meta: bool = True) -> np.ndarray:
+        """Host-origin burst, in place (dp_process_burst).  Returns PKT_RES
+        records (dp_pkt_out_t + dp_pkt_meta_t) -- or, with with_meta=False,
+        the dp_pkt_out_t array alone (no meta array passed to the path)."""
         if out is None:
             out = np.zeros(len(inp), dtype=A.PKT_OUT)
+        if meta is None and with_meta:
+            meta = np.zeros(len(inp), dtype=A.PKT_META)
         sp = stats.ctypes.data if stats is not None else None
         A.check(self.lib.dp_process_burst(self.ctx, buf.ctypes.data, buf.nbytes, inp.ctypes.data,
-                                          out.ctypes.data, len(inp), sp),
+                                          out.ctypes.data,
+                                          meta.ctypes.data if meta is not None else None,
+                                          len(inp), sp),
                 "dp_process_burst", self.lib)
-        return out
+        return A.join_results(out, meta) if meta is not None else out
 
     def attach_flows(self, flow_table) -> None:
         """FlowLookup::new(name, flow_table) (flow-entry/src/flow_table/nf_lookup.rs:24-32):
@@ -125,14 +143,6 @@ class GpuPathNf:
         None detaches it (an empty flow table)."""
         A.check(self.lib.dp_ctx_attach_flow_table(self.ctx, flow_table.h if flow_table else None),
                 "dp_ctx_attach_flow_table", self.lib)
-
-    def process_device_ex(self, dev_buf: int, buf_bytes: int, dev_in: int, dev_out: int, n: int,
-                          dev_stats: Optional[int] = None, dev_flow_refs: Optional[int] = None,
-                          stream: Optional[int] = None) -> None:
-        """dp_process_burst_device_ex: also each packet's attached flow (a ref)."""
-        A.check(self.lib.dp_process_burst_device_ex(self.ctx, dev_buf, buf_bytes, dev_in, dev_out,
-                                                    n, dev_stats, dev_flow_refs, stream),
-                "dp_process_burst_device_ex", self.lib)
 
     def process_mbufs(self, pool_base: int, pool_bytes: int, mbufs: np.ndarray,
                       port_ifindex: Optional[np.ndarray] = None,
@@ -142,20 +152,24 @@ class GpuPathNf:
         delivered mbufs hold their serialized frames, ready for tx."""
         mbufs = np.ascontiguousarray(mbufs, dtype=np.uint64)
         out = np.zeros(len(mbufs), dtype=A.PKT_OUT)
+        meta = np.zeros(len(mbufs), dtype=A.PKT_META)
         pif = None if port_ifindex is None else np.ascontiguousarray(port_ifindex, dtype=np.uint32)
         A.check(self.lib.dp_process_mbufs(self.ctx, pool_base, pool_bytes, mbufs.ctypes.data,
                                           len(mbufs), C.byref(layout or A.MBUF_LAYOUT_DPDK),
                                           pif.ctypes.data if pif is not None else None,
                                           len(pif) if pif is not None else 0, out.ctypes.data,
+                                          meta.ctypes.data,
                                           stats.ctypes.data if stats is not None else None),
                 "dp_process_mbufs", self.lib)
-        return out
+        return A.join_results(out, meta)
 
     def process_device(self, dev_buf: int, buf_bytes: int, dev_in: int, dev_out: int, n: int,
-                       dev_stats: Optional[int] = None, stream: Optional[int] = None) -> None:
-        """Device-resident burst (dp_process_burst_device): raw device pointers."""
+                       dev_stats: Optional[int] = None, stream: Optional[int] = None,
+                       dev_meta: Optional[int] = None) -> None:
+        """Device-resident burst (dp_process_burst_device): raw device pointers;
+        dev_meta (dp_pkt_meta_t[n]) is optional."""
         A.check(self.lib.dp_process_burst_device(self.ctx, dev_buf, buf_bytes, dev_in, dev_out,
-                                                 n, dev_stats, stream),
+                                                 dev_meta, n, dev_stats, stream),
                 "dp_process_burst_device", self.lib)
 
     @staticmethod
@@ -165,13 +179,15 @@ class GpuPathNf:
         (dp_process_burst_sharded): contiguous shards of whole packets, one
         per context, copied and processed concurrently."""
         out = np.zeros(len(inp), dtype=A.PKT_OUT)
+        meta = np.zeros(len(inp), dtype=A.PKT_META)
         ctxs = (C.c_void_p * len(nfs))(*[nf.ctx for nf in nfs])
         lib = nfs[0].lib
         sp = stats.ctypes.data if stats is not None else None
         A.check(lib.dp_process_burst_sharded(ctxs, len(nfs), buf.ctypes.data, buf.nbytes,
-                                             inp.ctypes.data, out.ctypes.data, len(inp), sp),
+                                             inp.ctypes.data, out.ctypes.data, meta.ctypes.data,
+                                             len(inp), sp),
                 "dp_process_burst_sharded", lib)
-        return out
+        return A.join_results(out, meta)
 
     def synchronize(self) -> None:
         A.check(self.lib.dp_ctx_synchronize(self.ctx), "dp_ctx_synchronize", self.lib)

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DPGPU_ABI_VERSION 1u
+#define DPGPU_ABI_VERSION 2u
 
 /* Bytes every frame must have in front of it (its own scratch, owned by the
  * packet).  Output headers are written in place into this headroom: VXLAN
@@ -138,6 +138,7 @@ typedef struct dp_pkt_in {
     uint32_t src_vni;  /* only with DP_IN_SEEDED_OVERLAY */
 } dp_pkt_in_t;
 
+/* What the driver needs to transmit or drop a packet (16 B, always written). */
 typedef struct dp_pkt_out {
     uint32_t off;        /* serialized frame start (only valid if Delivered) */
     uint16_t len;        /* serialized frame length (only valid if Delivered) */
@@ -146,13 +147,34 @@ typedef struct dp_pkt_out {
                             3: allow (peering default), 4: deny (peering default),
                             5: allow (no ACL for peering), 6: allow (reply of a
                             flow a Flow-scope rule allowed; acl_rule = that rule) */
-    uint32_t meta_flags; /* enum dp_meta_flag */
     uint32_t oif;        /* PacketMeta.oif (0 if None) */
+    uint16_t meta_flags; /* enum dp_meta_flag (MetaFlags, 11 bits) */
+    uint16_t pad;
+} dp_pkt_out_t;
+
+/* dp_pkt_meta_t.pm_flags: which Option<> fields of PacketMeta are Some */
+enum dp_pm_flag {
+    DP_PM_HAS_VRF = 1u << 0,   /* vrf */
+    DP_PM_HAS_NH = 1u << 1,    /* nh_addr */
+    DP_PM_HAS_DSCP = 1u << 2   /* dscp and ecn (set together, ipforward.rs:143-148) */
+};
+
+/* The rest of PacketMeta (net/src/packet/meta.rs:138-154), 48 B, written
+ * only when the caller passes a meta array: the fields a CPU stage kept
+ * after the GPU block (PacketStatsNF, per-VPC stats, a dumper) would read. */
+typedef struct dp_pkt_meta {
     uint32_t dst_vni;    /* PacketMeta.dst_vpcd VNI (0 if None) */
     uint32_t src_vni;    /* PacketMeta.src_vpcd VNI (0 if None) */
     uint32_t fib_entry;  /* index of the last FibEntry executed (UINT32_MAX: none) */
     uint32_t acl_rule;   /* index of the matching ACL rule in its table (UINT32_MAX: none) */
-} dp_pkt_out_t;
+    uint32_t vrf;        /* PacketMeta.vrf (DP_PM_HAS_VRF) */
+    uint8_t pm_flags;    /* enum dp_pm_flag */
+    uint8_t dscp;        /* PacketMeta.dscp (DP_PM_HAS_DSCP) */
+    uint8_t ecn;         /* PacketMeta.ecn (DP_PM_HAS_DSCP) */
+    uint8_t nh_family;   /* 4 / 6 (DP_PM_HAS_NH) */
+    uint8_t nh_addr[16]; /* PacketMeta.nh_addr, network order (v4: first 4 bytes) */
+    uint64_t flow_ref;   /* PacketMeta.flow_info as a flow-table ref (DP_FLOW_NONE: None) */
+} dp_pkt_meta_t;
 
 /* ------------------------------------------------------------------------ */
 /* Table descriptors: host arrays lowered from the reference's structures.  */
@@ -412,13 +434,14 @@ int64_t dp_tables_genid(const dp_ctx_t *ctx);
 /* Host-origin burst: `buf` is caller-owned (pinned for best speed) host
  * memory holding every frame at in[i].off with DP_HEADROOM bytes in front.
  * Frames are rewritten in place; out[i] tells where each serialized frame
- * now starts.  Synchronous.  `stats` (may be NULL) receives DP_DONE_COUNT
+ * now starts; `meta` (may be NULL) receives the rest of each PacketMeta.
+ * Synchronous.  `stats` (may be NULL) receives DP_DONE_COUNT
  * counters (PacketStatsNF, pipeline/src/sample_nfs.rs:225-273).  On any
  * error (layout violation, HIP failure) every out[i] is
  * DP_DONE_INTERNAL_FAILURE and the negative status is returned. */
 int dp_process_burst(dp_ctx_t *ctx, uint8_t *buf, uint64_t buf_bytes,
-                     const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
-                     uint64_t *stats);
+                     const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta,
+                     uint32_t n, uint64_t *stats);
 
 /* Device-resident burst: every pointer is device memory; enqueued on
  * `stream` (a hipStream_t; NULL = the context's stream).  Asynchronous.
@@ -428,11 +451,14 @@ int dp_process_burst(dp_ctx_t *ctx, uint8_t *buf, uint64_t buf_bytes,
  * without touching memory, and a burst that cannot run at all (no tables,
  * misaligned buffer, launch failure) has every dev_out[i] marked
  * DP_DONE_INTERNAL_FAILURE on `stream` besides the negative status.
+ * `dev_meta` (may be NULL: the bench path writes only the 16-byte out
+ * records) receives the rest of each PacketMeta, flow_info included.
  * `dev_stats` (may be NULL) is accumulated into (DP_DONE_COUNT u64).
  * Bursts of one context may run concurrently on different streams. */
 int dp_process_burst_device(dp_ctx_t *ctx, uint8_t *dev_buf, uint64_t buf_bytes,
                             const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out,
-                            uint32_t n, uint64_t *dev_stats, void *stream);
+                            dp_pkt_meta_t *dev_meta, uint32_t n, uint64_t *dev_stats,
+                            void *stream);
 
 /* Multi-GPU, host-origin burst: `ctxs` holds one
  * context per device (created by the caller, e.g. one per GPU of the node).
@@ -449,7 +475,7 @@ int dp_process_burst_device(dp_ctx_t *ctx, uint8_t *dev_buf, uint64_t buf_bytes,
  * A whole-burst failure marks every packet DP_DONE_INTERNAL_FAILURE. */
 int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf,
                              uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
-                             uint32_t n, uint64_t *stats);
+                             dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats);
 
 /* Wait for the context's stream. */
 int dp_ctx_synchronize(dp_ctx_t *ctx);
@@ -594,12 +620,6 @@ int dp_flow_count(dp_flow_table_t *ft, uint64_t *len, uint64_t *active);
  * must live on the context's device and outlive the attachment. */
 int dp_ctx_attach_flow_table(dp_ctx_t *ctx, dp_flow_table_t *ft);
 
-/* dp_process_burst_device plus, when `dev_flow_refs` is not NULL, the flow
- * FlowLookup attached to each packet (PacketMeta.flow_info) as a ref
- * (DP_FLOW_NONE: none). */
-int dp_process_burst_device_ex(dp_ctx_t *ctx, uint8_t *dev_buf, uint64_t buf_bytes,
-                               const dp_pkt_in_t *dev_in, dp_pkt_out_t *dev_out, uint32_t n,
-                               uint64_t *dev_stats, uint64_t *dev_flow_refs, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* DPDK rx / tx burst glue: an rx burst of rte_mbufs  */
@@ -644,14 +664,15 @@ int dp_mbuf_burst_in(const void *pool_base, uint64_t pool_bytes, void *const *mb
 int dp_mbuf_burst_out(void *const *mbufs, uint32_t n, const dp_mbuf_layout_t *layout,
                       const dp_pkt_in_t *in, const dp_pkt_out_t *out);
 /* dp_mbuf_burst_in, the pipeline over the mapped mempool region (zero copy),
- * dp_mbuf_burst_out.  `out` (host memory) receives every packet's result;
+ * dp_mbuf_burst_out.  `out` (host memory) receives every packet's result
+ * (`meta`, may be NULL, the rest of its PacketMeta);
  * the caller transmits the Delivered mbufs on their out[i].oif and frees the
  * others.  Synchronous.  A pool that is not device-mapped fails with
  * DP_EINVAL (every out[i] InternalFailure). */
 int dp_process_mbufs(dp_ctx_t *ctx, const void *pool_base, uint64_t pool_bytes,
                      void *const *mbufs, uint32_t n, const dp_mbuf_layout_t *layout,
                      const uint32_t *port_ifindex, uint32_t n_ports, dp_pkt_out_t *out,
-                     uint64_t *stats);
+                     dp_pkt_meta_t *meta, uint64_t *stats);
 
 /* Introspection: bytes of the device table image and its parts (for
  * DESIGN.md / bench), and the last HIP error string. */

@@ -1861,19 +1861,25 @@ void serialize(Packet &p) {
 
 // The stages before FlowFilter (Packet::new .. FlowLookup); false when the
 // frame is rejected (out is final then).
-bool process_pre(const dpo_tables &T, const dpo_flows *FL, uint8_t *buf, const dp_pkt_in_t &in,
-                 dp_pkt_out_t &out, Packet &p) {
-  p.buf = buf;
-  p.room_start = in.off >= DP_HEADROOM ? in.off - DP_HEADROOM : 0;
+// The records of a packet no stage annotated.
+void out_none(const dp_pkt_in_t &in, dp_pkt_out_t &out, dp_pkt_meta_t &meta, uint8_t done) {
+  out = dp_pkt_out_t{};
   out.off = in.off;
   out.len = in.len;
-  out.acl = 0;
-  out.oif = out.dst_vni = out.src_vni = 0;
-  out.fib_entry = out.acl_rule = UINT32_MAX;
+  out.done = done;
+  meta = dp_pkt_meta_t{};
+  meta.fib_entry = meta.acl_rule = UINT32_MAX;
+  meta.flow_ref = DP_FLOW_NONE;
+}
+
+bool process_pre(const dpo_tables &T, const dpo_flows *FL, uint8_t *buf, const dp_pkt_in_t &in,
+                 dp_pkt_out_t &out, dp_pkt_meta_t &meta, Packet &p) {
+  p.buf = buf;
+  p.room_start = in.off >= DP_HEADROOM ? in.off - DP_HEADROOM : 0;
+  out_none(in, out, meta, DP_DONE_NONE);
   int c = parse_headers(buf + in.off, in.len, p.h);
   if (c < 0) {  // Packet::new fails: frame rejected by the driver (worker.rs:409-421)
     out.done = DP_DONE_NOT_ETHERNET;
-    out.meta_flags = 0;
     return false;
   }
   p.pay_start = in.off + (uint64_t)c;
@@ -1899,7 +1905,7 @@ bool process_pre(const dpo_tables &T, const dpo_flows *FL, uint8_t *buf, const d
 }
 
 // The stages after FlowFilter (AclFilter .. Egress) and serialize.
-void process_post(const dpo_tables &T, dpo_flows *FL, Packet &p, dp_pkt_out_t &out) {
+void process_post(const dpo_tables &T, dpo_flows *FL, Packet &p, dp_pkt_out_t &out, dp_pkt_meta_t &meta) {
   stage_acl(T, FL, p);
   stage_static_nat(T, p);
   // PortForwarder / Masquerade: identity (no REQ_* flags from static-only tables)
@@ -1909,13 +1915,23 @@ void process_post(const dpo_tables &T, dpo_flows *FL, Packet &p, dp_pkt_out_t &o
   stage_egress(T, p);
   if (p.m.done == DP_DONE_DELIVERED) serialize(p);
   out.done = p.m.done < 0 ? (uint8_t)DP_DONE_NONE : (uint8_t)p.m.done;
-  out.meta_flags = p.m.flags;
+  out.meta_flags = (uint16_t)p.m.flags;
   out.oif = p.m.has_oif ? p.m.oif : 0;
-  out.dst_vni = p.m.dst_vni;
-  out.src_vni = p.m.src_vni;
-  out.fib_entry = p.m.fib_entry;
-  out.acl_rule = p.m.acl_rule;
   out.acl = p.m.acl;
+  // the rest of PacketMeta (net/src/packet/meta.rs:138-154)
+  meta.dst_vni = p.m.dst_vni;
+  meta.src_vni = p.m.src_vni;
+  meta.fib_entry = p.m.fib_entry;
+  meta.acl_rule = p.m.acl_rule;
+  meta.pm_flags = 0;
+  if (p.m.has_vrf) { meta.pm_flags |= DP_PM_HAS_VRF; meta.vrf = p.m.vrf; }
+  if (p.m.has_dscp) { meta.pm_flags |= DP_PM_HAS_DSCP; meta.dscp = p.m.dscp; meta.ecn = p.m.ecn; }
+  if (p.m.has_nh) {
+    meta.pm_flags |= DP_PM_HAS_NH;
+    meta.nh_family = p.m.nh.fam;
+    memcpy(meta.nh_addr, p.m.nh.b, p.m.nh.fam == 6 ? 16 : 4);  // IpAddr: v4 is 4 bytes
+  }
+  meta.flow_ref = p.flow >= 0 ? (uint64_t)p.flow : DP_FLOW_NONE;
   if (p.m.done == DP_DONE_DELIVERED) {
     out.off = (uint32_t)p.pay_start;
     out.len = (uint16_t)(p.pay_end - p.pay_start);
@@ -1924,13 +1940,14 @@ void process_post(const dpo_tables &T, dpo_flows *FL, Packet &p, dp_pkt_out_t &o
 
 // Without a flow table the stages of different packets share no state, so the
 // burst is processed packet by packet.
-void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pkt_out_t &out) {
+void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pkt_out_t &out,
+                 dp_pkt_meta_t &meta) {
   Packet p;
-  if (!process_pre(T, nullptr, buf, in, out, p)) return;
+  if (!process_pre(T, nullptr, buf, in, out, meta, p)) return;
   FfWork w;
   ff_classify(T, nullptr, p, w);
   ff_apply(T, nullptr, p, w);
-  process_post(T, nullptr, p, out);
+  process_post(T, nullptr, p, out, meta);
 }
 
 // With a flow table, in the reference's burst order: the lazy stages up to
@@ -1938,17 +1955,15 @@ void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pk
 // classifications, then all route applications: flow-filter/src/lib.rs:75-111,
 // 352-363), then the lazy stages after it packet by packet.
 void process_burst_flows(const dpo_tables &T, dpo_flows *FL, uint8_t *buf, const dp_pkt_in_t *in,
-                         dp_pkt_out_t *out, uint32_t n, uint64_t *flow_refs) {
+                         dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n) {
   std::vector<Packet> P(n);
   std::vector<char> live(n);
   std::vector<FfWork> W(n);
-  for (uint32_t i = 0; i < n; i++) live[i] = process_pre(T, FL, buf, in[i], out[i], P[i]);
+  for (uint32_t i = 0; i < n; i++) live[i] = process_pre(T, FL, buf, in[i], out[i], meta[i], P[i]);
   for (uint32_t i = 0; i < n; i++) if (live[i]) ff_classify(T, FL, P[i], W[i]);
   for (uint32_t i = 0; i < n; i++) if (live[i]) ff_apply(T, FL, P[i], W[i]);
-  for (uint32_t i = 0; i < n; i++) {
-    if (live[i]) process_post(T, FL, P[i], out[i]);
-    if (flow_refs) flow_refs[i] = live[i] && P[i].flow >= 0 ? (uint64_t)P[i].flow : DP_FLOW_NONE;
-  }
+  for (uint32_t i = 0; i < n; i++)
+    if (live[i]) process_post(T, FL, P[i], out[i], meta[i]);
 }
 
 FKey fkey_of(const dp_flow_key_t &x) {
@@ -2146,20 +2161,22 @@ int dpo_tables_build(const dp_tables_desc_t *d, dpo_tables_t **out) {
 void dpo_tables_free(dpo_tables_t *t) { delete t; }
 
 int dpo_process_burst(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes,
-                      const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, uint64_t *stats) {
-  if (!t || (!buf && n)) return DP_EINVAL;
+                      const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
+                      uint64_t *stats) {
+  if (!t || (!buf && n) || (!out && n)) return DP_EINVAL;
   for (uint32_t i = 0; i < n; i++) {
     if (in[i].off < DP_HEADROOM || (uint64_t)in[i].off + in[i].len > buf_bytes) return DP_EINVAL;
   }
   for (uint32_t i = 0; i < n; i++) {
-    process_one(*t, buf, in[i], out[i]);
+    dp_pkt_meta_t m;
+    process_one(*t, buf, in[i], out[i], meta ? meta[i] : m);
     if (stats && out[i].done < DP_DONE_COUNT) stats[out[i].done]++;
   }
   return 0;
 }
 
 int dpo_process_parallel(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes,
-                         const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
+                         const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
                          uint32_t burst, uint32_t threads) {
   if (!t || threads == 0 || burst == 0) return DP_EINVAL;
   std::atomic<uint32_t> next{0};
@@ -2170,7 +2187,7 @@ int dpo_process_parallel(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes
         uint32_t s = next.fetch_add(burst);
         if (s >= n) break;
         uint32_t e = std::min(n, s + burst);
-        dpo_process_burst(t, buf, buf_bytes, in + s, out + s, e - s, nullptr);
+        dpo_process_burst(t, buf, buf_bytes, in + s, out + s, meta ? meta + s : nullptr, e - s, nullptr);
       }
     });
   }
@@ -2179,18 +2196,15 @@ int dpo_process_parallel(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes
 }
 
 int dpo_process_burst_flows(const dpo_tables_t *t, dpo_flows_t *fl, uint8_t *buf, uint64_t buf_bytes,
-                            const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n, uint64_t *stats,
-                            uint64_t *flow_refs) {
-  if (!t || (!buf && n)) return DP_EINVAL;
+                            const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
+                            uint64_t *stats) {
+  if (!t || (!buf && n) || ((!out || !meta) && n)) return DP_EINVAL;
   for (uint32_t i = 0; i < n; i++)
     if (in[i].off < DP_HEADROOM || (uint64_t)in[i].off + in[i].len > buf_bytes) return DP_EINVAL;
   if (!fl) {
-    for (uint32_t i = 0; i < n; i++) {
-      process_one(*t, buf, in[i], out[i]);
-      if (flow_refs) flow_refs[i] = DP_FLOW_NONE;
-    }
+    for (uint32_t i = 0; i < n; i++) process_one(*t, buf, in[i], out[i], meta[i]);
   } else {
-    process_burst_flows(*t, fl, buf, in, out, n, flow_refs);
+    process_burst_flows(*t, fl, buf, in, out, meta, n);
   }
   if (stats)
     for (uint32_t i = 0; i < n; i++) if (out[i].done < DP_DONE_COUNT) stats[out[i].done]++;

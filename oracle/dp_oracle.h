@@ -39,15 +39,15 @@ void dpo_tables_free(dpo_tables_t *t);
 /* Run the reference stage sequence over a burst, in place, exactly like
  * dp_process_burst.  Single-threaded per call. */
 int dpo_process_burst(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes,
-                      const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
-                      uint64_t *stats);
+                      const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta,
+                      uint32_t n, uint64_t *stats);
 
 /* Multi-threaded CPU baseline: splits the burst into bursts of `burst`
  * packets (DPDK PKT_BURST_SIZE = 64, dpdk/src/queue/rx.rs:174) over
  * `threads` threads.  Returns 0 / negative errno. */
 int dpo_process_parallel(const dpo_tables_t *t, uint8_t *buf, uint64_t buf_bytes,
-                         const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n,
-                         uint32_t burst, uint32_t threads);
+                         const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta,
+                         uint32_t n, uint32_t burst, uint32_t threads);
 
 /* Flow table (flow-entry/src/flow_table/table.rs) with the dp_flow_* semantics
  * of include/dpgpu.h; refs are indices of the FlowInfos the table made. */
@@ -67,11 +67,11 @@ int dpo_flow_set_status(dpo_flows_t *fl, uint64_t ref, uint32_t status);
 int dpo_flow_sweep(dpo_flows_t *fl, uint64_t now, uint64_t *n_removed);
 int dpo_flow_count(dpo_flows_t *fl, uint64_t *len, uint64_t *active);
 /* One burst through the pipeline with FlowLookup on `fl` (NULL: an empty
- * flow table), in the reference's burst order; flow_refs (may be NULL)
- * receives each packet's PacketMeta.flow_info (DP_FLOW_NONE: none). */
+ * flow table), in the reference's burst order; meta[i].flow_ref is each
+ * packet's PacketMeta.flow_info (DP_FLOW_NONE: none). */
 int dpo_process_burst_flows(const dpo_tables_t *t, dpo_flows_t *fl, uint8_t *buf,
                             uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
-                            uint32_t n, uint64_t *stats, uint64_t *flow_refs);
+                            dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats);
 
 /* Primitive restatements exposed for unit tests. */
 uint16_t dpo_checksum_ipv4_header(const uint8_t *hdr, uint32_t hlen);

@@ -12,6 +12,8 @@ import os
 
 import numpy as np
 
+from dataplane_amd import _abi as A
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
 
@@ -26,8 +28,8 @@ def lib() -> C.CDLL:
         V = C.c_void_p
         l.dpo_tables_build.argtypes = [V, C.POINTER(V)]
         l.dpo_tables_free.argtypes = [V]
-        l.dpo_process_burst.argtypes = [V, V, C.c_uint64, V, V, C.c_uint32, V]
-        l.dpo_process_parallel.argtypes = [V, V, C.c_uint64, V, V, C.c_uint32, C.c_uint32,
+        l.dpo_process_burst.argtypes = [V, V, C.c_uint64, V, V, V, C.c_uint32, V]
+        l.dpo_process_parallel.argtypes = [V, V, C.c_uint64, V, V, V, C.c_uint32, C.c_uint32,
                                            C.c_uint32]
         l.dpo_lpm.argtypes = [V, C.c_uint32, C.c_uint8, V]
         l.dpo_lpm.restype = C.c_int64
@@ -42,7 +44,7 @@ def lib() -> C.CDLL:
         l.dpo_hash_bytes.restype = C.c_uint64
         l.dpo_reserialize.argtypes = [V, C.c_uint32, V, C.c_uint32]
         l.dpo_reserialize.restype = C.c_int
-        l.dpo_process_burst_flows.argtypes = [V, V, V, C.c_uint64, V, V, C.c_uint32, V, V]
+        l.dpo_process_burst_flows.argtypes = [V, V, V, C.c_uint64, V, V, V, C.c_uint32, V]
         l.dpo_flows_create.argtypes = [C.POINTER(V)]
         l.dpo_flows_free.argtypes = [V]
         l.dpo_flows_set_capacity.argtypes = [V, C.c_uint64]
@@ -67,32 +69,41 @@ class Oracle:
             raise ValueError(f"oracle rejected tables: rc={rc}")
         self.h = h
 
-    def process(self, buf: np.ndarray, inp: np.ndarray, out_dtype, stats: bool = False):
-        out = np.zeros(len(inp), dtype=out_dtype)
+    def process(self, buf: np.ndarray, inp: np.ndarray, stats: bool = False):
+        """One burst, in place: PKT_RES records (dp_pkt_out_t + dp_pkt_meta_t)."""
+        out = np.zeros(len(inp), dtype=A.PKT_OUT)
+        meta = np.zeros(len(inp), dtype=A.PKT_META)
         st = np.zeros(34, dtype=np.uint64)
         rc = lib().dpo_process_burst(self.h, buf.ctypes.data, buf.nbytes, inp.ctypes.data,
-                                     out.ctypes.data, len(inp), st.ctypes.data)
+                                     out.ctypes.data, meta.ctypes.data, len(inp), st.ctypes.data)
         if rc != 0:
             raise RuntimeError(f"oracle process failed rc={rc}")
-        return (out, st) if stats else out
+        res = A.join_results(out, meta)
+        return (res, st) if stats else res
 
-    def process_flows(self, buf: np.ndarray, inp: np.ndarray, out_dtype, flows, stats=False):
+    def process_flows(self, buf: np.ndarray, inp: np.ndarray, flows, stats=False):
         """One burst with FlowLookup on `flows` (an OracleFlows, or None for an
-        empty flow table): (out, flow_refs[, stats])."""
-        out = np.zeros(len(inp), dtype=out_dtype)
-        refs = np.zeros(len(inp), dtype=np.uint64)
+        empty flow table): (PKT_RES records, flow_refs[, stats]); flow_refs is
+        the records' flow_ref column (PacketMeta.flow_info)."""
+        out = np.zeros(len(inp), dtype=A.PKT_OUT)
+        meta = np.zeros(len(inp), dtype=A.PKT_META)
         st = np.zeros(34, dtype=np.uint64)
         rc = lib().dpo_process_burst_flows(self.h, flows.h if flows is not None else None,
                                            buf.ctypes.data, buf.nbytes, inp.ctypes.data,
-                                           out.ctypes.data, len(inp), st.ctypes.data,
-                                           refs.ctypes.data)
+                                           out.ctypes.data, meta.ctypes.data, len(inp),
+                                           st.ctypes.data)
         if rc != 0:
             raise RuntimeError(f"oracle process failed rc={rc}")
-        return (out, refs, st) if stats else (out, refs)
+        res = A.join_results(out, meta)
+        refs = res["flow_ref"].copy()
+        return (res, refs, st) if stats else (res, refs)
 
-    def process_parallel(self, buf, inp, out, threads: int, burst: int = 64):
+    def process_parallel(self, buf, inp, out, threads: int, burst: int = 64, meta=None):
+        """CPU baseline: `out` a PKT_OUT array, `meta` an optional PKT_META one."""
         rc = lib().dpo_process_parallel(self.h, buf.ctypes.data, buf.nbytes, inp.ctypes.data,
-                                        out.ctypes.data, len(inp), burst, threads)
+                                        out.ctypes.data,
+                                        meta.ctypes.data if meta is not None else None,
+                                        len(inp), burst, threads)
         if rc != 0:
             raise RuntimeError(f"oracle parallel failed rc={rc}")
 

@@ -36,7 +36,7 @@ def main():
     w = Workload(a.config, a.packets, seed=1, n_routes_v4=a.routes_v4, layout="dpdk")
     trips = np.zeros((w.n, 8), dtype=np.uint16)
     lib.dpemu_trips_out(trips.ctypes.data)
-    out = pyemu.process(w.tables, w.fresh_buf(), w.inp, A.PKT_OUT)
+    out = pyemu.process(w.tables, w.fresh_buf(), w.inp)
     lib.dpemu_trips_out(None)
     nw = w.n // 64
     t = trips[:nw * 64].reshape(nw, 64, 8).astype(np.int64)

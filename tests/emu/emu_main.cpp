@@ -7,10 +7,11 @@
 #include "../../dataplane_amd/csrc/dp_tables.h"
 
 extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uint8_t *buf,
-                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n);
+                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta,
+                          uint32_t n);
 
 extern "C" int dpemu_process(const dp_tables_desc_t *d, uint8_t *buf, uint64_t buf_bytes,
-                             const dp_pkt_in_t *in, dp_pkt_out_t *out, uint32_t n) {
+                             const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n) {
   dpd::BuiltImage bi;
   int rc = dpd::build_image(d, bi);
   if (rc) return rc;
@@ -22,7 +23,7 @@ extern "C" int dpemu_process(const dp_tables_desc_t *d, uint8_t *buf, uint64_t b
   std::vector<uint8_t> img(bi.bytes.size() + 16);
   uint8_t *ib = reinterpret_cast<uint8_t *>(((uintptr_t)img.data() + 15) & ~(uintptr_t)15);
   memcpy(ib, bi.bytes.data(), bi.bytes.size());
-  dpemu_run(ib, &bi.im, al, padded, in, out, n);
+  dpemu_run(ib, &bi.im, al, padded, in, out, meta, n);
   memcpy(buf, al, buf_bytes);
   return 0;
 }
@@ -55,7 +56,8 @@ extern "C" void dpemu_ctx_free(void *c) { delete static_cast<dpemu_ctx *>(c); }
 
 // `buf` must be 16-byte aligned with 16 bytes of slack past buf_bytes.
 extern "C" int dpemu_run_parallel(void *cv, uint8_t *buf, uint64_t buf_bytes, const dp_pkt_in_t *in,
-                                  dp_pkt_out_t *out, uint32_t n, uint32_t burst, uint32_t threads) {
+                                  dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n, uint32_t burst,
+                                  uint32_t threads) {
   auto *c = static_cast<dpemu_ctx *>(cv);
   if (!c || !threads || !burst || ((uintptr_t)buf & 15)) return -22;
   std::atomic<uint32_t> next{0};
@@ -66,7 +68,7 @@ extern "C" int dpemu_run_parallel(void *cv, uint8_t *buf, uint64_t buf_bytes, co
         const uint32_t s = next.fetch_add(burst);
         if (s >= n) break;
         const uint32_t e = s + burst < n ? s + burst : n;
-        dpemu_run(c->ib, &c->bi.im, buf, buf_bytes, in + s, out + s, e - s);
+        dpemu_run(c->ib, &c->bi.im, buf, buf_bytes, in + s, out + s, meta ? meta + s : nullptr, e - s);
       }
     });
   for (auto &t : th) t.join();

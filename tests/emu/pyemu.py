@@ -5,6 +5,8 @@ import subprocess
 
 import numpy as np
 
+from dataplane_amd import _abi as A
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 _libs = {}
 
@@ -19,20 +21,22 @@ def lib(variant: str = ""):
             subprocess.run(["make", "-s", "-C", HERE], check=True)
         l = C.CDLL(p)
         V = C.c_void_p
-        l.dpemu_process.argtypes = [V, V, C.c_uint64, V, V, C.c_uint32]
+        l.dpemu_process.argtypes = [V, V, C.c_uint64, V, V, V, C.c_uint32]
         l.dpemu_image_bytes.argtypes = [V]
         l.dpemu_image_bytes.restype = C.c_uint64
         _libs[variant] = l
     return _libs[variant]
 
 
-def process(tables_ptr, buf: np.ndarray, inp: np.ndarray, out_dtype, variant: str = ""):
-    out = np.zeros(len(inp), dtype=out_dtype)
+def process(tables_ptr, buf: np.ndarray, inp: np.ndarray, variant: str = ""):
+    """The kernel body over one burst, in place: PKT_RES records."""
+    out = np.zeros(len(inp), dtype=A.PKT_OUT)
+    meta = np.zeros(len(inp), dtype=A.PKT_META)
     rc = lib(variant).dpemu_process(C.cast(tables_ptr, C.c_void_p), buf.ctypes.data, buf.nbytes,
-                             inp.ctypes.data, out.ctypes.data, len(inp))
+                                    inp.ctypes.data, out.ctypes.data, meta.ctypes.data, len(inp))
     if rc != 0:
         raise RuntimeError(f"emu rejected tables rc={rc}")
-    return out
+    return A.join_results(out, meta)
 
 
 def classifier_forms(variant: str = ""):
@@ -65,15 +69,19 @@ class ParallelEmu:
         l.dpemu_ctx_create.argtypes = [V]
         l.dpemu_ctx_create.restype = V
         l.dpemu_ctx_free.argtypes = [V]
-        l.dpemu_run_parallel.argtypes = [V, V, C.c_uint64, V, V, C.c_uint32, C.c_uint32, C.c_uint32]
+        l.dpemu_run_parallel.argtypes = [V, V, C.c_uint64, V, V, V, C.c_uint32, C.c_uint32,
+                                         C.c_uint32]
         self.h = l.dpemu_ctx_create(C.cast(tables_ptr, C.c_void_p))
         if not self.h:
             raise RuntimeError("emu rejected tables")
 
     def run(self, buf: np.ndarray, buf_bytes: int, inp: np.ndarray, out: np.ndarray, threads: int,
-            burst: int = 64):
+            burst: int = 64, meta: np.ndarray = None):
+        """`out` a PKT_OUT array, `meta` an optional PKT_META one."""
         rc = self.l.dpemu_run_parallel(self.h, buf.ctypes.data, buf_bytes, inp.ctypes.data,
-                                       out.ctypes.data, len(inp), burst, threads)
+                                       out.ctypes.data,
+                                       meta.ctypes.data if meta is not None else None,
+                                       len(inp), burst, threads)
         if rc != 0:
             raise RuntimeError(f"emu run rc={rc}")
 

@@ -63,13 +63,13 @@ def main():
     for name in VECTORS:
         w = workload(name)
         b = w.fresh_buf()
-        out = Oracle(w.tables).process(b, w.inp, A.PKT_OUT)
+        out = Oracle(w.tables).process(b, w.inp)
         np.savez_compressed(os.path.join(HERE, f"vectors_{name}.npz"), buf_in=w.buf, inp=w.inp,
                             out=out, buf_out=b, tables_digest=np.array(tables_digest(w.tables)))
         print(name, w.n, "packets")
     t, tp, buf, inp = edge_burst()
     b = buf.copy()
-    out = Oracle(tp).process(b, inp, A.PKT_OUT)
+    out = Oracle(tp).process(b, inp)
     np.savez_compressed(os.path.join(HERE, "vectors_edge.npz"), buf_in=buf, inp=inp, out=out,
                         buf_out=b, tables_digest=np.array(tables_digest(tp)))
     print("edge", len(inp), "packets")

@@ -5,9 +5,11 @@ from dataplane_amd import _abi as A
 
 
 def compare(out_ref, buf_ref, out_dut, buf_dut, inp, label=""):
-    """Bit-exact: every dp_pkt_out_t field, and every serialized byte of every
-    Delivered packet (plus the whole buffer, which also pins that nothing else
-    was touched)."""
+    """Bit-exact: every dp_pkt_out_t field (and every dp_pkt_meta_t field when
+    both sides carry one -- PKT_RES records), and every serialized byte of
+    every Delivered packet (plus the whole buffer, which also pins that
+    nothing else was touched)."""
+    out_ref, out_dut = common_fields(out_ref, out_dut)
     mism = np.nonzero(out_ref != out_dut)[0]
     msg = []
     for i in mism[:5]:
@@ -37,6 +39,15 @@ def compare(out_ref, buf_ref, out_dut, buf_dut, inp, label=""):
         owner = int(np.searchsorted(inp["off"].astype(np.int64) - A.HEADROOM, d[0], "right")) - 1
         raise AssertionError(f"{label}: buffers differ outside delivered frames at {d[:8]} "
                              f"(packet {owner}: {out_ref[owner]} / {out_dut[owner]})")
+
+
+def common_fields(a, b):
+    """Both record arrays projected onto the fields they share (a device run
+    without a meta array yields dp_pkt_out_t alone).  flow_ref is left out:
+    the oracle's refs and the device table's are different handle spaces,
+    which the flow tests match up through the flows they name."""
+    names = [n for n in a.dtype.names if n in b.dtype.names and n not in ("pad", "flow_ref")]
+    return a[names], b[names]
 
 
 def hist(out):

@@ -31,6 +31,7 @@ def test_struct_layouts_match_c():
         assert C.sizeof(st) == lib.dpw_sizeof(name.encode()), name
     assert lib.dpw_sizeof(b"dp_pkt_in_t") == A.PKT_IN.itemsize
     assert lib.dpw_sizeof(b"dp_pkt_out_t") == A.PKT_OUT.itemsize
+    assert lib.dpw_sizeof(b"dp_pkt_meta_t") == A.PKT_META.itemsize
     assert C.sizeof(A.MbufLayout) == lib.dpw_sizeof(b"dp_mbuf_layout_t")
     for name, dt in A.NP_STRUCTS.items():
         assert dt.itemsize == lib.dpw_sizeof(name.encode()), name

@@ -26,8 +26,8 @@ def test_edge_emu_matches_oracle(tables, seed, form, cls_form):
     frames = edge_frames(4000, seed)
     buf, inp = pack_burst(frames)
     b_ref, b_dut = buf.copy(), buf.copy()
-    o_ref = Oracle(tp).process(b_ref, inp, A.PKT_OUT)
-    o_dut = pyemu.process(tp, b_dut, inp, A.PKT_OUT)
+    o_ref = Oracle(tp).process(b_ref, inp)
+    o_dut = pyemu.process(tp, b_dut, inp)
     compare(o_ref, b_ref, o_dut, b_dut, inp, f"edge seed {seed}")
 
 
@@ -38,8 +38,8 @@ def test_edge_small_window_matches_oracle(tables, seed):
     _, tp = tables
     buf, inp = pack_burst(edge_frames(4000, seed))
     b_ref, b_dut = buf.copy(), buf.copy()
-    o_ref = Oracle(tp).process(b_ref, inp, A.PKT_OUT)
-    o_dut = pyemu.process(tp, b_dut, inp, A.PKT_OUT, variant="w32")
+    o_ref = Oracle(tp).process(b_ref, inp)
+    o_dut = pyemu.process(tp, b_dut, inp, variant="w32")
     compare(o_ref, b_ref, o_dut, b_dut, inp, f"edge w32 seed {seed}")
 
 
@@ -49,8 +49,8 @@ def test_workload_small_window_matches_oracle(cfg):
     w = Workload(cfg, 2000, seed=900 + cfg, n_routes_v4=2000, n_routes_v6=1000, n_acl=200,
                  n_nat=32, tcp_percent=30)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
-    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
-    o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT, variant="w32")
+    o_ref = Oracle(w.tables).process(b_ref, w.inp)
+    o_dut = pyemu.process(w.tables, b_dut, w.inp, variant="w32")
     compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} w32")
 
 
@@ -59,7 +59,7 @@ def test_edge_corpus_coverage(tables):
     _, tp = tables
     frames = edge_frames(16000, 99)
     buf, inp = pack_burst(frames)
-    out = Oracle(tp).process(buf, inp, A.PKT_OUT)
+    out = Oracle(tp).process(buf, inp)
     h = hist(out)
     must = ["InterfaceUnknown", "InterfaceDetached", "InterfaceAdmDown", "InterfaceOperDown",
             "InterfaceUnsupported", "NotEthernet", "Unhandled", "MacNotForUs", "InvalidDstMac",
@@ -73,6 +73,12 @@ def test_edge_corpus_coverage(tables):
                  "REQ_STATIC_NAT_DST", "IS_L2_BCAST"):
         assert np.any(f & A.META[flag]), flag
     assert set(np.unique(out["acl"])) >= {0, 1, 2, 3, 4, 5}
+    # dp_pkt_meta_t: every Option<> of PacketMeta the path sets is reached
+    pm = out["pm_flags"]
+    for flag in (A.PM_HAS_VRF, A.PM_HAS_NH, A.PM_HAS_DSCP):
+        assert np.any(pm & flag), flag
+    assert set(np.unique(out["nh_family"][(pm & A.PM_HAS_NH) != 0])) == {4, 6}
+    assert len(np.unique(out["dscp"][(pm & A.PM_HAS_DSCP) != 0])) > 4
 
 
 @pytest.mark.parametrize("form", ["bv", "list"])
@@ -84,8 +90,8 @@ def test_edge_outline_matches_oracle(tables, form, cls_form):
     _, tp = tables
     buf, inp = pack_burst(edge_frames(3000, 7))
     b_ref, b_dut = buf.copy(), buf.copy()
-    o_ref = Oracle(tp).process(b_ref, inp, A.PKT_OUT)
-    o_dut = pyemu.process(tp, b_dut, inp, A.PKT_OUT, variant="outline")
+    o_ref = Oracle(tp).process(b_ref, inp)
+    o_dut = pyemu.process(tp, b_dut, inp, variant="outline")
     if form == "bv":
         assert pyemu.classifier_forms("outline")[0] > 0
     compare(o_ref, b_ref, o_dut, b_dut, inp, f"edge outline {form}")
@@ -98,6 +104,6 @@ def test_workload_outline_matches_oracle(cfg, cls_form):
     w = Workload(cfg, 2000, seed=950 + cfg, n_routes_v4=2000, n_routes_v6=1000, n_acl=200,
                  n_nat=32, tcp_percent=30)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
-    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
-    o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT, variant="outline")
+    o_ref = Oracle(w.tables).process(b_ref, w.inp)
+    o_dut = pyemu.process(w.tables, b_dut, w.inp, variant="outline")
     compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} outline")

@@ -19,8 +19,8 @@ def test_emu_matches_oracle(cfg, form, layout, cls_form):
     w = Workload(cfg, 3000, seed=100 + cfg, n_routes_v4=3000, n_routes_v6=1500, n_acl=400,
                  n_nat=48, tcp_percent=25, layout=layout)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
-    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
-    o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT)
+    o_ref = Oracle(w.tables).process(b_ref, w.inp)
+    o_dut = pyemu.process(w.tables, b_dut, w.inp)
     bv, lst = pyemu.classifier_forms()
     if cfg != 1:  # C1 has no overlay tables
         if form == "bv":
@@ -37,7 +37,7 @@ def test_emu_dir24_8(cfg):
     w = Workload(cfg, 20000, seed=400 + cfg, n_routes_v4=120000, n_routes_v6=4000, n_acl=400,
                  n_nat=48, tcp_percent=25, layout="dpdk")
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
-    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
-    o_dut = pyemu.process(w.tables, b_dut, w.inp, A.PKT_OUT)
+    o_ref = Oracle(w.tables).process(b_ref, w.inp)
+    o_dut = pyemu.process(w.tables, b_dut, w.inp)
     compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} dir24-8")
 

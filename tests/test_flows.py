@@ -18,7 +18,7 @@ class OracleBackend:
         return OracleFlows()
 
     def process(self, tb, buf, inp, ft):
-        return Oracle(tb.build()).process_flows(buf, inp, A.PKT_OUT, ft)
+        return Oracle(tb.build()).process_flows(buf, inp, ft)
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c.name for c in CASES])

@@ -33,7 +33,7 @@ def load(name):
 def test_golden_oracle(name):
     keep, tp, z = load(name)
     b = z["buf_in"].copy()
-    out = Oracle(tp).process(b, z["inp"], A.PKT_OUT)
+    out = Oracle(tp).process(b, z["inp"])
     compare(z["out"], z["buf_out"], out, b, z["inp"], f"golden {name} oracle")
 
 
@@ -41,5 +41,5 @@ def test_golden_oracle(name):
 def test_golden_emu(name):
     keep, tp, z = load(name)
     b = z["buf_in"].copy()
-    out = pyemu.process(tp, b, z["inp"], A.PKT_OUT)
+    out = pyemu.process(tp, b, z["inp"])
     compare(z["out"], z["buf_out"], out, b, z["inp"], f"golden {name} emu")

@@ -37,15 +37,15 @@ def run_device(nf, buf, inp, stats=False):
     db = torch.from_numpy(buf).to(dev)
     di = torch.from_numpy(inp.view(np.uint8).copy()).to(dev)
     do = torch.zeros(len(inp) * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
-    dr = torch.zeros(len(inp), dtype=torch.int64, device=dev)
+    dm = torch.zeros(len(inp) * A.PKT_META.itemsize, dtype=torch.uint8, device=dev)
     st = torch.zeros(A.DONE_COUNT, dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
-    nf.process_device_ex(db.data_ptr(), db.numel(), di.data_ptr(), do.data_ptr(), len(inp),
-                         st.data_ptr(), dr.data_ptr())
+    nf.process_device(db.data_ptr(), db.numel(), di.data_ptr(), do.data_ptr(), len(inp),
+                      st.data_ptr(), dev_meta=dm.data_ptr())
     nf.synchronize()
     buf[:] = db.cpu().numpy()
-    out = do.cpu().numpy().view(A.PKT_OUT)
-    refs = dr.cpu().numpy().view(np.uint64)
+    out = A.join_results(do.cpu().numpy().view(A.PKT_OUT), dm.cpu().numpy().view(A.PKT_META))
+    refs = out["flow_ref"].copy()
     return (out, refs, st.cpu().numpy().view(np.uint64)) if stats else (out, refs)
 
 
@@ -93,7 +93,7 @@ def test_gpu_flows_random_bursts(nf, cfg, seed):
     ora = Oracle(w.tables)
     frames = frames_of(w)
     ob = w.fresh_buf()
-    o0 = ora.process(ob, w.inp, A.PKT_OUT)
+    o0 = ora.process(ob, w.inp)
     items, burst = scenario(frames, o0["dst_vni"], genid=1, seed=seed, n_flows=600,
                             vnis=sorted(set(int(v) for v in o0["dst_vni"] if v)))
     if cfg == 5:
@@ -107,7 +107,7 @@ def test_gpu_flows_random_bursts(nf, cfg, seed):
         for rnd in range(2):
             buf, inp = pack_burst([(f, 1, A.IN_SEEDED_OVERLAY, v) for f, v in burst])
             obuf, gbuf = buf.copy(), buf.copy()
-            oout, oref, ost = ora.process_flows(obuf, inp, A.PKT_OUT, oft, stats=True)
+            oout, oref, ost = ora.process_flows(obuf, inp, oft, stats=True)
             gout, gref, gst = run_device(nf, gbuf, inp, stats=True)
             compare(oout, obuf, gout, gbuf, inp, f"flows C{cfg} seed {seed} burst {rnd}")
             mapped = np.array([g2o.get(int(r), A.FLOW_NONE) if int(r) != A.FLOW_NONE else A.FLOW_NONE
@@ -165,7 +165,7 @@ def test_gpu_flows_full_size(nf):
     nf.attach_flows(gft)
     try:
         obuf, gbuf = w.fresh_buf(), w.fresh_buf()
-        oout, orf = ora.process_flows(obuf, w.inp, A.PKT_OUT, oft)
+        oout, orf = ora.process_flows(obuf, w.inp, oft)
         gout, grf = run_device(nf, gbuf, w.inp)
     finally:
         nf.attach_flows(None)
@@ -197,7 +197,7 @@ def test_gpu_flows_host_origin(nf):
     nf.attach_flows(gft)
     try:
         obuf, hbuf = w.fresh_buf(), w.fresh_buf()
-        oout, _ = ora.process_flows(obuf, w.inp, A.PKT_OUT, oft)
+        oout, _ = ora.process_flows(obuf, w.inp, oft)
         hout = nf.process_arrays(hbuf, w.inp)
         with pytest.raises(RuntimeError):
             GpuPathNf.process_sharded([nf], w.fresh_buf(), w.inp)
@@ -218,7 +218,7 @@ def test_gpu_flows_two_contexts_one_table(nf):
     w = Workload(2, 8000, seed=21, n_routes_v4=3000, n_acl=400, n_nat=24, tcp_percent=30)
     ora = Oracle(w.tables)
     frames = frames_of(w)
-    o0 = ora.process(w.fresh_buf(), w.inp, A.PKT_OUT)
+    o0 = ora.process(w.fresh_buf(), w.inp)
     items, burst = scenario(frames, o0["dst_vni"], genid=1, seed=21, n_flows=700,
                             vnis=sorted(set(int(v) for v in o0["dst_vni"] if v)))
     oft, gft = OracleFlows(), FlowTable(0, 1 << 13)
@@ -240,13 +240,12 @@ def test_gpu_flows_two_contexts_one_table(nf):
             douts.append(torch.zeros(len(inp) * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev))
         torch.cuda.synchronize(dev)
         for k, x in enumerate((nf, nf2)):
-            x.process_device_ex(dbufs[k].data_ptr(), dbufs[k].numel(), dins[k].data_ptr(),
-                                douts[k].data_ptr(), len(bursts[k][1]), None, None,
-                                streams[k].cuda_stream)
+            x.process_device(dbufs[k].data_ptr(), dbufs[k].numel(), dins[k].data_ptr(),
+                             douts[k].data_ptr(), len(bursts[k][1]), None, streams[k].cuda_stream)
         torch.cuda.synchronize(dev)
         for k, (buf, inp) in enumerate(bursts):
             obuf = buf.copy()
-            oout, _ = ora.process_flows(obuf, inp, A.PKT_OUT, oft)
+            oout, _ = ora.process_flows(obuf, inp, oft)
             gbuf = dbufs[k].cpu().numpy()
             gout = douts[k].cpu().numpy().view(A.PKT_OUT)
             compare(oout, obuf, gout, gbuf, inp, f"two contexts, burst {k}")

@@ -42,10 +42,11 @@ def test_gpu_mbuf_burst(nf, cfg):
     st = np.zeros(A.DONE_COUNT, np.uint64)
     out = nf.process_mbufs(pool.base, pool.mem.nbytes, mbufs, stats=st)
     buf, inp = pack_burst([(f, int(p), 0, 0) for f, p in zip(frames, ports)])
-    oout = Oracle(w.tables).process(buf, inp, A.PKT_OUT)
+    oout = Oracle(w.tables).process(buf, inp)
     assert out[5]["done"] == A.DONE["InternalFailure"]
     keep = np.arange(len(frames)) != 5
-    for k in ("done", "acl", "meta_flags", "oif", "dst_vni", "src_vni", "fib_entry", "acl_rule"):
+    for k in ("done", "acl", "meta_flags", "oif", "dst_vni", "src_vni", "fib_entry", "acl_rule",
+              "vrf", "pm_flags", "dscp", "ecn", "nh_family", "nh_addr"):
         bad = np.nonzero((out[k] != oout[k]) & keep)[0]
         assert len(bad) == 0, f"{k} differs at {bad[:5]}: {out[bad[:1]]} vs {oout[bad[:1]]}"
     deliv = np.nonzero((oout["done"] == A.DONE["Delivered"]) & keep)[0]
@@ -81,7 +82,7 @@ def test_gpu_mbuf_burst_with_flows(nf):
     ports = w.inp["iif"]
     buf, inp = pack_burst([(f, int(p), 0, 0) for f, p in zip(frames, ports)])
     ora = Oracle(w.tables)
-    o0 = ora.process(buf.copy(), inp, A.PKT_OUT)
+    o0 = ora.process(buf.copy(), inp)
     genid = int(w.tables.contents.genid)
     vnis = sorted(set(int(v) for v in o0["dst_vni"] if v))
     fls, seen = [], set()
@@ -102,7 +103,7 @@ def test_gpu_mbuf_burst_with_flows(nf):
     oft, gft = OracleFlows(), FlowTable(0, 1 << 13)
     oref, _ = oft.insert(fl)
     gref, _ = gft.insert(fl)
-    oout, _ = ora.process_flows(buf, inp, A.PKT_OUT, oft)
+    oout, _ = ora.process_flows(buf, inp, oft)
     pool = FakeMempool(pinned(FakeMempool.bytes_for(len(frames) + 1)))
     mbufs = pool.load(frames, ports)
     nf.publish(w.tables)
@@ -111,7 +112,8 @@ def test_gpu_mbuf_burst_with_flows(nf):
         out = nf.process_mbufs(pool.base, pool.mem.nbytes, mbufs)
     finally:
         nf.attach_flows(None)
-    for k in ("done", "acl", "meta_flags", "oif", "dst_vni", "src_vni", "fib_entry", "acl_rule"):
+    for k in ("done", "acl", "meta_flags", "oif", "dst_vni", "src_vni", "fib_entry", "acl_rule",
+              "vrf", "pm_flags", "dscp", "ecn", "nh_family", "nh_addr"):
         bad = np.nonzero(out[k] != oout[k])[0]
         assert len(bad) == 0, f"{k} differs at {bad[:5]}"
     for i in np.nonzero(oout["done"] == A.DONE["Delivered"])[0]:

@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 from dataplane_amd import GpuPathNf, _abi as A
+from dataplane_amd.nf import Packet
 from dataplane_amd.workload import Workload
 from oracle.pyoracle import Oracle
 
@@ -37,7 +38,7 @@ def test_gpu_matches_oracle(nf, cfg, form, layout, cls_form):
                  n_nat=64, tcp_percent=25, layout=layout)
     nf.publish(w.tables)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
-    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+    o_ref = Oracle(w.tables).process(b_ref, w.inp)
     stats = np.zeros(A.DONE_COUNT, dtype=np.uint64)
     o_dut = nf.process_arrays(b_dut, w.inp, stats)
     compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg}")
@@ -61,7 +62,7 @@ def test_gpu_edge_corpus(nf, edge, seed, cls_form):
     nf.publish(tp)
     buf, inp = pack_burst(edge_frames(20000, seed))
     b_ref, b_dut = buf.copy(), buf.copy()
-    o_ref = Oracle(tp).process(b_ref, inp, A.PKT_OUT)
+    o_ref = Oracle(tp).process(b_ref, inp)
     o_dut = nf.process_arrays(b_dut, inp)
     compare(o_ref, b_ref, o_dut, b_dut, inp, f"edge {seed}")
 
@@ -76,9 +77,11 @@ def test_gpu_full_size(nf, cfg, layout):
     w = Workload(cfg, 1_000_000, seed=300 + cfg, tcp_percent=20, layout=layout)
     nf.publish(w.tables)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
-    o_ref = np.zeros(w.n, dtype=A.PKT_OUT)
+    o_ref, m_ref = np.zeros(w.n, dtype=A.PKT_OUT), np.zeros(w.n, dtype=A.PKT_META)
     orc = Oracle(w.tables)
-    orc.process_parallel(b_ref, w.inp, o_ref, threads=max(1, min(16, len(os.sched_getaffinity(0)))))
+    orc.process_parallel(b_ref, w.inp, o_ref, threads=max(1, min(16, len(os.sched_getaffinity(0)))),
+                         meta=m_ref)
+    o_ref = A.join_results(o_ref, m_ref)
     o_dut = nf.process_arrays(b_dut, w.inp)
     compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} full")
     assert hist(o_ref).get("Delivered", 0) > w.n // 4
@@ -91,7 +94,7 @@ def test_gpu_device_path_and_determinism(nf):
     w = Workload(2, 50000, seed=77, n_routes_v4=50000, n_acl=2000, n_nat=64, tcp_percent=30)
     nf.publish(w.tables)
     b_ref = w.fresh_buf()
-    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+    o_ref = Oracle(w.tables).process(b_ref, w.inp)
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(dev)
     outs = []
@@ -99,12 +102,13 @@ def test_gpu_device_path_and_determinism(nf):
         db = torch.from_numpy(w.fresh_buf()).to(dev)
         di = torch.from_numpy(w.inp.view(np.uint8)).to(dev)
         do = torch.zeros(w.n * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+        dm = torch.zeros(w.n * A.PKT_META.itemsize, dtype=torch.uint8, device=dev)
         st = torch.zeros(A.DONE_COUNT, dtype=torch.int64, device=dev)
         torch.cuda.synchronize(dev)
         nf.process_device(db.data_ptr(), db.numel(), di.data_ptr(), do.data_ptr(), w.n,
-                          st.data_ptr(), s.cuda_stream)
+                          st.data_ptr(), s.cuda_stream, dev_meta=dm.data_ptr())
         s.synchronize()
-        o = do.cpu().numpy().view(A.PKT_OUT)
+        o = A.join_results(do.cpu().numpy().view(A.PKT_OUT), dm.cpu().numpy().view(A.PKT_META))
         b = db.cpu().numpy()
         compare(o_ref, b_ref, o, b, w.inp, "device path")
         assert int(st.sum()) == w.n
@@ -123,7 +127,7 @@ def test_gpu_host_paths_pinned(nf, mode):
                  layout="dpdk")
     nf.publish(w.tables)
     b_ref = w.fresh_buf()
-    o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+    o_ref = Oracle(w.tables).process(b_ref, w.inp)
 
     def pinned(nbytes):
         return torch.empty(nbytes, dtype=torch.uint8).pin_memory().numpy()
@@ -165,7 +169,7 @@ def test_gpu_republish_and_empty(nf, edge):
     assert nf.data.genid != g1
     buf, inp = pack_burst(edge_frames(4096, 21))
     b_ref, b_dut = buf.copy(), buf.copy()
-    compare(Oracle(tp).process(b_ref, inp, A.PKT_OUT), b_ref, nf.process_arrays(b_dut, inp),
+    compare(Oracle(tp).process(b_ref, inp), b_ref, nf.process_arrays(b_dut, inp),
             b_dut, inp, "after republish")
     assert len(nf.process_arrays(buf.copy(), inp[:0])) == 0
     bad = inp[:4].copy()
@@ -213,7 +217,7 @@ def test_gpu_sharded_matches_single(nf, layout):
         for x in nfs:
             x.publish(w.tables)
         b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
-        o_ref = Oracle(w.tables).process(b_ref, w.inp, A.PKT_OUT)
+        o_ref = Oracle(w.tables).process(b_ref, w.inp)
         stats = np.zeros(A.DONE_COUNT, dtype=np.uint64)
         o_dut = GpuPathNf.process_sharded(nfs, b_dut, w.inp, stats)
         compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"sharded {layout}")
@@ -240,7 +244,7 @@ def test_gpu_whole_burst_failure_marks_internal_failure(nf):
     out["done"] = A.DONE["Delivered"]
     b = w.fresh_buf()
     rc = lib.dp_process_burst(nf.ctx, b.ctypes.data, b.nbytes, bad.ctypes.data, out.ctypes.data,
-                              len(bad), None)
+                              None, len(bad), None)
     assert rc < 0 and np.all(out["done"] == A.DONE["InternalFailure"])
     ovl = w.inp.copy()
     ovl["off"][5] = ovl["off"][4] + 8
@@ -248,18 +252,61 @@ def test_gpu_whole_burst_failure_marks_internal_failure(nf):
     out["done"] = A.DONE["Delivered"]
     ctxs = (C.c_void_p * 1)(nf.ctx)
     rc = lib.dp_process_burst_sharded(ctxs, 1, b.ctypes.data, b.nbytes, ovl.ctypes.data,
-                                      out.ctypes.data, len(ovl), None)
+                                      out.ctypes.data, None, len(ovl), None)
     assert rc < 0 and np.all(out["done"] == A.DONE["InternalFailure"])
     dev = torch.device("cuda", 0)
     db = torch.from_numpy(w.fresh_buf()).to(dev)
     di = torch.from_numpy(w.inp.view(np.uint8)).to(dev)
     do = torch.full((w.n * A.PKT_OUT.itemsize,), 0x1f, dtype=torch.uint8, device=dev)
     rc = lib.dp_process_burst_device(nf.ctx, db.data_ptr() + 1, db.numel() - 1, di.data_ptr(),
-                                     do.data_ptr(), w.n, None, None)
+                                     do.data_ptr(), None, w.n, None, None)
     nf.synchronize()
     o = do.cpu().numpy().view(A.PKT_OUT)
     assert rc < 0 and np.all(o["done"] == A.DONE["InternalFailure"])
     assert np.array_equal(o["off"], w.inp["off"])
+
+
+def test_gpu_meta_through_c_abi(nf, edge):
+    """ABI v2 through the raw C entry points: dp_process_burst with a
+    dp_pkt_meta_t array gives the oracle's PacketMeta fields (VNIs, FIB
+    entry, ACL rule, vrf, nh_addr, dscp / ecn, flow ref) bit-exact; without
+    one (meta = NULL) the dp_pkt_out_t records and bytes are the same; the
+    NetworkFunction adapter (GpuPathNf.process) carries them onto Packets."""
+    _, tp = edge
+    nf.publish(tp)
+    buf, inp = pack_burst(edge_frames(8000, 21))
+    b_ref = buf.copy()
+    o_ref = Oracle(tp).process(b_ref, inp)
+    lib = A.gpu_lib()
+    out = np.zeros(len(inp), A.PKT_OUT)
+    meta = np.zeros(len(inp), A.PKT_META)
+    meta.view(np.uint8)[:] = 0xA5
+    b1 = buf.copy()
+    assert lib.dp_process_burst(nf.ctx, b1.ctypes.data, b1.nbytes, inp.ctypes.data,
+                                out.ctypes.data, meta.ctypes.data, len(inp), None) == 0
+    res = A.join_results(out, meta)
+    for k in ("dst_vni", "src_vni", "fib_entry", "acl_rule", "vrf", "pm_flags", "dscp", "ecn",
+              "nh_family", "nh_addr", "flow_ref"):
+        bad = np.nonzero(np.any((res[k] != o_ref[k]).reshape(len(inp), -1), axis=1))[0]
+        assert len(bad) == 0, f"{k} differs at {bad[:5]}"
+    assert np.all(res["flow_ref"] == np.uint64(A.FLOW_NONE))
+    compare(o_ref, b_ref, res, b1, inp, "meta via C-ABI")
+    out2 = np.zeros(len(inp), A.PKT_OUT)
+    b2 = buf.copy()
+    assert lib.dp_process_burst(nf.ctx, b2.ctypes.data, b2.nbytes, inp.ctypes.data,
+                                out2.ctypes.data, None, len(inp), None) == 0
+    assert np.array_equal(out, out2) and np.array_equal(b1, b2)
+    pkts = [Packet(frame=bytes(buf[o:o + n]), iif=int(i), src_vni=int(v),
+                   seeded_overlay=bool(f & A.IN_SEEDED_OVERLAY))
+            for o, n, f, i, v in zip(inp["off"], inp["len"], inp["flags"], inp["iif"],
+                                     inp["src_vni"])]
+    got = list(nf.process(pkts))
+    pm = o_ref["pm_flags"]
+    for j, p in enumerate(got):
+        assert p.vrf == (int(o_ref[j]["vrf"]) if pm[j] & A.PM_HAS_VRF else None)
+        assert p.nh_addr == (A.nh_text(o_ref[j]) if pm[j] & A.PM_HAS_NH else None)
+        assert p.dscp == (int(o_ref[j]["dscp"]) if pm[j] & A.PM_HAS_DSCP else None)
+        assert p.done == A.DONE_NAMES[int(o_ref[j]["done"])]
 
 
 def test_gpu_sharded_full_size_c5(nf):
@@ -276,9 +323,11 @@ def test_gpu_sharded_full_size_c5(nf):
         for x in nfs:
             x.publish(w.tables)
         b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
-        o_ref = np.zeros(w.n, dtype=A.PKT_OUT)
+        o_ref, m_ref = np.zeros(w.n, dtype=A.PKT_OUT), np.zeros(w.n, dtype=A.PKT_META)
         Oracle(w.tables).process_parallel(b_ref, w.inp, o_ref,
-                                          threads=max(1, min(16, len(os.sched_getaffinity(0)))))
+                                          threads=max(1, min(16, len(os.sched_getaffinity(0)))),
+                                          meta=m_ref)
+        o_ref = A.join_results(o_ref, m_ref)
         stats = np.zeros(A.DONE_COUNT, dtype=np.uint64)
         o_dut = GpuPathNf.process_sharded(nfs, b_dut, w.inp, stats)
         compare(o_ref, b_ref, o_dut, b_dut, w.inp, "C5 sharded full size")

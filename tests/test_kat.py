@@ -12,11 +12,11 @@ CASES = all_cases()
 
 
 def oracle_process(tp, buf, inp):
-    return Oracle(tp).process(buf, inp, A.PKT_OUT)
+    return Oracle(tp).process(buf, inp)
 
 
 def emu_process(tp, buf, inp):
-    return pyemu.process(tp, buf, inp, A.PKT_OUT)
+    return pyemu.process(tp, buf, inp)
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c.name for c in CASES])

@@ -42,19 +42,19 @@ def _rank(rank, world, port, layout, q):
     span, rin = SH.scatter_burst(buf, inp_u8, shards, A.PKT_IN.itemsize, rank, world, dev)
     s = shards[rank]
     sb = span.numpy()
-    out = np.zeros(max(1, s.cnt), dtype=A.PKT_OUT)
+    out = np.zeros(max(1, s.cnt), dtype=A.PKT_RES)
     if s.cnt:
-        out = orc.process(sb, rin.numpy()[:s.cnt * A.PKT_IN.itemsize].view(A.PKT_IN), A.PKT_OUT)
-    out_all = torch.zeros(w.n * A.PKT_OUT.itemsize, dtype=torch.uint8)
+        out = orc.process(sb, rin.numpy()[:s.cnt * A.PKT_IN.itemsize].view(A.PKT_IN))
+    out_all = torch.zeros(w.n * A.PKT_RES.itemsize, dtype=torch.uint8)
     SH.gather_burst(span, torch.from_numpy(out.view(np.uint8).copy()), buf, out_all, shards,
-                    A.PKT_OUT.itemsize, rank, world)
+                    A.PKT_RES.itemsize, rank, world)
     hist = np.bincount(out["done"][:s.cnt], minlength=A.DONE_COUNT)[:A.DONE_COUNT]
     elapsed, total = SH.reduce_over_ranks(0.5 + rank, hist, "cpu")
     res = None
     if rank == 0:
-        merged = SH.rebase_gathered(out_all.numpy().view(A.PKT_OUT), shards)
+        merged = SH.rebase_gathered(out_all.numpy().view(A.PKT_RES), shards)
         b_ref = w.fresh_buf()
-        o_ref = orc.process(b_ref, w.inp, A.PKT_OUT)
+        o_ref = orc.process(b_ref, w.inp)
         res = dict(out_equal=bool(np.array_equal(merged, o_ref)),
                    buf_equal=bool(np.array_equal(buf.numpy(), b_ref)),
                    total=total.tolist(), ref_hist=np.bincount(o_ref["done"], minlength=A.DONE_COUNT)
@@ -109,13 +109,12 @@ def _timed_rank(rank, world, port, q):
     orc = Oracle(w.tables)
 
     def process(span, rin, cnt):
-        out = np.zeros(max(1, cnt), dtype=A.PKT_OUT)
+        out = np.zeros(max(1, cnt), dtype=A.PKT_RES)
         if cnt:
-            out = orc.process(span.numpy(), rin.numpy()[:cnt * A.PKT_IN.itemsize].view(A.PKT_IN),
-                              A.PKT_OUT)
+            out = orc.process(span.numpy(), rin.numpy()[:cnt * A.PKT_IN.itemsize].view(A.PKT_IN))
         return torch.from_numpy(out.view(np.uint8).copy())
     res = SH.timed_scatter_gather(w.inp, w.fresh_buf, process, rank, world, torch.device("cpu"),
-                                  A.PKT_IN.itemsize, A.PKT_OUT.itemsize, reps=2)
+                                  A.PKT_IN.itemsize, A.PKT_RES.itemsize, reps=2)
     q.put((rank, res))
     orc.close()
     dist.destroy_process_group()
