@@ -1996,15 +1996,20 @@ __device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_
   // walks start right after the pair context arrives
   const PairRec &PR = g.at<PairRec>(g.im.pair_recs)[pi];
   const VniRec &VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
+#ifdef DP_ONE_ACL_INDEX
+  constexpr int NW = 4;
+  Mbi m[NW] = {PR.ffl4, PR.acl4, PR.nsrc, VR.ndst};
+#else
   constexpr int NW = 5;
   Mbi m[NW] = {PR.ffl4, PR.acl4, PR.nsrc, VR.ndst, PR.acl4b};
+#endif
   uint32_t key[NW], e[NW];
   int rem0[NW];
   key[0] = mbi_key(S, m[0].field, true);
   key[1] = mbi_key(S, m[1].field, false);
   key[2] = S.v4src;
   key[3] = S.v4dst;
-  key[4] = mbi_key(S, m[4].field, false);
+  if constexpr (NW > 4) key[NW - 1] = mbi_key(S, m[NW - 1].field, false);
 #pragma unroll
   for (int k = 0; k < NW; k++) {
     rem0[k] = (int)m[k].kbits - (int)m[k].s0;
@@ -2013,13 +2018,16 @@ __device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_
   TRIP();
 #pragma unroll
   for (int l = 1; l <= 3; l++) {
-    if (!(e[0] & e[1] & e[2] & e[3] & e[4] & DPD_LEAF)) TRIP();
+    uint32_t all = DPD_LEAF;
+#pragma unroll
+    for (int k = 0; k < NW; k++) all &= e[k];
+    if (!all) TRIP();
 #pragma unroll
     for (int k = 0; k < NW; k++)
       if (!(e[k] & DPD_LEAF)) e[k] = g.at<uint32_t>(m[k].blocks)[(e[k] << 8) | ((key[k] >> (rem0[k] - 8 * l)) & 0xff)];
   }
   if (m[0].root) P.ffl = e[0] & ~DPD_LEAF;
-  if (m[1].root) P.acl = shorter_run(e[1] & ~DPD_LEAF, m[4].root ? e[4] & ~DPD_LEAF : NO_PRE);
+  if (m[1].root) P.acl = shorter_run(e[1] & ~DPD_LEAF, (NW > 4 && m[NW - 1].root) ? e[NW - 1] & ~DPD_LEAF : NO_PRE);
   if (m[2].root) P.nsrc = e[2] & ~DPD_LEAF;
   if (m[3].root) P.ndst = e[3] & ~DPD_LEAF;
 }
@@ -2547,7 +2555,10 @@ __device__ __forceinline__ dp_pkt_meta_t meta_of(const Img &g, const State &S) {
 // ---------------------------------------------------------------------------
 // FL: the flows variant -- FlowLookup on fc's table and the flow-aware
 // branches; fp receives the packet's flow and its flow-table effects.
-template <bool FL>
+// MT: the caller asked for PacketMeta records (pm); without them the values
+// only the meta record carries (vrf, dscp / ecn, nh_ref, ...) are dead and
+// the compiler drops them -- the transmit path keeps its registers.
+template <bool FL, bool MT>
 __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, lds_u8 *hs, uint8_t *buf, uint64_t buf_bytes,
                                   const dp_pkt_in_t &pin, dp_pkt_out_t &o, dp_pkt_meta_t *pm, int &fl0, int &fl1,
                                   bool inwin, const dpf::FlowCtx *fc, FlowPk &fp, uint32_t idx) {
@@ -2559,7 +2570,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   if (!frame_ok(pin, buf_bytes)) {
     // layout contract violated: never touch memory outside the buffer
     o = out_record(pin.off, pin.len, DP_DONE_INTERNAL_FAILURE);
-    if (pm) *pm = meta_none();
+    if constexpr (MT) *pm = meta_none();
     return o.done;
   }
   TS_DECL
@@ -2575,7 +2586,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   Hdr H;
   if (!parse(F, 0, H)) {
     o = out_record(pin.off, pin.len, DP_DONE_NOT_ETHERNET);
-    if (pm) *pm = meta_none();
+    if constexpr (MT) *pm = meta_none();
     return o.done;
   }
   o.off = pin.off; o.len = pin.len;
@@ -2660,7 +2671,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   o.oif = S.has_oif ? S.oif : 0;
   o.acl = S.acl;
   o.pad = 0;
-  if (pm) {
+  if constexpr (MT) {
     dp_pkt_meta_t m = meta_of(g, S);
     if constexpr (FL) if (fp.slot != dpf::kNoSlot) m.flow_ref = dpf::make_ref(fp.slot, fp.state);
     *pm = m;
@@ -2727,6 +2738,7 @@ __device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull
 
 // The flow-table effects of a wave's packets (FL only), wave-aggregated:
 // flow refs, invalidation marks and events, flow-dependent ACL verdicts.
+template <bool MT>
 __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, uint32_t i, const FlowPk &fp) {
   const int lane = threadIdx.x & 63;
   const bool has = live && fp.slot != dpf::kNoSlot;
@@ -2761,13 +2773,14 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
     if (sv) {
       dpf::SensRec *R = reinterpret_cast<dpf::SensRec *>(fc.sens + 8) + base + __popcll(ms & lanes_below(lane));
       *R = dpf::SensRec{i, fp.slot, fp.s_flags, fp.s_oif, fp.s_fib, fp.def_acl, fp.related, fp.related_tag,
-                        fp.s_dvni, fp.s_vrf, fp.s_nh, 0};
+                        MT ? fp.s_dvni : 0u, MT ? fp.s_vrf : 0u, MT ? fp.s_nh : NH_NONE, 0};
     }
   }
 }
 
-// FL: the flows variant (a flow table is attached to the context).
-template <bool FL>
+// FL: the flows variant (a flow table is attached to the context); MT: meta
+// records requested (meta != nullptr).
+template <bool FL, bool MT>
 __global__ void __launch_bounds__(TPB) DP_OCC
 dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict__ im, uint8_t *__restrict__ buf,
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
@@ -2798,12 +2811,12 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
     Img g{img_base, *im};
     dp_pkt_out_t o;
     lds_u8 *hs = (lds_u8 *)(hash_all + tid * HS);
-    dp_pkt_meta_t *pm = meta ? meta + i : nullptr;
-    if (all_fit) done_code = process_packet<FL>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, true, &fc, fp, i);
-    else done_code = process_packet<FL>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, false, &fc, fp, i);
+    dp_pkt_meta_t *pm = MT ? meta + i : nullptr;
+    if (all_fit) done_code = process_packet<FL, MT>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, true, &fc, fp, i);
+    else done_code = process_packet<FL, MT>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, false, &fc, fp, i);
     out[i] = o;
   }
-  if constexpr (FL) flow_effects(fc, live, i, fp);
+  if constexpr (FL) flow_effects<MT>(fc, live, i, fp);
   __syncthreads();
   // write-back: whole chunks by the wave, a partial tail by its owner
   wave_store_windows(buf, slab_wave, base, fl0 >> 4, fl1 >> 4);
@@ -2943,8 +2956,13 @@ extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uin
     const bool fit = (in[i].off & 15) + in[i].len <= (uint32_t)WIN && !(in[i].off & 1);
     FlowPk fp;
     dp_pkt_meta_t *pm = meta ? meta + i : nullptr;
-    if (fit) process_packet<false>(g, slab, hs, buf, buf_bytes, in[i], out[i], pm, fl0, fl1, true, nullptr, fp, i);
-    else process_packet<false>(g, slab, hs, buf, buf_bytes, in[i], out[i], pm, fl0, fl1, false, nullptr, fp, i);
+    if (pm) {
+      if (fit) process_packet<false, true>(g, slab, hs, buf, buf_bytes, in[i], out[i], pm, fl0, fl1, true, nullptr, fp, i);
+      else process_packet<false, true>(g, slab, hs, buf, buf_bytes, in[i], out[i], pm, fl0, fl1, false, nullptr, fp, i);
+    } else {
+      if (fit) process_packet<false, false>(g, slab, hs, buf, buf_bytes, in[i], out[i], pm, fl0, fl1, true, nullptr, fp, i);
+      else process_packet<false, false>(g, slab, hs, buf, buf_bytes, in[i], out[i], pm, fl0, fl1, false, nullptr, fp, i);
+    }
     if (fl1 > fl0) flush_range(buf + (in[i].off & ~15u), slab, fl0, fl1);
 #ifdef DP_TRIPS
     if (dp_trip_out)
@@ -2992,8 +3010,12 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_de
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
-  hipLaunchKernelGGL(dp_pipeline_kernel<false>, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                     buf_bytes, in, out, meta, n, part, dpf::FlowCtx{});
+  if (meta)
+    hipLaunchKernelGGL((dp_pipeline_kernel<false, true>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
+                       buf_bytes, in, out, meta, n, part, dpf::FlowCtx{});
+  else
+    hipLaunchKernelGGL((dp_pipeline_kernel<false, false>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
+                       buf_bytes, in, out, meta, n, part, dpf::FlowCtx{});
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));
@@ -3014,8 +3036,12 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
-  hipLaunchKernelGGL(dp_pipeline_kernel<true>, dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                     buf_bytes, in, out, meta, n, part, fc);
+  if (meta)
+    hipLaunchKernelGGL((dp_pipeline_kernel<true, true>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
+                       buf_bytes, in, out, meta, n, part, fc);
+  else
+    hipLaunchKernelGGL((dp_pipeline_kernel<true, false>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
+                       buf_bytes, in, out, meta, n, part, fc);
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));

@@ -28,12 +28,37 @@ def lib(variant: str = ""):
     return _libs[variant]
 
 
+_libc = C.CDLL(None)
+_libc.mprotect.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+
+
+def guarded_copy(buf: np.ndarray):
+    """A copy of `buf` that ends exactly at a PROT_NONE page (and has one in
+    front of its first page): any read or write past the burst buffer faults
+    on the host, as it would on the GPU.  Returns (mapping, view)."""
+    import mmap
+    pg = mmap.PAGESIZE
+    npg = max(1, (buf.nbytes + pg - 1) // pg)
+    m = mmap.mmap(-1, (npg + 2) * pg)
+    base = C.addressof(C.c_char.from_buffer(m))
+    if _libc.mprotect(base, pg, 0) or _libc.mprotect(base + (npg + 1) * pg, pg, 0):
+        raise OSError("mprotect failed")
+    v = np.frombuffer(m, dtype=np.uint8, count=buf.nbytes, offset=(npg + 1) * pg - buf.nbytes)
+    v[:] = buf
+    return m, v
+
+
 def process(tables_ptr, buf: np.ndarray, inp: np.ndarray, variant: str = ""):
-    """The kernel body over one burst, in place: PKT_RES records."""
+    """The kernel body over one burst, in place: PKT_RES records.  The body
+    runs on a guard-paged copy of the buffer (guarded_copy)."""
     out = np.zeros(len(inp), dtype=A.PKT_OUT)
     meta = np.zeros(len(inp), dtype=A.PKT_META)
-    rc = lib(variant).dpemu_process(C.cast(tables_ptr, C.c_void_p), buf.ctypes.data, buf.nbytes,
+    keep, g = guarded_copy(buf)
+    rc = lib(variant).dpemu_process(C.cast(tables_ptr, C.c_void_p), g.ctypes.data, buf.nbytes,
                                     inp.ctypes.data, out.ctypes.data, meta.ctypes.data, len(inp))
+    buf[:] = g
+    del g
+    keep.close()
     if rc != 0:
         raise RuntimeError(f"emu rejected tables rc={rc}")
     return A.join_results(out, meta)

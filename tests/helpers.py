@@ -50,6 +50,15 @@ def common_fields(a, b):
     return a[names], b[names]
 
 
+def field_diff(a, b, k):
+    """Indices of records whose field k differs (array fields such as nh_addr
+    compare whole rows)."""
+    d = a[k] != b[k]
+    if d.ndim > 1:
+        d = d.reshape(len(d), -1).any(axis=1)
+    return d
+
+
 def hist(out):
     h = np.bincount(out["done"].astype(np.int64), minlength=256)
     return {A.DONE_NAMES[i] if i < A.DONE_COUNT else str(i): int(c) for i, c in enumerate(h) if c}

@@ -10,6 +10,7 @@ from oracle.pyoracle import Oracle
 
 from edgecase import pack_burst
 from flowgen import frames_of
+from helpers import field_diff
 from mbufpool import HEADROOM, FakeMempool
 
 pytestmark = pytest.mark.gpu
@@ -47,7 +48,7 @@ def test_gpu_mbuf_burst(nf, cfg):
     keep = np.arange(len(frames)) != 5
     for k in ("done", "acl", "meta_flags", "oif", "dst_vni", "src_vni", "fib_entry", "acl_rule",
               "vrf", "pm_flags", "dscp", "ecn", "nh_family", "nh_addr"):
-        bad = np.nonzero((out[k] != oout[k]) & keep)[0]
+        bad = np.nonzero(field_diff(out, oout, k) & keep)[0]
         assert len(bad) == 0, f"{k} differs at {bad[:5]}: {out[bad[:1]]} vs {oout[bad[:1]]}"
     deliv = np.nonzero((oout["done"] == A.DONE["Delivered"]) & keep)[0]
     assert len(deliv) > len(frames) // 2
@@ -114,7 +115,7 @@ def test_gpu_mbuf_burst_with_flows(nf):
         nf.attach_flows(None)
     for k in ("done", "acl", "meta_flags", "oif", "dst_vni", "src_vni", "fib_entry", "acl_rule",
               "vrf", "pm_flags", "dscp", "ecn", "nh_family", "nh_addr"):
-        bad = np.nonzero(out[k] != oout[k])[0]
+        bad = np.nonzero(field_diff(out, oout, k))[0]
         assert len(bad) == 0, f"{k} differs at {bad[:5]}"
     for i in np.nonzero(oout["done"] == A.DONE["Delivered"])[0]:
         o, ln = int(oout[i]["off"]), int(oout[i]["len"])

@@ -136,9 +136,10 @@ def test_gpu_host_paths_pinned(nf, mode):
     pi = pinned(w.inp.nbytes).view(A.PKT_IN)
     pi[:] = w.inp
     po = pinned(w.n * A.PKT_OUT.itemsize).view(A.PKT_OUT)
+    pm = pinned(w.n * A.PKT_META.itemsize).view(A.PKT_META)
     nf.set_host_path(m)
     try:
-        o = nf.process_arrays(pb, pi, out=po)
+        o = nf.process_arrays(pb, pi, out=po, meta=pm)
     finally:
         nf.set_host_path(A.HOST_AUTO)
     compare(o_ref, b_ref, o, pb, w.inp, f"host path {mode}")
