@@ -59,11 +59,34 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def physical_cores(cpus) -> int:
+    """Physical cores among the logical CPUs `cpus` (SMT siblings counted
+    once), from /sys topology; len(cpus) if unreadable."""
+    seen = set()
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            seen.add((open(base + "physical_package_id").read().strip(),
+                      open(base + "core_id").read().strip()))
+        except OSError:
+            return len(cpus)
+    return len(seen) or len(cpus)
+
+
+def cpu_share() -> int:
+    """The CPU share this job may load: OMP_NUM_THREADS when the launcher
+    sets it (the GPU box sets 16, its per-GPU share -- nproc there shows the
+    whole machine), else unlimited."""
+    try:
+        return max(1, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        return 1 << 30
+
+
 def cpu_threads() -> int:
-    """Host threads for the CPU baseline: one per CPU this process may run
-    on, capped at the GPU box's per-GPU CPU share (16; the box's nproc shows
-    the whole machine)."""
-    return max(1, min(16, len(os.sched_getaffinity(0))))
+    """Host threads for the CPU baseline: one per physical
+    core of the affinity mask, within the job's CPU share."""
+    return max(1, min(cpu_share(), physical_cores(sorted(os.sched_getaffinity(0)))))
 
 
 def _time_cpu(run, n: int, budget_s: float, max_reps: int) -> tuple:
@@ -123,11 +146,15 @@ def cpu_baseline(w: Workload, sample: int, budget_s: float) -> dict:
     emu_n, ereps, t_emu = _time_cpu(emu_run(ne, threads), ne, budget_s / 2, 20)
     emu_1, _, _ = _time_cpu(emu_run(ne // 8, 1), ne // 8, budget_s / 4, 3)
     emu.close()
+    aff = sorted(os.sched_getaffinity(0))
     return {"value": round(port_n, 4), "unit": "Mpps", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "value_1_thread": round(port_1, 4),
+            "threads_rule": f"one per physical core of the affinity mask ({physical_cores(aff)} "
+                            f"physical / {len(aff)} logical CPUs) within the job's CPU share "
+                            f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')})",
             "sample": f"{reps} x {n} packets of the same workload, bursts of 64, C++ restatement "
-                      f"of the reference pipeline (oracle/), {t_port:.1f} s on {threads} threads "
-                      f"(the box's per-GPU CPU share); value_1_thread over {n1} packets",
+                      f"of the reference pipeline (oracle/), {t_port:.1f} s on {threads} threads; "
+                      f"value_1_thread over {n1} packets",
             "compiled": {"value": round(emu_n, 3), "unit": "Mpps", "cores": threads,
                          "value_1_thread": round(emu_1, 3),
                          "what": "the kernel's per-packet body compiled for the host (tests/emu, "

@@ -99,6 +99,12 @@ constexpr uint8_t DONE_NONE = 255;
 #else
 #define DP_COLD __attribute__((noinline))
 #endif
+// the bit-vector classifier (classify_bv): out of line unless DP_BV_INLINE
+#if defined(DP_BV_INLINE) && !defined(DP_EMU_OUTLINE)
+#define DP_BV __forceinline__
+#else
+#define DP_BV DP_COLD
+#endif
 
 // ---------------------------------------------------------------------------
 // Image access
@@ -976,7 +982,7 @@ __device__ __forceinline__ bool pfx_ok(Key128 k, uint64_t ahi, uint64_t alo, uin
 // common one.  Every argument is a value or a pointer into the table image
 // (global memory): nothing of the caller's private frame or LDS crosses the
 // call (DESIGN.md "Out-of-line device functions").
-__device__ DP_COLD int64_t classify_bv(const uint8_t *base, const Group *Gp, uint8_t proto, Key128 src,
+__device__ DP_BV int64_t classify_bv(const uint8_t *base, const Group *Gp, uint8_t proto, Key128 src,
                                        Key128 dst, uint16_t sp, uint16_t dp) {
   const ImgBase g{base};
   const Group G = *Gp;
@@ -1996,10 +2002,12 @@ __device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_
   // walks start right after the pair context arrives
   const PairRec &PR = g.at<PairRec>(g.im.pair_recs)[pi];
   const VniRec &VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
-#ifdef DP_ONE_ACL_INDEX
+#ifndef DP_TWO_ACL_INDEX
   constexpr int NW = 4;
   Mbi m[NW] = {PR.ffl4, PR.acl4, PR.nsrc, VR.ndst};
 #else
+  // experiment (negative results): a fifth walk over the ACL
+  // group's second list index, verifying the shorter run
   constexpr int NW = 5;
   Mbi m[NW] = {PR.ffl4, PR.acl4, PR.nsrc, VR.ndst, PR.acl4b};
 #endif

@@ -496,7 +496,12 @@ Classifier build_classifier(ImgBuf &ib, const std::vector<CRule> &rules, int fam
       // (the lookup verifies the shorter of the two runs a packet selects:
       // both hold every rule that can match it, in precedence order)
       int lf2 = -1;
-      if (kind == 0 && fam == 4 && form != 2)
+#ifdef DP_TWO_ACL_INDEX
+      const bool second = true;
+#else
+      const bool second = false;  // measured slower: off
+#endif
+      if (second && kind == 0 && fam == 4 && form != 2)
         for (int f = 0; f < 4; f++)
           if (f != lf && lmax[f] <= DPD_RUN_MAX && bnd[f].size() > 16 && (lf2 < 0 || lmean[f] < lmean[lf2]))
             lf2 = f;
