@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 HEADROOM = 96
 
 # DoneReason (net/src/packet/meta.rs:84-119)
@@ -99,8 +99,14 @@ FLOW = np.dtype([("key", FLOW_KEY), ("dst_vni", "<u4"), ("flags", "<u4"), ("pad"
                  ("genid", "<i8"), ("expires_at", "<u8")], align=True)
 FLOW_INFO = np.dtype([("ref", "<u8"), ("status", "<u4"), ("flags", "<u4"), ("dst_vni", "<u4"),
                       ("pad", "<u4"), ("genid", "<i8"), ("expires_at", "<u8"),
-                      ("related", "<u8")])
-assert FLOW_KEY.itemsize == 44 and FLOW.itemsize == 72 and FLOW_INFO.itemsize == 48
+                      ("related", "<u8"), ("pf", "u1"), ("pf_status", "u1"), ("pf_port", "<u2"),
+                      ("pf_rule", "<u4"), ("pf_family", "u1"), ("pad2", "u1", (7,)),
+                      ("pf_ip", "u1", (16,))])
+assert FLOW_KEY.itemsize == 44 and FLOW.itemsize == 72 and FLOW_INFO.itemsize == 80
+# enum dp_pf_action / dp_nat_flow_status (include/dpgpu.h)
+PF_NONE, PF_DST_NAT, PF_SRC_NAT = 0, 1, 2
+(NFS_ONE_WAY, NFS_TWO_WAY, NFS_ESTABLISHED, NFS_RESET, NFS_C_CLOSING, NFS_S_CLOSING,
+ NFS_C_HALF_CLOSE, NFS_S_HALF_CLOSE, NFS_LAST_ACK, NFS_CLOSED) = range(10)
 
 
 class IpAddr(C.Structure):
@@ -189,6 +195,13 @@ def _arr(t):
     return [("%s" % t[0], C.POINTER(t[1])), ("n_%s" % t[0], t[2])]
 
 
+class PortFwRule(C.Structure):
+    _fields_ = [("src_vni", C.c_uint32), ("proto", C.c_uint8), ("pad", C.c_uint8 * 3),
+                ("dst_vni", C.c_uint32), ("ext_lo", C.c_uint16), ("ext_hi", C.c_uint16),
+                ("int_lo", C.c_uint16), ("int_hi", C.c_uint16), ("init_timeout_s", C.c_uint32),
+                ("estab_timeout_s", C.c_uint32), ("ext_prefix", Prefix), ("int_prefix", Prefix)]
+
+
 class TablesDesc(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("pad0", C.c_uint32), ("genid", C.c_int64),
                 ("fibs", C.POINTER(Fib)), ("n_fibs", C.c_uint32),
@@ -209,14 +222,16 @@ class TablesDesc(C.Structure):
                 ("nat_tables", C.POINTER(NatTable)), ("n_nat_tables", C.c_uint32),
                 ("nat_entries", C.POINTER(NatEntry)), ("n_nat_entries", C.c_uint32),
                 ("nat_port_ranges", C.POINTER(PortRange)), ("n_nat_port_ranges", C.c_uint32),
-                ("nat_ranges", C.POINTER(NatRange)), ("n_nat_ranges", C.c_uint32)]
+                ("nat_ranges", C.POINTER(NatRange)), ("n_nat_ranges", C.c_uint32),
+                ("portfw", C.POINTER(PortFwRule)), ("n_portfw", C.c_uint32)]
 
 
 STRUCTS = dict(dp_ipaddr_t=IpAddr, dp_prefix_t=Prefix, dp_fib_t=Fib, dp_vni_fib_t=VniFib,
                dp_instr_t=Instr, dp_fib_entry_t=FibEntry, dp_route_nh_t=RouteNh,
                dp_route_t=Route, dp_iface_t=Iface, dp_adjacency_t=Adjacency, dp_rule_t=Rule,
                dp_acl_default_t=AclDefault, dp_nat_table_t=NatTable, dp_nat_entry_t=NatEntry,
-               dp_port_range_t=PortRange, dp_nat_range_t=NatRange, dp_tables_desc_t=TablesDesc)
+               dp_port_range_t=PortRange, dp_nat_range_t=NatRange, dp_portfw_rule_t=PortFwRule,
+               dp_tables_desc_t=TablesDesc)
 
 # every symbol include/dpgpu.h declares
 GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_publish",
@@ -242,6 +257,7 @@ MBUF_LAYOUT_DPDK = MbufLayout(0, 16, 20, 22, 36, 40, 54, 0)  # DP_MBUF_LAYOUT_DP
 
 # dp_ctx_set_option (include/dpgpu.h)
 OPT_HOST_PATH = 1
+OPT_CLOCK = 2
 HOST_AUTO, HOST_COPY, HOST_ZERO_COPY = 0, 1, 2
 
 _VP = C.c_void_p

@@ -78,6 +78,7 @@ class TablesBuilder:
         self.nat_entries: List[A.NatEntry] = []
         self.nat_prs: List[A.PortRange] = []
         self.nat_ranges: List[A.NatRange] = []
+        self.portfw: List[A.PortFwRule] = []
         self._keep = []
 
     # -- routing --------------------------------------------------------------
@@ -198,6 +199,22 @@ class TablesBuilder:
                                             gate=gate, src=src_prefix, sports=sports,
                                             priority=(plen + 1) << 1, action=src_nat))
 
+    # -- port forwarding -------------------------------------------------------
+    def add_portfw(self, src_vni: int, proto: int, dst_vni: int, ext_prefix: str, int_prefix: str,
+                   ext_ports, int_ports, init_timeout_s: int = 0, estab_timeout_s: int = 0) -> None:
+        """PortFwEntry::new(PortFwKey(src_vpcd, proto), dst_vpcd, ext, int, ext_ports,
+        int_ports, init, estab) (nat/src/portfw/portfwtable/objects.rs:70-103);
+        proto 6 (TCP) or 17 (UDP), timeouts in seconds (0: the defaults)."""
+        r = A.PortFwRule()
+        r.src_vni, r.proto, r.dst_vni = src_vni, proto, dst_vni
+        r.ext_lo, r.ext_hi = ext_ports
+        r.int_lo, r.int_hi = int_ports
+        r.init_timeout_s, r.estab_timeout_s = init_timeout_s, estab_timeout_s
+        # Prefix::from_str keeps the host bits out (70.71.72.70/24 is 70.71.72.0/24)
+        r.ext_prefix = mk_prefix(str(ipaddress.ip_network(ext_prefix, strict=False)))
+        r.int_prefix = mk_prefix(str(ipaddress.ip_network(int_prefix, strict=False)))
+        self.portfw.append(r)
+
     # -- static NAT -------------------------------------------------------------
     def add_nat_table(self, kind: int, src_vni: int, dst_vni: int,
                       entries: Sequence[dict]) -> None:
@@ -265,5 +282,6 @@ class TablesBuilder:
         d.nat_entries, d.n_nat_entries = self._arr(A.NatEntry, self.nat_entries)
         d.nat_port_ranges, d.n_nat_port_ranges = self._arr(A.PortRange, self.nat_prs)
         d.nat_ranges, d.n_nat_ranges = self._arr(A.NatRange, self.nat_ranges)
+        d.portfw, d.n_portfw = self._arr(A.PortFwRule, self.portfw)
         self._desc = d
         return C.pointer(d)

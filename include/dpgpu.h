@@ -14,8 +14,10 @@
  * dp_process_burst*() runs that whole block for a burst, on the GPU.  The
  * FlowTable FlowLookup and IcmpErrorHandler consult is a device flow table
  * attached to the context (dp_ctx_attach_flow_table; none attached = an
- * empty table).  Masquerade / port-forwarding exposes are
- * refused at publish: PortForwarder and Masquerade are identity.
+ * empty table).  PortForwarder runs on the GPU over the
+ * port-forwarding rules of the tables (dp_portfw_rule_t) and creates its flow
+ * pairs in the attached flow table; masquerade exposes are refused at
+ * publish.
  *
  * A Rust `GpuPathNf: NetworkFunction` materialises the burst
  * exactly like FlowFilter::process does (flow-filter/src/lib.rs:357-362),
@@ -45,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DPGPU_ABI_VERSION 2u
+#define DPGPU_ABI_VERSION 3u
 
 /* Bytes every frame must have in front of it (its own scratch, owned by the
  * packet).  Output headers are written in place into this headroom: VXLAN
@@ -367,6 +369,29 @@ typedef struct dp_nat_range {
     uint64_t offset;
 } dp_nat_range_t;
 
+/* Port-forwarding rule: PortFwEntry (nat/src/portfw/portfwtable/objects.rs:
+ * 30-39, checks of PortFwEntry::new :70-155).  A publish applies the rule set
+ * as PortFwTable::update does (:284-300): a rule that `matches` one of the
+ * previous generation on the same device (same key, prefixes, port ranges and
+ * destination VPC) is that same entry -- flows that refer to it stay valid
+ * (their Weak upgrades) and only its timeouts change; rules no longer present
+ * are gone; a new rule whose external range overlaps another of the same key
+ * and external prefix is skipped (RangeSet overlap error, logged by the
+ * reference).  Each entry has an id (dp_flow_info_t.pf_rule), stable while it
+ * lives. */
+typedef struct dp_portfw_rule {
+    uint32_t src_vni;          /* PortFwKey.src_vpcd */
+    uint8_t proto;             /* PortFwKey.proto: 6 (TCP) or 17 (UDP) */
+    uint8_t pad[3];
+    uint32_t dst_vni;          /* dst_vpcd (!= src_vni) */
+    uint16_t ext_lo, ext_hi;   /* ext_ports: non-zero, ext_lo <= ext_hi */
+    uint16_t int_lo, int_hi;   /* int_ports: same length */
+    uint32_t init_timeout_s;   /* 0: PortFwEntry::DEFAULT_INITIAL_TOUT (10 s) */
+    uint32_t estab_timeout_s;  /* 0: 30 min (TCP) / 30 s (UDP) */
+    dp_prefix_t ext_prefix;    /* external prefix (what the client addresses) */
+    dp_prefix_t int_prefix;    /* internal prefix (same family and length) */
+} dp_portfw_rule_t;
+
 typedef struct dp_tables_desc {
     uint32_t abi_version;   /* DPGPU_ABI_VERSION */
     uint32_t pad0;
@@ -394,6 +419,8 @@ typedef struct dp_tables_desc {
     const dp_nat_entry_t *nat_entries; uint32_t n_nat_entries;
     const dp_port_range_t *nat_port_ranges; uint32_t n_nat_port_ranges;
     const dp_nat_range_t *nat_ranges; uint32_t n_nat_ranges;
+
+    const dp_portfw_rule_t *portfw;  uint32_t n_portfw;
 } dp_tables_desc_t;
 
 /* ------------------------------------------------------------------------ */
@@ -403,7 +430,7 @@ typedef struct dp_tables_desc {
 #define DP_EINVAL (-22)
 #define DP_ENOMEM (-12)
 #define DP_ENODEV (-19)
-#define DP_ENOTSUP (-95)   /* e.g. masquerade / port-forwarding NAT modes */
+#define DP_ENOTSUP (-95)   /* e.g. masquerade NAT modes */
 #define DP_EIO (-5)        /* HIP runtime failure */
 #define DP_ENOTABLES (-61) /* no tables published yet (ENODATA) */
 
@@ -494,7 +521,13 @@ enum dp_ctx_option {
      *                     records over PCIe and writes the rewritten header
      *                     spans and records back in place; a burst that does
      *                     not qualify fails with DP_EINVAL. */
-    DP_OPT_HOST_PATH = 1
+    DP_OPT_HOST_PATH = 1,
+    /* The flow clock (nanoseconds, the caller's clock -- the unit of
+     * dp_flow_t.expires_at and dp_flow_sweep's `now`): Instant::now() for the
+     * bursts that follow.  PortForwarder sets the expiry of the flows it
+     * creates or refreshes to now + the rule's timeout
+     * (flow_state.rs:233-263, flow_info.rs:399-407). */
+    DP_OPT_CLOCK = 2
 };
 enum dp_host_path { DP_HOST_AUTO = 0, DP_HOST_COPY = 1, DP_HOST_ZERO_COPY = 2 };
 int dp_ctx_set_option(dp_ctx_t *ctx, int option, int64_t value);
@@ -507,9 +540,9 @@ int dp_ctx_set_option(dp_ctx_t *ctx, int option, int64_t value);
 /* (flow-filter/src/lib.rs:115-349) and AclFilter (acl-filter/src/lib.rs:    */
 /* 62-138) for every context it is attached to.                              */
 /*                                                                           */
-/* Flows carry no masquerade / port-forwarding state (that is §8f rank 3):   */
-/* FlowInfoLocked.nat_state and .port_fw_state are always None, and every    */
-/* flow has a destination VPC.                                               */
+/* Flows carry no masquerade state (FlowInfoLocked.nat_state is None); the  */
+/* port-forwarding state (.port_fw_state) of the flow pairs PortForwarder     */
+/* creates is carried, and every flow has a destination VPC.                 */
 /*                                                                           */
 /* Burst semantics are the reference pipeline's: FlowLookup, the flow-filter */
 /* bypass decision and IcmpErrorHandler see flow states as they were when    */
@@ -561,6 +594,14 @@ typedef struct dp_flow {
 
 /* A flow as stored.  `ref` names one stored FlowInfo (slot + fill tag); a
  * flow replaced or removed from the table no longer matches its ref. */
+/* PortFwState.action (nat/src/common/mod.rs:14-19) */
+enum dp_pf_action { DP_PF_NONE = 0, DP_PF_DST_NAT = 1, DP_PF_SRC_NAT = 2 };
+/* NatFlowStatus (nat/src/common/mod.rs:34-45), shared by the two flows of a
+ * port-forwarded pair */
+enum dp_nat_flow_status { DP_NFS_ONE_WAY = 0, DP_NFS_TWO_WAY = 1, DP_NFS_ESTABLISHED = 2,
+                          DP_NFS_RESET = 3, DP_NFS_C_CLOSING = 4, DP_NFS_S_CLOSING = 5,
+                          DP_NFS_C_HALF_CLOSE = 6, DP_NFS_S_HALF_CLOSE = 7,
+                          DP_NFS_LAST_ACK = 8, DP_NFS_CLOSED = 9 };
 typedef struct dp_flow_info {
     uint64_t ref;             /* DP_FLOW_NONE: not found */
     uint32_t status;          /* enum dp_flow_status */
@@ -570,6 +611,14 @@ typedef struct dp_flow_info {
     int64_t genid;
     uint64_t expires_at;
     uint64_t related;         /* ref of the related flow (FlowInfo.related), DP_FLOW_NONE */
+    /* FlowInfoLocked.port_fw_state (nat/src/portfw/flow_state.rs:29-35) */
+    uint8_t pf;               /* enum dp_pf_action (DP_PF_NONE: no state) */
+    uint8_t pf_status;        /* enum dp_nat_flow_status */
+    uint16_t pf_port;         /* use_port */
+    uint32_t pf_rule;         /* id of the PortFwEntry its Weak names (dp_portfw_rule_t) */
+    uint8_t pf_family;        /* use_ip family */
+    uint8_t pad2[7];
+    uint8_t pf_ip[16];        /* use_ip */
 } dp_flow_info_t;
 #define DP_FLOW_NONE UINT64_MAX
 

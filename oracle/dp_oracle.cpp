@@ -270,6 +270,31 @@ struct Meta {
   uint8_t acl = 0;
 };
 
+// FlowKey (net/src/flows/flow_key.rs:457-463) as a comparable value.  Its Hash
+// covers (src_vpcd, src_ip, src_port, dst_ip, dst_port) and its Eq the whole
+// key; the TCP/UDP port Eq is symmetric (flow_key.rs:57-60, 123-127) but a
+// port-swapped key hashes elsewhere, so a lookup matches the key exactly.
+struct FKey {
+  uint32_t vni = 0;
+  uint8_t fam = 0, kind = 0;
+  uint16_t sp = 0, dp = 0;
+  uint8_t src[16] = {0}, dst[16] = {0};
+  bool operator==(const FKey &o) const {
+    return vni == o.vni && fam == o.fam && kind == o.kind && sp == o.sp && dp == o.dp &&
+           memcmp(src, o.src, 16) == 0 && memcmp(dst, o.dst, 16) == 0;
+  }
+};
+struct FKeyHash {
+  size_t operator()(const FKey &k) const {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void *p, size_t n) {
+      for (size_t i = 0; i < n; i++) { h ^= ((const uint8_t *)p)[i]; h *= 1099511628211ull; }
+    };
+    mix(&k.vni, 4); mix(&k.fam, 1); mix(&k.kind, 1); mix(&k.sp, 2); mix(&k.dp, 2);
+    mix(k.src, 16); mix(k.dst, 16);
+    return (size_t)h;
+  }
+};
 struct Packet {
   Headers h;
   uint8_t *buf;
@@ -277,6 +302,8 @@ struct Packet {
   uint64_t room_start;          // first byte this packet may write
   Meta m;
   int64_t flow = -1;            // PacketMeta.flow_info (a flow of the oracle's table)
+  bool has_ikey = false;        // PacketMeta.flow_key: the key before static NAT
+  FKey ikey;                    // (flow-filter/src/lib.rs:193-201)
   void done(int r) { if (m.done < 0) m.done = r; }
   void done_force(int r) { m.done = r; }
   bool is_done() const { return m.done >= 0; }
@@ -1024,6 +1051,13 @@ struct NatTable {
   std::vector<NatEntry> entries;
 };
 
+// PortFwEntry (nat/src/portfw/portfwtable/objects.rs:30-39) and its id
+struct PfRule {
+  dp_portfw_rule_t r;
+  uint32_t id;
+  uint64_t init_ns, estab_ns;  // init_timeout / estab_timeout
+};
+
 struct MacKey {
   uint32_t ifindex;
   Ip ip;
@@ -1051,43 +1085,28 @@ struct dpo_tables {
   std::vector<Rule> ffr4, ffl4, ffr6, ffl6;
   std::map<uint32_t, NatTable> nat_dst;                          // src_vni
   std::map<std::pair<uint32_t, uint32_t>, NatTable> nat_src;     // (src_vni, dst_vni)
+  std::vector<PfRule> pf;   // PortFwTable entries (ids stable across generations)
+  uint32_t pf_next_id = 1;  // the lineage's next entry id
 };
 
 namespace {
-// FlowKey (net/src/flows/flow_key.rs:457-463) as a comparable value.  Its Hash
-// covers (src_vpcd, src_ip, src_port, dst_ip, dst_port) and its Eq the whole
-// key; the TCP/UDP port Eq is symmetric (flow_key.rs:57-60, 123-127) but a
-// port-swapped key hashes elsewhere, so a lookup matches the key exactly.
-struct FKey {
-  uint32_t vni = 0;
-  uint8_t fam = 0, kind = 0;
-  uint16_t sp = 0, dp = 0;
-  uint8_t src[16] = {0}, dst[16] = {0};
-  bool operator==(const FKey &o) const {
-    return vni == o.vni && fam == o.fam && kind == o.kind && sp == o.sp && dp == o.dp &&
-           memcmp(src, o.src, 16) == 0 && memcmp(dst, o.dst, 16) == 0;
-  }
-};
-struct FKeyHash {
-  size_t operator()(const FKey &k) const {
-    uint64_t h = 1469598103934665603ull;
-    auto mix = [&](const void *p, size_t n) {
-      for (size_t i = 0; i < n; i++) { h ^= ((const uint8_t *)p)[i]; h *= 1099511628211ull; }
-    };
-    mix(&k.vni, 4); mix(&k.fam, 1); mix(&k.kind, 1); mix(&k.sp, 2); mix(&k.dp, 2);
-    mix(k.src, 16); mix(k.dst, 16);
-    return (size_t)h;
-  }
-};
-// FlowInfo (net/src/flows/flow_info.rs:189-199) without masquerade / port-
-// forwarding state; `related` is the Weak of related_pair, alive while the
-// related flow is in the table.
+// FlowInfo (net/src/flows/flow_info.rs:189-199) without masquerade state;
+// `related` is the Weak of related_pair, alive while the related flow is in
+// the table.  The port-forwarding state (PortFwState, nat/src/portfw/
+// flow_state.rs:29-35): action, use_ip / use_port, the rule's Weak (an entry
+// id, alive while the tables hold that entry) and the NatFlowStatus shared
+// with the related flow (an index into dpo_flows::nfs).
 struct OFlow {
   dp_flow_t d{};
   FKey key;
   uint32_t status = DP_FLOW_DETACHED;
   int64_t related = -1;
   bool in_table = false;
+  uint8_t pf = DP_PF_NONE;
+  int64_t pf_status = -1;
+  Ip pf_ip;
+  uint16_t pf_port = 0;
+  uint32_t pf_rule = 0;
 };
 }  // namespace
 
@@ -1096,6 +1115,8 @@ struct dpo_flows {
   std::vector<OFlow> f;                                 // every FlowInfo ever made (ref = index)
   std::unordered_map<FKey, uint64_t, FKeyHash> map;     // the table
   uint64_t capacity = 10000000;                         // FlowTable::DEFAULT_CAPACITY
+  std::vector<uint8_t> nfs;                             // AtomicNatFlowStatus cells
+  uint64_t now = 0;                                     // Instant::now() (ns, DP_OPT_CLOCK)
 };
 
 namespace {
@@ -1519,11 +1540,12 @@ void stage_flow_lookup(const dpo_flows *FL, Packet &p) {
   if (packet_flow_key(p, k)) p.flow = flow_find(FL, k);
 }
 // FlowSummary::from_meta (flow-filter/src/lib.rs:380-398): every stored flow
-// has a destination VPC and neither masquerade nor port-forwarding state.
+// has a destination VPC and no masquerade state.
 struct FlowSummary {
   bool present = false;
   int64_t genid = 0;
   uint32_t dst_vni = 0;
+  bool needs_pf = false;
 };
 
 // FlowFilter (flow-filter/src/lib.rs:75-246, context/tables.rs:800-915), in
@@ -1531,6 +1553,7 @@ struct FlowSummary {
 // the burst, then apply_route (C) for every packet.
 struct FfWork {
   bool lookup = false;
+  uint8_t gate = 0;  // SourceGate of the local lookup (1: PortFwdReply)
   FlowSummary fs;
   int64_t ri = -1, li = -1;  // remote / local rule (-1: miss)
 };
@@ -1539,16 +1562,20 @@ void ff_classify(const dpo_tables &T, const dpo_flows *FL, Packet &p, FfWork &w)
   if (p.is_done() || !p.overlay() || p.m.dst_vni) return;
   if (FL && p.flow >= 0) {
     const OFlow &f = FL->f[p.flow];
-    w.fs = FlowSummary{true, f.d.genid, f.d.dst_vni};
+    w.fs = FlowSummary{true, f.d.genid, f.d.dst_vni, f.pf != DP_PF_NONE};
     // dst_vpcd_from_valid_flow (lib.rs:327-349) -> tag_for_bypass (:213-231)
     if (f.status == DP_FLOW_ACTIVE && f.d.genid >= T.genid) {
       p.m.dst_vni = f.d.dst_vni;
+      if (w.fs.needs_pf) p.m.flags |= DP_META_REQ_PORT_FORWARDING;
       if (f.d.flags & DP_FLOW_REQ_STATIC_NAT_SRC) p.m.flags |= DP_META_REQ_STATIC_NAT_SRC;
       if (f.d.flags & DP_FLOW_REQ_STATIC_NAT_DST) p.m.flags |= DP_META_REQ_STATIC_NAT_DST;
       return;
     }
-    // flow_revalidation_data (:296-325): without masquerade / port-forwarding
-    // state it is (None, Ungated) -- the regular lookup below
+    // flow_revalidation_data (:296-325): the reply flow of a port-forwarded
+    // pair is revalidated against the local rules gated on PortFwdReply
+    if (f.status == DP_FLOW_ACTIVE && f.d.genid < T.genid && !(f.d.flags & DP_FLOW_INITIATOR) &&
+        w.fs.needs_pf)
+      w.gate = 1;
   }
   if (p.h.net == 0) { p.done(DP_DONE_NOT_IP); return; }
   if (!p.m.src_vni) { p.done(DP_DONE_UNROUTABLE); return; }
@@ -1565,7 +1592,7 @@ void ff_classify(const dpo_tables &T, const dpo_flows *FL, Packet &p, FfWork &w)
   Key k{proto, p.m.src_vni, 0 /* GateVni: dst_vpcd None */, 0, zero16, dst, 0, dpp};
   w.ri = classify(rem, k, p.h.net);
   if (w.ri < 0) return;  // DestinationMiss
-  Key k2{proto, p.m.src_vni, rem[w.ri].r.action, 0 /* SourceGate::Ungated */, src, zero16, sp, 0};
+  Key k2{proto, p.m.src_vni, rem[w.ri].r.action, w.gate, src, zero16, sp, 0};
   w.li = classify(loc, k2, p.h.net);
 }
 void ff_apply(const dpo_tables &T, dpo_flows *FL, Packet &p, const FfWork &w) {
@@ -1588,10 +1615,19 @@ void ff_apply(const dpo_tables &T, dpo_flows *FL, Packet &p, const FfWork &w) {
   };
   apply(src_nat, DP_META_REQ_STATIC_NAT_SRC);
   apply(dst_nat, DP_META_REQ_STATIC_NAT_DST);
+  // the key before static NAT, for the flows port forwarding / masquerade
+  // create (lib.rs:193-201)
+  const uint32_t stat = DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST;
+  if ((p.m.flags & (DP_META_REQ_PORT_FORWARDING | DP_META_REQ_MASQUERADE)) && (p.m.flags & stat))
+    p.has_ikey = packet_flow_key(p, p.ikey);
   // should_invalidate_flow (lib.rs:258-294): a flow of another generation is
-  // outdated -- a different destination, or (no masquerade / port-forwarding
-  // requirement) no longer needed
-  if (w.fs.present && w.fs.genid != T.genid) flow_invalidate_pair(FL, p.flow);
+  // outdated if its destination or its NAT requirements differ, or if none
+  // of its stateful NAT is still required
+  if (w.fs.present && w.fs.genid != T.genid) {
+    const bool pf = p.m.flags & DP_META_REQ_PORT_FORWARDING, masq = p.m.flags & DP_META_REQ_MASQUERADE;
+    if (w.fs.dst_vni != p.m.dst_vni || masq || pf != w.fs.needs_pf || !pf)
+      flow_invalidate_pair(FL, p.flow);
+  }
 }
 
 // AclFilter (acl-filter/src/lib.rs:51-152)
@@ -1749,13 +1785,310 @@ void stage_static_nat(const dpo_tables &T, Packet &p) {
   if (modified) p.m.flags |= DP_META_REFR_CHKSUM;
 }
 
+
+// ---------------------------------------------------------------------------
+// Port forwarding (nat/src/portfw/)
+// ---------------------------------------------------------------------------
+int32_t flow_insert_one(dpo_flows *FL, const dp_flow_t &d, int64_t partner, int64_t &ref);
+
+bool same_prefix(const dp_prefix_t &a, const dp_prefix_t &b) {
+  return a.family == b.family && a.len == b.len && memcmp(a.addr, b.addr, a.family == 4 ? 4 : 16) == 0;
+}
+// PortFwEntry::matches (objects.rs:159-166): everything but the timeouts
+bool pf_matches(const dp_portfw_rule_t &a, const dp_portfw_rule_t &b) {
+  return a.src_vni == b.src_vni && a.proto == b.proto && same_prefix(a.ext_prefix, b.ext_prefix) &&
+         same_prefix(a.int_prefix, b.int_prefix) && a.ext_lo == b.ext_lo && a.ext_hi == b.ext_hi &&
+         a.int_lo == b.int_lo && a.int_hi == b.int_hi && a.dst_vni == b.dst_vni;
+}
+uint64_t pf_init_ns(const dp_portfw_rule_t &r) {  // DEFAULT_INITIAL_TOUT (objects.rs:50)
+  return (uint64_t)(r.init_timeout_s ? r.init_timeout_s : 10) * 1000000000ull;
+}
+uint64_t pf_estab_ns(const dp_portfw_rule_t &r) {  // DEFAULT_ESTABLISHED_TOUT_TCP / _UDP (:51-52)
+  return (uint64_t)(r.estab_timeout_s ? r.estab_timeout_s : (r.proto == 6 ? 1800 : 30)) * 1000000000ull;
+}
+// PortFwTable::update (objects.rs:284-300): entries absent from the new rule
+// set are removed; the rules are then added last to first (add_entry,
+// :256-274): one that matches an entry at its (key, prefix, port range)
+// keeps that entry (new timeouts), one whose range overlaps another of the
+// same key and prefix is refused (RangeSet::insert_range, rangeset.rs:73-79).
+void pf_update(dpo_tables &T, const dpo_tables *prev, const dp_portfw_rule_t *rs, uint32_t n) {
+  T.pf_next_id = prev ? prev->pf_next_id : 1;
+  if (prev)
+    for (const PfRule &e : prev->pf) {
+      bool keep = false;
+      for (uint32_t i = 0; i < n && !keep; i++) keep = pf_matches(e.r, rs[i]);
+      if (keep) T.pf.push_back(e);
+    }
+  for (uint32_t k = n; k-- > 0;) {
+    const dp_portfw_rule_t &r = rs[k];
+    PfRule *exist = nullptr;
+    bool overlap = false;
+    for (PfRule &e : T.pf) {
+      if (e.r.src_vni != r.src_vni || e.r.proto != r.proto || !same_prefix(e.r.ext_prefix, r.ext_prefix)) continue;
+      if (e.r.ext_lo == r.ext_lo && e.r.ext_hi == r.ext_hi) exist = &e;
+      if (e.r.ext_lo <= r.ext_hi && r.ext_lo <= e.r.ext_hi) overlap = true;
+    }
+    if (exist && pf_matches(exist->r, r)) {
+      exist->r.init_timeout_s = r.init_timeout_s;
+      exist->r.estab_timeout_s = r.estab_timeout_s;
+      exist->init_ns = pf_init_ns(r);
+      exist->estab_ns = pf_estab_ns(r);
+      continue;
+    }
+    if (overlap) continue;  // "Failure adding port-forwarding rule"
+    T.pf.push_back(PfRule{r, T.pf_next_id++, pf_init_ns(r), pf_estab_ns(r)});
+  }
+}
+// PortFwEntry::new's checks (objects.rs:70-155, portrange.rs:33-42)
+bool pf_valid(const dp_portfw_rule_t &r) {
+  if (r.proto != 6 && r.proto != 17) return false;
+  if (r.ext_prefix.family != r.int_prefix.family || r.ext_prefix.len != r.int_prefix.len) return false;
+  if (r.src_vni == r.dst_vni || !r.src_vni || !r.dst_vni) return false;
+  if (!r.ext_lo || !r.int_lo || r.ext_hi < r.ext_lo || r.int_hi < r.int_lo) return false;
+  return r.ext_hi - r.ext_lo == r.int_hi - r.int_lo;
+}
+const PfRule *pf_by_id(const dpo_tables &T, uint32_t id) {  // Weak::upgrade of an entry
+  for (const PfRule &e : T.pf) if (e.id == id) return &e;
+  return nullptr;
+}
+// PortFwTable::lookup_matching_rule -> LpmMap::lookup_cumulative
+// (objects.rs:304-313, lpmmap.rs:108-116): of the key's prefixes holding the
+// address, longest first, the first whose port ranges hold the port
+const PfRule *pf_lookup(const dpo_tables &T, uint32_t src_vni, uint8_t proto, const Ip &a, uint16_t port) {
+  const PfRule *best = nullptr;
+  for (const PfRule &e : T.pf) {
+    if (e.r.src_vni != src_vni || e.r.proto != proto || e.r.ext_prefix.family != a.fam) continue;
+    if (!prefix_covers(e.r.ext_prefix.addr, e.r.ext_prefix.len, a.b)) continue;
+    if (port < e.r.ext_lo || port > e.r.ext_hi) continue;
+    if (!best || e.r.ext_prefix.len > best->r.ext_prefix.len) best = &e;
+  }
+  return best;
+}
+bool ip_unicast(const Ip &a) {  // UnicastIpv4Addr / UnicastIpv6Addr::new
+  if (a.fam == 4) return !((a.b[0] >> 4) == 0xe || (a.b[0] == 255 && a.b[1] == 255 && a.b[2] == 255 && a.b[3] == 255));
+  return a.b[0] != 0xff;
+}
+// PortFwEntry::map_address_port (objects.rs:168-203): the port's index in
+// ext_ports into int_ports; the address's offset from the external network
+// onto the internal one (wrapping integer arithmetic); a unicast result
+bool pf_map(const PfRule &e, const Ip &a, uint16_t port, Ip &na, uint16_t &np) {
+  if (port < e.r.ext_lo || port > e.r.ext_hi) return false;
+  np = (uint16_t)(e.r.int_lo + (port - e.r.ext_lo));
+  na = Ip{};
+  na.fam = a.fam;
+  const int nb = a.fam == 4 ? 4 : 16;
+  int carry = 0, borrow = 0;
+  uint8_t off[16];
+  for (int i = nb - 1; i >= 0; i--) {  // offset = address - ext network
+    int d = (int)a.b[i] - e.r.ext_prefix.addr[i] - borrow;
+    borrow = d < 0;
+    off[i] = (uint8_t)(d + (borrow ? 256 : 0));
+  }
+  for (int i = nb - 1; i >= 0; i--) {  // int network + offset
+    int v = (int)e.r.int_prefix.addr[i] + off[i] + carry;
+    carry = v > 255;
+    na.b[i] = (uint8_t)v;
+  }
+  return ip_unicast(na);
+}
+Ip pkt_src(const Packet &p) { return p.h.net == 4 ? ip4(p.h.v4.src) : ip6(p.h.v6.src); }
+Ip pkt_dst(const Packet &p) { return p.h.net == 4 ? ip4(p.h.v4.dst) : ip6(p.h.v6.dst); }
+uint8_t pkt_proto(const Packet &p) { return p.h.net == 4 ? p.h.v4.proto : p.h.v6.nh; }
+bool pkt_ports(const Packet &p, uint16_t &sp, uint16_t &dpp) {  // transport src / dst port
+  if (p.h.l4 == L4_TCP) { sp = p.h.tcp.sport; dpp = p.h.tcp.dport; return true; }
+  if (p.h.l4 == L4_UDP) { sp = p.h.udp.sport; dpp = p.h.udp.dport; return true; }
+  return false;
+}
+void set_ip(Packet &p, bool src, const Ip &a) {
+  uint8_t *q = p.h.net == 4 ? (src ? p.h.v4.src : p.h.v4.dst) : (src ? p.h.v6.src : p.h.v6.dst);
+  memcpy(q, a.b, p.h.net == 4 ? 4 : 16);
+}
+// nat_packet (portfw/packet.rs:42-154): DstNat rewrites the destination
+// address and port, SrcNat the source; an ICMP packet only its address.
+// false: unsupported traffic (-> InternalFailure)
+bool pf_nat_packet(Packet &p, uint8_t action, const Ip &a, uint16_t port) {
+  const bool src = action == DP_PF_SRC_NAT;
+  if (p.h.net == 0 || a.fam != p.h.net) return false;
+  const uint8_t proto = pkt_proto(p);
+  bool mod = false;
+  if ((proto == 6 || proto == 17) && (p.h.l4 == L4_TCP || p.h.l4 == L4_UDP)) {
+    Ip cur = src ? pkt_src(p) : pkt_dst(p);
+    if (!(cur == a)) { set_ip(p, src, a); mod = true; }
+    uint16_t *pp = p.h.l4 == L4_TCP ? (src ? &p.h.tcp.sport : &p.h.tcp.dport)
+                                    : (src ? &p.h.udp.sport : &p.h.udp.dport);
+    if (*pp != port) { *pp = port; mod = true; }
+  } else if ((p.h.net == 4 ? proto == 1 && p.h.l4 == L4_ICMP4 : proto == 58 && p.h.l4 == L4_ICMP6)) {
+    Ip cur = src ? pkt_src(p) : pkt_dst(p);
+    if (!(cur == a)) { set_ip(p, src, a); mod = true; }
+  } else {
+    return false;
+  }
+  if (mod) p.m.flags |= DP_META_REFR_CHKSUM | (src ? DP_META_NATTED_SRC : DP_META_NATTED_DST);
+  return true;
+}
+// get_rule_from_pkt (portfw/nf.rs:206-324): is the stale state of this flow
+// still what the current rules would do?  The entry, or null.
+const PfRule *pf_rule_from_pkt(const dpo_tables &T, const Packet &p, const OFlow &f) {
+  uint16_t sp, dpp;
+  if (!p.m.src_vni || p.h.net == 0 || !pkt_ports(p, sp, dpp)) return nullptr;
+  const uint8_t proto = pkt_proto(p);
+  if (f.pf == DP_PF_DST_NAT) {  // forward path (:206-244)
+    const PfRule *e = pf_lookup(T, p.m.src_vni, proto, pkt_dst(p), dpp);
+    Ip na; uint16_t np;
+    if (!e || !pf_map(*e, pkt_dst(p), dpp, na, np)) return nullptr;
+    if (!(na == f.pf_ip) || np != f.pf_port || e->r.dst_vni != f.d.dst_vni) return nullptr;
+    return e;
+  }
+  // reverse path (:246-288)
+  const PfRule *e = pf_lookup(T, f.d.dst_vni, proto, f.pf_ip, f.pf_port);
+  Ip ta; uint16_t tp;
+  if (!e || !pf_map(*e, f.pf_ip, f.pf_port, ta, tp)) return nullptr;
+  if (!(ta == pkt_src(p)) || tp != sp || e->r.dst_vni != p.m.src_vni) return nullptr;
+  return e;
+}
+// next_flow_status (portfw/protocol.rs:17-69)
+uint8_t pf_next_status(const Packet &p, uint8_t action, uint8_t st) {
+  if (p.h.l4 == L4_TCP) {
+    const uint8_t fl = p.h.tcp.flags;
+    const bool fin = fl & 0x01, syn = fl & 0x02, rst = fl & 0x04, ack = fl & 0x10;
+    if (action == DP_PF_DST_NAT) {
+      if (st == DP_NFS_TWO_WAY && !syn && ack) return DP_NFS_ESTABLISHED;
+      if (st == DP_NFS_ESTABLISHED && fin) return DP_NFS_C_CLOSING;
+      if (st == DP_NFS_S_CLOSING && !fin && ack) return DP_NFS_S_HALF_CLOSE;
+      if (st == DP_NFS_S_CLOSING && fin && ack) return DP_NFS_LAST_ACK;
+      if (st == DP_NFS_S_HALF_CLOSE && fin) return DP_NFS_LAST_ACK;
+      if (st == DP_NFS_LAST_ACK && ack) return DP_NFS_CLOSED;
+    } else {
+      if (st == DP_NFS_ONE_WAY && syn && ack) return DP_NFS_TWO_WAY;
+      if (st == DP_NFS_ESTABLISHED && fin) return DP_NFS_S_CLOSING;
+      if (st == DP_NFS_C_CLOSING && !fin && ack) return DP_NFS_C_HALF_CLOSE;
+      if (st == DP_NFS_C_CLOSING && fin && ack) return DP_NFS_LAST_ACK;
+      if (st == DP_NFS_C_HALF_CLOSE && fin) return DP_NFS_LAST_ACK;
+      if (st == DP_NFS_LAST_ACK && ack) return DP_NFS_CLOSED;
+    }
+    return rst ? (uint8_t)DP_NFS_RESET : st;
+  }
+  if (action == DP_PF_DST_NAT) return st == DP_NFS_TWO_WAY ? (uint8_t)DP_NFS_ESTABLISHED : st;
+  return st == DP_NFS_ONE_WAY ? (uint8_t)DP_NFS_TWO_WAY : st;
+}
+// FlowInfo::reset_expiry_unchecked (flow_info.rs:399-407)
+void reset_expiry(OFlow &f, uint64_t now, uint64_t dur) {
+  const uint64_t nw = now + dur;
+  if (nw >= f.d.expires_at) f.d.expires_at = nw;
+}
+// refresh_port_fw_entry (portfw/flow_state.rs:216-264)
+void pf_refresh(const dpo_tables &T, dpo_flows *FL, Packet &p, const PfRule &e, int64_t fi) {
+  OFlow &f = FL->f[fi];
+  uint8_t &st = FL->nfs[f.pf_status];
+  const uint8_t cur = st, nw = pf_next_status(p, f.pf, cur);
+  st = nw;
+  uint64_t ext;
+  if (nw == DP_NFS_ESTABLISHED) ext = e.estab_ns;
+  else if (nw == DP_NFS_CLOSED || nw == DP_NFS_RESET) { flow_invalidate_pair(FL, fi); return; }
+  else ext = e.init_ns;
+  reset_expiry(f, FL->now, ext);
+  if (nw == DP_NFS_ESTABLISHED && nw != cur && flow_alive(FL, f.related))
+    reset_expiry(FL->f[f.related], FL->now, ext);
+  f.d.genid = T.genid;
+}
+// FlowInfo::related_pair + insert_from_arc of both (portfw/nf.rs:96-172)
+void pf_create(const dpo_tables &T, dpo_flows *FL, Packet &p, const PfRule &e, const Ip &dst,
+               uint16_t dport, const Ip &na, uint16_t np) {
+  FKey cur;
+  uint16_t sp, dpp;
+  if (!packet_flow_key(p, cur) || !pkt_ports(p, sp, dpp)) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+  const FKey fwk = p.has_ikey ? p.ikey : cur;  // build_portfw_flow_keys (flow_state.rs:102-131)
+  FKey rk;                                     // (current key DNATed).reverse(dst_vpcd)
+  rk.vni = e.r.dst_vni;
+  rk.fam = cur.fam;
+  rk.kind = cur.kind;
+  memcpy(rk.src, na.b, 16);
+  if (na.fam == 4) memset(rk.src + 4, 0, 12);
+  memcpy(rk.dst, cur.src, 16);
+  rk.sp = np;
+  rk.dp = cur.sp;
+  if (fwk == rk) { p.done(DP_DONE_INTERNAL_FAILURE); return; }  // related_pair: identical keys
+  dp_flow_t fd{}, rd{};
+  auto to_key = [](const FKey &k, dp_flow_key_t &x) {
+    x.src_vni = k.vni; x.family = k.fam; x.kind = k.kind; x.sport = k.sp; x.dport = k.dp;
+    memcpy(x.src, k.src, 16); memcpy(x.dst, k.dst, 16);
+  };
+  to_key(fwk, fd.key);
+  to_key(rk, rd.key);
+  // compute_flow_flags_forward / _reverse (net/src/packet/meta.rs:264-287)
+  fd.flags = DP_FLOW_INITIATOR;
+  if (p.m.flags & DP_META_REQ_STATIC_NAT_SRC) { fd.flags |= DP_FLOW_REQ_STATIC_NAT_SRC; rd.flags |= DP_FLOW_REQ_STATIC_NAT_DST; }
+  if (p.m.flags & DP_META_REQ_STATIC_NAT_DST) { fd.flags |= DP_FLOW_REQ_STATIC_NAT_DST; rd.flags |= DP_FLOW_REQ_STATIC_NAT_SRC; }
+  fd.dst_vni = e.r.dst_vni;   // setup_forward_flow (flow_state.rs:133-157)
+  rd.dst_vni = e.r.src_vni;   // setup_reverse_flow (:159-177)
+  fd.genid = rd.genid = T.genid;  // set_genid_pair
+  fd.expires_at = rd.expires_at = FL->now + e.init_ns;
+  // the DNAT of this packet, before any insert (nf.rs:144-150)
+  if (!pf_nat_packet(p, DP_PF_DST_NAT, na, np)) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+  const int64_t cell = (int64_t)FL->nfs.size();
+  FL->nfs.push_back(DP_NFS_ONE_WAY);
+  int64_t rf, rr;
+  // the forward insert: its related flow is not in the table yet
+  if (flow_insert_one(FL, fd, -1, rf) < 0) { p.done(DP_DONE_FLOW_CAPACITY_EXCEEDED); return; }
+  OFlow *F = &FL->f[rf];
+  F->pf = DP_PF_DST_NAT; F->pf_status = cell; F->pf_ip = na; F->pf_port = np; F->pf_rule = e.id;
+  if (flow_insert_one(FL, rd, rf, rr) < 0) {  // admitted at capacity: its related flow is Active
+    flow_invalidate(FL, rf);
+    p.done(DP_DONE_FLOW_CAPACITY_EXCEEDED);
+    return;
+  }
+  OFlow &R = FL->f[rr];
+  R.pf = DP_PF_SRC_NAT; R.pf_status = cell; R.pf_ip = dst; R.pf_port = dport; R.pf_rule = e.id;
+  FL->f[rf].related = rr;
+  R.related = rf;
+}
+// PortForwarder (portfw/nf.rs:326-397)
+void stage_portfw(const dpo_tables &T, dpo_flows *FL, Packet &p) {
+  if (p.is_done() || !(p.m.flags & DP_META_REQ_PORT_FORWARDING) || icmp_is_error_msg(p.h)) return;
+  if (!FL) { p.done(DP_DONE_INTERNAL_FAILURE); return; }  // its Arc<FlowTable> is not optional
+  // get_packet_port_fw_state (flow_state.rs:181-204): an Active flow with state
+  if (p.flow >= 0 && FL->f[p.flow].status == DP_FLOW_ACTIVE && FL->f[p.flow].pf != DP_PF_NONE) {
+    OFlow &f = FL->f[p.flow];
+    const PfRule *e = pf_by_id(T, f.pf_rule);
+    if (!e) {  // a stale rule: would the current rules still do this?
+      e = pf_rule_from_pkt(T, p, f);
+      if (!e) {
+        p.done(DP_DONE_NAT_NOT_PORT_FORWARDED);
+        flow_invalidate_pair(FL, p.flow);
+        return;
+      }
+      f.pf_rule = e->id;  // reassign_port_fw_rule, both flows (nf.rs:290-320)
+      if (flow_alive(FL, f.related)) FL->f[f.related].pf_rule = e->id;
+    }
+    if (!pf_nat_packet(p, f.pf, f.pf_ip, f.pf_port)) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+    pf_refresh(T, FL, p, *e, p.flow);
+    return;
+  }
+  // try_port_forwarding (nf.rs:174-204); can_be_port_forwarded (:54-94)
+  if (!p.m.src_vni) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+  uint16_t sp, dpp;
+  if (!p.h.has_eth || p.h.net == 0 || !pkt_ports(p, sp, dpp)) { p.done(DP_DONE_NAT_NOT_PORT_FORWARDED); return; }
+  if (p.h.l4 == L4_TCP) {  // Tcp::is_first_segment (net/src/tcp/mod.rs:310-312)
+    const uint8_t fl = p.h.tcp.flags;
+    if (!((fl & 0x02) && !(fl & 0x3d))) { p.done(DP_DONE_NAT_NOT_PORT_FORWARDED); return; }
+  }
+  const Ip dst = pkt_dst(p);
+  if (!ip_unicast(dst)) { p.done(DP_DONE_NAT_NOT_PORT_FORWARDED); return; }
+  const PfRule *e = pf_lookup(T, p.m.src_vni, pkt_proto(p), dst, dpp);
+  if (!e) { p.done(DP_DONE_NAT_NOT_PORT_FORWARDED); return; }
+  Ip na;
+  uint16_t np;
+  if (!pf_map(*e, dst, dpp, na, np)) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+  pf_create(T, FL, p, *e, dst, dpp, na, np);
+}
+
 // IcmpErrorHandler (nat/src/icmp_handler/nf.rs:61-194) with an empty flow
 // table: an overlay ICMP error message must carry an embedded IP header and
 // transport (IcmpErrorPacket::new, net/src/packet/icmp_err.rs:37-53), valid
 // ICMP and embedded IPv4 checksums (validate_checksums, :71-87) and a flow
 // key (embedded ports, or an ICMP query identifier: flow_key.rs:635-660);
 // then no flow is found and the packet goes on (nf.rs:113-120).
-void stage_icmp_error(const dpo_tables &T, const dpo_flows *FL, Packet &p) {
+void stage_icmp_error(const dpo_tables &T, dpo_flows *FL, Packet &p) {
   if (p.is_done() || !p.overlay() || !icmp_is_error_msg(p.h)) return;
   const Emb &e = p.h.emb;
   if (!e.present || e.tk == L4_NONE) { p.done(DP_DONE_ICMP_ERROR_INCOMPLETE); return; }
@@ -1799,8 +2132,27 @@ void stage_icmp_error(const dpo_tables &T, const dpo_flows *FL, Packet &p) {
   const OFlow &f = FL->f[r];
   if (f.status != DP_FLOW_ACTIVE) { p.done(DP_DONE_FILTERED); return; }  // nf.rs:126-130
   p.m.dst_vni = f.d.dst_vni;  // nf.rs:139-140
-  // no masquerade / port-forwarding state to translate with (nf.rs:143-152)
-  p.done(DP_DONE_FILTERED);
+  // no NAT state to translate with (nf.rs:143-152)
+  if (f.pf == DP_PF_NONE) { p.done(DP_DONE_FILTERED); return; }
+  // handle_icmp_error_port_forwarding (portfw/icmp_handling.rs:51-90): the
+  // embedded packet back to its form before the state's translation
+  // (nat_translate_icmp_inner, icmp_error_msg.rs:46-146), then the error
+  // itself NATed by the state (nat_packet)
+  Emb &em = p.h.emb;
+  const Ip &a = f.pf_ip;
+  if (em.net != a.fam || (f.pf == DP_PF_DST_NAT && !ip_unicast(a))) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+  const bool src = f.pf == DP_PF_DST_NAT;  // DstNat: the inner source
+  uint8_t *q = em.net == 4 ? (src ? em.v4.src : em.v4.dst) : (src ? em.v6.src : em.v6.dst);
+  memcpy(q, a.b, a.fam == 4 ? 4 : 16);
+  uint16_t old;
+  if (emb_port(em, src, old) && old != f.pf_port) emb_set_port(em, src, f.pf_port);
+  if (!pf_nat_packet(p, f.pf, a, f.pf_port)) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+  // is_icmp_unrecoverable (nf.rs:42-60): destination unreachable other than
+  // fragmentation needed (v4), any destination unreachable (v6)
+  const uint8_t t = p.h.icmp.raw[0], c = p.h.icmp.raw[1];
+  const bool unrec = p.h.l4 == L4_ICMP4 ? (t == 3 && c != 4) : t == 1;
+  if (unrec && FL->nfs[f.pf_status] == DP_NFS_ONE_WAY) flow_invalidate_pair(FL, r);
+  p.m.flags |= DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST;  // nf.rs:176-179
 }
 
 bool adj_lookup(const dpo_tables &T, const Ip &ip, uint32_t oif, uint8_t mac[6]) {
@@ -1872,7 +2224,7 @@ void out_none(const dp_pkt_in_t &in, dp_pkt_out_t &out, dp_pkt_meta_t &meta, uin
   meta.flow_ref = DP_FLOW_NONE;
 }
 
-bool process_pre(const dpo_tables &T, const dpo_flows *FL, uint8_t *buf, const dp_pkt_in_t &in,
+bool process_pre(const dpo_tables &T, dpo_flows *FL, uint8_t *buf, const dp_pkt_in_t &in,
                  dp_pkt_out_t &out, dp_pkt_meta_t &meta, Packet &p) {
   p.buf = buf;
   p.room_start = in.off >= DP_HEADROOM ? in.off - DP_HEADROOM : 0;
@@ -1908,9 +2260,9 @@ bool process_pre(const dpo_tables &T, const dpo_flows *FL, uint8_t *buf, const d
 void process_post(const dpo_tables &T, dpo_flows *FL, Packet &p, dp_pkt_out_t &out, dp_pkt_meta_t &meta) {
   stage_acl(T, FL, p);
   stage_static_nat(T, p);
-  // PortForwarder / Masquerade: identity (no REQ_* flags from static-only tables)
-  if (!p.is_done() && (p.m.flags & (DP_META_REQ_MASQUERADE | DP_META_REQ_PORT_FORWARDING)))
-    p.done(DP_DONE_INTERNAL_FAILURE);
+  stage_portfw(T, FL, p);
+  // Masquerade: masquerade exposes are refused at publish
+  if (!p.is_done() && (p.m.flags & DP_META_REQ_MASQUERADE)) p.done(DP_DONE_INTERNAL_FAILURE);
   stage_ipforward(T, p);  // IP-Forward-2
   stage_egress(T, p);
   if (p.m.done == DP_DONE_DELIVERED) serialize(p);
@@ -2027,6 +2379,14 @@ void flow_info_of(const dpo_flows *FL, int64_t r, dp_flow_info_t &o) {
   o.genid = f.d.genid;
   o.expires_at = f.d.expires_at;
   if (flow_alive(FL, f.related)) o.related = (uint64_t)f.related;
+  o.pf = f.pf;
+  if (f.pf != DP_PF_NONE) {
+    o.pf_status = FL->nfs[f.pf_status];
+    o.pf_port = f.pf_port;
+    o.pf_rule = f.pf_rule;
+    o.pf_family = f.pf_ip.fam;
+    memcpy(o.pf_ip, f.pf_ip.b, f.pf_ip.fam == 4 ? 4 : 16);
+  }
 }
 
 bool valid_prefix(const dp_prefix_t &p) {
@@ -2041,7 +2401,7 @@ bool valid_prefix(const dp_prefix_t &p) {
 
 extern "C" {
 
-int dpo_tables_build(const dp_tables_desc_t *d, dpo_tables_t **out) {
+int dpo_tables_build2(const dp_tables_desc_t *d, const dpo_tables_t *prev, dpo_tables_t **out) {
   if (!d || !out) return DP_EINVAL;
   auto T = std::make_unique<dpo_tables>();
   T->genid = d->genid;
@@ -2117,12 +2477,13 @@ int dpo_tables_build(const dp_tables_desc_t *d, dpo_tables_t **out) {
   if ((rc = load(d->ff_local_v6, d->n_ff_local_v6, T->ffl6, true))) return rc;
   for (auto *v : {&T->ffr4, &T->ffr6})
     for (auto &r : *v) {
-      if (r.r.action2 == DP_NAT_MASQUERADE || r.r.action2 == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
+      if (r.r.action2 == DP_NAT_MASQUERADE) return DP_ENOTSUP;
       if (r.r.src.len != 0 || r.r.sport_lo != 0 || r.r.sport_hi != 65535 || r.r.gate != 0) return DP_EINVAL;
     }
   for (auto *v : {&T->ffl4, &T->ffl6})
     for (auto &r : *v) {
-      if (r.r.action == DP_NAT_MASQUERADE || r.r.action == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
+      if (r.r.action == DP_NAT_MASQUERADE) return DP_ENOTSUP;
+      if (r.r.gate > 1) return DP_EINVAL;
       if (r.r.dst.len != 0 || r.r.dport_lo != 0 || r.r.dport_hi != 65535) return DP_EINVAL;
     }
   for (auto *v : {&T->acl4, &T->acl6})
@@ -2154,9 +2515,23 @@ int dpo_tables_build(const dp_tables_desc_t *d, dpo_tables_t **out) {
       if (!replaced) tab->entries.push_back(std::move(ne));
     }
   }
+  for (uint32_t i = 0; i < d->n_portfw; i++) {
+    const dp_portfw_rule_t &r = d->portfw[i];
+    if (!pf_valid(r) || !valid_prefix(r.ext_prefix) || !valid_prefix(r.int_prefix)) return DP_EINVAL;
+  }
+  pf_update(*T, prev, d->portfw, d->n_portfw);
   *out = T.release();
   return 0;
 }
+
+int dpo_tables_build(const dp_tables_desc_t *d, dpo_tables_t **out) { return dpo_tables_build2(d, nullptr, out); }
+
+int dpo_flows_set_clock(dpo_flows_t *fl, uint64_t now) {
+  if (!fl) return DP_EINVAL;
+  fl->now = now;
+  return 0;
+}
+int dpo_portfw_rule_alive(const dpo_tables_t *t, uint32_t id) { return t && pf_by_id(*t, id) ? 1 : 0; }
 
 void dpo_tables_free(dpo_tables_t *t) { delete t; }
 

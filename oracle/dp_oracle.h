@@ -34,6 +34,12 @@ typedef struct dpo_tables dpo_tables_t;
 /* Build oracle tables from the lowered descriptors (same semantics as
  * dp_tables_publish).  Returns 0 / negative errno. */
 int dpo_tables_build(const dp_tables_desc_t *desc, dpo_tables_t **out);
+/* The same as the next generation of `prev` (NULL: the first): the
+ * port-forwarding entries are updated as PortFwTable::update does, so entry
+ * ids carry over as dp_tables_publish carries them on one device. */
+int dpo_tables_build2(const dp_tables_desc_t *desc, const dpo_tables_t *prev, dpo_tables_t **out);
+/* Is port-forwarding entry `id` in these tables (its Weak upgrades)? */
+int dpo_portfw_rule_alive(const dpo_tables_t *t, uint32_t id);
 void dpo_tables_free(dpo_tables_t *t);
 
 /* Run the reference stage sequence over a burst, in place, exactly like
@@ -66,6 +72,8 @@ int dpo_flow_invalidate(dpo_flows_t *fl, const uint64_t *refs, uint32_t n);
 int dpo_flow_set_status(dpo_flows_t *fl, uint64_t ref, uint32_t status);
 int dpo_flow_sweep(dpo_flows_t *fl, uint64_t now, uint64_t *n_removed);
 int dpo_flow_count(dpo_flows_t *fl, uint64_t *len, uint64_t *active);
+/* Instant::now() for the bursts that follow (DP_OPT_CLOCK, nanoseconds). */
+int dpo_flows_set_clock(dpo_flows_t *fl, uint64_t now);
 /* One burst through the pipeline with FlowLookup on `fl` (NULL: an empty
  * flow table), in the reference's burst order; meta[i].flow_ref is each
  * packet's PacketMeta.flow_info (DP_FLOW_NONE: none). */

@@ -27,6 +27,9 @@ def lib() -> C.CDLL:
         l = C.CDLL(p)
         V = C.c_void_p
         l.dpo_tables_build.argtypes = [V, C.POINTER(V)]
+        l.dpo_tables_build2.argtypes = [V, V, C.POINTER(V)]
+        l.dpo_portfw_rule_alive.argtypes = [V, C.c_uint32]
+        l.dpo_flows_set_clock.argtypes = [V, C.c_uint64]
         l.dpo_tables_free.argtypes = [V]
         l.dpo_process_burst.argtypes = [V, V, C.c_uint64, V, V, V, C.c_uint32, V]
         l.dpo_process_parallel.argtypes = [V, V, C.c_uint64, V, V, V, C.c_uint32, C.c_uint32,
@@ -62,12 +65,19 @@ def lib() -> C.CDLL:
 
 
 class Oracle:
-    def __init__(self, tables_ptr):
+    def __init__(self, tables_ptr, prev: "Oracle | None" = None):
+        """`prev`: the previous generation on the same device (port-forwarding
+        entries carry over as PortFwTable::update keeps them)."""
         h = C.c_void_p()
-        rc = lib().dpo_tables_build(C.cast(tables_ptr, C.c_void_p), C.byref(h))
+        rc = lib().dpo_tables_build2(C.cast(tables_ptr, C.c_void_p), prev.h if prev else None,
+                                     C.byref(h))
         if rc != 0:
             raise ValueError(f"oracle rejected tables: rc={rc}")
         self.h = h
+
+    def rule_alive(self, rule_id: int) -> bool:
+        """Does port-forwarding entry `rule_id` live in these tables?"""
+        return bool(lib().dpo_portfw_rule_alive(self.h, rule_id))
 
     def process(self, buf: np.ndarray, inp: np.ndarray, stats: bool = False):
         """One burst, in place: PKT_RES records (dp_pkt_out_t + dp_pkt_meta_t)."""
@@ -140,6 +150,10 @@ class OracleFlows:
 
     def set_capacity(self, capacity: int) -> None:
         self._chk(lib().dpo_flows_set_capacity(self.h, capacity), "set_capacity")
+
+    def set_clock(self, now_ns: int) -> None:
+        """Instant::now() for the bursts that follow (DP_OPT_CLOCK)."""
+        self._chk(lib().dpo_flows_set_clock(self.h, now_ns), "set_clock")
 
     def insert(self, flows):
         from dataplane_amd import _abi as A
