@@ -325,6 +325,17 @@ struct NatTab {
   uint8_t pad[3];
 };
 
+// A port-forwarding entry (PortFwEntry, nat/src/portfw/portfwtable/
+// objects.rs:30-39) with its id (the identity its Weak refs name).
+struct PfRuleRec {
+  uint32_t id;
+  uint32_t src_vni, dst_vni;
+  uint8_t proto, fam, plen, pad;
+  uint16_t ext_lo, ext_hi, int_lo, int_hi;
+  uint32_t ext[4], inn[4];       // networks, big-endian words (v4: word 0)
+  uint64_t init_ns, estab_ns;    // init_timeout / estab_timeout
+};
+
 struct Image {
   uint64_t bytes;
   int64_t genid;
@@ -359,6 +370,13 @@ struct Image {
   uint64_t nat_ents;         // NatEnt[]
   uint64_t nat_prs;          // uint32_t[]
   uint64_t nat_ranges;       // NatRange[]
+  // port forwarding: (src_vni, proto) -> run of PfRuleRec sorted by prefix
+  // length, longest first (val = first << 16 | count); entry id -> index
+  HashMap pf_keys;
+  HashMap pf_ids;
+  uint64_t pf_rules;         // PfRuleRec[]
+  uint32_t n_pf;
+  uint32_t pad_pf;
 };
 
 // 32-bit mixing hash for the open-addressing maps (host and device agree)

@@ -16,6 +16,9 @@ namespace dpf {
 enum : uint32_t { FS_EMPTY = 0, FS_BUSY = 1, FS_FULL = 2, FS_TOMB = 3 };
 constexpr uint32_t kNoSlot = 0xffffffffu;
 constexpr uint32_t kIdleMark = 0xffffffffu;
+// FlowSlot::flags bit (above the FlowInfoFlags of dpgpu.h): the flow holds
+// port-forwarding state (FlowInfoLocked.port_fw_state is Some)
+constexpr uint32_t kFlagPf = 1u << 8;
 
 struct alignas(128) FlowSlot {
   uint32_t state;       // FS_* | tag << 2
@@ -32,7 +35,14 @@ struct alignas(128) FlowSlot {
   uint32_t mark;        // burst-local invalidation mark (kIdleMark between bursts)
   int64_t genid;
   uint64_t expires_at;
-  uint32_t pad[10];
+  // PortFwState (nat/src/portfw/flow_state.rs:29-35), valid with kFlagPf:
+  // action (dp_pf_action) | NatFlowStatus << 8 | use_port << 16, the entry id
+  // its Weak names, use_ip (big-endian words; v4 in word 0)
+  uint32_t pf;
+  uint32_t pf_rule;
+  uint32_t pf_ip[4];
+  uint32_t pf_fam;
+  uint32_t pad[3];
 };
 static_assert(sizeof(FlowSlot) == 128, "one L2 line per slot");
 
@@ -52,12 +62,47 @@ __host__ __device__ inline uint32_t fkey_hash(const FKey &k) {
   return (uint32_t)(h ^ (h >> 29));
 }
 
+// One packet that reached PortForwarder (nat/src/portfw/nf.rs:373-397) in
+// the burst's first pass: what the sequential port-forwarding pass
+// (dp_pf_resolve) needs, then its decision for the replay pass.
+struct PfReq {
+  uint32_t idx;          // packet index
+  uint32_t bits;         // kPq* below
+  uint32_t slot, state;  // the flow FlowLookup attached (kNoSlot: none) and its fill
+  uint32_t status0;      // its FlowStatus and flags as the burst started
+  uint32_t fflags0;
+  uint32_t src_vni;      // PacketMeta.src_vpcd (0: None)
+  uint32_t proto;        // IP next header | family << 8 | TCP flags << 16
+  uint32_t ports;        // sport << 16 | dport (TCP / UDP)
+  uint32_t src[4], dst[4];  // current addresses (big-endian words)
+  uint32_t ikey[11];     // PacketMeta.flow_key (kPqIkey): the key before static NAT
+  uint32_t acl_def;      // ACL: the peering default verdict of a kPqSens packet (out.acl 3/4/5)
+  uint32_t acl_rule6;    // ... and the rule of its verdict 6
+  uint32_t dst_vni0, related0, related_tag0;  // the attached flow as the burst started
+  int64_t genid0;
+  // decision (dp_pf_resolve -> replay)
+  uint32_t verdict;      // DoneReason to drop with, or kPfForward
+  uint32_t nat;          // dp_pf_action | port << 16
+  uint32_t nat_ip[4];
+  uint32_t acl_over;     // 0, or the ACL verdict the sens check left (out.acl code)
+};
+constexpr uint32_t kPqReached = 1u << 0;  // the packet reached PortForwarder (else dropped on the way)
+constexpr uint32_t kPqTcp = 1u << 1;
+constexpr uint32_t kPqUdp = 1u << 2;
+constexpr uint32_t kPqIkey = 1u << 3;
+constexpr uint32_t kPqSens = 1u << 4;     // ACL verdict 6 (reply of a flow-scope-allowed flow)
+constexpr uint32_t kPqRelated = 1u << 5;  // related / related_tag valid at attach
+constexpr uint32_t kPqEth = 1u << 6;
+constexpr uint32_t kPqSnatSrc = 1u << 7;  // PacketMeta requires static NAT of the source / destination
+constexpr uint32_t kPqSnatDst = 1u << 8;
+constexpr uint32_t kPfForward = 0xffu;
+
 // The launch-time view of a flow table for one burst.
 struct FlowCtx {
   FlowSlot *slots;
   uint32_t mask;        // slots - 1
   uint32_t n;           // packets of the burst
-  uint32_t max_probe;   // probe bound (dp_flow_table::max_probe)
+  uint32_t max_probe;   // unused (the bound lives in tmeta[0])
   uint32_t pad;
   // invalidation events: [0] count, then (slot, state word) of each
   // invalidated flow (<= 2 per packet); the state word is the fill the event
@@ -67,6 +112,23 @@ struct FlowCtx {
   // SensRec records
   uint32_t *sens;
   int64_t genid;        // the burst's PipelineData genid
+  // device words of the table: [0] probe bound (largest displacement of any
+  // stored flow), [2..3] FlowTable::len (u64)
+  uint32_t *tmeta;
+  uint64_t capacity;    // FlowTable capacity
+  uint64_t hard;        // slots - slots / 8: no new slot beyond it
+  uint64_t now;         // the flow clock (DP_OPT_CLOCK)
+  // port forwarding: records, [0] count then packet -> record index, the
+  // bitmap of packets that reached PortForwarder (+ its summary, 1 bit per
+  // 1024 packets), the order of the records (resolve), replaced fills
+  PfReq *pf;
+  uint32_t *pf_cnt;     // [0] records, [1] replay packets, [2] replaced fills
+  uint32_t *pf_of;      // packet -> record
+  uint32_t *pf_bits;
+  uint32_t *pf_sum;
+  uint32_t *pf_order;
+  uint32_t *pf_repl;    // (slot, old state, packet index, old mark) of each fill replaced
+  uint32_t replay;      // 1: the replay pass (packets pf_order[0..pf_cnt[1]))
 };
 
 // A packet whose ACL verdict was "allow: reply of a flow-scope-allowed flow";
@@ -84,7 +146,7 @@ struct SensRec {
   uint32_t dst_vni;     // PacketMeta at the ACL: dst_vpcd, vrf (bit 31: Some), the nh_addr source
   uint32_t vrf;
   uint32_t nh_ref;
-  uint32_t pad;
+  uint32_t slot_tag;    // its flow's state word at attach (a refill by dp_pf_resolve changes it)
 };
 
 __host__ __device__ inline uint64_t make_ref(uint32_t slot, uint32_t state) {

@@ -64,6 +64,16 @@ __device__ void fill_info(const FlowSlot *slots, uint32_t mask, uint32_t sl, dp_
   o.related = DP_FLOW_NONE;
   if (s.related <= mask && slots[s.related].state == s.related_tag)
     o.related = dpf::make_ref(s.related, s.related_tag);
+  o.flags = s.flags & 7u;
+  if (s.flags & dpf::kFlagPf) {  // PortFwState (nat/src/portfw/flow_state.rs:29-35)
+    o.pf = (uint8_t)(s.pf & 0xffu);
+    o.pf_status = (uint8_t)((s.pf >> 8) & 0xffu);
+    o.pf_port = (uint16_t)(s.pf >> 16);
+    o.pf_rule = s.pf_rule;
+    o.pf_family = (uint8_t)s.pf_fam;
+    for (int j = 0; j < 4; j++)
+      for (int b = 0; b < 4; b++) o.pf_ip[4 * j + b] = (uint8_t)(s.pf_ip[j] >> (24 - 8 * b));
+  }
 }
 
 __global__ void __launch_bounds__(kTB) fl_find_k(const FlowSlot *slots, uint32_t mask, uint32_t max_probe,
@@ -121,6 +131,8 @@ __global__ void __launch_bounds__(kTB) fl_insert_k(FlowSlot *slots, uint32_t mas
   s.mark = dpf::kIdleMark;
   s.genid = r.genid;
   s.expires_at = r.expires_at;
+  s.pf = 0;
+  s.pf_rule = 0;
   const uint32_t tag = ((old >> 2) + 1) & 0x3fffffffu;
   const uint32_t st = (tag << 2) | dpf::FS_FULL;
   __hip_atomic_store(&s.state, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -320,6 +332,30 @@ int run(dp_flow_table *ft, const char *what, F f) {
 
 uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kTB - 1) / kTB); }
 
+// The table's device words ([0] probe bound, [2..3] len): bursts that create
+// flows (port forwarding) move them on the device, so a management call that
+// decides on the host reads them first and writes them back after.
+int pull_meta(dp_flow_table *ft) {
+  uint32_t m[4] = {0, 0, 0, 0};
+  int rc = run(ft, "flow table counters", [&](hipStream_t st) {
+    if (hipMemcpyAsync(m, ft->d_meta, sizeof(m), hipMemcpyDeviceToHost, st) != hipSuccess)
+      return dpr_fail(DP_EIO, "flow table counters copy");
+    return 0;
+  });
+  if (rc) return rc;
+  ft->max_probe = m[0];
+  ft->len = ((uint64_t)m[3] << 32) | m[2];
+  return 0;
+}
+int push_meta(dp_flow_table *ft) {
+  const uint32_t m[4] = {ft->max_probe, 0, (uint32_t)ft->len, (uint32_t)(ft->len >> 32)};
+  return run(ft, "flow table counters", [&](hipStream_t st) {
+    if (hipMemcpyAsync(ft->d_meta, m, sizeof(m), hipMemcpyHostToDevice, st) != hipSuccess)
+      return dpr_fail(DP_EIO, "flow table counters copy");
+    return 0;
+  });
+}
+
 // Upload a host array into scratch `s`, returning its device copy.
 template <class T>
 T *upload(Scratch &s, const T *host, size_t n, hipStream_t st) {
@@ -480,6 +516,7 @@ int dpf_debug_table_stats(dp_flow_table_t *ft, uint64_t *out) {
     return 0;
   });
   if (rc) return rc;
+  if (int rc2 = pull_meta(ft)) return rc2;
   out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = ft->max_probe;
   return 0;
 }
@@ -496,6 +533,7 @@ int dp_flow_insert(dp_flow_table_t *ft, const dp_flow_t *flows, uint32_t n, uint
   for (uint32_t i = 0; i < n; i++)
     if (!flow_valid(flows[i])) return dpr_fail(DP_EINVAL, "invalid flow");
   std::lock_guard<std::mutex> lk(ft->mu);
+  if (int rc = pull_meta(ft)) return rc;
   // a key repeated within the batch splits it: each part holds distinct keys
   uint32_t s = 0;
   while (s < n) {
@@ -508,10 +546,10 @@ int dp_flow_insert(dp_flow_table_t *ft, const dp_flow_t *flows, uint32_t n, uint
     std::vector<int32_t> partner(e - s, -1);
     int rc = insert_batch(ft, flows + s, e - s, partner.data(), refs ? refs + s : nullptr,
                           results ? results + s : nullptr);
-    if (rc) return rc;
+    if (rc) { (void)push_meta(ft); return rc; }
     s = e;
   }
-  return 0;
+  return push_meta(ft);
 }
 
 int dp_flow_insert_pair(dp_flow_table_t *ft, const dp_flow_t *a, const dp_flow_t *b, uint64_t *refs,
@@ -522,11 +560,13 @@ int dp_flow_insert_pair(dp_flow_table_t *ft, const dp_flow_t *a, const dp_flow_t
   if (memcmp(&ka, &kb, sizeof(FKey)) == 0) return dpr_fail(DP_EINVAL, "a pair of identical keys");
   if (((a->flags ^ b->flags) & DP_FLOW_INITIATOR) == 0) return dpr_fail(DP_EINVAL, "exactly one initiator");
   std::lock_guard<std::mutex> lk(ft->mu);
+  if (int rc = pull_meta(ft)) return rc;
   dp_flow_t both[2] = {*a, *b};
   const int32_t partner[2] = {-1, 0};
   uint64_t r[2];
   int32_t res[2];
   int rc = insert_batch(ft, both, 2, partner, r, res);
+  if (int rc2 = push_meta(ft)) rc = rc ? rc : rc2;
   if (rc) return rc;
   if (r[0] != DP_FLOW_NONE && r[1] != DP_FLOW_NONE) {
     rc = run(ft, "flow link", [&](hipStream_t st) {
@@ -544,6 +584,7 @@ int dp_flow_lookup(dp_flow_table_t *ft, const dp_flow_key_t *keys, uint32_t n, d
   if (!ft || ((!keys || !out) && n)) return dpr_fail(DP_EINVAL, "null argument");
   if (!n) return 0;
   std::lock_guard<std::mutex> lk(ft->mu);
+  if (int rc = pull_meta(ft)) return rc;
   std::vector<FKey> k(n);
   for (uint32_t i = 0; i < n; i++) k[i] = key_words(keys[i]);
   Scratch &sk = ft->scr[0], &so = ft->scr[1];
@@ -578,6 +619,7 @@ int dp_flow_get(dp_flow_table_t *ft, const uint64_t *refs, uint32_t n, dp_flow_i
 int dp_flow_remove(dp_flow_table_t *ft, const dp_flow_key_t *keys, uint32_t n, uint32_t *n_removed) {
   if (!ft || (!keys && n)) return dpr_fail(DP_EINVAL, "null argument");
   std::lock_guard<std::mutex> lk(ft->mu);
+  if (int rc = pull_meta(ft)) return rc;
   std::vector<FKey> k(n ? n : 1);
   for (uint32_t i = 0; i < n; i++) k[i] = key_words(keys[i]);
   Scratch &sk = ft->scr[0], &sc = ft->scr[1];
@@ -597,7 +639,7 @@ int dp_flow_remove(dp_flow_table_t *ft, const dp_flow_key_t *keys, uint32_t n, u
   if (rc) return rc;
   ft->len -= cnt;
   if (n_removed) *n_removed = cnt;
-  return 0;
+  return push_meta(ft);
 }
 
 int dp_flow_invalidate(dp_flow_table_t *ft, const uint64_t *refs, uint32_t n) {
@@ -633,6 +675,7 @@ int dp_flow_set_status(dp_flow_table_t *ft, uint64_t ref, uint32_t status) {
 int dp_flow_sweep(dp_flow_table_t *ft, uint64_t now, uint64_t *n_removed) {
   if (!ft) return dpr_fail(DP_EINVAL, "null table");
   std::lock_guard<std::mutex> lk(ft->mu);
+  if (int rc = pull_meta(ft)) return rc;
   Scratch &sc = ft->scr[0];
   unsigned long long cnt = 0;
   int rc = run(ft, "flow sweep", [&](hipStream_t st) {
@@ -650,7 +693,7 @@ int dp_flow_sweep(dp_flow_table_t *ft, uint64_t now, uint64_t *n_removed) {
   if (rc) return rc;
   ft->len -= cnt;
   if (n_removed) *n_removed = cnt;
-  return 0;
+  return push_meta(ft);
 }
 
 int dp_flow_count(dp_flow_table_t *ft, uint64_t *len, uint64_t *active) {

@@ -1507,6 +1507,10 @@ struct FlowPk {
   bool sens;           // ACL allowed it as the reply of a flow-scope-allowed flow
   uint32_t def_acl, s_flags, s_oif, s_fib;
   uint32_t s_dvni, s_vrf, s_nh;  // dst_vni, vrf (bit 31: Some) and nh_ref at the ACL
+  uint32_t ev2, ev2_tag; // an ICMP error's invalidation of the flow it found (kNoSlot: none)
+  uint32_t pf_rec;       // its port-forwarding record (dpf::PfReq), kNoSlot: none
+  bool deferred;         // reached PortForwarder in the first pass: finished by the replay
+  uint32_t acl_rule6;    // the rule of an ACL verdict 6
 };
 
 __device__ __forceinline__ uint4 ld4(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
@@ -1526,8 +1530,9 @@ __device__ __forceinline__ uint32_t be16_bytes(const Frame &F, int f) {
 __device__ __forceinline__ uint32_t flow_probe(const dpf::FlowCtx &fc, const dpf::FKey &k, uint32_t &state,
                                                uint4 &v, uint4 &w) {
   uint32_t i = dpf::fkey_hash(k) & fc.mask;
+  const uint32_t bound = fc.tmeta[0];  // moved by the bursts' own inserts (dp_pf_resolve)
 #pragma unroll 1
-  for (uint32_t p = 0; p <= fc.max_probe; p++) {
+  for (uint32_t p = 0; p <= bound; p++) {
     const dpf::FlowSlot *s = fc.slots + i;
     const uint4 a = ld4(&s->state), b = ld4(&s->src[0]), c = ld4(&s->dst[0]);
     v = ld4(&s->status);
@@ -1605,7 +1610,8 @@ __device__ __forceinline__ void flow_attach(uint32_t slot, uint32_t state, const
 // found inactive filters the error; an active one sets the destination VPC
 // and -- with no masquerade / port-forwarding state to translate with --
 // filters it too.  Runs after icmp_error_check accepted the message.
-__device__ __forceinline__ void icmp_error_flow(const dpf::FlowCtx &fc, const Frame &F, const Hdr &H, State &S) {
+__device__ __forceinline__ void icmp_error_flow(const dpf::FlowCtx &fc, const Frame &F, const Hdr &H, State &S,
+                                                FlowPk &fp) {
   const EmbV E = emb_view(F, H);
   dpf::FKey k;
   uint32_t kind, ports;
@@ -1630,8 +1636,47 @@ __device__ __forceinline__ void icmp_error_flow(const dpf::FlowCtx &fc, const Fr
   uint4 v, w;
   const uint32_t sl = flow_probe(fc, k, st, v, w);
   if (sl == dpf::kNoSlot) return;  // no flow: let it through (nf.rs:114-121)
-  if (v.x == DP_FLOW_ACTIVE) S.dst_vni = v.z;  // nf.rs:139-140
-  done(S, DP_DONE_FILTERED);                   // inactive (:126-130) / no NAT state (:143-152)
+  if (v.x != DP_FLOW_ACTIVE) { done(S, DP_DONE_FILTERED); return; }  // nf.rs:126-130
+  S.dst_vni = v.z;                                                   // nf.rs:139-140
+  if (!(v.y & dpf::kFlagPf)) { done(S, DP_DONE_FILTERED); return; }  // no NAT state (:143-152)
+#ifdef DP_X_NOICMP
+  return;
+#endif
+  // handle_icmp_error_port_forwarding (nat/src/portfw/icmp_handling.rs:51-90):
+  // the embedded packet back to its form before the flow's translation
+  // (nat_translate_icmp_inner, icmp_error_msg.rs:46-146: DstNat state ->
+  // the inner source, SrcNat -> the inner destination, address and TCP / UDP
+  // port), then the error itself NATed by the state (nat_packet: its address)
+  const dpf::FlowSlot *fs = fc.slots + sl;
+  const uint4 pfa = ld4(&fs->pf), pfb = ld4(&fs->pf_ip[2]);
+  const uint32_t act = pfa.x & 0xffu, nfs = (pfa.x >> 8) & 0xffu, port = pfa.x >> 16;
+  const uint32_t ip[4] = {pfa.z, pfa.w, pfb.x, pfb.y};
+  const uint32_t fam = pfb.z;
+  const bool inner_src = act == DP_PF_DST_NAT;
+  const bool unicast = fam == 4 ? !((ip[0] >> 28) == 0xe || ip[0] == 0xffffffffu) : (ip[0] >> 24) != 0xff;
+  if ((int)fam != E.net || (inner_src && !unicast)) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
+  const int ao = E.off + (E.net == 4 ? (inner_src ? 12 : 16) : (inner_src ? 8 : 24));
+  for (int j = 0; j < (E.net == 4 ? 1 : 4); j++) wput32(F, ao + 4 * j, ip[j]);
+  if ((E.tk == L4_TCP || E.tk == L4_UDP) && F.be16(E.t_off + (inner_src ? 0 : 2)) != port)
+    wput16(F, E.t_off + (inner_src ? 0 : 2), port);
+  // the outer header: an ICMP message keeps its ports, only the address moves
+  const bool osrc = act == DP_PF_SRC_NAT;
+  bool mod = false;
+  if (H.net == 4) {
+    uint32_t &a = osrc ? S.v4src : S.v4dst;
+    if (a != ip[0]) { a = ip[0]; mod = true; }
+  } else {
+    const int oo = H.net_off + (osrc ? 8 : 24);
+    for (int j = 0; j < 4; j++)
+      if (F.be32(oo + 4 * j) != ip[j]) { wput32(F, oo + 4 * j, ip[j]); mod = true; }
+  }
+  if (mod) S.flags |= DP_META_REFR_CHKSUM | (osrc ? DP_META_NATTED_SRC : DP_META_NATTED_DST);
+  // is_icmp_unrecoverable (nf.rs:42-60) with a one-way flow: the pair goes
+  // (before any flow-filter decision of the burst: mark 0)
+  const uint8_t t = F.b(H.l4_off), c = F.b(H.l4_off + 1);
+  const bool unrec = H.l4 == L4_ICMP4 ? (t == 3 && c != 4) : t == 1;
+  if (unrec && nfs == DP_NFS_ONE_WAY) { fp.ev2 = sl; fp.ev2_tag = st; }
+  S.flags |= DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST;  // nf.rs:176-179
 }
 
 // ---------------------------------------------------------------------------
@@ -2053,13 +2098,20 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
                                                   FlowPk &fp, const dpf::FlowCtx *fc) {
   P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY) || S.dst_vni) return;
+  uint8_t gate = 0;  // SourceGate of the local lookup
   if constexpr (FL) {
     if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid) {
       S.dst_vni = fp.dst_vni;
+      if (fp.fflags & dpf::kFlagPf) S.flags |= DP_META_REQ_PORT_FORWARDING;
       if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_SRC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
       if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_DST) S.flags |= DP_META_REQ_STATIC_NAT_DST;
       return;
     }
+    // flow_revalidation_data (:296-325): the reply flow of a port-forwarded
+    // pair is revalidated against the local rules gated on PortFwdReply
+    if (fp.slot != dpf::kNoSlot && fp.active && fp.genid < fc->genid && !(fp.fflags & DP_FLOW_INITIATOR) &&
+        (fp.fflags & dpf::kFlagPf))
+      gate = 1;
   }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
   if (!S.src_vni) { done(S, DP_DONE_UNROUTABLE); return; }
@@ -2086,7 +2138,13 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   TRIP();
   int32_t lg = g.at<PairRec>(g.im.pair_recs)[pi].ffl[t];
   if (t == 0) hoist_walks(g, S, pi, P);
-  const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, proto, src, Key128{0, 0}, S.sport, 0, P.ffl);
+  uint32_t lpre = P.ffl;
+  if (gate) {  // the (src, dst, PortFwdReply) group: no hoisted walk, the classifier walks it
+    uint32_t gi;
+    lg = hash_find(g, g.im.ff_local[t].groups, S.src_vni, dvni, gate, gi) ? (int32_t)gi : -1;
+    lpre = NO_PRE;
+  }
+  const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, proto, src, Key128{0, 0}, S.sport, 0, lpre);
   if (lh.rule < 0) {
     if constexpr (FL) if (fp.slot != dpf::kNoSlot) fp.ev0 = fp.slot;
     done(S, DP_DONE_FILTERED);
@@ -2095,9 +2153,34 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   uint32_t snat = lh.action;
   S.dst_vni = dvni;
   S.pair = pi;
+  // set_nat_requirements (lib.rs:233-246)
   if (snat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
   if (dnat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_DST;
-  if constexpr (FL) if (fp.slot != dpf::kNoSlot && fp.genid != fc->genid) fp.ev0 = fp.slot;
+  if (snat == DP_NAT_PORT_FORWARDING || dnat == DP_NAT_PORT_FORWARDING) S.flags |= DP_META_REQ_PORT_FORWARDING;
+  if constexpr (FL) {
+    // the key before static NAT, for the flow pair port forwarding creates
+    // (lib.rs:193-201): recorded in the packet's port-forwarding record
+#ifndef DP_X_NOIKEY
+    if ((S.flags & DP_META_REQ_PORT_FORWARDING) &&
+        (S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST)) && !fc->replay) {
+      dpf::FKey k;
+      if (packet_fkey(F, H, S, k)) {
+        fp.pf_rec = atomicAdd(&fc->pf_cnt[0], 1u);
+        dpf::PfReq *R = fc->pf + fp.pf_rec;
+#pragma unroll
+        for (int j = 0; j < 11; j++) R->ikey[j] = k.w[j];
+        R->bits = dpf::kPqIkey;
+      }
+    }
+#endif
+    // should_invalidate_flow (lib.rs:258-294): a flow of another generation
+    // is outdated if its destination or its NAT requirements differ, or if
+    // it no longer needs state
+    if (fp.slot != dpf::kNoSlot && fp.genid != fc->genid) {
+      const bool pf = S.flags & DP_META_REQ_PORT_FORWARDING, need = fp.fflags & dpf::kFlagPf;
+      if (fp.dst_vni != dvni || (S.flags & DP_META_REQ_MASQUERADE) || pf != need || !pf) fp.ev0 = fp.slot;
+    }
+  }
 }
 
 // AclFilter (acl-filter/src/lib.rs:51-138).  The classifier action word
@@ -2110,9 +2193,12 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
 // ACL -- an invalidation by the flow filter (any packet of the burst) or by
 // an earlier packet's deny turns it into the peering default
 // (dp_flow_fixup).  A deny invalidates the packet's flow pair.
+// The replay pass (rp: the packet's port-forwarding record) takes a flow-
+// dependent verdict from the first pass, as dp_pf_resolve left it.
 template <bool FL>
 __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S, const Pre &P,
-                                          FlowPk &fp, const dpf::FlowCtx *fc, uint32_t idx) {
+                                          FlowPk &fp, const dpf::FlowCtx *fc, uint32_t idx,
+                                          const dpf::PfReq *rp) {
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY)) return;
   if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
@@ -2133,7 +2219,13 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
     action = v ? v - 1 : DP_ACL_ALLOW;
     S.acl = def;
     if constexpr (FL) {
-      if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid && fp.related <= fc->mask) {
+      if (rp) {
+        if ((rp->bits & dpf::kPqSens) && rp->acl_over == 0) {
+          action = DP_ACL_ALLOW;
+          S.acl = 6;
+          S.acl_rule = rp->acl_rule6;
+        }
+      } else if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid && fp.related <= fc->mask) {
         const dpf::FlowSlot *r = fc->slots + fp.related;
         const uint4 a = ld4(&r->state), b = ld4(&r->src[0]), c = ld4(&r->dst[0]);
         if (a.x == fp.related_tag) {  // the related flow is still in the table (Weak::upgrade)
@@ -2169,14 +2261,102 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
           fp.s_dvni = S.dst_vni;
           fp.s_vrf = S.has_vrf ? (0x80000000u | S.vrf) : 0u;
           fp.s_nh = S.nh_ref;
+          fp.acl_rule6 = rh.orig;
         }
         }
       }
     }
   }
   if (action == DP_ACL_DENY) {
-    if constexpr (FL) if (fp.slot != dpf::kNoSlot) { fp.ev1 = fp.slot; fp.ev_mark = idx + 1; }
+    if constexpr (FL) if (fp.slot != dpf::kNoSlot && !rp) { fp.ev1 = fp.slot; fp.ev_mark = idx + 1; }
     done(S, DP_DONE_ACL_DROPPED);
+  }
+}
+
+// PortForwarder (nat/src/portfw/nf.rs:373-397) for a packet that requires
+// port forwarding and is not an ICMP error.  Its outcome depends on the flow
+// states the earlier packets of the burst leave (NatFlowStatus, expiry,
+// invalidations, the flow pairs they create), so the first pass records the
+// packet (dpf::PfReq) and stops it here; dp_pf_resolve runs the reference's
+// PortForwarder over the records in packet order, and the replay pass takes
+// each packet through the rest of the path with its decision.  Without a
+// flow table (whose Arc the reference's PortForwarder always holds) the
+// stage fails the packet.
+template <bool FL>
+__device__ __forceinline__ void stage_portfw(const Frame &F, const Hdr &H, State &S, FlowPk &fp,
+                                             const dpf::FlowCtx *fc, uint32_t idx, const dpf::PfReq *rp) {
+  if (S.done != DONE_NONE || !(S.flags & DP_META_REQ_PORT_FORWARDING)) return;
+  if ((H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) && icmp_err_at(F, H.l4_off, H.l4 == L4_ICMP6)) return;
+  if constexpr (!FL) {
+    done(S, DP_DONE_INTERNAL_FAILURE);
+  } else if (!rp) {
+#ifdef DP_X_NOREC
+    fp.deferred = true; return;
+#endif
+    const uint32_t rec = fp.pf_rec != dpf::kNoSlot ? fp.pf_rec : atomicAdd(&fc->pf_cnt[0], 1u);
+    dpf::PfReq *R = fc->pf + rec;
+    uint32_t bits = (fp.pf_rec != dpf::kNoSlot ? R->bits : 0u) | dpf::kPqReached | dpf::kPqEth;
+    if (H.l4 == L4_TCP) bits |= dpf::kPqTcp;
+    if (H.l4 == L4_UDP) bits |= dpf::kPqUdp;
+    if (fp.sens) bits |= dpf::kPqSens;
+    if (S.flags & DP_META_REQ_STATIC_NAT_SRC) bits |= dpf::kPqSnatSrc;
+    if (S.flags & DP_META_REQ_STATIC_NAT_DST) bits |= dpf::kPqSnatDst;
+    R->idx = idx;
+    R->slot = fp.slot;
+    R->state = fp.state;
+    if (fp.slot != dpf::kNoSlot) {
+      bits |= dpf::kPqRelated;
+      R->status0 = fp.active ? DP_FLOW_ACTIVE : DP_FLOW_CANCELLED;
+      R->fflags0 = fp.fflags;
+      R->dst_vni0 = fp.dst_vni;
+      R->related0 = fp.related;
+      R->related_tag0 = fp.related_tag;
+      R->genid0 = fp.genid;
+    }
+    R->bits = bits;
+    R->src_vni = S.src_vni;
+    const uint32_t tflags = H.l4 == L4_TCP ? F.b(H.l4_off + 13) : 0u;
+    R->proto = (uint32_t)net_proto(F, H) | ((uint32_t)H.net << 8) | (tflags << 16);
+    R->ports = ((uint32_t)S.sport << 16) | S.dport;
+    if (H.net == 4) {
+      R->src[0] = S.v4src; R->dst[0] = S.v4dst;
+      R->src[1] = R->src[2] = R->src[3] = R->dst[1] = R->dst[2] = R->dst[3] = 0;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        R->src[j] = F.be32(H.net_off + 8 + 4 * j);
+        R->dst[j] = F.be32(H.net_off + 24 + 4 * j);
+      }
+    }
+    R->acl_def = fp.def_acl;
+    R->acl_rule6 = fp.acl_rule6;
+    R->acl_over = 0;
+    R->src_vni = S.src_vni;
+    fc->pf_of[idx] = rec;
+    atomicOr(&fc->pf_bits[idx >> 5], 1u << (idx & 31));
+    atomicOr(&fc->pf_sum[idx >> 15], 1u << ((idx >> 10) & 31));
+    fp.pf_rec = rec;
+    fp.deferred = true;
+  } else {
+    if (rp->verdict != dpf::kPfForward) { done(S, (uint8_t)rp->verdict); return; }
+    // nat_packet (portfw/packet.rs:42-154): address and port of the side the
+    // action names, each only if it changes
+    const bool src = (rp->nat & 0xffu) == DP_PF_SRC_NAT;
+    const uint16_t port = (uint16_t)(rp->nat >> 16);
+    bool mod = false;
+    if (H.net == 4) {
+      uint32_t &a = src ? S.v4src : S.v4dst;
+      if (a != rp->nat_ip[0]) { a = rp->nat_ip[0]; mod = true; }
+    } else {
+      const int oo = H.net_off + (src ? 8 : 24);
+      for (int j = 0; j < 4; j++)
+        if (F.be32(oo + 4 * j) != rp->nat_ip[j]) { wput32(F, oo + 4 * j, rp->nat_ip[j]); mod = true; }
+    }
+    if (H.l4 == L4_TCP || H.l4 == L4_UDP) {
+      uint16_t &pp = src ? S.sport : S.dport;
+      if (pp != port) { pp = port; mod = true; }
+    }
+    if (mod) S.flags |= DP_META_REFR_CHKSUM | (src ? DP_META_NATTED_SRC : DP_META_NATTED_DST);
   }
 }
 
@@ -2569,11 +2749,13 @@ __device__ __forceinline__ dp_pkt_meta_t meta_of(const Img &g, const State &S) {
 template <bool FL, bool MT>
 __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, lds_u8 *hs, uint8_t *buf, uint64_t buf_bytes,
                                   const dp_pkt_in_t &pin, dp_pkt_out_t &o, dp_pkt_meta_t *pm, int &fl0, int &fl1,
-                                  bool inwin, const dpf::FlowCtx *fc, FlowPk &fp, uint32_t idx) {
+                                  bool inwin, const dpf::FlowCtx *fc, FlowPk &fp, uint32_t idx,
+                                  const dpf::PfReq *rp = nullptr) {
   fl0 = fl1 = 0;
   if constexpr (FL) {
-    fp.slot = fp.ev0 = fp.ev1 = dpf::kNoSlot;
+    fp.slot = fp.ev0 = fp.ev1 = fp.ev2 = fp.pf_rec = dpf::kNoSlot;
     fp.sens = false;
+    fp.deferred = false;
   }
   if (!frame_ok(pin, buf_bytes)) {
     // layout contract violated: never touch memory outside the buffer
@@ -2623,17 +2805,30 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
       icmp_err_at(F, H.l4_off, H.l4 == L4_ICMP6)) {
     const uint8_t r = icmp_error_check(F, H, S);
     if (r != DONE_NONE) done(S, r);
-    else if constexpr (FL) icmp_error_flow(*fc, F, H, S);
+    else if constexpr (FL) icmp_error_flow(*fc, F, H, S, fp);
   }
   // FlowLookup (flow-entry/src/flow_table/nf_lookup.rs:34-55); identity
   // without a flow table
   if constexpr (FL) {
-    dpf::FKey k;
-    uint32_t st;
-    if (S.done == DONE_NONE && (S.flags & DP_META_IS_OVERLAY) && !S.dst_vni && packet_fkey(F, H, S, k)) {
-      uint4 v, w;
-      const uint32_t sl = flow_probe(*fc, k, st, v, w);
-      if (sl != dpf::kNoSlot) flow_attach(sl, st, v, w, fp);
+    if (rp) {  // replay: the flow as FlowLookup attached it in the first pass
+      if (rp->slot != dpf::kNoSlot) {
+        fp.slot = rp->slot;
+        fp.state = rp->state;
+        fp.active = rp->status0 == DP_FLOW_ACTIVE;
+        fp.fflags = rp->fflags0;
+        fp.dst_vni = rp->dst_vni0;
+        fp.related = rp->related0;
+        fp.related_tag = rp->related_tag0;
+        fp.genid = rp->genid0;
+      }
+    } else {
+      dpf::FKey k;
+      uint32_t st;
+      if (S.done == DONE_NONE && (S.flags & DP_META_IS_OVERLAY) && !S.dst_vni && packet_fkey(F, H, S, k)) {
+        uint4 v, w;
+        const uint32_t sl = flow_probe(*fc, k, st, v, w);
+        if (sl != dpf::kNoSlot) flow_attach(sl, st, v, w, fp);
+      }
     }
   }
   Pre P;
@@ -2646,13 +2841,20 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   TS(3);
   TRIP_ST(4);
 #ifndef DP_PROBE_NOACL
-  stage_acl<FL>(g, F, H, S, P, fp, fc, idx);
+  stage_acl<FL>(g, F, H, S, P, fp, fc, idx, rp);
 #endif
   TS(4);
   TRIP_ST(5);
 #ifndef DP_PROBE_NONAT
   stage_static_nat(g, F, H, S, P);
 #endif
+  stage_portfw<FL>(F, H, S, fp, fc, idx, rp);
+  if constexpr (FL) {
+    if (fp.deferred) {  // finished by the replay pass
+      o.done = DONE_NONE;
+      return DONE_NONE;
+    }
+  }
   TS(5);
   TRIP_ST(6);
 #ifndef DP_PROBE_NOIPF2
@@ -2751,9 +2953,22 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
   const int lane = threadIdx.x & 63;
   const bool has = live && fp.slot != dpf::kNoSlot;
   const bool e0 = has && fp.ev0 != dpf::kNoSlot, e1 = has && fp.ev1 != dpf::kNoSlot;
+  const bool e2 = live && fp.ev2 != dpf::kNoSlot;  // an ICMP error's (mark 0, like the flow filter's)
   if (e0) atomicMin(&fc.slots[fp.ev0].mark, 0u);
   if (e1) atomicMin(&fc.slots[fp.ev1].mark, fp.ev_mark);
-  const uint64_t m0 = __ballot(e0), m1 = __ballot(e1);
+  if (e2) atomicMin(&fc.slots[fp.ev2].mark, 0u);
+  const uint64_t m0 = __ballot(e0), m1 = __ballot(e1), m2 = __ballot(e2);
+  if (m2) {
+    const int leader = __ffsll((long long)m2) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&fc.events[0], (uint32_t)__popcll(m2));
+    base = (uint32_t)__shfl((int)base, leader);
+    if (e2) {
+      const uint32_t k = base + __popcll(m2 & lanes_below(lane));
+      fc.events[1 + 2 * k] = fp.ev2;
+      fc.events[2 + 2 * k] = fp.ev2_tag;
+    }
+  }
   if (m0 | m1) {
     const int leader = __ffsll((long long)(m0 | m1)) - 1;
     uint32_t base = 0;
@@ -2771,7 +2986,7 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
       fc.events[2 + 2 * k] = fp.state;
     }
   }
-  const bool sv = has && fp.sens;
+  const bool sv = has && fp.sens && !fp.deferred;  // a deferred packet's verdict: dp_pf_resolve
   const uint64_t ms = __ballot(sv);
   if (ms) {
     const int leader = __ffsll((long long)ms) - 1;
@@ -2781,14 +2996,15 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
     if (sv) {
       dpf::SensRec *R = reinterpret_cast<dpf::SensRec *>(fc.sens + 8) + base + __popcll(ms & lanes_below(lane));
       *R = dpf::SensRec{i, fp.slot, fp.s_flags, fp.s_oif, fp.s_fib, fp.def_acl, fp.related, fp.related_tag,
-                        MT ? fp.s_dvni : 0u, MT ? fp.s_vrf : 0u, MT ? fp.s_nh : NH_NONE, 0};
+                        MT ? fp.s_dvni : 0u, MT ? fp.s_vrf : 0u, MT ? fp.s_nh : NH_NONE, fp.state};
     }
   }
 }
 
 // FL: the flows variant (a flow table is attached to the context); MT: meta
-// records requested (meta != nullptr).
-template <bool FL, bool MT>
+// records requested (meta != nullptr); RP: the replay pass of the packets
+// that reached PortForwarder (FL only).
+template <bool FL, bool MT, bool RP = false>
 __global__ void __launch_bounds__(TPB) DP_OCC
 dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict__ im, uint8_t *__restrict__ buf,
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
@@ -2801,8 +3017,19 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   const int lane = tid & 63;
   uint8_t *slab_wave = slab_all + (tid - lane) * SLAB;
   lds_u8 *slab = (lds_u8 *)(slab_all + tid * SLAB);
-  const uint32_t i = blockIdx.x * TPB + tid;
-  const bool live = i < n;
+  // the replay pass (port forwarding, FL only): thread t finishes packet
+  // pf_order[t] of the records dp_pf_resolve ordered
+  constexpr bool rep = FL && RP;
+  uint32_t i = blockIdx.x * TPB + tid;
+  bool live = i < n;
+  const dpf::PfReq *rp = nullptr;
+  if constexpr (FL) {
+    if (rep) {
+      live = i < fc.pf_cnt[1];
+      i = live ? fc.pf_order[i] : n;
+      if (live) rp = fc.pf + fc.pf_of[i];
+    }
+  }
   dp_pkt_in_t pin{};
   if (live) pin = in[i];
   const uint32_t base = pin.off & ~15u;
@@ -2820,11 +3047,11 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
     dp_pkt_out_t o;
     lds_u8 *hs = (lds_u8 *)(hash_all + tid * HS);
     dp_pkt_meta_t *pm = MT ? meta + i : nullptr;
-    if (all_fit) done_code = process_packet<FL, MT>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, true, &fc, fp, i);
-    else done_code = process_packet<FL, MT>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, false, &fc, fp, i);
+    if (all_fit) done_code = process_packet<FL, MT>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, true, &fc, fp, i, rp);
+    else done_code = process_packet<FL, MT>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, false, &fc, fp, i, rp);
     out[i] = o;
   }
-  if constexpr (FL) flow_effects<MT>(fc, live, i, fp);
+  if constexpr (FL) if (!rep) flow_effects<MT>(fc, live, i, fp);
   __syncthreads();
   // write-back: whole chunks by the wave, a partial tail by its owner
   wave_store_windows(buf, slab_wave, base, fl0 >> 4, fl1 >> 4);
@@ -2844,6 +3071,377 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Port forwarding: the sequential pass (nat/src/portfw/nf.rs:326-397)
+// ---------------------------------------------------------------------------
+namespace pfw {
+
+// PortFwTable::lookup_matching_rule -> LpmMap::lookup_cumulative
+// (portfwtable/objects.rs:304-313, lpmmap.rs:108-116): the key's entries are
+// sorted longest prefix first; the first that holds the address and whose
+// range holds the port.  -1: none.
+__device__ int32_t lookup(const Img &g, uint32_t src_vni, uint32_t proto, uint32_t fam, const uint32_t *a,
+                          uint32_t port) {
+  uint32_t v;
+  if (!hash_find(g, g.im.pf_keys, src_vni, proto, 0, v)) return -1;
+  const PfRuleRec *R = g.at<PfRuleRec>(g.im.pf_rules);
+  for (uint32_t k = v >> 16, e = (v >> 16) + (v & 0xffffu); k < e; k++) {
+    const PfRuleRec &r = R[k];
+    if (r.fam != fam || port < r.ext_lo || port > r.ext_hi) continue;
+    bool in = true;
+    for (int j = 0; j < 4 && in; j++) {
+      const int bits = (int)r.plen - 32 * j;
+      const uint32_t m = bits >= 32 ? 0xffffffffu : bits <= 0 ? 0u : ~0u << (32 - bits);
+      in = ((a[j] ^ r.ext[j]) & m) == 0;
+    }
+    if (in) return (int32_t)k;
+  }
+  return -1;
+}
+// Weak::upgrade of an entry: its index in these tables, -1 if gone
+__device__ int32_t by_id(const Img &g, uint32_t id) {
+  uint32_t v;
+  return id && hash_find(g, g.im.pf_ids, id, 0, 0, v) ? (int32_t)v : -1;
+}
+__device__ bool unicast(uint32_t fam, const uint32_t *a) {  // UnicastIpv4Addr / UnicastIpv6Addr::new
+  return fam == 4 ? !((a[0] >> 28) == 0xe || a[0] == 0xffffffffu) : (a[0] >> 24) != 0xff;
+}
+// PortFwEntry::map_address_port (objects.rs:168-203): the port's index in
+// ext_ports into int_ports, the address's offset from the external network
+// onto the internal one (wrapping), and a unicast result
+__device__ bool map(const PfRuleRec &r, const uint32_t *a, uint32_t port, uint32_t *na, uint32_t &np) {
+  if (port < r.ext_lo || port > r.ext_hi) return false;
+  np = r.int_lo + (port - r.ext_lo);
+  const int nw = r.fam == 4 ? 1 : 4;
+  uint64_t borrow = 0, carry = 0;
+  uint32_t off[4] = {0, 0, 0, 0};
+  for (int j = nw - 1; j >= 0; j--) {
+    const uint64_t d = (uint64_t)a[j] - r.ext[j] - borrow;
+    off[j] = (uint32_t)d;
+    borrow = (d >> 63) & 1;
+  }
+  for (int j = 3; j >= 0; j--) na[j] = 0;
+  for (int j = nw - 1; j >= 0; j--) {
+    const uint64_t v = (uint64_t)r.inn[j] + off[j] + carry;
+    na[j] = (uint32_t)v;
+    carry = v >> 32;
+  }
+  return unicast(r.fam, na);
+}
+// next_flow_status (portfw/protocol.rs:17-69)
+__device__ uint32_t next_status(bool tcp, uint32_t fl, uint32_t act, uint32_t st) {
+  if (tcp) {
+    const bool fin = fl & 1, syn = fl & 2, rst = fl & 4, ack = fl & 16;
+    if (act == DP_PF_DST_NAT) {
+      if (st == DP_NFS_TWO_WAY && !syn && ack) return DP_NFS_ESTABLISHED;
+      if (st == DP_NFS_ESTABLISHED && fin) return DP_NFS_C_CLOSING;
+      if (st == DP_NFS_S_CLOSING && !fin && ack) return DP_NFS_S_HALF_CLOSE;
+      if (st == DP_NFS_S_CLOSING && fin && ack) return DP_NFS_LAST_ACK;
+      if (st == DP_NFS_S_HALF_CLOSE && fin) return DP_NFS_LAST_ACK;
+      if (st == DP_NFS_LAST_ACK && ack) return DP_NFS_CLOSED;
+    } else {
+      if (st == DP_NFS_ONE_WAY && syn && ack) return DP_NFS_TWO_WAY;
+      if (st == DP_NFS_ESTABLISHED && fin) return DP_NFS_S_CLOSING;
+      if (st == DP_NFS_C_CLOSING && !fin && ack) return DP_NFS_C_HALF_CLOSE;
+      if (st == DP_NFS_C_CLOSING && fin && ack) return DP_NFS_LAST_ACK;
+      if (st == DP_NFS_C_HALF_CLOSE && fin) return DP_NFS_LAST_ACK;
+      if (st == DP_NFS_LAST_ACK && ack) return DP_NFS_CLOSED;
+    }
+    return rst ? (uint32_t)DP_NFS_RESET : st;
+  }
+  if (act == DP_PF_DST_NAT) return st == DP_NFS_TWO_WAY ? (uint32_t)DP_NFS_ESTABLISHED : st;
+  return st == DP_NFS_ONE_WAY ? (uint32_t)DP_NFS_TWO_WAY : st;
+}
+
+// The sequential pass's view of the table.
+struct Seq {
+  const dpf::FlowCtx &fc;
+  const Img &g;
+  __device__ bool alive(uint32_t sl, uint32_t tag) const { return sl <= fc.mask && fc.slots[sl].state == tag; }
+  // the pair is invalid for packet idx: either flow's burst-local mark says
+  // so (invalidate_pair reaches the related flow only while it is alive)
+  __device__ bool pair_valid(uint32_t sl, uint32_t idx) const {
+    const dpf::FlowSlot &s = fc.slots[sl];
+    if (s.mark <= idx) return false;
+    return !(alive(s.related, s.related_tag) && fc.slots[s.related].mark <= idx);
+  }
+  // FlowInfo::invalidate_pair by packet idx: marks + the event apply turns
+  // into the flows' status
+  __device__ void invalidate(uint32_t sl, uint32_t idx) const {
+    dpf::FlowSlot &s = fc.slots[sl];
+    if (s.mark > idx + 1) s.mark = idx + 1;
+    const uint32_t k = fc.events[0]++;
+    fc.events[1 + 2 * k] = sl;
+    fc.events[2 + 2 * k] = s.state;
+  }
+  __device__ void set_nfs(uint32_t sl, uint32_t st) const {
+    dpf::FlowSlot &s = fc.slots[sl];
+    s.pf = (s.pf & ~0xff00u) | (st << 8);
+    if (alive(s.related, s.related_tag)) {
+      dpf::FlowSlot &r = fc.slots[s.related];
+      r.pf = (r.pf & ~0xff00u) | (st << 8);
+    }
+  }
+  __device__ void reset_expiry(uint32_t sl, uint64_t dur) const {  // reset_expiry_unchecked (flow_info.rs:399-407)
+    const uint64_t nw = fc.now + dur;
+    if (nw >= fc.slots[sl].expires_at) fc.slots[sl].expires_at = nw;
+  }
+  // FlowTable::insert_common (flow-entry/src/flow_table/table.rs:215-260):
+  // capacity (the second half of a pair is admitted at capacity while its
+  // related flow is active), replacement of a flow of the same key (that
+  // fill is Detached: gone from its slot), else the first free slot of the
+  // key's probe sequence.  Returns the slot, kNoSlot when refused.
+  __device__ uint32_t insert(const dpf::FKey &k, bool exception, uint32_t idx) const {
+    uint64_t len = ((uint64_t)fc.tmeta[3] << 32) | fc.tmeta[2];
+    if (len >= fc.capacity && !exception) return dpf::kNoSlot;
+    const uint32_t home = dpf::fkey_hash(k) & fc.mask;
+    const uint32_t bound = fc.tmeta[0];
+    uint32_t i = home, found = dpf::kNoSlot, free_ = dpf::kNoSlot;
+    for (uint32_t p = 0; p <= bound; p++, i = (i + 1) & fc.mask) {
+      const dpf::FlowSlot &s = fc.slots[i];
+      const uint32_t st = s.state & 3u;
+      if (st == dpf::FS_EMPTY) { if (free_ == dpf::kNoSlot) free_ = i; break; }
+      if (st == dpf::FS_TOMB) { if (free_ == dpf::kNoSlot) free_ = i; continue; }
+      if (s.src_vni == k.w[0] && s.fk == k.w[1] && s.ports == k.w[2] && s.src[0] == k.w[3] &&
+          s.src[1] == k.w[4] && s.src[2] == k.w[5] && s.src[3] == k.w[6] && s.dst[0] == k.w[7] &&
+          s.dst[1] == k.w[8] && s.dst[2] == k.w[9] && s.dst[3] == k.w[10]) { found = i; break; }
+    }
+    uint32_t sl = found;
+    if (sl != dpf::kNoSlot) {
+      // the replaced fill, for the ACL verdicts that rest on it (dp_flow_fixup)
+      const uint32_t r = fc.pf_cnt[2]++;
+      fc.pf_repl[4 * r] = sl;
+      fc.pf_repl[4 * r + 1] = fc.slots[sl].state;
+      fc.pf_repl[4 * r + 2] = idx;
+      fc.pf_repl[4 * r + 3] = fc.slots[sl].mark;
+    } else {
+      if (len >= fc.hard) return dpf::kNoSlot;  // the table stays at most 7/8 full
+      if (free_ == dpf::kNoSlot) {  // beyond the probe bound: the first free slot further on
+        for (uint32_t p = bound + 1; p <= fc.mask; p++) {
+          const uint32_t j = (home + p) & fc.mask;
+          if ((fc.slots[j].state & 3u) != dpf::FS_FULL) { free_ = j; break; }
+        }
+        if (free_ == dpf::kNoSlot) return dpf::kNoSlot;
+      }
+      sl = free_;
+      const uint32_t disp = (sl - home) & fc.mask;
+      if (disp > fc.tmeta[0]) fc.tmeta[0] = disp;
+      len++;
+      fc.tmeta[2] = (uint32_t)len;
+      fc.tmeta[3] = (uint32_t)(len >> 32);
+    }
+    dpf::FlowSlot &s = fc.slots[sl];
+    const uint32_t old = s.state;
+    s.src_vni = k.w[0]; s.fk = k.w[1]; s.ports = k.w[2];
+    for (int j = 0; j < 4; j++) { s.src[j] = k.w[3 + j]; s.dst[j] = k.w[7 + j]; }
+    s.status = DP_FLOW_ACTIVE;
+    s.related = dpf::kNoSlot;
+    s.related_tag = 0;
+    s.mark = dpf::kIdleMark;
+    s.state = ((((old >> 2) + 1) & 0x3fffffffu) << 2) | dpf::FS_FULL;
+    return sl;
+  }
+};
+
+__device__ inline uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// One record, in packet order.
+__device__ void resolve_one(const Seq &q, dpf::PfReq &R) {
+  const dpf::FlowCtx &fc = q.fc;
+  const Img &g = q.g;
+  const uint32_t idx = R.idx;
+  R.verdict = dpf::kPfForward;
+  R.acl_over = 0;
+  const bool attached = R.slot != dpf::kNoSlot;
+  // the flow is still the fill FlowLookup attached (not replaced earlier in
+  // the burst) and valid for this packet
+  const bool same = attached && q.alive(R.slot, R.state);
+  const bool valid = same && R.status0 == DP_FLOW_ACTIVE && q.pair_valid(R.slot, idx);
+  // the ACL's "reply of a flow-scope-allowed flow" verdict needs the pair
+  // still valid when the packet reached the ACL (dp_flow_fixup's rule)
+  if (R.bits & dpf::kPqSens) {
+    const bool rel = (R.bits & dpf::kPqRelated) && q.alive(R.related0, R.related_tag0);
+    const bool ok = same && fc.slots[R.slot].mark > idx && (!rel || fc.slots[R.related0].mark > idx);
+    if (!ok) {
+      R.acl_over = R.acl_def;
+      if (R.acl_def == 4) {  // the peering default denies: dropped at the ACL, its pair invalidated
+        R.verdict = DP_DONE_ACL_DROPPED;
+        if (same) q.invalidate(R.slot, idx);
+        return;
+      }
+    }
+  }
+  const uint32_t fam = (R.proto >> 8) & 0xffu, proto = R.proto & 0xffu, tfl = R.proto >> 16;
+  const bool tcp = R.bits & dpf::kPqTcp, ports = R.bits & (dpf::kPqTcp | dpf::kPqUdp);
+  const uint32_t sport = R.ports >> 16, dport = R.ports & 0xffffu;
+  // get_packet_port_fw_state (flow_state.rs:181-204): an Active flow with state
+  if (valid && (fc.slots[R.slot].flags & dpf::kFlagPf)) {
+    dpf::FlowSlot &f = fc.slots[R.slot];
+    const uint32_t act = f.pf & 0xffu;
+    int32_t e = by_id(g, f.pf_rule);
+    if (e < 0) {
+      // get_rule_from_pkt (nf.rs:206-324): would the current rules still do this?
+      const PfRuleRec *RR = g.at<PfRuleRec>(g.im.pf_rules);
+      uint32_t na[4], np;
+      if (R.src_vni && ports) {
+        if (act == DP_PF_DST_NAT) {
+          const int32_t k = lookup(g, R.src_vni, proto, fam, R.dst, dport);
+          if (k >= 0 && map(RR[k], R.dst, dport, na, np) && np == (f.pf >> 16) && RR[k].dst_vni == f.dst_vni &&
+              na[0] == f.pf_ip[0] && na[1] == f.pf_ip[1] && na[2] == f.pf_ip[2] && na[3] == f.pf_ip[3])
+            e = k;
+        } else {
+          const int32_t k = lookup(g, f.dst_vni, proto, f.pf_fam, f.pf_ip, f.pf >> 16);
+          if (k >= 0 && map(RR[k], f.pf_ip, f.pf >> 16, na, np) && np == sport && RR[k].dst_vni == R.src_vni &&
+              na[0] == R.src[0] && na[1] == R.src[1] && na[2] == R.src[2] && na[3] == R.src[3])
+            e = k;
+        }
+      }
+      if (e < 0) {
+        R.verdict = DP_DONE_NAT_NOT_PORT_FORWARDED;
+        q.invalidate(R.slot, idx);
+        return;
+      }
+      // reassign_port_fw_rule, both flows (nf.rs:290-320)
+      f.pf_rule = RR[e].id;
+      if (q.alive(f.related, f.related_tag)) fc.slots[f.related].pf_rule = RR[e].id;
+    }
+    const PfRuleRec &E = g.at<PfRuleRec>(g.im.pf_rules)[e];
+    R.nat = act | (f.pf & 0xffff0000u);
+    for (int j = 0; j < 4; j++) R.nat_ip[j] = f.pf_ip[j];
+    // refresh_port_fw_entry (flow_state.rs:216-264)
+    const uint32_t cur = (f.pf >> 8) & 0xffu, nw = next_status(tcp, tfl, act, cur);
+    q.set_nfs(R.slot, nw);
+    if (nw == DP_NFS_CLOSED || nw == DP_NFS_RESET) { q.invalidate(R.slot, idx); return; }
+    const uint64_t ext = nw == DP_NFS_ESTABLISHED ? E.estab_ns : E.init_ns;
+    q.reset_expiry(R.slot, ext);
+    if (nw == DP_NFS_ESTABLISHED && nw != cur && q.alive(f.related, f.related_tag)) q.reset_expiry(f.related, ext);
+    f.genid = fc.genid;
+    return;
+  }
+  // try_port_forwarding (nf.rs:174-204); can_be_port_forwarded (:54-94)
+  if (!R.src_vni) { R.verdict = DP_DONE_INTERNAL_FAILURE; return; }
+  const bool first_seg = (tfl & 2) && !(tfl & 0x3du);  // Tcp::is_first_segment (net/src/tcp/mod.rs:310-312)
+  if (!(R.bits & dpf::kPqEth) || !ports || (tcp && !first_seg) || !unicast(fam, R.dst)) {
+    R.verdict = DP_DONE_NAT_NOT_PORT_FORWARDED;
+    return;
+  }
+  const int32_t e = lookup(g, R.src_vni, proto, fam, R.dst, dport);
+  if (e < 0) { R.verdict = DP_DONE_NAT_NOT_PORT_FORWARDED; return; }
+  const PfRuleRec &E = g.at<PfRuleRec>(g.im.pf_rules)[e];
+  uint32_t na[4], np;
+  if (!map(E, R.dst, dport, na, np)) { R.verdict = DP_DONE_INTERNAL_FAILURE; return; }
+  // build_portfw_flow_keys (flow_state.rs:102-131): the key before static
+  // NAT (or the current one) and the reverse of the DNATed current key
+  dpf::FKey fk, rk;
+  const uint32_t kind = tcp ? DP_FLOW_TCP : DP_FLOW_UDP;
+  if (R.bits & dpf::kPqIkey) {
+    for (int j = 0; j < 11; j++) fk.w[j] = R.ikey[j];
+  } else {
+    fk.w[0] = R.src_vni;
+    fk.w[1] = fam | (kind << 8);
+    fk.w[2] = R.ports;
+    for (int j = 0; j < 4; j++) { fk.w[3 + j] = bswap(R.src[j]); fk.w[7 + j] = bswap(R.dst[j]); }
+  }
+  rk.w[0] = E.dst_vni;
+  rk.w[1] = fam | (kind << 8);
+  rk.w[2] = (np << 16) | sport;
+  for (int j = 0; j < 4; j++) { rk.w[3 + j] = bswap(na[j]); rk.w[7 + j] = bswap(R.src[j]); }
+  // (keys of distinct VPCs: related_pair never meets identical keys here)
+  R.nat = DP_PF_DST_NAT | (np << 16);
+  for (int j = 0; j < 4; j++) R.nat_ip[j] = na[j];
+  const uint64_t exp = fc.now + E.init_ns;
+  // compute_flow_flags_forward / _reverse (net/src/packet/meta.rs:264-287)
+  const bool ss = R.bits & dpf::kPqSnatSrc, sd = R.bits & dpf::kPqSnatDst;
+  const uint32_t fw_flags = DP_FLOW_INITIATOR | (ss ? DP_FLOW_REQ_STATIC_NAT_SRC : 0u) |
+                            (sd ? DP_FLOW_REQ_STATIC_NAT_DST : 0u);
+  const uint32_t rv_flags = (ss ? DP_FLOW_REQ_STATIC_NAT_DST : 0u) | (sd ? DP_FLOW_REQ_STATIC_NAT_SRC : 0u);
+  const uint32_t sf = q.insert(fk, false, idx);
+  if (sf == dpf::kNoSlot) { R.verdict = DP_DONE_FLOW_CAPACITY_EXCEEDED; return; }
+  dpf::FlowSlot &F = fc.slots[sf];
+  F.flags = fw_flags | dpf::kFlagPf;
+  F.dst_vni = E.dst_vni;  // setup_forward_flow (flow_state.rs:133-157)
+  F.genid = fc.genid;     // set_genid_pair
+  F.expires_at = exp;
+  F.pf = DP_PF_DST_NAT | (np << 16);  // NatFlowStatus::OneWay
+  F.pf_rule = E.id;
+  for (int j = 0; j < 4; j++) F.pf_ip[j] = na[j];
+  F.pf_fam = fam;
+  const uint32_t sr = q.insert(rk, true, idx);  // admitted at capacity: its related flow is Active
+  if (sr == dpf::kNoSlot) {
+    q.invalidate(sf, idx);
+    R.verdict = DP_DONE_FLOW_CAPACITY_EXCEEDED;
+    return;
+  }
+  dpf::FlowSlot &Rv = fc.slots[sr];
+  Rv.flags = rv_flags | dpf::kFlagPf;
+  Rv.dst_vni = E.src_vni;  // setup_reverse_flow (:159-177)
+  Rv.genid = fc.genid;
+  Rv.expires_at = exp;
+  Rv.pf = DP_PF_SRC_NAT | (dport << 16);
+  Rv.pf_rule = E.id;
+  for (int j = 0; j < 4; j++) Rv.pf_ip[j] = R.dst[j];
+  Rv.pf_fam = fam;
+  F.related = sr;
+  F.related_tag = Rv.state;
+  Rv.related = sf;
+  Rv.related_tag = F.state;
+}
+
+}  // namespace pfw
+
+// dp_pf_resolve: one workgroup.  The packets that reached PortForwarder, in
+// packet order (their bitmap, scanned 1024 packets per summary bit; the bits
+// are cleared for the next burst), then the reference's PortForwarder over
+// them one after the other -- the NatFlowStatus machine, expiries, rule
+// revalidation, invalidations and the flow pairs created, with
+// FlowTable::insert's capacity and replacement semantics -- leaving each
+// packet's decision in its record for the replay pass.
+__global__ void __launch_bounds__(1024) dp_pf_resolve(const uint8_t *__restrict__ img_base,
+                                                      const Image *__restrict__ im, dpf::FlowCtx fc) {
+  __shared__ uint32_t cnt[1024];
+  __shared__ uint32_t total;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) total = 0;
+  const uint32_t regions = (fc.n + 1023) / 1024;
+  for (uint32_t r0 = 0; r0 < regions; r0 += 1024) {
+    __syncthreads();
+    const uint32_t r = r0 + t;
+    uint32_t c = 0;
+    const bool hit = r < regions && ((fc.pf_sum[r >> 5] >> (r & 31)) & 1u);
+    if (hit) for (int w = 0; w < 32; w++) c += __popc(fc.pf_bits[r * 32 + w]);
+    cnt[t] = c;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan
+      const uint32_t v = t >= o ? cnt[t - o] : 0u;
+      __syncthreads();
+      cnt[t] += v;
+      __syncthreads();
+    }
+    uint32_t pos = total + cnt[t] - c;
+    if (hit) {
+      for (int w = 0; w < 32; w++) {
+        uint32_t b = fc.pf_bits[r * 32 + w];
+        fc.pf_bits[r * 32 + w] = 0;
+        while (b) {
+          const int k = __ffs(b) - 1;
+          b &= b - 1;
+          fc.pf_order[pos++] = r * 1024 + w * 32 + k;
+        }
+      }
+    }
+    __syncthreads();
+    if (t == 1023) total += cnt[1023];
+  }
+  __syncthreads();
+  for (uint32_t w = t; w < (regions + 31) / 32; w += 1024) fc.pf_sum[w] = 0;
+  if (t != 0) return;
+  fc.pf_cnt[1] = total;
+  const Img g{img_base, *im};
+  const pfw::Seq q{fc, g};
+  for (uint32_t k = 0; k < total; k++) pfw::resolve_one(q, fc.pf[fc.pf_of[fc.pf_order[k]]]);
+}
+
 // After the burst's pipeline kernel (flows variant), on its stream.
 // dp_flow_fixup: a verdict "allowed as the reply of a flow-scope-allowed
 // flow" stands only if the flow pair was still valid when the packet reached
@@ -2859,12 +3457,28 @@ __global__ void __launch_bounds__(256) dp_flow_fixup(const uint8_t *__restrict__
                                                      unsigned long long *__restrict__ stats) {
   const uint32_t cnt = fc.sens[0];
   const dpf::SensRec *recs = reinterpret_cast<const dpf::SensRec *>(fc.sens + 8);
+  const uint32_t nrep = fc.pf_cnt[2];
+  // a fill for packet idx: 1 in the table (its burst-local mark), 0 not in
+  // the table as the burst started, -1 replaced by dp_pf_resolve before idx
+  // (a fill replaced by packet j > idx counts with the mark it had)
+  auto fill_at = [&](uint32_t sl, uint32_t tag, uint32_t idx, uint32_t &mark) -> int {
+    if (sl > fc.mask) return 0;
+    if (fc.slots[sl].state == tag) { mark = fc.slots[sl].mark; return 1; }
+    for (uint32_t k = 0; k < nrep; k++)
+      if (fc.pf_repl[4 * k] == sl && fc.pf_repl[4 * k + 1] == tag) {
+        mark = fc.pf_repl[4 * k + 3];
+        return fc.pf_repl[4 * k + 2] > idx ? 1 : -1;
+      }
+    return 0;
+  };
   for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < cnt; r += gridDim.x * 256) {
     const dpf::SensRec R = recs[r];
     // the pair is invalid if either flow was invalidated (invalidate_pair
     // marks the flow it was called on; the related flow only while alive)
-    const bool rel = R.related <= fc.mask && fc.slots[R.related].state == R.related_tag;
-    if (fc.slots[R.slot].mark > R.idx && (!rel || fc.slots[R.related].mark > R.idx)) continue;  // still valid
+    uint32_t ms = 0, mr = dpf::kIdleMark;
+    const int own = fill_at(R.slot, R.slot_tag, R.idx, ms);
+    const int rel = fill_at(R.related, R.related_tag, R.idx, mr);
+    if (own == 1 && ms > R.idx && rel >= 0 && (rel == 0 || mr > R.idx)) continue;  // still valid
     dp_pkt_out_t o = out[R.idx];
     o.acl = (uint8_t)R.def_acl;
     if (meta) meta[R.idx].acl_rule = 0xffffffffu;
@@ -3038,18 +3652,30 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
                                          dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
                                          const void *fc_host, hipStream_t stream) {
   if (n == 0) return 0;
-  const dpf::FlowCtx fc = *reinterpret_cast<const dpf::FlowCtx *>(fc_host);
+  dpf::FlowCtx fc = *reinterpret_cast<const dpf::FlowCtx *>(fc_host);
   if (hipMemsetAsync(fc.events, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
   if (hipMemsetAsync(fc.sens, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
+  if (hipMemsetAsync(fc.pf_cnt, 0, sizeof(uint32_t) * 4, stream) != hipSuccess) return -5;
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
+  // first pass; PortForwarder's records in packet order; the replay of the
+  // packets that reached it (dp_pf_resolve's decisions)
+  fc.replay = 0;
   if (meta)
     hipLaunchKernelGGL((dp_pipeline_kernel<true, true>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
                        buf_bytes, in, out, meta, n, part, fc);
   else
     hipLaunchKernelGGL((dp_pipeline_kernel<true, false>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
                        buf_bytes, in, out, meta, n, part, fc);
+  hipLaunchKernelGGL(dp_pf_resolve, dim3(1), dim3(1024), 0, stream, img_base, im, fc);
+  fc.replay = 1;
+  if (meta)
+    hipLaunchKernelGGL((dp_pipeline_kernel<true, true, true>), dim3(blocks), dim3(TPB), 0, stream, img_base, im,
+                       buf, buf_bytes, in, out, meta, n, part, fc);
+  else
+    hipLaunchKernelGGL((dp_pipeline_kernel<true, false, true>), dim3(blocks), dim3(TPB), 0, stream, img_base, im,
+                       buf, buf_bytes, in, out, meta, n, part, fc);
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));

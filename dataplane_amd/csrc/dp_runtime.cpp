@@ -113,6 +113,7 @@ struct DevImage {
 struct DeviceTables {
   std::mutex mu;
   std::shared_ptr<DevImage> cur;
+  dpd::PfLineage pf;  // the port-forwarding entries of `cur` (PortFwTable::update lineage)
 };
 
 std::mutex g_dev_mu;
@@ -180,8 +181,13 @@ struct dp_ctx {
   dp_pkt_meta_t *mb_meta = nullptr;
   uint32_t mb_cap = 0;
   FlowScratch fl_ev, fl_sens;
+  // port forwarding scratch (dpf::FlowCtx pf*): records, counters, packet ->
+  // record, bitmaps (kept zero between bursts), order, replaced fills
+  FlowScratch pf_req, pf_cnt, pf_of, pf_bits, pf_order, pf_repl;
+  uint64_t pf_bits_n = 0;
   hipEvent_t fl_used = nullptr;
   bool fl_armed = false;
+  uint64_t clock = 0;                  // dp_ctx_set_option(DP_OPT_CLOCK)
 };
 
 namespace {
@@ -282,6 +288,7 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   c->fl_ev.release();
   c->fl_sens.release();
+  for (FlowScratch *x : {&c->pf_req, &c->pf_cnt, &c->pf_of, &c->pf_bits, &c->pf_order, &c->pf_repl}) x->release();
   if (c->mb_in) (void)hipHostFree(c->mb_in);
   if (c->mb_out) (void)hipHostFree(c->mb_out);
   if (c->mb_meta) (void)hipHostFree(c->mb_meta);
@@ -298,7 +305,13 @@ int dp_ctx_destroy(dp_ctx_t *c) {
 int dp_tables_publish(dp_ctx_t *c, const dp_tables_desc_t *tables) {
   if (!c || !tables) return fail(DP_EINVAL, "null argument");
   dpd::BuiltImage bi;
-  int rc = dpd::build_image(tables, bi);
+  DeviceTables &dt = dev_tables(c->device);
+  dpd::PfLineage pf;
+  {
+    std::lock_guard<std::mutex> lk(dt.mu);
+    pf = dt.pf;
+  }
+  int rc = dpd::build_image(tables, bi, &pf);
   if (rc) return fail(rc, "table compile rejected the descriptors");
   (void)hipSetDevice(c->device);
   drain_graveyard(c->device);  // images no burst reads any more
@@ -314,12 +327,12 @@ int dp_tables_publish(dp_ctx_t *c, const dp_tables_desc_t *tables) {
   if ((e = hipMemcpy(img->dev, bi.bytes.data(), bi.bytes.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return fail(DP_EIO, "upload table image", e);
   img->im = bi.im;
-  DeviceTables &dt = dev_tables(c->device);
   std::shared_ptr<DevImage> old;
   {
     std::lock_guard<std::mutex> lk(dt.mu);
     old = dt.cur;
     dt.cur = img;
+    dt.pf = std::move(pf);
   }
   // `old` is retired here only if no in-flight burst still references it
   return 0;
@@ -381,12 +394,34 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     dpf::FlowCtx fc{};
     fc.slots = ft->slots;
     fc.mask = ft->mask;
-    fc.max_probe = ft->max_probe;
+    fc.max_probe = 0;
     fc.n = n;
-    fc.events = static_cast<uint32_t *>(c->fl_ev.get(sizeof(uint32_t) * (1 + 4 * (uint64_t)n)));
+    fc.events = static_cast<uint32_t *>(c->fl_ev.get(sizeof(uint32_t) * (1 + 8 * (uint64_t)n)));
     fc.sens = static_cast<uint32_t *>(c->fl_sens.get(sizeof(uint32_t) * 8 + sizeof(dpf::SensRec) * (uint64_t)n));
     fc.genid = img->im.genid;
-    if (!fc.events || !fc.sens) {
+    fc.tmeta = ft->d_meta;
+    fc.capacity = ft->capacity;
+    fc.hard = ft->nslots - ft->nslots / 8;
+    fc.now = c->clock;
+    // port forwarding: the bitmaps stay zero between bursts (dp_pf_resolve
+    // clears what it reads); grown bitmaps start zeroed
+    const uint64_t words = ((uint64_t)n + 31) / 32, sum_words = ((uint64_t)n + 32767) / 32768;
+    fc.pf = static_cast<dpf::PfReq *>(c->pf_req.get(sizeof(dpf::PfReq) * (uint64_t)n));
+    fc.pf_cnt = static_cast<uint32_t *>(c->pf_cnt.get(sizeof(uint32_t) * 4));
+    fc.pf_of = static_cast<uint32_t *>(c->pf_of.get(sizeof(uint32_t) * (uint64_t)n));
+    fc.pf_order = static_cast<uint32_t *>(c->pf_order.get(sizeof(uint32_t) * (uint64_t)n));
+    fc.pf_repl = static_cast<uint32_t *>(c->pf_repl.get(sizeof(uint32_t) * 8 * ((uint64_t)n + 1)));
+    if (words + sum_words > c->pf_bits_n) {
+      c->pf_bits.release();
+      c->pf_bits_n = 0;
+      void *b = c->pf_bits.get(sizeof(uint32_t) * (words + sum_words));
+      if (b && hipMemsetAsync(b, 0, sizeof(uint32_t) * (words + sum_words), s) == hipSuccess)
+        c->pf_bits_n = words + sum_words;
+    }
+    fc.pf_bits = static_cast<uint32_t *>(c->pf_bits.p);
+    fc.pf_sum = fc.pf_bits ? fc.pf_bits + words : nullptr;
+    if (!fc.events || !fc.sens || !fc.pf || !fc.pf_cnt || !fc.pf_of || !fc.pf_order || !fc.pf_repl ||
+        c->pf_bits_n < words + sum_words) {
       (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
       return fail(DP_ENOMEM, "flow burst scratch");
     }
@@ -453,6 +488,11 @@ int dp_ctx_set_option(dp_ctx_t *c, int option, int64_t value) {
   if (option == DP_OPT_HOST_PATH) {
     if (value < DP_HOST_AUTO || value > DP_HOST_ZERO_COPY) return fail(DP_EINVAL, "bad host path mode");
     c->host_path = (int)value;
+    return 0;
+  }
+  if (option == DP_OPT_CLOCK) {
+    if (value < 0) return fail(DP_EINVAL, "negative clock");
+    c->clock = (uint64_t)value;
     return 0;
   }
   return fail(DP_EINVAL, "unknown option");

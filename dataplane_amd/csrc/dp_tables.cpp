@@ -604,11 +604,12 @@ int load_rules(const dp_rule_t *rs, uint32_t n, int fam, bool by_prio, int kind,
       return DP_EINVAL;                                                   // ACL
     if (kind == 1) {                                                      // FF remote
       if (r.src.len != 0 || r.sport_lo != 0 || r.sport_hi != 65535 || r.gate != 0) return DP_EINVAL;
-      if (r.action2 == DP_NAT_MASQUERADE || r.action2 == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
+      if (r.action2 == DP_NAT_MASQUERADE) return DP_ENOTSUP;
     }
     if (kind == 2) {                                                      // FF local
       if (r.dst.len != 0 || r.dport_lo != 0 || r.dport_hi != 65535) return DP_EINVAL;
-      if (r.action == DP_NAT_MASQUERADE || r.action == DP_NAT_PORT_FORWARDING) return DP_ENOTSUP;
+      if (r.action == DP_NAT_MASQUERADE) return DP_ENOTSUP;
+      if (r.gate > 1) return DP_EINVAL;                                   // SourceGate
     }
     out.push_back(CRule{r, i});
     // ACL: the verdict and its AclScope travel in one action word (both
@@ -621,9 +622,68 @@ int load_rules(const dp_rule_t *rs, uint32_t n, int fam, bool by_prio, int kind,
   return 0;
 }
 
+// ------------------------------------------------------------ port forwarding
+bool same_prefix(const dp_prefix_t &a, const dp_prefix_t &b) {
+  return a.family == b.family && a.len == b.len && memcmp(a.addr, b.addr, a.family == 4 ? 4 : 16) == 0;
+}
+// PortFwEntry::matches (objects.rs:159-166): all but the timeouts
+bool pf_matches(const dp_portfw_rule_t &a, const dp_portfw_rule_t &b) {
+  return a.src_vni == b.src_vni && a.proto == b.proto && a.dst_vni == b.dst_vni &&
+         same_prefix(a.ext_prefix, b.ext_prefix) && same_prefix(a.int_prefix, b.int_prefix) &&
+         a.ext_lo == b.ext_lo && a.ext_hi == b.ext_hi && a.int_lo == b.int_lo && a.int_hi == b.int_hi;
+}
+// PortFwEntry::new's checks (objects.rs:70-155, portrange.rs:33-42)
+bool pf_rule_ok(const dp_portfw_rule_t &r) {
+  if (r.proto != 6 && r.proto != 17) return false;
+  if (!valid_prefix(r.ext_prefix) || !valid_prefix(r.int_prefix)) return false;
+  if (r.ext_prefix.family != r.int_prefix.family || r.ext_prefix.len != r.int_prefix.len) return false;
+  if (!r.src_vni || !r.dst_vni || r.src_vni == r.dst_vni || r.src_vni >= (1u << 24) || r.dst_vni >= (1u << 24))
+    return false;
+  if (!r.ext_lo || !r.int_lo || r.ext_hi < r.ext_lo || r.int_hi < r.int_lo) return false;
+  return r.ext_hi - r.ext_lo == r.int_hi - r.int_lo;
+}
+// PortFwTable::update (objects.rs:284-300): entries of the previous
+// generation absent from the rule set go (their Weak refs die); the rules
+// are added last to first (add_entry, :256-274): one matching an entry at
+// its (key, prefix, port range) keeps it with the new timeouts, one whose
+// range overlaps another of the same key and prefix is refused
+// (RangeSet::insert_range, rangeset.rs:73-79).
+PfLineage pf_update(const PfLineage &prev, const dp_portfw_rule_t *rs, uint32_t n) {
+  PfLineage L;
+  L.next_id = prev.next_id;
+  for (const PfEntry &e : prev.live) {
+    bool keep = false;
+    for (uint32_t i = 0; i < n && !keep; i++) keep = pf_matches(e.r, rs[i]);
+    if (keep) L.live.push_back(e);
+  }
+  for (uint32_t k = n; k-- > 0;) {
+    const dp_portfw_rule_t &r = rs[k];
+    PfEntry *exist = nullptr;
+    bool overlap = false;
+    for (PfEntry &e : L.live) {
+      if (e.r.src_vni != r.src_vni || e.r.proto != r.proto || !same_prefix(e.r.ext_prefix, r.ext_prefix)) continue;
+      if (e.r.ext_lo == r.ext_lo && e.r.ext_hi == r.ext_hi) exist = &e;
+      if (e.r.ext_lo <= r.ext_hi && r.ext_lo <= e.r.ext_hi) overlap = true;
+    }
+    if (exist && pf_matches(exist->r, r)) {
+      exist->r.init_timeout_s = r.init_timeout_s;
+      exist->r.estab_timeout_s = r.estab_timeout_s;
+      continue;
+    }
+    if (!overlap) L.live.push_back(PfEntry{r, L.next_id++});
+  }
+  return L;
+}
+void be_words(const dp_prefix_t &p, uint32_t w[4]) {
+  for (int j = 0; j < 4; j++) {
+    w[j] = 0;
+    for (int b = 0; b < 4; b++) w[j] = (w[j] << 8) | (p.family == 4 && j > 0 ? 0 : p.addr[4 * j + b]);
+  }
+}
+
 }  // namespace
 
-int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
+int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   g_forms[0] = g_forms[1] = 0;
   g_group_stats.clear();
   if (!d || d->abi_version != DPGPU_ABI_VERSION) return DP_EINVAL;
@@ -1178,6 +1238,47 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
   im.nat_prs = ib.put(nprs);
   im.nat_ranges = ib.put(nranges);
 
+  // --- port forwarding (nat/src/portfw/portfwtable/)
+  for (uint32_t i = 0; i < d->n_portfw; i++)
+    if (!pf_rule_ok(d->portfw[i])) return DP_EINVAL;
+  const PfLineage none;
+  PfLineage L = pf_update(pf ? *pf : none, d->portfw, d->n_portfw);
+  std::vector<PfEntry> ents = L.live;
+  // lookup_cumulative (lpmmap.rs:108-116) over one key's entries: longest
+  // prefix first, the first whose prefix holds the address and range the port
+  std::stable_sort(ents.begin(), ents.end(), [](const PfEntry &a, const PfEntry &b) {
+    if (a.r.src_vni != b.r.src_vni) return a.r.src_vni < b.r.src_vni;
+    if (a.r.proto != b.r.proto) return a.r.proto < b.r.proto;
+    return a.r.ext_prefix.len > b.r.ext_prefix.len;
+  });
+  std::vector<PfRuleRec> pfrecs;
+  std::vector<KV> pkkv, pidkv;
+  for (size_t i = 0; i < ents.size(); i++) {
+    const dp_portfw_rule_t &r = ents[i].r;
+    PfRuleRec q{};
+    q.id = ents[i].id;
+    q.src_vni = r.src_vni;
+    q.dst_vni = r.dst_vni;
+    q.proto = r.proto;
+    q.fam = r.ext_prefix.family;
+    q.plen = r.ext_prefix.len;
+    q.ext_lo = r.ext_lo; q.ext_hi = r.ext_hi; q.int_lo = r.int_lo; q.int_hi = r.int_hi;
+    be_words(r.ext_prefix, q.ext);
+    be_words(r.int_prefix, q.inn);
+    q.init_ns = (uint64_t)(r.init_timeout_s ? r.init_timeout_s : 10) * 1000000000ull;  // objects.rs:50-52
+    q.estab_ns = (uint64_t)(r.estab_timeout_s ? r.estab_timeout_s : (r.proto == 6 ? 1800 : 30)) * 1000000000ull;
+    if (i == 0 || ents[i - 1].r.src_vni != r.src_vni || ents[i - 1].r.proto != r.proto)
+      pkkv.push_back(KV{r.src_vni, r.proto, 0, (uint32_t)i << 16});
+    pkkv.back().v++;
+    pidkv.push_back(KV{q.id, 0, 0, (uint32_t)i});
+    pfrecs.push_back(q);
+  }
+  if (pfrecs.size() >= 65536) return DP_ENOTSUP;
+  im.pf_keys = build_hash(ib, pkkv);
+  im.pf_ids = build_hash(ib, pidkv);
+  im.pf_rules = pfrecs.empty() ? ib.alloc(sizeof(PfRuleRec)) : ib.put(pfrecs);
+  im.n_pf = (uint32_t)pfrecs.size();
+
   ib.alloc(64);
   im.bytes = ib.b.size();
   // context records carry 32-bit image offsets (Mbi)
@@ -1185,6 +1286,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out) {
   out.bytes.swap(ib.b);
   out.im = im;
   out.pt_nodes = pb.nodes.size();
+  if (pf) *pf = std::move(L);
   return 0;
 }
 

@@ -16,7 +16,20 @@ struct BuiltImage {
   uint64_t pt_nodes = 0;
 };
 
-// Validate + lower the descriptors; returns 0 or a negative errno.
-int build_image(const dp_tables_desc_t *desc, BuiltImage &out);
+// The port-forwarding entries of a device's current generation (the lineage
+// PortFwTable::update carries from one publish to the next).
+struct PfEntry {
+  dp_portfw_rule_t r;
+  uint32_t id;
+};
+struct PfLineage {
+  std::vector<PfEntry> live;
+  uint32_t next_id = 1;
+};
+
+// Validate + lower the descriptors; returns 0 or a negative errno.  `pf`:
+// the device's port-forwarding lineage, updated with the new rule set (only
+// when the build succeeds).
+int build_image(const dp_tables_desc_t *desc, BuiltImage &out, PfLineage *pf = nullptr);
 
 }  // namespace dpd

@@ -118,6 +118,15 @@ class GpuPathNf:
         A.check(self.lib.dp_ctx_set_option(self.ctx, A.OPT_HOST_PATH, mode), "dp_ctx_set_option",
                 self.lib)
 
+    def set_option(self, option: int, value: int) -> None:
+        """dp_ctx_set_option (A.OPT_HOST_PATH, A.OPT_CLOCK: the flow clock in ns)."""
+        A.check(self.lib.dp_ctx_set_option(self.ctx, option, value), "dp_ctx_set_option", self.lib)
+
+    def set_clock(self, now_ns: int) -> None:
+        """Instant::now() for the bursts that follow (DP_OPT_CLOCK): the expiry
+        port forwarding gives the flows it creates and refreshes."""
+        self.set_option(A.OPT_CLOCK, now_ns)
+
     def process_arrays(self, buf: np.ndarray, inp: np.ndarray,
                        stats: Optional[np.ndarray] = None,
                        out: Optional[np.ndarray] = None,

@@ -25,6 +25,9 @@ struct uint4 { uint32_t x, y, z, w; };
 inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
 static inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
 static inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x); }
+// single-threaded host emulation: plain read-modify-write
+static inline uint32_t atomicAdd(uint32_t *p, uint32_t v) { uint32_t o = *p; *p = o + v; return o; }
+static inline uint32_t atomicOr(uint32_t *p, uint32_t v) { uint32_t o = *p; *p = o | v; return o; }
 static inline uint64_t __umul64hi(uint64_t a, uint64_t b) {
   return (uint64_t)(((unsigned __int128)a * b) >> 64);
 }

@@ -247,7 +247,7 @@ class OracleRunner:
     """The oracle (CPU restatement) as one device: tables generation lineage,
     a flow table and the flow clock."""
 
-    def __init__(self):
+    def __init__(self, **_):
         from oracle.pyoracle import Oracle, OracleFlows
         self._Oracle = Oracle
         self.fl = OracleFlows()

@@ -1,0 +1,88 @@
+"""GPU: port forwarding through the C ABI against the
+oracle -- the reference's PortForwarder tests (tests/golden/pfkat.py), every
+step compared bit-exactly: records, delivered bytes, the packet's flow
+(FlowStatus, port-forwarding state, expiry, generation, entry id) and the
+flow count."""
+import numpy as np
+import pytest
+
+from dataplane_amd import _abi as A
+from golden import pfkat
+from helpers import common_fields
+
+pytestmark = pytest.mark.gpu
+
+INFO = ("status", "flags", "dst_vni", "genid", "expires_at", "pf", "pf_status", "pf_port",
+        "pf_rule", "pf_family", "pf_ip")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def torch_first():
+    import torch
+    torch.cuda.init()
+
+
+@pytest.mark.parametrize("s", pfkat.scenarios(), ids=lambda s: s.name)
+def test_gpu_portfw_kat(s):
+    steps_o, steps_g = [], []
+    errs = pfkat.run_scenario(s, pfkat.OracleRunner(),
+                              lambda i, res, buf, info: steps_o.append((res.copy(), buf.copy(), info)))
+    assert not errs, errs
+    g = pfkat.GpuRunner()
+    try:
+        errs = pfkat.run_scenario(s, g, lambda i, res, buf, info: steps_g.append(
+            (res.copy(), buf.copy(), info, g.count())))
+    finally:
+        g.close()
+    assert not errs, "\n".join(errs)
+    for i, ((ro, bo, io), (rg, bg, ig, cnt)) in enumerate(zip(steps_o, steps_g)):
+        a, b = common_fields(ro, rg)
+        assert np.array_equal(a, b), f"step {i}: records {a} != {b}"
+        o = ro[0]
+        if o["done"] == A.DONE["Delivered"]:
+            assert bo[o["off"]:o["off"] + o["len"]].tobytes() == bg[o["off"]:o["off"] + o["len"]].tobytes(), \
+                f"step {i}: frame"
+        assert (io is None) == (ig is None), f"step {i}: flow attached"
+        if io is not None:
+            for k in INFO:
+                assert np.array_equal(io[k], ig[k]), f"step {i}: flow {k} {io[k]} != {ig[k]}"
+
+
+@pytest.mark.parametrize("seed,n_conn,capacity", [(1, 600, None), (2, 2000, None), (5, 400, 300)])
+def test_gpu_portfw_random_bursts(seed, n_conn, capacity):
+    """Seeded bursts (tests/pfgen.py): creations, repeats, replies, TCP
+    handshakes / teardowns / resets, uncovered packets, a rule-set change --
+    and, with a small capacity, flow-pair creation refused at capacity; GPU ==
+    oracle per burst (records, bytes, each packet's flow, every connection's
+    two flows by key) and the flow counts."""
+    import pfgen
+    got = {}
+    for name, mk in (("oracle", pfkat.OracleRunner), ("gpu", pfkat.GpuRunner)):
+        r = mk(slots=1 << 14) if name == "gpu" else mk()
+        steps = []
+        try:
+            pfgen.run(r, seed, n_conn, capacity, lambda k, res, buf, infos, look: steps.append(
+                (res.copy(), buf.copy(), infos.copy(), look.copy(), r.count())))
+        finally:
+            if name == "gpu":
+                r.close()
+        got[name] = steps
+    hist = {}
+    for k, (o, g) in enumerate(zip(got["oracle"], got["gpu"])):
+        (ro, bo, io, lo, co), (rg, bg, ig, lg, cg) = o, g
+        a, b = common_fields(ro, rg)
+        bad = np.nonzero(a != b)[0]
+        assert len(bad) == 0, f"burst {k}: {len(bad)} records differ, first {a[bad[0]]} vs {b[bad[0]]}"
+        for i in np.nonzero(ro["done"] == A.DONE["Delivered"])[0]:
+            s0, n0 = int(ro[i]["off"]), int(ro[i]["len"])
+            assert np.array_equal(bo[s0:s0 + n0], bg[s0:s0 + n0]), f"burst {k} packet {i}: frame"
+        for key in INFO:
+            assert np.array_equal(io[key], ig[key]), f"burst {k}: packets' flow {key} differ"
+            assert np.array_equal(lo[key], lg[key]), f"burst {k}: flows by key: {key} differ"
+        assert np.array_equal(lo["ref"] == A.FLOW_NONE, lg["ref"] == A.FLOW_NONE), f"burst {k}: presence"
+        assert co == cg, f"burst {k}: counts {co} vs {cg}"
+        for d in ro["done"]:
+            hist[A.DONE_NAMES[d]] = hist.get(A.DONE_NAMES[d], 0) + 1
+    assert hist.get("Delivered", 0) > n_conn
+    if capacity is not None:
+        assert hist.get("FlowCapacityExceeded", 0) > 0

@@ -41,3 +41,20 @@ def test_oracle_portfw_rule_lineage():
     o5 = tabs([], o4)
     o6 = tabs([pfkat.tcp_rule(ext_ports=(3022, 3022), int_ports=(1022, 1022))], o5)
     assert not o6.rule_alive(3) and o6.rule_alive(4)
+
+
+def test_oracle_portfw_random_bursts():
+    """The seeded port-forwarding bursts (tests/pfgen.py) through the oracle:
+    every kind of outcome occurs, and the flow table holds pairs."""
+    import pfgen
+    from dataplane_amd import _abi as A
+    seen = {}
+
+    def on_burst(k, res, buf, infos, look):
+        for d in res["done"]:
+            seen[A.DONE_NAMES[d]] = seen.get(A.DONE_NAMES[d], 0) + 1
+    r = pfkat.OracleRunner()
+    pfgen.run(r, seed=3, n_conn=300, on_burst=on_burst)
+    assert seen.get("Delivered", 0) > 500 and seen.get("NatNotPortForwarded", 0) > 10
+    ln, act = r.count()
+    assert ln > 200 and ln % 1 == 0 and act <= ln
