@@ -30,6 +30,12 @@ namespace {
 
 using namespace dpd;
 
+// Split build (Makefile): DP_PART k compiles pipeline instantiation k
+// (1..6) or everything else (0); without DP_PART one unit holds all.
+#ifndef DP_PART
+#define DP_PART -1
+#endif
+#define DP_IN_PART(k) (DP_PART < 0 || DP_PART == (k))
 #ifndef DP_TPB
 #define DP_TPB 128
 #endif
@@ -3390,6 +3396,7 @@ __device__ void resolve_one(const Seq &q, dpf::PfReq &R) {
 
 }  // namespace pfw
 
+#if DP_IN_PART(0)
 // dp_pf_resolve: one workgroup.  The packets that reached PortForwarder, in
 // packet order (their bitmap, scanned 1024 packets per summary bit; the bits
 // are cleared for the next burst), then the reference's PortForwarder over
@@ -3426,7 +3433,7 @@ __global__ void __launch_bounds__(1024) dp_pf_resolve(const uint8_t *__restrict_
         while (b) {
           const int k = __ffs(b) - 1;
           b &= b - 1;
-          fc.pf_order[pos++] = r * 1024 + w * 32 + k;
+          fc.pf_order[pos++] = r * 1024 + w * 32 + k;  // < n: only packets set bits
         }
       }
     }
@@ -3547,6 +3554,7 @@ __global__ void __launch_bounds__(DPD_STAT_SLOTS) dp_stats_reduce(unsigned long 
     if (t) atomicAdd(&stats[r], t);
   }
 }
+#endif  // DP_IN_PART(0)
 #endif
 
 }  // namespace
@@ -3596,7 +3604,45 @@ extern "C" void dpemu_run(const uint8_t *img_base, const void *image_struct, uin
 extern "C" void dpemu_trips_out(uint16_t *p) { dp_trip_out = p; }
 #endif
 #else
-// Launch wrapper used by the runtime (dp_runtime.cpp).
+// Launch wrappers used by the runtime (dp_runtime.cpp).  The pipeline
+// kernel's six instantiations (flows FL, meta MT, replay RP) each have a
+// runner; the split build compiles each in its own translation unit.
+#define DP_RUN_ARGS                                                                                             \
+  uint32_t blocks, hipStream_t s, const uint8_t *img_base, const Image *im, uint8_t *buf, uint64_t buf_bytes, \
+      const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n, unsigned long long *part,   \
+      const dpf::FlowCtx &fc
+#define DP_RUNNER(NAME, FL, MT, RP)                                                                   \
+  extern "C" void NAME(DP_RUN_ARGS) {                                                                 \
+    hipLaunchKernelGGL((dp_pipeline_kernel<FL, MT, RP>), dim3(blocks), dim3(TPB), 0, s, img_base, im, \
+                       buf, buf_bytes, in, out, meta, n, part, fc);                                   \
+  }
+extern "C" {
+void dpk_run_pipeline_000(DP_RUN_ARGS);
+void dpk_run_pipeline_010(DP_RUN_ARGS);
+void dpk_run_pipeline_100(DP_RUN_ARGS);
+void dpk_run_pipeline_110(DP_RUN_ARGS);
+void dpk_run_pipeline_101(DP_RUN_ARGS);
+void dpk_run_pipeline_111(DP_RUN_ARGS);
+}
+#if DP_IN_PART(1)
+DP_RUNNER(dpk_run_pipeline_000, false, false, false)
+#endif
+#if DP_IN_PART(2)
+DP_RUNNER(dpk_run_pipeline_010, false, true, false)
+#endif
+#if DP_IN_PART(3)
+DP_RUNNER(dpk_run_pipeline_100, true, false, false)
+#endif
+#if DP_IN_PART(4)
+DP_RUNNER(dpk_run_pipeline_110, true, true, false)
+#endif
+#if DP_IN_PART(5)
+DP_RUNNER(dpk_run_pipeline_101, true, false, true)
+#endif
+#if DP_IN_PART(6)
+DP_RUNNER(dpk_run_pipeline_111, true, true, true)
+#endif
+#if DP_IN_PART(0)
 #if defined(DP_TIMING)
 extern "C" int dp_debug_stage_cycles(unsigned long long *out16, int reset) {
   if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stage_cycles), 16 * sizeof(unsigned long long)) != hipSuccess) return -5;
@@ -3632,12 +3678,9 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_de
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
-  if (meta)
-    hipLaunchKernelGGL((dp_pipeline_kernel<false, true>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                       buf_bytes, in, out, meta, n, part, dpf::FlowCtx{});
-  else
-    hipLaunchKernelGGL((dp_pipeline_kernel<false, false>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                       buf_bytes, in, out, meta, n, part, dpf::FlowCtx{});
+  const dpf::FlowCtx nofc{};
+  if (meta) dpk_run_pipeline_010(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, nofc);
+  else dpk_run_pipeline_000(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, nofc);
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));
@@ -3662,20 +3705,12 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   // first pass; PortForwarder's records in packet order; the replay of the
   // packets that reached it (dp_pf_resolve's decisions)
   fc.replay = 0;
-  if (meta)
-    hipLaunchKernelGGL((dp_pipeline_kernel<true, true>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                       buf_bytes, in, out, meta, n, part, fc);
-  else
-    hipLaunchKernelGGL((dp_pipeline_kernel<true, false>), dim3(blocks), dim3(TPB), 0, stream, img_base, im, buf,
-                       buf_bytes, in, out, meta, n, part, fc);
+  if (meta) dpk_run_pipeline_110(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+  else dpk_run_pipeline_100(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   hipLaunchKernelGGL(dp_pf_resolve, dim3(1), dim3(1024), 0, stream, img_base, im, fc);
   fc.replay = 1;
-  if (meta)
-    hipLaunchKernelGGL((dp_pipeline_kernel<true, true, true>), dim3(blocks), dim3(TPB), 0, stream, img_base, im,
-                       buf, buf_bytes, in, out, meta, n, part, fc);
-  else
-    hipLaunchKernelGGL((dp_pipeline_kernel<true, false, true>), dim3(blocks), dim3(TPB), 0, stream, img_base, im,
-                       buf, buf_bytes, in, out, meta, n, part, fc);
+  if (meta) dpk_run_pipeline_111(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+  else dpk_run_pipeline_101(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));
@@ -3685,4 +3720,5 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   hipLaunchKernelGGL(dp_flow_apply, dim3(fb), dim3(256), 0, stream, fc);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+#endif  // DP_IN_PART(0)
 #endif

@@ -404,8 +404,10 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.hard = ft->nslots - ft->nslots / 8;
     fc.now = c->clock;
     // port forwarding: the bitmaps stay zero between bursts (dp_pf_resolve
-    // clears what it reads); grown bitmaps start zeroed
-    const uint64_t words = ((uint64_t)n + 31) / 32, sum_words = ((uint64_t)n + 32767) / 32768;
+    // clears what it reads); grown bitmaps start zeroed.  dp_pf_resolve reads
+    // the bitmap a whole 1024-packet region (32 words) at a time, so it spans
+    // whole regions; the summary words sit after them
+    const uint64_t words = ((uint64_t)n + 1023) / 1024 * 32, sum_words = ((uint64_t)n + 32767) / 32768;
     fc.pf = static_cast<dpf::PfReq *>(c->pf_req.get(sizeof(dpf::PfReq) * (uint64_t)n));
     fc.pf_cnt = static_cast<uint32_t *>(c->pf_cnt.get(sizeof(uint32_t) * 4));
     fc.pf_of = static_cast<uint32_t *>(c->pf_of.get(sizeof(uint32_t) * (uint64_t)n));
