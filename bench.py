@@ -434,13 +434,21 @@ def main() -> None:
                         t_host.append(time.perf_counter() - t0)
                 return sorted(t_host)[len(t_host) // 2]
             th = time_host(A.HOST_COPY)
-            pcie_bytes = 2 * w.buf.nbytes + n * (A.PKT_IN.itemsize + A.PKT_OUT.itemsize)
+            # what crosses PCIe: each frame's 16-byte span in (+ its position)
+            # and out (+ the 96 B headroom where routes encapsulate: C4), the
+            # in / out records
+            off = w.inp["off"].astype(np.int64)
+            span = int((((off + w.inp["len"] + 15) >> 4) - (off >> 4)).sum()) * 16
+            grow = 96 * n if w.config == 4 else 0
+            pcie_bytes = 2 * span + grow + n * (A.PKT_IN.itemsize + A.PKT_OUT.itemsize + 4)
             host = {"mpps_median": round(n / th / 1e6, 3), "runs": 5,
                     "pcie_bytes_per_burst": pcie_bytes,
+                    "pcie_bytes_per_pkt": round(pcie_bytes / n, 1),
                     "pcie_gbs": round(pcie_bytes / th / 1e9, 2),
-                    "what": "dp_process_burst on pinned host buffers: the burst's slot spans "
-                            "(headroom + frame) and records H2D, kernel, D2H, in chunks of 64K+ "
-                            "packets on 3 streams"}
+                    "what": "dp_process_burst on pinned host buffers, staged copies: host "
+                            "threads pack the frames' 16-byte spans, spans + records H2D, "
+                            "kernel, packed spans + records D2H, frames written back in "
+                            "place; chunks of 64K+ packets on 3 streams"}
             try:
                 tz = time_host(A.HOST_ZERO_COPY)
                 host["zero_copy"] = {

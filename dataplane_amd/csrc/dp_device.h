@@ -376,7 +376,7 @@ struct Image {
   HashMap pf_ids;
   uint64_t pf_rules;         // PfRuleRec[]
   uint32_t n_pf;
-  uint32_t pad_pf;
+  uint32_t may_encap;        // some FibEntry encapsulates: an output may start before its frame
 };
 
 // 32-bit mixing hash for the open-addressing maps (host and device agree)

@@ -2344,7 +2344,10 @@ __device__ __forceinline__ void stage_portfw(const Frame &F, const Hdr &H, State
     fp.pf_rec = rec;
     fp.deferred = true;
   } else {
-    if (rp->verdict != dpf::kPfForward) { done(S, (uint8_t)rp->verdict); return; }
+    // a flow pair refused at capacity was translated before the inserts
+    // (do_port_forwarding, nf.rs:142-163): its metadata says so
+    const uint32_t v = rp->verdict;
+    if (v != dpf::kPfForward && v != DP_DONE_FLOW_CAPACITY_EXCEEDED) { done(S, (uint8_t)v); return; }
     // nat_packet (portfw/packet.rs:42-154): address and port of the side the
     // action names, each only if it changes
     const bool src = (rp->nat & 0xffu) == DP_PF_SRC_NAT;
@@ -2363,6 +2366,7 @@ __device__ __forceinline__ void stage_portfw(const Frame &F, const Hdr &H, State
       if (pp != port) { pp = port; mod = true; }
     }
     if (mod) S.flags |= DP_META_REFR_CHKSUM | (src ? DP_META_NATTED_SRC : DP_META_NATTED_DST);
+    if (v != dpf::kPfForward) done(S, (uint8_t)v);
   }
 }
 
@@ -3661,6 +3665,55 @@ __global__ void __launch_bounds__(256) dp_mark_failed(const dp_pkt_in_t *__restr
   if (i >= n) return;
   out[i] = out_record(in[i].off, in[i].len, DP_DONE_INTERNAL_FAILURE);
   if (meta) meta[i] = meta_none();
+}
+
+// Compact host staging (dp_process_burst, staged copies).  Packet i's span
+// is [in.off & ~15, (in.off + in.len + 15) & ~15) of the burst buffer; the
+// host sends the spans back to back (span i at 16 * pos[i] of `cin`).
+// dp_stage_expand puts each span at its own offset of the device burst
+// buffer; dp_stage_collect packs [span start - grow, span end) of every
+// packet at 16 * pos[i] + grow * i of `cout` (grow: DP_HEADROOM when an output may
+// start in front of its frame -- VXLAN encap -- else 0).  One wave per 64
+// packets, each lane its own packet's 16-byte chunks.
+__device__ __forceinline__ uint32_t span_lo(const dp_pkt_in_t &p) { return p.off & ~15u; }
+__device__ __forceinline__ uint32_t span_hi(const dp_pkt_in_t &p) { return (p.off + p.len + 15u) & ~15u; }
+
+__global__ void __launch_bounds__(256) dp_stage_expand(const uint8_t *__restrict__ cin, const uint32_t *__restrict__ pos,
+                                                       const dp_pkt_in_t *__restrict__ in, uint8_t *__restrict__ buf,
+                                                       uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const dp_pkt_in_t p = in[i];
+  const uint4 *s = reinterpret_cast<const uint4 *>(cin + 16ull * pos[i]);
+  uint4 *d = reinterpret_cast<uint4 *>(buf + span_lo(p));
+  const uint32_t c = (span_hi(p) - span_lo(p)) >> 4;
+  for (uint32_t k = 0; k < c; k++) d[k] = s[k];
+}
+
+__global__ void __launch_bounds__(256) dp_stage_collect(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ pos,
+                                                        const dp_pkt_in_t *__restrict__ in, uint8_t *__restrict__ cout,
+                                                        uint32_t grow, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const dp_pkt_in_t p = in[i];
+  const uint4 *s = reinterpret_cast<const uint4 *>(buf + span_lo(p) - grow);
+  uint4 *d = reinterpret_cast<uint4 *>(cout + 16ull * pos[i] + (uint64_t)grow * i);
+  const uint32_t c = (span_hi(p) - span_lo(p) + grow) >> 4;
+  for (uint32_t k = 0; k < c; k++) d[k] = s[k];
+}
+
+extern "C" int dpk_stage_expand(const uint8_t *cin, const uint32_t *pos, const dp_pkt_in_t *in, uint8_t *buf,
+                                uint32_t n, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dp_stage_expand, dim3((n + 255) / 256), dim3(256), 0, stream, cin, pos, in, buf, n);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int dpk_stage_collect(const uint8_t *buf, const uint32_t *pos, const dp_pkt_in_t *in, uint8_t *cout,
+                                 uint32_t grow, uint32_t n, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dp_stage_collect, dim3((n + 255) / 256), dim3(256), 0, stream, buf, pos, in, cout, grow, n);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,

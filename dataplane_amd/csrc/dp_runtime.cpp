@@ -24,6 +24,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dpgpu.h"
@@ -36,6 +37,10 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_de
                                    hipStream_t stream);
 extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
                                hipStream_t stream);
+extern "C" int dpk_stage_expand(const uint8_t *cin, const uint32_t *pos, const dp_pkt_in_t *in, uint8_t *buf,
+                                uint32_t n, hipStream_t stream);
+extern "C" int dpk_stage_collect(const uint8_t *buf, const uint32_t *pos, const dp_pkt_in_t *in, uint8_t *cout,
+                                 uint32_t grow, uint32_t n, hipStream_t stream);
 extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                          dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
@@ -167,6 +172,16 @@ struct dp_ctx {
   dp_pkt_meta_t *d_meta = nullptr;
   uint64_t *d_stats = nullptr;
   uint32_t cap_n = 0;
+  uint32_t *d_pos = nullptr;           // staged copies: span positions (16-byte units)
+  // staged copies: pinned host side (records, positions, packed spans in and
+  // out) and the packed spans on the device
+  dp_pkt_in_t *h_in = nullptr;
+  dp_pkt_out_t *h_out = nullptr;
+  dp_pkt_meta_t *h_meta = nullptr;
+  uint32_t *h_pos = nullptr;
+  uint8_t *h_cin = nullptr, *h_cout = nullptr, *d_cin = nullptr, *d_cout = nullptr;
+  uint64_t cin_cap = 0, cout_cap = 0;
+  std::vector<hipEvent_t> chunk_ev;    // per chunk: its D2H has landed
   hipStream_t hs[kHostStreams] = {};   // host-path copy/compute streams
   hipEvent_t hev[kHostStreams + 1] = {};
   bool host_streams = false;
@@ -211,6 +226,25 @@ hipEvent_t take_event(dp_ctx *c) {
   hipEvent_t e = nullptr;
   if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
   return e;
+}
+
+// Host threads for a burst's gather / write-back: one per 32K packets, at
+// most the machine's threads (capped at 16).
+uint32_t host_threads(uint32_t n) {
+  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  return std::max(1u, std::min(hw, n / 32768));
+}
+template <class F>
+void par_for(uint32_t parts, F &&f) {
+  if (parts <= 1) {
+    f(0u);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(parts - 1);
+  for (uint32_t t = 1; t < parts; t++) th.emplace_back([&f, t] { f(t); });
+  f(0u);
+  for (auto &x : th) x.join();
 }
 
 // Every packet of a failed burst is InternalFailure (dpgpu.h conventions,
@@ -285,6 +319,10 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->d_in) (void)hipFree(c->d_in);
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_meta) (void)hipFree(c->d_meta);
+  for (void *p : {(void *)c->d_pos, (void *)c->d_cin, (void *)c->d_cout}) if (p) (void)hipFree(p);
+  for (void *p : {(void *)c->h_in, (void *)c->h_out, (void *)c->h_meta, (void *)c->h_pos, (void *)c->h_cin, (void *)c->h_cout})
+    if (p) (void)hipHostFree(p);
+  for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
   if (c->d_stats) (void)hipFree(c->d_stats);
   c->fl_ev.release();
   c->fl_sens.release();
@@ -547,7 +585,18 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     }
     if (c->host_path == DP_HOST_ZERO_COPY) return bail(DP_EINVAL, "zero-copy needs pinned, mapped, 16-byte aligned buffers", hipSuccess);
   }
-  uint64_t need = ((buf_bytes + 15) & ~15ull) + 16;
+  // Staged copies (memory the device cannot map): only the frames cross the
+  // link.  Host threads pack each packet's 16-byte span [off & ~15,
+  // (off + len + 15) & ~15) back to back into pinned staging.  Per chunk of
+  // >= kHostChunk packets, on kHostStreams streams: the spans, their
+  // positions and the records go H2D, dp_stage_expand puts every span at its
+  // own offset of a device copy of the burst buffer, the pipeline runs, and
+  // dp_stage_collect packs each span -- grown in front by the headroom (DP_HEADROOM) when an
+  // output may start before its frame (VXLAN encap) -- for the D2H.  Host
+  // threads then write each delivered frame back in place.  PCIe carries the
+  // frame spans, 16 B of record each way (+ the meta records) and, with
+  // encap, DP_HEADROOM bytes of headroom out (a VXLAN-over-IPv6 outer stack is 70 B).  With a flow table the burst is one launch.
+  const uint64_t need = ((buf_bytes + 15) & ~15ull) + 16;
   if (need > c->d_buf_cap) {
     if (c->d_buf) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->d_buf); }
     c->d_buf = nullptr;
@@ -556,25 +605,66 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
   }
   if (n > c->cap_n) {
     (void)hipStreamSynchronize(c->stream);
-    if (c->d_in) (void)hipFree(c->d_in);
-    if (c->d_out) (void)hipFree(c->d_out);
-    if (c->d_meta) (void)hipFree(c->d_meta);
-    c->d_in = nullptr; c->d_out = nullptr; c->d_meta = nullptr; c->cap_n = 0;
-    if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess) return bail(DP_ENOMEM, "hipMalloc in", e);
-    if ((e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess) return bail(DP_ENOMEM, "hipMalloc out", e);
-    if ((e = hipMalloc(&c->d_meta, sizeof(dp_pkt_meta_t) * n)) != hipSuccess) return bail(DP_ENOMEM, "hipMalloc meta", e);
+    for (void *p : {(void *)c->d_in, (void *)c->d_out, (void *)c->d_meta, (void *)c->d_pos}) if (p) (void)hipFree(p);
+    for (void *p : {(void *)c->h_in, (void *)c->h_out, (void *)c->h_meta, (void *)c->h_pos}) if (p) (void)hipHostFree(p);
+    c->d_in = nullptr; c->d_out = nullptr; c->d_meta = nullptr; c->d_pos = nullptr;
+    c->h_in = nullptr; c->h_out = nullptr; c->h_meta = nullptr; c->h_pos = nullptr;
+    c->cap_n = 0;
+    if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess ||
+        (e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess ||
+        (e = hipMalloc(&c->d_meta, sizeof(dp_pkt_meta_t) * n)) != hipSuccess ||
+        (e = hipMalloc(&c->d_pos, sizeof(uint32_t) * n)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_meta, sizeof(dp_pkt_meta_t) * n)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_pos, sizeof(uint32_t) * n)) != hipSuccess)
+      return bail(DP_ENOMEM, "burst records (device / pinned)", e);
     c->cap_n = n;
   }
   dp_pkt_meta_t *dm = meta ? c->d_meta : nullptr;
   hipStream_t s = c->stream;
-  // packets in buffer order with disjoint slots: chunked, overlapped copies
-  // of each chunk's own byte span; anything else: one whole-buffer copy
-  bool ordered = true;
-  for (uint32_t i = 1; i < n && ordered; i++)
-    ordered = in[i].off - DP_HEADROOM >= (uint64_t)in[i - 1].off + in[i - 1].len;
-  // with a flow table the burst stays one launch: its packets share flow state
-  // in the reference's burst order
-  const uint32_t nch = ordered && !c->ft ? std::max<uint32_t>(1, std::min<uint32_t>(n / kHostChunk, 256)) : 1;
+  const uint32_t grow = [&] {
+    auto img = current(c);
+    return img && img->im.may_encap ? (uint32_t)DP_HEADROOM : 0u;
+  }();
+  // spans: per-thread sums, then positions (16-byte units) and the gather
+  const uint32_t T = host_threads(n);
+  std::vector<uint64_t> acc(T + 1, 0);
+  par_for(T, [&](uint32_t t) {
+    uint64_t sum = 0;
+    for (uint32_t i = (uint32_t)((uint64_t)n * t / T), b = (uint32_t)((uint64_t)n * (t + 1) / T); i < b; i++)
+      sum += ((in[i].off + in[i].len + 15u) >> 4) - (in[i].off >> 4);
+    acc[t + 1] = sum;
+  });
+  for (uint32_t t = 0; t < T; t++) acc[t + 1] += acc[t];
+  const uint64_t units = acc[T];
+  if (units >= (1ull << 32)) return bail(DP_EINVAL, "burst spans beyond 64 GiB", hipSuccess);
+  const uint64_t in_bytes = 16 * units, out_bytes = in_bytes + (uint64_t)grow * n;
+  if (in_bytes > c->cin_cap || out_bytes > c->cout_cap) {
+    (void)hipStreamSynchronize(c->stream);
+    for (void *p : {(void *)c->d_cin, (void *)c->d_cout}) if (p) (void)hipFree(p);
+    for (void *p : {(void *)c->h_cin, (void *)c->h_cout}) if (p) (void)hipHostFree(p);
+    c->d_cin = c->d_cout = c->h_cin = c->h_cout = nullptr;
+    c->cin_cap = c->cout_cap = 0;
+    const uint64_t ci = std::max<uint64_t>(in_bytes, 1 << 20), co = std::max<uint64_t>(out_bytes, 1 << 20);
+    if ((e = hipMalloc(&c->d_cin, ci)) != hipSuccess || (e = hipMalloc(&c->d_cout, co)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_cin, ci)) != hipSuccess || (e = hipHostMalloc(&c->h_cout, co)) != hipSuccess)
+      return bail(DP_ENOMEM, "frame staging (device / pinned)", e);
+    c->cin_cap = ci;
+    c->cout_cap = co;
+  }
+  par_for(T, [&](uint32_t t) {
+    uint64_t p = acc[t];
+    for (uint32_t i = (uint32_t)((uint64_t)n * t / T), b = (uint32_t)((uint64_t)n * (t + 1) / T); i < b; i++) {
+      const uint64_t lo = in[i].off & ~15u, u = ((in[i].off + in[i].len + 15u) >> 4) - (in[i].off >> 4);
+      c->h_pos[i] = (uint32_t)p;
+      // the rounded-up end may lie past the caller's buffer: never read there
+      memcpy(c->h_cin + 16 * p, buf + lo, std::min<uint64_t>(16 * u, buf_bytes - lo));
+      c->h_in[i] = in[i];
+      p += u;
+    }
+  });
+  const uint32_t nch = !c->ft ? std::max<uint32_t>(1, std::min<uint32_t>(n / kHostChunk, 256)) : 1;
   if (nch > 1 && !c->host_streams) {
     for (int k = 0; k < kHostStreams; k++)
       if ((e = hipStreamCreateWithFlags(&c->hs[k], hipStreamNonBlocking)) != hipSuccess)
@@ -584,61 +674,93 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
         return bail(DP_EIO, "hipEventCreate (host path)", e);
     c->host_streams = true;
   }
+  while (c->chunk_ev.size() < nch) {
+    hipEvent_t ev = nullptr;
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bail(DP_EIO, "hipEventCreate (chunks)", e);
+    c->chunk_ev.push_back(ev);
+  }
   if (stats && (e = hipMemsetAsync(c->d_stats, 0, sizeof(uint64_t) * DP_DONE_COUNT, s)) != hipSuccess)
     return bail(DP_EIO, "memset stats", e);
-  if (nch == 1) {
-    if ((e = hipMemcpyAsync(c->d_buf, buf, buf_bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D burst", e);
-    if ((e = hipMemcpyAsync(c->d_in, in, sizeof(dp_pkt_in_t) * n, hipMemcpyHostToDevice, s)) != hipSuccess) return bail(DP_EIO, "H2D records", e);
-    int rc = dp_process_burst_device(c, c->d_buf, need, c->d_in, c->d_out, dm, n, stats ? c->d_stats : nullptr, s);
-    if (rc) {
-      (void)hipStreamSynchronize(s);
-      mark_failed_host(in, out, meta, n);
-      return rc;
-    }
-    if ((e = hipMemcpyAsync(buf, c->d_buf, buf_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H burst", e);
-    if ((e = hipMemcpyAsync(out, c->d_out, sizeof(dp_pkt_out_t) * n, hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H records", e);
-    if (meta && (e = hipMemcpyAsync(meta, dm, sizeof(dp_pkt_meta_t) * n, hipMemcpyDeviceToHost, s)) != hipSuccess)
-      return bail(DP_EIO, "D2H meta", e);
-  } else {
-    // every host stream starts after the context stream's prior work (and
-    // the stats clear); the context stream then waits for all of them
+  // every host stream starts after the context stream's prior work (and the
+  // stats clear); the context stream then waits for all of them
+  if (nch > 1) {
     if ((e = hipEventRecord(c->hev[kHostStreams], s)) != hipSuccess) return bail(DP_EIO, "event record", e);
     for (int k = 0; k < kHostStreams; k++)
       if ((e = hipStreamWaitEvent(c->hs[k], c->hev[kHostStreams], 0)) != hipSuccess) return bail(DP_EIO, "stream wait", e);
-    int rc = 0;
-    for (uint32_t k = 0; k < nch && !rc; k++) {
-      const uint32_t first = (uint32_t)((uint64_t)n * k / nch);
-      const uint32_t cnt = (uint32_t)((uint64_t)n * (k + 1) / nch) - first;
-      // byte span [lo, hi) of the chunk: from its first packet's headroom (16-aligned, never
-      // below the previous packet's end) to its last frame's end -- disjoint across chunks
-      const uint64_t prev_end = first ? (uint64_t)in[first - 1].off + in[first - 1].len : 0;
-      const uint64_t lo = std::max<uint64_t>(prev_end, (in[first].off - DP_HEADROOM) & ~15ull);
-      const uint64_t hi = (uint64_t)in[first + cnt - 1].off + in[first + cnt - 1].len;
-      hipStream_t hs = c->hs[k % kHostStreams];
-      if ((e = hipMemcpyAsync(c->d_buf + lo, buf + lo, hi - lo, hipMemcpyHostToDevice, hs)) != hipSuccess ||
-          (e = hipMemcpyAsync(c->d_in + first, in + first, sizeof(dp_pkt_in_t) * cnt, hipMemcpyHostToDevice, hs)) != hipSuccess) {
-        rc = fail(DP_EIO, "H2D chunk", e);
-        break;
-      }
-      if ((rc = dp_process_burst_device(c, c->d_buf, need, c->d_in + first, c->d_out + first, dm ? dm + first : nullptr,
-                                        cnt, stats ? c->d_stats : nullptr, hs)))
-        break;
-      if ((e = hipMemcpyAsync(buf + lo, c->d_buf + lo, hi - lo, hipMemcpyDeviceToHost, hs)) != hipSuccess ||
-          (e = hipMemcpyAsync(out + first, c->d_out + first, sizeof(dp_pkt_out_t) * cnt, hipMemcpyDeviceToHost, hs)) != hipSuccess ||
-          (meta && (e = hipMemcpyAsync(meta + first, dm + first, sizeof(dp_pkt_meta_t) * cnt, hipMemcpyDeviceToHost, hs)) != hipSuccess)) {
-        rc = fail(DP_EIO, "D2H chunk", e);
-        break;
-      }
+  }
+  int rc = 0;
+  auto chunk_of = [&](uint32_t k, uint32_t &first, uint32_t &cnt) {
+    first = (uint32_t)((uint64_t)n * k / nch);
+    cnt = (uint32_t)((uint64_t)n * (k + 1) / nch) - first;
+  };
+  for (uint32_t k = 0; k < nch && !rc; k++) {
+    uint32_t first, cnt;
+    chunk_of(k, first, cnt);
+    hipStream_t hs = nch == 1 ? s : c->hs[k % kHostStreams];
+    const uint64_t b0 = 16ull * c->h_pos[first], b1 = first + cnt < n ? 16ull * c->h_pos[first + cnt] : in_bytes;
+    const uint64_t o0 = b0 + (uint64_t)grow * first, o1 = b1 + (uint64_t)grow * (first + cnt);
+    if ((e = hipMemcpyAsync(c->d_cin + b0, c->h_cin + b0, b1 - b0, hipMemcpyHostToDevice, hs)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->d_pos + first, c->h_pos + first, sizeof(uint32_t) * cnt, hipMemcpyHostToDevice, hs)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->d_in + first, c->h_in + first, sizeof(dp_pkt_in_t) * cnt, hipMemcpyHostToDevice, hs)) != hipSuccess) {
+      rc = fail(DP_EIO, "H2D chunk", e);
+      break;
     }
+    if (dpk_stage_expand(c->d_cin, c->d_pos + first, c->d_in + first, c->d_buf, cnt, hs)) { rc = fail(DP_EIO, "stage expand"); break; }
+    if ((rc = dp_process_burst_device(c, c->d_buf, need, c->d_in + first, c->d_out + first, dm ? dm + first : nullptr,
+                                      cnt, stats ? c->d_stats : nullptr, hs)))
+      break;
+    if (dpk_stage_collect(c->d_buf, c->d_pos + first, c->d_in + first, c->d_cout + (uint64_t)grow * first, grow, cnt, hs)) {
+      rc = fail(DP_EIO, "stage collect");
+      break;
+    }
+    if ((e = hipMemcpyAsync(c->h_cout + o0, c->d_cout + o0, o1 - o0, hipMemcpyDeviceToHost, hs)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->h_out + first, c->d_out + first, sizeof(dp_pkt_out_t) * cnt, hipMemcpyDeviceToHost, hs)) != hipSuccess ||
+        (meta && (e = hipMemcpyAsync(c->h_meta + first, dm + first, sizeof(dp_pkt_meta_t) * cnt, hipMemcpyDeviceToHost, hs)) != hipSuccess) ||
+        (e = hipEventRecord(c->chunk_ev[k], hs)) != hipSuccess) {
+      rc = fail(DP_EIO, "D2H chunk", e);
+      break;
+    }
+  }
+  if (nch > 1) {
     for (int k = 0; k < kHostStreams; k++) {
       (void)hipEventRecord(c->hev[k], c->hs[k]);
       (void)hipStreamWaitEvent(s, c->hev[k], 0);
     }
-    if (rc) {
-      (void)hipStreamSynchronize(s);
-      mark_failed_host(in, out, meta, n);
-      return rc;
+  }
+  if (rc) {
+    (void)hipStreamSynchronize(s);
+    mark_failed_host(in, out, meta, n);
+    return rc;
+  }
+  // write-back as each chunk lands: records, and each delivered frame from
+  // its packed span (an output outside its staged span -- a publish that
+  // added encapsulation between this burst's staging and its launch -- is an
+  // InternalFailure of that packet)
+  std::atomic<int> werr{0};
+  const uint32_t W = std::min<uint32_t>(T, nch);
+  par_for(W, [&](uint32_t t) {
+    (void)hipSetDevice(c->device);
+    for (uint32_t k = t; k < nch; k += W) {
+      if (hipEventSynchronize(c->chunk_ev[k]) != hipSuccess) { werr = 1; continue; }
+      uint32_t first, cnt;
+      chunk_of(k, first, cnt);
+      for (uint32_t i = first; i < first + cnt; i++) {
+        dp_pkt_out_t o = c->h_out[i];
+        if (o.done == DP_DONE_DELIVERED) {
+          const uint64_t lo = (uint64_t)(in[i].off & ~15u) - grow, hi = (in[i].off + in[i].len + 15u) & ~15u;
+          if (o.off >= lo && (uint64_t)o.off + o.len <= hi && (uint64_t)o.off + o.len <= buf_bytes)
+            memcpy(buf + o.off, c->h_cout + 16ull * c->h_pos[i] + (uint64_t)grow * i + (o.off - lo), o.len);
+          else
+            o = dp_pkt_out_t{in[i].off, in[i].len, DP_DONE_INTERNAL_FAILURE};
+        }
+        out[i] = o;
+        if (meta) meta[i] = c->h_meta[i];
+      }
     }
+  });
+  if (werr) {
+    (void)hipStreamSynchronize(s);
+    return bail(DP_EIO, "chunk completion", hipSuccess);
   }
   uint64_t hstats[DP_DONE_COUNT];
   if (stats && (e = hipMemcpyAsync(hstats, c->d_stats, sizeof(hstats), hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H stats", e);

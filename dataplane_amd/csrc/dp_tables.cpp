@@ -343,6 +343,7 @@ constexpr double kListMean = DP_LIST_MEAN;
 // forms chosen by the most recent build on this thread (test introspection)
 thread_local uint32_t g_forms[2];
 thread_local std::string g_group_stats;  // per-group list statistics (dpd_debug_group_stats)
+thread_local std::string g_sections;     // image bytes per section (dpd_debug_image_sections)
 std::atomic<int> g_cls_form{0};
 
 int cls_form_override() { return g_cls_form.load(std::memory_order_relaxed); }
@@ -689,6 +690,13 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   if (!d || d->abi_version != DPGPU_ABI_VERSION) return DP_EINVAL;
   ImgBuf ib;
   ib.alloc(64);  // offset 0 is never a valid structure
+  g_sections.clear();
+  uint64_t sec0 = ib.b.size();
+  auto section = [&](const char *name) {
+    g_sections += name;
+    g_sections += "=" + std::to_string(ib.b.size() - sec0) + " ";
+    sec0 = ib.b.size();
+  };
   Image im{};
   im.genid = d->genid;
 
@@ -703,6 +711,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
       if (encaps && (kd == DP_INSTR_LOCAL || kd == DP_INSTR_ENCAP_VXLAN)) return DP_ENOTSUP;
       if (kd == DP_INSTR_ENCAP_VXLAN) encaps++;
     }
+    if (encaps) im.may_encap = 1;
   }
   for (uint32_t i = 0; i < d->n_route_nhs; i++) {
     const dp_route_nh_t &n = d->route_nhs[i];
@@ -861,6 +870,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   }
   im.nh_recs = ib.put(nhrecs);
 
+  section("fib");
   // --- interfaces / adjacencies
   std::vector<IfRec> ifs;
   std::vector<KV> ifkv;
@@ -928,6 +938,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
     im.adjs.count = count;
   }
 
+  section("ifaces");
   // --- classifiers
   int rc;
   struct T { const dp_rule_t *r; uint32_t n; int fam; bool prio; int kind; Classifier *dst; };
@@ -966,6 +977,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
     defkv.push_back(KV{d->acl_defaults[i].src_vni, d->acl_defaults[i].dst_vni, 0, d->acl_defaults[i].action + 1});
   im.acl_default = build_hash(ib, defkv);
 
+  section("classifiers");
   // --- static NAT
   std::vector<NatTab> ntabs;
   std::vector<NatEnt> nents;
@@ -1114,6 +1126,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   im.nat_tabs = build_hash(ib, ntkv);
   im.nat_pervni = build_hash(ib, pervni);
 
+  section("nat");
   // --- per-VNI and per-VNI-pair contexts (precomputed joins)
   std::unordered_map<unsigned __int128, int32_t, U128Hash> ntmap;
   std::unordered_map<uint32_t, uint32_t> has_pervni;
@@ -1238,6 +1251,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   im.nat_prs = ib.put(nprs);
   im.nat_ranges = ib.put(nranges);
 
+  section("contexts");
   // --- port forwarding (nat/src/portfw/portfwtable/)
   for (uint32_t i = 0; i < d->n_portfw; i++)
     if (!pf_rule_ok(d->portfw[i])) return DP_EINVAL;
@@ -1279,6 +1293,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   im.pf_rules = pfrecs.empty() ? ib.alloc(sizeof(PfRuleRec)) : ib.put(pfrecs);
   im.n_pf = (uint32_t)pfrecs.size();
 
+  section("portfw");
   ib.alloc(64);
   im.bytes = ib.b.size();
   // context records carry 32-bit image offsets (Mbi)
@@ -1301,6 +1316,7 @@ extern "C" void dpd_debug_set_classifier_form(int form) {
 }
 
 extern "C" const char *dpd_debug_group_stats(void) { return dpd::g_group_stats.c_str(); }
+extern "C" const char *dpd_debug_image_sections(void) { return dpd::g_sections.c_str(); }
 
 extern "C" void dpd_debug_classifier_forms(uint32_t out[2]) {
   out[0] = dpd::g_forms[0];

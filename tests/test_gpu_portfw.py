@@ -94,7 +94,7 @@ def test_gpu_portfw_random_bursts(seed, n_conn, capacity):
                 r.close()
         got[name] = steps
     hist = {}
-    co, cg = IdCanon(), IdCanon()
+    ido, idg = IdCanon(), IdCanon()
     for k, (o, g) in enumerate(zip(got["oracle"], got["gpu"])):
         (ro, bo, io, lo, co), (rg, bg, ig, lg, cg) = o, g
         a, b = common_fields(ro, rg)
@@ -103,8 +103,8 @@ def test_gpu_portfw_random_bursts(seed, n_conn, capacity):
         for i in np.nonzero(ro["done"] == A.DONE["Delivered"])[0]:
             s0, n0 = int(ro[i]["off"]), int(ro[i]["len"])
             assert np.array_equal(bo[s0:s0 + n0], bg[s0:s0 + n0]), f"burst {k} packet {i}: frame"
-        same_info(io, ig, co, cg, f"burst {k}: packets'")
-        same_info(lo, lg, co, cg, f"burst {k}: flows by key:")
+        same_info(io, ig, ido, idg, f"burst {k}: packets'")
+        same_info(lo, lg, ido, idg, f"burst {k}: flows by key:")
         assert np.array_equal(lo["ref"] == A.FLOW_NONE, lg["ref"] == A.FLOW_NONE), f"burst {k}: presence"
         assert co == cg, f"burst {k}: counts {co} vs {cg}"
         for d in ro["done"]:
