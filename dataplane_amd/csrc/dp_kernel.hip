@@ -2858,7 +2858,9 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
 #ifndef DP_PROBE_NONAT
   stage_static_nat(g, F, H, S, P);
 #endif
+#ifndef DP_X_NOPF
   stage_portfw<FL>(F, H, S, fp, fc, idx, rp);
+#endif
   if constexpr (FL) {
     if (fp.deferred) {  // finished by the replay pass
       o.done = DONE_NONE;
@@ -2938,6 +2940,19 @@ __device__ __forceinline__ void wave_load_windows(const uint8_t *buf, uint8_t *s
   }
 }
 
+// 16-byte global store of the write-back and the out records.  DP_SC1_STORES
+// (A/B variant): sc1 stores, which leave the XCD's L2 without keeping the
+// line (MI355X_MICROARCH.md), so the streamed frames do not evict table lines.
+__device__ __forceinline__ void st16(void *p, uint4 v) {
+#ifdef DP_SC1_STORES
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 d = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(d) : "memory");
+#else
+  *reinterpret_cast<uint4 *>(p) = v;
+#endif
+}
+
 __device__ __forceinline__ void wave_store_windows(uint8_t *buf, const uint8_t *slab_wave, uint32_t base, int c0, int c1) {
   const int lane = threadIdx.x & 63;
   const int lg = log2_up(wave_max(c1));
@@ -2949,7 +2964,7 @@ __device__ __forceinline__ void wave_store_windows(uint8_t *buf, const uint8_t *
     const int q0 = __shfl(c0, q), q1 = __shfl(c1, q);
     if (c >= q0 && c < q1) {
       const lds_u32 *w = (const lds_u32 *)(slab_wave + q * SLAB + 16 * c);
-      *reinterpret_cast<uint4 *>(buf + qb + 16 * c) = make_uint4(w[0], w[1], w[2], w[3]);
+      st16(buf + qb + 16 * c, make_uint4(w[0], w[1], w[2], w[3]));
     }
   }
 }
@@ -3034,6 +3049,9 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   bool live = i < n;
   const dpf::PfReq *rp = nullptr;
   if constexpr (FL) {
+    // the replay grid is the burst's; workgroups past the replayed packets
+    // leave at once (uniform per workgroup: before any barrier)
+    if (rep && blockIdx.x * TPB >= fc.pf_cnt[1]) return;
     if (rep) {
       live = i < fc.pf_cnt[1];
       i = live ? fc.pf_order[i] : n;
@@ -3059,7 +3077,8 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
     dp_pkt_meta_t *pm = MT ? meta + i : nullptr;
     if (all_fit) done_code = process_packet<FL, MT>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, true, &fc, fp, i, rp);
     else done_code = process_packet<FL, MT>(g, slab, hs, buf, buf_bytes, pin, o, pm, fl0, fl1, false, &fc, fp, i, rp);
-    out[i] = o;
+    static_assert(sizeof(dp_pkt_out_t) == 16, "one 16-byte store");
+    st16(out + i, *reinterpret_cast<const uint4 *>(&o));
   }
   if constexpr (FL) if (!rep) flow_effects<MT>(fc, live, i, fp);
   __syncthreads();

@@ -17,6 +17,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <deque>
@@ -228,23 +232,110 @@ hipEvent_t take_event(dp_ctx *c) {
   return e;
 }
 
+// Phase timing of the staged-copy path, printed when DPGPU_HOST_TRACE is set
+// (diagnostics for the host-inclusive rate).
+struct HostTrace {
+  const bool on = getenv("DPGPU_HOST_TRACE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::string s;
+  void mark(const char *what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    s += std::string(what) + " " + std::to_string(std::chrono::duration<double, std::micro>(now - t).count()) + " us; ";
+    t = now;
+  }
+  void done(uint32_t n, uint32_t threads, uint32_t chunks) {
+    if (on) fprintf(stderr, "[dpgpu host] n=%u threads=%u chunks=%u: %s\n", n, threads, chunks, s.c_str());
+  }
+};
+
 // Host threads for a burst's gather / write-back: one per 32K packets, at
 // most the machine's threads (capped at 16).
 uint32_t host_threads(uint32_t n) {
   const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   return std::max(1u, std::min(hw, n / 32768));
 }
+// A pool of host threads for the staged-copy path's gather and write-back,
+// created on first use and kept for the process (thread creation per burst
+// cost more than the gather itself).  run(parts, f) calls f(t) for every t in
+// [0, parts) -- the caller takes part of the work -- and returns when all
+// are done; concurrent callers take turns.
+class HostPool {
+ public:
+  static HostPool &get() {
+    static HostPool p;
+    return p;
+  }
+  void run(uint32_t parts, const std::function<void(uint32_t)> &f) {
+    if (parts <= 1) {
+      f(0u);
+      return;
+    }
+    std::lock_guard<std::mutex> turn(run_mu_);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while (th_.size() + 1 < parts) th_.emplace_back([this] { work(); });
+      job_ = &f;
+      parts_ = parts;
+      next_ = 0;
+      pending_ = parts;
+      gen_++;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+
+ private:
+  void drain() {  // take parts until none is left
+    for (;;) {
+      uint32_t t;
+      const std::function<void(uint32_t)> *f;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!job_ || next_ >= parts_) return;
+        t = next_++;
+        f = job_;
+      }
+      (*f)(t);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  void work() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      drain();
+    }
+  }
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  const std::function<void(uint32_t)> *job_ = nullptr;
+  uint32_t parts_ = 0, next_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 template <class F>
 void par_for(uint32_t parts, F &&f) {
-  if (parts <= 1) {
-    f(0u);
-    return;
-  }
-  std::vector<std::thread> th;
-  th.reserve(parts - 1);
-  for (uint32_t t = 1; t < parts; t++) th.emplace_back([&f, t] { f(t); });
-  f(0u);
-  for (auto &x : th) x.join();
+  HostPool::get().run(parts, std::function<void(uint32_t)>(std::forward<F>(f)));
 }
 
 // Every packet of a failed burst is InternalFailure (dpgpu.h conventions,
@@ -628,6 +719,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     return img && img->im.may_encap ? (uint32_t)DP_HEADROOM : 0u;
   }();
   // spans: per-thread sums, then positions (16-byte units) and the gather
+  HostTrace tr;
   const uint32_t T = host_threads(n);
   std::vector<uint64_t> acc(T + 1, 0);
   par_for(T, [&](uint32_t t) {
@@ -653,17 +745,27 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     c->cin_cap = ci;
     c->cout_cap = co;
   }
+  tr.mark("sums+alloc");
   par_for(T, [&](uint32_t t) {
     uint64_t p = acc[t];
     for (uint32_t i = (uint32_t)((uint64_t)n * t / T), b = (uint32_t)((uint64_t)n * (t + 1) / T); i < b; i++) {
-      const uint64_t lo = in[i].off & ~15u, u = ((in[i].off + in[i].len + 15u) >> 4) - (in[i].off >> 4);
       c->h_pos[i] = (uint32_t)p;
-      // the rounded-up end may lie past the caller's buffer: never read there
-      memcpy(c->h_cin + 16 * p, buf + lo, std::min<uint64_t>(16 * u, buf_bytes - lo));
       c->h_in[i] = in[i];
-      p += u;
+      p += ((in[i].off + in[i].len + 15u) >> 4) - (in[i].off >> 4);
     }
   });
+  // the frames of packets [a, b): host threads pack their spans
+  auto gather = [&](uint32_t a, uint32_t b) {
+    par_for(T, [&](uint32_t t) {
+      for (uint32_t i = a + (uint32_t)((uint64_t)(b - a) * t / T), e = a + (uint32_t)((uint64_t)(b - a) * (t + 1) / T);
+           i < e; i++) {
+        const uint64_t lo = in[i].off & ~15u, u = ((in[i].off + in[i].len + 15u) >> 4) - (in[i].off >> 4);
+        // the rounded-up end may lie past the caller's buffer: never read there
+        memcpy(c->h_cin + 16ull * c->h_pos[i], buf + lo, std::min<uint64_t>(16 * u, buf_bytes - lo));
+      }
+    });
+  };
+  tr.mark("positions");
   const uint32_t nch = !c->ft ? std::max<uint32_t>(1, std::min<uint32_t>(n / kHostChunk, 256)) : 1;
   if (nch > 1 && !c->host_streams) {
     for (int k = 0; k < kHostStreams; k++)
@@ -693,8 +795,19 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     first = (uint32_t)((uint64_t)n * k / nch);
     cnt = (uint32_t)((uint64_t)n * (k + 1) / nch) - first;
   };
+  // in phases of chunks: a phase's frames are packed while the previous
+  // phases' copies and kernels run
+  const uint32_t phases = std::min<uint32_t>(nch, 4);
+  uint32_t gathered = 0;  // chunks whose frames are packed
   for (uint32_t k = 0; k < nch && !rc; k++) {
     uint32_t first, cnt;
+    if (k == gathered) {  // phase ph holds chunks [nch * ph / phases, nch * (ph + 1) / phases)
+      uint32_t ph = 0;
+      while ((uint64_t)nch * (ph + 1) / phases <= k) ph++;
+      const uint32_t k1 = (uint32_t)((uint64_t)nch * (ph + 1) / phases);
+      gather((uint32_t)((uint64_t)n * k / nch), (uint32_t)((uint64_t)n * k1 / nch));
+      gathered = k1;
+    }
     chunk_of(k, first, cnt);
     hipStream_t hs = nch == 1 ? s : c->hs[k % kHostStreams];
     const uint64_t b0 = 16ull * c->h_pos[first], b1 = first + cnt < n ? 16ull * c->h_pos[first + cnt] : in_bytes;
@@ -736,6 +849,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
   // its packed span (an output outside its staged span -- a publish that
   // added encapsulation between this burst's staging and its launch -- is an
   // InternalFailure of that packet)
+  tr.mark("gather+enqueue");
   std::atomic<int> werr{0};
   const uint32_t W = std::min<uint32_t>(T, nch);
   par_for(W, [&](uint32_t t) {
@@ -758,6 +872,8 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
       }
     }
   });
+  tr.mark("wait+write-back");
+  tr.done(n, T, nch);
   if (werr) {
     (void)hipStreamSynchronize(s);
     return bail(DP_EIO, "chunk completion", hipSuccess);

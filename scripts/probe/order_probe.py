@@ -40,7 +40,7 @@ def main():
     ptr = [0] * G
     blocks = []
     b = 0
-    while sum(len(g) - p for g, p in zip(groups, ptr)) > 0:
+    while any(p < len(g) for g, p in zip(groups, ptr)):
         gi = (b % 8) * G // 8
         for k in range(G):  # the preferred group, else the next non-empty one
             j = (gi + k) % G
@@ -51,6 +51,24 @@ def main():
         b += 1
     orders["xcd_src_vni"] = np.concatenate(blocks)
     orders["by_dst"] = np.argsort(dst, kind="stable")
+    # sorted by destination, each XCD on its own eighth of the sorted order:
+    # workgroup b takes the next 128 packets of part b % 8
+    srt = np.argsort(dst, kind="stable")
+    parts = np.array_split(srt, 8)
+    pos8 = [0] * 8
+    xb = []
+    b = 0
+    while any(p < len(q) for q, p in zip(parts, pos8)):
+        j = b % 8
+        if pos8[j] < len(parts[j]):
+            xb.append(parts[j][pos8[j]:pos8[j] + 128])
+            pos8[j] += 128
+        else:
+            xb.append(np.zeros(0, dtype=srt.dtype))  # keep the XCD rotation
+        b += 1
+    orders["xcd_dst"] = np.concatenate(xb)
+    # source VNI, then the destination's top 8 bits within it
+    orders["by_vni_dst8"] = np.lexsort((dst >> 24, vni))
     bb = (w.buf.nbytes + 255) & ~255
     pristine = torch.from_numpy(w.buf).to(dev)
     buf = torch.empty(bb, dtype=torch.uint8, device=dev)
