@@ -1,5 +1,5 @@
-# One GPU pass: a subset (or all) of the GPU suite, then bench.py with the
-# given arguments.  TESTS="tests/test_gpu_portfw.py" BENCH="--no-cpu" bash scripts/gpu_round.sh
+# A subset (or all) of the GPU suite, then bench.py with the
+# given arguments.  TESTS="tests/test_gpu_portfw.py" BENCH="--no-cpu" bash scripts/gpu_subset.sh
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

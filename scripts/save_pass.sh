@@ -1,4 +1,4 @@
-# Copy a gpu_round.sh pass out of gpurun_out/ into profiles/<dir>/:
+# Copy a gpu_pass.sh pass out of gpurun_out/ into profiles/<dir>/:
 #   bash scripts/save_pass.sh profiles/r03/head_<sha> [cfg]
 set -e
 d=$1; c=${2:-2}
