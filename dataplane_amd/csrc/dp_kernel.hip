@@ -2933,7 +2933,13 @@ __device__ __forceinline__ void wave_load_windows(const uint8_t *buf, uint8_t *s
     const uint32_t qb = (uint32_t)__shfl((int)base, q);
     const int qn = __shfl(nch, q);
     if (c < qn) {
+#ifdef DP_NT_LOADS  // A/B variant: the frames streamed in with the nontemporal policy
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(buf + qb + 16 * c));
+      const uint4 v = make_uint4(t.x, t.y, t.z, t.w);
+#else
       const uint4 v = *reinterpret_cast<const uint4 *>(buf + qb + 16 * c);
+#endif
       lds_u32 *d = (lds_u32 *)(slab_wave + q * SLAB + 16 * c);
       d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
     }
@@ -2944,10 +2950,13 @@ __device__ __forceinline__ void wave_load_windows(const uint8_t *buf, uint8_t *s
 // (A/B variant): sc1 stores, which leave the XCD's L2 without keeping the
 // line (MI355X_MICROARCH.md), so the streamed frames do not evict table lines.
 __device__ __forceinline__ void st16(void *p, uint4 v) {
-#ifdef DP_SC1_STORES
+#if defined(DP_SC1_STORES)
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 d = {v.x, v.y, v.z, v.w};
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(d) : "memory");
+#elif defined(DP_NT_STORES)
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(p));
 #else
   *reinterpret_cast<uint4 *>(p) = v;
 #endif

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc CSVs of dp_pipeline_kernel<false, false> (the non-flow, no-meta variant
+"""Summarise rocprofv3 --pmc CSVs of dp_pipeline_kernel<false, false, ...> (the non-flow, no-meta variant
 the metric times; the bench flow-table leg launches the <true> variant): per-dispatch mean of
 every counter (summed over dimensions), plus derived ratios.
     python scripts/pmc_summary.py gpurun_out/pmc [n_packets]"""
@@ -16,7 +16,7 @@ def main():
     per = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "dp_pipeline_kernel<false, false>" not in r.get("Kernel_Name", ""):
+            if "dp_pipeline_kernel<false, false" not in r.get("Kernel_Name", ""):
                 continue
             per[(f, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     tot, cnt = defaultdict(float), defaultdict(int)
