@@ -62,6 +62,14 @@ struct Lpm {
   uint64_t blocks;     // != 0: DIR-24-8 -- a non-leaf direct entry is the index of a
                        // uint16_t[256] block of next hops for the last 8 bits (v4 with a
                        // 24-bit direct table); 0: Poptrie nodes below the direct table
+  // v6 window (wtab != 0): the routes longer than /16 share their top wbits
+  // bits (wpfx = those bits); a key inside that prefix reads
+  // wtab[the 16 bits after them] -- leaf, or a Poptrie node at bit wbits + 16
+  // -- instead of walking the Poptrie down from bit 16
+  uint64_t wtab;       // offset of uint32_t[65536]
+  uint64_t wpfx;
+  uint32_t wbits;      // 24..48
+  uint32_t pad;
 };
 
 struct FibRec {
@@ -204,20 +212,26 @@ struct AdjMap {
 //    then 8-bit blocks; an entry with bit 31 set is the interval's row id,
 //    otherwise the index of the next 256-entry block (<= 3 more levels);
 //  - sorted bounds (v6, or few intervals): binary search, narrowed by an
-//    optional 16-bit jump table, then rows[interval].
+//    optional 16-bit jump table, then rows[interval].  A v6 address field's
+//    jump table buckets the 16 key bits after the top `win` bits every bound
+//    shares (`pfx`; keys outside that prefix lie in interval `below` or
+//    `above`), so the buckets split the rules' own address space.
 #define DPD_LEAF 0x80000000u
 struct FieldIdx {
   uint64_t bounds;     // offset of uint64_t[2*n] (hi, lo) interval starts, ascending
   uint64_t rows;       // offset of uint32_t[n] row index per interval
   uint64_t jump;       // offset of uint32_t[65537]: interval containing the start of
-                       // each 16-bit top-bits bucket (0: no jump table, n small)
+                       // each 16-bit bucket (0: no jump table, n small)
   uint64_t root;       // multibit root uint32_t[1 << s0] (0: bounds form)
   uint64_t blocks;     // multibit blocks uint32_t[256 * k]
   uint32_t n;          // number of intervals (>= 1; bounds[0] = 0)
   uint8_t shift;       // key >> shift = bucket (v4 ip: 16, port: 0, v6: hi >> 48)
   uint8_t s0;          // multibit root stride (bits)
   uint8_t kbits;       // multibit key width (32 or 16)
-  uint8_t pad;
+  uint8_t win;         // v6 jump window: the bounds' shared top bits (1..64; 0: none)
+  uint64_t pfx;        // their value (key.hi >> (64 - win))
+  uint32_t below;      // interval of keys below / above that prefix
+  uint32_t above;
 };
 
 // Candidate-list form of a group (mode DPD_GROUP_LIST): one field (`lfield`)

@@ -880,19 +880,25 @@ __device__ __forceinline__ uint32_t key6(uint64_t hi, uint64_t lo, int off) {
 }
 
 __device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t direct_off, uint32_t dbits, uint64_t blocks,
-                                             const Addr16 &a) {
-  const uint32_t *direct = g.at<uint32_t>(direct_off);
-  const uint32_t idx = a.w[0] >> (32 - dbits);  // dbits <= 32 for both families
-  uint32_t e = direct[idx];
+                                             const Addr16 &a, uint64_t wtab = 0, uint64_t wpfx = 0,
+                                             uint32_t wbits = 0) {
+  const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1], klo = ((uint64_t)a.w[2] << 32) | a.w[3];
+  uint32_t e;
+  int off;
+  if (wtab && (khi >> (64 - wbits)) == wpfx) {  // v6 key inside the FIB's window
+    e = g.at<uint32_t>(wtab)[(uint32_t)(khi >> (48 - wbits)) & 0xffffu];
+    off = (int)wbits + 16;
+  } else {
+    e = g.at<uint32_t>(direct_off)[a.w[0] >> (32 - dbits)];  // dbits <= 32 for both families
+    off = (int)dbits;
+  }
   TRIP();
   if (e & 0x80000000u) return e & 0x7fffffffu;
   TRIP();
   if (blocks) return g.at<uint16_t>(blocks)[(e << 8) | (a.w[0] & 0xff)];  // DIR-24-8 (v4)
   const PtNode *nodes = g.at<PtNode>(g.im.pt_nodes);
   const uint32_t *leaves = g.at<uint32_t>(g.im.pt_leaves);
-  int off = (int)dbits;
   uint32_t ni = e;
-  const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1], klo = ((uint64_t)a.w[2] << 32) | a.w[3];
   for (int guard = 0; guard < 24; guard++) {
     const PtNode &nd = nodes[ni];
     TRIP();
@@ -910,7 +916,7 @@ __device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t direct_off, 
   return g.im.drop_nh;  // unreachable for a well-formed image
 }
 __device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
-  return lpm_walk(g, L.direct, L.dbits, L.blocks, a);
+  return lpm_walk(g, L.direct, L.dbits, L.blocks, a, L.wtab, L.wpfx, L.wbits);
 }
 
 // Multibit index walk from a context record's descriptor (Mbi): leaf value
@@ -934,9 +940,25 @@ struct Key128 { uint64_t hi, lo; };
 // index into the kernel-argument image header (which would force a private copy)
 #define CLS(arr, t, field) ((t) ? g.im.arr[1].field : g.im.arr[0].field)
 
-// bucket of a key for a field's jump table
-__device__ __forceinline__ uint32_t bucket_of(const FieldIdx &f, Key128 k) {
-  return f.shift == 48 ? (uint32_t)(k.hi >> 48) : (uint32_t)(k.lo >> f.shift) & 0xffff;
+// The bounds range [lo, hi) a field's jump table leaves for a key: its
+// bucket's (the 16 bits after a v6 window's shared top bits, or the key's top
+// 16 bits), or the one interval of a v6 key outside the window's prefix.
+__device__ __forceinline__ void jump_range(const uint32_t *jt, const FieldIdx &f, Key128 k, uint32_t &lo,
+                                           uint32_t &hi) {
+  uint32_t b;
+  if (f.win) {
+    const uint64_t top = f.win == 64 ? k.hi : k.hi >> (64 - f.win);
+    if (top != f.pfx) {
+      lo = top < f.pfx ? f.below : f.above;
+      hi = lo + 1;
+      return;
+    }
+    b = (uint32_t)((f.win == 64 ? k.lo : (k.hi << f.win) | (k.lo >> (64 - f.win))) >> 48);
+  } else {
+    b = f.shift == 48 ? (uint32_t)(k.hi >> 48) : (uint32_t)(k.lo >> f.shift) & 0xffff;
+  }
+  lo = jt[b];
+  hi = jt[b + 1] + 1;
 }
 
 // Elementary interval of one key in one field index -> its leaf value
@@ -957,12 +979,7 @@ __device__ __forceinline__ uint32_t field_leaf(const Img &g, const FieldIdx &F, 
     return e & ~DPD_LEAF;
   }
   uint32_t lo = 0, hi = F.n;
-  if (F.jump) {
-    const uint32_t *jt = g.at<uint32_t>(F.jump);
-    uint32_t t = bucket_of(F, key);
-    lo = jt[t];
-    hi = jt[t + 1] + 1;
-  }
+  if (F.jump) jump_range(g.at<uint32_t>(F.jump), F, key, lo, hi);
   const uint64_t *bd = g.at<uint64_t>(F.bounds);
   while (hi - lo > 1) {
     TRIP();
@@ -1005,10 +1022,7 @@ __device__ DP_BV int64_t classify_bv(const uint8_t *base, const Group *Gp, uint8
       e[f] = g.at<uint32_t>(G.f[f].root)[k >> (G.f[f].kbits - G.f[f].s0)];
       hi[f] = lo[f] + 1;  // no bounds search
     } else if (G.f[f].jump) {
-      const uint32_t *jt = g.at<uint32_t>(G.f[f].jump);
-      uint32_t t = bucket_of(G.f[f], key[f]);
-      lo[f] = jt[t];
-      hi[f] = jt[t + 1] + 1;
+      jump_range(g.at<uint32_t>(G.f[f].jump), G.f[f], key[f], lo[f], hi[f]);
     }
   }
   // multibit levels (8 bits each), in lockstep
@@ -1938,13 +1952,18 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   cur_dst(F, H, S, fam, dst);
   // one walk for every lane: v4 and v6 lanes of a wave issue their direct-table
   // loads together (two call sites would run one after the other)
+  uint64_t wt = 0, wp = 0;
+  uint32_t wb = 0;
   if (!(fam == 4 && d4)) {
     const Lpm &L = fam == 4 ? fb.v4 : fb.v6;
     d4 = L.direct;
     b4 = L.dbits;
     k4 = L.blocks;
+    wt = L.wtab;
+    wp = L.wpfx;
+    wb = L.wbits;
   }
-  const uint32_t nhi = lpm_walk(g, d4, b4, k4, dst);
+  const uint32_t nhi = lpm_walk(g, d4, b4, k4, dst, wt, wp, wb);
   TRIP();
   const NhRec nr = g.at<NhRec>(g.im.nh_recs)[nhi];
   if (nr.kind != DPD_NH_CHAIN) {

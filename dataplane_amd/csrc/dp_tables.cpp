@@ -161,6 +161,71 @@ struct PtBuilder {
   }
 };
 
+// v6 window (Lpm.wtab): the routes longer than the 16-bit direct table share
+// their top bits (a site's or provider's prefix, e.g. 2001:db8::/32); keys
+// inside that prefix read a 65536-entry table over the next 16 bits -- the
+// best route of length <= wbits + 16, or a Poptrie node for the longer ones
+// -- instead of walking (wbits + 16 - 16) / 6 Poptrie levels down to it.
+// `uniq` is sorted by (key, length).
+void add_v6_window(ImgBuf &ib, PtBuilder &pb, const std::vector<PRoute> &uniq, Lpm &L) {
+  bool any = false;
+  u128 lo = 0, hi = 0;
+  int minlen = 129;
+  for (const PRoute &r : uniq) {
+    if (r.len <= 16) continue;
+    if (!any) lo = r.key;
+    hi = r.key;
+    any = true;
+    minlen = std::min(minlen, r.len);
+  }
+  if (!any) return;
+  const u128 x = lo ^ hi;
+  int c = x == 0 ? 128 : ((uint64_t)(x >> 64) ? __builtin_clzll((uint64_t)(x >> 64)) : 64 + __builtin_clzll((uint64_t)x));
+  c = std::min({c, minlen, 48});
+  if (c < 24) return;
+  const int sh = 128 - c;
+  const u128 P = lo >> sh, base = P << sh;
+  // the longest route of length <= c covering the window (the /0 at least)
+  uint32_t d = 0;
+  int dl = -1;
+  for (const PRoute &r : uniq)
+    if (r.len <= c && r.len > dl && (r.len == 0 || (r.key >> (128 - r.len)) == (base >> (128 - r.len)))) {
+      d = r.nh;
+      dl = r.len;
+    }
+  std::vector<uint32_t> val(65536, d);
+  std::vector<const PRoute *> mid;
+  for (const PRoute &r : uniq)
+    if (r.len > c && r.len <= c + 16) mid.push_back(&r);
+  std::stable_sort(mid.begin(), mid.end(), [](const PRoute *a, const PRoute *b) { return a->len < b->len; });
+  for (const PRoute *p : mid) {
+    const uint32_t span = 1u << (c + 16 - p->len);
+    const uint32_t v0 = kbits(p->key, c, 16) & ~(span - 1);
+    std::fill(val.begin() + v0, val.begin() + v0 + span, p->nh);
+  }
+  std::vector<uint32_t> tab(65536);
+  for (size_t k = 0; k < tab.size(); k++) tab[k] = 0x80000000u | val[k];
+  size_t i = 0;
+  while (i < uniq.size()) {
+    if (uniq[i].len <= c + 16) { i++; continue; }
+    const uint32_t slot = kbits(uniq[i].key, c, 16);
+    std::vector<PRoute> sub;
+    size_t j = i;
+    while (j < uniq.size() && (uniq[j].key >> sh) == P && kbits(uniq[j].key, c, 16) == slot) {
+      if (uniq[j].len > c + 16) sub.push_back(uniq[j]);
+      j++;
+    }
+    const uint32_t idx = (uint32_t)pb.nodes.size();
+    pb.nodes.emplace_back();
+    pb.build_node(idx, sub.data(), sub.size(), val[slot], c + 16);
+    tab[slot] = idx;
+    i = j;
+  }
+  L.wtab = ib.put(tab);
+  L.wpfx = (uint64_t)P;
+  L.wbits = (uint32_t)c;
+}
+
 // Build one FIB/family LPM; routes must include a /0.
 Lpm build_lpm(ImgBuf &ib, PtBuilder &pb, std::vector<PRoute> &routes, int width, uint32_t dbits) {
   // sort by (key, len), keep the last insert of a duplicate prefix
@@ -248,6 +313,9 @@ Lpm build_lpm(ImgBuf &ib, PtBuilder &pb, std::vector<PRoute> &routes, int width,
   L.direct = ib.put(direct);
   L.dbits = dbits;
   L.width = (uint32_t)width;
+#ifndef DP_NO_V6_WINDOW
+  if (width == 128) add_v6_window(ib, pb, uniq, L);
+#endif
   return L;
 }
 
@@ -312,15 +380,37 @@ void build_field_index(ImgBuf &ib, FieldIdx &F, int f, int fam, size_t ngroups,
   // bucket = top 16 bits of the key: v4 address >> 16, port itself,
   // v6 address hi64 >> 48
   F.shift = f >= 2 ? 0 : (fam == 4 ? 16 : 48);
+  F.win = 0;
   if (m > 16) {
-    std::vector<uint32_t> jump(65537);
-    size_t j = 0;
-    for (uint32_t b = 0; b < 65536; b++) {
-      u128 start = f >= 2 ? (u128)b : (fam == 4 ? ((u128)b << 16) : ((u128)b << 112));
-      while (j + 1 < m && bnd[j + 1] <= start) j++;
-      jump[b] = (uint32_t)j;
+    auto ivl = [&](u128 x) -> uint32_t {
+      return (uint32_t)(std::upper_bound(bnd.begin(), bnd.end(), x) - bnd.begin()) - 1;
+    };
+    // v6 address: bucket the 16 bits after the longest prefix (<= 64 bits)
+    // every bound but 0 and that prefix's end shares -- rules of one site or
+    // VPC share their top bits, and a top-16-bit bucket would hold them all
+    u128 base = 0;
+    int bsh = f >= 2 ? 0 : (fam == 4 ? 16 : 112);  // bucket b starts at base + (b << bsh)
+#ifndef DP_NO_V6_WINDOW
+    if (fam == 6 && f < 2) {
+      for (int c = 64; c >= 1; c--) {
+        const int sh = 128 - c;
+        const u128 P = bnd[1] >> sh, end = (P + 1) << sh;  // end wraps to 0 past the top
+        bool ok = true;
+        for (size_t k = 1; k < m && ok; k++) ok = (bnd[k] >> sh) == P || bnd[k] == end;
+        if (!ok) continue;
+        F.win = (uint8_t)c;
+        F.pfx = (uint64_t)P;
+        F.below = P ? ivl((P << sh) - 1) : 0;
+        F.above = end ? ivl(end) : (uint32_t)(m - 1);
+        base = P << sh;
+        bsh = sh - 16;
+        break;
+      }
     }
-    jump[65536] = (uint32_t)(m - 1);
+#endif
+    std::vector<uint32_t> jump(65537);
+    for (uint32_t b = 0; b < 65536; b++) jump[b] = ivl(base + ((u128)b << bsh));
+    jump[65536] = F.win ? ivl(base + ((u128)65536 << bsh) - 1) : (uint32_t)(m - 1);
     F.jump = ib.put(jump);
   }
 }

@@ -28,6 +28,12 @@ static inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long l
 // single-threaded host emulation: plain read-modify-write
 static inline uint32_t atomicAdd(uint32_t *p, uint32_t v) { uint32_t o = *p; *p = o + v; return o; }
 static inline uint32_t atomicOr(uint32_t *p, uint32_t v) { uint32_t o = *p; *p = o | v; return o; }
+static inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) {
+  unsigned long long o = *p; *p = o + v; return o;
+}
+static inline uint32_t atomicMin(uint32_t *p, uint32_t v) { uint32_t o = *p; if (v < o) *p = v; return o; }
+static inline int __popc(uint32_t x) { return __builtin_popcount(x); }
+static inline int __ffs(uint32_t x) { return __builtin_ffs((int)x); }
 static inline uint64_t __umul64hi(uint64_t a, uint64_t b) {
   return (uint64_t)(((unsigned __int128)a * b) >> 64);
 }
