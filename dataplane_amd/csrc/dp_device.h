@@ -212,26 +212,20 @@ struct AdjMap {
 //    then 8-bit blocks; an entry with bit 31 set is the interval's row id,
 //    otherwise the index of the next 256-entry block (<= 3 more levels);
 //  - sorted bounds (v6, or few intervals): binary search, narrowed by an
-//    optional 16-bit jump table, then rows[interval].  A v6 address field's
-//    jump table buckets the 16 key bits after the top `win` bits every bound
-//    shares (`pfx`; keys outside that prefix lie in interval `below` or
-//    `above`), so the buckets split the rules' own address space.
+//    optional 16-bit jump table, then rows[interval].
 #define DPD_LEAF 0x80000000u
 struct FieldIdx {
   uint64_t bounds;     // offset of uint64_t[2*n] (hi, lo) interval starts, ascending
   uint64_t rows;       // offset of uint32_t[n] row index per interval
   uint64_t jump;       // offset of uint32_t[65537]: interval containing the start of
-                       // each 16-bit bucket (0: no jump table, n small)
+                       // each 16-bit top-bits bucket (0: no jump table, n small)
   uint64_t root;       // multibit root uint32_t[1 << s0] (0: bounds form)
   uint64_t blocks;     // multibit blocks uint32_t[256 * k]
   uint32_t n;          // number of intervals (>= 1; bounds[0] = 0)
   uint8_t shift;       // key >> shift = bucket (v4 ip: 16, port: 0, v6: hi >> 48)
   uint8_t s0;          // multibit root stride (bits)
   uint8_t kbits;       // multibit key width (32 or 16)
-  uint8_t win;         // v6 jump window: the bounds' shared top bits (1..64; 0: none)
-  uint64_t pfx;        // their value (key.hi >> (64 - win))
-  uint32_t below;      // interval of keys below / above that prefix
-  uint32_t above;
+  uint8_t pad;
 };
 
 // Candidate-list form of a group (mode DPD_GROUP_LIST): one field (`lfield`)
@@ -391,6 +385,14 @@ struct Image {
   uint64_t pf_rules;         // PfRuleRec[]
   uint32_t n_pf;
   uint32_t may_encap;        // some FibEntry encapsulates: an output may start before its frame
+  // v6 window of the classifiers' v6 address indexes (0: none): every v6
+  // rule prefix lies inside one prefix of v6w_c bits (value v6w_p), and the
+  // bounds and jump tables of v6 address fields are over the key transformed
+  // by v6_window_key (dp_kernel.hip): 0 below it, all ones above it, else the
+  // key shifted left by v6w_c with bit 0 set
+  uint32_t v6w_c;
+  uint32_t v6w_fib;  // 1: some v6 FIB has a window table (Lpm.wtab)
+  uint64_t v6w_p;
 };
 
 // 32-bit mixing hash for the open-addressing maps (host and device agree)

@@ -36,6 +36,17 @@ using namespace dpd;
 #define DP_PART -1
 #endif
 #define DP_IN_PART(k) (DP_PART < 0 || DP_PART == (k))
+// DP_V6W: the v6 window lookups (a v6 FIB's window table, the classifiers'
+// v6 key window -- Image.v6w_fib / v6w_c) compiled in.  Parts 1 and 2 build
+// the non-flow pipeline without them, parts 7 and 8 with them, and
+// dpk_launch_pipeline picks by the image; every other unit has them.
+#ifndef DP_V6W
+#if DP_PART == 1 || DP_PART == 2
+#define DP_V6W 0
+#else
+#define DP_V6W 1
+#endif
+#endif
 #ifndef DP_TPB
 #define DP_TPB 128
 #endif
@@ -879,19 +890,23 @@ __device__ __forceinline__ uint32_t key6(uint64_t hi, uint64_t lo, int off) {
   return (uint32_t)(x >> 58);
 }
 
-__device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t direct_off, uint32_t dbits, uint64_t blocks,
-                                             const Addr16 &a, uint64_t wtab = 0, uint64_t wpfx = 0,
-                                             uint32_t wbits = 0) {
+// sel = off | shift << 8 | bits << 16: the first table is indexed by `bits`
+// key bits taken at (khi >> shift), and the Poptrie below it starts at key bit
+// `off` -- the direct table (bits = off = dbits, shift = 64 - dbits) or a v6
+// FIB's window table (Lpm.wtab: 16 bits after the window's shared prefix)
+__device__ __forceinline__ uint32_t lpm_sel(uint32_t off, uint32_t shift, uint32_t bits) {
+  return off | (shift << 8) | (bits << 16);
+}
+__device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t table_off, uint32_t sel, uint64_t blocks,
+                                             const Addr16 &a) {
   const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1], klo = ((uint64_t)a.w[2] << 32) | a.w[3];
-  uint32_t e;
-  int off;
-  if (wtab && (khi >> (64 - wbits)) == wpfx) {  // v6 key inside the FIB's window
-    e = g.at<uint32_t>(wtab)[(uint32_t)(khi >> (48 - wbits)) & 0xffffu];
-    off = (int)wbits + 16;
-  } else {
-    e = g.at<uint32_t>(direct_off)[a.w[0] >> (32 - dbits)];  // dbits <= 32 for both families
-    off = (int)dbits;
-  }
+  int off = (int)(sel & 0xffu);
+#if DP_V6W
+  const uint32_t e = g.at<uint32_t>(table_off)[(uint32_t)(khi >> ((sel >> 8) & 0xffu)) &
+                                               ((1u << (sel >> 16)) - 1u)];
+#else
+  const uint32_t e = g.at<uint32_t>(table_off)[a.w[0] >> (32 - off)];  // the direct table (dbits <= 32)
+#endif
   TRIP();
   if (e & 0x80000000u) return e & 0x7fffffffu;
   TRIP();
@@ -916,7 +931,10 @@ __device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t direct_off, 
   return g.im.drop_nh;  // unreachable for a well-formed image
 }
 __device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
-  return lpm_walk(g, L.direct, L.dbits, L.blocks, a, L.wtab, L.wpfx, L.wbits);
+  const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1];
+  if (DP_V6W && L.wtab && (khi >> (64 - L.wbits)) == L.wpfx)
+    return lpm_walk(g, L.wtab, lpm_sel(L.wbits + 16, 48 - L.wbits, 16), 0, a);
+  return lpm_walk(g, L.direct, lpm_sel(L.dbits, 64 - L.dbits, L.dbits), L.blocks, a);
 }
 
 // Multibit index walk from a context record's descriptor (Mbi): leaf value
@@ -941,24 +959,23 @@ struct Key128 { uint64_t hi, lo; };
 #define CLS(arr, t, field) ((t) ? g.im.arr[1].field : g.im.arr[0].field)
 
 // The bounds range [lo, hi) a field's jump table leaves for a key: its
-// bucket's (the 16 bits after a v6 window's shared top bits, or the key's top
-// 16 bits), or the one interval of a v6 key outside the window's prefix.
+// 16-bit bucket's (v4 address >> 16, port, v6 address >> 112).
 __device__ __forceinline__ void jump_range(const uint32_t *jt, const FieldIdx &f, Key128 k, uint32_t &lo,
                                            uint32_t &hi) {
-  uint32_t b;
-  if (f.win) {
-    const uint64_t top = f.win == 64 ? k.hi : k.hi >> (64 - f.win);
-    if (top != f.pfx) {
-      lo = top < f.pfx ? f.below : f.above;
-      hi = lo + 1;
-      return;
-    }
-    b = (uint32_t)((f.win == 64 ? k.lo : (k.hi << f.win) | (k.lo >> (64 - f.win))) >> 48);
-  } else {
-    b = f.shift == 48 ? (uint32_t)(k.hi >> 48) : (uint32_t)(k.lo >> f.shift) & 0xffff;
-  }
+  const uint32_t b = f.shift == 48 ? (uint32_t)(k.hi >> 48) : (uint32_t)(k.lo >> f.shift) & 0xffff;
   lo = jt[b];
   hi = jt[b + 1] + 1;
+}
+
+// A v6 address key in the space of the classifiers' v6 indexes (Image.v6w_*):
+// the rules of one site share their top bits, so the indexes order the bits
+// after them (a top-16-bit jump table would hold every rule in one bucket).
+// Image-wide and uniform: the window test is one compare per key.
+__device__ __forceinline__ Key128 v6_window_key(uint32_t c, uint64_t p, Key128 k) {
+  if (!c) return k;
+  const uint64_t top = k.hi >> (64 - c);
+  if (top != p) return top < p ? Key128{0, 0} : Key128{~0ull, ~0ull};
+  return Key128{(k.hi << c) | (k.lo >> (64 - c)), (k.lo << c) | 1};
 }
 
 // Elementary interval of one key in one field index -> its leaf value
@@ -978,6 +995,7 @@ __device__ __forceinline__ uint32_t field_leaf(const Img &g, const FieldIdx &F, 
     }
     return e & ~DPD_LEAF;
   }
+  if (DP_V6W && F.shift == 48) key = v6_window_key(g.im.v6w_c, g.im.v6w_p, key);  // a v6 address field
   uint32_t lo = 0, hi = F.n;
   if (F.jump) jump_range(g.at<uint32_t>(F.jump), F, key, lo, hi);
   const uint64_t *bd = g.at<uint64_t>(F.bounds);
@@ -1006,10 +1024,13 @@ __device__ __forceinline__ bool pfx_ok(Key128 k, uint64_t ahi, uint64_t alo, uin
 // (global memory): nothing of the caller's private frame or LDS crosses the
 // call (DESIGN.md "Out-of-line device functions").
 __device__ DP_BV int64_t classify_bv(const uint8_t *base, const Group *Gp, uint8_t proto, Key128 src,
-                                       Key128 dst, uint16_t sp, uint16_t dp) {
+                                       Key128 dst, uint16_t sp, uint16_t dp, uint32_t wc, uint64_t wp) {
   const ImgBase g{base};
   const Group G = *Gp;
   Key128 key[4] = {src, dst, Key128{0, sp}, Key128{0, dp}};
+  // v6 address fields index the window's key space (v6_window_key)
+  if (DP_V6W && G.f[0].shift == 48) key[0] = v6_window_key(wc, wp, key[0]);
+  if (DP_V6W && G.f[1].shift == 48) key[1] = v6_window_key(wc, wp, key[1]);
   uint32_t lo[4], hi[4], e[4];
   // level 0 of every field: multibit root entry, or the jump-table range
 #pragma unroll
@@ -1192,7 +1213,7 @@ __device__ __forceinline__ Hit classify(const Img &g, const ClsArrays &A, int32_
     GTRIP(12);
     return verify_run(g, A.recs, field_leaf(g, F, k), v6, proto, src, dst, sp, dp, (WANT & W_ORIG) != 0);
   }
-  const int64_t ri = classify_bv(g.base, Gp, proto, src, dst, sp, dp);
+  const int64_t ri = classify_bv(g.base, Gp, proto, src, dst, sp, dp, g.im.v6w_c, g.im.v6w_p);
   if (ri < 0) return h;
   h.rule = ri;
   if (WANT & W_ACTION) h.action = g.at<uint32_t>(A.action)[ri];
@@ -1952,18 +1973,21 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   cur_dst(F, H, S, fam, dst);
   // one walk for every lane: v4 and v6 lanes of a wave issue their direct-table
   // loads together (two call sites would run one after the other)
-  uint64_t wt = 0, wp = 0;
-  uint32_t wb = 0;
+  uint32_t sel = 0;
   if (!(fam == 4 && d4)) {
     const Lpm &L = fam == 4 ? fb.v4 : fb.v6;
     d4 = L.direct;
     b4 = L.dbits;
     k4 = L.blocks;
-    wt = L.wtab;
-    wp = L.wpfx;
-    wb = L.wbits;
+    // a v6 key inside the FIB's window reads the window table instead
+    if (DP_V6W && fam == 6 && L.wtab && ((((uint64_t)dst.w[0] << 32) | dst.w[1]) >> (64 - L.wbits)) == L.wpfx) {
+      d4 = L.wtab;
+      k4 = 0;
+      sel = lpm_sel(L.wbits + 16, 48 - L.wbits, 16);
+    }
   }
-  const uint32_t nhi = lpm_walk(g, d4, b4, k4, dst, wt, wp, wb);
+  if (!sel) sel = lpm_sel(b4, 64 - b4, b4);
+  const uint32_t nhi = lpm_walk(g, d4, sel, k4, dst);
   TRIP();
   const NhRec nr = g.at<NhRec>(g.im.nh_recs)[nhi];
   if (nr.kind != DPD_NH_CHAIN) {
@@ -3057,7 +3081,8 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
 // FL: the flows variant (a flow table is attached to the context); MT: meta
 // records requested (meta != nullptr); RP: the replay pass of the packets
 // that reached PortForwarder (FL only).
-template <bool FL, bool MT, bool RP = false>
+// VW: DP_V6W of the unit (a distinct kernel name per build of it).
+template <bool FL, bool MT, bool RP, int VW>
 __global__ void __launch_bounds__(TPB) DP_OCC
 dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict__ im, uint8_t *__restrict__ buf,
                    uint64_t buf_bytes, const dp_pkt_in_t *__restrict__ in,
@@ -3664,12 +3689,14 @@ extern "C" void dpemu_trips_out(uint16_t *p) { dp_trip_out = p; }
       const dpf::FlowCtx &fc
 #define DP_RUNNER(NAME, FL, MT, RP)                                                                   \
   extern "C" void NAME(DP_RUN_ARGS) {                                                                 \
-    hipLaunchKernelGGL((dp_pipeline_kernel<FL, MT, RP>), dim3(blocks), dim3(TPB), 0, s, img_base, im, \
+    hipLaunchKernelGGL((dp_pipeline_kernel<FL, MT, RP, DP_V6W>), dim3(blocks), dim3(TPB), 0, s, img_base, im, \
                        buf, buf_bytes, in, out, meta, n, part, fc);                                   \
   }
 extern "C" {
 void dpk_run_pipeline_000(DP_RUN_ARGS);
 void dpk_run_pipeline_010(DP_RUN_ARGS);
+void dpk_run_pipeline_000w(DP_RUN_ARGS);
+void dpk_run_pipeline_010w(DP_RUN_ARGS);
 void dpk_run_pipeline_100(DP_RUN_ARGS);
 void dpk_run_pipeline_110(DP_RUN_ARGS);
 void dpk_run_pipeline_101(DP_RUN_ARGS);
@@ -3680,6 +3707,12 @@ DP_RUNNER(dpk_run_pipeline_000, false, false, false)
 #endif
 #if DP_IN_PART(2)
 DP_RUNNER(dpk_run_pipeline_010, false, true, false)
+#endif
+#if DP_IN_PART(7)
+DP_RUNNER(dpk_run_pipeline_000w, false, false, false)
+#endif
+#if DP_IN_PART(8)
+DP_RUNNER(dpk_run_pipeline_010w, false, true, false)
 #endif
 #if DP_IN_PART(3)
 DP_RUNNER(dpk_run_pipeline_100, true, false, false)
@@ -3773,14 +3806,17 @@ extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
-                                   hipStream_t stream) {
+                                   int v6w, hipStream_t stream) {
   if (n == 0) return 0;
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
   const dpf::FlowCtx nofc{};
-  if (meta) dpk_run_pipeline_010(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, nofc);
-  else dpk_run_pipeline_000(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, nofc);
+  // an image with v6 windows needs the units that look them up
+  if (meta) (v6w ? dpk_run_pipeline_010w : dpk_run_pipeline_010)(blocks, stream, img_base, im, buf, buf_bytes, in,
+                                                                  out, meta, n, part, nofc);
+  else (v6w ? dpk_run_pipeline_000w : dpk_run_pipeline_000)(blocks, stream, img_base, im, buf, buf_bytes, in, out,
+                                                             meta, n, part, nofc);
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));

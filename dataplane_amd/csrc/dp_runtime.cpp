@@ -38,7 +38,7 @@
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
-                                   hipStream_t stream);
+                                   int v6w, hipStream_t stream);
 extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
                                hipStream_t stream);
 extern "C" int dpk_stage_expand(const uint8_t *cin, const uint32_t *pos, const dp_pkt_in_t *in, uint8_t *buf,
@@ -567,7 +567,7 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     }
   } else {
     rc = dpk_launch_pipeline(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out, dev_meta, n,
-                             dev_stats, part, s);
+                             dev_stats, part, img->im.v6w_c || img->im.v6w_fib, s);
   }
   if (rc) {
     hipError_t e = hipGetLastError();

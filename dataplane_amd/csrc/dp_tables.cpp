@@ -338,8 +338,32 @@ Iv prefix_iv(const dp_prefix_t &p, int fam) {
 // ports; > 16 intervals) or sorted bounds (+ 16-bit jump table).  `leaf[k]`
 // (< 2^31) is the value of interval k: a bit-vector row id, or a packed
 // candidate run (DPD_GROUP_LIST).
+// The v6 window of this image's classifiers (Image.v6w_*), set by build_image
+// before the classifiers are built: every v6 rule prefix lies inside the
+// prefix of g_v6w_c bits with value g_v6w_p (0 bits: no window).
+thread_local int g_v6w_c = 0;
+thread_local u128 g_v6w_p = 0;
+
+// A v6 bound in the window's key space (dp_kernel.hip v6_window_key): 0 below
+// the window, all ones above it, else shifted left by the window's bits with
+// bit 0 set (distinct from both).  Monotonic, so the intervals keep their order.
+u128 v6_window_bound(u128 x) {
+  if (!g_v6w_c) return x;
+  const int sh = 128 - g_v6w_c;
+  if ((x >> sh) < g_v6w_p) return 0;
+  if ((x >> sh) > g_v6w_p) return ~(u128)0;
+  return (x << g_v6w_c) | 1;
+}
+
 void build_field_index(ImgBuf &ib, FieldIdx &F, int f, int fam, size_t ngroups,
-                       const std::vector<u128> &bnd, const std::vector<uint32_t> &leaf) {
+                       const std::vector<u128> &bnd_in, const std::vector<uint32_t> &leaf) {
+  // a v6 address field indexes the window's key space
+  std::vector<u128> wbnd;
+  if (fam == 6 && f < 2 && g_v6w_c) {
+    for (const u128 &x : bnd_in) wbnd.push_back(v6_window_bound(x));
+    wbnd[0] = 0;
+  }
+  const std::vector<u128> &bnd = wbnd.empty() ? bnd_in : wbnd;
   const size_t m = bnd.size();
   F.n = (uint32_t)m;
   F.jump = 0;
@@ -380,37 +404,15 @@ void build_field_index(ImgBuf &ib, FieldIdx &F, int f, int fam, size_t ngroups,
   // bucket = top 16 bits of the key: v4 address >> 16, port itself,
   // v6 address hi64 >> 48
   F.shift = f >= 2 ? 0 : (fam == 4 ? 16 : 48);
-  F.win = 0;
   if (m > 16) {
-    auto ivl = [&](u128 x) -> uint32_t {
-      return (uint32_t)(std::upper_bound(bnd.begin(), bnd.end(), x) - bnd.begin()) - 1;
-    };
-    // v6 address: bucket the 16 bits after the longest prefix (<= 64 bits)
-    // every bound but 0 and that prefix's end shares -- rules of one site or
-    // VPC share their top bits, and a top-16-bit bucket would hold them all
-    u128 base = 0;
-    int bsh = f >= 2 ? 0 : (fam == 4 ? 16 : 112);  // bucket b starts at base + (b << bsh)
-#ifndef DP_NO_V6_WINDOW
-    if (fam == 6 && f < 2) {
-      for (int c = 64; c >= 1; c--) {
-        const int sh = 128 - c;
-        const u128 P = bnd[1] >> sh, end = (P + 1) << sh;  // end wraps to 0 past the top
-        bool ok = true;
-        for (size_t k = 1; k < m && ok; k++) ok = (bnd[k] >> sh) == P || bnd[k] == end;
-        if (!ok) continue;
-        F.win = (uint8_t)c;
-        F.pfx = (uint64_t)P;
-        F.below = P ? ivl((P << sh) - 1) : 0;
-        F.above = end ? ivl(end) : (uint32_t)(m - 1);
-        base = P << sh;
-        bsh = sh - 16;
-        break;
-      }
-    }
-#endif
     std::vector<uint32_t> jump(65537);
-    for (uint32_t b = 0; b < 65536; b++) jump[b] = ivl(base + ((u128)b << bsh));
-    jump[65536] = F.win ? ivl(base + ((u128)65536 << bsh) - 1) : (uint32_t)(m - 1);
+    size_t j = 0;
+    for (uint32_t b = 0; b < 65536; b++) {
+      u128 start = f >= 2 ? (u128)b : (fam == 4 ? ((u128)b << 16) : ((u128)b << 112));
+      while (j + 1 < m && bnd[j + 1] <= start) j++;
+      jump[b] = (uint32_t)j;
+    }
+    jump[65536] = (uint32_t)(m - 1);
     F.jump = ib.put(jump);
   }
 }
@@ -910,6 +912,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
     uint32_t d4 = r4[f].size() > 65536 ? 24 : 16;
     fr.v4 = build_lpm(ib, pb, r4[f], 32, d4);
     fr.v6 = build_lpm(ib, pb, r6[f], 128, 16);
+    if (fr.v6.wtab) im.v6w_fib = 1;
     fibs.push_back(fr);
     vrfkv.push_back(KV{s.vrf_id, 0, 0, f});
   }
@@ -1044,9 +1047,37 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   std::vector<std::vector<CRule>> keep(6);
   std::vector<const dp_rule_t *> ffr_order[2];
   std::vector<std::pair<uint64_t, const dp_rule_t *>> ffr_aux[2];
+  for (int ti = 0; ti < 6; ti++)
+    if ((rc = load_rules(tabs[ti].r, tabs[ti].n, tabs[ti].fam, tabs[ti].prio, tabs[ti].kind, keep[ti]))) return rc;
+  // the v6 window: the longest prefix (17..48 bits) holding every v6 rule
+  // prefix of every classifier -- one site's rules share their top bits, and
+  // the v6 address indexes then order the bits after them
+  {
+    int c = 48;
+    bool any = false;
+    u128 p0 = 0;
+    for (int ti : {1, 3, 5})
+      for (const CRule &cr : keep[ti])
+        for (const dp_prefix_t *q : {&cr.r.src, &cr.r.dst}) {
+          if (q->len == 0) continue;
+          const u128 a = key128(6, q->addr);
+          if (!any) p0 = a;
+          any = true;
+          const u128 x = a ^ p0;
+          const int lcp = x == 0 ? 128 : ((uint64_t)(x >> 64) ? __builtin_clzll((uint64_t)(x >> 64))
+                                                               : 64 + __builtin_clzll((uint64_t)x));
+          c = std::min({c, (int)q->len, lcp});
+        }
+#ifdef DP_NO_V6_WINDOW
+    any = false;
+#endif
+    g_v6w_c = any && c >= 17 ? c : 0;
+    g_v6w_p = g_v6w_c ? p0 >> (128 - g_v6w_c) : 0;
+    im.v6w_c = (uint32_t)g_v6w_c;
+    im.v6w_p = (uint64_t)g_v6w_p;
+  }
   for (int ti = 0; ti < 6; ti++) {
     auto &t = tabs[ti];
-    if ((rc = load_rules(t.r, t.n, t.fam, t.prio, t.kind, keep[ti]))) return rc;
     bool ffr = ti == 2 || ti == 3;
     *t.dst = build_classifier(ib, keep[ti], t.fam, t.kind, &gkv[ti], ffr ? &ffr_order[ti - 2] : nullptr,
                               ffr ? &ffr_aux[ti - 2] : nullptr);

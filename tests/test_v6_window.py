@@ -1,12 +1,14 @@
-"""CPU: the v6 address index of the classifiers (dp_tables.cpp
-build_field_index).  Rules of one site share their top address bits, so the
-16-bit jump table over a v6 address field buckets the 16 bits after the
-longest prefix every bound shares (a top-16-bit bucket would hold every
-rule, leaving a binary search over all bounds).  Keys outside that prefix
-fall in the interval just below or just above it.  The kernel body on the
-host (tests/emu) against the oracle, for rule sets whose shared prefix is
-/48, /32, /8 or none, with addresses inside the rules, between them, at the
-prefix's edges and outside it on both sides, in both classifier forms."""
+"""CPU: v6 address lookups of one site against the oracle -- the kernel body
+on the host (tests/emu).
+
+- The classifiers' v6 address index (dp_tables.cpp build_field_index:
+  sorted bounds narrowed by a 16-bit jump table), for rule sets whose shared
+  prefix is /48, /32, /8 or none, with addresses inside the rules, between
+  them, at the site's edges and outside it on both sides, in both classifier
+  forms.
+- The v6 FIB's window table (Lpm.wtab, dp_tables.cpp add_v6_window): routes of
+  one site, a shorter route covering it and the /0, looked up from inside the
+  site, at its edges and outside it."""
 import ipaddress
 import random
 
