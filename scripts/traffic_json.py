@@ -31,7 +31,7 @@ def main():
             "l2_hit": s.get("l2_hit"),
             "packets_per_launch_measured": 2000000,
             "source": f"{dst}/c{c}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum "
-                      "TCC_MISS_sum, separate passes; dp_pipeline_kernel<false, false, false> dispatches only)",
+                      "TCC_MISS_sum, separate passes; dp_pipeline_kernel<false, false, false, *> dispatches only)",
             "correction": "FETCH_SIZE doubled, WRITE_SIZE as read (MI355X_MICROARCH.md, HBM section); KB units x1024",
             "traffic_over_algorithmic": round(b / ALG[c], 2),
         }
