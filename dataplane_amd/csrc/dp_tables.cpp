@@ -28,6 +28,10 @@
 #include <unordered_map>
 #include <vector>
 
+#ifndef DP_SMALL_DBITS
+#define DP_SMALL_DBITS 20  // direct-table bits of small v4 FIBs with long routes (16: off)
+#endif
+
 namespace dpd {
 namespace {
 
@@ -901,6 +905,17 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   PtBuilder pb;
   std::vector<FibRec> fibs;
   std::vector<KV> vrfkv, vnikv;
+  // v4 direct tables: DIR-24-8 above 64 Ki routes; below, a 16-bit table,
+  // or a 2^DP_SMALL_DBITS one for a FIB holding routes longer than /16 (host
+  // routes, the VTEP /32: one Poptrie level fewer, 20 -> 26 -> leaf), while
+  // those tables stay within 256 MiB over the image
+  uint32_t small_long = 0;
+  for (uint32_t f = 0; f < d->n_fibs; f++)
+    if (r4[f].size() <= 65536)
+      for (const PRoute &p : r4[f])
+        if (p.len > 16) { small_long++; break; }
+  const uint32_t small_d =
+      (uint64_t)small_long * (4ull << DP_SMALL_DBITS) <= (256ull << 20) ? (uint32_t)DP_SMALL_DBITS : 16u;
   for (uint32_t f = 0; f < d->n_fibs; f++) {
     const dp_fib_t &s = d->fibs[f];
     FibRec fr{};
@@ -909,7 +924,11 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
     fr.vtep_fam = s.vtep_ip.family;
     memcpy(fr.vtep_mac, s.vtep_mac, 6);
     memcpy(fr.vtep_ip, s.vtep_ip.addr, s.vtep_ip.family == 6 ? 16 : 4);
-    uint32_t d4 = r4[f].size() > 65536 ? 24 : 16;
+    uint32_t d4 = 16;
+    if (r4[f].size() > 65536) d4 = 24;
+    else
+      for (const PRoute &p : r4[f])
+        if (p.len > 16) { d4 = small_d; break; }
     fr.v4 = build_lpm(ib, pb, r4[f], 32, d4);
     fr.v6 = build_lpm(ib, pb, r6[f], 128, 16);
     if (fr.v6.wtab) im.v6w_fib = 1;
