@@ -64,12 +64,12 @@ struct Lpm {
                        // 24-bit direct table); 0: Poptrie nodes below the direct table
   // v6 window (wtab != 0): the routes longer than /16 share their top wbits
   // bits (wpfx = those bits); a key inside that prefix reads
-  // wtab[the 16 bits after them] -- leaf, or a Poptrie node at bit wbits + 16
+  // wtab[the wtb bits after them] -- leaf, or a Poptrie node at bit wbits + wtb
   // -- instead of walking the Poptrie down from bit 16
-  uint64_t wtab;       // offset of uint32_t[65536]
+  uint64_t wtab;       // offset of uint32_t[1 << wtb]
   uint64_t wpfx;
   uint32_t wbits;      // 24..48
-  uint32_t pad;
+  uint32_t wtb;        // window table bits (wtab holds 2^wtb entries)
 };
 
 struct FibRec {

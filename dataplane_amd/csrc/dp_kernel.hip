@@ -893,7 +893,7 @@ __device__ __forceinline__ uint32_t key6(uint64_t hi, uint64_t lo, int off) {
 // sel = off | shift << 8 | bits << 16: the first table is indexed by `bits`
 // key bits taken at (khi >> shift), and the Poptrie below it starts at key bit
 // `off` -- the direct table (bits = off = dbits, shift = 64 - dbits) or a v6
-// FIB's window table (Lpm.wtab: 16 bits after the window's shared prefix)
+// FIB's window table (Lpm.wtab: the wtb bits after the window's shared prefix)
 __device__ __forceinline__ uint32_t lpm_sel(uint32_t off, uint32_t shift, uint32_t bits) {
   return off | (shift << 8) | (bits << 16);
 }
@@ -933,7 +933,7 @@ __device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t table_off, u
 __device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
   const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1];
   if (DP_V6W && L.wtab && (khi >> (64 - L.wbits)) == L.wpfx)
-    return lpm_walk(g, L.wtab, lpm_sel(L.wbits + 16, 48 - L.wbits, 16), 0, a);
+    return lpm_walk(g, L.wtab, lpm_sel(L.wbits + L.wtb, 64 - L.wbits - L.wtb, L.wtb), 0, a);
   return lpm_walk(g, L.direct, lpm_sel(L.dbits, 64 - L.dbits, L.dbits), L.blocks, a);
 }
 
@@ -1983,7 +1983,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
     if (DP_V6W && fam == 6 && L.wtab && ((((uint64_t)dst.w[0] << 32) | dst.w[1]) >> (64 - L.wbits)) == L.wpfx) {
       d4 = L.wtab;
       k4 = 0;
-      sel = lpm_sel(L.wbits + 16, 48 - L.wbits, 16);
+      sel = lpm_sel(L.wbits + L.wtb, 64 - L.wbits - L.wtb, L.wtb);
     }
   }
   if (!sel) sel = lpm_sel(b4, 64 - b4, b4);

@@ -28,6 +28,9 @@
 #include <unordered_map>
 #include <vector>
 
+#ifndef DP_V6_WTB
+#define DP_V6_WTB 20  // v6 window table bits (16: 256 KiB per FIB, 20: 4 MiB)
+#endif
 #ifndef DP_SMALL_DBITS
 #define DP_SMALL_DBITS 20  // direct-table bits of small v4 FIBs with long routes (16: off)
 #endif
@@ -167,10 +170,10 @@ struct PtBuilder {
 
 // v6 window (Lpm.wtab): the routes longer than the 16-bit direct table share
 // their top bits (a site's or provider's prefix, e.g. 2001:db8::/32); keys
-// inside that prefix read a 65536-entry table over the next 16 bits -- the
-// best route of length <= wbits + 16, or a Poptrie node for the longer ones
-// -- instead of walking (wbits + 16 - 16) / 6 Poptrie levels down to it.
-// `uniq` is sorted by (key, length).
+// inside that prefix read a table over the next wtb bits (DP_V6_WTB, 20: 4 MiB;
+// 16 when the prefix is longer than 64 - 20) -- the best route of length
+// <= wbits + wtb, or a Poptrie node for the longer ones -- instead of walking
+// the Poptrie levels down to it.  `uniq` is sorted by (key, length).
 void add_v6_window(ImgBuf &ib, PtBuilder &pb, const std::vector<PRoute> &uniq, Lpm &L) {
   bool any = false;
   u128 lo = 0, hi = 0;
@@ -187,6 +190,7 @@ void add_v6_window(ImgBuf &ib, PtBuilder &pb, const std::vector<PRoute> &uniq, L
   int c = x == 0 ? 128 : ((uint64_t)(x >> 64) ? __builtin_clzll((uint64_t)(x >> 64)) : 64 + __builtin_clzll((uint64_t)x));
   c = std::min({c, minlen, 48});
   if (c < 24) return;
+  const int wb = c + DP_V6_WTB <= 64 ? DP_V6_WTB : 16;  // window table bits
   const int sh = 128 - c;
   const u128 P = lo >> sh, base = P << sh;
   // the longest route of length <= c covering the window (the /0 at least)
@@ -197,36 +201,37 @@ void add_v6_window(ImgBuf &ib, PtBuilder &pb, const std::vector<PRoute> &uniq, L
       d = r.nh;
       dl = r.len;
     }
-  std::vector<uint32_t> val(65536, d);
+  std::vector<uint32_t> val((size_t)1 << wb, d);
   std::vector<const PRoute *> mid;
   for (const PRoute &r : uniq)
-    if (r.len > c && r.len <= c + 16) mid.push_back(&r);
+    if (r.len > c && r.len <= c + wb) mid.push_back(&r);
   std::stable_sort(mid.begin(), mid.end(), [](const PRoute *a, const PRoute *b) { return a->len < b->len; });
   for (const PRoute *p : mid) {
-    const uint32_t span = 1u << (c + 16 - p->len);
-    const uint32_t v0 = kbits(p->key, c, 16) & ~(span - 1);
+    const uint32_t span = 1u << (c + wb - p->len);
+    const uint32_t v0 = kbits(p->key, c, wb) & ~(span - 1);
     std::fill(val.begin() + v0, val.begin() + v0 + span, p->nh);
   }
-  std::vector<uint32_t> tab(65536);
+  std::vector<uint32_t> tab((size_t)1 << wb);
   for (size_t k = 0; k < tab.size(); k++) tab[k] = 0x80000000u | val[k];
   size_t i = 0;
   while (i < uniq.size()) {
-    if (uniq[i].len <= c + 16) { i++; continue; }
-    const uint32_t slot = kbits(uniq[i].key, c, 16);
+    if (uniq[i].len <= c + wb) { i++; continue; }
+    const uint32_t slot = kbits(uniq[i].key, c, wb);
     std::vector<PRoute> sub;
     size_t j = i;
-    while (j < uniq.size() && (uniq[j].key >> sh) == P && kbits(uniq[j].key, c, 16) == slot) {
-      if (uniq[j].len > c + 16) sub.push_back(uniq[j]);
+    while (j < uniq.size() && (uniq[j].key >> sh) == P && kbits(uniq[j].key, c, wb) == slot) {
+      if (uniq[j].len > c + wb) sub.push_back(uniq[j]);
       j++;
     }
     const uint32_t idx = (uint32_t)pb.nodes.size();
     pb.nodes.emplace_back();
-    pb.build_node(idx, sub.data(), sub.size(), val[slot], c + 16);
+    pb.build_node(idx, sub.data(), sub.size(), val[slot], c + wb);
     tab[slot] = idx;
     i = j;
   }
   L.wtab = ib.put(tab);
   L.wpfx = (uint64_t)P;
+  L.wtb = (uint32_t)wb;
   L.wbits = (uint32_t)c;
 }
 
