@@ -121,6 +121,9 @@ struct DevImage {
 
 struct DeviceTables {
   std::mutex mu;
+  // publishes of one device, one at a time: each builds on the lineage (the
+  // port-forwarding entry ids) the previous one stored
+  std::mutex pub_mu;
   std::shared_ptr<DevImage> cur;
   dpd::PfLineage pf;  // the port-forwarding entries of `cur` (PortFwTable::update lineage)
 };
@@ -153,6 +156,7 @@ constexpr int kPartSlots = 4;
 // duplex).
 constexpr uint32_t kHostChunk = 65536;
 constexpr int kHostStreams = 3;
+class HostPool;
 struct PartSlot {
   uint64_t *part = nullptr;
   hipEvent_t used = nullptr;
@@ -207,6 +211,9 @@ struct dp_ctx {
   hipEvent_t fl_used = nullptr;
   bool fl_armed = false;
   uint64_t clock = 0;                  // dp_ctx_set_option(DP_OPT_CLOCK)
+  // host threads of the staged-copy path, the context's own: a staged burst
+  // waits for its own chunks only, never for another worker's
+  std::unique_ptr<HostPool> pool;
 };
 
 namespace {
@@ -256,16 +263,13 @@ uint32_t host_threads(uint32_t n) {
   return std::max(1u, std::min(hw, n / 32768));
 }
 // A pool of host threads for the staged-copy path's gather and write-back,
-// created on first use and kept for the process (thread creation per burst
-// cost more than the gather itself).  run(parts, f) calls f(t) for every t in
+// one per context, created on its first staged burst and kept until the
+// context is destroyed (thread creation per burst cost more than the gather
+// itself).  run(parts, f) calls f(t) for every t in
 // [0, parts) -- the caller takes part of the work -- and returns when all
 // are done; concurrent callers take turns.
 class HostPool {
  public:
-  static HostPool &get() {
-    static HostPool p;
-    return p;
-  }
   void run(uint32_t parts, const std::function<void(uint32_t)> &f) {
     if (parts <= 1) {
       f(0u);
@@ -334,8 +338,34 @@ class HostPool {
 };
 
 template <class F>
-void par_for(uint32_t parts, F &&f) {
-  HostPool::get().run(parts, std::function<void(uint32_t)>(std::forward<F>(f)));
+void par_for(dp_ctx *c, uint32_t parts, F &&f) {
+  if (!c->pool) c->pool.reset(new HostPool());
+  c->pool->run(parts, std::function<void(uint32_t)>(std::forward<F>(f)));
+}
+
+// Every per-packet array of the host paths (the device records and span
+// positions, their pinned host sides), grown together to at least n packets:
+// the staged and the sharded paths share them, so one capacity covers all.
+hipError_t ensure_records(dp_ctx *c, uint32_t n) {
+  if (n <= c->cap_n) return hipSuccess;
+  (void)hipStreamSynchronize(c->stream);
+  for (void *p : {(void *)c->d_in, (void *)c->d_out, (void *)c->d_meta, (void *)c->d_pos}) if (p) (void)hipFree(p);
+  for (void *p : {(void *)c->h_in, (void *)c->h_out, (void *)c->h_meta, (void *)c->h_pos}) if (p) (void)hipHostFree(p);
+  c->d_in = nullptr; c->d_out = nullptr; c->d_meta = nullptr; c->d_pos = nullptr;
+  c->h_in = nullptr; c->h_out = nullptr; c->h_meta = nullptr; c->h_pos = nullptr;
+  c->cap_n = 0;
+  hipError_t e;
+  if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&c->d_meta, sizeof(dp_pkt_meta_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&c->d_pos, sizeof(uint32_t) * n)) != hipSuccess ||
+      (e = hipHostMalloc(&c->h_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess ||
+      (e = hipHostMalloc(&c->h_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess ||
+      (e = hipHostMalloc(&c->h_meta, sizeof(dp_pkt_meta_t) * n)) != hipSuccess ||
+      (e = hipHostMalloc(&c->h_pos, sizeof(uint32_t) * n)) != hipSuccess)
+    return e;
+  c->cap_n = n;
+  return hipSuccess;
 }
 
 // Every packet of a failed burst is InternalFailure (dpgpu.h conventions,
@@ -435,6 +465,7 @@ int dp_tables_publish(dp_ctx_t *c, const dp_tables_desc_t *tables) {
   if (!c || !tables) return fail(DP_EINVAL, "null argument");
   dpd::BuiltImage bi;
   DeviceTables &dt = dev_tables(c->device);
+  std::lock_guard<std::mutex> publishing(dt.pub_mu);
   dpd::PfLineage pf;
   {
     std::lock_guard<std::mutex> lk(dt.mu);
@@ -694,24 +725,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     if ((e = hipMalloc(&c->d_buf, need)) != hipSuccess) { c->d_buf_cap = 0; return bail(DP_ENOMEM, "hipMalloc burst", e); }
     c->d_buf_cap = need;
   }
-  if (n > c->cap_n) {
-    (void)hipStreamSynchronize(c->stream);
-    for (void *p : {(void *)c->d_in, (void *)c->d_out, (void *)c->d_meta, (void *)c->d_pos}) if (p) (void)hipFree(p);
-    for (void *p : {(void *)c->h_in, (void *)c->h_out, (void *)c->h_meta, (void *)c->h_pos}) if (p) (void)hipHostFree(p);
-    c->d_in = nullptr; c->d_out = nullptr; c->d_meta = nullptr; c->d_pos = nullptr;
-    c->h_in = nullptr; c->h_out = nullptr; c->h_meta = nullptr; c->h_pos = nullptr;
-    c->cap_n = 0;
-    if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess ||
-        (e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess ||
-        (e = hipMalloc(&c->d_meta, sizeof(dp_pkt_meta_t) * n)) != hipSuccess ||
-        (e = hipMalloc(&c->d_pos, sizeof(uint32_t) * n)) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_in, sizeof(dp_pkt_in_t) * n)) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_out, sizeof(dp_pkt_out_t) * n)) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_meta, sizeof(dp_pkt_meta_t) * n)) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_pos, sizeof(uint32_t) * n)) != hipSuccess)
-      return bail(DP_ENOMEM, "burst records (device / pinned)", e);
-    c->cap_n = n;
-  }
+  if ((e = ensure_records(c, n)) != hipSuccess) return bail(DP_ENOMEM, "burst records (device / pinned)", e);
   dp_pkt_meta_t *dm = meta ? c->d_meta : nullptr;
   hipStream_t s = c->stream;
   const uint32_t grow = [&] {
@@ -722,7 +736,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
   HostTrace tr;
   const uint32_t T = host_threads(n);
   std::vector<uint64_t> acc(T + 1, 0);
-  par_for(T, [&](uint32_t t) {
+  par_for(c, T, [&](uint32_t t) {
     uint64_t sum = 0;
     for (uint32_t i = (uint32_t)((uint64_t)n * t / T), b = (uint32_t)((uint64_t)n * (t + 1) / T); i < b; i++)
       sum += ((in[i].off + in[i].len + 15u) >> 4) - (in[i].off >> 4);
@@ -746,7 +760,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     c->cout_cap = co;
   }
   tr.mark("sums+alloc");
-  par_for(T, [&](uint32_t t) {
+  par_for(c, T, [&](uint32_t t) {
     uint64_t p = acc[t];
     for (uint32_t i = (uint32_t)((uint64_t)n * t / T), b = (uint32_t)((uint64_t)n * (t + 1) / T); i < b; i++) {
       c->h_pos[i] = (uint32_t)p;
@@ -756,7 +770,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
   });
   // the frames of packets [a, b): host threads pack their spans
   auto gather = [&](uint32_t a, uint32_t b) {
-    par_for(T, [&](uint32_t t) {
+    par_for(c, T, [&](uint32_t t) {
       for (uint32_t i = a + (uint32_t)((uint64_t)(b - a) * t / T), e = a + (uint32_t)((uint64_t)(b - a) * (t + 1) / T);
            i < e; i++) {
         const uint64_t lo = in[i].off & ~15u, u = ((in[i].off + in[i].len + 15u) >> 4) - (in[i].off >> 4);
@@ -852,7 +866,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
   tr.mark("gather+enqueue");
   std::atomic<int> werr{0};
   const uint32_t W = std::min<uint32_t>(T, nch);
-  par_for(W, [&](uint32_t t) {
+  par_for(c, W, [&](uint32_t t) {
     (void)hipSetDevice(c->device);
     for (uint32_t k = t; k < nch; k += W) {
       if (hipEventSynchronize(c->chunk_ev[k]) != hipSuccess) { werr = 1; continue; }
@@ -946,20 +960,7 @@ int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf
       if ((e = hipMalloc(&c->d_buf, need)) != hipSuccess) { rc = fail(DP_ENOMEM, "hipMalloc shard", e); break; }
       c->d_buf_cap = need;
     }
-    if (S.cnt > c->cap_n) {
-      (void)hipStreamSynchronize(c->stream);
-      if (c->d_in) (void)hipFree(c->d_in);
-      if (c->d_out) (void)hipFree(c->d_out);
-      if (c->d_meta) (void)hipFree(c->d_meta);
-      c->d_in = nullptr; c->d_out = nullptr; c->d_meta = nullptr; c->cap_n = 0;
-      if ((e = hipMalloc(&c->d_in, sizeof(dp_pkt_in_t) * S.cnt)) != hipSuccess ||
-          (e = hipMalloc(&c->d_out, sizeof(dp_pkt_out_t) * S.cnt)) != hipSuccess ||
-          (e = hipMalloc(&c->d_meta, sizeof(dp_pkt_meta_t) * S.cnt)) != hipSuccess) {
-        rc = fail(DP_ENOMEM, "hipMalloc shard records", e);
-        break;
-      }
-      c->cap_n = S.cnt;
-    }
+    if ((e = ensure_records(c, S.cnt)) != hipSuccess) { rc = fail(DP_ENOMEM, "hipMalloc shard records", e); break; }
     hipStream_t s = c->stream;
     dp_pkt_meta_t *dm = meta ? c->d_meta : nullptr;
     if ((e = hipMemcpyAsync(c->d_buf, buf + S.lo, bytes, hipMemcpyHostToDevice, s)) != hipSuccess ||

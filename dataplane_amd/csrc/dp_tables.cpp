@@ -170,11 +170,13 @@ struct PtBuilder {
 
 // v6 window (Lpm.wtab): the routes longer than the 16-bit direct table share
 // their top bits (a site's or provider's prefix, e.g. 2001:db8::/32); keys
-// inside that prefix read a table over the next wtb bits (DP_V6_WTB, 20: 4 MiB;
-// 16 when the prefix is longer than 64 - 20) -- the best route of length
+// inside that prefix read a table over the next wtb bits (`wtb_max`: DP_V6_WTB,
+// 20: 4 MiB, while every FIB's window fits a 256 MiB budget over the image,
+// else 16; 16 also when the prefix is longer than 64 - 20) -- the best route of length
 // <= wbits + wtb, or a Poptrie node for the longer ones -- instead of walking
 // the Poptrie levels down to it.  `uniq` is sorted by (key, length).
-void add_v6_window(ImgBuf &ib, PtBuilder &pb, const std::vector<PRoute> &uniq, Lpm &L) {
+void add_v6_window(ImgBuf &ib, PtBuilder &pb, const std::vector<PRoute> &uniq, Lpm &L, int wtb_max) {
+  if (wtb_max <= 0) return;
   bool any = false;
   u128 lo = 0, hi = 0;
   int minlen = 129;
@@ -190,7 +192,7 @@ void add_v6_window(ImgBuf &ib, PtBuilder &pb, const std::vector<PRoute> &uniq, L
   int c = x == 0 ? 128 : ((uint64_t)(x >> 64) ? __builtin_clzll((uint64_t)(x >> 64)) : 64 + __builtin_clzll((uint64_t)x));
   c = std::min({c, minlen, 48});
   if (c < 24) return;
-  const int wb = c + DP_V6_WTB <= 64 ? DP_V6_WTB : 16;  // window table bits
+  const int wb = c + wtb_max <= 64 ? wtb_max : 16;  // window table bits
   const int sh = 128 - c;
   const u128 P = lo >> sh, base = P << sh;
   // the longest route of length <= c covering the window (the /0 at least)
@@ -236,7 +238,7 @@ void add_v6_window(ImgBuf &ib, PtBuilder &pb, const std::vector<PRoute> &uniq, L
 }
 
 // Build one FIB/family LPM; routes must include a /0.
-Lpm build_lpm(ImgBuf &ib, PtBuilder &pb, std::vector<PRoute> &routes, int width, uint32_t dbits) {
+Lpm build_lpm(ImgBuf &ib, PtBuilder &pb, std::vector<PRoute> &routes, int width, uint32_t dbits, int v6wtb = 0) {
   // sort by (key, len), keep the last insert of a duplicate prefix
   std::stable_sort(routes.begin(), routes.end(), [](const PRoute &a, const PRoute &b) {
     if (a.key != b.key) return a.key < b.key;
@@ -323,7 +325,7 @@ Lpm build_lpm(ImgBuf &ib, PtBuilder &pb, std::vector<PRoute> &routes, int width,
   L.dbits = dbits;
   L.width = (uint32_t)width;
 #ifndef DP_NO_V6_WINDOW
-  if (width == 128) add_v6_window(ib, pb, uniq, L);
+  if (width == 128) add_v6_window(ib, pb, uniq, L, v6wtb);
 #endif
   return L;
 }
@@ -921,6 +923,16 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
         if (p.len > 16) { small_long++; break; }
   const uint32_t small_d =
       (uint64_t)small_long * (4ull << DP_SMALL_DBITS) <= (256ull << 20) ? (uint32_t)DP_SMALL_DBITS : 16u;
+  // v6 window tables likewise within 256 MiB over the image: 2^DP_V6_WTB
+  // entries per FIB while every FIB with routes longer than /16 fits, else
+  // 2^16, else none (an image with ~1000 VPC FIBs must not grow by GiB)
+  uint64_t v6_long = 0;
+  for (uint32_t f = 0; f < d->n_fibs; f++)
+    for (const PRoute &p : r6[f])
+      if (p.len > 16) { v6_long++; break; }
+  const int v6wtb = v6_long * (4ull << DP_V6_WTB) <= (256ull << 20) ? DP_V6_WTB
+                    : v6_long * (4ull << 16) <= (256ull << 20)      ? 16
+                                                                    : 0;
   for (uint32_t f = 0; f < d->n_fibs; f++) {
     const dp_fib_t &s = d->fibs[f];
     FibRec fr{};
@@ -935,7 +947,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
       for (const PRoute &p : r4[f])
         if (p.len > 16) { d4 = small_d; break; }
     fr.v4 = build_lpm(ib, pb, r4[f], 32, d4);
-    fr.v6 = build_lpm(ib, pb, r6[f], 128, 16);
+    fr.v6 = build_lpm(ib, pb, r6[f], 128, 16, v6wtb);
     if (fr.v6.wtab) im.v6w_fib = 1;
     fibs.push_back(fr);
     vrfkv.push_back(KV{s.vrf_id, 0, 0, f});

@@ -338,3 +338,25 @@ def test_gpu_sharded_full_size_c5(nf):
     finally:
         for x in nfs:
             x.close()
+
+
+def test_gpu_sharded_then_larger_staged_burst():
+    """One context first runs a sharded burst (which sizes its device records)
+    and then a larger staged-copy burst (pageable buffers): every per-packet
+    array of the host paths grows together (dp_runtime.cpp ensure_records), so
+    the staged burst never writes past a smaller allocation."""
+    w_small = Workload(2, 3000, seed=41, n_routes_v4=5000, n_acl=200, n_nat=16)
+    w_big = Workload(2, 40000, seed=42, n_routes_v4=5000, n_acl=200, n_nat=16)
+    x = GpuPathNf(0)
+    try:
+        x.publish(w_small.tables)
+        b_ref, b_dut = w_small.fresh_buf(), w_small.fresh_buf()
+        compare(Oracle(w_small.tables).process(b_ref, w_small.inp), b_ref,
+                GpuPathNf.process_sharded([x], b_dut, w_small.inp), b_dut, w_small.inp, "sharded first")
+        x.publish(w_big.tables)
+        x.set_host_path(A.HOST_COPY)
+        b_ref, b_dut = w_big.fresh_buf(), w_big.fresh_buf()
+        compare(Oracle(w_big.tables).process(b_ref, w_big.inp), b_ref,
+                x.process_arrays(b_dut, w_big.inp), b_dut, w_big.inp, "staged after sharded")
+    finally:
+        x.close()

@@ -11,6 +11,7 @@ on the host (tests/emu).
   site, at its edges and outside it."""
 import ipaddress
 import random
+import zlib
 
 import pytest
 
@@ -75,7 +76,7 @@ def probes(rule_nets, site: str, r: random.Random):
                                        ("2000::/8", 40), ("::/0", 24)])
 @pytest.mark.parametrize("form", ["list", "bv"])
 def test_v6_window_index(site, plen, form, cls_form):
-    r = random.Random(hash((site, plen)) & 0xffff)
+    r = random.Random(zlib.crc32(f"{site}/{plen}".encode()))
     n = ipaddress.ip_network(site)
     rule_nets = []
     for k in range(60):
@@ -117,7 +118,7 @@ def test_v6_fib_window(site, lens):
     route covering the site and the /0, looked up from inside the site, at its
     edges and outside it; each route its own FibEntry, so the packet's
     metadata names the route that matched."""
-    r = random.Random(hash(site) & 0xffff)
+    r = random.Random(zlib.crc32(str(site).encode()))
     t = TB(genid=1)
     t.add_iface(1, IF_MAC)
     t.add_iface(10, OIF_MAC)
@@ -162,3 +163,43 @@ def test_v6_fib_window(site, lens):
     o_dut = pyemu.process(tp, b_dut, inp)
     compare(o_ref, b_ref, o_dut, b_dut, inp, f"v6 FIB window {site}")
     assert len(set(o_ref["fib_entry"].tolist())) >= 10  # many routes, the covering one and the /0 hit
+
+
+def test_v6_window_budget():
+    """Window tables stay within a budget over the image (dp_tables.cpp
+    build_image v6wtb): 100 VPC FIBs, each with one /40 route, would need
+    100 x 4 MiB of 20-bit windows; they get 16-bit ones instead, and lookups
+    through them still match the oracle."""
+    r = random.Random(7)
+    t = TB(genid=1)
+    t.add_iface(1, IF_MAC)
+    t.add_iface(10, OIF_MAC)
+    t.add_adjacency("192.0.2.1", 10, NH_MAC)
+    t.add_adjacency("192.0.2.2", 10, NH_MAC)
+    nh0 = t.add_nh([[TB.egress(10, "192.0.2.1")]])
+    nh1 = t.add_nh([[TB.egress(10, "192.0.2.2")]])
+    t.add_route(t.add_fib(0), "0.0.0.0/0", nh0)
+    vnis = [5000 + k for k in range(100)]
+    for k, v in enumerate(vnis):
+        f = t.add_fib(v, vnis=[v])
+        t.add_route(f, "0.0.0.0/0", nh0)
+        t.add_route(f, "::/0", nh0)
+        t.add_route(f, f"2001:db8:{k:x}00::/40", nh1)
+    t.add_ff_remote(VNI_A, "::/0", vnis[3])
+    t.add_ff_local(VNI_A, vnis[3], "::/0")
+    t.add_fib(VNI_A, vnis=[VNI_A])
+    tp = t.build()
+    assert pyemu.lib().dpemu_image_bytes(tp) < (128 << 20)
+    frames = []
+    for k in range(400):
+        dst = f"2001:db8:{3 if k % 2 else 4:x}{r.randrange(256):02x}::{r.randrange(1, 65535):x}"
+        src = "2001:db8:ffff::1"
+        body = P.udp(1234, 80, b"x" * 8, P.pseudo6(src, dst, 17, 16))
+        fr = P.eth(IF_MAC, PEER_MAC, 0x86DD) + P.ipv6(src, dst, 17, len(body)) + body
+        frames.append((fr, 1, A.IN_SEEDED_OVERLAY, VNI_A))
+    buf, inp = pack_burst(frames)
+    b_ref, b_dut = buf.copy(), buf.copy()
+    o_ref = Oracle(tp).process(b_ref, inp)
+    o_dut = pyemu.process(tp, b_dut, inp)
+    compare(o_ref, b_ref, o_dut, b_dut, inp, "v6 window budget")
+    assert len(set(o_ref["fib_entry"].tolist())) == 2
