@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 HEADROOM = 96
 
 # DoneReason (net/src/packet/meta.rs:84-119)
@@ -101,8 +101,9 @@ FLOW_INFO = np.dtype([("ref", "<u8"), ("status", "<u4"), ("flags", "<u4"), ("dst
                       ("pad", "<u4"), ("genid", "<i8"), ("expires_at", "<u8"),
                       ("related", "<u8"), ("pf", "u1"), ("pf_status", "u1"), ("pf_port", "<u2"),
                       ("pf_rule", "<u4"), ("pf_family", "u1"), ("pad2", "u1", (7,)),
-                      ("pf_ip", "u1", (16,))])
-assert FLOW_KEY.itemsize == 44 and FLOW.itemsize == 72 and FLOW_INFO.itemsize == 80
+                      ("pf_ip", "u1", (16,)), ("masq", "u1"), ("masq_alloc", "u1"),
+                      ("pad3", "<u2"), ("idle_timeout_s", "<u4")])
+assert FLOW_KEY.itemsize == 44 and FLOW.itemsize == 72 and FLOW_INFO.itemsize == 88
 # enum dp_pf_action / dp_nat_flow_status (include/dpgpu.h)
 PF_NONE, PF_DST_NAT, PF_SRC_NAT = 0, 1, 2
 (NFS_ONE_WAY, NFS_TWO_WAY, NFS_ESTABLISHED, NFS_RESET, NFS_C_CLOSING, NFS_S_CLOSING,
@@ -202,6 +203,20 @@ class PortFwRule(C.Structure):
                 ("estab_timeout_s", C.c_uint32), ("ext_prefix", Prefix), ("int_prefix", Prefix)]
 
 
+class MasqExpose(C.Structure):
+    _fields_ = [("src_vni", C.c_uint32), ("dst_vni", C.c_uint32), ("idle_timeout_s", C.c_uint32),
+                ("first_prefix", C.c_uint32), ("n_private", C.c_uint16), ("n_public", C.c_uint16),
+                ("first_claim", C.c_uint32), ("n_claims", C.c_uint32)]
+
+
+class MasqClaim(C.Structure):
+    _fields_ = [("prefix", Prefix), ("lo", C.c_uint16), ("hi", C.c_uint16), ("protos", C.c_uint32)]
+
+
+MASQ_TCP, MASQ_UDP = 1, 2
+MASQ_REGION_ADDRS = 4096
+
+
 class TablesDesc(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("pad0", C.c_uint32), ("genid", C.c_int64),
                 ("fibs", C.POINTER(Fib)), ("n_fibs", C.c_uint32),
@@ -223,7 +238,11 @@ class TablesDesc(C.Structure):
                 ("nat_entries", C.POINTER(NatEntry)), ("n_nat_entries", C.c_uint32),
                 ("nat_port_ranges", C.POINTER(PortRange)), ("n_nat_port_ranges", C.c_uint32),
                 ("nat_ranges", C.POINTER(NatRange)), ("n_nat_ranges", C.c_uint32),
-                ("portfw", C.POINTER(PortFwRule)), ("n_portfw", C.c_uint32)]
+                ("portfw", C.POINTER(PortFwRule)), ("n_portfw", C.c_uint32),
+                ("masq", C.POINTER(MasqExpose)), ("n_masq", C.c_uint32),
+                ("masq_prefixes", C.POINTER(Prefix)), ("n_masq_prefixes", C.c_uint32),
+                ("masq_claims", C.POINTER(MasqClaim)), ("n_masq_claims", C.c_uint32),
+                ("masq_config_tag", C.c_uint64)]
 
 
 STRUCTS = dict(dp_ipaddr_t=IpAddr, dp_prefix_t=Prefix, dp_fib_t=Fib, dp_vni_fib_t=VniFib,
@@ -231,7 +250,7 @@ STRUCTS = dict(dp_ipaddr_t=IpAddr, dp_prefix_t=Prefix, dp_fib_t=Fib, dp_vni_fib_
                dp_route_t=Route, dp_iface_t=Iface, dp_adjacency_t=Adjacency, dp_rule_t=Rule,
                dp_acl_default_t=AclDefault, dp_nat_table_t=NatTable, dp_nat_entry_t=NatEntry,
                dp_port_range_t=PortRange, dp_nat_range_t=NatRange, dp_portfw_rule_t=PortFwRule,
-               dp_tables_desc_t=TablesDesc)
+               dp_masq_expose_t=MasqExpose, dp_masq_claim_t=MasqClaim, dp_tables_desc_t=TablesDesc)
 
 # every symbol include/dpgpu.h declares
 GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_publish",

@@ -79,6 +79,10 @@ class TablesBuilder:
         self.nat_prs: List[A.PortRange] = []
         self.nat_ranges: List[A.NatRange] = []
         self.portfw: List[A.PortFwRule] = []
+        self.masq: List[A.MasqExpose] = []
+        self.masq_prefixes: List[A.Prefix] = []
+        self.masq_claims: List[A.MasqClaim] = []
+        self.masq_config_tag = 0
         self._keep = []
 
     # -- routing --------------------------------------------------------------
@@ -215,6 +219,28 @@ class TablesBuilder:
         r.int_prefix = mk_prefix(str(ipaddress.ip_network(int_prefix, strict=False)))
         self.portfw.append(r)
 
+    # -- masquerade -------------------------------------------------------------
+    def add_masquerade(self, src_vni: int, dst_vni: int, private: Sequence[str],
+                       public: Sequence[str], idle_timeout_s: int = 0,
+                       claims: Sequence[Tuple[str, int, int, int]] = ()) -> None:
+        """A masquerade expose of the peering src_vni -> dst_vni (VpcExpose::
+        make_masquerade(idle).ip(private...).as_range(public...)); `claims`: the
+        port-forwarding exposes of the same local manifest as (public prefix,
+        lo, hi, protos) with protos of A.MASQ_TCP | A.MASQ_UDP."""
+        e = A.MasqExpose(src_vni=src_vni, dst_vni=dst_vni, idle_timeout_s=idle_timeout_s)
+        e.first_prefix = len(self.masq_prefixes)
+        for p in private:
+            self.masq_prefixes.append(mk_prefix(str(ipaddress.ip_network(p, strict=False))))
+        for p in public:
+            self.masq_prefixes.append(mk_prefix(str(ipaddress.ip_network(p, strict=False))))
+        e.n_private, e.n_public = len(private), len(public)
+        e.first_claim = len(self.masq_claims)
+        for (pfx, lo, hi, protos) in claims:
+            self.masq_claims.append(A.MasqClaim(prefix=mk_prefix(str(ipaddress.ip_network(pfx, strict=False))),
+                                                lo=lo, hi=hi, protos=protos))
+        e.n_claims = len(claims)
+        self.masq.append(e)
+
     # -- static NAT -------------------------------------------------------------
     def add_nat_table(self, kind: int, src_vni: int, dst_vni: int,
                       entries: Sequence[dict]) -> None:
@@ -283,5 +309,9 @@ class TablesBuilder:
         d.nat_port_ranges, d.n_nat_port_ranges = self._arr(A.PortRange, self.nat_prs)
         d.nat_ranges, d.n_nat_ranges = self._arr(A.NatRange, self.nat_ranges)
         d.portfw, d.n_portfw = self._arr(A.PortFwRule, self.portfw)
+        d.masq, d.n_masq = self._arr(A.MasqExpose, self.masq)
+        d.masq_prefixes, d.n_masq_prefixes = self._arr(A.Prefix, self.masq_prefixes)
+        d.masq_claims, d.n_masq_claims = self._arr(A.MasqClaim, self.masq_claims)
+        d.masq_config_tag = self.masq_config_tag
         self._desc = d
         return C.pointer(d)

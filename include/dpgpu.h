@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DPGPU_ABI_VERSION 3u
+#define DPGPU_ABI_VERSION 4u
 
 /* Bytes every frame must have in front of it (its own scratch, owned by the
  * packet).  Output headers are written in place into this headroom: VXLAN
@@ -392,6 +392,46 @@ typedef struct dp_portfw_rule {
     dp_prefix_t int_prefix;    /* internal prefix (same family and length) */
 } dp_portfw_rule_t;
 
+/* Masquerade (stateful source NAT, nat/src/masquerade/).  One record per
+ * masquerade expose of a stateful-NAT peering, in configuration order
+ * (MasqueradeConfig::new, nat/src/masquerade/allocator_writer.rs:43-61;
+ * gather_exposes, apalloc/setup.rs:95-137): the VPC whose private sources are
+ * masqueraded towards the peer VPC, the expose's private prefixes (ips()),
+ * its public ranges (as_range, the pools), its idle timeout, and the public
+ * tuples the port-forwarding exposes of the same local manifest may claim
+ * (claims_for, setup.rs:73-92), which the pools never hand out
+ * (apalloc/reserved.rs).  An expose is one address family: its private and
+ * public prefixes are all v4 (NAT44) or all v6 (NAT66).  The allocator is
+ * the reference's deterministic one (MasqueradeConfig::set_randomize(false),
+ * the mode its own collision test runs, nat/src/masquerade/test.rs:1399-1406):
+ * port blocks in index order, ports in bitmap order, addresses lowest first. */
+typedef struct dp_masq_expose {
+    uint32_t src_vni;          /* MasqueradePeering.src_vpcd */
+    uint32_t dst_vni;          /* MasqueradePeering.dst_vpcd */
+    uint32_t idle_timeout_s;   /* expose idle_timeout (0: 120 s, setup.rs:25) */
+    uint32_t first_prefix;     /* into masq_prefixes: n_private private prefixes,
+                                  then n_public public ones */
+    uint16_t n_private, n_public;
+    uint32_t first_claim;      /* into masq_claims */
+    uint32_t n_claims;
+} dp_masq_expose_t;
+
+/* A public (prefix, port range) a port-forwarding expose may claim, and the
+ * L4 protocols of its rule (ExposeNat.proto). */
+enum dp_masq_proto { DP_MASQ_TCP = 1u << 0, DP_MASQ_UDP = 1u << 1 };
+typedef struct dp_masq_claim {
+    dp_prefix_t prefix;
+    uint16_t lo, hi;           /* inclusive */
+    uint32_t protos;           /* enum dp_masq_proto */
+} dp_masq_claim_t;
+
+/* Addresses of one allocator region (a disjoint public range of one
+ * protocol towards one peer VPC, apalloc/region.rs) that can be in use at
+ * once: the region's lowest DP_MASQ_REGION_ADDRS offsets (the reference's
+ * u32 offset bitmap, alloc.rs:349-377, bounded for device memory; each
+ * address carries 64512 TCP / UDP ports). */
+#define DP_MASQ_REGION_ADDRS 4096u
+
 typedef struct dp_tables_desc {
     uint32_t abi_version;   /* DPGPU_ABI_VERSION */
     uint32_t pad0;
@@ -421,6 +461,16 @@ typedef struct dp_tables_desc {
     const dp_nat_range_t *nat_ranges; uint32_t n_nat_ranges;
 
     const dp_portfw_rule_t *portfw;  uint32_t n_portfw;
+
+    /* masquerade (NatAllocatorWriter::update_nat_allocator,
+     * allocator_writer.rs:120-154, applied to the attached flow tables) */
+    const dp_masq_expose_t *masq;    uint32_t n_masq;
+    const dp_prefix_t *masq_prefixes; uint32_t n_masq_prefixes;
+    const dp_masq_claim_t *masq_claims; uint32_t n_masq_claims;
+    /* MasqueradeConfig identity: two generations with the same non-zero tag
+     * are the same configuration (the allocator and its flows are kept, only
+     * the generation advances); 0: compared by the exposes and claims above */
+    uint64_t masq_config_tag;
 } dp_tables_desc_t;
 
 /* ------------------------------------------------------------------------ */
@@ -430,7 +480,7 @@ typedef struct dp_tables_desc {
 #define DP_EINVAL (-22)
 #define DP_ENOMEM (-12)
 #define DP_ENODEV (-19)
-#define DP_ENOTSUP (-95)   /* e.g. masquerade NAT modes */
+#define DP_ENOTSUP (-95)   /* a table form the path does not support */
 #define DP_EIO (-5)        /* HIP runtime failure */
 #define DP_ENOTABLES (-61) /* no tables published yet (ENODATA) */
 
@@ -540,9 +590,11 @@ int dp_ctx_set_option(dp_ctx_t *ctx, int option, int64_t value);
 /* (flow-filter/src/lib.rs:115-349) and AclFilter (acl-filter/src/lib.rs:    */
 /* 62-138) for every context it is attached to.                              */
 /*                                                                           */
-/* Flows carry no masquerade state (FlowInfoLocked.nat_state is None); the  */
-/* port-forwarding state (.port_fw_state) of the flow pairs PortForwarder     */
-/* creates is carried, and every flow has a destination VPC.                 */
+/* The NAT state of the flow pairs the data path creates is carried:        */
+/* port forwarding's (.port_fw_state) and masquerade's (.nat_state, with the */
+/* allocation the SrcNat flow owns, released when that flow leaves the table:*/
+/* a sweep, a remove, or a replacement -- at the end of the burst that       */
+/* replaced it).  Every flow has a destination VPC.                          */
 /*                                                                           */
 /* Burst semantics are the reference pipeline's: FlowLookup, the flow-filter */
 /* bypass decision and IcmpErrorHandler see flow states as they were when    */
@@ -619,6 +671,13 @@ typedef struct dp_flow_info {
     uint8_t pf_family;        /* use_ip family */
     uint8_t pad2[7];
     uint8_t pf_ip[16];        /* use_ip */
+    /* FlowInfoLocked.nat_state (MasqueradeState, nat/src/masquerade/state.rs:
+     * 13-20): action, with the status / use_ip / use_port in pf_status /
+     * pf_ip / pf_port (pf_family) */
+    uint8_t masq;             /* enum dp_pf_action (DP_PF_NONE: no state) */
+    uint8_t masq_alloc;       /* 1: the state owns an allocation (the SrcNat flow) */
+    uint16_t pad3;
+    uint32_t idle_timeout_s;  /* MasqueradeState.idle_timeout */
 } dp_flow_info_t;
 #define DP_FLOW_NONE UINT64_MAX
 

@@ -14,7 +14,10 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <deque>
 #include <map>
+#include <set>
+#include <string>
 #include <memory>
 #include <thread>
 #include <unordered_map>
@@ -1032,6 +1035,459 @@ struct Trie {  // binary trie with LPM (prefix-trie get_lpm semantics)
   }
 };
 
+// ---------------------------------------------------------------------------
+// Masquerade address / port allocator (nat/src/masquerade/apalloc/), with the
+// reference's ownership: an allocated port holds its port block, a block its
+// address, an address its pool (Arc back-references); dropping the last holder
+// releases the tuple (the Drop impls, port_alloc.rs:513-565, alloc.rs:322-326).
+// The deterministic mode (randomize = false): block i covers ports
+// [256 i, 256 i + 255].  A region's offsets are bounded by
+// DP_MASQ_REGION_ADDRS (dpgpu.h), as the reference bounds them by u32.
+// ---------------------------------------------------------------------------
+typedef unsigned __int128 u128;
+
+u128 addr_bits(int fam, const uint8_t *a) {
+  u128 v = 0;
+  for (int i = 0; i < (fam == 4 ? 4 : 16); i++) v = (v << 8) | a[i];
+  return v;
+}
+Ip bits_addr(int fam, u128 v) {
+  Ip r;
+  r.fam = (uint8_t)fam;
+  const int n = fam == 4 ? 4 : 16;
+  for (int i = n - 1; i >= 0; i--) { r.b[i] = (uint8_t)v; v >>= 8; }
+  return r;
+}
+u128 prefix_first(const dp_prefix_t &p) { return addr_bits(p.family, p.addr); }
+u128 prefix_last(const dp_prefix_t &p) {
+  const int w = p.family == 4 ? 32 : 128;
+  const u128 host = p.len >= w ? (u128)0 : (p.len == 0 && w == 128 ? ~(u128)0 : (((u128)1 << (w - p.len)) - 1));
+  return prefix_first(p) | host;
+}
+
+// AllocatorError (nat/src/masquerade/allocation.rs:12-36)
+enum MErr { M_OK = 0, M_NO_FREE_IP, M_NO_PORT_BLOCK, M_NO_FREE_PORT, M_PORT_ALLOC_FAILED,
+            M_PORT_RESERVATION_FAILED, M_INTERNAL, M_DENIED, M_NO_POOL_FOUND };
+bool m_exhaustion(MErr e) { return e == M_NO_FREE_IP || e == M_NO_PORT_BLOCK || e == M_NO_FREE_PORT; }
+// From<&AllocatorError> for DoneReason (allocation.rs:59-73)
+int m_done(MErr e) {
+  switch (e) {
+    case M_NO_FREE_IP: case M_NO_PORT_BLOCK: case M_NO_FREE_PORT: return DP_DONE_NAT_OUT_OF_RESOURCES;
+    case M_PORT_ALLOC_FAILED: case M_PORT_RESERVATION_FAILED: return DP_DONE_NAT_FAILURE;
+    case M_INTERNAL: return DP_DONE_INTERNAL_FAILURE;
+    default: return DP_DONE_FILTERED;  // Denied, NoPoolFound
+  }
+}
+
+struct MClaim {  // a (prefix, port range) of ReservedPorts (reserved.rs:23)
+  dp_prefix_t pfx;
+  uint16_t lo, hi;
+};
+
+// Bitmap256 (port_alloc.rs:749-882)
+struct Bitmap256 {
+  uint64_t w[4] = {0, 0, 0, 0};
+  bool get(int i) const { return (w[i >> 6] >> (i & 63)) & 1; }
+  void set(int i, bool v) { if (v) w[i >> 6] |= 1ull << (i & 63); else w[i >> 6] &= ~(1ull << (i & 63)); }
+  bool full() const { return (w[0] & w[1] & w[2] & w[3]) == ~0ull; }
+  // Bitmap256::for_block: the claims clipped to the block, port 0 if it may not be given out
+  static Bitmap256 for_block(uint16_t base, const std::vector<std::pair<uint16_t, uint16_t>> &claimed,
+                             bool reserve_null) {
+    Bitmap256 b;
+    if (reserve_null && base == 0) b.set(0, true);
+    for (auto &r : claimed) {
+      const int s = std::max<int>(r.first, base), e = std::min<int>(r.second, base | 0xff);
+      for (int p = s; p <= e; p++) b.set(p - base, true);
+    }
+    return b;
+  }
+  // allocate_port_from_bitmap: the lowest free offset (trailing ones of each half)
+  int alloc() {
+    for (int i = 0; i < 256; i++) if (!get(i)) { set(i, true); return i; }
+    return -1;
+  }
+};
+
+struct MPool;
+struct MIp;
+struct MBlock;
+
+// PortAllocator (port_alloc.rs:84-93); one thread: ThreadPortMap is one slot
+struct MPortAlloc {
+  bool free[256];
+  uint16_t usable = 0;
+  size_t cur = 0;                                      // current_alloc_index
+  int thread_block = -1;
+  std::map<size_t, std::weak_ptr<MBlock>> allocated;   // AllocatedPortBlockMap
+  std::vector<std::pair<uint16_t, uint16_t>> reserved; // ReservedForAddr
+  bool excl_wk = false;
+};
+
+// NatPool behind its IpAllocator (alloc.rs:27-30, 336-345)
+struct MPool {
+  int fam = 4;
+  u128 start = 0;
+  uint32_t cap = 0;                         // offsets [0, cap)
+  std::set<uint32_t> free;                  // PoolBitmap
+  std::deque<std::weak_ptr<MIp>> in_use;
+  std::vector<MClaim> claims;               // ReservedPorts of the region
+  bool excl_wk = false;
+};
+
+struct MIp {  // AllocatedIp (alloc.rs:251-255)
+  u128 bits = 0;
+  uint32_t offset = 0;
+  std::shared_ptr<MPool> pool;
+  MPortAlloc pa;
+  ~MIp() { pool->free.insert(offset); }     // Drop: deallocate_from_pool
+};
+
+struct MBlock {  // AllocatedPortBlock (port_alloc.rs:396-401)
+  std::shared_ptr<MIp> ip;
+  uint16_t base = 0;
+  size_t index = 0;
+  Bitmap256 bm;
+  ~MBlock() {  // Drop: deallocate_block (port_alloc.rs:200-212)
+    ip->pa.free[index] = true;
+    ip->pa.usable++;
+  }
+};
+
+struct MPort {  // AllocatedPort (port_alloc.rs:530-533)
+  uint16_t port = 0;
+  bool ident = false;                       // NatPort::Identifier
+  std::shared_ptr<MBlock> blk;
+  ~MPort() { blk->bm.set(port - blk->base, false); }  // Drop: deallocate_port_from_block
+  Ip ip() const { return bits_addr(blk->ip->pool->fam, blk->ip->bits); }
+};
+
+// ReservedPorts::for_addr (reserved.rs:45-70): the claims covering the address
+std::vector<std::pair<uint16_t, uint16_t>> m_reserved_for(const MPool &P, u128 bits) {
+  std::vector<std::pair<uint16_t, uint16_t>> out;
+  const Ip a = bits_addr(P.fam, bits);
+  for (auto &c : P.claims)
+    if (c.pfx.family == P.fam && prefix_covers(c.pfx.addr, c.pfx.len, a.b)) out.push_back({c.lo, c.hi});
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+// AllocatedIp::new -> PortAllocator::new (port_alloc.rs:100-145)
+std::shared_ptr<MIp> m_new_ip(const std::shared_ptr<MPool> &P, uint32_t offset) {
+  auto ip = std::make_shared<MIp>();
+  ip->bits = P->start + offset;
+  ip->offset = offset;
+  ip->pool = P;
+  ip->pa.reserved = m_reserved_for(*P, ip->bits);
+  ip->pa.excl_wk = P->excl_wk;
+  for (int i = 0; i < 256; i++) {
+    const uint16_t base = (uint16_t)(i * 256);
+    const bool wk = P->excl_wk && base < 1024;
+    const bool whole = Bitmap256::for_block(base, ip->pa.reserved, false).full();
+    ip->pa.free[i] = !(wk || whole);
+    if (ip->pa.free[i]) ip->pa.usable++;
+  }
+  return ip;
+}
+
+std::shared_ptr<MBlock> m_block_get(MPortAlloc &pa, size_t idx) {  // AllocatedPortBlockMap::get
+  auto it = pa.allocated.find(idx);
+  if (it == pa.allocated.end()) return nullptr;
+  auto b = it->second.lock();
+  if (!b) pa.allocated.erase(it);
+  return b;
+}
+bool m_has_free_ports(MPortAlloc &pa) {  // PortAllocator::has_free_ports
+  if (pa.usable > 0) return true;
+  for (auto &kv : pa.allocated) {
+    auto b = kv.second.lock();
+    if (b && !b->bm.full()) return true;
+  }
+  return false;
+}
+// AllocatedPortBlock::allocate_port_from_block (port_alloc.rs:449-471)
+MErr m_port_from_block(const std::shared_ptr<MBlock> &b, bool allow_null, std::shared_ptr<MPort> &out) {
+  const int off = b->bm.alloc();
+  if (off < 0) return M_NO_FREE_PORT;
+  const uint16_t port = (uint16_t)(b->base + off);
+  // NatPort::new_port_checked: never 0 (bit 0 of block 0 is preset then)
+  if (!allow_null && port == 0) return M_PORT_ALLOC_FAILED;
+  auto p = std::make_shared<MPort>();
+  p->blk = b;
+  p->port = port;
+  p->ident = allow_null;
+  out = p;
+  return M_OK;
+}
+// PortAllocator::allocate_port (port_alloc.rs:264-284)
+MErr m_allocate_port(const std::shared_ptr<MIp> &ip, bool allow_null, std::shared_ptr<MPort> &out) {
+  MPortAlloc &pa = ip->pa;
+  if (pa.thread_block >= 0) {
+    auto cb = m_block_get(pa, (size_t)pa.thread_block);
+    if (cb && !cb->bm.full()) return m_port_from_block(cb, allow_null, out);
+  }
+  // allocate_block: pick_available_block cycling from current_alloc_index
+  int idx = -1;
+  for (size_t k = 0; k < 256; k++) {
+    const size_t i = (pa.cur + k) % 256;
+    if (pa.free[i]) { pa.free[i] = false; idx = (int)i; break; }
+  }
+  if (idx < 0) return M_NO_PORT_BLOCK;
+  pa.thread_block = idx;
+  pa.cur = (size_t)idx;
+  pa.usable--;
+  auto b = std::make_shared<MBlock>();
+  b->ip = ip;
+  b->index = (size_t)idx;
+  b->base = (uint16_t)(idx * 256);
+  b->bm = Bitmap256::for_block(b->base, pa.reserved, !allow_null);
+  pa.allocated[(size_t)idx] = b;
+  return m_port_from_block(b, allow_null, out);
+}
+// IpAllocator::allocate (alloc.rs:113-127): cleanup, the addresses in use in
+// order, else a new address
+MErr m_pool_allocate(const std::shared_ptr<MPool> &P, bool allow_null, std::shared_ptr<MPort> &out) {
+  // cleanup_used_ips
+  std::deque<std::weak_ptr<MIp>> keep;
+  for (auto &w : P->in_use) if (!w.expired()) keep.push_back(w);
+  P->in_use.swap(keep);
+  // reuse_allocated_ip
+  MErr outcome = M_NO_FREE_IP;
+  {
+    std::vector<std::shared_ptr<MIp>> examined;
+    for (auto &w : P->in_use) {
+      auto ip = w.lock();
+      if (!ip) continue;
+      examined.push_back(ip);
+      if (!m_has_free_ports(ip->pa)) continue;
+      MErr e = m_allocate_port(ip, allow_null, out);
+      if (e == M_OK) return M_OK;
+      if (e == M_NO_FREE_PORT) continue;
+      outcome = e;
+      break;
+    }
+  }
+  if (!m_exhaustion(outcome)) return outcome;
+  // allocate_from_new_ip: the lowest free offset
+  if (P->free.empty()) return M_NO_FREE_IP;
+  const uint32_t off = *P->free.begin();
+  P->free.erase(P->free.begin());
+  auto ip = m_new_ip(P, off);
+  P->in_use.push_back(ip);
+  return m_allocate_port(ip, allow_null, out);
+}
+
+struct MRegion {
+  u128 lo, hi;
+  std::shared_ptr<MPool> pool;
+};
+struct MPoolSet {  // PoolSet (alloc.rs:182-185)
+  std::vector<MRegion> regions;
+  uint64_t idle_ns = 0;
+};
+// PoolSet::allocate (alloc.rs:208-224)
+MErr m_set_allocate(const MPoolSet &S, bool allow_null, std::shared_ptr<MPort> &out) {
+  MErr ex = M_OK;
+  for (auto &r : S.regions) {
+    MErr e = m_pool_allocate(r.pool, allow_null, out);
+    if (e == M_OK) return M_OK;
+    if (m_exhaustion(e)) { ex = e; continue; }
+    return e;
+  }
+  return ex == M_OK ? M_NO_FREE_IP : ex;
+}
+// PoolSet::reserve -> IpAllocator::reserve (alloc.rs:140-147, 227-239,
+// 437-478) -> PortAllocator::reserve_port (port_alloc.rs:353-374)
+MErr m_set_reserve(const MPoolSet &S, const Ip &a, uint16_t port, bool ident, std::shared_ptr<MPort> &out) {
+  const u128 bits = addr_bits(a.fam, a.b);
+  const MRegion *R = nullptr;
+  for (auto &r : S.regions) if (r.lo <= bits && bits <= r.hi) { R = &r; break; }
+  if (!R) return M_NO_POOL_FOUND;
+  const std::shared_ptr<MPool> &P = R->pool;
+  const u128 o = bits - P->start;
+  if (o >= P->cap) return M_NO_POOL_FOUND;  // map_address: not an offset this pool serves
+  std::shared_ptr<MIp> ip;
+  {
+    std::vector<std::shared_ptr<MIp>> examined;
+    for (auto &w : P->in_use) {
+      auto x = w.lock();
+      if (!x) continue;
+      examined.push_back(x);
+      if (x->bits == bits) { ip = x; break; }
+    }
+  }
+  if (!ip) {
+    P->free.erase((uint32_t)o);
+    ip = m_new_ip(P, (uint32_t)o);
+    P->in_use.push_back(ip);
+  }
+  MPortAlloc &pa = ip->pa;
+  if (pa.excl_wk && port < 1024) return M_DENIED;
+  for (auto &r : pa.reserved) if (r.first <= port && port <= r.second) return M_DENIED;
+  // find_block_for_port: the block covering the port, taken if free, else the
+  // live block holding it (the retries change nothing single-threaded)
+  const size_t idx = port >> 8;
+  std::shared_ptr<MBlock> b;
+  if (pa.free[idx]) {
+    pa.free[idx] = false;
+    pa.usable--;
+    b = std::make_shared<MBlock>();
+    b->ip = ip;
+    b->index = idx;
+    b->base = (uint16_t)(idx * 256);
+    b->bm = Bitmap256::for_block(b->base, pa.reserved, !ident);
+    pa.allocated[idx] = b;
+  } else {
+    for (auto &kv : pa.allocated) {
+      auto x = kv.second.lock();
+      if (x && x->base <= port && port - x->base < 256) { b = x; break; }
+    }
+    if (!b) return M_PORT_RESERVATION_FAILED;
+  }
+  if (b->bm.get(port - b->base)) return M_PORT_RESERVATION_FAILED;  // already handed out
+  b->bm.set(port - b->base, true);
+  auto p = std::make_shared<MPort>();
+  p->blk = b;
+  p->port = port;
+  p->ident = ident;
+  out = p;
+  return M_OK;
+}
+
+// A masquerade expose as the tables hold it (dp_masq_expose_t)
+struct MExpose {
+  uint32_t src_vni, dst_vni;
+  uint64_t idle_ns;
+  int fam;
+  std::vector<dp_prefix_t> priv, pub;
+  std::vector<dp_masq_claim_t> claims;
+};
+
+// PoolTableKey (apalloc/mod.rs:111-117) and its table
+struct MPoolKey {
+  uint8_t proto;
+  uint32_t src, dst;
+  u128 lo, hi;
+  bool operator<(const MPoolKey &o) const {
+    if (proto != o.proto) return proto < o.proto;
+    if (src != o.src) return src < o.src;
+    if (dst != o.dst) return dst < o.dst;
+    if (lo != o.lo) return lo < o.lo;
+    return hi < o.hi;
+  }
+};
+
+// NatAllocator (apalloc/mod.rs:248-253)
+struct MAlloc {
+  std::string config;  // MasqueradeConfig, as its canonical bytes
+  uint64_t tag = 0;
+  int64_t genid = 0;
+  std::vector<MExpose> exposes;
+  std::map<MPoolKey, MPoolSet> pools[2];  // [0] src44, [1] src66
+
+  // PoolTable::get (apalloc/mod.rs:155-180): of the entries of this protocol
+  // and pair of VPCs covering the address, the one starting nearest to it,
+  // then the narrowest
+  const MPoolSet *lookup(int fam, uint8_t proto, uint32_t src, uint32_t dst, u128 a) const {
+    const MPoolSet *best = nullptr;
+    u128 bl = 0, bh = 0;
+    for (auto &kv : pools[fam == 4 ? 0 : 1]) {
+      const MPoolKey &k = kv.first;
+      if (k.proto != proto || k.src != src || k.dst != dst || !(k.lo <= a && a <= k.hi)) continue;
+      if (!best || k.lo > bl || (k.lo == bl && k.hi < bh)) { best = &kv.second; bl = k.lo; bh = k.hi; }
+    }
+    return best;
+  }
+};
+
+// decompose + regions_by_owner (apalloc/region.rs:43-130): the public space
+// of the exposes cut into disjoint regions with constant owners; per owner its
+// regions, fewest sharers first, then widest, then by address
+struct MRegionSpec {
+  u128 lo, hi;
+  std::vector<size_t> owners;
+};
+std::vector<MRegionSpec> m_decompose(const std::vector<std::vector<std::pair<u128, u128>>> &own) {
+  std::set<u128> cuts;
+  for (auto &rs : own)
+    for (auto &r : rs) {
+      cuts.insert(r.first);
+      if (r.second != ~(u128)0) cuts.insert(r.second + 1);
+    }
+  std::vector<u128> c(cuts.begin(), cuts.end());
+  std::vector<MRegionSpec> out;
+  for (size_t i = 0; i < c.size(); i++) {
+    const u128 s = c[i], e = i + 1 < c.size() ? c[i + 1] - 1 : ~(u128)0;
+    std::vector<size_t> owners;
+    for (size_t o = 0; o < own.size(); o++)
+      for (auto &r : own[o]) if (r.first <= s && s <= r.second) { owners.push_back(o); break; }
+    if (owners.empty()) continue;
+    if (!out.empty() && out.back().hi + 1 == s && out.back().owners == owners) out.back().hi = e;
+    else out.push_back(MRegionSpec{s, e, owners});
+  }
+  return out;
+}
+
+// NatAllocator::new -> build_pools_generic (apalloc/setup.rs:158-204)
+std::shared_ptr<MAlloc> m_build(const std::vector<MExpose> &ex, const std::string &cfg, uint64_t tag,
+                                int64_t genid) {
+  auto A = std::make_shared<MAlloc>();
+  A->config = cfg;
+  A->tag = tag;
+  A->genid = genid;
+  A->exposes = ex;
+  for (int fam : {4, 6}) {
+    std::map<uint32_t, std::vector<const MExpose *>> groups;  // by destination VPC
+    for (auto &e : ex) if (e.fam == fam) groups[e.dst_vni].push_back(&e);
+    for (auto &g : groups) {
+      for (uint8_t proto : {(uint8_t)6, (uint8_t)17, (uint8_t)(fam == 4 ? 1 : 58)}) {
+        std::vector<std::vector<std::pair<u128, u128>>> own;
+        for (auto *e : g.second) {
+          std::vector<std::pair<u128, u128>> rs;
+          for (auto &p : e->pub) rs.push_back({prefix_first(p), prefix_last(p)});
+          own.push_back(rs);
+        }
+        const auto regions = m_decompose(own);
+        std::vector<std::shared_ptr<MPool>> pools;
+        for (auto &R : regions) {
+          auto P = std::make_shared<MPool>();
+          P->fam = fam;
+          P->start = R.lo;
+          const u128 span = R.hi - R.lo;  // len - 1
+          P->cap = span >= DP_MASQ_REGION_ADDRS - 1 ? DP_MASQ_REGION_ADDRS : (uint32_t)span + 1;
+          for (uint32_t o = 0; o < P->cap; o++) P->free.insert(o);
+          P->excl_wk = proto == 6 || proto == 17;
+          // claims_for: the claims of every owner, for this protocol (TCP / UDP only)
+          const uint32_t bit = proto == 6 ? DP_MASQ_TCP : proto == 17 ? DP_MASQ_UDP : 0;
+          for (size_t o : R.owners)
+            for (auto &c : g.second[o]->claims)
+              if (c.protos & bit) P->claims.push_back(MClaim{c.prefix, c.lo, c.hi});
+          pools.push_back(P);
+        }
+        for (size_t o = 0; o < g.second.size(); o++) {
+          std::vector<size_t> mine;
+          for (size_t r = 0; r < regions.size(); r++)
+            if (std::find(regions[r].owners.begin(), regions[r].owners.end(), o) != regions[r].owners.end())
+              mine.push_back(r);
+          std::stable_sort(mine.begin(), mine.end(), [&](size_t a, size_t b) {
+            const auto &x = regions[a], &y = regions[b];
+            if (x.owners.size() != y.owners.size()) return x.owners.size() < y.owners.size();
+            const u128 lx = x.hi - x.lo, ly = y.hi - y.lo;
+            if (lx != ly) return lx > ly;
+            return x.lo < y.lo;
+          });
+          MPoolSet S;
+          S.idle_ns = g.second[o]->idle_ns;
+          for (size_t r : mine) S.regions.push_back(MRegion{regions[r].lo, regions[r].hi, pools[r]});
+          const MExpose *e = g.second[o];
+          for (auto &p : e->priv)  // add_pool_entries: a later expose's entry replaces
+            A->pools[fam == 4 ? 0 : 1][MPoolKey{proto, e->src_vni, g.first, prefix_first(p), prefix_last(p)}] = S;
+        }
+      }
+    }
+  }
+  return A;
+}
+
 struct Fib {
   dp_fib_t d;
   Trie v4, v6;
@@ -1087,6 +1543,11 @@ struct dpo_tables {
   std::map<std::pair<uint32_t, uint32_t>, NatTable> nat_src;     // (src_vni, dst_vni)
   std::vector<PfRule> pf;   // PortFwTable entries (ids stable across generations)
   uint32_t pf_next_id = 1;  // the lineage's next entry id
+  // MasqueradeConfig: the masquerade exposes, their canonical bytes, the tag
+  std::vector<MExpose> masq;
+  std::string masq_cfg;
+  uint64_t masq_tag = 0;
+  uint64_t serial = 0;      // this build (a flow table syncs its allocator once per build)
 };
 
 namespace {
@@ -1107,6 +1568,17 @@ struct OFlow {
   Ip pf_ip;
   uint16_t pf_port = 0;
   uint32_t pf_rule = 0;
+  // MasqueradeState (nat/src/masquerade/state.rs:13-20): action, use_ip /
+  // use_port (NatPort: a port, or an ICMP identifier), idle timeout, the
+  // NatFlowStatus cell shared with the related flow, and the allocation the
+  // SrcNat flow owns
+  uint8_t masq = DP_PF_NONE;
+  int64_t m_status = -1;
+  Ip m_ip;
+  uint16_t m_port = 0;
+  bool m_ident = false;
+  uint64_t m_idle_ns = 0;
+  std::shared_ptr<MPort> m_alloc;
 };
 }  // namespace
 
@@ -1117,6 +1589,16 @@ struct dpo_flows {
   uint64_t capacity = 10000000;                         // FlowTable::DEFAULT_CAPACITY
   std::vector<uint8_t> nfs;                             // AtomicNatFlowStatus cells
   uint64_t now = 0;                                     // Instant::now() (ns, DP_OPT_CLOCK)
+  // NatAllocatorWriter's slot (nat/src/masquerade/allocator_writer.rs:95):
+  // the allocator masquerade flows of this table draw from, and the tables
+  // build it reflects
+  std::shared_ptr<MAlloc> alloc;
+  uint64_t synced = 0;
+  // flows that left the table during the running burst: their allocations are
+  // released when the burst ends (a detached FlowInfo lives on in its timer
+  // task until the runtime polls it, table.rs:161-213)
+  bool in_burst = false;
+  std::vector<int64_t> departed;
 };
 
 namespace {
@@ -1493,6 +1975,12 @@ void flow_invalidate(dpo_flows *FL, int64_t r) {  // FlowInfo::invalidate (flow_
   if (FL && r >= 0) FL->f[r].status = DP_FLOW_CANCELLED;
 }
 bool flow_alive(const dpo_flows *FL, int64_t r) { return r >= 0 && FL->f[r].in_table; }
+// A flow left the table: its FlowInfo (and the allocation its masquerade
+// state owns) is dropped now, or when the running burst ends.
+void flow_depart(dpo_flows *FL, int64_t r) {
+  if (FL->in_burst) FL->departed.push_back(r);
+  else FL->f[r].m_alloc.reset();
+}
 void flow_invalidate_pair(dpo_flows *FL, int64_t r) {  // invalidate_pair (flow_info.rs:449-455)
   if (!FL || r < 0) return;
   flow_invalidate(FL, r);
@@ -1546,6 +2034,7 @@ struct FlowSummary {
   int64_t genid = 0;
   uint32_t dst_vni = 0;
   bool needs_pf = false;
+  bool needs_masq = false;
 };
 
 // FlowFilter (flow-filter/src/lib.rs:75-246, context/tables.rs:800-915), in
@@ -1554,6 +2043,7 @@ struct FlowSummary {
 struct FfWork {
   bool lookup = false;
   uint8_t gate = 0;  // SourceGate of the local lookup (1: PortFwdReply)
+  uint32_t gate_vni = 0;  // LookupInput.dst_vpcd: the GateVni of the remote lookup
   FlowSummary fs;
   int64_t ri = -1, li = -1;  // remote / local rule (-1: miss)
 };
@@ -1562,20 +2052,24 @@ void ff_classify(const dpo_tables &T, const dpo_flows *FL, Packet &p, FfWork &w)
   if (p.is_done() || !p.overlay() || p.m.dst_vni) return;
   if (FL && p.flow >= 0) {
     const OFlow &f = FL->f[p.flow];
-    w.fs = FlowSummary{true, f.d.genid, f.d.dst_vni, f.pf != DP_PF_NONE};
+    w.fs = FlowSummary{true, f.d.genid, f.d.dst_vni, f.pf != DP_PF_NONE, f.masq != DP_PF_NONE};
     // dst_vpcd_from_valid_flow (lib.rs:327-349) -> tag_for_bypass (:213-231)
     if (f.status == DP_FLOW_ACTIVE && f.d.genid >= T.genid) {
       p.m.dst_vni = f.d.dst_vni;
+      if (w.fs.needs_masq) p.m.flags |= DP_META_REQ_MASQUERADE;
       if (w.fs.needs_pf) p.m.flags |= DP_META_REQ_PORT_FORWARDING;
       if (f.d.flags & DP_FLOW_REQ_STATIC_NAT_SRC) p.m.flags |= DP_META_REQ_STATIC_NAT_SRC;
       if (f.d.flags & DP_FLOW_REQ_STATIC_NAT_DST) p.m.flags |= DP_META_REQ_STATIC_NAT_DST;
       return;
     }
-    // flow_revalidation_data (:296-325): the reply flow of a port-forwarded
-    // pair is revalidated against the local rules gated on PortFwdReply
-    if (f.status == DP_FLOW_ACTIVE && f.d.genid < T.genid && !(f.d.flags & DP_FLOW_INITIATOR) &&
-        w.fs.needs_pf)
-      w.gate = 1;
+    // flow_revalidation_data (:296-325): the reply flow of a masqueraded
+    // pair is revalidated against the remote rules gated on its destination
+    // VPC, that of a port-forwarded pair against the local rules gated on
+    // PortFwdReply
+    if (f.status == DP_FLOW_ACTIVE && f.d.genid < T.genid && !(f.d.flags & DP_FLOW_INITIATOR)) {
+      if (w.fs.needs_masq) w.gate_vni = f.d.dst_vni;
+      else if (w.fs.needs_pf) w.gate = 1;
+    }
   }
   if (p.h.net == 0) { p.done(DP_DONE_NOT_IP); return; }
   if (!p.m.src_vni) { p.done(DP_DONE_UNROUTABLE); return; }
@@ -1589,7 +2083,7 @@ void ff_classify(const dpo_tables &T, const dpo_flows *FL, Packet &p, FfWork &w)
   const auto &rem = p.h.net == 4 ? T.ffr4 : T.ffr6;
   const auto &loc = p.h.net == 4 ? T.ffl4 : T.ffl6;
   static const uint8_t zero16[16] = {0};
-  Key k{proto, p.m.src_vni, 0 /* GateVni: dst_vpcd None */, 0, zero16, dst, 0, dpp};
+  Key k{proto, p.m.src_vni, w.gate_vni /* GateVni: 0 = dst_vpcd None */, 0, zero16, dst, 0, dpp};
   w.ri = classify(rem, k, p.h.net);
   if (w.ri < 0) return;  // DestinationMiss
   Key k2{proto, p.m.src_vni, rem[w.ri].r.action, w.gate, src, zero16, sp, 0};
@@ -1625,7 +2119,7 @@ void ff_apply(const dpo_tables &T, dpo_flows *FL, Packet &p, const FfWork &w) {
   // of its stateful NAT is still required
   if (w.fs.present && w.fs.genid != T.genid) {
     const bool pf = p.m.flags & DP_META_REQ_PORT_FORWARDING, masq = p.m.flags & DP_META_REQ_MASQUERADE;
-    if (w.fs.dst_vni != p.m.dst_vni || masq || pf != w.fs.needs_pf || !pf)
+    if (w.fs.dst_vni != p.m.dst_vni || masq != w.fs.needs_masq || pf != w.fs.needs_pf || (!pf && !masq))
       flow_invalidate_pair(FL, p.flow);
   }
 }
@@ -2082,6 +2576,275 @@ void stage_portfw(const dpo_tables &T, dpo_flows *FL, Packet &p) {
   pf_create(T, FL, p, *e, dst, dpp, na, np);
 }
 
+// ---------------------------------------------------------------------------
+// Masquerade (nat/src/masquerade/nf.rs)
+// ---------------------------------------------------------------------------
+const uint64_t kMasqOneWayNs = 5000000000ull;   // MASQUERADE_ONEWAY_TIMEOUT (nf.rs:86)
+const uint64_t kMasqTwoWayNs = 3000000000ull;   // MASQUERADE_TWOWAY_TIMEOUT (:87)
+const uint64_t kMasqClosingNs = 2000000000ull;  // MASQUERADE_CLOSING_TIMEOUT (:88)
+
+// masquerade (packet.rs:35-195): the snat / dnat of a state -- the address,
+// and a TCP / UDP port (always, NatPort::Port) or an ICMP query identifier
+// (when it changes).  false: the error (UnusableAddress, UnsupportedTraffic,
+// a header of the other family).
+bool masq_xlate(Packet &p, uint8_t action, const Ip &a, uint16_t port, bool ident) {
+  const bool src = action == DP_PF_SRC_NAT;
+  if (src && !ip_unicast(a)) return false;  // UnicastIpAddr::try_from
+  if (!p.h.has_eth || p.h.net == 0) return false;
+  bool mod = false;
+  auto set_addr = [&]() -> bool {
+    if (a.fam != p.h.net) return false;  // NetError
+    const Ip cur = src ? pkt_src(p) : pkt_dst(p);
+    if (!(cur == a)) { set_ip(p, src, a); mod = true; }
+    return true;
+  };
+  if (p.h.l4 == L4_TCP || p.h.l4 == L4_UDP) {
+    if (!set_addr()) return false;
+    if (!ident) {
+      uint16_t *pp = p.h.l4 == L4_TCP ? (src ? &p.h.tcp.sport : &p.h.tcp.dport)
+                                      : (src ? &p.h.udp.sport : &p.h.udp.dport);
+      *pp = port;
+      mod = true;
+    }
+  } else if (p.h.l4 == L4_ICMP4 || p.h.l4 == L4_ICMP6) {
+    if (!set_addr()) return false;
+    uint16_t cur;
+    if (ident && icmp_full_identifier(p.h.icmp, p.h.l4 == L4_ICMP6, cur) && cur != port) {
+      put16(p.h.icmp.raw + 4, port);
+      mod = true;
+    }
+  } else {
+    return false;
+  }
+  if (mod) p.m.flags |= DP_META_REFR_CHKSUM | (src ? DP_META_NATTED_SRC : DP_META_NATTED_DST);
+  return true;
+}
+
+// next_flow_status (masquerade/protocol.rs:93-116) on the IP header's next
+// header: TCP by its flags, UDP (a DstNat reply from port 53 / 853 / 8853
+// closes), ICMP
+uint8_t masq_next_status(const Packet &p, uint8_t action, uint8_t st) {
+  const uint8_t proto = pkt_proto(p);
+  const bool snat = action == DP_PF_SRC_NAT;
+  if (proto == 17) {
+    uint8_t n = st;
+    if (snat) { if (st == DP_NFS_TWO_WAY) n = DP_NFS_ESTABLISHED; }
+    else if (st == DP_NFS_ONE_WAY) n = DP_NFS_TWO_WAY;
+    if (!snat && p.h.has_eth && p.h.l4 == L4_UDP) {
+      const uint16_t sp = p.h.udp.sport;
+      if (sp == 53 || sp == 853 || sp == 8853) n = DP_NFS_CLOSED;
+    }
+    return n;
+  }
+  if (proto == 1 || proto == 58) return (!snat && st == DP_NFS_ONE_WAY) ? (uint8_t)DP_NFS_TWO_WAY : st;
+  if (proto == 6 && p.h.l4 == L4_TCP)
+    // the same machine as port forwarding's, the initiator's side being SrcNat here
+    return pf_next_status(p, snat ? (uint8_t)DP_PF_DST_NAT : (uint8_t)DP_PF_SRC_NAT, st);
+  return st;
+}
+
+// refresh_masquerade_state (nf.rs:151-194)
+void masq_refresh(dpo_flows *FL, Packet &p, int64_t fi) {
+  OFlow &f = FL->f[fi];
+  uint8_t &st = FL->nfs[f.m_status];
+  const uint8_t cur = st, nw = masq_next_status(p, f.masq, cur);
+  st = nw;
+  uint64_t ext = 0;
+  switch (nw) {
+    case DP_NFS_TWO_WAY: ext = kMasqTwoWayNs; break;
+    case DP_NFS_ESTABLISHED: ext = f.m_idle_ns; break;
+    case DP_NFS_CLOSED: case DP_NFS_RESET: flow_invalidate_pair(FL, fi); return;
+    case DP_NFS_ONE_WAY: return;
+    default: ext = kMasqClosingNs; break;
+  }
+  reset_expiry(f, FL->now, ext);
+  if (cur != nw && nw == DP_NFS_ESTABLISHED && flow_alive(FL, f.related))
+    reset_expiry(FL->f[f.related], FL->now, ext);
+}
+
+uint8_t key_proto(const FKey &k) {  // FlowKey::proto (flow_key.rs:536-548)
+  if (k.kind == DP_FLOW_TCP) return 6;
+  if (k.kind == DP_FLOW_UDP) return 17;
+  return k.fam == 4 ? 1 : 58;
+}
+Ip key_src(const FKey &k) { Ip a; a.fam = k.fam; memcpy(a.b, k.src, 16); if (k.fam == 4) memset(a.b + 4, 0, 12); return a; }
+
+// Masquerade::masquerade_packet (nf.rs:384-475); returns the DoneReason of the
+// error (MasqueradeError -> DoneReason, nf.rs:547-568) or -1
+int masq_packet(const dpo_tables &T, dpo_flows *FL, Packet &p) {
+  // get_masquerade_state (nf.rs:198-213): an Active flow with masquerade state
+  if (p.flow >= 0 && FL->f[p.flow].status == DP_FLOW_ACTIVE && FL->f[p.flow].masq != DP_PF_NONE) {
+    OFlow &f = FL->f[p.flow];
+    const uint8_t act = f.masq;
+    const Ip ip = f.m_ip;
+    const uint16_t port = f.m_port;
+    const bool ident = f.m_ident;
+    masq_refresh(FL, p, p.flow);
+    return masq_xlate(p, act, ip, port, ident) ? -1 : DP_DONE_NAT_FAILURE;
+  }
+  const std::shared_ptr<MAlloc> A = FL->alloc;
+  if (!A) return DP_DONE_NAT_FAILURE;  // NoAllocator
+  if (p.h.l4 == L4_TCP) {  // "TCP without SYN": Tcp::is_first_segment
+    const uint8_t fl = p.h.tcp.flags;
+    if (!((fl & 0x02) && !(fl & 0x3d))) return DP_DONE_FILTERED;
+  }
+  FKey cur;
+  if (!packet_flow_key(p, cur)) return DP_DONE_MALFORMED;  // FlowKeyError
+  const FKey init = p.has_ikey ? p.ikey : cur;
+  const uint8_t proto = key_proto(init);
+  // NatAllocator::allocate (apalloc/mod.rs:317-375)
+  const Ip sip = key_src(init);
+  const MPoolSet *S = A->lookup(init.fam, proto, p.m.src_vni, p.m.dst_vni, addr_bits(init.fam, sip.b));
+  if (!S) return DP_DONE_FILTERED;  // Denied
+  std::shared_ptr<MPort> alloc;
+  const MErr e = m_set_allocate(*S, proto == 1 || proto == 58, alloc);
+  if (e != M_OK) return m_done(e);
+  const Ip aip = alloc->ip();
+  if (!ip_unicast(aip)) return DP_DONE_FILTERED;  // Bug("allocated unusable ip"); the allocation drops here
+  // create_flow_pair (nf.rs:265-325): the reverse key from the current key
+  // (new_reverse_session, :327-373), the original source (get_reverse_mapping)
+  FKey rk;
+  rk.vni = p.m.dst_vni;
+  rk.fam = cur.fam;
+  rk.kind = cur.kind;
+  memcpy(rk.src, cur.dst, 16);
+  memcpy(rk.dst, aip.b, 16);
+  if (aip.fam == 4) memset(rk.dst + 4, 0, 12);
+  if (cur.kind == DP_FLOW_TCP || cur.kind == DP_FLOW_UDP) {
+    if (alloc->port == 0) return DP_DONE_MALFORMED;  // InvalidPort
+    rk.sp = cur.dp;
+    rk.dp = alloc->port;
+  } else if (cur.kind == DP_FLOW_ICMP_QUERY) {
+    rk.sp = alloc->port;
+    rk.dp = 0;
+  } else {
+    return DP_DONE_NAT_FAILURE;  // UnexpectedKeyVariant
+  }
+  uint16_t rport;
+  bool rident;
+  if (init.kind == DP_FLOW_TCP || init.kind == DP_FLOW_UDP) { rport = init.sp; rident = false; }
+  else if (init.kind == DP_FLOW_ICMP_QUERY) { rport = init.sp; rident = true; }
+  else return DP_DONE_NAT_FAILURE;  // IcmpUnsupportedCategory
+  if (init == rk) return DP_DONE_INTERNAL_FAILURE;  // related_pair: FlowInfoError
+  dp_flow_t fd{}, rd{};
+  auto to_key = [](const FKey &k, dp_flow_key_t &x) {
+    x.src_vni = k.vni; x.family = k.fam; x.kind = k.kind; x.sport = k.sp; x.dport = k.dp;
+    memcpy(x.src, k.src, 16); memcpy(x.dst, k.dst, 16);
+  };
+  to_key(init, fd.key);
+  to_key(rk, rd.key);
+  fd.flags = DP_FLOW_INITIATOR;
+  if (p.m.flags & DP_META_REQ_STATIC_NAT_SRC) { fd.flags |= DP_FLOW_REQ_STATIC_NAT_SRC; rd.flags |= DP_FLOW_REQ_STATIC_NAT_DST; }
+  if (p.m.flags & DP_META_REQ_STATIC_NAT_DST) { fd.flags |= DP_FLOW_REQ_STATIC_NAT_DST; rd.flags |= DP_FLOW_REQ_STATIC_NAT_SRC; }
+  fd.dst_vni = p.m.dst_vni;   // setup_flow_masquerade_state: the forward flow goes to dst_vpcd,
+  rd.dst_vni = p.m.src_vni;   // the reverse one to src_vpcd
+  fd.genid = rd.genid = A->genid;  // set_genid_pair(allocator.genid())
+  fd.expires_at = rd.expires_at = FL->now + kMasqOneWayNs;
+  const int64_t cell = (int64_t)FL->nfs.size();
+  FL->nfs.push_back(DP_NFS_ONE_WAY);
+  int64_t rf, rr;
+  if (flow_insert_one(FL, fd, -1, rf) < 0) return DP_DONE_FLOW_CAPACITY_EXCEEDED;  // the allocation drops here
+  OFlow *F = &FL->f[rf];
+  F->masq = DP_PF_SRC_NAT; F->m_status = cell; F->m_ip = aip; F->m_port = alloc->port;
+  F->m_ident = alloc->ident; F->m_idle_ns = S->idle_ns; F->m_alloc = alloc;
+  if (flow_insert_one(FL, rd, rf, rr) < 0) {  // admitted at capacity: its related flow is Active
+    flow_invalidate(FL, rf);
+    return DP_DONE_FLOW_CAPACITY_EXCEEDED;
+  }
+  OFlow &R = FL->f[rr];
+  R.masq = DP_PF_DST_NAT; R.m_status = cell; R.m_ip = sip; R.m_port = rport; R.m_ident = rident;
+  R.m_idle_ns = S->idle_ns;
+  FL->f[rf].related = rr;
+  R.related = rf;
+  // the packet with the forward state; a failure invalidates the new pair
+  if (!masq_xlate(p, DP_PF_SRC_NAT, aip, alloc->port, alloc->ident)) {
+    flow_invalidate_pair(FL, rf);
+    return DP_DONE_NAT_FAILURE;
+  }
+  return -1;  // recheck_flow: the allocator cannot change within a burst
+}
+
+// Masquerade::process (nf.rs:511-586)
+void stage_masquerade(const dpo_tables &T, dpo_flows *FL, Packet &p) {
+  if (p.is_done() || !(p.m.flags & DP_META_REQ_MASQUERADE) || icmp_is_error_msg(p.h)) return;
+  if (!FL) { p.done(DP_DONE_INTERNAL_FAILURE); return; }  // its Arc<FlowTable> is not optional
+  if (!p.m.src_vni || !p.m.dst_vni) { p.done(DP_DONE_UNROUTABLE); return; }
+  if (p.h.net == 0) { p.done(DP_DONE_NOT_IP); return; }
+  const int r = masq_packet(T, FL, p);
+  if (r >= 0) p.done(r);
+  else p.m.flags |= DP_META_REFR_CHKSUM;
+}
+
+// check_masquerading_flow (masquerade/flows.rs:94-174) for the flows of the
+// table, then the allocator installed (update_nat_allocator,
+// allocator_writer.rs:120-154).  The reference visits the flows in its
+// DashMap's order; the restatement (and the GPU) re-reserve the carried
+// allocations in ascending (address, port) order.
+void masq_sync(const dpo_tables &T, dpo_flows *FL) {
+  if (FL->synced == T.serial) return;
+  FL->synced = T.serial;
+  const std::shared_ptr<MAlloc> cur = FL->alloc;
+  const bool same = cur && (cur->tag || T.masq_tag ? cur->tag == T.masq_tag && T.masq_tag != 0
+                                                   : cur->config == T.masq_cfg);
+  if (same) {  // upgrade_all_masquerading_flows (flows.rs:30-44)
+    cur->genid = T.genid;
+    for (auto &kv : FL->map) {
+      OFlow &f = FL->f[kv.second];
+      if (f.status == DP_FLOW_ACTIVE && f.masq != DP_PF_NONE) f.d.genid = T.genid;
+    }
+    return;
+  }
+  if (T.masq.empty()) {  // invalidate_masquerade_flows (flows.rs:19-27)
+    if (cur) {
+      FL->alloc.reset();
+      for (auto &kv : FL->map)
+        if (FL->f[kv.second].masq != DP_PF_NONE) flow_invalidate_pair(FL, (int64_t)kv.second);
+    }
+    return;
+  }
+  auto A = m_build(T.masq, T.masq_cfg, T.masq_tag, T.genid);
+  std::vector<int64_t> fwd;
+  for (auto &kv : FL->map) {
+    const OFlow &f = FL->f[kv.second];
+    if (f.status == DP_FLOW_ACTIVE && f.masq != DP_PF_NONE && f.d.genid != A->genid && f.m_alloc)
+      fwd.push_back((int64_t)kv.second);
+  }
+  std::sort(fwd.begin(), fwd.end(), [&](int64_t a, int64_t b) {
+    const OFlow &x = FL->f[a], &y = FL->f[b];
+    const int c = memcmp(x.m_ip.b, y.m_ip.b, 16);
+    if (c) return c < 0;
+    return x.m_port < y.m_port;
+  });
+  for (int64_t fi : fwd) {
+    OFlow &f = FL->f[fi];
+    if (f.status != DP_FLOW_ACTIVE) continue;  // invalidated with an earlier flow of its pair
+    const Ip &ip = f.m_ip;
+    const Ip src = key_src(f.key);
+    // find_masquerade_peering + the expose checks
+    bool peering = false, ip_ok = false, compatible = false;
+    for (auto &e : T.masq) {
+      if (e.src_vni != f.key.vni || e.dst_vni != f.d.dst_vni) continue;
+      peering = true;
+      bool pub = false;
+      for (auto &q : e.pub) pub |= q.family == ip.fam && prefix_covers(q.addr, q.len, ip.b);
+      if (!pub) continue;
+      ip_ok = true;
+      bool pri = false;
+      for (auto &q : e.priv) pri |= q.family == src.fam && prefix_covers(q.addr, q.len, src.b);
+      if (pri) { compatible = true; break; }
+    }
+    if (!peering || !ip_ok || !compatible) { flow_invalidate_pair(FL, fi); continue; }
+    // re_reserve_ip_and_port -> NatAllocator::reserve_port (apalloc/mod.rs:425-449)
+    const MPoolSet *S = A->lookup(f.key.fam, key_proto(f.key), f.key.vni, f.d.dst_vni, addr_bits(src.fam, src.b));
+    std::shared_ptr<MPort> np;
+    if (!S || m_set_reserve(*S, ip, f.m_port, f.m_ident, np) != M_OK) { flow_invalidate_pair(FL, fi); continue; }
+    f.m_alloc = np;  // the allocation from the replaced allocator drops
+    f.d.genid = A->genid;  // set_genid_pair
+    if (flow_alive(FL, f.related)) FL->f[f.related].d.genid = A->genid;
+  }
+  FL->alloc = A;
+}
+
 // IcmpErrorHandler (nat/src/icmp_handler/nf.rs:61-194) with an empty flow
 // table: an overlay ICMP error message must carry an embedded IP header and
 // transport (IcmpErrorPacket::new, net/src/packet/icmp_err.rs:37-53), valid
@@ -2132,6 +2895,45 @@ void stage_icmp_error(const dpo_tables &T, dpo_flows *FL, Packet &p) {
   const OFlow &f = FL->f[r];
   if (f.status != DP_FLOW_ACTIVE) { p.done(DP_DONE_FILTERED); return; }  // nf.rs:126-130
   p.m.dst_vni = f.d.dst_vni;  // nf.rs:139-140
+  if (f.masq != DP_PF_NONE) {
+    // handle_icmp_error_masquerading (masquerade/icmp_handling.rs:16-48):
+    // the embedded packet by reverse_translation_data (state.rs:89-98: SrcNat
+    // its destination, DstNat its source, with the port or ICMP identifier),
+    // then the error itself by the state; any failure is InternalFailure
+    Emb &em = p.h.emb;
+    const Ip &a = f.m_ip;
+    const bool src = f.masq == DP_PF_DST_NAT;
+    if (em.net != a.fam || (src && !ip_unicast(a))) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+    uint8_t *q = em.net == 4 ? (src ? em.v4.src : em.v4.dst) : (src ? em.v6.src : em.v6.dst);
+    memcpy(q, a.b, a.fam == 4 ? 4 : 16);
+    uint16_t old;
+    if (emb_port(em, src, old)) {
+      if (f.m_port == 0) { p.done(DP_DONE_INTERNAL_FAILURE); return; }  // InvalidPort
+      if (old != f.m_port) emb_set_port(em, src, f.m_port);
+    } else if (src && (em.tk == L4_ICMP4 || em.tk == L4_ICMP6)) {
+      // translate_inner_icmp (icmp_error_msg.rs:149-173): the identifier, if
+      // the embedded message has one (its checksum is left as it was)
+      const bool v6 = em.tk == L4_ICMP6;
+      uint16_t id;
+      bool has;
+      if (em.full) has = icmp_full_identifier(em.icmp, v6, id);
+      else {
+        const uint8_t t = em.part[0];
+        has = (v6 ? (t == 128 || t == 129) : (t == 0 || t == 8 || t == 13 || t == 14)) && em.part.size() >= 6;
+        if (has) id = be16(em.part.data() + 4);
+      }
+      if (has && id != f.m_port) {
+        if (em.full) put16(em.icmp.raw + 4, f.m_port);
+        else put16(em.part.data() + 4, f.m_port);
+      }
+    }
+    if (!masq_xlate(p, f.masq, a, f.m_port, f.m_ident)) { p.done(DP_DONE_INTERNAL_FAILURE); return; }
+    const uint8_t t = p.h.icmp.raw[0], c = p.h.icmp.raw[1];
+    const bool unrec = p.h.l4 == L4_ICMP4 ? (t == 3 && c != 4) : t == 1;
+    if (unrec && FL->nfs[f.m_status] == DP_NFS_ONE_WAY) flow_invalidate_pair(FL, r);
+    p.m.flags |= DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST;
+    return;
+  }
   // no NAT state to translate with (nf.rs:143-152)
   if (f.pf == DP_PF_NONE) { p.done(DP_DONE_FILTERED); return; }
   // handle_icmp_error_port_forwarding (portfw/icmp_handling.rs:51-90): the
@@ -2261,8 +3063,7 @@ void process_post(const dpo_tables &T, dpo_flows *FL, Packet &p, dp_pkt_out_t &o
   stage_acl(T, FL, p);
   stage_static_nat(T, p);
   stage_portfw(T, FL, p);
-  // Masquerade: masquerade exposes are refused at publish
-  if (!p.is_done() && (p.m.flags & DP_META_REQ_MASQUERADE)) p.done(DP_DONE_INTERNAL_FAILURE);
+  stage_masquerade(T, FL, p);
   stage_ipforward(T, p);  // IP-Forward-2
   stage_egress(T, p);
   if (p.m.done == DP_DONE_DELIVERED) serialize(p);
@@ -2308,6 +3109,8 @@ void process_one(const dpo_tables &T, uint8_t *buf, const dp_pkt_in_t &in, dp_pk
 // 352-363), then the lazy stages after it packet by packet.
 void process_burst_flows(const dpo_tables &T, dpo_flows *FL, uint8_t *buf, const dp_pkt_in_t *in,
                          dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n) {
+  masq_sync(T, FL);
+  FL->in_burst = true;
   std::vector<Packet> P(n);
   std::vector<char> live(n);
   std::vector<FfWork> W(n);
@@ -2316,6 +3119,10 @@ void process_burst_flows(const dpo_tables &T, dpo_flows *FL, uint8_t *buf, const
   for (uint32_t i = 0; i < n; i++) if (live[i]) ff_apply(T, FL, P[i], W[i]);
   for (uint32_t i = 0; i < n; i++)
     if (live[i]) process_post(T, FL, P[i], out[i], meta[i]);
+  // the flows replaced during the burst are dropped after it
+  FL->in_burst = false;
+  for (int64_t r : FL->departed) FL->f[r].m_alloc.reset();
+  FL->departed.clear();
 }
 
 FKey fkey_of(const dp_flow_key_t &x) {
@@ -2358,6 +3165,7 @@ int32_t flow_insert_one(dpo_flows *FL, const dp_flow_t &d, int64_t partner, int6
     const bool was_expired = old.status == DP_FLOW_EXPIRED;
     old.status = DP_FLOW_DETACHED;
     old.in_table = false;
+    flow_depart(FL, (int64_t)it->second);
     it->second = (uint64_t)ref;
     if (!was_expired) res = DP_FLOW_REPLACED;
   } else {
@@ -2380,6 +3188,15 @@ void flow_info_of(const dpo_flows *FL, int64_t r, dp_flow_info_t &o) {
   o.expires_at = f.d.expires_at;
   if (flow_alive(FL, f.related)) o.related = (uint64_t)f.related;
   o.pf = f.pf;
+  o.masq = f.masq;
+  if (f.masq != DP_PF_NONE) {  // the NAT state's fields share pf_*
+    o.pf_status = FL->nfs[f.m_status];
+    o.pf_port = f.m_port;
+    o.pf_family = f.m_ip.fam;
+    memcpy(o.pf_ip, f.m_ip.b, f.m_ip.fam == 4 ? 4 : 16);
+    o.masq_alloc = f.m_alloc ? 1 : 0;
+    o.idle_timeout_s = (uint32_t)(f.m_idle_ns / 1000000000ull);
+  }
   if (f.pf != DP_PF_NONE) {
     o.pf_status = FL->nfs[f.pf_status];
     o.pf_port = f.pf_port;
@@ -2477,12 +3294,12 @@ int dpo_tables_build2(const dp_tables_desc_t *d, const dpo_tables_t *prev, dpo_t
   if ((rc = load(d->ff_local_v6, d->n_ff_local_v6, T->ffl6, true))) return rc;
   for (auto *v : {&T->ffr4, &T->ffr6})
     for (auto &r : *v) {
-      if (r.r.action2 == DP_NAT_MASQUERADE) return DP_ENOTSUP;
+      if (r.r.action2 > DP_NAT_PORT_FORWARDING) return DP_EINVAL;
       if (r.r.src.len != 0 || r.r.sport_lo != 0 || r.r.sport_hi != 65535 || r.r.gate != 0) return DP_EINVAL;
     }
   for (auto *v : {&T->ffl4, &T->ffl6})
     for (auto &r : *v) {
-      if (r.r.action == DP_NAT_MASQUERADE) return DP_ENOTSUP;
+      if (r.r.action > DP_NAT_PORT_FORWARDING) return DP_EINVAL;
       if (r.r.gate > 1) return DP_EINVAL;
       if (r.r.dst.len != 0 || r.r.dport_lo != 0 || r.r.dport_hi != 65535) return DP_EINVAL;
     }
@@ -2520,11 +3337,55 @@ int dpo_tables_build2(const dp_tables_desc_t *d, const dpo_tables_t *prev, dpo_t
     if (!pf_valid(r) || !valid_prefix(r.ext_prefix) || !valid_prefix(r.int_prefix)) return DP_EINVAL;
   }
   pf_update(*T, prev, d->portfw, d->n_portfw);
+  // masquerade exposes: one family each, a non-empty public range
+  // (ValidatedExpose), and the configuration's canonical bytes
+  if (d->n_masq && (!d->masq || !d->masq_prefixes)) return DP_EINVAL;
+  auto put = [&](const void *x, size_t k) { T->masq_cfg.append(static_cast<const char *>(x), k); };
+  for (uint32_t i = 0; i < d->n_masq; i++) {
+    const dp_masq_expose_t &x = d->masq[i];
+    if (!x.src_vni || !x.dst_vni || x.src_vni == x.dst_vni || !x.n_public || !x.n_private) return DP_EINVAL;
+    if ((uint64_t)x.first_prefix + x.n_private + x.n_public > d->n_masq_prefixes) return DP_EINVAL;
+    if ((uint64_t)x.first_claim + x.n_claims > d->n_masq_claims) return DP_EINVAL;
+    MExpose e;
+    e.src_vni = x.src_vni;
+    e.dst_vni = x.dst_vni;
+    e.idle_ns = (uint64_t)(x.idle_timeout_s ? x.idle_timeout_s : 120) * 1000000000ull;
+    e.fam = d->masq_prefixes[x.first_prefix].family;
+    for (uint32_t k = 0; k < (uint32_t)x.n_private + x.n_public; k++) {
+      const dp_prefix_t &q = d->masq_prefixes[x.first_prefix + k];
+      if (!valid_prefix(q) || q.family != e.fam) return DP_EINVAL;
+      (k < x.n_private ? e.priv : e.pub).push_back(q);
+    }
+    for (uint32_t k = 0; k < x.n_claims; k++) {
+      const dp_masq_claim_t &c = d->masq_claims[x.first_claim + k];
+      if (!valid_prefix(c.prefix) || c.lo > c.hi) return DP_EINVAL;
+      e.claims.push_back(c);
+    }
+    put(&x.src_vni, 4); put(&x.dst_vni, 4); put(&e.idle_ns, 8);
+    for (auto *v : {&e.priv, &e.pub}) {
+      const uint32_t m = (uint32_t)v->size();
+      put(&m, 4);
+      for (auto &q : *v) put(&q, sizeof q);
+    }
+    const uint32_t m = (uint32_t)e.claims.size();
+    put(&m, 4);
+    for (auto &c : e.claims) put(&c, sizeof c);
+    T->masq.push_back(std::move(e));
+  }
+  T->masq_tag = d->masq_config_tag;
+  static std::atomic<uint64_t> serials{1};
+  T->serial = serials++;
   *out = T.release();
   return 0;
 }
 
 int dpo_tables_build(const dp_tables_desc_t *d, dpo_tables_t **out) { return dpo_tables_build2(d, nullptr, out); }
+
+int dpo_flows_sync(dpo_flows_t *fl, const dpo_tables_t *t) {
+  if (!fl || !t) return DP_EINVAL;
+  masq_sync(*t, fl);
+  return 0;
+}
 
 int dpo_flows_set_clock(dpo_flows_t *fl, uint64_t now) {
   if (!fl) return DP_EINVAL;
@@ -2648,6 +3509,7 @@ int dpo_flow_remove(dpo_flows_t *fl, const dp_flow_key_t *keys, uint32_t n, uint
     OFlow &f = fl->f[it->second];
     f.status = DP_FLOW_DETACHED;
     f.in_table = false;
+    flow_depart(fl, (int64_t)it->second);
     fl->map.erase(it);
     c++;
   }
@@ -2678,7 +3540,7 @@ int dpo_flow_sweep(dpo_flows_t *fl, uint64_t now, uint64_t *n_removed) {
     } else if (f.status == DP_FLOW_CANCELLED || f.status == DP_FLOW_EXPIRED) {
       gone = true;
     }
-    if (gone) { f.in_table = false; it = fl->map.erase(it); c++; }
+    if (gone) { f.in_table = false; flow_depart(fl, (int64_t)it->second); it = fl->map.erase(it); c++; }
     else ++it;
   }
   if (n_removed) *n_removed = c;

@@ -72,6 +72,12 @@ int dpo_flow_invalidate(dpo_flows_t *fl, const uint64_t *refs, uint32_t n);
 int dpo_flow_set_status(dpo_flows_t *fl, uint64_t ref, uint32_t status);
 int dpo_flow_sweep(dpo_flows_t *fl, uint64_t now, uint64_t *n_removed);
 int dpo_flow_count(dpo_flows_t *fl, uint64_t *len, uint64_t *active);
+/* NatAllocatorWriter::update_nat_allocator for the tables `t` (what
+ * dp_tables_publish does for every flow table attached on the device): keep
+ * the allocator of an unchanged masquerade configuration, drop it (and
+ * invalidate the masquerade flows) for one without masquerade, else build a
+ * new one and carry the flows it can still serve.  A burst runs it too. */
+int dpo_flows_sync(dpo_flows_t *fl, const dpo_tables_t *t);
 /* Instant::now() for the bursts that follow (DP_OPT_CLOCK, nanoseconds). */
 int dpo_flows_set_clock(dpo_flows_t *fl, uint64_t now);
 /* One burst through the pipeline with FlowLookup on `fl` (NULL: an empty

@@ -30,6 +30,7 @@ def lib() -> C.CDLL:
         l.dpo_tables_build2.argtypes = [V, V, C.POINTER(V)]
         l.dpo_portfw_rule_alive.argtypes = [V, C.c_uint32]
         l.dpo_flows_set_clock.argtypes = [V, C.c_uint64]
+        l.dpo_flows_sync.argtypes = [V, V]
         l.dpo_tables_free.argtypes = [V]
         l.dpo_process_burst.argtypes = [V, V, C.c_uint64, V, V, V, C.c_uint32, V]
         l.dpo_process_parallel.argtypes = [V, V, C.c_uint64, V, V, V, C.c_uint32, C.c_uint32,
@@ -154,6 +155,11 @@ class OracleFlows:
     def set_clock(self, now_ns: int) -> None:
         """Instant::now() for the bursts that follow (DP_OPT_CLOCK)."""
         self._chk(lib().dpo_flows_set_clock(self.h, now_ns), "set_clock")
+
+    def sync(self, oracle: "Oracle") -> None:
+        """update_nat_allocator for `oracle`'s tables (what dp_tables_publish does
+        for the flow tables attached on the device)."""
+        self._chk(lib().dpo_flows_sync(self.h, oracle.h), "sync")
 
     def insert(self, flows):
         from dataplane_amd import _abi as A

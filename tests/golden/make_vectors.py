@@ -36,7 +36,7 @@ def tables_digest(tp) -> str:
     d = tp.contents
     h = hashlib.sha256()
     for name, _ in A.TablesDesc._fields_:
-        if name.startswith("n_") or name in ("abi_version", "pad0", "genid"):
+        if name.startswith("n_") or name in ("abi_version", "pad0", "genid", "masq_config_tag"):
             continue
         n = getattr(d, "n_" + name)
         if n:

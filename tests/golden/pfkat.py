@@ -311,6 +311,9 @@ class GpuRunner:
     def sweep(self, now):
         return self.ft.sweep(now)
 
+    def lookup(self, keys):
+        return self.ft.lookup(keys)
+
     def close(self):
         self.nf.attach_flows(None)
         self.nf.close()
