@@ -16,9 +16,13 @@ namespace dpf {
 enum : uint32_t { FS_EMPTY = 0, FS_BUSY = 1, FS_FULL = 2, FS_TOMB = 3 };
 constexpr uint32_t kNoSlot = 0xffffffffu;
 constexpr uint32_t kIdleMark = 0xffffffffu;
-// FlowSlot::flags bit (above the FlowInfoFlags of dpgpu.h): the flow holds
-// port-forwarding state (FlowInfoLocked.port_fw_state is Some)
+// FlowSlot::flags bits (above the FlowInfoFlags of dpgpu.h): the flow holds
+// port-forwarding state (FlowInfoLocked.port_fw_state is Some), masquerade
+// state (nat/src/masquerade/state.rs:13-20), whose use_port is an ICMP
+// identifier (NatPort::Identifier)
 constexpr uint32_t kFlagPf = 1u << 8;
+constexpr uint32_t kFlagMasq = 1u << 9;
+constexpr uint32_t kFlagMasqIdent = 1u << 10;
 
 struct alignas(128) FlowSlot {
   uint32_t state;       // FS_* | tag << 2
@@ -37,12 +41,18 @@ struct alignas(128) FlowSlot {
   uint64_t expires_at;
   // PortFwState (nat/src/portfw/flow_state.rs:29-35), valid with kFlagPf:
   // action (dp_pf_action) | NatFlowStatus << 8 | use_port << 16, the entry id
-  // its Weak names, use_ip (big-endian words; v4 in word 0)
+  // its Weak names, use_ip (big-endian words; v4 in word 0).  MasqueradeState
+  // (kFlagMasq) in the same words: action | status << 8 | use_port << 16,
+  // the idle timeout in seconds, use_ip
   uint32_t pf;
   uint32_t pf_rule;
   uint32_t pf_ip[4];
   uint32_t pf_fam;
-  uint32_t pad[3];
+  // the allocation a masquerading SrcNat flow owns (its AllocatedPort):
+  // address record + 1 (0: none) and the allocator generation it lives in
+  uint32_t mq_rec;
+  uint32_t mq_gen;
+  uint32_t pad;
 };
 static_assert(sizeof(FlowSlot) == 128, "one L2 line per slot");
 
@@ -80,11 +90,15 @@ struct PfReq {
   uint32_t acl_rule6;    // ... and the rule of its verdict 6
   uint32_t dst_vni0, related0, related_tag0;  // the attached flow as the burst started
   int64_t genid0;
+  uint32_t dst_vni;      // PacketMeta.dst_vpcd at the NAT stages
   // decision (dp_pf_resolve -> replay)
-  uint32_t verdict;      // DoneReason to drop with, or kPfForward
+  uint32_t verdict;      // PortForwarder: DoneReason to drop with, or kPfForward
   uint32_t nat;          // dp_pf_action | port << 16
   uint32_t nat_ip[4];
   uint32_t acl_over;     // 0, or the ACL verdict the sens check left (out.acl code)
+  uint32_t mverdict;     // Masquerade: DoneReason, or kPfForward
+  uint32_t mnat;         // dp_pf_action | ident (1 << 8) | port << 16
+  uint32_t mnat_ip[4];
 };
 constexpr uint32_t kPqReached = 1u << 0;  // the packet reached PortForwarder (else dropped on the way)
 constexpr uint32_t kPqTcp = 1u << 1;
@@ -95,6 +109,10 @@ constexpr uint32_t kPqRelated = 1u << 5;  // related / related_tag valid at atta
 constexpr uint32_t kPqEth = 1u << 6;
 constexpr uint32_t kPqSnatSrc = 1u << 7;  // PacketMeta requires static NAT of the source / destination
 constexpr uint32_t kPqSnatDst = 1u << 8;
+constexpr uint32_t kPqPf = 1u << 9;       // PortForwarder runs on it (REQ_PORT_FORWARDING)
+constexpr uint32_t kPqMasq = 1u << 10;    // Masquerade runs on it (REQ_MASQUERADE)
+constexpr uint32_t kPqIcmp = 1u << 11;    // an ICMP v4 / v6 header
+constexpr uint32_t kPqQuery = 1u << 12;   // its flow key is an ICMP query's (echo, code 0)
 constexpr uint32_t kPfForward = 0xffu;
 
 // The launch-time view of a flow table for one burst.
@@ -122,13 +140,19 @@ struct FlowCtx {
   // bitmap of packets that reached PortForwarder (+ its summary, 1 bit per
   // 1024 packets), the order of the records (resolve), replaced fills
   PfReq *pf;
-  uint32_t *pf_cnt;     // [0] records, [1] replay packets, [2] replaced fills
+  uint32_t *pf_cnt;     // [0] records, [1] replay packets, [2] replaced fills, [3] releases
   uint32_t *pf_of;      // packet -> record
   uint32_t *pf_bits;
   uint32_t *pf_sum;
   uint32_t *pf_order;
   uint32_t *pf_repl;    // (slot, old state, packet index, old mark) of each fill replaced
   uint32_t replay;      // 1: the replay pass (packets pf_order[0..pf_cnt[1]))
+  // masquerade: the table's allocator (dp_masq.h; nullptr: none) and its
+  // generation, the allocations of fills replaced in the burst (record,
+  // port), released when the sequential pass ends
+  uint8_t *mq;
+  uint32_t mq_gen;
+  uint32_t *mq_rel;
 };
 
 // A packet whose ACL verdict was "allow: reply of a flow-scope-allowed flow";

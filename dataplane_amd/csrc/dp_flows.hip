@@ -12,13 +12,17 @@
 // call returns sees it.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstddef>
 #include <cstring>
+#include <map>
 #include <unordered_set>
 #include <string>
 #include <vector>
 
 #include "../../include/dpgpu.h"
 #include "dp_flows_rt.h"
+#include "dp_masq.h"
 
 using dpf::FlowSlot;
 using dpf::FKey;
@@ -65,6 +69,17 @@ __device__ void fill_info(const FlowSlot *slots, uint32_t mask, uint32_t sl, dp_
   if (s.related <= mask && slots[s.related].state == s.related_tag)
     o.related = dpf::make_ref(s.related, s.related_tag);
   o.flags = s.flags & 7u;
+  if (s.flags & dpf::kFlagMasq) {  // MasqueradeState (nat/src/masquerade/state.rs:13-20)
+    o.masq = (uint8_t)(s.pf & 0xffu);
+    o.pf_status = (uint8_t)((s.pf >> 8) & 0xffu);
+    o.pf_port = (uint16_t)(s.pf >> 16);
+    o.pf_family = (uint8_t)s.pf_fam;
+    for (int j = 0; j < 4; j++)
+      for (int b = 0; b < 4; b++) o.pf_ip[4 * j + b] = (uint8_t)(s.pf_ip[j] >> (24 - 8 * b));
+    if (s.pf_fam == 4) for (int b = 4; b < 16; b++) o.pf_ip[b] = 0;
+    o.masq_alloc = s.mq_rec != 0;
+    o.idle_timeout_s = s.pf_rule;
+  }
   if (s.flags & dpf::kFlagPf) {  // PortFwState (nat/src/portfw/flow_state.rs:29-35)
     o.pf = (uint8_t)(s.pf & 0xffu);
     o.pf_status = (uint8_t)((s.pf >> 8) & 0xffu);
@@ -74,6 +89,32 @@ __device__ void fill_info(const FlowSlot *slots, uint32_t mask, uint32_t sl, dp_
     for (int j = 0; j < 4; j++)
       for (int b = 0; b < 4; b++) o.pf_ip[4 * j + b] = (uint8_t)(s.pf_ip[j] >> (24 - 8 * b));
   }
+}
+
+// A flow leaving the table drops its FlowInfo, and with it the allocation its
+// masquerade state owns (the Drop of its AllocatedPort, port_alloc.rs:
+// 553-565): the (address record, port) goes on the call's release list, which
+// one thread of fl_release_k works through afterwards (the allocator is
+// sequential state).  false: the list is full -- the caller keeps the flow
+// for a later round.
+struct MqRel {
+  uint32_t gen;   // the table's allocator generation (allocations of older ones are gone)
+  uint32_t cap;
+  uint32_t *cnt;  // [0] entries appended (may pass cap)
+  uint32_t *list; // (record, port) pairs; nullptr: no allocator
+};
+__device__ __forceinline__ bool mq_depart(const MqRel &r, const FlowSlot &s) {
+  if (!r.list || !(s.flags & dpf::kFlagMasq) || !s.mq_rec || s.mq_gen != r.gen) return true;
+  const uint32_t k = atomicAdd(r.cnt, 1u);
+  if (k >= r.cap) return false;
+  r.list[2 * k] = s.mq_rec - 1;
+  r.list[2 * k + 1] = s.pf >> 16;
+  return true;
+}
+__global__ void fl_release_k(uint8_t *mq, const uint32_t *list, const uint32_t *cnt, uint32_t cap) {
+  const dpm::View V{mq};
+  const uint32_t n = *cnt < cap ? *cnt : cap;
+  for (uint32_t k = 0; k < n; k++) dpm::release(V, list[2 * k], list[2 * k + 1]);
 }
 
 __global__ void __launch_bounds__(kTB) fl_find_k(const FlowSlot *slots, uint32_t mask, uint32_t max_probe,
@@ -97,13 +138,14 @@ struct InsRec {
 // is Active (table.rs:235-240), with no related flow yet.  A new slot's
 // displacement from the key's home raises the table's probe bound (*meta).
 __global__ void __launch_bounds__(kTB) fl_insert_k(FlowSlot *slots, uint32_t mask, const InsRec *recs, uint32_t n,
-                                                  uint64_t *refs, uint32_t *meta) {
+                                                  uint64_t *refs, uint32_t *meta, MqRel rel) {
   const uint32_t i = blockIdx.x * kTB + threadIdx.x;
   if (i >= n) return;
   const InsRec r = recs[i];
   uint32_t sl = r.slot, old = 0;
   if (sl != dpf::kNoSlot) {
     old = slots[sl].state;
+    (void)mq_depart(rel, slots[sl]);  // the replaced flow (one per record: room for all)
     atomicExch(&slots[sl].state, (old & ~3u) | dpf::FS_BUSY);
   } else {
     uint32_t p = dpf::fkey_hash(r.k) & mask;
@@ -133,6 +175,7 @@ __global__ void __launch_bounds__(kTB) fl_insert_k(FlowSlot *slots, uint32_t mas
   s.expires_at = r.expires_at;
   s.pf = 0;
   s.pf_rule = 0;
+  s.mq_rec = 0;
   const uint32_t tag = ((old >> 2) + 1) & 0x3fffffffu;
   const uint32_t st = (tag << 2) | dpf::FS_FULL;
   __hip_atomic_store(&s.state, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -175,7 +218,7 @@ __global__ void __launch_bounds__(kTB) fl_get_k(const FlowSlot *slots, uint32_t 
 
 // FlowTable::remove (table.rs:282-295): Detached, out of the table
 __global__ void __launch_bounds__(kTB) fl_remove_k(FlowSlot *slots, uint32_t mask, uint32_t max_probe,
-                                                  const FKey *keys, uint32_t n, uint32_t *count) {
+                                                  const FKey *keys, uint32_t n, uint32_t *count, MqRel rel) {
   const uint32_t i = blockIdx.x * kTB + threadIdx.x;
   if (i >= n) return;
   uint32_t st;
@@ -183,6 +226,7 @@ __global__ void __launch_bounds__(kTB) fl_remove_k(FlowSlot *slots, uint32_t mas
   if (sl == dpf::kNoSlot) return;
   slots[sl].status = DP_FLOW_DETACHED;
   if (atomicCAS(&slots[sl].state, st, (st & ~3u) | dpf::FS_TOMB) != st) return;
+  (void)mq_depart(rel, slots[sl]);  // one flow per key: room for all
   atomicAdd(count, 1u);
   // the new tombstone ends a cluster: it and the tombstones before it
   // become EMPTY (as fl_reclaim_k; a missed reclaim only costs probe length)
@@ -214,8 +258,10 @@ __global__ void fl_set_status_k(FlowSlot *slots, uint32_t mask, uint64_t ref, ui
 }
 
 // The flow timers up to `now` (FlowTable::start_timer, table.rs:160-213)
+// A flow whose allocation finds the release list full stays (Expired) for
+// the next round of the same call.
 __global__ void __launch_bounds__(kTB) fl_sweep_k(FlowSlot *slots, uint64_t nslots, uint64_t now,
-                                                 unsigned long long *count) {
+                                                 unsigned long long *count, MqRel rel) {
   for (uint64_t i = blockIdx.x * (uint64_t)kTB + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * kTB) {
     FlowSlot &s = slots[i];
     const uint32_t st = s.state;
@@ -226,7 +272,8 @@ __global__ void __launch_bounds__(kTB) fl_sweep_k(FlowSlot *slots, uint64_t nslo
     } else if (s.status == DP_FLOW_CANCELLED || s.status == DP_FLOW_EXPIRED) {
       gone = true;
     }
-    if (gone && atomicCAS(&s.state, st, (st & ~3u) | dpf::FS_TOMB) == st) atomicAdd(count, 1ull);
+    if (gone && mq_depart(rel, s) && atomicCAS(&s.state, st, (st & ~3u) | dpf::FS_TOMB) == st)
+      atomicAdd(count, 1ull);
   }
 }
 
@@ -332,6 +379,21 @@ int run(dp_flow_table *ft, const char *what, F f) {
 
 uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kTB - 1) / kTB); }
 
+// A management call's release list for `cap` departures (counter zeroed on
+// the stream); no list when the table has no allocator.  false: no memory.
+bool rel_list(dp_flow_table *ft, uint32_t cap, hipStream_t st, MqRel &r) {
+  r = MqRel{ft->mq_gen, cap, nullptr, nullptr};
+  if (!ft->mq) return true;
+  uint32_t *b = static_cast<uint32_t *>(ft->mq_rel.get(sizeof(uint32_t) * (2 * (size_t)(cap ? cap : 1) + 1)));
+  if (!b || hipMemsetAsync(b, 0, sizeof(uint32_t), st) != hipSuccess) return false;
+  r.cnt = b;
+  r.list = b + 1;
+  return true;
+}
+void rel_run(dp_flow_table *ft, const MqRel &r, hipStream_t st) {
+  if (r.list) hipLaunchKernelGGL(fl_release_k, dim3(1), dim3(1), 0, st, ft->mq, r.list, r.cnt, r.cap);
+}
+
 // The table's device words ([0] probe bound, [2..3] len): bursts that create
 // flows (port forwarding) move them on the device, so a management call that
 // decides on the host reads them first and writes them back after.
@@ -416,9 +478,11 @@ int insert_batch(dp_flow_table *ft, const dp_flow_t *flows, uint32_t n, const in
     rc = run(ft, "flow insert", [&](hipStream_t st) {
       InsRec *dr = upload(s_recs, recs.data(), recs.size(), st);
       uint64_t *df = static_cast<uint64_t *>(s_refs.get(sizeof(uint64_t) * recs.size()));
-      if (!dr || !df) return dpr_fail(DP_ENOMEM, "flow scratch");
+      MqRel rel;
+      if (!dr || !df || !rel_list(ft, (uint32_t)recs.size(), st, rel)) return dpr_fail(DP_ENOMEM, "flow scratch");
       hipLaunchKernelGGL(fl_insert_k, dim3(blocks_for(recs.size())), dim3(kTB), 0, st, ft->slots, ft->mask, dr,
-                         (uint32_t)recs.size(), df, ft->d_meta);
+                         (uint32_t)recs.size(), df, ft->d_meta, rel);
+      rel_run(ft, rel, st);
       if (hipMemcpyAsync(got.data(), df, sizeof(uint64_t) * recs.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
           hipMemcpyAsync(&maxp, ft->d_meta, sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess)
         return dpr_fail(DP_EIO, "flow insert copy");
@@ -445,7 +509,423 @@ int insert_batch(dp_flow_table *ft, const dp_flow_t *flows, uint32_t n, const in
   return 0;
 }
 
+// --------------------------------------------------------------------------
+// masquerade allocator: build and sync (update_nat_allocator)
+// --------------------------------------------------------------------------
+typedef unsigned __int128 u128;
+
+u128 pfx_first(const dp_prefix_t &p) {
+  u128 v = 0;
+  const int n = p.family == 4 ? 4 : 16;
+  for (int i = 0; i < n; i++) v = (v << 8) | p.addr[i];
+  return v;
+}
+u128 pfx_last(const dp_prefix_t &p) {
+  const int w = p.family == 4 ? 32 : 128;
+  const u128 host = p.len >= w ? (u128)0 : (p.len == 0 && w == 128 ? ~(u128)0 : (((u128)1 << (w - p.len)) - 1));
+  return pfx_first(p) | host;
+}
+dpm::A128 to_a(u128 v) {
+  dpm::A128 a;
+  for (int i = 3; i >= 0; i--) { a.w[i] = (uint32_t)v; v >>= 32; }
+  return a;
+}
+
+// decompose + regions_by_owner (apalloc/region.rs:43-130): the public space of
+// one destination VPC's exposes cut into disjoint regions of constant owners
+struct RegionSpec {
+  u128 lo, hi;
+  std::vector<size_t> owners;
+};
+std::vector<RegionSpec> decompose(const std::vector<std::vector<std::pair<u128, u128>>> &own) {
+  std::vector<u128> c;
+  for (auto &rs : own)
+    for (auto &r : rs) {
+      c.push_back(r.first);
+      if (r.second != ~(u128)0) c.push_back(r.second + 1);
+    }
+  std::sort(c.begin(), c.end());
+  c.erase(std::unique(c.begin(), c.end()), c.end());
+  std::vector<RegionSpec> out;
+  for (size_t i = 0; i < c.size(); i++) {
+    const u128 s = c[i], e = i + 1 < c.size() ? c[i + 1] - 1 : ~(u128)0;
+    std::vector<size_t> owners;
+    for (size_t o = 0; o < own.size(); o++)
+      for (auto &r : own[o]) if (r.first <= s && s <= r.second) { owners.push_back(o); break; }
+    if (owners.empty()) continue;
+    if (!out.empty() && out.back().hi + 1 == s && out.back().owners == owners) out.back().hi = e;
+    else out.push_back(RegionSpec{s, e, owners});
+  }
+  return out;
+}
+
+// NatAllocator::new -> build_pools_generic (apalloc/setup.rs:158-204) into the
+// dp_masq.h layout: per family, per destination VPC, per protocol the regions
+// of its exposes' public prefixes (each its own NatPool), per expose a PoolSet
+// of its regions (fewest sharers, widest, lowest first), per private prefix a
+// PoolTable entry.  `used`: bytes through the address records (the records
+// area is not initialised; a new address writes its whole record).
+constexpr uint32_t kNeverUsed = dpm::kNone - 1;
+std::vector<uint8_t> masq_build(const dpd::MasqConfig &cfg, int64_t genid, uint32_t gen) {
+  struct EKey {
+    uint32_t proto, src, dst;
+    u128 lo, hi;
+    bool operator<(const EKey &o) const {
+      if (proto != o.proto) return proto < o.proto;
+      if (src != o.src) return src < o.src;
+      if (dst != o.dst) return dst < o.dst;
+      if (lo != o.lo) return lo < o.lo;
+      return hi < o.hi;
+    }
+  };
+  std::map<EKey, uint32_t> table;  // add_pool_entries: a later expose's entry replaces
+  std::vector<dpm::Set> sets;
+  std::vector<uint32_t> setreg;
+  std::vector<dpm::Region> regions;
+  std::vector<dpm::Claim> claims;
+  uint32_t bit_words = 0;
+  uint64_t sum_cap = 0;
+  for (int fam : {4, 6}) {
+    std::map<uint32_t, std::vector<const dpd::MasqExpose *>> groups;  // by destination VPC
+    for (auto &e : cfg.exposes) if (e.fam == fam) groups[e.dst_vni].push_back(&e);
+    for (auto &g : groups) {
+      for (uint32_t proto : {6u, 17u, fam == 4 ? 1u : 58u}) {
+        std::vector<std::vector<std::pair<u128, u128>>> own;
+        for (auto *e : g.second) {
+          std::vector<std::pair<u128, u128>> rs;
+          for (auto &p : e->pub) rs.push_back({pfx_first(p), pfx_last(p)});
+          own.push_back(rs);
+        }
+        const auto specs = decompose(own);
+        const uint32_t r0 = (uint32_t)regions.size();
+        for (auto &R : specs) {
+          dpm::Region x{};
+          x.fam = (uint32_t)fam;
+          const u128 span = R.hi - R.lo;
+          x.cap = span >= DP_MASQ_REGION_ADDRS - 1 ? DP_MASQ_REGION_ADDRS : (uint32_t)span + 1;
+          x.excl_wk = proto == 6 || proto == 17;
+          x.start = to_a(R.lo);
+          x.last = to_a(R.hi);
+          x.claim_first = (uint32_t)claims.size();
+          const uint32_t bit = proto == 6 ? DP_MASQ_TCP : proto == 17 ? DP_MASQ_UDP : 0u;
+          for (size_t o : R.owners)
+            for (auto &c : g.second[o]->claims)
+              if (c.protos & bit) {
+                dpm::Claim k{};
+                k.net = to_a(pfx_first(c.prefix));
+                k.fam = c.prefix.family;
+                k.len = c.prefix.len;
+                k.lo = c.lo;
+                k.hi = c.hi;
+                claims.push_back(k);
+              }
+          x.claim_n = (uint32_t)claims.size() - x.claim_first;
+          x.head = x.tail = dpm::kNone;
+          x.bits = bit_words;
+          x.hint = 0;
+          bit_words += (x.cap + 31) / 32;
+          sum_cap += x.cap;
+          regions.push_back(x);
+        }
+        for (size_t o = 0; o < g.second.size(); o++) {
+          std::vector<size_t> mine;
+          for (size_t r = 0; r < specs.size(); r++)
+            if (std::find(specs[r].owners.begin(), specs[r].owners.end(), o) != specs[r].owners.end())
+              mine.push_back(r);
+          std::stable_sort(mine.begin(), mine.end(), [&](size_t a, size_t b) {
+            const auto &x = specs[a], &y = specs[b];
+            if (x.owners.size() != y.owners.size()) return x.owners.size() < y.owners.size();
+            const u128 lx = x.hi - x.lo, ly = y.hi - y.lo;
+            if (lx != ly) return lx > ly;
+            return x.lo < y.lo;
+          });
+          dpm::Set S{};
+          S.idle_ns = g.second[o]->idle_ns;
+          S.first_reg = (uint32_t)setreg.size();
+          S.n_reg = (uint32_t)mine.size();
+          for (size_t r : mine) setreg.push_back(r0 + (uint32_t)r);
+          const uint32_t si = (uint32_t)sets.size();
+          sets.push_back(S);
+          for (auto &p : g.second[o]->priv)
+            table[EKey{proto | ((uint32_t)fam << 8), g.second[o]->src_vni, g.first, pfx_first(p), pfx_last(p)}] = si;
+        }
+      }
+    }
+  }
+  // the table's runs: one per (protocol | family, source, destination)
+  std::vector<dpm::Ent> ents;
+  std::vector<dpm::KeySlot> runs;
+  for (auto &kv : table) {
+    const EKey &k = kv.first;
+    if (runs.empty() || runs.back().proto != k.proto || runs.back().src != k.src ||
+        (runs.back().dst & 0x7fffffffu) != k.dst)
+      runs.push_back(dpm::KeySlot{k.proto, k.src, k.dst | 0x80000000u, (uint32_t)ents.size(), 0, {0, 0, 0}});
+    runs.back().n++;
+    dpm::Ent e{};
+    e.lo = to_a(k.lo);
+    e.hi = to_a(k.hi);
+    e.set = kv.second;
+    ents.push_back(e);
+  }
+  uint32_t ksz = 1;
+  while (ksz < 2 * runs.size() + 2) ksz <<= 1;
+  std::vector<dpm::KeySlot> keys(ksz);
+  for (auto &r : runs) {
+    uint32_t i = dpm::kmix(r.proto, r.src, r.dst & 0x7fffffffu) & (ksz - 1);
+    while (keys[i].dst >> 31) i = (i + 1) & (ksz - 1);
+    keys[i] = r;
+  }
+  const uint32_t n_recs = (uint32_t)std::min<uint64_t>(sum_cap, DP_MASQ_ADDRS);
+  dpm::Header H{};
+  H.magic = dpm::kMagic;
+  H.gen = gen;
+  H.genid = genid;
+  H.key_mask = ksz - 1;
+  H.n_keys = (uint32_t)runs.size();
+  H.n_regions = (uint32_t)regions.size();
+  H.n_recs = n_recs;
+  H.free_top = n_recs;
+  H.live = 0;
+  H.max_live = DP_MASQ_ADDRS;
+  uint64_t off = (sizeof(dpm::Header) + 63) & ~63ull;
+  auto place = [&](uint64_t bytes) { const uint64_t o = off; off = (off + bytes + 63) & ~63ull; return o; };
+  H.o_keys = place(sizeof(dpm::KeySlot) * keys.size());
+  H.o_ents = place(sizeof(dpm::Ent) * ents.size());
+  H.o_sets = place(sizeof(dpm::Set) * sets.size());
+  H.o_setreg = place(sizeof(uint32_t) * setreg.size());
+  H.o_regions = place(sizeof(dpm::Region) * regions.size());
+  H.o_claims = place(sizeof(dpm::Claim) * claims.size());
+  H.o_bits = place(sizeof(uint32_t) * bit_words);
+  H.o_free = place(sizeof(uint32_t) * n_recs);
+  H.o_recs = place(0);
+  H.bytes = H.o_recs + sizeof(dpm::Addr) * (uint64_t)n_recs;
+  std::vector<uint8_t> b(H.bytes, 0);
+  memcpy(b.data(), &H, sizeof H);
+  // records never handed out are marked so (the upload stops after the last one used)
+  dpm::Addr *ra = reinterpret_cast<dpm::Addr *>(b.data() + H.o_recs);
+  for (uint32_t i = 0; i < n_recs; i++) ra[i].region = kNeverUsed;
+  auto copy = [&](uint64_t o, const void *p, size_t n) { if (n) memcpy(b.data() + o, p, n); };
+  copy(H.o_keys, keys.data(), sizeof(dpm::KeySlot) * keys.size());
+  copy(H.o_ents, ents.data(), sizeof(dpm::Ent) * ents.size());
+  copy(H.o_sets, sets.data(), sizeof(dpm::Set) * sets.size());
+  copy(H.o_setreg, setreg.data(), sizeof(uint32_t) * setreg.size());
+  copy(H.o_regions, regions.data(), sizeof(dpm::Region) * regions.size());
+  copy(H.o_claims, claims.data(), sizeof(dpm::Claim) * claims.size());
+  uint32_t *bw = reinterpret_cast<uint32_t *>(b.data() + H.o_bits);
+  for (auto &R : regions)
+    for (uint32_t o = 0; o < R.cap; o++) bw[R.bits + (o >> 5)] |= 1u << (o & 31);
+  // the free records, popped lowest first
+  uint32_t *fs = reinterpret_cast<uint32_t *>(b.data() + H.o_free);
+  for (uint32_t i = 0; i < n_recs; i++) fs[i] = n_recs - 1 - i;
+  return b;
+}
+
+// A masquerading flow holding an allocation, as check_masquerading_flow sees it
+struct MqFlow {
+  uint32_t slot, state, vni, fk;
+  uint32_t src[4];   // key source (address bytes as stored)
+  uint32_t dst_vni, pf, fam, flags;
+  uint32_t ip[4];    // use_ip (big-endian words)
+};
+struct MqDecision {
+  uint32_t slot, state, rec;  // rec: the new allocation's record, kNone: invalidate the pair
+};
+
+// Active masquerading flows with an allocation and another generation than the
+// new allocator's (the flows check_masquerading_flow re-reserves).
+__global__ void __launch_bounds__(kTB) mq_collect_k(const FlowSlot *slots, uint64_t nslots, int64_t genid,
+                                                   MqFlow *out, uint32_t cap, uint32_t *cnt) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kTB + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * kTB) {
+    const FlowSlot &s = slots[i];
+    const uint32_t st = s.state;
+    if ((st & 3u) != dpf::FS_FULL || s.status != DP_FLOW_ACTIVE || !(s.flags & dpf::kFlagMasq) || !s.mq_rec ||
+        s.genid == genid)
+      continue;
+    const uint32_t k = atomicAdd(cnt, 1u);
+    if (k >= cap) continue;
+    MqFlow f;
+    f.slot = (uint32_t)i;
+    f.state = st;
+    f.vni = s.src_vni;
+    f.fk = s.fk;
+    for (int j = 0; j < 4; j++) { f.src[j] = s.src[j]; f.ip[j] = s.pf_ip[j]; }
+    f.dst_vni = s.dst_vni;
+    f.pf = s.pf;
+    f.fam = s.pf_fam;
+    f.flags = s.flags;
+    out[k] = f;
+  }
+}
+// set_genid_pair / invalidate_pair of the re-reserved / dropped flows
+__global__ void __launch_bounds__(kTB) mq_apply_k(FlowSlot *slots, uint32_t mask, const MqDecision *d, uint32_t n,
+                                                 int64_t genid, uint32_t gen) {
+  const uint32_t i = blockIdx.x * kTB + threadIdx.x;
+  if (i >= n) return;
+  const MqDecision x = d[i];
+  FlowSlot &s = slots[x.slot];
+  if (s.state != x.state) return;
+  const bool rel = s.related <= mask && slots[s.related].state == s.related_tag;
+  if (x.rec == dpm::kNone) {
+    s.status = DP_FLOW_CANCELLED;
+    if (rel) slots[s.related].status = DP_FLOW_CANCELLED;
+  } else {
+    s.mq_rec = x.rec + 1;
+    s.mq_gen = gen;
+    s.genid = genid;
+    if (rel) slots[s.related].genid = genid;
+  }
+}
+// upgrade_all_masquerading_flows (flows.rs:30-44)
+__global__ void __launch_bounds__(kTB) mq_upgrade_k(FlowSlot *slots, uint64_t nslots, int64_t genid) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kTB + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * kTB) {
+    FlowSlot &s = slots[i];
+    if ((s.state & 3u) == dpf::FS_FULL && s.status == DP_FLOW_ACTIVE && (s.flags & dpf::kFlagMasq)) s.genid = genid;
+  }
+}
+// invalidate_masquerade_flows (flows.rs:19-27): every masquerading flow's pair
+__global__ void __launch_bounds__(kTB) mq_drop_k(FlowSlot *slots, uint64_t nslots, uint32_t mask) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kTB + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * kTB) {
+    FlowSlot &s = slots[i];
+    if ((s.state & 3u) != dpf::FS_FULL || !(s.flags & dpf::kFlagMasq)) continue;
+    s.status = DP_FLOW_CANCELLED;
+    if (s.related <= mask && slots[s.related].state == s.related_tag) slots[s.related].status = DP_FLOW_CANCELLED;
+  }
+}
+
+bool covers(const dp_prefix_t &p, int fam, u128 a) { return p.family == fam && pfx_first(p) <= a && a <= pfx_last(p); }
+
 }  // namespace
+
+int dpf_masq_sync(dp_flow_table *ft, const std::shared_ptr<const dpd::MasqConfig> &cfg, int64_t genid,
+                  uint64_t serial) {
+  if (!cfg || ft->mq_serial == serial) return 0;
+  const uint32_t b = blocks_for(ft->nslots) < 4096 ? blocks_for(ft->nslots) : 4096;
+  if (ft->mq && ft->mq_cfg && ft->mq_cfg->same(*cfg)) {
+    // the same config: the allocator stays, its flows move to the new generation
+    int rc = run(ft, "masquerade upgrade", [&](hipStream_t st) {
+      if (hipMemcpyAsync(ft->mq + offsetof(dpm::Header, genid), &genid, sizeof genid, hipMemcpyHostToDevice, st) !=
+          hipSuccess)
+        return dpr_fail(DP_EIO, "allocator genid");
+      hipLaunchKernelGGL(mq_upgrade_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, genid);
+      return 0;
+    });
+    if (!rc) ft->mq_serial = serial;
+    return rc;
+  }
+  if (cfg->exposes.empty()) {
+    if (ft->mq) {
+      int rc = run(ft, "masquerade drop", [&](hipStream_t st) {
+        hipLaunchKernelGGL(mq_drop_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, ft->mask);
+        return 0;
+      });
+      if (rc) return rc;
+      (void)hipFree(ft->mq);
+      ft->mq = nullptr;
+      ft->mq_cfg.reset();
+      ft->mq_gen = 0;
+    }
+    ft->mq_serial = serial;
+    return 0;
+  }
+  const uint32_t gen = ft->mq_next_gen++;
+  std::vector<uint8_t> buf = masq_build(*cfg, genid, gen);
+  // (the device copy is the whole layout; records past the ones handed out are
+  // written by the first allocation that takes them)
+  const dpm::View V{buf.data()};
+  // the flows to carry over
+  Scratch &sa = ft->scr[0], &sb = ft->scr[1];
+  uint32_t n = 0;
+  std::vector<MqFlow> flows;
+  for (int pass = 0; pass < 2; pass++) {
+    const uint32_t cap = pass ? n : 0;
+    flows.resize(cap);
+    uint32_t got = 0;
+    int rc = run(ft, "masquerade flows", [&](hipStream_t st) {
+      uint32_t *dc = static_cast<uint32_t *>(sa.get(sizeof(uint32_t)));
+      MqFlow *df = static_cast<MqFlow *>(sb.get(sizeof(MqFlow) * (cap ? cap : 1)));
+      if (!dc || !df) return dpr_fail(DP_ENOMEM, "flow scratch");
+      if (hipMemsetAsync(dc, 0, sizeof(uint32_t), st) != hipSuccess) return dpr_fail(DP_EIO, "memset");
+      hipLaunchKernelGGL(mq_collect_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, genid, df, cap, dc);
+      if (hipMemcpyAsync(&got, dc, sizeof got, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          (cap && hipMemcpyAsync(flows.data(), df, sizeof(MqFlow) * cap, hipMemcpyDeviceToHost, st) != hipSuccess))
+        return dpr_fail(DP_EIO, "masquerade flows copy");
+      return 0;
+    });
+    if (rc) return rc;
+    n = got;
+    if (!n) break;
+  }
+  // check_masquerading_flow for each, in ascending (address, port) order
+  auto ip_bytes = [](const MqFlow &f, uint8_t out[16]) {
+    memset(out, 0, 16);
+    for (int j = 0; j < (f.fam == 4 ? 1 : 4); j++)
+      for (int k = 0; k < 4; k++) out[4 * j + k] = (uint8_t)(f.ip[j] >> (24 - 8 * k));
+  };
+  std::stable_sort(flows.begin(), flows.end(), [&](const MqFlow &x, const MqFlow &y) {
+    uint8_t a[16], c[16];
+    ip_bytes(x, a);
+    ip_bytes(y, c);
+    const int r = memcmp(a, c, 16);
+    if (r) return r < 0;
+    return (x.pf >> 16) < (y.pf >> 16);
+  });
+  std::vector<MqDecision> dec;
+  for (const MqFlow &f : flows) {
+    const int kfam = (int)(f.fk & 0xffu), kind = (int)(f.fk >> 8);
+    u128 ip = 0, src = 0;
+    for (int j = 0; j < (f.fam == 4 ? 1 : 4); j++) ip = (ip << 32) | f.ip[j];
+    uint8_t sb8[16];
+    memcpy(sb8, f.src, 16);
+    for (int j = 0; j < (kfam == 4 ? 4 : 16); j++) src = (src << 8) | sb8[j];
+    bool peering = false, ip_ok = false, compatible = false;
+    for (auto &e : cfg->exposes) {
+      if (e.src_vni != f.vni || e.dst_vni != f.dst_vni) continue;
+      peering = true;
+      bool pub = false;
+      for (auto &q : e.pub) pub |= covers(q, (int)f.fam, ip);
+      if (!pub) continue;
+      ip_ok = true;
+      bool pri = false;
+      for (auto &q : e.priv) pri |= covers(q, kfam, src);
+      if (pri) { compatible = true; break; }
+    }
+    uint32_t rec = dpm::kNone;
+    if (peering && ip_ok && compatible) {
+      const uint32_t proto = kind == DP_FLOW_TCP ? 6u : kind == DP_FLOW_UDP ? 17u : kfam == 4 ? 1u : 58u;
+      const uint32_t set = dpm::lookup(V, proto | ((uint32_t)kfam << 8), f.vni, f.dst_vni, to_a(src));
+      uint32_t r = 0;
+      if (set != dpm::kNone &&
+          dpm::set_reserve(V, set, to_a(ip), f.pf >> 16, (f.flags & dpf::kFlagMasqIdent) != 0, r) == dpm::OK)
+        rec = r;
+    }
+    dec.push_back(MqDecision{f.slot, f.state, rec});
+  }
+  uint8_t *dev = nullptr;
+  if (hipSetDevice(ft->device) != hipSuccess || hipMalloc(&dev, buf.size()) != hipSuccess)
+    return dpr_fail(DP_ENOMEM, "masquerade allocator");
+  int rc = run(ft, "masquerade allocator", [&](hipStream_t st) {
+    // the records handed out sit lowest (the free stack pops them in order)
+    uint32_t hi = 0;
+    while (hi < V.h().n_recs && V.recs()[hi].region != kNeverUsed) hi++;
+    const uint64_t used = V.h().o_recs + sizeof(dpm::Addr) * (uint64_t)hi;
+    if (hipMemcpyAsync(dev, buf.data(), used, hipMemcpyHostToDevice, st) != hipSuccess)
+      return dpr_fail(DP_EIO, "masquerade allocator upload");
+    if (!dec.empty()) {
+      MqDecision *dd = upload(sa, dec.data(), dec.size(), st);
+      if (!dd) return dpr_fail(DP_ENOMEM, "flow scratch");
+      hipLaunchKernelGGL(mq_apply_k, dim3(blocks_for(dec.size())), dim3(kTB), 0, st, ft->slots, ft->mask, dd,
+                         (uint32_t)dec.size(), genid, gen);
+    }
+    return 0;
+  });
+  if (rc) { (void)hipFree(dev); return rc; }
+  if (ft->mq) (void)hipFree(ft->mq);
+  ft->mq = dev;
+  ft->mq_gen = gen;
+  ft->mq_cfg = cfg;
+  ft->mq_serial = serial;
+  return 0;
+}
 
 extern "C" {
 
@@ -486,11 +966,14 @@ int dp_flow_table_create(int device_ordinal, uint64_t slots, dp_flow_table_t **o
 
 int dp_flow_table_destroy(dp_flow_table_t *ft) {
   if (!ft) return DP_EINVAL;
+  dpr_forget_flow_table(ft);
   (void)hipSetDevice(ft->device);
   if (ft->burst_armed) (void)hipEventSynchronize(ft->last_burst);
   (void)hipStreamSynchronize(ft->stream);
   (void)hipFree(ft->slots);
   (void)hipFree(ft->d_meta);
+  if (ft->mq) (void)hipFree(ft->mq);
+  ft->mq_rel.release();
   for (auto &x : ft->scr) x.release();
   (void)hipEventDestroy(ft->last_burst);
   (void)hipStreamDestroy(ft->stream);
@@ -627,11 +1110,14 @@ int dp_flow_remove(dp_flow_table_t *ft, const dp_flow_key_t *keys, uint32_t n, u
   int rc = run(ft, "flow remove", [&](hipStream_t st) {
     FKey *dk = upload(sk, k.data(), n, st);
     uint32_t *dc = static_cast<uint32_t *>(sc.get(sizeof(uint32_t)));
-    if (!dk || !dc) return dpr_fail(DP_ENOMEM, "flow scratch");
+    MqRel rel;
+    if (!dk || !dc || !rel_list(ft, n, st, rel)) return dpr_fail(DP_ENOMEM, "flow scratch");
     if (hipMemsetAsync(dc, 0, sizeof(uint32_t), st) != hipSuccess) return dpr_fail(DP_EIO, "memset");
-    if (n)
+    if (n) {
       hipLaunchKernelGGL(fl_remove_k, dim3(blocks_for(n)), dim3(kTB), 0, st, ft->slots, ft->mask, ft->max_probe,
-                         dk, n, dc);
+                         dk, n, dc, rel);
+      rel_run(ft, rel, st);
+    }
     if (hipMemcpyAsync(&cnt, dc, sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess)
       return dpr_fail(DP_EIO, "flow remove copy");
     return 0;
@@ -678,18 +1164,33 @@ int dp_flow_sweep(dp_flow_table_t *ft, uint64_t now, uint64_t *n_removed) {
   if (int rc = pull_meta(ft)) return rc;
   Scratch &sc = ft->scr[0];
   unsigned long long cnt = 0;
-  int rc = run(ft, "flow sweep", [&](hipStream_t st) {
-    unsigned long long *dc = static_cast<unsigned long long *>(sc.get(2 * sizeof(cnt)));
-    if (!dc) return dpr_fail(DP_ENOMEM, "flow scratch");
-    if (hipMemsetAsync(dc, 0, 2 * sizeof(cnt), st) != hipSuccess) return dpr_fail(DP_EIO, "memset");
-    const uint32_t b = blocks_for(ft->nslots) < 4096 ? blocks_for(ft->nslots) : 4096;
-    hipLaunchKernelGGL(fl_sweep_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, now, dc);
-    if (hipMemcpyAsync(&cnt, dc, sizeof(cnt), hipMemcpyDeviceToHost, st) != hipSuccess)
-      return dpr_fail(DP_EIO, "flow sweep copy");
-    // the tombstones the timers left, wherever they end a cluster
-    hipLaunchKernelGGL(fl_reclaim_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, dc + 1);
-    return 0;
-  });
+  // rounds of at most kRelCap allocations released (a flow that found the
+  // list full is Expired and goes in a later round)
+  constexpr uint32_t kRelCap = 1u << 20;
+  const uint32_t cap = ft->nslots < kRelCap ? (uint32_t)ft->nslots : kRelCap;
+  uint32_t appended = 0;
+  int rc = 0;
+  do {
+    rc = run(ft, "flow sweep", [&](hipStream_t st) {
+      unsigned long long *dc = static_cast<unsigned long long *>(sc.get(2 * sizeof(cnt)));
+      MqRel rel;
+      if (!dc || !rel_list(ft, cap, st, rel)) return dpr_fail(DP_ENOMEM, "flow scratch");
+      if (hipMemsetAsync(dc, 0, 2 * sizeof(cnt), st) != hipSuccess) return dpr_fail(DP_EIO, "memset");
+      const uint32_t b = blocks_for(ft->nslots) < 4096 ? blocks_for(ft->nslots) : 4096;
+      hipLaunchKernelGGL(fl_sweep_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, now, dc, rel);
+      rel_run(ft, rel, st);
+      unsigned long long c = 0;
+      appended = 0;
+      if (hipMemcpyAsync(&c, dc, sizeof(c), hipMemcpyDeviceToHost, st) != hipSuccess ||
+          (rel.cnt && hipMemcpyAsync(&appended, rel.cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess))
+        return dpr_fail(DP_EIO, "flow sweep copy");
+      if (hipStreamSynchronize(st) != hipSuccess) return dpr_fail(DP_EIO, "flow sweep");
+      cnt += c;
+      // the tombstones the timers left, wherever they end a cluster
+      hipLaunchKernelGGL(fl_reclaim_k, dim3(b), dim3(kTB), 0, st, ft->slots, ft->nslots, dc + 1);
+      return 0;
+    });
+  } while (!rc && appended > cap);
   if (rc) return rc;
   ft->len -= cnt;
   if (n_removed) *n_removed = cnt;

@@ -7,9 +7,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <mutex>
 
 #include "dp_flow.h"
+#include "dp_tables.h"
 
 // A device buffer grown on demand and kept (hipFree synchronises the device,
 // so it never runs on a call that bursts may overlap).
@@ -54,7 +56,28 @@ struct dp_flow_table {
   hipEvent_t last_burst = nullptr;
   bool burst_armed = false;
   FlowScratch scr[4];              // management-call buffers
+  // the masquerade allocator (dp_masq.h): its device buffer (nullptr: none),
+  // its generation (the one the flows' allocations name), the config it was
+  // built from, the image build the table last synced with, the next
+  // generation, the departures' release list
+  uint8_t *mq = nullptr;
+  uint32_t mq_gen = 0;
+  uint32_t mq_next_gen = 1;
+  std::shared_ptr<const dpd::MasqConfig> mq_cfg;
+  uint64_t mq_serial = 0;
+  FlowScratch mq_rel;
 };
+
+// update_nat_allocator (nat/src/masquerade/allocator_writer.rs:120-154) for
+// one flow table and the published image's masquerade config: the same config
+// upgrades the masquerading flows' generation, none drops the allocator and
+// invalidates them, a new one replaces the allocator and carries over the
+// flows it still serves (check_masquerading_flow, flows.rs:94-174).  Once per
+// image build (`serial`); the caller holds ft->mu.  dp_flows.hip.
+int dpf_masq_sync(dp_flow_table *ft, const std::shared_ptr<const dpd::MasqConfig> &cfg, int64_t genid,
+                  uint64_t serial);
+// A destroyed flow table leaves the publish registry (dp_runtime.cpp).
+extern "C" void dpr_forget_flow_table(dp_flow_table *ft);
 
 // Error reporting of the library (dp_last_error), defined in dp_runtime.cpp.
 int dpr_fail(int rc, const char *what, hipError_t e = hipSuccess);

@@ -25,6 +25,7 @@
 #include "../../include/dpgpu.h"
 #include "dp_device.h"
 #include "dp_flow.h"
+#include "dp_masq.h"
 
 namespace {
 
@@ -1645,6 +1646,53 @@ __device__ __forceinline__ void flow_attach(uint32_t slot, uint32_t state, const
   fp.genid = (int64_t)(((uint64_t)w.w << 32) | w.z);
 }
 
+// handle_icmp_error_masquerading (nat/src/masquerade/icmp_handling.rs:16-48)
+// for the active flow an overlay ICMP error names: the embedded packet by the
+// state's reverse_translation_data (state.rs:89-98: a SrcNat state restores
+// the inner destination, a DstNat state the inner source, with its TCP / UDP
+// port or -- translate_inner_icmp, icmp_error_msg.rs:149-173 -- its ICMP
+// identifier), then the error itself by the state (masquerade, packet.rs:
+// 35-195: the address; an error message carries no identifier).  Any failure
+// is InternalFailure.  An unrecoverable error on a one-way flow invalidates
+// the pair (before any flow-filter decision of the burst: mark 0).
+__device__ DP_COLD void icmp_error_masq(const dpf::FlowCtx &fc, const Frame &F, const Hdr &H, State &S,
+                                             FlowPk &fp, uint32_t sl, uint32_t st) {
+  const EmbV E = emb_view(F, H);
+  const dpf::FlowSlot *fs = fc.slots + sl;
+  const uint4 pfa = ld4(&fs->pf), pfb = ld4(&fs->pf_ip[2]);
+  const uint32_t act = pfa.x & 0xffu, nfs = (pfa.x >> 8) & 0xffu, port = pfa.x >> 16;
+  const uint32_t ip[4] = {pfa.z, pfa.w, pfb.x, pfb.y};
+  const uint32_t fam = pfb.z;
+  const bool inner_src = act == DP_PF_DST_NAT;
+  const bool unicast = fam == 4 ? !((ip[0] >> 28) == 0xe || ip[0] == 0xffffffffu) : (ip[0] >> 24) != 0xff;
+  // the inner side needs a unicast address (DstNat), the outer one too (SrcNat)
+  if ((int)fam != E.net || !unicast) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
+  const int ao = E.off + (E.net == 4 ? (inner_src ? 12 : 16) : (inner_src ? 8 : 24));
+  for (int j = 0; j < (E.net == 4 ? 1 : 4); j++) wput32(F, ao + 4 * j, ip[j]);
+  if (E.tk == L4_TCP || E.tk == L4_UDP) {
+    if (port == 0) { done(S, DP_DONE_INTERNAL_FAILURE); return; }  // InvalidPort
+    if (F.be16(E.t_off + (inner_src ? 0 : 2)) != port) wput16(F, E.t_off + (inner_src ? 0 : 2), port);
+  } else if (inner_src && F.be16(E.t_off + 4) != port) {
+    // the embedded ICMP query's identifier (icmp_error_check: it has one)
+    wput16(F, E.t_off + 4, port);
+  }
+  const bool osrc = act == DP_PF_SRC_NAT;
+  bool mod = false;
+  if (H.net == 4) {
+    uint32_t &a = osrc ? S.v4src : S.v4dst;
+    if (a != ip[0]) { a = ip[0]; mod = true; }
+  } else {
+    const int oo = H.net_off + (osrc ? 8 : 24);
+    for (int j = 0; j < 4; j++)
+      if (F.be32(oo + 4 * j) != ip[j]) { wput32(F, oo + 4 * j, ip[j]); mod = true; }
+  }
+  if (mod) S.flags |= DP_META_REFR_CHKSUM | (osrc ? DP_META_NATTED_SRC : DP_META_NATTED_DST);
+  const uint8_t t = F.b(H.l4_off), c = F.b(H.l4_off + 1);
+  const bool unrec = H.l4 == L4_ICMP4 ? (t == 3 && c != 4) : t == 1;
+  if (unrec && nfs == DP_NFS_ONE_WAY) { fp.ev2 = sl; fp.ev2_tag = st; }
+  S.flags |= DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST;
+}
+
 // IcmpErrorHandler with a flow table (nat/src/icmp_handler/nf.rs:102-152):
 // the embedded packet's flow key, reversed, from the error's source VPC
 // (embedded_flowkey flow_key.rs:635-660, FlowKey::reverse :567-576).  A flow
@@ -1679,10 +1727,11 @@ __device__ __forceinline__ void icmp_error_flow(const dpf::FlowCtx &fc, const Fr
   if (sl == dpf::kNoSlot) return;  // no flow: let it through (nf.rs:114-121)
   if (v.x != DP_FLOW_ACTIVE) { done(S, DP_DONE_FILTERED); return; }  // nf.rs:126-130
   S.dst_vni = v.z;                                                   // nf.rs:139-140
-  if (!(v.y & dpf::kFlagPf)) { done(S, DP_DONE_FILTERED); return; }  // no NAT state (:143-152)
+  if (!(v.y & (dpf::kFlagPf | dpf::kFlagMasq))) { done(S, DP_DONE_FILTERED); return; }  // no NAT state (:143-152)
 #ifdef DP_X_NOICMP
   return;
 #endif
+  if (v.y & dpf::kFlagMasq) { icmp_error_masq(fc, F, H, S, fp, sl, st); return; }
   // handle_icmp_error_port_forwarding (nat/src/portfw/icmp_handling.rs:51-90):
   // the embedded packet back to its form before the flow's translation
   // (nat_translate_icmp_inner, icmp_error_msg.rs:46-146: DstNat state ->
@@ -2148,19 +2197,24 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY) || S.dst_vni) return;
   uint8_t gate = 0;  // SourceGate of the local lookup
+  uint32_t gate_vni = 0;  // GateVni of the remote lookup (LookupInput.dst_vpcd; 0: None)
   if constexpr (FL) {
     if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid) {
       S.dst_vni = fp.dst_vni;
+      if (fp.fflags & dpf::kFlagMasq) S.flags |= DP_META_REQ_MASQUERADE;
       if (fp.fflags & dpf::kFlagPf) S.flags |= DP_META_REQ_PORT_FORWARDING;
       if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_SRC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
       if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_DST) S.flags |= DP_META_REQ_STATIC_NAT_DST;
       return;
     }
-    // flow_revalidation_data (:296-325): the reply flow of a port-forwarded
-    // pair is revalidated against the local rules gated on PortFwdReply
-    if (fp.slot != dpf::kNoSlot && fp.active && fp.genid < fc->genid && !(fp.fflags & DP_FLOW_INITIATOR) &&
-        (fp.fflags & dpf::kFlagPf))
-      gate = 1;
+    // flow_revalidation_data (:296-325): the reply flow of a masqueraded pair
+    // is revalidated against the remote rules gated on its destination VPC,
+    // that of a port-forwarded pair against the local rules gated on
+    // PortFwdReply
+    if (fp.slot != dpf::kNoSlot && fp.active && fp.genid < fc->genid && !(fp.fflags & DP_FLOW_INITIATOR)) {
+      if (fp.fflags & dpf::kFlagMasq) gate_vni = fp.dst_vni;
+      else if (fp.fflags & dpf::kFlagPf) gate = 1;
+    }
   }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
   if (!S.src_vni) { done(S, DP_DONE_UNROUTABLE); return; }
@@ -2168,11 +2222,16 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   int t = H.net == 4 ? 0 : 1;
   Key128 src = key_of(F, H, S, true), dst = key_of(F, H, S, false);
   const VniRec &VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
-  const int32_t rg = VR.ffr[t];
+  int32_t rg = VR.ffr[t];
   // v4 candidate-list group: walk its index straight from the VNI context
-  const uint32_t pre = (t == 0 && VR.ffr4.root) ? mbi_walk(g, VR.ffr4, mbi_key(S, VR.ffr4.field, false) *
-                                                                          (VR.ffr4.field & 1))
-                                                : NO_PRE;
+  uint32_t pre = (t == 0 && VR.ffr4.root) ? mbi_walk(g, VR.ffr4, mbi_key(S, VR.ffr4.field, false) *
+                                                                    (VR.ffr4.field & 1))
+                                          : NO_PRE;
+  if (gate_vni) {  // the (src, GateVni) group: no hoisted walk, the classifier walks it
+    uint32_t gi;
+    rg = hash_find(g, g.im.ff_remote[t].groups, S.src_vni, gate_vni, 0, gi) ? (int32_t)gi : -1;
+    pre = NO_PRE;
+  }
   const Hit rh = classify<W_ACTION | W_ACTION2 | W_AUX>(g, CLS_ARRAYS(ff_remote, t), rg, t, proto,
                                                        Key128{0, 0}, dst, 0, S.dport, pre);
   if (rh.rule < 0) {
@@ -2206,11 +2265,12 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   if (snat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
   if (dnat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_DST;
   if (snat == DP_NAT_PORT_FORWARDING || dnat == DP_NAT_PORT_FORWARDING) S.flags |= DP_META_REQ_PORT_FORWARDING;
+  if (snat == DP_NAT_MASQUERADE || dnat == DP_NAT_MASQUERADE) S.flags |= DP_META_REQ_MASQUERADE;
   if constexpr (FL) {
-    // the key before static NAT, for the flow pair port forwarding creates
-    // (lib.rs:193-201): recorded in the packet's port-forwarding record
+    // the key before static NAT, for the flow pair port forwarding or
+    // masquerade creates (lib.rs:193-201): recorded in the packet's NAT record
 #ifndef DP_X_NOIKEY
-    if ((S.flags & DP_META_REQ_PORT_FORWARDING) &&
+    if ((S.flags & (DP_META_REQ_PORT_FORWARDING | DP_META_REQ_MASQUERADE)) &&
         (S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST)) && !fc->replay) {
       dpf::FKey k;
       if (packet_fkey(F, H, S, k)) {
@@ -2226,8 +2286,9 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
     // is outdated if its destination or its NAT requirements differ, or if
     // it no longer needs state
     if (fp.slot != dpf::kNoSlot && fp.genid != fc->genid) {
-      const bool pf = S.flags & DP_META_REQ_PORT_FORWARDING, need = fp.fflags & dpf::kFlagPf;
-      if (fp.dst_vni != dvni || (S.flags & DP_META_REQ_MASQUERADE) || pf != need || !pf) fp.ev0 = fp.slot;
+      const bool pf = S.flags & DP_META_REQ_PORT_FORWARDING, need_pf = fp.fflags & dpf::kFlagPf;
+      const bool mq = S.flags & DP_META_REQ_MASQUERADE, need_mq = fp.fflags & dpf::kFlagMasq;
+      if (fp.dst_vni != dvni || mq != need_mq || pf != need_pf || (!pf && !mq)) fp.ev0 = fp.slot;
     }
   }
 }
@@ -2322,11 +2383,76 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
   }
 }
 
+// The NAT record of a packet that reached PortForwarder or Masquerade in the
+// first pass (dpf::PfReq): what the sequential NAT pass (dp_pf_resolve) needs
+// to run the reference's NFs over it in packet order.  The packet stops here;
+// the replay pass finishes it with the pass's decisions.
+__device__ __forceinline__ void nat_record(const Frame &F, const Hdr &H, const State &S, FlowPk &fp,
+                                           const dpf::FlowCtx *fc, uint32_t idx) {
+  const uint32_t rec = fp.pf_rec != dpf::kNoSlot ? fp.pf_rec : atomicAdd(&fc->pf_cnt[0], 1u);
+  dpf::PfReq *R = fc->pf + rec;
+  uint32_t bits = (fp.pf_rec != dpf::kNoSlot ? R->bits : 0u) | dpf::kPqReached | dpf::kPqEth;
+  if (S.flags & DP_META_REQ_PORT_FORWARDING) bits |= dpf::kPqPf;
+  if (S.flags & DP_META_REQ_MASQUERADE) bits |= dpf::kPqMasq;
+  if (H.l4 == L4_TCP) bits |= dpf::kPqTcp;
+  if (H.l4 == L4_UDP) bits |= dpf::kPqUdp;
+  if (H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) {
+    bits |= dpf::kPqIcmp;
+    // IcmpProtoKey::new_icmp_v4/v6 (flow_key.rs:318-338): Echo Request / Reply
+    const uint8_t t = F.b(H.l4_off), c = F.b(H.l4_off + 1);
+    if (c == 0 && (H.l4 == L4_ICMP6 ? (t == 128 || t == 129) : (t == 0 || t == 8))) bits |= dpf::kPqQuery;
+  }
+  if (fp.sens) bits |= dpf::kPqSens;
+  if (S.flags & DP_META_REQ_STATIC_NAT_SRC) bits |= dpf::kPqSnatSrc;
+  if (S.flags & DP_META_REQ_STATIC_NAT_DST) bits |= dpf::kPqSnatDst;
+  R->idx = idx;
+  R->slot = fp.slot;
+  R->state = fp.state;
+  if (fp.slot != dpf::kNoSlot) {
+    bits |= dpf::kPqRelated;
+    R->status0 = fp.active ? DP_FLOW_ACTIVE : DP_FLOW_CANCELLED;
+    R->fflags0 = fp.fflags;
+    R->dst_vni0 = fp.dst_vni;
+    R->related0 = fp.related;
+    R->related_tag0 = fp.related_tag;
+    R->genid0 = fp.genid;
+  }
+  R->bits = bits;
+  R->src_vni = S.src_vni;
+  R->dst_vni = S.dst_vni;
+  const uint32_t tflags = H.l4 == L4_TCP ? F.b(H.l4_off + 13) : 0u;
+  R->proto = (uint32_t)net_proto(F, H) | ((uint32_t)H.net << 8) | (tflags << 16);
+  // TCP / UDP ports; an ICMP query's identifier (its flow key's)
+  R->ports = (bits & dpf::kPqQuery) ? be16_bytes(F, H.l4_off + 4) << 16 : ((uint32_t)S.sport << 16) | S.dport;
+  if (H.net == 4) {
+    R->src[0] = S.v4src; R->dst[0] = S.v4dst;
+    R->src[1] = R->src[2] = R->src[3] = R->dst[1] = R->dst[2] = R->dst[3] = 0;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      R->src[j] = F.be32(H.net_off + 8 + 4 * j);
+      R->dst[j] = F.be32(H.net_off + 24 + 4 * j);
+    }
+  }
+  R->acl_def = fp.def_acl;
+  R->acl_rule6 = fp.acl_rule6;
+  R->acl_over = 0;
+  fc->pf_of[idx] = rec;
+  atomicOr(&fc->pf_bits[idx >> 5], 1u << (idx & 31));
+  atomicOr(&fc->pf_sum[idx >> 15], 1u << ((idx >> 10) & 31));
+  fp.pf_rec = rec;
+  fp.deferred = true;
+}
+
+__device__ __forceinline__ bool icmp_error_pkt(const Frame &F, const Hdr &H) {
+  return (H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) && icmp_err_at(F, H.l4_off, H.l4 == L4_ICMP6);
+}
+
 // PortForwarder (nat/src/portfw/nf.rs:373-397) for a packet that requires
 // port forwarding and is not an ICMP error.  Its outcome depends on the flow
 // states the earlier packets of the burst leave (NatFlowStatus, expiry,
 // invalidations, the flow pairs they create), so the first pass records the
-// packet (dpf::PfReq) and stops it here; dp_pf_resolve runs the reference's
+// packet (nat_record) and stops it here; dp_pf_resolve runs the reference's
 // PortForwarder over the records in packet order, and the replay pass takes
 // each packet through the rest of the path with its decision.  Without a
 // flow table (whose Arc the reference's PortForwarder always holds) the
@@ -2335,57 +2461,14 @@ template <bool FL>
 __device__ __forceinline__ void stage_portfw(const Frame &F, const Hdr &H, State &S, FlowPk &fp,
                                              const dpf::FlowCtx *fc, uint32_t idx, const dpf::PfReq *rp) {
   if (S.done != DONE_NONE || !(S.flags & DP_META_REQ_PORT_FORWARDING)) return;
-  if ((H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) && icmp_err_at(F, H.l4_off, H.l4 == L4_ICMP6)) return;
+  if (icmp_error_pkt(F, H)) return;
   if constexpr (!FL) {
     done(S, DP_DONE_INTERNAL_FAILURE);
   } else if (!rp) {
 #ifdef DP_X_NOREC
     fp.deferred = true; return;
 #endif
-    const uint32_t rec = fp.pf_rec != dpf::kNoSlot ? fp.pf_rec : atomicAdd(&fc->pf_cnt[0], 1u);
-    dpf::PfReq *R = fc->pf + rec;
-    uint32_t bits = (fp.pf_rec != dpf::kNoSlot ? R->bits : 0u) | dpf::kPqReached | dpf::kPqEth;
-    if (H.l4 == L4_TCP) bits |= dpf::kPqTcp;
-    if (H.l4 == L4_UDP) bits |= dpf::kPqUdp;
-    if (fp.sens) bits |= dpf::kPqSens;
-    if (S.flags & DP_META_REQ_STATIC_NAT_SRC) bits |= dpf::kPqSnatSrc;
-    if (S.flags & DP_META_REQ_STATIC_NAT_DST) bits |= dpf::kPqSnatDst;
-    R->idx = idx;
-    R->slot = fp.slot;
-    R->state = fp.state;
-    if (fp.slot != dpf::kNoSlot) {
-      bits |= dpf::kPqRelated;
-      R->status0 = fp.active ? DP_FLOW_ACTIVE : DP_FLOW_CANCELLED;
-      R->fflags0 = fp.fflags;
-      R->dst_vni0 = fp.dst_vni;
-      R->related0 = fp.related;
-      R->related_tag0 = fp.related_tag;
-      R->genid0 = fp.genid;
-    }
-    R->bits = bits;
-    R->src_vni = S.src_vni;
-    const uint32_t tflags = H.l4 == L4_TCP ? F.b(H.l4_off + 13) : 0u;
-    R->proto = (uint32_t)net_proto(F, H) | ((uint32_t)H.net << 8) | (tflags << 16);
-    R->ports = ((uint32_t)S.sport << 16) | S.dport;
-    if (H.net == 4) {
-      R->src[0] = S.v4src; R->dst[0] = S.v4dst;
-      R->src[1] = R->src[2] = R->src[3] = R->dst[1] = R->dst[2] = R->dst[3] = 0;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        R->src[j] = F.be32(H.net_off + 8 + 4 * j);
-        R->dst[j] = F.be32(H.net_off + 24 + 4 * j);
-      }
-    }
-    R->acl_def = fp.def_acl;
-    R->acl_rule6 = fp.acl_rule6;
-    R->acl_over = 0;
-    R->src_vni = S.src_vni;
-    fc->pf_of[idx] = rec;
-    atomicOr(&fc->pf_bits[idx >> 5], 1u << (idx & 31));
-    atomicOr(&fc->pf_sum[idx >> 15], 1u << ((idx >> 10) & 31));
-    fp.pf_rec = rec;
-    fp.deferred = true;
+    nat_record(F, H, S, fp, fc, idx);
   } else {
     // a flow pair refused at capacity was translated before the inserts
     // (do_port_forwarding, nf.rs:142-163): its metadata says so
@@ -2410,6 +2493,57 @@ __device__ __forceinline__ void stage_portfw(const Frame &F, const Hdr &H, State
     }
     if (mod) S.flags |= DP_META_REFR_CHKSUM | (src ? DP_META_NATTED_SRC : DP_META_NATTED_DST);
     if (v != dpf::kPfForward) done(S, (uint8_t)v);
+  }
+}
+
+// Masquerade (nat/src/masquerade/nf.rs:511-586) for a packet that requires
+// masquerading and is not an ICMP error: like PortForwarder, its outcome
+// rests on what the earlier packets of the burst did to the flows and to the
+// allocator, so the first pass records it (one record with PortForwarder's
+// when the packet needs both) and dp_pf_resolve decides.  The replay applies
+// the decision: masquerade (packet.rs:35-195) -- the address, a TCP / UDP
+// port always, an ICMP query identifier when it changes -- and the checksum
+// refresh the NF always asks for.  Without a flow table: InternalFailure.
+template <bool FL>
+__device__ __forceinline__ void stage_masquerade(const Frame &F, const Hdr &H, State &S, FlowPk &fp,
+                                                 const dpf::FlowCtx *fc, uint32_t idx, const dpf::PfReq *rp) {
+  if (S.done != DONE_NONE || !(S.flags & DP_META_REQ_MASQUERADE)) return;
+  if (icmp_error_pkt(F, H)) return;
+  if constexpr (!FL) {
+    done(S, DP_DONE_INTERNAL_FAILURE);
+  } else if (!rp) {
+    if (!fp.deferred) nat_record(F, H, S, fp, fc, idx);
+  } else {
+    const uint32_t v = rp->mverdict;
+    if (v != dpf::kPfForward) { done(S, (uint8_t)v); return; }
+    const bool src = (rp->mnat & 0xffu) == DP_PF_SRC_NAT, ident = rp->mnat & 0x100u;
+    const uint16_t port = (uint16_t)(rp->mnat >> 16);
+    bool mod = false;
+    if (H.net == 4) {
+      uint32_t &a = src ? S.v4src : S.v4dst;
+      if (a != rp->mnat_ip[0]) { a = rp->mnat_ip[0]; mod = true; }
+    } else {
+      const int oo = H.net_off + (src ? 8 : 24);
+      for (int j = 0; j < 4; j++)
+        if (F.be32(oo + 4 * j) != rp->mnat_ip[j]) { wput32(F, oo + 4 * j, rp->mnat_ip[j]); mod = true; }
+    }
+    if (H.l4 == L4_TCP || H.l4 == L4_UDP) {
+      if (!ident) {  // NatPort::Port: set, changed or not
+        (src ? S.sport : S.dport) = port;
+        mod = true;
+      }
+    } else if (ident) {
+      // an ICMP query's identifier (icmp_full_identifier: v4 echo / timestamp,
+      // v6 echo, code 0), only if it changes
+      const uint8_t t = F.b(H.l4_off), c = F.b(H.l4_off + 1);
+      const bool q = c == 0 && (H.l4 == L4_ICMP6 ? (t == 128 || t == 129) : (t == 0 || t == 8 || t == 13 || t == 14));
+      if (q && F.be16(H.l4_off + 4) != port) {
+        wput16(F, H.l4_off + 4, port);
+        mod = true;
+      }
+    }
+    if (mod) S.flags |= src ? DP_META_NATTED_SRC : DP_META_NATTED_DST;
+    S.flags |= DP_META_REFR_CHKSUM;
   }
 }
 
@@ -2904,6 +3038,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
 #ifndef DP_X_NOPF
   stage_portfw<FL>(F, H, S, fp, fc, idx, rp);
 #endif
+  stage_masquerade<FL>(F, H, S, fp, fc, idx, rp);
   if constexpr (FL) {
     if (fp.deferred) {  // finished by the replay pass
       o.done = DONE_NONE;
@@ -3297,6 +3432,14 @@ struct Seq {
       fc.pf_repl[4 * r + 1] = fc.slots[sl].state;
       fc.pf_repl[4 * r + 2] = idx;
       fc.pf_repl[4 * r + 3] = fc.slots[sl].mark;
+      // its FlowInfo is dropped when the burst ends, and with it the
+      // allocation its masquerade state owns
+      const dpf::FlowSlot &o = fc.slots[sl];
+      if ((o.flags & dpf::kFlagMasq) && o.mq_rec && o.mq_gen == fc.mq_gen && fc.mq) {
+        const uint32_t k = fc.pf_cnt[3]++;
+        fc.mq_rel[2 * k] = o.mq_rec - 1;
+        fc.mq_rel[2 * k + 1] = o.pf >> 16;
+      }
     } else {
       if (len >= fc.hard) return dpf::kNoSlot;  // the table stays at most 7/8 full
       if (free_ == dpf::kNoSlot) {  // beyond the probe bound: the first free slot further on
@@ -3321,6 +3464,7 @@ struct Seq {
     s.related = dpf::kNoSlot;
     s.related_tag = 0;
     s.mark = dpf::kIdleMark;
+    s.mq_rec = 0;
     s.state = ((((old >> 2) + 1) & 0x3fffffffu) << 2) | dpf::FS_FULL;
     return sl;
   }
@@ -3328,8 +3472,8 @@ struct Seq {
 
 __device__ inline uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
-// One record, in packet order.
-__device__ void resolve_one(const Seq &q, dpf::PfReq &R) {
+// PortForwarder for one record, in packet order.
+__device__ void resolve_pf(const Seq &q, dpf::PfReq &R) {
   const dpf::FlowCtx &fc = q.fc;
   const Img &g = q.g;
   const uint32_t idx = R.idx;
@@ -3354,6 +3498,7 @@ __device__ void resolve_one(const Seq &q, dpf::PfReq &R) {
       }
     }
   }
+  if (!(R.bits & dpf::kPqPf)) return;
   const uint32_t fam = (R.proto >> 8) & 0xffu, proto = R.proto & 0xffu, tfl = R.proto >> 16;
   const bool tcp = R.bits & dpf::kPqTcp, ports = R.bits & (dpf::kPqTcp | dpf::kPqUdp);
   const uint32_t sport = R.ports >> 16, dport = R.ports & 0xffffu;
@@ -3470,6 +3615,208 @@ __device__ void resolve_one(const Seq &q, dpf::PfReq &R) {
   Rv.related_tag = F.state;
 }
 
+// ---------------------------------------------------------------------------
+// Masquerade: the sequential pass (nat/src/masquerade/nf.rs:384-586)
+// ---------------------------------------------------------------------------
+constexpr uint64_t kMasqOneWayNs = 5000000000ull;   // MASQUERADE_ONEWAY_TIMEOUT (nf.rs:86)
+constexpr uint64_t kMasqTwoWayNs = 3000000000ull;   // MASQUERADE_TWOWAY_TIMEOUT (:87)
+constexpr uint64_t kMasqClosingNs = 2000000000ull;  // MASQUERADE_CLOSING_TIMEOUT (:88)
+
+// next_flow_status (masquerade/protocol.rs:93-116) on the IP header's next
+// header: UDP (a DstNat reply from port 53 / 853 / 8853 closes), ICMP, TCP by
+// its flags -- port forwarding's machine with the initiator's side SrcNat
+__device__ uint32_t masq_next_status(uint32_t proto, bool udp_hdr, uint32_t sport, uint32_t tfl, bool tcp_hdr,
+                                     uint32_t act, uint32_t st) {
+  const bool snat = act == DP_PF_SRC_NAT;
+  if (proto == 17) {
+    uint32_t n = st;
+    if (snat) { if (st == DP_NFS_TWO_WAY) n = DP_NFS_ESTABLISHED; }
+    else if (st == DP_NFS_ONE_WAY) n = DP_NFS_TWO_WAY;
+    if (!snat && udp_hdr && (sport == 53 || sport == 853 || sport == 8853)) n = DP_NFS_CLOSED;
+    return n;
+  }
+  if (proto == 1 || proto == 58) return (!snat && st == DP_NFS_ONE_WAY) ? (uint32_t)DP_NFS_TWO_WAY : st;
+  if (proto == 6 && tcp_hdr) return next_status(true, tfl, snat ? DP_PF_DST_NAT : DP_PF_SRC_NAT, st);
+  return st;
+}
+
+// From<&AllocatorError> for DoneReason (allocation.rs:59-73)
+__device__ uint32_t masq_done(uint32_t e) {
+  switch (e) {
+    case dpm::NO_FREE_IP: case dpm::NO_PORT_BLOCK: case dpm::NO_FREE_PORT: return DP_DONE_NAT_OUT_OF_RESOURCES;
+    case dpm::PORT_ALLOC_FAILED: case dpm::PORT_RESERVATION_FAILED: return DP_DONE_NAT_FAILURE;
+    case dpm::INTERNAL: return DP_DONE_INTERNAL_FAILURE;
+    default: return DP_DONE_FILTERED;  // Denied, NoPoolFound
+  }
+}
+
+// Masquerade::masquerade_packet (nf.rs:384-475) for one record, after its
+// PortForwarder decision (the packet as PortForwarder left it).
+__device__ void resolve_masq(const Seq &q, dpf::PfReq &R) {
+  const dpf::FlowCtx &fc = q.fc;
+  const uint32_t idx = R.idx;
+  const uint32_t fam = (R.proto >> 8) & 0xffu, proto = R.proto & 0xffu, tfl = R.proto >> 16;
+  const bool tcp = R.bits & dpf::kPqTcp, udp = R.bits & dpf::kPqUdp, icmp = R.bits & dpf::kPqIcmp;
+  // the current addresses and ports: PortForwarder's translation applied
+  uint32_t src[4], dst[4];
+  uint32_t sport = R.ports >> 16, dport = R.ports & 0xffffu;
+  for (int j = 0; j < 4; j++) { src[j] = R.src[j]; dst[j] = R.dst[j]; }
+  if ((R.bits & dpf::kPqPf) && (R.nat & 0xffu)) {
+    const bool s = (R.nat & 0xffu) == DP_PF_SRC_NAT;
+    for (int j = 0; j < 4; j++) (s ? src : dst)[j] = R.nat_ip[j];
+    if (tcp || udp) (s ? sport : dport) = R.nat >> 16;
+  }
+  // get_masquerade_state (nf.rs:198-213): the attached flow, still that fill,
+  // Active for this packet (its own PortForwarder step included), with state
+  const bool same = R.slot != dpf::kNoSlot && q.alive(R.slot, R.state);
+  const bool valid = same && R.status0 == DP_FLOW_ACTIVE && q.pair_valid(R.slot, idx + 1);
+  if (valid && (fc.slots[R.slot].flags & dpf::kFlagMasq)) {
+    dpf::FlowSlot &f = fc.slots[R.slot];
+    const uint32_t act = f.pf & 0xffu, port = f.pf >> 16;
+    const bool ident = f.flags & dpf::kFlagMasqIdent;
+    // refresh_masquerade_state (nf.rs:151-194)
+    const uint32_t cur = (f.pf >> 8) & 0xffu;
+    const uint32_t nw = masq_next_status(proto, udp, sport, tfl, tcp, act, cur);
+    q.set_nfs(R.slot, nw);
+    if (nw == DP_NFS_CLOSED || nw == DP_NFS_RESET) {
+      q.invalidate(R.slot, idx);  // and the packet is still translated
+    } else if (nw != DP_NFS_ONE_WAY) {
+      const uint64_t ext = nw == DP_NFS_TWO_WAY ? kMasqTwoWayNs
+                         : nw == DP_NFS_ESTABLISHED ? (uint64_t)f.pf_rule * 1000000000ull : kMasqClosingNs;
+      q.reset_expiry(R.slot, ext);
+      if (nw == DP_NFS_ESTABLISHED && nw != cur && q.alive(f.related, f.related_tag)) q.reset_expiry(f.related, ext);
+    }
+    // masquerade (packet.rs:35-195): a SrcNat state needs a unicast address, the
+    // packet one of the state's family and a TCP / UDP / ICMP header
+    if ((act == DP_PF_SRC_NAT && !unicast(f.pf_fam, f.pf_ip)) || f.pf_fam != fam || !(tcp || udp || icmp)) {
+      R.mverdict = DP_DONE_NAT_FAILURE;
+      return;
+    }
+    R.mnat = act | (ident ? 0x100u : 0u) | (port << 16);
+    for (int j = 0; j < 4; j++) R.mnat_ip[j] = f.pf_ip[j];
+    return;
+  }
+  dpm::View V{fc.mq};
+  if (!fc.mq) { R.mverdict = DP_DONE_NAT_FAILURE; return; }  // NoAllocator
+  if (tcp && !((tfl & 2) && !(tfl & 0x3du))) { R.mverdict = DP_DONE_FILTERED; return; }  // TCP without SYN
+  // FlowKey::try_from(&Packet) (flow_key.rs:589-621): the current key
+  uint32_t kind;
+  if (tcp) kind = DP_FLOW_TCP;
+  else if (udp) kind = DP_FLOW_UDP;
+  else if (icmp) kind = (R.bits & dpf::kPqQuery) ? DP_FLOW_ICMP_QUERY : DP_FLOW_ICMP_OTHER;
+  else { R.mverdict = DP_DONE_MALFORMED; return; }  // FlowKeyError
+  const uint32_t cports = kind == DP_FLOW_ICMP_OTHER ? 0u : ((sport << 16) | dport);
+  dpf::FKey ck, ik;
+  ck.w[0] = R.src_vni;
+  ck.w[1] = fam | (kind << 8);
+  ck.w[2] = cports;
+  for (int j = 0; j < 4; j++) { ck.w[3 + j] = bswap(src[j]); ck.w[7 + j] = bswap(dst[j]); }
+  // the initial key: the one before static NAT, else the current one
+  if (R.bits & dpf::kPqIkey) for (int j = 0; j < 11; j++) ik.w[j] = R.ikey[j];
+  else ik = ck;
+  const uint32_t ifam = ik.w[1] & 0xffu, ikind = ik.w[1] >> 8;
+  const uint32_t iproto = ikind == DP_FLOW_TCP ? 6u : ikind == DP_FLOW_UDP ? 17u : ifam == 4 ? 1u : 58u;
+  // NatAllocator::allocate (apalloc/mod.rs:317-375): the pool of (protocol,
+  // VPCs, original source); a port, or an ICMP identifier (port 0 allowed)
+  dpm::A128 sip{};
+  if (ifam == 4) sip.w[3] = bswap(ik.w[3]);
+  else for (int j = 0; j < 4; j++) sip.w[j] = bswap(ik.w[3 + j]);
+  const uint32_t set = dpm::lookup(V, iproto | (ifam << 8), R.src_vni, R.dst_vni, sip);
+  if (set == dpm::kNone) { R.mverdict = DP_DONE_FILTERED; return; }  // Denied
+  uint32_t rec = 0, aport = 0;
+  const bool allow_null = iproto == 1 || iproto == 58;
+  const uint32_t e = dpm::set_alloc(V, set, allow_null, rec, aport);
+  if (e != dpm::OK) { R.mverdict = masq_done(e); return; }
+  const dpm::A128 aa = dpm::addr_of(V, V.recs()[rec]);
+  uint32_t aip[4] = {0, 0, 0, 0};  // big-endian words, v4 in word 0
+  if (fam == 4) aip[0] = aa.w[3];
+  else for (int j = 0; j < 4; j++) aip[j] = aa.w[j];
+  if (!unicast(fam, aip)) { dpm::release(V, rec, aport); R.mverdict = DP_DONE_FILTERED; return; }
+  // create_flow_pair (nf.rs:265-325): the reverse of the current key towards
+  // the allocated tuple (new_reverse_session, :327-373)
+  dpf::FKey rk;
+  rk.w[0] = R.dst_vni;
+  rk.w[1] = ck.w[1];
+  for (int j = 0; j < 4; j++) { rk.w[3 + j] = ck.w[7 + j]; rk.w[7 + j] = bswap(aip[j]); }
+  if (kind == DP_FLOW_TCP || kind == DP_FLOW_UDP) {
+    if (aport == 0) { dpm::release(V, rec, aport); R.mverdict = DP_DONE_MALFORMED; return; }  // InvalidPort
+    rk.w[2] = (dport << 16) | aport;
+  } else if (kind == DP_FLOW_ICMP_QUERY) {
+    rk.w[2] = aport << 16;
+  } else {
+    dpm::release(V, rec, aport);
+    R.mverdict = DP_DONE_NAT_FAILURE;  // UnexpectedKeyVariant
+    return;
+  }
+  // get_reverse_mapping: the original source tuple
+  if (ikind != DP_FLOW_TCP && ikind != DP_FLOW_UDP && ikind != DP_FLOW_ICMP_QUERY) {
+    dpm::release(V, rec, aport);
+    R.mverdict = DP_DONE_NAT_FAILURE;  // IcmpUnsupportedCategory
+    return;
+  }
+  const uint32_t rport = ik.w[2] >> 16;
+  const bool rident = ikind == DP_FLOW_ICMP_QUERY;
+  bool eq = true;
+  for (int j = 0; j < 11; j++) eq = eq && ik.w[j] == rk.w[j];
+  if (eq) { dpm::release(V, rec, aport); R.mverdict = DP_DONE_INTERNAL_FAILURE; return; }  // related_pair
+  const bool ss = R.bits & dpf::kPqSnatSrc, sd = R.bits & dpf::kPqSnatDst;
+  const uint32_t fw_flags = DP_FLOW_INITIATOR | (ss ? DP_FLOW_REQ_STATIC_NAT_SRC : 0u) |
+                            (sd ? DP_FLOW_REQ_STATIC_NAT_DST : 0u);
+  const uint32_t rv_flags = (ss ? DP_FLOW_REQ_STATIC_NAT_DST : 0u) | (sd ? DP_FLOW_REQ_STATIC_NAT_SRC : 0u);
+  const int64_t genid = V.h().genid;  // set_genid_pair(allocator.genid())
+  const uint64_t exp = fc.now + kMasqOneWayNs;
+  const uint32_t idle_s = (uint32_t)(V.sets()[set].idle_ns / 1000000000ull);
+  const uint32_t sf = q.insert(ik, false, idx);
+  if (sf == dpf::kNoSlot) {  // the allocation drops here
+    dpm::release(V, rec, aport);
+    R.mverdict = DP_DONE_FLOW_CAPACITY_EXCEEDED;
+    return;
+  }
+  dpf::FlowSlot &F = fc.slots[sf];
+  F.flags = fw_flags | dpf::kFlagMasq | (allow_null ? dpf::kFlagMasqIdent : 0u);
+  F.dst_vni = R.dst_vni;  // setup_flow_masquerade_state: the forward flow to dst_vpcd
+  F.genid = genid;
+  F.expires_at = exp;
+  F.pf = DP_PF_SRC_NAT | (aport << 16);  // NatFlowStatus::OneWay
+  F.pf_rule = idle_s;
+  for (int j = 0; j < 4; j++) F.pf_ip[j] = aip[j];
+  F.pf_fam = fam;
+  F.mq_rec = rec + 1;
+  F.mq_gen = fc.mq_gen;
+  const uint32_t sr = q.insert(rk, true, idx);  // admitted at capacity: its related flow is Active
+  if (sr == dpf::kNoSlot) {
+    q.invalidate(sf, idx);
+    R.mverdict = DP_DONE_FLOW_CAPACITY_EXCEEDED;
+    return;
+  }
+  dpf::FlowSlot &Rv = fc.slots[sr];
+  Rv.flags = rv_flags | dpf::kFlagMasq | (rident ? dpf::kFlagMasqIdent : 0u);
+  Rv.dst_vni = R.src_vni;  // the reverse one to src_vpcd
+  Rv.genid = genid;
+  Rv.expires_at = exp;
+  Rv.pf = DP_PF_DST_NAT | (rport << 16);
+  Rv.pf_rule = idle_s;
+  for (int j = 0; j < 4; j++) Rv.pf_ip[j] = 0;
+  if (ifam == 4) Rv.pf_ip[0] = bswap(ik.w[3]);
+  else for (int j = 0; j < 4; j++) Rv.pf_ip[j] = bswap(ik.w[3 + j]);
+  Rv.pf_fam = ifam;
+  F.related = sr;
+  F.related_tag = Rv.state;
+  Rv.related = sf;
+  Rv.related_tag = F.state;
+  // the packet with the forward state (no Ethernet header: a failure that
+  // invalidates the new pair -- never here, every frame has one)
+  R.mnat = DP_PF_SRC_NAT | (allow_null ? 0x100u : 0u) | (aport << 16);
+  for (int j = 0; j < 4; j++) R.mnat_ip[j] = aip[j];
+}
+
+// One record, in packet order: PortForwarder, then Masquerade on what it left.
+__device__ void resolve_one(const Seq &q, dpf::PfReq &R) {
+  R.mverdict = dpf::kPfForward;
+  resolve_pf(q, R);
+  if ((R.bits & dpf::kPqMasq) && R.verdict == dpf::kPfForward) resolve_masq(q, R);
+}
+
 }  // namespace pfw
 
 #if DP_IN_PART(0)
@@ -3523,6 +3870,12 @@ __global__ void __launch_bounds__(1024) dp_pf_resolve(const uint8_t *__restrict_
   const Img g{img_base, *im};
   const pfw::Seq q{fc, g};
   for (uint32_t k = 0; k < total; k++) pfw::resolve_one(q, fc.pf[fc.pf_of[fc.pf_order[k]]]);
+  // the flows replaced during the burst are dropped after it, with the
+  // allocations their masquerade state owns
+  if (fc.mq) {
+    const dpm::View V{fc.mq};
+    for (uint32_t k = 0; k < fc.pf_cnt[3]; k++) dpm::release(V, fc.mq_rel[2 * k], fc.mq_rel[2 * k + 1]);
+  }
 }
 
 // After the burst's pipeline kernel (flows variant), on its stream.

@@ -114,6 +114,10 @@ struct DevImage {
   uint8_t *dev = nullptr;
   dpd::Image im{};
   uint64_t im_off = 0;  // the Image descriptor, uploaded after the table bytes
+  // the masquerade config the flow tables build their allocators from, and
+  // this build's serial (a table syncs once per build)
+  std::shared_ptr<const dpd::MasqConfig> masq;
+  uint64_t serial = 0;
   ~DevImage() {
     if (dev) bury(device, dev);  // freed later, off the burst path
   }
@@ -126,7 +130,13 @@ struct DeviceTables {
   std::mutex pub_mu;
   std::shared_ptr<DevImage> cur;
   dpd::PfLineage pf;  // the port-forwarding entries of `cur` (PortFwTable::update lineage)
+  // the flow tables attached to contexts of this device (attach count each):
+  // a publish syncs their masquerade allocators (update_nat_allocator runs
+  // when the config is applied).  Order: pub_mu, then reg_mu, then a table's mu.
+  std::mutex reg_mu;
+  std::map<dp_flow_table *, int> fts;
 };
+std::atomic<uint64_t> g_serial{1};
 
 std::mutex g_dev_mu;
 std::map<int, std::unique_ptr<DeviceTables>> g_dev;
@@ -206,7 +216,7 @@ struct dp_ctx {
   FlowScratch fl_ev, fl_sens;
   // port forwarding scratch (dpf::FlowCtx pf*): records, counters, packet ->
   // record, bitmaps (kept zero between bursts), order, replaced fills
-  FlowScratch pf_req, pf_cnt, pf_of, pf_bits, pf_order, pf_repl;
+  FlowScratch pf_req, pf_cnt, pf_of, pf_bits, pf_order, pf_repl, mq_rel;
   uint64_t pf_bits_n = 0;
   hipEvent_t fl_used = nullptr;
   bool fl_armed = false;
@@ -447,7 +457,14 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   c->fl_ev.release();
   c->fl_sens.release();
-  for (FlowScratch *x : {&c->pf_req, &c->pf_cnt, &c->pf_of, &c->pf_bits, &c->pf_order, &c->pf_repl}) x->release();
+  for (FlowScratch *x : {&c->pf_req, &c->pf_cnt, &c->pf_of, &c->pf_bits, &c->pf_order, &c->pf_repl, &c->mq_rel})
+    x->release();
+  if (c->ft) {
+    DeviceTables &dt = dev_tables(c->device);
+    std::lock_guard<std::mutex> lk(dt.reg_mu);
+    auto it = dt.fts.find(c->ft);
+    if (it != dt.fts.end() && --it->second <= 0) dt.fts.erase(it);
+  }
   if (c->mb_in) (void)hipHostFree(c->mb_in);
   if (c->mb_out) (void)hipHostFree(c->mb_out);
   if (c->mb_meta) (void)hipHostFree(c->mb_meta);
@@ -487,12 +504,24 @@ int dp_tables_publish(dp_ctx_t *c, const dp_tables_desc_t *tables) {
   if ((e = hipMemcpy(img->dev, bi.bytes.data(), bi.bytes.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return fail(DP_EIO, "upload table image", e);
   img->im = bi.im;
+  img->masq = bi.masq;
+  img->serial = g_serial++;
   std::shared_ptr<DevImage> old;
   {
     std::lock_guard<std::mutex> lk(dt.mu);
     old = dt.cur;
     dt.cur = img;
     dt.pf = std::move(pf);
+  }
+  // the attached flow tables' allocators follow the new config now (a table
+  // attached later syncs at its first burst)
+  {
+    std::lock_guard<std::mutex> reg(dt.reg_mu);
+    for (auto &kv : dt.fts) {
+      std::lock_guard<std::mutex> lk(kv.first->mu);
+      if ((rc = dpf_masq_sync(kv.first, img->masq, img->im.genid, img->serial)))
+        return fail(rc, "masquerade allocator update");
+    }
   }
   // `old` is retired here only if no in-flight burst still references it
   return 0;
@@ -548,6 +577,13 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     // earlier flows burst of any context attached to the table
     dp_flow_table *ft = c->ft;
     std::lock_guard<std::mutex> lk(ft->mu);
+    // the table's allocator follows the image's masquerade config
+    if (ft->mq_serial != img->serial) {
+      if ((rc = dpf_masq_sync(ft, img->masq, img->im.genid, img->serial))) {
+        (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
+        return fail(rc, "masquerade allocator update");
+      }
+    }
     if (c->fl_armed && hipStreamWaitEvent(s, c->fl_used, 0) != hipSuccess) return fail(DP_EIO, "stream wait");
     if (ft->burst_armed && hipStreamWaitEvent(s, ft->last_burst, 0) != hipSuccess)
       return fail(DP_EIO, "stream wait (flow table)");
@@ -573,6 +609,11 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.pf_of = static_cast<uint32_t *>(c->pf_of.get(sizeof(uint32_t) * (uint64_t)n));
     fc.pf_order = static_cast<uint32_t *>(c->pf_order.get(sizeof(uint32_t) * (uint64_t)n));
     fc.pf_repl = static_cast<uint32_t *>(c->pf_repl.get(sizeof(uint32_t) * 8 * ((uint64_t)n + 1)));
+    // masquerade: the allocator, and the allocations of replaced fills (at
+    // most two fills per packet) released after the sequential pass
+    fc.mq = ft->mq;
+    fc.mq_gen = ft->mq_gen;
+    fc.mq_rel = static_cast<uint32_t *>(c->mq_rel.get(sizeof(uint32_t) * 4 * ((uint64_t)n + 1)));
     if (words + sum_words > c->pf_bits_n) {
       c->pf_bits.release();
       c->pf_bits_n = 0;
@@ -582,7 +623,7 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     }
     fc.pf_bits = static_cast<uint32_t *>(c->pf_bits.p);
     fc.pf_sum = fc.pf_bits ? fc.pf_bits + words : nullptr;
-    if (!fc.events || !fc.sens || !fc.pf || !fc.pf_cnt || !fc.pf_of || !fc.pf_order || !fc.pf_repl ||
+    if (!fc.events || !fc.sens || !fc.pf || !fc.pf_cnt || !fc.pf_of || !fc.pf_order || !fc.pf_repl || !fc.mq_rel ||
         c->pf_bits_n < words + sum_words) {
       (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
       return fail(DP_ENOMEM, "flow burst scratch");
@@ -628,8 +669,22 @@ int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
   if (ft && ft->device != c->device) return fail(DP_EINVAL, "flow table on another device");
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  DeviceTables &dt = dev_tables(c->device);
+  std::lock_guard<std::mutex> reg(dt.reg_mu);
+  if (c->ft) {
+    auto it = dt.fts.find(c->ft);
+    if (it != dt.fts.end() && --it->second <= 0) dt.fts.erase(it);
+  }
+  if (ft) dt.fts[ft]++;
   c->ft = ft;
   return 0;
+}
+
+// A flow table being destroyed leaves every device's registry.
+void dpr_forget_flow_table(dp_flow_table *ft) {
+  DeviceTables &dt = dev_tables(ft->device);
+  std::lock_guard<std::mutex> reg(dt.reg_mu);
+  dt.fts.erase(ft);
 }
 
 // The device-visible address of pinned, device-mapped host memory (the

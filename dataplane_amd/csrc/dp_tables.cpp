@@ -708,11 +708,11 @@ int load_rules(const dp_rule_t *rs, uint32_t n, int fam, bool by_prio, int kind,
       return DP_EINVAL;                                                   // ACL
     if (kind == 1) {                                                      // FF remote
       if (r.src.len != 0 || r.sport_lo != 0 || r.sport_hi != 65535 || r.gate != 0) return DP_EINVAL;
-      if (r.action2 == DP_NAT_MASQUERADE) return DP_ENOTSUP;
+      if (r.action2 > DP_NAT_PORT_FORWARDING) return DP_EINVAL;           // NatRequirement
     }
     if (kind == 2) {                                                      // FF local
       if (r.dst.len != 0 || r.dport_lo != 0 || r.dport_hi != 65535) return DP_EINVAL;
-      if (r.action == DP_NAT_MASQUERADE) return DP_ENOTSUP;
+      if (r.action > DP_NAT_PORT_FORWARDING) return DP_EINVAL;
       if (r.gate > 1) return DP_EINVAL;                                   // SourceGate
     }
     out.push_back(CRule{r, i});
@@ -1451,6 +1451,47 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   im.n_pf = (uint32_t)pfrecs.size();
 
   section("portfw");
+  // --- masquerade exposes (nat/src/masquerade/): validated and kept with the
+  // image; each flow table builds its allocator from them (dp_masq.h)
+  auto mc = std::make_shared<MasqConfig>();
+  if (d->n_masq && (!d->masq || !d->masq_prefixes)) return DP_EINVAL;
+  if (d->n_masq_claims && !d->masq_claims) return DP_EINVAL;
+  auto put = [&](const void *x, size_t k) { mc->canon.append(static_cast<const char *>(x), k); };
+  for (uint32_t i = 0; i < d->n_masq; i++) {
+    const dp_masq_expose_t &x = d->masq[i];
+    if (!x.src_vni || !x.dst_vni || x.src_vni == x.dst_vni || !x.n_public || !x.n_private) return DP_EINVAL;
+    if ((uint64_t)x.first_prefix + x.n_private + x.n_public > d->n_masq_prefixes) return DP_EINVAL;
+    if ((uint64_t)x.first_claim + x.n_claims > d->n_masq_claims) return DP_EINVAL;
+    MasqExpose e;
+    e.src_vni = x.src_vni;
+    e.dst_vni = x.dst_vni;
+    // the expose's idle timeout, by default 2 minutes (masquerade/state.rs)
+    e.idle_ns = (uint64_t)(x.idle_timeout_s ? x.idle_timeout_s : 120) * 1000000000ull;
+    e.fam = d->masq_prefixes[x.first_prefix].family;
+    for (uint32_t k = 0; k < (uint32_t)x.n_private + x.n_public; k++) {
+      const dp_prefix_t &q = d->masq_prefixes[x.first_prefix + k];
+      if (!valid_prefix(q) || q.family != e.fam) return DP_EINVAL;
+      (k < x.n_private ? e.priv : e.pub).push_back(q);
+    }
+    for (uint32_t k = 0; k < x.n_claims; k++) {
+      const dp_masq_claim_t &c = d->masq_claims[x.first_claim + k];
+      if (!valid_prefix(c.prefix) || c.lo > c.hi) return DP_EINVAL;
+      e.claims.push_back(c);
+    }
+    // canonical bytes: the same layout as the restatement's (a config is
+    // "the same" when these match, absent a tag)
+    put(&x.src_vni, 4); put(&x.dst_vni, 4); put(&e.idle_ns, 8);
+    for (auto *v : {&e.priv, &e.pub}) {
+      const uint32_t m = (uint32_t)v->size();
+      put(&m, 4);
+      for (auto &q : *v) put(&q, sizeof q);
+    }
+    const uint32_t m = (uint32_t)e.claims.size();
+    put(&m, 4);
+    for (auto &c : e.claims) put(&c, sizeof c);
+    mc->exposes.push_back(std::move(e));
+  }
+  mc->tag = d->masq_config_tag;
   ib.alloc(64);
   im.bytes = ib.b.size();
   // context records carry 32-bit image offsets (Mbi)
@@ -1458,6 +1499,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   out.bytes.swap(ib.b);
   out.im = im;
   out.pt_nodes = pb.nodes.size();
+  out.masq = mc;
   if (pf) *pf = std::move(L);
   return 0;
 }

@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <memory>
+#include <string>
 #include <vector>
 
 #include "../../include/dpgpu.h"
@@ -10,10 +12,34 @@
 
 namespace dpd {
 
+// A masquerade expose as the tables hold it (dp_masq_expose_t, validated):
+// one family, private and public prefixes, the port-forwarding claims on its
+// public range.
+struct MasqExpose {
+  uint32_t src_vni, dst_vni;
+  uint64_t idle_ns;
+  int fam;
+  std::vector<dp_prefix_t> priv, pub;
+  std::vector<dp_masq_claim_t> claims;
+};
+// MasqueradeConfig: the exposes, their canonical bytes and the caller's tag
+// (a flow table's allocator is kept across publishes of the same config,
+// nat/src/masquerade/allocator_writer.rs:120-154).  The allocator itself is
+// flow-table state (dp_masq.h), built from this when a table syncs.
+struct MasqConfig {
+  std::vector<MasqExpose> exposes;
+  std::string canon;
+  uint64_t tag = 0;
+  bool same(const MasqConfig &o) const {
+    return tag || o.tag ? tag == o.tag && o.tag != 0 : canon == o.canon;
+  }
+};
+
 struct BuiltImage {
   std::vector<uint8_t> bytes;  // host copy of the device image
   Image im;                    // offsets into `bytes`
   uint64_t pt_nodes = 0;
+  std::shared_ptr<const MasqConfig> masq;  // never null after a successful build
 };
 
 // The port-forwarding entries of a device's current generation (the lineage

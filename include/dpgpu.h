@@ -431,6 +431,10 @@ typedef struct dp_masq_claim {
  * u32 offset bitmap, alloc.rs:349-377, bounded for device memory; each
  * address carries 64512 TCP / UDP ports). */
 #define DP_MASQ_REGION_ADDRS 4096u
+/* Addresses in use at once over one flow table's allocator (each carries its
+ * PortAllocator, ~9 KiB of device memory): a new address past this many fails
+ * as the region's exhaustion does (NoFreeIp; NoPoolFound when reserving). */
+#define DP_MASQ_ADDRS 65536u
 
 typedef struct dp_tables_desc {
     uint32_t abi_version;   /* DPGPU_ABI_VERSION */

@@ -1132,6 +1132,7 @@ struct MPool {
   std::deque<std::weak_ptr<MIp>> in_use;
   std::vector<MClaim> claims;               // ReservedPorts of the region
   bool excl_wk = false;
+  std::shared_ptr<uint32_t> live;           // addresses in use over the allocator (DP_MASQ_ADDRS)
 };
 
 struct MIp {  // AllocatedIp (alloc.rs:251-255)
@@ -1139,7 +1140,10 @@ struct MIp {  // AllocatedIp (alloc.rs:251-255)
   uint32_t offset = 0;
   std::shared_ptr<MPool> pool;
   MPortAlloc pa;
-  ~MIp() { pool->free.insert(offset); }     // Drop: deallocate_from_pool
+  ~MIp() {                                  // Drop: deallocate_from_pool
+    pool->free.insert(offset);
+    (*pool->live)--;
+  }
 };
 
 struct MBlock {  // AllocatedPortBlock (port_alloc.rs:396-401)
@@ -1173,6 +1177,8 @@ std::vector<std::pair<uint16_t, uint16_t>> m_reserved_for(const MPool &P, u128 b
 
 // AllocatedIp::new -> PortAllocator::new (port_alloc.rs:100-145)
 std::shared_ptr<MIp> m_new_ip(const std::shared_ptr<MPool> &P, uint32_t offset) {
+  if (*P->live >= DP_MASQ_ADDRS) return nullptr;
+  (*P->live)++;
   auto ip = std::make_shared<MIp>();
   ip->bits = P->start + offset;
   ip->offset = offset;
@@ -1270,8 +1276,9 @@ MErr m_pool_allocate(const std::shared_ptr<MPool> &P, bool allow_null, std::shar
   // allocate_from_new_ip: the lowest free offset
   if (P->free.empty()) return M_NO_FREE_IP;
   const uint32_t off = *P->free.begin();
-  P->free.erase(P->free.begin());
   auto ip = m_new_ip(P, off);
+  if (!ip) return M_NO_FREE_IP;  // every address record of the allocator in use
+  P->free.erase(P->free.begin());
   P->in_use.push_back(ip);
   return m_allocate_port(ip, allow_null, out);
 }
@@ -1316,8 +1323,9 @@ MErr m_set_reserve(const MPoolSet &S, const Ip &a, uint16_t port, bool ident, st
     }
   }
   if (!ip) {
-    P->free.erase((uint32_t)o);
     ip = m_new_ip(P, (uint32_t)o);
+    if (!ip) return M_NO_POOL_FOUND;
+    P->free.erase((uint32_t)o);
     P->in_use.push_back(ip);
   }
   MPortAlloc &pa = ip->pa;
@@ -1435,6 +1443,7 @@ std::shared_ptr<MAlloc> m_build(const std::vector<MExpose> &ex, const std::strin
   A->tag = tag;
   A->genid = genid;
   A->exposes = ex;
+  auto live = std::make_shared<uint32_t>(0);
   for (int fam : {4, 6}) {
     std::map<uint32_t, std::vector<const MExpose *>> groups;  // by destination VPC
     for (auto &e : ex) if (e.fam == fam) groups[e.dst_vni].push_back(&e);
@@ -1456,6 +1465,7 @@ std::shared_ptr<MAlloc> m_build(const std::vector<MExpose> &ex, const std::strin
           P->cap = span >= DP_MASQ_REGION_ADDRS - 1 ? DP_MASQ_REGION_ADDRS : (uint32_t)span + 1;
           for (uint32_t o = 0; o < P->cap; o++) P->free.insert(o);
           P->excl_wk = proto == 6 || proto == 17;
+          P->live = live;
           // claims_for: the claims of every owner, for this protocol (TCP / UDP only)
           const uint32_t bit = proto == 6 ? DP_MASQ_TCP : proto == 17 ? DP_MASQ_UDP : 0;
           for (size_t o : R.owners)
