@@ -219,6 +219,74 @@ def flows_leg(nf, w, dev, stream, steps: int) -> dict:
                     "(median of %d launches)" % steps}
 
 
+def nat_leg(dev, stream, steps: int, n: int) -> dict:
+    """Port forwarding under load: a burst of n 64-byte
+    packets of which a share opens new port-forwarded connections
+    (dataplane_amd/natwork.py), through the flows variant with its NAT pass
+    (dp_nat_prep + dp_nat_resolve: one lane per connection) and replay; the
+    table is emptied between launches (untimed), so every launch creates its
+    connections anew.  The last line: the same at the largest share with the
+    NAT pass forced onto one lane in packet order (the round-3 resolver).
+    Reported beside `value`, never inside it."""
+    from dataplane_amd import natwork as W
+    from dataplane_amd.flows import FlowTable
+    lib = A.gpu_lib()
+    nf2 = GpuPathNf(dev.index)
+    nf2.publish(W.tables().build())
+    slots = 1 << max(12, int(np.ceil(np.log2(max(1, 4 * n)))))
+    ft = FlowTable(dev.index, slots)
+    nf2.attach_flows(ft)
+    sptr = stream.cuda_stream
+    res = {"packets": n, "table_slots": slots, "legs": []}
+    hour = 3600 * 10**9
+    clock = [0]
+
+    def run(share, reps, one_lane=False):
+        buf, inp, npf = W.burst(n, share, 0)
+        pristine = torch.from_numpy(buf).to(dev)
+        b = torch.empty_like(pristine)
+        dinp = torch.from_numpy(inp.view(np.uint8)).to(dev)
+        dout = torch.empty(n * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+        ms, flows = [], 0
+        lib.dpf_debug_nat_sequential(1 if one_lane else 0)
+        try:
+            for k in range(reps):
+                clock[0] += hour
+                nf2.set_option(A.OPT_CLOCK, clock[0])
+                ft.sweep(clock[0])  # every flow of the last launch expired: an empty table
+                b.copy_(pristine)
+                torch.cuda.synchronize(dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                nf2.process_device(b.data_ptr(), b.numel(), dinp.data_ptr(), dout.data_ptr(), n, None, sptr)
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                ms.append(e0.elapsed_time(e1))
+                flows = ft.count()[0]
+        finally:
+            lib.dpf_debug_nat_sequential(0)
+        out = np.frombuffer(dout.cpu().numpy().tobytes(), dtype=A.PKT_OUT)
+        done = {A.DONE_NAMES[d]: int(c) for d, c in zip(*np.unique(out["done"], return_counts=True))}
+        keep = ms[1:] if len(ms) > 1 else ms
+        med = sorted(keep)[len(keep) // 2]
+        return {"pf_share": share, "pf_packets": npf, "one_lane": one_lane, "launch_ms_median": round(med, 4),
+                "mpps_median": round(n / (med / 1e3) / 1e6, 3), "flows_after": int(flows), "launches": len(keep),
+                "done_histogram": done}
+
+    for share in (0.0, 0.01, 0.05, 0.25):
+        res["legs"].append(run(share, steps + 1))
+        log(0, f"[bench] NAT leg share {share}: {res['legs'][-1]['launch_ms_median']} ms")
+    res["legs"].append(run(0.25, 2, one_lane=True))
+    log(0, f"[bench] NAT leg one lane: {res['legs'][-1]['launch_ms_median']} ms")
+    nf2.attach_flows(None)
+    ft.close()
+    nf2.close()
+    res["what"] = ("flows variant with port-forwarding creations: first pass, NAT pass (dp_nat_prep + "
+                   "dp_nat_resolve), replay, fix-up, invalidation, per launch (HIP events, median); "
+                   "per-kernel times: profiles/ rocprofv3 stats of this leg")
+    return res
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -232,6 +300,8 @@ def main() -> None:
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--no-flows", action="store_true", help="skip the flow-table leg")
+    ap.add_argument("--no-nat", action="store_true", help="skip the port-forwarding (NAT pass) leg")
+    ap.add_argument("--nat-only", action="store_true", help="only the NAT leg (profiling)")
     ap.add_argument("--no-rccl", action="store_true",
                     help="N > 1: skip the resident-burst scatter / process / gather measurement")
     # ablation knobs (0 = the config's default table sizes)
@@ -259,6 +329,10 @@ def main() -> None:
         if world > 1:
             torch.distributed.barrier()
 
+    if args.nat_only:  # the NAT leg alone (rocprofv3 of its kernels)
+        print(json.dumps({"nat_portfw": nat_leg(dev, torch.cuda.Stream(dev), min(args.steps, 10), args.packets)}),
+              flush=True)
+        return
     cfg = args.config
     t0 = time.perf_counter()
     w = Workload(cfg, args.packets, seed=shard_seed(args.seed, rank), n_routes_v4=args.routes_v4,
@@ -414,6 +488,8 @@ def main() -> None:
             result["resident_burst_scatter_gather"] = rccl
         if world == 1 and not args.no_flows:
             result["flow_table"] = flows_leg(nf, w, dev, stream, args.steps)
+        if world == 1 and not args.no_nat:
+            result["nat_portfw"] = nat_leg(dev, stream, min(args.steps, 10), n)
         if world == 1 and not args.no_host:
             # host-origin rate (dp_process_burst): pinned host burst buffer and
             # records, chunked H2D / kernel / D2H overlapped on several streams

@@ -74,7 +74,7 @@ __host__ __device__ inline uint32_t fkey_hash(const FKey &k) {
 
 // One packet that reached PortForwarder (nat/src/portfw/nf.rs:373-397) in
 // the burst's first pass: what the sequential port-forwarding pass
-// (dp_pf_resolve) needs, then its decision for the replay pass.
+// (dp_nat_prep, dp_nat_resolve) needs, then its decision for the replay pass.
 struct PfReq {
   uint32_t idx;          // packet index
   uint32_t bits;         // kPq* below
@@ -91,7 +91,7 @@ struct PfReq {
   uint32_t dst_vni0, related0, related_tag0;  // the attached flow as the burst started
   int64_t genid0;
   uint32_t dst_vni;      // PacketMeta.dst_vpcd at the NAT stages
-  // decision (dp_pf_resolve -> replay)
+  // decision (dp_nat_resolve -> replay)
   uint32_t verdict;      // PortForwarder: DoneReason to drop with, or kPfForward
   uint32_t nat;          // dp_pf_action | port << 16
   uint32_t nat_ip[4];
@@ -140,7 +140,7 @@ struct FlowCtx {
   // bitmap of packets that reached PortForwarder (+ its summary, 1 bit per
   // 1024 packets), the order of the records (resolve), replaced fills
   PfReq *pf;
-  uint32_t *pf_cnt;     // [0] records, [1] replay packets, [2] replaced fills, [3] releases
+  uint32_t *pf_cnt;     // [0] records, [1] replay packets, [2] replaced fills, [3] releases, [4..7] below
   uint32_t *pf_of;      // packet -> record
   uint32_t *pf_bits;
   uint32_t *pf_sum;
@@ -153,6 +153,19 @@ struct FlowCtx {
   uint8_t *mq;
   uint32_t mq_gen;
   uint32_t *mq_rel;
+  // the NAT pass's connections (dp_nat_prep / dp_nat_resolve): per hash slot
+  // (burst << 32 | connection key) and (burst << 32 | its last record), per
+  // record (packet index << 32 | the connection's record before it), the
+  // slots claimed this burst; [4] their count, [5] a record the parallel
+  // pass cannot take, [6..7] the table length as the pass starts
+  unsigned long long *grp_tab, *grp_head, *grp_next;
+  uint32_t *grp_list;
+  uint32_t grp_mask;
+  uint32_t burst;       // this burst's tag (never 0): entries of other bursts are empty
+  // keyed index of the replaced fills: (burst, slot, old state, pf_repl index)
+  uint4 *repl;
+  uint32_t rmask;
+  uint32_t force_seq;   // test hook (dpf_debug_nat_sequential): the one-lane NAT pass always
 };
 
 // A packet whose ACL verdict was "allow: reply of a flow-scope-allowed flow";
@@ -170,8 +183,16 @@ struct SensRec {
   uint32_t dst_vni;     // PacketMeta at the ACL: dst_vpcd, vrf (bit 31: Some), the nh_addr source
   uint32_t vrf;
   uint32_t nh_ref;
-  uint32_t slot_tag;    // its flow's state word at attach (a refill by dp_pf_resolve changes it)
+  uint32_t slot_tag;    // its flow's state word at attach (a refill by dp_nat_resolve changes it)
 };
+
+// the keyed index of the fills a burst's NAT pass replaced (FlowCtx::repl)
+__host__ __device__ inline uint32_t repl_hash(uint32_t slot, uint32_t state) {
+  uint32_t h = slot * 0x9E3779B1u ^ (state + 0x7F4A7C15u) * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  return h ^ (h >> 12);
+}
 
 __host__ __device__ inline uint64_t make_ref(uint32_t slot, uint32_t state) {
   return ((uint64_t)(state >> 2) << 32) | slot;

@@ -1572,7 +1572,7 @@ __device__ __forceinline__ uint32_t be16_bytes(const Frame &F, int f) {
 __device__ __forceinline__ uint32_t flow_probe(const dpf::FlowCtx &fc, const dpf::FKey &k, uint32_t &state,
                                                uint4 &v, uint4 &w) {
   uint32_t i = dpf::fkey_hash(k) & fc.mask;
-  const uint32_t bound = fc.tmeta[0];  // moved by the bursts' own inserts (dp_pf_resolve)
+  const uint32_t bound = fc.tmeta[0];  // moved by the bursts' own inserts (dp_nat_resolve)
 #pragma unroll 1
   for (uint32_t p = 0; p <= bound; p++) {
     const dpf::FlowSlot *s = fc.slots + i;
@@ -1655,7 +1655,7 @@ __device__ __forceinline__ void flow_attach(uint32_t slot, uint32_t state, const
 // 35-195: the address; an error message carries no identifier).  Any failure
 // is InternalFailure.  An unrecoverable error on a one-way flow invalidates
 // the pair (before any flow-filter decision of the burst: mark 0).
-__device__ DP_COLD void icmp_error_masq(const dpf::FlowCtx &fc, const Frame &F, const Hdr &H, State &S,
+__device__ __forceinline__ void icmp_error_masq(const dpf::FlowCtx &fc, const Frame &F, const Hdr &H, State &S,
                                              FlowPk &fp, uint32_t sl, uint32_t st) {
   const EmbV E = emb_view(F, H);
   const dpf::FlowSlot *fs = fc.slots + sl;
@@ -2304,7 +2304,7 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
 // an earlier packet's deny turns it into the peering default
 // (dp_flow_fixup).  A deny invalidates the packet's flow pair.
 // The replay pass (rp: the packet's port-forwarding record) takes a flow-
-// dependent verdict from the first pass, as dp_pf_resolve left it.
+// dependent verdict from the first pass, as dp_nat_resolve left it.
 template <bool FL>
 __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hdr &H, State &S, const Pre &P,
                                           FlowPk &fp, const dpf::FlowCtx *fc, uint32_t idx,
@@ -2384,7 +2384,7 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
 }
 
 // The NAT record of a packet that reached PortForwarder or Masquerade in the
-// first pass (dpf::PfReq): what the sequential NAT pass (dp_pf_resolve) needs
+// first pass (dpf::PfReq): what the sequential NAT pass (dp_nat_resolve) needs
 // to run the reference's NFs over it in packet order.  The packet stops here;
 // the replay pass finishes it with the pass's decisions.
 __device__ __forceinline__ void nat_record(const Frame &F, const Hdr &H, const State &S, FlowPk &fp,
@@ -2452,7 +2452,7 @@ __device__ __forceinline__ bool icmp_error_pkt(const Frame &F, const Hdr &H) {
 // port forwarding and is not an ICMP error.  Its outcome depends on the flow
 // states the earlier packets of the burst leave (NatFlowStatus, expiry,
 // invalidations, the flow pairs they create), so the first pass records the
-// packet (nat_record) and stops it here; dp_pf_resolve runs the reference's
+// packet (nat_record) and stops it here; dp_nat_resolve runs the reference's
 // PortForwarder over the records in packet order, and the replay pass takes
 // each packet through the rest of the path with its decision.  Without a
 // flow table (whose Arc the reference's PortForwarder always holds) the
@@ -2500,7 +2500,7 @@ __device__ __forceinline__ void stage_portfw(const Frame &F, const Hdr &H, State
 // masquerading and is not an ICMP error: like PortForwarder, its outcome
 // rests on what the earlier packets of the burst did to the flows and to the
 // allocator, so the first pass records it (one record with PortForwarder's
-// when the packet needs both) and dp_pf_resolve decides.  The replay applies
+// when the packet needs both) and dp_nat_resolve decides.  The replay applies
 // the decision: masquerade (packet.rs:35-195) -- the address, a TCP / UDP
 // port always, an ICMP query identifier when it changes -- and the checksum
 // refresh the NF always asks for.  Without a flow table: InternalFailure.
@@ -3198,7 +3198,7 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
       fc.events[2 + 2 * k] = fp.state;
     }
   }
-  const bool sv = has && fp.sens && !fp.deferred;  // a deferred packet's verdict: dp_pf_resolve
+  const bool sv = has && fp.sens && !fp.deferred;  // a deferred packet's verdict: dp_nat_resolve
   const uint64_t ms = __ballot(sv);
   if (ms) {
     const int leader = __ffsll((long long)ms) - 1;
@@ -3231,7 +3231,7 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   uint8_t *slab_wave = slab_all + (tid - lane) * SLAB;
   lds_u8 *slab = (lds_u8 *)(slab_all + tid * SLAB);
   // the replay pass (port forwarding, FL only): thread t finishes packet
-  // pf_order[t] of the records dp_pf_resolve ordered
+  // pf_order[t] of the records dp_nat_prep ordered
   constexpr bool rep = FL && RP;
   uint32_t i = blockIdx.x * TPB + tid;
   bool live = i < n;
@@ -3371,10 +3371,15 @@ __device__ uint32_t next_status(bool tcp, uint32_t fl, uint32_t act, uint32_t st
   return st == DP_NFS_ONE_WAY ? (uint32_t)DP_NFS_TWO_WAY : st;
 }
 
-// The sequential pass's view of the table.
+// The NAT pass's view of the table.  par: one of many lanes, each running the
+// records of its own connections in packet order (dp_nat_resolve) -- the
+// burst-wide counters (events, replaced fills, table length, probe bound) and
+// the claim of a free slot are atomic; a connection's own slots are its lane's.
 struct Seq {
   const dpf::FlowCtx &fc;
   const Img &g;
+  bool par;
+  __device__ uint32_t bump(uint32_t *c) const { return par ? atomicAdd(c, 1u) : (*c)++; }
   __device__ bool alive(uint32_t sl, uint32_t tag) const { return sl <= fc.mask && fc.slots[sl].state == tag; }
   // the pair is invalid for packet idx: either flow's burst-local mark says
   // so (invalidate_pair reaches the related flow only while it is alive)
@@ -3388,9 +3393,27 @@ struct Seq {
   __device__ void invalidate(uint32_t sl, uint32_t idx) const {
     dpf::FlowSlot &s = fc.slots[sl];
     if (s.mark > idx + 1) s.mark = idx + 1;
-    const uint32_t k = fc.events[0]++;
+    const uint32_t k = bump(&fc.events[0]);
     fc.events[1 + 2 * k] = sl;
     fc.events[2 + 2 * k] = s.state;
+  }
+  // the replaced fill's entry in the keyed index of replacements (dp_flow_fixup)
+  __device__ void index_repl(uint32_t sl, uint32_t old, uint32_t r) const {
+    uint32_t h = dpf::repl_hash(sl, old) & fc.rmask;
+    const unsigned long long want = ((unsigned long long)fc.burst << 32) | sl;
+    for (uint32_t p = 0; p <= fc.rmask;) {
+      unsigned long long *w = reinterpret_cast<unsigned long long *>(&fc.repl[h].x);
+      const unsigned long long cur = *w;
+      if ((uint32_t)(cur >> 32) == fc.burst) {  // taken this burst: the next entry
+        h = (h + 1) & fc.rmask;
+        p++;
+        continue;
+      }
+      if (atomicCAS(w, cur, want) != cur) continue;  // lost the race for it: look again
+      fc.repl[h].z = old;
+      fc.repl[h].w = r;
+      return;
+    }
   }
   __device__ void set_nfs(uint32_t sl, uint32_t st) const {
     dpf::FlowSlot &s = fc.slots[sl];
@@ -3426,12 +3449,24 @@ struct Seq {
     }
     uint32_t sl = found;
     if (sl != dpf::kNoSlot) {
+      // an invalidation of the replaced fill earlier in the burst reached its
+      // related flow too (invalidate_pair): with the fill gone, that flow
+      // carries the mark and the event itself
+      const dpf::FlowSlot &x = fc.slots[sl];
+      if (x.mark != dpf::kIdleMark && alive(x.related, x.related_tag)) {
+        dpf::FlowSlot &y = fc.slots[x.related];
+        if (y.mark > x.mark) y.mark = x.mark;
+        const uint32_t e = bump(&fc.events[0]);
+        fc.events[1 + 2 * e] = x.related;
+        fc.events[2 + 2 * e] = y.state;
+      }
       // the replaced fill, for the ACL verdicts that rest on it (dp_flow_fixup)
-      const uint32_t r = fc.pf_cnt[2]++;
+      const uint32_t r = bump(&fc.pf_cnt[2]);
       fc.pf_repl[4 * r] = sl;
       fc.pf_repl[4 * r + 1] = fc.slots[sl].state;
       fc.pf_repl[4 * r + 2] = idx;
       fc.pf_repl[4 * r + 3] = fc.slots[sl].mark;
+      index_repl(sl, fc.slots[sl].state, r);
       // its FlowInfo is dropped when the burst ends, and with it the
       // allocation its masquerade state owns
       const dpf::FlowSlot &o = fc.slots[sl];
@@ -3440,7 +3475,7 @@ struct Seq {
         fc.mq_rel[2 * k] = o.mq_rec - 1;
         fc.mq_rel[2 * k + 1] = o.pf >> 16;
       }
-    } else {
+    } else if (!par) {
       if (len >= fc.hard) return dpf::kNoSlot;  // the table stays at most 7/8 full
       if (free_ == dpf::kNoSlot) {  // beyond the probe bound: the first free slot further on
         for (uint32_t p = bound + 1; p <= fc.mask; p++) {
@@ -3455,9 +3490,23 @@ struct Seq {
       len++;
       fc.tmeta[2] = (uint32_t)len;
       fc.tmeta[3] = (uint32_t)(len >> 32);
+    } else {
+      // (the parallel pass runs only when no insert of the burst can meet the
+      // capacity or the 7/8 bound: dp_nat_resolve)  The first free slot of
+      // the probe sequence that this lane claims; other lanes claim theirs.
+      sl = dpf::kNoSlot;
+      for (uint32_t p = free_ == dpf::kNoSlot ? 0 : ((free_ - home) & fc.mask); p <= fc.mask; p++) {
+        const uint32_t j = (home + p) & fc.mask;
+        const uint32_t st = __hip_atomic_load(&fc.slots[j].state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((st & 3u) != dpf::FS_EMPTY && (st & 3u) != dpf::FS_TOMB) continue;
+        if (atomicCAS(&fc.slots[j].state, st, (st & ~3u) | dpf::FS_BUSY) == st) { sl = j; break; }
+      }
+      if (sl == dpf::kNoSlot) return dpf::kNoSlot;
+      atomicMax(&fc.tmeta[0], (sl - home) & fc.mask);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), 1ull);
     }
     dpf::FlowSlot &s = fc.slots[sl];
-    const uint32_t old = s.state;
+    const uint32_t old = s.state;  // (a claimed slot: BUSY, its tag kept)
     s.src_vni = k.w[0]; s.fk = k.w[1]; s.ports = k.w[2];
     for (int j = 0; j < 4; j++) { s.src[j] = k.w[3 + j]; s.dst[j] = k.w[7 + j]; }
     s.status = DP_FLOW_ACTIVE;
@@ -3817,64 +3866,241 @@ __device__ void resolve_one(const Seq &q, dpf::PfReq &R) {
   if ((R.bits & dpf::kPqMasq) && R.verdict == dpf::kPfForward) resolve_masq(q, R);
 }
 
+// ---------------------------------------------------------------------------
+// The NAT pass in parallel: connections
+// ---------------------------------------------------------------------------
+// PortForwarder's decisions couple only the records of one connection (its
+// flow pair, the pair a packet of it creates) and the table-wide insert
+// admission.  A record's connection is named by the key its reply direction
+// carries: the reverse flow's key (a forward flow's related flow, or derived
+// from its state), or, for a packet that may create a pair, the reverse key
+// try_port_forwarding would insert (nf.rs:174-204, flow_state.rs:102-131).
+// Records of one connection run in packet order on one lane; connections run
+// in parallel.  Hash collisions only merge connections.
+
+// The reverse key the creation path would insert for this record (the same
+// preconditions and mapping as resolve_pf's creation), false: it creates none.
+__device__ bool creation_rk(const Img &g, const dpf::PfReq &R, dpf::FKey &rk) {
+  if (!(R.bits & dpf::kPqPf) || !R.src_vni) return false;
+  const uint32_t fam = (R.proto >> 8) & 0xffu, proto = R.proto & 0xffu, tfl = R.proto >> 16;
+  const bool tcp = R.bits & dpf::kPqTcp, ports = R.bits & (dpf::kPqTcp | dpf::kPqUdp);
+  const bool first_seg = (tfl & 2) && !(tfl & 0x3du);
+  if (!(R.bits & dpf::kPqEth) || !ports || (tcp && !first_seg) || !unicast(fam, R.dst)) return false;
+  const uint32_t sport = R.ports >> 16, dport = R.ports & 0xffffu;
+  const int32_t e = lookup(g, R.src_vni, proto, fam, R.dst, dport);
+  if (e < 0) return false;
+  const PfRuleRec &E = g.at<PfRuleRec>(g.im.pf_rules)[e];
+  uint32_t na[4], np;
+  if (!map(E, R.dst, dport, na, np)) return false;
+  rk.w[0] = E.dst_vni;
+  rk.w[1] = fam | ((tcp ? DP_FLOW_TCP : DP_FLOW_UDP) << 8);
+  rk.w[2] = (np << 16) | sport;
+  for (int j = 0; j < 4; j++) { rk.w[3 + j] = bswap(na[j]); rk.w[7 + j] = bswap(R.src[j]); }
+  return true;
+}
+
+__device__ inline dpf::FKey slot_key(const dpf::FlowSlot &s) {
+  dpf::FKey k;
+  k.w[0] = s.src_vni; k.w[1] = s.fk; k.w[2] = s.ports;
+  for (int j = 0; j < 4; j++) { k.w[3 + j] = s.src[j]; k.w[7 + j] = s.dst[j]; }
+  return k;
+}
+
+// The record's connection key; false: the record needs the sequential pass
+// (masquerade: one allocator; a flow without port-forwarding state; a pair it
+// may create that is not its flow's).
+__device__ bool conn_key(const Img &g, const dpf::FlowCtx &fc, const dpf::PfReq &R, uint32_t &key) {
+  if (R.bits & dpf::kPqMasq) return false;
+  dpf::FKey rk;
+  const bool cand = creation_rk(g, R, rk);
+  if (cand) {
+    // a flow already holding that key must be a port-forwarded reply flow
+    // (whose packets name the same connection); anything else couples
+    // connections
+    uint32_t st;
+    uint4 v, w;
+    const uint32_t z = flow_probe(fc, rk, st, v, w);
+    if (z != dpf::kNoSlot && !((v.y & dpf::kFlagPf) && (fc.slots[z].pf & 0xffu) == DP_PF_SRC_NAT)) return false;
+  }
+  if (R.slot == dpf::kNoSlot) {
+    key = cand ? dpf::fkey_hash(rk) : (R.idx * 0x9E3779B1u) ^ 0x5bd1e995u;  // no flow, no pair: alone
+    return true;
+  }
+  const dpf::FlowSlot &A = fc.slots[R.slot];
+  if (!(A.flags & dpf::kFlagPf)) return false;
+  dpf::FKey ak;
+  if ((A.pf & 0xffu) == DP_PF_SRC_NAT) {
+    ak = slot_key(A);  // the reverse flow itself
+  } else if (A.related <= fc.mask && fc.slots[A.related].state == A.related_tag) {
+    ak = slot_key(fc.slots[A.related]);
+  } else {  // the reverse key from the forward flow's state
+    ak.w[0] = A.dst_vni;
+    ak.w[1] = A.fk;
+    ak.w[2] = (A.pf & 0xffff0000u) | (A.ports >> 16);
+    for (int j = 0; j < 4; j++) { ak.w[3 + j] = bswap(A.pf_ip[j]); ak.w[7 + j] = A.src[j]; }
+  }
+  if (cand)
+    for (int j = 0; j < 11; j++)
+      if (rk.w[j] != ak.w[j]) return false;
+  key = dpf::fkey_hash(ak);
+  return true;
+}
+
+// The records of one connection (a list through grp_next, pushed in any
+// order) sorted by packet index: a merge sort of the linked list.
+__device__ uint32_t sort_conn(unsigned long long *nx, uint32_t list) {
+  auto next = [&](uint32_t r) { return (uint32_t)nx[r]; };
+  auto set_next = [&](uint32_t r, uint32_t v) { nx[r] = (nx[r] & 0xffffffff00000000ull) | v; };
+  if (list == dpf::kNoSlot || next(list) == dpf::kNoSlot) return list;
+  for (uint32_t insize = 1;; insize *= 2) {
+    uint32_t p = list, tail = dpf::kNoSlot, merges = 0;
+    list = dpf::kNoSlot;
+    while (p != dpf::kNoSlot) {
+      merges++;
+      uint32_t q = p, psize = 0;
+      for (uint32_t i = 0; i < insize; i++) {
+        psize++;
+        q = next(q);
+        if (q == dpf::kNoSlot) break;
+      }
+      uint32_t qsize = insize;
+      while (psize > 0 || (qsize > 0 && q != dpf::kNoSlot)) {
+        uint32_t e;
+        if (psize == 0) { e = q; q = next(q); qsize--; }
+        else if (qsize == 0 || q == dpf::kNoSlot || (nx[p] >> 32) <= (nx[q] >> 32)) { e = p; p = next(p); psize--; }
+        else { e = q; q = next(q); qsize--; }
+        if (tail != dpf::kNoSlot) set_next(tail, e);
+        else list = e;
+        tail = e;
+      }
+      p = q;
+    }
+    set_next(tail, dpf::kNoSlot);
+    if (merges <= 1) return list;
+  }
+}
+
 }  // namespace pfw
 
 #if DP_IN_PART(0)
-// dp_pf_resolve: one workgroup.  The packets that reached PortForwarder, in
-// packet order (their bitmap, scanned 1024 packets per summary bit; the bits
-// are cleared for the next burst), then the reference's PortForwarder over
-// them one after the other -- the NatFlowStatus machine, expiries, rule
-// revalidation, invalidations and the flow pairs created, with
-// FlowTable::insert's capacity and replacement semantics -- leaving each
-// packet's decision in its record for the replay pass.
-__global__ void __launch_bounds__(1024) dp_pf_resolve(const uint8_t *__restrict__ img_base,
-                                                      const Image *__restrict__ im, dpf::FlowCtx fc) {
-  __shared__ uint32_t cnt[1024];
-  __shared__ uint32_t total;
+// dp_nat_prep: the records of the burst's NAT pass.  Workgroup 0 puts the
+// packets that reached PortForwarder / Masquerade in packet order (their
+// bitmap, scanned 1024 packets per summary bit; the bits are cleared for the
+// next burst) for the replay pass; every workgroup files each record under its
+// connection (pfw::conn_key) -- a hash slot claimed for this burst by CAS on
+// (burst, key), a list of its records pushed by CAS on (burst, last record).
+__global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ img_base,
+                                                    const Image *__restrict__ im, dpf::FlowCtx fc) {
   const uint32_t t = threadIdx.x;
-  if (t == 0) total = 0;
-  const uint32_t regions = (fc.n + 1023) / 1024;
-  for (uint32_t r0 = 0; r0 < regions; r0 += 1024) {
-    __syncthreads();
-    const uint32_t r = r0 + t;
-    uint32_t c = 0;
-    const bool hit = r < regions && ((fc.pf_sum[r >> 5] >> (r & 31)) & 1u);
-    if (hit) for (int w = 0; w < 32; w++) c += __popc(fc.pf_bits[r * 32 + w]);
-    cnt[t] = c;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan
-      const uint32_t v = t >= o ? cnt[t - o] : 0u;
+  if (blockIdx.x == 0) {
+    __shared__ uint32_t cnt[1024];
+    __shared__ uint32_t total;
+    if (t == 0) total = 0;
+    const uint32_t regions = (fc.n + 1023) / 1024;
+    for (uint32_t r0 = 0; r0 < regions; r0 += 1024) {
       __syncthreads();
-      cnt[t] += v;
+      const uint32_t r = r0 + t;
+      uint32_t c = 0;
+      const bool hit = r < regions && ((fc.pf_sum[r >> 5] >> (r & 31)) & 1u);
+      if (hit) for (int w = 0; w < 32; w++) c += __popc(fc.pf_bits[r * 32 + w]);
+      cnt[t] = c;
       __syncthreads();
-    }
-    uint32_t pos = total + cnt[t] - c;
-    if (hit) {
-      for (int w = 0; w < 32; w++) {
-        uint32_t b = fc.pf_bits[r * 32 + w];
-        fc.pf_bits[r * 32 + w] = 0;
-        while (b) {
-          const int k = __ffs(b) - 1;
-          b &= b - 1;
-          fc.pf_order[pos++] = r * 1024 + w * 32 + k;  // < n: only packets set bits
+      for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan
+        const uint32_t v = t >= o ? cnt[t - o] : 0u;
+        __syncthreads();
+        cnt[t] += v;
+        __syncthreads();
+      }
+      uint32_t pos = total + cnt[t] - c;
+      if (hit) {
+        for (int w = 0; w < 32; w++) {
+          uint32_t b = fc.pf_bits[r * 32 + w];
+          fc.pf_bits[r * 32 + w] = 0;
+          while (b) {
+            const int k = __ffs(b) - 1;
+            b &= b - 1;
+            fc.pf_order[pos++] = r * 1024 + w * 32 + k;  // < n: only packets set bits
+          }
         }
       }
+      __syncthreads();
+      if (t == 1023) total += cnt[1023];
     }
     __syncthreads();
-    if (t == 1023) total += cnt[1023];
+    for (uint32_t w = t; w < (regions + 31) / 32; w += 1024) fc.pf_sum[w] = 0;
+    if (t == 0) {
+      fc.pf_cnt[1] = total;
+      fc.pf_cnt[6] = fc.tmeta[2];  // the table length before the pass
+      fc.pf_cnt[7] = fc.tmeta[3];
+    }
   }
-  __syncthreads();
-  for (uint32_t w = t; w < (regions + 31) / 32; w += 1024) fc.pf_sum[w] = 0;
-  if (t != 0) return;
-  fc.pf_cnt[1] = total;
+  const uint32_t nrec = fc.pf_cnt[0];
+  if (!nrec) return;
   const Img g{img_base, *im};
-  const pfw::Seq q{fc, g};
-  for (uint32_t k = 0; k < total; k++) pfw::resolve_one(q, fc.pf[fc.pf_of[fc.pf_order[k]]]);
-  // the flows replaced during the burst are dropped after it, with the
-  // allocations their masquerade state owns
-  if (fc.mq) {
-    const dpm::View V{fc.mq};
-    for (uint32_t k = 0; k < fc.pf_cnt[3]; k++) dpm::release(V, fc.mq_rel[2 * k], fc.mq_rel[2 * k + 1]);
+  const unsigned long long tag = (unsigned long long)fc.burst << 32;
+  for (uint32_t rec = blockIdx.x * 1024 + t; rec < nrec; rec += gridDim.x * 1024) {
+    const dpf::PfReq &R = fc.pf[rec];
+    if (!(R.bits & dpf::kPqReached)) continue;  // a flow-filter record of a packet dropped before NAT
+    uint32_t key;
+    if (!pfw::conn_key(g, fc, R, key)) { atomicOr(&fc.pf_cnt[5], 1u); continue; }
+    const unsigned long long want = tag | key;
+    uint32_t h = dpm::kmix(key, 0x2545f491u, 0u) & fc.grp_mask;
+    for (uint32_t p = 0; p <= fc.grp_mask;) {
+      const unsigned long long cur = fc.grp_tab[h];
+      if (cur == want) break;
+      if ((cur >> 32) == fc.burst) { h = (h + 1) & fc.grp_mask; p++; continue; }
+      if (atomicCAS(&fc.grp_tab[h], cur, want) == cur) {
+        fc.grp_list[atomicAdd(&fc.pf_cnt[4], 1u)] = h;
+        break;
+      }
+    }
+    unsigned long long old = fc.grp_head[h];
+    for (;;) {
+      const uint32_t prev = (old >> 32) == fc.burst ? (uint32_t)old : dpf::kNoSlot;
+      fc.grp_next[rec] = ((unsigned long long)R.idx << 32) | prev;
+      const unsigned long long got = atomicCAS(&fc.grp_head[h], old, tag | rec);
+      if (got == old) break;
+      old = got;
+    }
+  }
+}
+
+// dp_nat_resolve: the reference's PortForwarder and Masquerade over the
+// records -- NatFlowStatus, expiries, invalidation marks and events, rule
+// revalidation, allocations, the inserts of new pairs -- leaving each
+// packet's decision in its record for the replay pass.  In parallel, one
+// lane per connection (its records in packet order), when no record needs
+// the sequential pass and no insert of the burst can meet the capacity or
+// the 7/8 bound (the admissions of insert_common,
+// flow-entry/src/flow_table/table.rs:215-260, then cannot depend on the
+// order of connections); else one lane over all records in packet order.
+__global__ void __launch_bounds__(256) dp_nat_resolve(const uint8_t *__restrict__ img_base,
+                                                      const Image *__restrict__ im, dpf::FlowCtx fc) {
+  const uint32_t total = fc.pf_cnt[1];
+  if (!total) return;
+  const Img g{img_base, *im};
+  const uint64_t len0 = ((uint64_t)fc.pf_cnt[7] << 32) | fc.pf_cnt[6];
+  const bool seq = fc.force_seq || fc.pf_cnt[5] || len0 + 2ull * total > fc.capacity ||
+                   len0 + 2ull * total > fc.hard;
+  const uint32_t gt = blockIdx.x * 256 + threadIdx.x;
+  if (seq) {
+    if (gt != 0) return;
+    const pfw::Seq q{fc, g, false};
+    for (uint32_t k = 0; k < total; k++) pfw::resolve_one(q, fc.pf[fc.pf_of[fc.pf_order[k]]]);
+    // the flows replaced during the burst are dropped after it, with the
+    // allocations their masquerade state owns
+    if (fc.mq) {
+      const dpm::View V{fc.mq};
+      for (uint32_t k = 0; k < fc.pf_cnt[3]; k++) dpm::release(V, fc.mq_rel[2 * k], fc.mq_rel[2 * k + 1]);
+    }
+    return;
+  }
+  const pfw::Seq q{fc, g, true};
+  const uint32_t ng = fc.pf_cnt[4];
+  for (uint32_t e = gt; e < ng; e += gridDim.x * 256) {
+    const uint32_t h = fc.grp_list[e];
+    uint32_t r = pfw::sort_conn(fc.grp_next, (uint32_t)fc.grp_head[h]);
+    for (; r != dpf::kNoSlot; r = (uint32_t)fc.grp_next[r]) pfw::resolve_one(q, fc.pf[r]);
   }
 }
 
@@ -3895,16 +4121,22 @@ __global__ void __launch_bounds__(256) dp_flow_fixup(const uint8_t *__restrict__
   const dpf::SensRec *recs = reinterpret_cast<const dpf::SensRec *>(fc.sens + 8);
   const uint32_t nrep = fc.pf_cnt[2];
   // a fill for packet idx: 1 in the table (its burst-local mark), 0 not in
-  // the table as the burst started, -1 replaced by dp_pf_resolve before idx
-  // (a fill replaced by packet j > idx counts with the mark it had)
+  // the table as the burst started, -1 replaced by the NAT pass before idx
+  // (a fill replaced by packet j > idx counts with the mark it had); the
+  // replaced fills by their keyed index
   auto fill_at = [&](uint32_t sl, uint32_t tag, uint32_t idx, uint32_t &mark) -> int {
     if (sl > fc.mask) return 0;
     if (fc.slots[sl].state == tag) { mark = fc.slots[sl].mark; return 1; }
-    for (uint32_t k = 0; k < nrep; k++)
-      if (fc.pf_repl[4 * k] == sl && fc.pf_repl[4 * k + 1] == tag) {
-        mark = fc.pf_repl[4 * k + 3];
-        return fc.pf_repl[4 * k + 2] > idx ? 1 : -1;
+    if (!nrep) return 0;
+    uint32_t h = dpf::repl_hash(sl, tag) & fc.rmask;
+    for (uint32_t p = 0; p <= fc.rmask; p++, h = (h + 1) & fc.rmask) {
+      const uint4 e = fc.repl[h];
+      if (e.y != fc.burst) return 0;
+      if (e.x == sl && e.z == tag) {
+        mark = fc.pf_repl[4 * e.w + 3];
+        return fc.pf_repl[4 * e.w + 2] > idx ? 1 : -1;
       }
+    }
     return 0;
   };
   for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < cnt; r += gridDim.x * 256) {
@@ -4187,16 +4419,20 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   dpf::FlowCtx fc = *reinterpret_cast<const dpf::FlowCtx *>(fc_host);
   if (hipMemsetAsync(fc.events, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
   if (hipMemsetAsync(fc.sens, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
-  if (hipMemsetAsync(fc.pf_cnt, 0, sizeof(uint32_t) * 4, stream) != hipSuccess) return -5;
+  if (hipMemsetAsync(fc.pf_cnt, 0, sizeof(uint32_t) * 8, stream) != hipSuccess) return -5;
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
   // first pass; PortForwarder's records in packet order; the replay of the
-  // packets that reached it (dp_pf_resolve's decisions)
+  // packets that reached it (dp_nat_resolve's decisions)
   fc.replay = 0;
   if (meta) dpk_run_pipeline_110(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   else dpk_run_pipeline_100(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
-  hipLaunchKernelGGL(dp_pf_resolve, dim3(1), dim3(1024), 0, stream, img_base, im, fc);
+  // the NAT pass: records filed by connection, then resolved
+  const uint32_t pb = (n + 1023) / 1024 < 256 ? (n + 1023) / 1024 : 256;
+  hipLaunchKernelGGL(dp_nat_prep, dim3(pb), dim3(1024), 0, stream, img_base, im, fc);
+  const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(dp_nat_resolve, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   fc.replay = 1;
   if (meta) dpk_run_pipeline_111(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   else dpk_run_pipeline_101(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);

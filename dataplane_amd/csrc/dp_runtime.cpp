@@ -137,6 +137,7 @@ struct DeviceTables {
   std::map<dp_flow_table *, int> fts;
 };
 std::atomic<uint64_t> g_serial{1};
+std::atomic<uint32_t> g_nat_seq{0};  // dpf_debug_nat_sequential
 
 std::mutex g_dev_mu;
 std::map<int, std::unique_ptr<DeviceTables>> g_dev;
@@ -217,6 +218,10 @@ struct dp_ctx {
   // port forwarding scratch (dpf::FlowCtx pf*): records, counters, packet ->
   // record, bitmaps (kept zero between bursts), order, replaced fills
   FlowScratch pf_req, pf_cnt, pf_of, pf_bits, pf_order, pf_repl, mq_rel;
+  // the NAT pass's connection tables and the keyed index of replaced fills:
+  // entries carry the burst's tag, so they are zeroed only when allocated
+  FlowScratch grp_tab, grp_head, grp_next, grp_list, repl;
+  uint32_t burst_tag = 0;
   uint64_t pf_bits_n = 0;
   hipEvent_t fl_used = nullptr;
   bool fl_armed = false;
@@ -457,7 +462,8 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   c->fl_ev.release();
   c->fl_sens.release();
-  for (FlowScratch *x : {&c->pf_req, &c->pf_cnt, &c->pf_of, &c->pf_bits, &c->pf_order, &c->pf_repl, &c->mq_rel})
+  for (FlowScratch *x : {&c->pf_req, &c->pf_cnt, &c->pf_of, &c->pf_bits, &c->pf_order, &c->pf_repl, &c->mq_rel,
+                         &c->grp_tab, &c->grp_head, &c->grp_next, &c->grp_list, &c->repl})
     x->release();
   if (c->ft) {
     DeviceTables &dt = dev_tables(c->device);
@@ -592,20 +598,22 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.mask = ft->mask;
     fc.max_probe = 0;
     fc.n = n;
-    fc.events = static_cast<uint32_t *>(c->fl_ev.get(sizeof(uint32_t) * (1 + 8 * (uint64_t)n)));
+    // (slot, state) events: <= 2 per packet in the first pass, <= 6 in the
+    // sequential NAT pass (invalidations and their hand-over at refills)
+    fc.events = static_cast<uint32_t *>(c->fl_ev.get(sizeof(uint32_t) * (1 + 16 * (uint64_t)n)));
     fc.sens = static_cast<uint32_t *>(c->fl_sens.get(sizeof(uint32_t) * 8 + sizeof(dpf::SensRec) * (uint64_t)n));
     fc.genid = img->im.genid;
     fc.tmeta = ft->d_meta;
     fc.capacity = ft->capacity;
     fc.hard = ft->nslots - ft->nslots / 8;
     fc.now = c->clock;
-    // port forwarding: the bitmaps stay zero between bursts (dp_pf_resolve
-    // clears what it reads); grown bitmaps start zeroed.  dp_pf_resolve reads
+    // port forwarding: the bitmaps stay zero between bursts (dp_nat_prep
+    // clears what it reads); grown bitmaps start zeroed.  dp_nat_prep reads
     // the bitmap a whole 1024-packet region (32 words) at a time, so it spans
     // whole regions; the summary words sit after them
     const uint64_t words = ((uint64_t)n + 1023) / 1024 * 32, sum_words = ((uint64_t)n + 32767) / 32768;
     fc.pf = static_cast<dpf::PfReq *>(c->pf_req.get(sizeof(dpf::PfReq) * (uint64_t)n));
-    fc.pf_cnt = static_cast<uint32_t *>(c->pf_cnt.get(sizeof(uint32_t) * 4));
+    fc.pf_cnt = static_cast<uint32_t *>(c->pf_cnt.get(sizeof(uint32_t) * 8));
     fc.pf_of = static_cast<uint32_t *>(c->pf_of.get(sizeof(uint32_t) * (uint64_t)n));
     fc.pf_order = static_cast<uint32_t *>(c->pf_order.get(sizeof(uint32_t) * (uint64_t)n));
     fc.pf_repl = static_cast<uint32_t *>(c->pf_repl.get(sizeof(uint32_t) * 8 * ((uint64_t)n + 1)));
@@ -614,6 +622,38 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.mq = ft->mq;
     fc.mq_gen = ft->mq_gen;
     fc.mq_rel = static_cast<uint32_t *>(c->mq_rel.get(sizeof(uint32_t) * 4 * ((uint64_t)n + 1)));
+    // the NAT pass's connections: a hash table of at least 2n slots, a list
+    // link per record, the slots claimed; the replaced fills (<= 2 per
+    // record) keyed at load <= 1/2.  Tagged by the burst: zeroed only when
+    // (re)allocated, never cleared between bursts
+    uint64_t gt = 1024;
+    while (gt < 2 * (uint64_t)n) gt <<= 1;
+    uint64_t rt = 1024;
+    while (rt < 4 * (uint64_t)n + 2) rt <<= 1;
+    auto zeroed = [&](FlowScratch &x, size_t bytes) -> void * {
+      const bool fresh = bytes > x.cap;
+      void *p = x.get(bytes);
+      if (p && fresh && hipMemsetAsync(p, 0, x.cap, s) != hipSuccess) return nullptr;
+      return p;
+    };
+    fc.grp_tab = static_cast<unsigned long long *>(zeroed(c->grp_tab, sizeof(uint64_t) * gt));
+    fc.grp_head = static_cast<unsigned long long *>(zeroed(c->grp_head, sizeof(uint64_t) * gt));
+    fc.grp_next = static_cast<unsigned long long *>(c->grp_next.get(sizeof(uint64_t) * ((uint64_t)n + 1)));
+    fc.grp_list = static_cast<uint32_t *>(c->grp_list.get(sizeof(uint32_t) * ((uint64_t)n + 1)));
+    fc.repl = static_cast<uint4 *>(zeroed(c->repl, sizeof(uint4) * rt));
+    // a table grown since the last burst holds the smallest power of two
+    // that fits (its mask names that many entries, zeroed)
+    fc.grp_mask = (uint32_t)(c->grp_tab.cap / sizeof(uint64_t) < c->grp_head.cap / sizeof(uint64_t)
+                                 ? c->grp_tab.cap / sizeof(uint64_t) - 1 : c->grp_head.cap / sizeof(uint64_t) - 1);
+    fc.rmask = (uint32_t)(c->repl.cap / sizeof(uint4) - 1);
+    if (++c->burst_tag == 0) {  // tags wrapped: every entry is zeroed again
+      c->burst_tag = 1;
+      if (fc.grp_tab) (void)hipMemsetAsync(fc.grp_tab, 0, c->grp_tab.cap, s);
+      if (fc.grp_head) (void)hipMemsetAsync(fc.grp_head, 0, c->grp_head.cap, s);
+      if (fc.repl) (void)hipMemsetAsync(fc.repl, 0, c->repl.cap, s);
+    }
+    fc.burst = c->burst_tag;
+    fc.force_seq = g_nat_seq.load(std::memory_order_relaxed);
     if (words + sum_words > c->pf_bits_n) {
       c->pf_bits.release();
       c->pf_bits_n = 0;
@@ -624,6 +664,7 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.pf_bits = static_cast<uint32_t *>(c->pf_bits.p);
     fc.pf_sum = fc.pf_bits ? fc.pf_bits + words : nullptr;
     if (!fc.events || !fc.sens || !fc.pf || !fc.pf_cnt || !fc.pf_of || !fc.pf_order || !fc.pf_repl || !fc.mq_rel ||
+        !fc.grp_tab || !fc.grp_head || !fc.grp_next || !fc.grp_list || !fc.repl ||
         c->pf_bits_n < words + sum_words) {
       (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
       return fail(DP_ENOMEM, "flow burst scratch");
@@ -679,6 +720,10 @@ int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
   c->ft = ft;
   return 0;
 }
+
+// Test hook (not part of dpgpu.h): 1 runs every burst's NAT pass on one lane
+// in packet order (the parallel pass's reference in the parity tests and A/Bs).
+void dpf_debug_nat_sequential(int on) { g_nat_seq.store(on ? 1u : 0u, std::memory_order_relaxed); }
 
 // A flow table being destroyed leaves every device's registry.
 void dpr_forget_flow_table(dp_flow_table *ft) {

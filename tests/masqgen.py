@@ -81,7 +81,7 @@ def rev_of(c: Conn, out: dict, flags=0) -> Pkt:
     return Pkt(M.l4_frame(out["dst"], out["src"], c.proto, out["dport"], out["sport"], flags), V2)
 
 
-def run(r, seed: int, n_conn: int, capacity=None, on_burst=None):
+def run(r, seed: int, n_conn: int, capacity=None, on_burst=None, before_burst=None):
     """The bursts of one seed on runner r (masqkat.OracleRunner / GpuRunner);
     on_burst(k, res, buf, infos, lookups, related_infos) after each.  Replies
     are built from the runner's own translated packets."""
@@ -142,6 +142,8 @@ def run(r, seed: int, n_conn: int, capacity=None, on_burst=None):
             r.publish(world(*pub))
         if sweep:
             r.sweep(now)
+        if before_burst:
+            before_burst(k, r.lookup(keys))
         rng.shuffle(pk)
         pkts, who = [], []
         for (c, d, fl) in pk:
@@ -162,4 +164,4 @@ def run(r, seed: int, n_conn: int, capacity=None, on_burst=None):
         look = r.lookup(keys)
         rel = r.get(look["related"])
         if on_burst:
-            on_burst(k, res, buf, infos, look, rel)
+            on_burst(k, res, buf, infos, look, rel, pkts)

@@ -68,7 +68,7 @@ def test_gpu_masquerade_random_bursts(seed, n_conn, capacity):
         r = mk(slots=1 << 15) if name == "gpu" else mk()
         steps = []
         try:
-            masqgen.run(r, seed, n_conn, capacity, lambda k, res, buf, infos, look, rel: steps.append(
+            masqgen.run(r, seed, n_conn, capacity, lambda k, res, buf, infos, look, rel, pkts: steps.append(
                 (res.copy(), buf.copy(), infos.copy(), look.copy(), rel.copy(), r.count())))
         finally:
             if name == "gpu":

@@ -74,25 +74,33 @@ def test_gpu_portfw_kat(s):
             same_info(io, ig, co, cg, f"step {i}")
 
 
-@pytest.mark.parametrize("seed,n_conn,capacity", [(1, 600, None), (2, 2000, None), (5, 400, 300)])
-def test_gpu_portfw_random_bursts(seed, n_conn, capacity):
+@pytest.mark.parametrize("seed,n_conn,capacity,one_lane", [(1, 600, None, False), (2, 2000, None, False),
+                                                          (2, 2000, None, True), (5, 400, 300, False)])
+def test_gpu_portfw_random_bursts(seed, n_conn, capacity, one_lane):
     """Seeded bursts (tests/pfgen.py): creations, repeats, replies, TCP
     handshakes / teardowns / resets, uncovered packets, a rule-set change --
     and, with a small capacity, flow-pair creation refused at capacity; GPU ==
     oracle per burst (records, bytes, each packet's flow, every connection's
-    two flows by key) and the flow counts."""
+    two flows by key) and the flow counts.  The NAT pass runs one lane per
+    connection unless the capacity could bind (then, and with one_lane, one
+    lane in packet order)."""
     import pfgen
     got = {}
-    for name, mk in (("oracle", pfkat.OracleRunner), ("gpu", pfkat.GpuRunner)):
-        r = mk(slots=1 << 14) if name == "gpu" else mk()
-        steps = []
-        try:
-            pfgen.run(r, seed, n_conn, capacity, lambda k, res, buf, infos, look: steps.append(
-                (res.copy(), buf.copy(), infos.copy(), look.copy(), r.count())))
-        finally:
-            if name == "gpu":
-                r.close()
-        got[name] = steps
+    lib = A.gpu_lib()
+    lib.dpf_debug_nat_sequential(1 if one_lane else 0)
+    try:
+        for name, mk in (("oracle", pfkat.OracleRunner), ("gpu", pfkat.GpuRunner)):
+            r = mk(slots=1 << 14) if name == "gpu" else mk()
+            steps = []
+            try:
+                pfgen.run(r, seed, n_conn, capacity, lambda k, res, buf, infos, look: steps.append(
+                    (res.copy(), buf.copy(), infos.copy(), look.copy(), r.count())))
+            finally:
+                if name == "gpu":
+                    r.close()
+            got[name] = steps
+    finally:
+        lib.dpf_debug_nat_sequential(0)
     hist = {}
     ido, idg = IdCanon(), IdCanon()
     for k, (o, g) in enumerate(zip(got["oracle"], got["gpu"])):
