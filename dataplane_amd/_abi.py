@@ -261,8 +261,14 @@ GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_p
                "dp_flow_insert_pair", "dp_flow_lookup", "dp_flow_get", "dp_flow_remove",
                "dp_flow_invalidate", "dp_flow_set_status", "dp_flow_sweep", "dp_flow_count",
                "dp_ctx_attach_flow_table", "dp_mbuf_burst_in", "dp_mbuf_burst_out",
-               "dp_process_mbufs"]
-NP_STRUCTS = dict(dp_flow_key_t=FLOW_KEY, dp_flow_t=FLOW, dp_flow_info_t=FLOW_INFO)
+               "dp_process_mbufs", "dp_acl_classify", "dp_acl_classify_device"]
+# dp_acl_key_t / dp_acl_result_t (the ACL classifier alone)
+ACL_KEY = np.dtype([("src_vni", "<u4"), ("dst_vni", "<u4"), ("family", "u1"), ("proto", "u1"),
+                    ("sport", "<u2"), ("dport", "<u2"), ("pad", "u1", 2), ("src", "u1", 16),
+                    ("dst", "u1", 16)])
+ACL_RESULT = np.dtype([("rule", "<u4"), ("action", "u1"), ("scope", "u1"), ("acl", "u1"), ("pad", "u1")])
+NP_STRUCTS = dict(dp_flow_key_t=FLOW_KEY, dp_flow_t=FLOW, dp_flow_info_t=FLOW_INFO, dp_acl_key_t=ACL_KEY,
+                  dp_acl_result_t=ACL_RESULT)
 
 
 class MbufLayout(C.Structure):
@@ -332,6 +338,9 @@ def gpu_lib() -> C.CDLL:
         lib.dp_mbuf_burst_out.argtypes = [_VP, C.c_uint32, C.POINTER(MbufLayout), _VP, _VP]
         lib.dp_process_mbufs.argtypes = [_VP, _VP, C.c_uint64, _VP, C.c_uint32,
                                          C.POINTER(MbufLayout), _VP, C.c_uint32, _VP, _VP, _VP]
+        lib.dp_acl_classify.argtypes = [_VP, _VP, _VP, C.c_uint32]
+        lib.dp_acl_classify_device.argtypes = [_VP, _VP, _VP, C.c_uint32, _VP]
+        lib.dpf_debug_nat_sequential.argtypes = [C.c_int]
         if lib.dp_abi_version() != ABI_VERSION:
             raise RuntimeError("libdpgpu.so ABI version mismatch")
         _gpu = lib

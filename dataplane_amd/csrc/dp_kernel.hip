@@ -3948,9 +3948,18 @@ __device__ bool conn_key(const Img &g, const dpf::FlowCtx &fc, const dpf::PfReq 
 
 // The records of one connection (a list through grp_next, pushed in any
 // order) sorted by packet index: a merge sort of the linked list.
+// (The links are read and rewritten through relaxed atomics: a lane's
+// rewrite of a link must be what its next read of that link returns -- with
+// plain accesses the GPU build lost records of longer lists.)
+__device__ inline unsigned long long link_ld(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void link_st(unsigned long long *p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ uint32_t sort_conn(unsigned long long *nx, uint32_t list) {
-  auto next = [&](uint32_t r) { return (uint32_t)nx[r]; };
-  auto set_next = [&](uint32_t r, uint32_t v) { nx[r] = (nx[r] & 0xffffffff00000000ull) | v; };
+  auto next = [&](uint32_t r) { return (uint32_t)link_ld(&nx[r]); };
+  auto set_next = [&](uint32_t r, uint32_t v) { link_st(&nx[r], (link_ld(&nx[r]) & 0xffffffff00000000ull) | v); };
   if (list == dpf::kNoSlot || next(list) == dpf::kNoSlot) return list;
   for (uint32_t insize = 1;; insize *= 2) {
     uint32_t p = list, tail = dpf::kNoSlot, merges = 0;
@@ -3967,7 +3976,9 @@ __device__ uint32_t sort_conn(unsigned long long *nx, uint32_t list) {
       while (psize > 0 || (qsize > 0 && q != dpf::kNoSlot)) {
         uint32_t e;
         if (psize == 0) { e = q; q = next(q); qsize--; }
-        else if (qsize == 0 || q == dpf::kNoSlot || (nx[p] >> 32) <= (nx[q] >> 32)) { e = p; p = next(p); psize--; }
+        else if (qsize == 0 || q == dpf::kNoSlot || (link_ld(&nx[p]) >> 32) <= (link_ld(&nx[q]) >> 32)) {
+          e = p; p = next(p); psize--;
+        }
         else { e = q; q = next(q); qsize--; }
         if (tail != dpf::kNoSlot) set_next(tail, e);
         else list = e;
@@ -4046,7 +4057,7 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
     const unsigned long long want = tag | key;
     uint32_t h = dpm::kmix(key, 0x2545f491u, 0u) & fc.grp_mask;
     for (uint32_t p = 0; p <= fc.grp_mask;) {
-      const unsigned long long cur = fc.grp_tab[h];
+      const unsigned long long cur = __hip_atomic_load(&fc.grp_tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (cur == want) break;
       if ((cur >> 32) == fc.burst) { h = (h + 1) & fc.grp_mask; p++; continue; }
       if (atomicCAS(&fc.grp_tab[h], cur, want) == cur) {
@@ -4054,7 +4065,7 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
         break;
       }
     }
-    unsigned long long old = fc.grp_head[h];
+    unsigned long long old = __hip_atomic_load(&fc.grp_head[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
       const uint32_t prev = (old >> 32) == fc.burst ? (uint32_t)old : dpf::kNoSlot;
       fc.grp_next[rec] = ((unsigned long long)R.idx << 32) | prev;
@@ -4099,9 +4110,69 @@ __global__ void __launch_bounds__(256) dp_nat_resolve(const uint8_t *__restrict_
   const uint32_t ng = fc.pf_cnt[4];
   for (uint32_t e = gt; e < ng; e += gridDim.x * 256) {
     const uint32_t h = fc.grp_list[e];
+#ifdef DP_DEBUG_NAT_NOSORT
+    uint32_t r = (uint32_t)fc.grp_head[h];
+#else
     uint32_t r = pfw::sort_conn(fc.grp_next, (uint32_t)fc.grp_head[h]);
-    for (; r != dpf::kNoSlot; r = (uint32_t)fc.grp_next[r]) pfw::resolve_one(q, fc.pf[r]);
+#endif
+    for (; r != dpf::kNoSlot; r = (uint32_t)pfw::link_ld(&fc.grp_next[r])) {
+#ifdef DP_DEBUG_NAT
+      fc.pf[r].mnat_ip[0] = e;
+      atomicAdd(&fc.pf[r].mnat_ip[1], 1u);
+#endif
+      pfw::resolve_one(q, fc.pf[r]);
+    }
   }
+}
+
+// dp_acl_classify: AclFilter's classification alone (dpgpu.h "The ACL
+// classifier alone"), one key per work-item: the peering's ACL group, its
+// first matching rule, else the peering default, else Allow -- stage_acl's
+// decision without a packet around it.
+__global__ void __launch_bounds__(256) dp_acl_classify_k(const uint8_t *__restrict__ img_base,
+                                                         const Image *__restrict__ im,
+                                                         const dp_acl_key_t *__restrict__ keys,
+                                                         dp_acl_result_t *__restrict__ out, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const dp_acl_key_t k = keys[i];
+  dp_acl_result_t r{};
+  r.rule = 0xffffffffu;
+  if (k.family != 4 && k.family != 6) { out[i] = r; return; }
+  const Img g{img_base, *im};
+  const int t = k.family == 4 ? 0 : 1;
+  auto be = [&](const uint8_t *a, int o) {
+    return ((uint32_t)a[o] << 24) | ((uint32_t)a[o + 1] << 16) | ((uint32_t)a[o + 2] << 8) | a[o + 3];
+  };
+  Key128 ks, kd;
+  if (t == 0) {
+    ks = Key128{0, be(k.src, 0)};
+    kd = Key128{0, be(k.dst, 0)};
+  } else {
+    ks = Key128{((uint64_t)be(k.src, 0) << 32) | be(k.src, 4), ((uint64_t)be(k.src, 8) << 32) | be(k.src, 12)};
+    kd = Key128{((uint64_t)be(k.dst, 0) << 32) | be(k.dst, 4), ((uint64_t)be(k.dst, 8) << 32) | be(k.dst, 12)};
+  }
+  int32_t ag = -1;
+  uint32_t def = 0, pi;
+  if (hash_find(g, g.im.pairs, k.src_vni, k.dst_vni, 0, pi)) {
+    const PairRec &P = g.at<PairRec>(g.im.pair_recs)[pi];
+    ag = P.acl[t];
+    def = P.acl_def;
+  }
+  const Hit h = classify<W_ACTION | W_ORIG>(g, CLS_ARRAYS(acl, t), ag, t, k.proto, ks, kd, k.sport, k.dport);
+  if (h.rule >= 0) {
+    r.rule = h.orig;
+    r.action = (uint8_t)(h.action & 0xffu);
+    r.scope = (uint8_t)(h.action >> 8);
+    r.acl = r.action == DP_ACL_DENY ? 2 : 1;
+  } else if (def) {
+    r.action = (uint8_t)(def - 1);
+    r.acl = r.action == DP_ACL_DENY ? 4 : 3;
+  } else {
+    r.action = DP_ACL_ALLOW;
+    r.acl = 5;
+  }
+  out[i] = r;
 }
 
 // After the burst's pipeline kernel (flows variant), on its stream.
@@ -4378,6 +4449,14 @@ extern "C" int dpk_stage_collect(const uint8_t *buf, const uint32_t *pos, const 
                                  uint32_t grow, uint32_t n, hipStream_t stream) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(dp_stage_collect, dim3((n + 255) / 256), dim3(256), 0, stream, buf, pos, in, cout, grow, n);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int dpk_acl_classify(const uint8_t *img_base, const void *image_dev, const dp_acl_key_t *keys,
+                                dp_acl_result_t *out, uint32_t n, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dp_acl_classify_k, dim3((n + 255) / 256), dim3(256), 0, stream, img_base,
+                     reinterpret_cast<const Image *>(image_dev), keys, out, n);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -39,6 +39,8 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_de
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
                                    int v6w, hipStream_t stream);
+extern "C" int dpk_acl_classify(const uint8_t *img_base, const void *image_dev, const dp_acl_key_t *keys,
+                                dp_acl_result_t *out, uint32_t n, hipStream_t stream);
 extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
                                hipStream_t stream);
 extern "C" int dpk_stage_expand(const uint8_t *cin, const uint32_t *pos, const dp_pkt_in_t *in, uint8_t *buf,
@@ -705,6 +707,52 @@ int dp_process_burst_device(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes,
   return launch_burst(c, dev_buf, buf_bytes, dev_in, dev_out, dev_meta, n, dev_stats, stream);
 }
 
+int dp_acl_classify_device(dp_ctx_t *c, const dp_acl_key_t *dev_keys, dp_acl_result_t *dev_out, uint32_t n,
+                           void *stream) {
+  if (!c) return fail(DP_EINVAL, "null ctx");
+  if (n == 0) return 0;
+  if (!dev_keys || !dev_out) return fail(DP_EINVAL, "null keys / results");
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  reap(c);
+  auto img = current(c);
+  if (!img) return fail(DP_ENOTABLES, "no tables published");
+  if (dpk_acl_classify(img->dev, img->dev + img->im_off, dev_keys, dev_out, n, s))
+    return fail(DP_EIO, "ACL classify launch failed", hipGetLastError());
+  // the image stays alive until the lookups that read it complete
+  InFlight f;
+  f.img = img;
+  f.done = take_event(c);
+  if (f.done) (void)hipEventRecord(f.done, s);
+  c->inflight.push_back(std::move(f));
+  return 0;
+}
+
+int dp_acl_classify(dp_ctx_t *c, const dp_acl_key_t *keys, dp_acl_result_t *out, uint32_t n) {
+  if (!c) return fail(DP_EINVAL, "null ctx");
+  if (n == 0) return 0;
+  if (!keys || !out) return fail(DP_EINVAL, "null keys / results");
+  (void)hipSetDevice(c->device);
+  dp_acl_key_t *dk = nullptr;
+  dp_acl_result_t *dr = nullptr;
+  hipError_t e;
+  if ((e = hipMallocAsync((void **)&dk, sizeof(dp_acl_key_t) * (size_t)n, c->stream)) != hipSuccess ||
+      (e = hipMallocAsync((void **)&dr, sizeof(dp_acl_result_t) * (size_t)n, c->stream)) != hipSuccess) {
+    if (dk) (void)hipFreeAsync(dk, c->stream);
+    return fail(DP_ENOMEM, "ACL classify buffers", e);
+  }
+  int rc = 0;
+  if ((e = hipMemcpyAsync(dk, keys, sizeof(dp_acl_key_t) * (size_t)n, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    rc = fail(DP_EIO, "ACL keys copy", e);
+  if (!rc) rc = dp_acl_classify_device(c, dk, dr, n, c->stream);
+  if (!rc && (e = hipMemcpyAsync(out, dr, sizeof(dp_acl_result_t) * (size_t)n, hipMemcpyDeviceToHost, c->stream)) !=
+                 hipSuccess)
+    rc = fail(DP_EIO, "ACL results copy", e);
+  (void)hipFreeAsync(dk, c->stream);
+  (void)hipFreeAsync(dr, c->stream);
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess && !rc) rc = fail(DP_EIO, "ACL classify", e);
+  return rc;
+}
+
 int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
   if (!c) return fail(DP_EINVAL, "null ctx");
   if (ft && ft->device != c->device) return fail(DP_EINVAL, "flow table on another device");
@@ -724,6 +772,34 @@ int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
 // Test hook (not part of dpgpu.h): 1 runs every burst's NAT pass on one lane
 // in packet order (the parallel pass's reference in the parity tests and A/Bs).
 void dpf_debug_nat_sequential(int on) { g_nat_seq.store(on ? 1u : 0u, std::memory_order_relaxed); }
+
+// Test hook (not part of dpgpu.h): the context's last flows burst's NAT pass
+// -- its counters (pf_cnt[0..7]) and up to `max` records (dpf::PfReq).
+// With `next` (u64 per record) and `heads` (u64 per connection): the
+// records' list links and each connection's list head.
+int dpf_debug_nat_records(dp_ctx_t *c, uint32_t *cnt8, void *recs, uint32_t max, uint64_t *next,
+                          uint64_t *heads) {
+  if (!c || !cnt8) return DP_EINVAL;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (!c->pf_cnt.p) return DP_EINVAL;
+  if (hipMemcpy(cnt8, c->pf_cnt.p, sizeof(uint32_t) * 8, hipMemcpyDeviceToHost) != hipSuccess) return DP_EIO;
+  const uint32_t k = cnt8[0] < max ? cnt8[0] : max;
+  if (k && recs && hipMemcpy(recs, c->pf_req.p, sizeof(dpf::PfReq) * k, hipMemcpyDeviceToHost) != hipSuccess)
+    return DP_EIO;
+  if (k && next && hipMemcpy(next, c->grp_next.p, sizeof(uint64_t) * k, hipMemcpyDeviceToHost) != hipSuccess)
+    return DP_EIO;
+  if (heads && cnt8[4] && c->grp_list.p) {
+    std::vector<uint32_t> lst(cnt8[4]);
+    std::vector<uint64_t> tab(c->grp_head.cap / 8);
+    if (hipMemcpy(lst.data(), c->grp_list.p, 4 * lst.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(tab.data(), c->grp_head.p, c->grp_head.cap, hipMemcpyDeviceToHost) != hipSuccess)
+      return DP_EIO;
+    for (size_t e = 0; e < lst.size(); e++) heads[e] = tab[lst[e]];
+  }
+  return 0;
+}
+uint32_t dpf_debug_nat_record_bytes(void) { return sizeof(dpf::PfReq); }
 
 // A flow table being destroyed leaves every device's registry.
 void dpr_forget_flow_table(dp_flow_table *ft) {

@@ -204,6 +204,16 @@ class GpuPathNf:
     def device_table_bytes(self) -> int:
         return int(self.lib.dp_tables_device_bytes(self.ctx))
 
+    def acl_classify(self, keys: np.ndarray) -> np.ndarray:
+        """The ACL classifier alone (dp_acl_classify): A.ACL_KEY records ->
+        A.ACL_RESULT records (the batch Lookup<K, A> of the reference's
+        DpdkAclLookup, acl/src/dpdk/lookup.rs:112-155)."""
+        keys = np.ascontiguousarray(np.atleast_1d(keys), dtype=A.ACL_KEY)
+        out = np.zeros(len(keys), dtype=A.ACL_RESULT)
+        A.check(self.lib.dp_acl_classify(self.ctx, keys.ctypes.data, out.ctypes.data, len(keys)),
+                "dp_acl_classify", self.lib)
+        return out
+
     def close(self) -> None:
         if self.ctx:
             self.lib.dp_ctx_destroy(self.ctx)

@@ -587,6 +587,43 @@ enum dp_host_path { DP_HOST_AUTO = 0, DP_HOST_COPY = 1, DP_HOST_ZERO_COPY = 2 };
 int dp_ctx_set_option(dp_ctx_t *ctx, int option, int64_t value);
 
 /* ------------------------------------------------------------------------ */
+/* The ACL classifier alone (the narrower drop-in for A14):   */
+/* AclFilter's classification as a batch lookup -- the reference's           */
+/* Lookup<K, A> / DpdkAclLookup::lookup_batch (lookup/src/lib.rs:24-38,      */
+/* acl/src/dpdk/lookup.rs:112-155), an rte_acl replacement.  Each key is     */
+/* matched against the ACL of its (source VPC, destination VPC) peering in   */
+/* the published tables: the first rule in rule order whose prefixes, ports  */
+/* and protocol hold it, else the peering's default, else Allow              */
+/* (acl-filter/src/lib.rs:96-137, acl/src/reference/table.rs:94-101).        */
+/* ------------------------------------------------------------------------ */
+typedef struct dp_acl_key {
+    uint32_t src_vni, dst_vni;  /* the peering */
+    uint8_t family;             /* 4 or 6 */
+    uint8_t proto;              /* IP next header */
+    uint16_t sport, dport;      /* 0 for a protocol without ports */
+    uint8_t pad[2];
+    uint8_t src[16], dst[16];   /* network byte order; v4 in the first 4 bytes */
+} dp_acl_key_t;                 /* 48 B */
+
+typedef struct dp_acl_result {
+    uint32_t rule;    /* index of the matching rule in the published acl_v4 / acl_v6,
+                         UINT32_MAX when none matched */
+    uint8_t action;   /* enum dp_acl_action the key gets */
+    uint8_t scope;    /* enum dp_acl_scope of the matching rule (0 without one) */
+    uint8_t acl;      /* dp_pkt_out_t.acl's code: 1 / 2 rule allow / deny, 3 / 4 peering
+                         default allow / deny, 5 no ACL for the peering; 0: a key of
+                         another family than 4 / 6 (not classified) */
+    uint8_t pad;
+} dp_acl_result_t;    /* 8 B */
+
+/* Classify n keys resident on the context's device into dev_out (stream as in
+ * dp_process_burst_device; asynchronous there). */
+int dp_acl_classify_device(dp_ctx_t *ctx, const dp_acl_key_t *dev_keys, dp_acl_result_t *dev_out,
+                           uint32_t n, void *stream);
+/* The same for keys and results in host memory (synchronous). */
+int dp_acl_classify(dp_ctx_t *ctx, const dp_acl_key_t *keys, dp_acl_result_t *out, uint32_t n);
+
+/* ------------------------------------------------------------------------ */
 /* Flow table: FlowTable                              */
 /* (flow-entry/src/flow_table/table.rs:24-330) resident in HBM, consulted by */
 /* the FlowLookup stage (nf_lookup.rs:34-55) and by the flow-aware branches  */

@@ -3592,6 +3592,39 @@ int64_t dpo_acl_lookup(const dpo_tables_t *t, uint8_t family, uint8_t proto, uin
   return r < 0 ? -1 : (int64_t)tab[r].orig_index;
 }
 
+// The ACL classifier alone (dpgpu.h dp_acl_classify): AclFilter's decision
+// for a key (acl-filter/src/lib.rs:96-137): the first matching rule of the
+// peering, else its default, else Allow.
+int dpo_acl_classify(const dpo_tables_t *t, const dp_acl_key_t *keys, dp_acl_result_t *out, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) {
+    const dp_acl_key_t &k = keys[i];
+    dp_acl_result_t r{};
+    r.rule = UINT32_MAX;
+    if (k.family == 4 || k.family == 6) {
+      const Key key{k.proto, k.src_vni, k.dst_vni, 0, k.src, k.dst, k.sport, k.dport};
+      const auto &tab = k.family == 4 ? t->acl4 : t->acl6;
+      const int64_t ri = classify(tab, key, k.family);
+      if (ri >= 0) {
+        r.rule = tab[ri].orig_index;
+        r.action = (uint8_t)tab[ri].r.action;
+        r.scope = (uint8_t)tab[ri].r.action2;
+        r.acl = r.action == DP_ACL_DENY ? 2 : 1;
+      } else {
+        auto it = t->acl_default.find({k.src_vni, k.dst_vni});
+        if (it != t->acl_default.end()) {
+          r.action = (uint8_t)it->second;
+          r.acl = r.action == DP_ACL_DENY ? 4 : 3;
+        } else {
+          r.action = DP_ACL_ALLOW;
+          r.acl = 5;
+        }
+      }
+    }
+    out[i] = r;
+  }
+  return 0;
+}
+
 int dpo_nat_lookup(const dpo_tables_t *t, uint32_t kind, uint32_t src_vni, uint32_t dst_vni,
                    const uint8_t *addr4, int has_port, uint16_t port, uint8_t *new_addr4,
                    uint16_t *new_port) {

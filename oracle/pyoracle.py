@@ -40,6 +40,7 @@ def lib() -> C.CDLL:
         l.dpo_acl_lookup.argtypes = [V, C.c_uint8, C.c_uint8, C.c_uint32, C.c_uint32, V, V,
                                      C.c_int, C.c_uint16, C.c_uint16]
         l.dpo_acl_lookup.restype = C.c_int64
+        l.dpo_acl_classify.argtypes = [V, V, V, C.c_uint32]
         l.dpo_nat_lookup.argtypes = [V, C.c_uint32, C.c_uint32, C.c_uint32, V, C.c_int,
                                      C.c_uint16, V, V]
         l.dpo_checksum_ipv4_header.argtypes = [V, C.c_uint32]
@@ -79,6 +80,14 @@ class Oracle:
     def rule_alive(self, rule_id: int) -> bool:
         """Does port-forwarding entry `rule_id` live in these tables?"""
         return bool(lib().dpo_portfw_rule_alive(self.h, rule_id))
+
+    def acl_classify(self, keys: np.ndarray) -> np.ndarray:
+        """AclFilter's decision per A.ACL_KEY record (dpgpu.h dp_acl_classify)."""
+        keys = np.ascontiguousarray(keys, dtype=A.ACL_KEY)
+        out = np.zeros(len(keys), dtype=A.ACL_RESULT)
+        if lib().dpo_acl_classify(self.h, keys.ctypes.data, out.ctypes.data, len(keys)) != 0:
+            raise RuntimeError("oracle acl_classify failed")
+        return out
 
     def process(self, buf: np.ndarray, inp: np.ndarray, stats: bool = False):
         """One burst, in place: PKT_RES records (dp_pkt_out_t + dp_pkt_meta_t)."""

@@ -2,6 +2,7 @@
 they first differ (flows by key before a burst, then the burst's packets)."""
 import sys
 sys.path.insert(0, "tests")
+sys.path.insert(0, ".")
 import numpy as np
 import masqgen
 from golden import masqkat as M
