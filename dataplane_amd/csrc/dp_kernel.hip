@@ -3443,6 +3443,8 @@ struct Seq {
       const uint32_t st = s.state & 3u;
       if (st == dpf::FS_EMPTY) { if (free_ == dpf::kNoSlot) free_ = i; break; }
       if (st == dpf::FS_TOMB) { if (free_ == dpf::kNoSlot) free_ = i; continue; }
+      // a slot another lane is filling still shows the key of its last fill
+      if (st == dpf::FS_BUSY) continue;
       if (s.src_vni == k.w[0] && s.fk == k.w[1] && s.ports == k.w[2] && s.src[0] == k.w[3] &&
           s.src[1] == k.w[4] && s.src[2] == k.w[5] && s.src[3] == k.w[6] && s.dst[0] == k.w[7] &&
           s.dst[1] == k.w[8] && s.dst[2] == k.w[9] && s.dst[3] == k.w[10]) { found = i; break; }
