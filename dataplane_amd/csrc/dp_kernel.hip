@@ -125,6 +125,28 @@ constexpr uint8_t DONE_NONE = 255;
 #endif
 
 // ---------------------------------------------------------------------------
+// Wave-aggregated counters
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// The next index of a burst-wide counter for each active lane that wants one
+// (want): one atomic per wave, not one per lane -- lanes of a whole chip
+// adding to one word are served one by one at its L2 channel.  Every active
+// lane calls it; a lane that does not want one gets an unspecified value.
+__device__ __forceinline__ uint32_t wave_claim(uint32_t *ctr, bool want) {
+#ifdef DP_EMU  // one lane at a time
+  return want ? atomicAdd(ctr, 1u) : 0u;
+#else
+  const uint64_t m = __ballot(want);
+  if (!m) return 0;
+  const int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+  return (uint32_t)__shfl((int)base, leader) + (uint32_t)__popcll(m & lanes_below(lane));
+#endif
+}
+
+// ---------------------------------------------------------------------------
 // Image access
 // ---------------------------------------------------------------------------
 struct ImgBase {
@@ -2274,7 +2296,7 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
         (S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST)) && !fc->replay) {
       dpf::FKey k;
       if (packet_fkey(F, H, S, k)) {
-        fp.pf_rec = atomicAdd(&fc->pf_cnt[0], 1u);
+        fp.pf_rec = wave_claim(&fc->pf_cnt[0], true);
         dpf::PfReq *R = fc->pf + fp.pf_rec;
 #pragma unroll
         for (int j = 0; j < 11; j++) R->ikey[j] = k.w[j];
@@ -2389,7 +2411,8 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
 // the replay pass finishes it with the pass's decisions.
 __device__ __forceinline__ void nat_record(const Frame &F, const Hdr &H, const State &S, FlowPk &fp,
                                            const dpf::FlowCtx *fc, uint32_t idx) {
-  const uint32_t rec = fp.pf_rec != dpf::kNoSlot ? fp.pf_rec : atomicAdd(&fc->pf_cnt[0], 1u);
+  const uint32_t claim = wave_claim(&fc->pf_cnt[0], fp.pf_rec == dpf::kNoSlot);
+  const uint32_t rec = fp.pf_rec != dpf::kNoSlot ? fp.pf_rec : claim;
   dpf::PfReq *R = fc->pf + rec;
   uint32_t bits = (fp.pf_rec != dpf::kNoSlot ? R->bits : 0u) | dpf::kPqReached | dpf::kPqEth;
   if (S.flags & DP_META_REQ_PORT_FORWARDING) bits |= dpf::kPqPf;
@@ -2437,9 +2460,7 @@ __device__ __forceinline__ void nat_record(const Frame &F, const Hdr &H, const S
   R->acl_def = fp.def_acl;
   R->acl_rule6 = fp.acl_rule6;
   R->acl_over = 0;
-  fc->pf_of[idx] = rec;
-  atomicOr(&fc->pf_bits[idx >> 5], 1u << (idx & 31));
-  atomicOr(&fc->pf_sum[idx >> 15], 1u << ((idx >> 10) & 31));
+  fc->pf_of[idx] = rec;  // (its bit in the burst's bitmap: flow_effects, per wave)
   fp.pf_rec = rec;
   fp.deferred = true;
 }
@@ -3156,8 +3177,6 @@ __device__ __forceinline__ void wave_store_windows(uint8_t *buf, const uint8_t *
   }
 }
 
-__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
-
 // The flow-table effects of a wave's packets (FL only), wave-aggregated:
 // flow refs, invalidation marks and events, flow-dependent ACL verdicts.
 template <bool MT>
@@ -3197,6 +3216,19 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
       fc.events[1 + 2 * k] = fp.ev1;
       fc.events[2 + 2 * k] = fp.state;
     }
+  }
+  // the packets recorded for the NAT pass: a wave's 64 packets are the two
+  // bitmap words it alone owns (first pass: packet i on lane i % 64), stored
+  // whole; the region's summary bit once per wave, read first (a chip's
+  // worth of waves on a few summary words would queue at one L2 channel)
+  const uint64_t mr = __ballot(live && fp.deferred);
+  if (mr && lane == __ffsll((long long)mr) - 1) {
+    const uint32_t w0 = (i - lane) >> 5;
+    if ((uint32_t)mr) fc.pf_bits[w0] = (uint32_t)mr;
+    if (mr >> 32) fc.pf_bits[w0 + 1] = (uint32_t)(mr >> 32);
+    uint32_t *sw = &fc.pf_sum[i >> 15];
+    const uint32_t sb = 1u << ((i >> 10) & 31);
+    if (!(__hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & sb)) atomicOr(sw, sb);
   }
   const bool sv = has && fp.sens && !fp.deferred;  // a deferred packet's verdict: dp_nat_resolve
   const uint64_t ms = __ballot(sv);
@@ -3379,6 +3411,10 @@ struct Seq {
   const dpf::FlowCtx &fc;
   const Img &g;
   bool par;
+  // par: the lane's inserts, added to the table length once per wave when
+  // the pass ends (no insert of a parallel pass reads the length: it cannot
+  // reach the capacity)
+  mutable uint32_t added = 0;
   __device__ uint32_t bump(uint32_t *c) const { return par ? atomicAdd(c, 1u) : (*c)++; }
   __device__ bool alive(uint32_t sl, uint32_t tag) const { return sl <= fc.mask && fc.slots[sl].state == tag; }
   // the pair is invalid for packet idx: either flow's burst-local mark says
@@ -3504,8 +3540,10 @@ struct Seq {
         if (atomicCAS(&fc.slots[j].state, st, (st & ~3u) | dpf::FS_BUSY) == st) { sl = j; break; }
       }
       if (sl == dpf::kNoSlot) return dpf::kNoSlot;
-      atomicMax(&fc.tmeta[0], (sl - home) & fc.mask);
-      atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), 1ull);
+      const uint32_t disp = (sl - home) & fc.mask;
+      if (disp > __hip_atomic_load(&fc.tmeta[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(&fc.tmeta[0], disp);
+      added++;
     }
     dpf::FlowSlot &s = fc.slots[sl];
     const uint32_t old = s.state;  // (a claimed slot: BUSY, its tag kept)
@@ -4015,7 +4053,13 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
       const uint32_t r = r0 + t;
       uint32_t c = 0;
       const bool hit = r < regions && ((fc.pf_sum[r >> 5] >> (r & 31)) & 1u);
-      if (hit) for (int w = 0; w < 32; w++) c += __popc(fc.pf_bits[r * 32 + w]);
+      // the region's 32 words, loaded together and kept (the stores below
+      // may alias them for the compiler: reloading serialised 32 round trips)
+      uint32_t bw[32];
+#pragma unroll
+      for (int w = 0; w < 32; w++) bw[w] = hit ? fc.pf_bits[r * 32 + w] : 0u;
+#pragma unroll
+      for (int w = 0; w < 32; w++) c += __popc(bw[w]);
       cnt[t] = c;
       __syncthreads();
       for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan
@@ -4026,9 +4070,10 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
       }
       uint32_t pos = total + cnt[t] - c;
       if (hit) {
+#pragma unroll
         for (int w = 0; w < 32; w++) {
-          uint32_t b = fc.pf_bits[r * 32 + w];
-          fc.pf_bits[r * 32 + w] = 0;
+          uint32_t b = bw[w];
+          if (b) fc.pf_bits[r * 32 + w] = 0;
           while (b) {
             const int k = __ffs(b) - 1;
             b &= b - 1;
@@ -4055,18 +4100,24 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
     const dpf::PfReq &R = fc.pf[rec];
     if (!(R.bits & dpf::kPqReached)) continue;  // a flow-filter record of a packet dropped before NAT
     uint32_t key;
-    if (!pfw::conn_key(g, fc, R, key)) { atomicOr(&fc.pf_cnt[5], 1u); continue; }
+    if (!pfw::conn_key(g, fc, R, key)) {
+      if (!__hip_atomic_load(&fc.pf_cnt[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicOr(&fc.pf_cnt[5], 1u);
+      continue;
+    }
     const unsigned long long want = tag | key;
     uint32_t h = dpm::kmix(key, 0x2545f491u, 0u) & fc.grp_mask;
+    bool fresh = false;
     for (uint32_t p = 0; p <= fc.grp_mask;) {
       const unsigned long long cur = __hip_atomic_load(&fc.grp_tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (cur == want) break;
       if ((cur >> 32) == fc.burst) { h = (h + 1) & fc.grp_mask; p++; continue; }
       if (atomicCAS(&fc.grp_tab[h], cur, want) == cur) {
-        fc.grp_list[atomicAdd(&fc.pf_cnt[4], 1u)] = h;
+        fresh = true;
         break;
       }
     }
+    const uint32_t at = wave_claim(&fc.pf_cnt[4], fresh);
+    if (fresh) fc.grp_list[at] = h;
     unsigned long long old = __hip_atomic_load(&fc.grp_head[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
       const uint32_t prev = (old >> 32) == fc.burst ? (uint32_t)old : dpf::kNoSlot;
@@ -4125,6 +4176,11 @@ __global__ void __launch_bounds__(256) dp_nat_resolve(const uint8_t *__restrict_
       pfw::resolve_one(q, fc.pf[r]);
     }
   }
+  // the table length, one add per wave (every lane of the wave is here)
+  uint32_t v = q.added;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0 && v)
+    atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), (unsigned long long)v);
 }
 
 // dp_acl_classify: AclFilter's classification alone (dpgpu.h "The ACL
@@ -4510,9 +4566,11 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   if (meta) dpk_run_pipeline_110(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   else dpk_run_pipeline_100(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   // the NAT pass: records filed by connection, then resolved
-  const uint32_t pb = (n + 1023) / 1024 < 256 ? (n + 1023) / 1024 : 256;
+  // (grids of a lane per possible record / connection: each lane's work is a
+  // chain of dependent table accesses, so lanes, not bandwidth, set the pace)
+  const uint32_t pb = (n + 1023) / 1024 < 2048 ? (n + 1023) / 1024 : 2048;
   hipLaunchKernelGGL(dp_nat_prep, dim3(pb), dim3(1024), 0, stream, img_base, im, fc);
-  const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  const uint32_t rb = (n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192;
   hipLaunchKernelGGL(dp_nat_resolve, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   fc.replay = 1;
   if (meta) dpk_run_pipeline_111(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);

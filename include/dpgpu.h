@@ -16,8 +16,10 @@
  * attached to the context (dp_ctx_attach_flow_table; none attached = an
  * empty table).  PortForwarder runs on the GPU over the
  * port-forwarding rules of the tables (dp_portfw_rule_t) and creates its flow
- * pairs in the attached flow table; masquerade exposes are refused at
- * publish.
+ * pairs in the attached flow table; Masquerade runs on the GPU over the
+ * masquerade exposes (dp_masq_expose_t) with its port allocator as device
+ * state of the attached flow table.  AclFilter's classifier is also callable
+ * alone (dp_acl_classify: the batch Lookup of acl/src/dpdk/lookup.rs).
  *
  * A Rust `GpuPathNf: NetworkFunction` materialises the burst
  * exactly like FlowFilter::process does (flow-filter/src/lib.rs:357-362),

@@ -31,6 +31,8 @@ static inline uint32_t atomicOr(uint32_t *p, uint32_t v) { uint32_t o = *p; *p =
 static inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) {
   unsigned long long o = *p; *p = o + v; return o;
 }
+#define __HIP_MEMORY_SCOPE_AGENT 0
+template <class T> static inline T __hip_atomic_load(const T *p, int, int) { return *p; }
 static inline uint32_t atomicMin(uint32_t *p, uint32_t v) { uint32_t o = *p; if (v < o) *p = v; return o; }
 static inline int __popc(uint32_t x) { return __builtin_popcount(x); }
 static inline int __ffs(uint32_t x) { return __builtin_ffs((int)x); }
