@@ -69,6 +69,13 @@ def main():
     orders["xcd_dst"] = np.concatenate(xb)
     # source VNI, then the destination's top 8 bits within it
     orders["by_vni_dst8"] = np.lexsort((dst >> 24, vni))
+    # coarse destination buckets (a device counting sort's key): top 8 / 12 / 16 bits,
+    # packets of one bucket in burst order
+    for b in (8, 12, 16):
+        orders[f"by_dst{b}"] = np.argsort(dst >> (32 - b), kind="stable")
+    only = os.environ.get("ORDERS")
+    if only:
+        orders = {k: v for k, v in orders.items() if k in only.split(",")}
     bb = (w.buf.nbytes + 255) & ~255
     pristine = torch.from_numpy(w.buf).to(dev)
     buf = torch.empty(bb, dtype=torch.uint8, device=dev)
