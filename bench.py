@@ -196,7 +196,8 @@ def flows_leg(nf, w, dev, stream, steps: int) -> dict:
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps + 2)]
     for k2 in range(steps + 2):
-        b[:w.buf.nbytes].copy_(pristine)
+        with torch.cuda.stream(stream):  # on the launch stream: no copy overlaps a launch
+            b[:w.buf.nbytes].copy_(pristine)
         ev[k2][0].record(stream)
         nf.process_device(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None, sptr,
                           dev_meta=dmeta.data_ptr())

@@ -341,6 +341,8 @@ def gpu_lib() -> C.CDLL:
         lib.dp_acl_classify.argtypes = [_VP, _VP, _VP, C.c_uint32]
         lib.dp_acl_classify_device.argtypes = [_VP, _VP, _VP, C.c_uint32, _VP]
         lib.dpf_debug_nat_sequential.argtypes = [C.c_int]
+        lib.dpf_debug_flows_full.argtypes = [C.c_int]
+        lib.dpf_debug_last_lean.restype = C.c_int
         if lib.dp_abi_version() != ABI_VERSION:
             raise RuntimeError("libdpgpu.so ABI version mismatch")
         _gpu = lib

@@ -393,6 +393,11 @@ struct Image {
   uint32_t v6w_c;
   uint32_t v6w_fib;  // 1: some v6 FIB has a window table (Lpm.wtab)
   uint64_t v6w_p;
+  // 1: the image configures stateful NAT -- a flow-filter rule requiring port
+  // forwarding or masquerade, a port-forwarding rule or a masquerade expose
+  // (the flows variant without that code serves tables that never held it)
+  uint32_t snat;
+  uint32_t pad_snat;
 };
 
 // 32-bit mixing hash for the open-addressing maps (host and device agree)

@@ -166,6 +166,7 @@ struct FlowCtx {
   uint4 *repl;
   uint32_t rmask;
   uint32_t force_seq;   // test hook (dpf_debug_nat_sequential): the one-lane NAT pass always
+  uint32_t lean;        // the launch runs the flows variant without stateful NAT (dp_kernel.hip DP_SNAT)
 };
 
 // A packet whose ACL verdict was "allow: reply of a flow-scope-allowed flow";

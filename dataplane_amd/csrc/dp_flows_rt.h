@@ -66,6 +66,9 @@ struct dp_flow_table {
   std::shared_ptr<const dpd::MasqConfig> mq_cfg;
   uint64_t mq_serial = 0;
   FlowScratch mq_rel;
+  // a burst under an image that configures stateful NAT ran on the table (its
+  // flows may carry NAT state from then on): bursts keep the full flows variant
+  bool snat_seen = false;
 };
 
 // update_nat_allocator (nat/src/masquerade/allocator_writer.rs:120-154) for

@@ -42,12 +42,25 @@ using namespace dpd;
 // the non-flow pipeline without them, parts 7 and 8 with them, and
 // dpk_launch_pipeline picks by the image; every other unit has them.
 #ifndef DP_V6W
-#if DP_PART == 1 || DP_PART == 2
+#if DP_PART == 1 || DP_PART == 2 || DP_PART == 9 || DP_PART == 10
 #define DP_V6W 0
 #else
 #define DP_V6W 1
 #endif
 #endif
+// DP_SNAT: stateful NAT (port forwarding, masquerade: their records, the
+// flow-filter and ICMP-error branches of flows with NAT state) compiled into
+// the flows variant.  Parts 9 and 10 build the flows first pass without it
+// (and without the v6 window lookups) for images that configure no stateful
+// NAT served by flow tables that never held NAT state (dpk_launch_pipeline_flows).
+#ifndef DP_SNAT
+#if DP_PART == 9 || DP_PART == 10
+#define DP_SNAT 0
+#else
+#define DP_SNAT 1
+#endif
+#endif
+constexpr bool SNAT = DP_SNAT;
 #ifndef DP_TPB
 #define DP_TPB 128
 #endif
@@ -1749,7 +1762,7 @@ __device__ __forceinline__ void icmp_error_flow(const dpf::FlowCtx &fc, const Fr
   if (sl == dpf::kNoSlot) return;  // no flow: let it through (nf.rs:114-121)
   if (v.x != DP_FLOW_ACTIVE) { done(S, DP_DONE_FILTERED); return; }  // nf.rs:126-130
   S.dst_vni = v.z;                                                   // nf.rs:139-140
-  if (!(v.y & (dpf::kFlagPf | dpf::kFlagMasq))) { done(S, DP_DONE_FILTERED); return; }  // no NAT state (:143-152)
+  if (!SNAT || !(v.y & (dpf::kFlagPf | dpf::kFlagMasq))) { done(S, DP_DONE_FILTERED); return; }  // no NAT state (:143-152)
 #ifdef DP_X_NOICMP
   return;
 #endif
@@ -2223,8 +2236,8 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   if constexpr (FL) {
     if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid) {
       S.dst_vni = fp.dst_vni;
-      if (fp.fflags & dpf::kFlagMasq) S.flags |= DP_META_REQ_MASQUERADE;
-      if (fp.fflags & dpf::kFlagPf) S.flags |= DP_META_REQ_PORT_FORWARDING;
+      if (SNAT && (fp.fflags & dpf::kFlagMasq)) S.flags |= DP_META_REQ_MASQUERADE;
+      if (SNAT && (fp.fflags & dpf::kFlagPf)) S.flags |= DP_META_REQ_PORT_FORWARDING;
       if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_SRC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
       if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_DST) S.flags |= DP_META_REQ_STATIC_NAT_DST;
       return;
@@ -2233,7 +2246,7 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
     // is revalidated against the remote rules gated on its destination VPC,
     // that of a port-forwarded pair against the local rules gated on
     // PortFwdReply
-    if (fp.slot != dpf::kNoSlot && fp.active && fp.genid < fc->genid && !(fp.fflags & DP_FLOW_INITIATOR)) {
+    if (SNAT && fp.slot != dpf::kNoSlot && fp.active && fp.genid < fc->genid && !(fp.fflags & DP_FLOW_INITIATOR)) {
       if (fp.fflags & dpf::kFlagMasq) gate_vni = fp.dst_vni;
       else if (fp.fflags & dpf::kFlagPf) gate = 1;
     }
@@ -2286,13 +2299,13 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   // set_nat_requirements (lib.rs:233-246)
   if (snat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
   if (dnat == DP_NAT_STATIC) S.flags |= DP_META_REQ_STATIC_NAT_DST;
-  if (snat == DP_NAT_PORT_FORWARDING || dnat == DP_NAT_PORT_FORWARDING) S.flags |= DP_META_REQ_PORT_FORWARDING;
-  if (snat == DP_NAT_MASQUERADE || dnat == DP_NAT_MASQUERADE) S.flags |= DP_META_REQ_MASQUERADE;
+  if (SNAT && (snat == DP_NAT_PORT_FORWARDING || dnat == DP_NAT_PORT_FORWARDING)) S.flags |= DP_META_REQ_PORT_FORWARDING;
+  if (SNAT && (snat == DP_NAT_MASQUERADE || dnat == DP_NAT_MASQUERADE)) S.flags |= DP_META_REQ_MASQUERADE;
   if constexpr (FL) {
     // the key before static NAT, for the flow pair port forwarding or
     // masquerade creates (lib.rs:193-201): recorded in the packet's NAT record
 #ifndef DP_X_NOIKEY
-    if ((S.flags & (DP_META_REQ_PORT_FORWARDING | DP_META_REQ_MASQUERADE)) &&
+    if (SNAT && (S.flags & (DP_META_REQ_PORT_FORWARDING | DP_META_REQ_MASQUERADE)) &&
         (S.flags & (DP_META_REQ_STATIC_NAT_SRC | DP_META_REQ_STATIC_NAT_DST)) && !fc->replay) {
       dpf::FKey k;
       if (packet_fkey(F, H, S, k)) {
@@ -2308,8 +2321,8 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
     // is outdated if its destination or its NAT requirements differ, or if
     // it no longer needs state
     if (fp.slot != dpf::kNoSlot && fp.genid != fc->genid) {
-      const bool pf = S.flags & DP_META_REQ_PORT_FORWARDING, need_pf = fp.fflags & dpf::kFlagPf;
-      const bool mq = S.flags & DP_META_REQ_MASQUERADE, need_mq = fp.fflags & dpf::kFlagMasq;
+      const bool pf = SNAT && (S.flags & DP_META_REQ_PORT_FORWARDING), need_pf = SNAT && (fp.fflags & dpf::kFlagPf);
+      const bool mq = SNAT && (S.flags & DP_META_REQ_MASQUERADE), need_mq = SNAT && (fp.fflags & dpf::kFlagMasq);
       if (fp.dst_vni != dvni || mq != need_mq || pf != need_pf || (!pf && !mq)) fp.ev0 = fp.slot;
     }
   }
@@ -3056,11 +3069,13 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
 #ifndef DP_PROBE_NONAT
   stage_static_nat(g, F, H, S, P);
 #endif
+  if constexpr (SNAT) {
 #ifndef DP_X_NOPF
-  stage_portfw<FL>(F, H, S, fp, fc, idx, rp);
+    stage_portfw<FL>(F, H, S, fp, fc, idx, rp);
 #endif
-  stage_masquerade<FL>(F, H, S, fp, fc, idx, rp);
-  if constexpr (FL) {
+    stage_masquerade<FL>(F, H, S, fp, fc, idx, rp);
+  }
+  if constexpr (FL && SNAT) {
     if (fp.deferred) {  // finished by the replay pass
       o.done = DONE_NONE;
       return DONE_NONE;
@@ -3221,7 +3236,7 @@ __device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, 
   // bitmap words it alone owns (first pass: packet i on lane i % 64), stored
   // whole; the region's summary bit once per wave, read first (a chip's
   // worth of waves on a few summary words would queue at one L2 channel)
-  const uint64_t mr = __ballot(live && fp.deferred);
+  const uint64_t mr = SNAT ? __ballot(live && fp.deferred) : 0ull;
   if (mr && lane == __ffsll((long long)mr) - 1) {
     const uint32_t w0 = (i - lane) >> 5;
     if ((uint32_t)mr) fc.pf_bits[w0] = (uint32_t)mr;
@@ -4401,9 +4416,11 @@ extern "C" void dpemu_trips_out(uint16_t *p) { dp_trip_out = p; }
   uint32_t blocks, hipStream_t s, const uint8_t *img_base, const Image *im, uint8_t *buf, uint64_t buf_bytes, \
       const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n, unsigned long long *part,   \
       const dpf::FlowCtx &fc
+// (the kernel's last template argument names the unit's build: DP_V6W, + 2
+// without stateful NAT)
 #define DP_RUNNER(NAME, FL, MT, RP)                                                                   \
   extern "C" void NAME(DP_RUN_ARGS) {                                                                 \
-    hipLaunchKernelGGL((dp_pipeline_kernel<FL, MT, RP, DP_V6W>), dim3(blocks), dim3(TPB), 0, s, img_base, im, \
+    hipLaunchKernelGGL((dp_pipeline_kernel<FL, MT, RP, DP_V6W + (DP_SNAT ? 0 : 2)>), dim3(blocks), dim3(TPB), 0, s, img_base, im, \
                        buf, buf_bytes, in, out, meta, n, part, fc);                                   \
   }
 extern "C" {
@@ -4415,6 +4432,8 @@ void dpk_run_pipeline_100(DP_RUN_ARGS);
 void dpk_run_pipeline_110(DP_RUN_ARGS);
 void dpk_run_pipeline_101(DP_RUN_ARGS);
 void dpk_run_pipeline_111(DP_RUN_ARGS);
+void dpk_run_pipeline_100s(DP_RUN_ARGS);
+void dpk_run_pipeline_110s(DP_RUN_ARGS);
 }
 #if DP_IN_PART(1)
 DP_RUNNER(dpk_run_pipeline_000, false, false, false)
@@ -4439,6 +4458,12 @@ DP_RUNNER(dpk_run_pipeline_101, true, false, true)
 #endif
 #if DP_IN_PART(6)
 DP_RUNNER(dpk_run_pipeline_111, true, true, true)
+#endif
+#if DP_PART == 9 || DP_PART < 0  // (a one-unit build: the full variant under the lean name)
+DP_RUNNER(dpk_run_pipeline_100s, true, false, false)
+#endif
+#if DP_PART == 10 || DP_PART < 0
+DP_RUNNER(dpk_run_pipeline_110s, true, true, false)
 #endif
 #if DP_IN_PART(0)
 #if defined(DP_TIMING)
@@ -4560,21 +4585,30 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
+  fc.replay = 0;
+  if (fc.lean) {
+    // no stateful NAT (Image.snat clear, no flow of the table ever had NAT
+    // state) and no v6 windows: the one pass without that code, and no NAT
+    // pass (no packet can reach PortForwarder or Masquerade)
+    if (meta) dpk_run_pipeline_110s(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+    else dpk_run_pipeline_100s(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+  } else {
   // first pass; PortForwarder's records in packet order; the replay of the
   // packets that reached it (dp_nat_resolve's decisions)
-  fc.replay = 0;
   if (meta) dpk_run_pipeline_110(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   else dpk_run_pipeline_100(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   // the NAT pass: records filed by connection, then resolved
-  // (grids of a lane per possible record / connection: each lane's work is a
-  // chain of dependent table accesses, so lanes, not bandwidth, set the pace)
-  const uint32_t pb = (n + 1023) / 1024 < 2048 ? (n + 1023) / 1024 : 2048;
+  // (grids of about one chip's worth of resident lanes: a burst with no
+  // records leaves at once -- 8192 empty workgroups cost 76 us; more lanes
+  // than that did not make the 500k-record burst faster)
+  const uint32_t pb = (n + 1023) / 1024 < 256 ? (n + 1023) / 1024 : 256;
   hipLaunchKernelGGL(dp_nat_prep, dim3(pb), dim3(1024), 0, stream, img_base, im, fc);
-  const uint32_t rb = (n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192;
+  const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
   hipLaunchKernelGGL(dp_nat_resolve, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   fc.replay = 1;
   if (meta) dpk_run_pipeline_111(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   else dpk_run_pipeline_101(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+  }
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));

@@ -14,6 +14,7 @@
 // the publishing (mgmt) thread -- hipFree synchronises the device, so it never
 // runs on a worker's burst path.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -140,6 +141,8 @@ struct DeviceTables {
 };
 std::atomic<uint64_t> g_serial{1};
 std::atomic<uint32_t> g_nat_seq{0};  // dpf_debug_nat_sequential
+std::atomic<uint32_t> g_flows_full{0};  // dpf_debug_flows_full
+std::atomic<uint32_t> g_last_lean{0};   // dpf_debug_last_lean
 
 std::mutex g_dev_mu;
 std::map<int, std::unique_ptr<DeviceTables>> g_dev;
@@ -272,6 +275,22 @@ struct HostTrace {
     if (on) fprintf(stderr, "[dpgpu host] n=%u threads=%u chunks=%u: %s\n", n, threads, chunks, s.c_str());
   }
 };
+
+// The staged path's byte moves.  A span goes into pinned staging that only
+// the DMA engine reads: streaming stores (no read for ownership of the
+// staging lines, no cache pollution), fenced before the copies are enqueued.
+// A frame comes back from staging the DMA engine wrote: 16-byte moves.
+void put_span(uint8_t *dst, const uint8_t *src, uint64_t units) {  // dst 16-byte aligned
+  for (uint64_t k = 0; k < units; k++)
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 16 * k),
+                     _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 16 * k)));
+}
+void put_frame(uint8_t *dst, const uint8_t *src, uint32_t len) {
+  uint32_t k = 0;
+  for (; k + 16 <= len; k += 16)
+    _mm_storeu_si128(reinterpret_cast<__m128i *>(dst + k), _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + k)));
+  if (k < len) memcpy(dst + k, src + k, len - k);
+}
 
 // Host threads for a burst's gather / write-back: one per 32K packets, at
 // most the machine's threads (capped at 16).
@@ -656,6 +675,12 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     }
     fc.burst = c->burst_tag;
     fc.force_seq = g_nat_seq.load(std::memory_order_relaxed);
+    // the flows variant without stateful NAT: an image without it, on a table
+    // no such image's burst ever ran on (only those bursts make NAT state),
+    // and no v6 windows (the lean units leave those lookups out)
+    if (img->im.snat) ft->snat_seen = true;
+    fc.lean = !ft->snat_seen && !img->im.v6w_c && !img->im.v6w_fib && !g_flows_full.load(std::memory_order_relaxed);
+    g_last_lean.store(fc.lean, std::memory_order_relaxed);
     if (words + sum_words > c->pf_bits_n) {
       c->pf_bits.release();
       c->pf_bits_n = 0;
@@ -772,6 +797,11 @@ int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
 // Test hook (not part of dpgpu.h): 1 runs every burst's NAT pass on one lane
 // in packet order (the parallel pass's reference in the parity tests and A/Bs).
 void dpf_debug_nat_sequential(int on) { g_nat_seq.store(on ? 1u : 0u, std::memory_order_relaxed); }
+// Test hook (not part of dpgpu.h): 1 runs every flows burst through the full
+// flows variant (stateful NAT compiled in) even where the lean one serves.
+void dpf_debug_flows_full(int on) { g_flows_full.store(on ? 1u : 0u, std::memory_order_relaxed); }
+// Test hook: 1 if the last flows burst launched ran the lean variant.
+int dpf_debug_last_lean() { return (int)g_last_lean.load(std::memory_order_relaxed); }
 
 // Test hook (not part of dpgpu.h): the context's last flows burst's NAT pass
 // -- its counters (pf_cnt[0..7]) and up to `max` records (dpf::PfReq).
@@ -945,14 +975,20 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     }
   });
   // the frames of packets [a, b): host threads pack their spans
+  // (DPGPU_HOST_PLAIN: plain memcpy both ways, the A/B of scripts/probe/host_ab.py)
+  const bool plain = getenv("DPGPU_HOST_PLAIN") != nullptr;
   auto gather = [&](uint32_t a, uint32_t b) {
     par_for(c, T, [&](uint32_t t) {
       for (uint32_t i = a + (uint32_t)((uint64_t)(b - a) * t / T), e = a + (uint32_t)((uint64_t)(b - a) * (t + 1) / T);
            i < e; i++) {
+        if (i + 8 < e) __builtin_prefetch(buf + (in[i + 8].off & ~15u));
         const uint64_t lo = in[i].off & ~15u, u = ((in[i].off + in[i].len + 15u) >> 4) - (in[i].off >> 4);
+        uint8_t *dst = c->h_cin + 16ull * c->h_pos[i];
         // the rounded-up end may lie past the caller's buffer: never read there
-        memcpy(c->h_cin + 16ull * c->h_pos[i], buf + lo, std::min<uint64_t>(16 * u, buf_bytes - lo));
+        if (!plain && lo + 16 * u <= buf_bytes) put_span(dst, buf + lo, u);
+        else memcpy(dst, buf + lo, buf_bytes - lo);
       }
+      _mm_sfence();  // the streamed spans are visible before the copies are enqueued
     });
   };
   tr.mark("positions");
@@ -1049,11 +1085,16 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
       uint32_t first, cnt;
       chunk_of(k, first, cnt);
       for (uint32_t i = first; i < first + cnt; i++) {
+        if (i + 8 < first + cnt) __builtin_prefetch(buf + in[i + 8].off, 1);
         dp_pkt_out_t o = c->h_out[i];
         if (o.done == DP_DONE_DELIVERED) {
           const uint64_t lo = (uint64_t)(in[i].off & ~15u) - grow, hi = (in[i].off + in[i].len + 15u) & ~15u;
           if (o.off >= lo && (uint64_t)o.off + o.len <= hi && (uint64_t)o.off + o.len <= buf_bytes)
-            memcpy(buf + o.off, c->h_cout + 16ull * c->h_pos[i] + (uint64_t)grow * i + (o.off - lo), o.len);
+          {
+            const uint8_t *src = c->h_cout + 16ull * c->h_pos[i] + (uint64_t)grow * i + (o.off - lo);
+            if (plain) memcpy(buf + o.off, src, o.len);
+            else put_frame(buf + o.off, src, o.len);
+          }
           else
             o = dp_pkt_out_t{in[i].off, in[i].len, DP_DONE_INTERNAL_FAILURE};
         }

@@ -1085,6 +1085,13 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   std::vector<std::pair<uint64_t, const dp_rule_t *>> ffr_aux[2];
   for (int ti = 0; ti < 6; ti++)
     if ((rc = load_rules(tabs[ti].r, tabs[ti].n, tabs[ti].fam, tabs[ti].prio, tabs[ti].kind, keep[ti]))) return rc;
+  // a flow-filter rule requiring port forwarding or masquerade (NatRequirement:
+  // remote action2, local action)
+  for (int ti = 2; ti < 6; ti++)
+    for (uint32_t i = 0; i < tabs[ti].n; i++) {
+      const uint32_t m = tabs[ti].kind == 1 ? tabs[ti].r[i].action2 : tabs[ti].r[i].action;
+      if (m == DP_NAT_PORT_FORWARDING || m == DP_NAT_MASQUERADE) im.snat = 1;
+    }
   // the v6 window: the longest prefix (17..48 bits) holding every v6 rule
   // prefix of every classifier -- one site's rules share their top bits, and
   // the v6 address indexes then order the bits after them
@@ -1449,6 +1456,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   im.pf_ids = build_hash(ib, pidkv);
   im.pf_rules = pfrecs.empty() ? ib.alloc(sizeof(PfRuleRec)) : ib.put(pfrecs);
   im.n_pf = (uint32_t)pfrecs.size();
+  if (im.n_pf || d->n_masq) im.snat = 1;
 
   section("portfw");
   // --- masquerade exposes (nat/src/masquerade/): validated and kept with the

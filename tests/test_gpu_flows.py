@@ -82,12 +82,15 @@ def _ref_map(a, b):
     return {x: y for x, y in zip(a, b) if x != A.FLOW_NONE}
 
 
+@pytest.mark.parametrize("full", [False, True], ids=["auto", "full"])
 @pytest.mark.parametrize("cfg,seed", [(2, 1), (2, 2), (5, 3)])
-def test_gpu_flows_random_bursts(nf, cfg, seed):
+def test_gpu_flows_random_bursts(nf, cfg, seed, full):
     """Seeded scenarios (tests/flowgen.py) over a C2-shaped workload, and a
     C5-shaped one (v4 / v6 mix: v6 flow keys, v6 ACL reply path): two bursts
     in a row, then the flow timers; outputs, serialized bytes, flow refs and
-    every flow's state equal the oracle's."""
+    every flow's state equal the oracle's.  auto: the C2 image configures no
+    stateful NAT and has no v6 windows, so its bursts run the lean flows
+    variant (parts 9 / 10); full: the variant with stateful NAT compiled in."""
     w = Workload(cfg, 6000, seed=seed, n_routes_v4=3000, n_routes_v6=2000 if cfg == 5 else 0,
                  n_acl=400, n_nat=24, tcp_percent=30)
     ora = Oracle(w.tables)
@@ -103,12 +106,16 @@ def test_gpu_flows_random_bursts(nf, cfg, seed):
     g2o = _ref_map(grefs, orefs)
     nf.publish(w.tables)
     nf.attach_flows(gft)
+    lib = A.gpu_lib()
+    lib.dpf_debug_flows_full(1 if full else 0)
     try:
         for rnd in range(2):
             buf, inp = pack_burst([(f, 1, A.IN_SEEDED_OVERLAY, v) for f, v in burst])
             obuf, gbuf = buf.copy(), buf.copy()
             oout, oref, ost = ora.process_flows(obuf, inp, oft, stats=True)
             gout, gref, gst = run_device(nf, gbuf, inp, stats=True)
+            if cfg == 2:
+                assert lib.dpf_debug_last_lean() == (0 if full else 1), "flows variant
             compare(oout, obuf, gout, gbuf, inp, f"flows C{cfg} seed {seed} burst {rnd}")
             mapped = np.array([g2o.get(int(r), A.FLOW_NONE) if int(r) != A.FLOW_NONE else A.FLOW_NONE
                                for r in gref], dtype=np.uint64)
@@ -125,6 +132,7 @@ def test_gpu_flows_random_bursts(nf, cfg, seed):
         assert gft.sweep(1 << 62) == oft.sweep(1 << 62)
         assert gft.count() == oft.count()
     finally:
+        lib.dpf_debug_flows_full(0)
         nf.attach_flows(None)
 
 
