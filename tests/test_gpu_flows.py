@@ -115,7 +115,7 @@ def test_gpu_flows_random_bursts(nf, cfg, seed, full):
             oout, oref, ost = ora.process_flows(obuf, inp, oft, stats=True)
             gout, gref, gst = run_device(nf, gbuf, inp, stats=True)
             if cfg == 2:
-                assert lib.dpf_debug_last_lean() == (0 if full else 1), "flows variant
+                assert lib.dpf_debug_last_lean() == (0 if full else 1), "flows variant"
             compare(oout, obuf, gout, gbuf, inp, f"flows C{cfg} seed {seed} burst {rnd}")
             mapped = np.array([g2o.get(int(r), A.FLOW_NONE) if int(r) != A.FLOW_NONE else A.FLOW_NONE
                                for r in gref], dtype=np.uint64)
