@@ -986,7 +986,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
         uint8_t *dst = c->h_cin + 16ull * c->h_pos[i];
         // the rounded-up end may lie past the caller's buffer: never read there
         if (!plain && lo + 16 * u <= buf_bytes) put_span(dst, buf + lo, u);
-        else memcpy(dst, buf + lo, buf_bytes - lo);
+        else memcpy(dst, buf + lo, std::min<uint64_t>(16 * u, buf_bytes - lo));
       }
       _mm_sfence();  // the streamed spans are visible before the copies are enqueued
     });
