@@ -1076,16 +1076,34 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
   // added encapsulation between this burst's staging and its launch -- is an
   // InternalFailure of that packet)
   tr.mark("gather+enqueue");
+  // Work items of at most kWbItem packets, taken in chunk order by whichever
+  // thread is free (a whole chunk per thread left the last chunks to a few
+  // threads while the rest idled)
   std::atomic<int> werr{0};
-  const uint32_t W = std::min<uint32_t>(T, nch);
-  par_for(c, W, [&](uint32_t t) {
+  constexpr uint32_t kWbItem = 8192;
+  std::vector<uint32_t> item0(nch + 1, 0);  // first work item of each chunk
+  for (uint32_t k = 0; k < nch; k++) {
+    uint32_t first, cnt;
+    chunk_of(k, first, cnt);
+    item0[k + 1] = item0[k] + (cnt + kWbItem - 1) / kWbItem;
+  }
+  std::atomic<uint32_t> next_item{0};
+  std::vector<std::atomic<uint8_t>> landed(nch);
+  for (auto &x : landed) x.store(0, std::memory_order_relaxed);
+  par_for(c, T, [&](uint32_t) {
     (void)hipSetDevice(c->device);
-    for (uint32_t k = t; k < nch; k += W) {
-      if (hipEventSynchronize(c->chunk_ev[k]) != hipSuccess) { werr = 1; continue; }
+    uint32_t k = 0;
+    for (uint32_t it; (it = next_item.fetch_add(1, std::memory_order_relaxed)) < item0[nch];) {
+      while (item0[k + 1] <= it) k++;
+      if (!landed[k].load(std::memory_order_acquire)) {
+        if (hipEventSynchronize(c->chunk_ev[k]) != hipSuccess) { werr = 1; continue; }
+        landed[k].store(1, std::memory_order_release);
+      }
       uint32_t first, cnt;
       chunk_of(k, first, cnt);
-      for (uint32_t i = first; i < first + cnt; i++) {
-        if (i + 8 < first + cnt) __builtin_prefetch(buf + in[i + 8].off, 1);
+      const uint32_t a = first + (it - item0[k]) * kWbItem, b = std::min(first + cnt, a + kWbItem);
+      for (uint32_t i = a; i < b; i++) {
+        if (i + 8 < b) __builtin_prefetch(buf + in[i + 8].off, 1);
         dp_pkt_out_t o = c->h_out[i];
         if (o.done == DP_DONE_DELIVERED) {
           const uint64_t lo = (uint64_t)(in[i].off & ~15u) - grow, hi = (in[i].off + in[i].len + 15u) & ~15u;
