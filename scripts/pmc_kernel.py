@@ -1,12 +1,12 @@
 # Summarise rocprofv3 --pmc CSVs: per-dispatch mean of each counter for one
-# kernel (default dp_pipeline_kernel<false, false>, the non-flow variant the metric times), over every pass directory given.
+# kernel (default dp_pipeline_kernel<false, false, false, *>, the non-flow variant the metric times), over every pass directory given.
 import csv
 import glob
 import sys
 from collections import defaultdict
 
 
-def summarise(dirs, kernel="dp_pipeline_kernel<false, false>"):
+def summarise(dirs, kernel="dp_pipeline_kernel<false, false, false"):
     vals = defaultdict(lambda: defaultdict(float))
     for d in dirs:
         files = glob.glob(f"{d}/**/run_counter_collection.csv", recursive=True)
