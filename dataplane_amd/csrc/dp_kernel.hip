@@ -2959,6 +2959,76 @@ __device__ __forceinline__ dp_pkt_meta_t meta_of(const Img &g, const State &S) {
   return m;
 }
 
+#ifndef DP_EMU
+// The flow-table effects of a wave's packets (FL only), wave-aggregated:
+// flow refs, invalidation marks and events, flow-dependent ACL verdicts.
+template <bool MT>
+__device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, uint32_t i, const FlowPk &fp) {
+  const int lane = threadIdx.x & 63;
+  const bool has = live && fp.slot != dpf::kNoSlot;
+  const bool e0 = has && fp.ev0 != dpf::kNoSlot, e1 = has && fp.ev1 != dpf::kNoSlot;
+  const bool e2 = live && fp.ev2 != dpf::kNoSlot;  // an ICMP error's (mark 0, like the flow filter's)
+  if (e0) atomicMin(&fc.slots[fp.ev0].mark, 0u);
+  if (e1) atomicMin(&fc.slots[fp.ev1].mark, fp.ev_mark);
+  if (e2) atomicMin(&fc.slots[fp.ev2].mark, 0u);
+  const uint64_t m0 = __ballot(e0), m1 = __ballot(e1), m2 = __ballot(e2);
+  if (m2) {
+    const int leader = __ffsll((long long)m2) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&fc.events[0], (uint32_t)__popcll(m2));
+    base = (uint32_t)__shfl((int)base, leader);
+    if (e2) {
+      const uint32_t k = base + __popcll(m2 & lanes_below(lane));
+      fc.events[1 + 2 * k] = fp.ev2;
+      fc.events[2 + 2 * k] = fp.ev2_tag;
+    }
+  }
+  if (m0 | m1) {
+    const int leader = __ffsll((long long)(m0 | m1)) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&fc.events[0], (uint32_t)(__popcll(m0) + __popcll(m1)));
+    base = (uint32_t)__shfl((int)base, leader);
+    // (slot, state word) pairs: the fill of the packet's flow (ev0 / ev1 are fp.slot)
+    if (e0) {
+      const uint32_t k = base + __popcll(m0 & lanes_below(lane));
+      fc.events[1 + 2 * k] = fp.ev0;
+      fc.events[2 + 2 * k] = fp.state;
+    }
+    if (e1) {
+      const uint32_t k = base + __popcll(m0) + __popcll(m1 & lanes_below(lane));
+      fc.events[1 + 2 * k] = fp.ev1;
+      fc.events[2 + 2 * k] = fp.state;
+    }
+  }
+  // the packets recorded for the NAT pass: a wave's 64 packets are the two
+  // bitmap words it alone owns (first pass: packet i on lane i % 64), stored
+  // whole; the region's summary bit once per wave, read first (a chip's
+  // worth of waves on a few summary words would queue at one L2 channel)
+  const uint64_t mr = SNAT ? __ballot(live && fp.deferred) : 0ull;
+  if (mr && lane == __ffsll((long long)mr) - 1) {
+    const uint32_t w0 = (i - lane) >> 5;
+    if ((uint32_t)mr) fc.pf_bits[w0] = (uint32_t)mr;
+    if (mr >> 32) fc.pf_bits[w0 + 1] = (uint32_t)(mr >> 32);
+    uint32_t *sw = &fc.pf_sum[i >> 15];
+    const uint32_t sb = 1u << ((i >> 10) & 31);
+    if (!(__hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & sb)) atomicOr(sw, sb);
+  }
+  const bool sv = has && fp.sens && !fp.deferred;  // a deferred packet's verdict: dp_nat_resolve
+  const uint64_t ms = __ballot(sv);
+  if (ms) {
+    const int leader = __ffsll((long long)ms) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&fc.sens[0], (uint32_t)__popcll(ms));
+    base = (uint32_t)__shfl((int)base, leader);
+    if (sv) {
+      dpf::SensRec *R = reinterpret_cast<dpf::SensRec *>(fc.sens + 8) + base + __popcll(ms & lanes_below(lane));
+      *R = dpf::SensRec{i, fp.slot, fp.s_flags, fp.s_oif, fp.s_fib, fp.def_acl, fp.related, fp.related_tag,
+                        MT ? fp.s_dvni : 0u, MT ? fp.s_vrf : 0u, MT ? fp.s_nh : NH_NONE, fp.state};
+    }
+  }
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // Per-packet body
 // ---------------------------------------------------------------------------
@@ -3075,6 +3145,13 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
 #endif
     stage_masquerade<FL>(F, H, S, fp, fc, idx, rp);
   }
+#if !defined(DP_EMU) && defined(DP_EARLY_EFFECTS)
+  // (A/B, measured slower: DESIGN §8) the packet's flow-table effects are all
+  // decided here, so emitting them now, wave-aggregated over the lanes still
+  // running, leaves the flow state dead through IP-Forward-2, Egress and
+  // serialize
+  if constexpr (FL) if (!rp) flow_effects<MT>(*fc, true, idx, fp);
+#endif
   if constexpr (FL && SNAT) {
     if (fp.deferred) {  // finished by the replay pass
       o.done = DONE_NONE;
@@ -3192,74 +3269,6 @@ __device__ __forceinline__ void wave_store_windows(uint8_t *buf, const uint8_t *
   }
 }
 
-// The flow-table effects of a wave's packets (FL only), wave-aggregated:
-// flow refs, invalidation marks and events, flow-dependent ACL verdicts.
-template <bool MT>
-__device__ __forceinline__ void flow_effects(const dpf::FlowCtx &fc, bool live, uint32_t i, const FlowPk &fp) {
-  const int lane = threadIdx.x & 63;
-  const bool has = live && fp.slot != dpf::kNoSlot;
-  const bool e0 = has && fp.ev0 != dpf::kNoSlot, e1 = has && fp.ev1 != dpf::kNoSlot;
-  const bool e2 = live && fp.ev2 != dpf::kNoSlot;  // an ICMP error's (mark 0, like the flow filter's)
-  if (e0) atomicMin(&fc.slots[fp.ev0].mark, 0u);
-  if (e1) atomicMin(&fc.slots[fp.ev1].mark, fp.ev_mark);
-  if (e2) atomicMin(&fc.slots[fp.ev2].mark, 0u);
-  const uint64_t m0 = __ballot(e0), m1 = __ballot(e1), m2 = __ballot(e2);
-  if (m2) {
-    const int leader = __ffsll((long long)m2) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&fc.events[0], (uint32_t)__popcll(m2));
-    base = (uint32_t)__shfl((int)base, leader);
-    if (e2) {
-      const uint32_t k = base + __popcll(m2 & lanes_below(lane));
-      fc.events[1 + 2 * k] = fp.ev2;
-      fc.events[2 + 2 * k] = fp.ev2_tag;
-    }
-  }
-  if (m0 | m1) {
-    const int leader = __ffsll((long long)(m0 | m1)) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&fc.events[0], (uint32_t)(__popcll(m0) + __popcll(m1)));
-    base = (uint32_t)__shfl((int)base, leader);
-    // (slot, state word) pairs: the fill of the packet's flow (ev0 / ev1 are fp.slot)
-    if (e0) {
-      const uint32_t k = base + __popcll(m0 & lanes_below(lane));
-      fc.events[1 + 2 * k] = fp.ev0;
-      fc.events[2 + 2 * k] = fp.state;
-    }
-    if (e1) {
-      const uint32_t k = base + __popcll(m0) + __popcll(m1 & lanes_below(lane));
-      fc.events[1 + 2 * k] = fp.ev1;
-      fc.events[2 + 2 * k] = fp.state;
-    }
-  }
-  // the packets recorded for the NAT pass: a wave's 64 packets are the two
-  // bitmap words it alone owns (first pass: packet i on lane i % 64), stored
-  // whole; the region's summary bit once per wave, read first (a chip's
-  // worth of waves on a few summary words would queue at one L2 channel)
-  const uint64_t mr = SNAT ? __ballot(live && fp.deferred) : 0ull;
-  if (mr && lane == __ffsll((long long)mr) - 1) {
-    const uint32_t w0 = (i - lane) >> 5;
-    if ((uint32_t)mr) fc.pf_bits[w0] = (uint32_t)mr;
-    if (mr >> 32) fc.pf_bits[w0 + 1] = (uint32_t)(mr >> 32);
-    uint32_t *sw = &fc.pf_sum[i >> 15];
-    const uint32_t sb = 1u << ((i >> 10) & 31);
-    if (!(__hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & sb)) atomicOr(sw, sb);
-  }
-  const bool sv = has && fp.sens && !fp.deferred;  // a deferred packet's verdict: dp_nat_resolve
-  const uint64_t ms = __ballot(sv);
-  if (ms) {
-    const int leader = __ffsll((long long)ms) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&fc.sens[0], (uint32_t)__popcll(ms));
-    base = (uint32_t)__shfl((int)base, leader);
-    if (sv) {
-      dpf::SensRec *R = reinterpret_cast<dpf::SensRec *>(fc.sens + 8) + base + __popcll(ms & lanes_below(lane));
-      *R = dpf::SensRec{i, fp.slot, fp.s_flags, fp.s_oif, fp.s_fib, fp.def_acl, fp.related, fp.related_tag,
-                        MT ? fp.s_dvni : 0u, MT ? fp.s_vrf : 0u, MT ? fp.s_nh : NH_NONE, fp.state};
-    }
-  }
-}
-
 // FL: the flows variant (a flow table is attached to the context); MT: meta
 // records requested (meta != nullptr); RP: the replay pass of the packets
 // that reached PortForwarder (FL only).
@@ -3315,7 +3324,9 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
     static_assert(sizeof(dp_pkt_out_t) == 16, "one 16-byte store");
     st16(out + i, *reinterpret_cast<const uint4 *>(&o));
   }
+#ifndef DP_EARLY_EFFECTS  // the flow-table effects after the whole body, every lane of the wave
   if constexpr (FL) if (!rep) flow_effects<MT>(fc, live, i, fp);
+#endif
   __syncthreads();
   // write-back: whole chunks by the wave, a partial tail by its owner
   wave_store_windows(buf, slab_wave, base, fl0 >> 4, fl1 >> 4);
