@@ -17,6 +17,6 @@ echo PROF_OK
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc/p$i -o run -- python bench.py --config $CFG --steps 3 --warmup 1 --no-cpu --no-host > gpurun_out/pmc/p$i.json 2> gpurun_out/pmc/p$i.err || { echo "PMC pass $i failed"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc/p$i -o run -- python bench.py --config $CFG --steps 3 --warmup 1 --no-cpu --no-host --no-nat --no-flows > gpurun_out/pmc/p$i.json 2> gpurun_out/pmc/p$i.err || { echo "PMC pass $i failed"; exit 1; }
 done
 echo END
