@@ -110,7 +110,7 @@ __device__ unsigned long long g_stage_cycles[16];
 #define DP_WIN 96
 #endif
 #ifndef DP_HS
-#define DP_HS 60
+#define DP_HS 76
 #endif
 #ifndef DP_CAND4
 #define DP_CAND4 2  // v4 classifier candidates fetched per round trip (2 or 4; 4 measured slower)
@@ -120,7 +120,7 @@ __device__ unsigned long long g_stage_cycles[16];
 #endif
 constexpr int WIN = DP_WIN;       // header window bytes per packet (rest read from HBM)
 constexpr int SLAB = WIN + 4;     // odd dword stride: conflict-free byte reads
-constexpr int HS = DP_HS;         // hash input scratch (packet_hash_* input <= 59 B)
+constexpr int HS = DP_HS;         // hash input scratch (packet_hash_vxlan's stream <= 75 B)
 constexpr uint8_t DONE_NONE = 255;
 // out-of-line cold paths (the emulator inlines freely, except its
 // DP_EMU_OUTLINE build, which keeps every function out of line so the CPU
@@ -892,24 +892,34 @@ __device__ __forceinline__ uint64_t rapid(const lds_u8 *p, int len) {
   return mixh(a ^ s0 ^ (uint64_t)len, b ^ s1);
 }
 
+// The stream is what the reference's Hasher calls feed it, in order
+// (net/src/packet/hash.rs:17-68; DESIGN.md §4 lists each field's Hash):
+// every write_uN(v) as v's native (little-endian) bytes -- the Hasher
+// trait's default encoding -- a slice's length prefix as write_usize.  An
+// address's Hash is write_u32 / write_u128 of u32 / u128::from_ne_bytes(octets),
+// so its bytes are the octets in network order.
+__device__ __forceinline__ void hb_u16(HBuf &h, uint32_t v) { hb_put(h, (uint8_t)v); hb_put(h, (uint8_t)(v >> 8)); }
+__device__ __forceinline__ void hb_usize(HBuf &h, uint32_t v) {
+  hb_u16(h, v); hb_u16(h, 0); hb_u16(h, 0); hb_u16(h, 0);
+}
 __device__ __forceinline__ void hash_ip_fields(const Frame &F, const Hdr &H, const State &S, HBuf &h) {
   if (H.net == 4) {
-    for (int i = 0; i < 4; i++) hb_put(h, (uint8_t)(S.v4src >> (24 - 8 * i)));
-    for (int i = 0; i < 4; i++) hb_put(h, (uint8_t)(S.v4dst >> (24 - 8 * i)));
-    hb_put(h, F.b(H.net_off + 9));
+    for (int i = 0; i < 4; i++) hb_put(h, (uint8_t)(S.v4src >> (24 - 8 * i)));  // source(): write_u32
+    for (int i = 0; i < 4; i++) hb_put(h, (uint8_t)(S.v4dst >> (24 - 8 * i)));  // destination(): write_u32
+    hb_put(h, F.b(H.net_off + 9));                                              // protocol(): write_u8
   } else if (H.net == 6) {
-    for (int i = 0; i < 32; i++) hb_put(h, F.b(H.net_off + 8 + i));
-    hb_put(h, F.b(H.net_off + 6));
+    for (int i = 0; i < 32; i++) hb_put(h, F.b(H.net_off + 8 + i));            // write_u128 x 2
+    hb_put(h, F.b(H.net_off + 6));                                              // next_header(): write_u8
   } else {
     return;
   }
-  if (H.l4 == L4_TCP || H.l4 == L4_UDP) {
-    hb_put(h, S.sport >> 8); hb_put(h, S.sport & 0xff);
-    hb_put(h, S.dport >> 8); hb_put(h, S.dport & 0xff);
+  if (H.l4 == L4_TCP || H.l4 == L4_UDP) {  // TcpPort / UdpPort: write_u16 each
+    hb_u16(h, S.sport);
+    hb_u16(h, S.dport);
   } else if (H.l4 == L4_ICMP4 || H.l4 == L4_ICMP6) {
     uint8_t t = F.b(H.l4_off);
     bool echo = H.l4 == L4_ICMP4 ? (t == 0 || t == 8) : (t == 128 || t == 129);
-    if (echo) { hb_put(h, F.b(H.l4_off + 4)); hb_put(h, F.b(H.l4_off + 5)); }
+    if (echo) hb_u16(h, ((uint32_t)F.b(H.l4_off + 4) << 8) | F.b(H.l4_off + 5));  // identifier(): write_u16
   }
 }
 
@@ -1976,13 +1986,12 @@ __device__ __forceinline__ void vxlan_encap(const Img &g, const Frame &F, const 
   if (inner_start < -(int)DP_HEADROOM) { done(S, DP_DONE_VXLAN_ENCAP_FAILURE); return; }
   // packet_hash_vxlan over the (updated) inner headers
   HBuf hbuf{F.hs, 0};
+  hb_usize(hbuf, 6);  // source(): a [u8; 6] hashes as a slice -- length prefix, then the bytes
   for (int i = 0; i < 6; i++) hb_put(hbuf, mac_b(S.esrc, i));
+  hb_usize(hbuf, 6);  // destination()
   for (int i = 0; i < 6; i++) hb_put(hbuf, mac_b(S.edst, i));
-  hb_put(hbuf, F.b(H.hb + 12)); hb_put(hbuf, F.b(H.hb + 13));
-  for (int v = 0; v < H.nvlan; v++) {
-    uint16_t vid = F.be16(H.hb + 14 + 4 * v) & 0x0fff;
-    hb_put(hbuf, vid >> 8); hb_put(hbuf, vid & 0xff);
-  }
+  hb_u16(hbuf, ((uint32_t)F.b(H.hb + 12) << 8) | F.b(H.hb + 13));  // ether_type(): write_u16
+  for (int v = 0; v < H.nvlan; v++) hb_u16(hbuf, F.be16(H.hb + 14 + 4 * v) & 0x0fff);  // vid(): write_u16
   hash_ip_fields(F, H, S, hbuf);
   uint64_t x = rapid(hbuf.b, hbuf.n);
   ob.sport = (uint16_t)(x % 16384 + 49152);

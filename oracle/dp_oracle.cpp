@@ -1764,15 +1764,24 @@ void stage_ingress(const dpo_tables &T, Packet &p, uint32_t iif) {
 
 Ip ip_dst(const Headers &h) { return h.net == 4 ? ip4(h.v4.dst) : ip6(h.v6.dst); }
 
-void hash_ip_bytes(const Headers &h, std::vector<uint8_t> &o) {
+// The bytes the Hasher calls of net/src/packet/hash.rs:17-68 feed it, in
+// order, under the Hasher trait's default encodings: write_uN(v) = v's
+// native (little-endian) bytes, a slice's length prefix = write_usize.
+// Field types: Ipv4Addr / Ipv6Addr hash as write_u32 / write_u128
+// of from_ne_bytes(octets) (the octets in order), IpNumber write_u8, ports,
+// VIDs, ethertypes and ICMP identifiers write_u16, MACs ([u8; 6]) a length
+// prefix and six bytes.
+void hash_u16(std::vector<uint8_t> &o, uint16_t v) { o.push_back((uint8_t)v); o.push_back((uint8_t)(v >> 8)); }
+void hash_usize(std::vector<uint8_t> &o, uint64_t v) { for (int i = 0; i < 8; i++) o.push_back((uint8_t)(v >> (8 * i))); }
+void hash_ip_bytes(const Headers &h, std::vector<uint8_t> &o) {  // hash_ip (hash.rs:17-54)
   if (h.net == 0) return;
   if (h.net == 4) { o.insert(o.end(), h.v4.src, h.v4.src + 4); o.insert(o.end(), h.v4.dst, h.v4.dst + 4); o.push_back(h.v4.proto); }
   else { o.insert(o.end(), h.v6.src, h.v6.src + 16); o.insert(o.end(), h.v6.dst, h.v6.dst + 16); o.push_back(h.v6.nh); }
-  uint8_t b[4];
-  if (h.l4 == L4_TCP) { put16(b, h.tcp.sport); put16(b + 2, h.tcp.dport); o.insert(o.end(), b, b + 4); }
-  else if (h.l4 == L4_UDP) { put16(b, h.udp.sport); put16(b + 2, h.udp.dport); o.insert(o.end(), b, b + 4); }
-  else if (h.l4 == L4_ICMP4 && (h.icmp.raw[0] == 0 || h.icmp.raw[0] == 8)) o.insert(o.end(), h.icmp.raw + 4, h.icmp.raw + 6);
-  else if (h.l4 == L4_ICMP6 && (h.icmp.raw[0] == 128 || h.icmp.raw[0] == 129)) o.insert(o.end(), h.icmp.raw + 4, h.icmp.raw + 6);
+  if (h.l4 == L4_TCP) { hash_u16(o, h.tcp.sport); hash_u16(o, h.tcp.dport); }
+  else if (h.l4 == L4_UDP) { hash_u16(o, h.udp.sport); hash_u16(o, h.udp.dport); }
+  else if ((h.l4 == L4_ICMP4 && (h.icmp.raw[0] == 0 || h.icmp.raw[0] == 8)) ||
+           (h.l4 == L4_ICMP6 && (h.icmp.raw[0] == 128 || h.icmp.raw[0] == 129)))
+    hash_u16(o, (uint16_t)((h.icmp.raw[4] << 8) | h.icmp.raw[5]));
 }
 
 // packet_hash_ecmp (net/src/packet/hash.rs:74-78)
@@ -1784,12 +1793,14 @@ uint64_t hash_ecmp(const Headers &h) {
 // packet_hash_vxlan (net/src/packet/hash.rs:84-88)
 uint16_t hash_vxlan(const Headers &h) {
   std::vector<uint8_t> o;
-  if (h.has_eth) {
+  if (h.has_eth) {  // hash_l2_frame (hash.rs:57-68)
+    hash_usize(o, 6);
     o.insert(o.end(), h.eth.src, h.eth.src + 6);
+    hash_usize(o, 6);
     o.insert(o.end(), h.eth.dst, h.eth.dst + 6);
-    uint8_t b[2]; put16(b, h.eth.type); o.insert(o.end(), b, b + 2);
+    hash_u16(o, h.eth.type);
   }
-  for (auto &v : h.vlans) { uint8_t b[2]; put16(b, v.vid()); o.insert(o.end(), b, b + 2); }
+  for (auto &v : h.vlans) hash_u16(o, v.vid());
   hash_ip_bytes(h, o);
   uint64_t x = rapid(o.data(), o.size());
   return (uint16_t)(x % 16384 + 49152);
