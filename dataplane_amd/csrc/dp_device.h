@@ -397,8 +397,16 @@ struct Image {
   // forwarding or masquerade, a port-forwarding rule or a masquerade expose
   // (the flows variant without that code serves tables that never held it)
   uint32_t snat;
-  uint32_t pad_snat;
+  uint32_t n_nh;             // NhRec count
+  // The context tables every packet reads -- VNI slots, the pair map's slots,
+  // PairRecs, NhRecs -- copied into each workgroup's LDS when together they
+  // fit DPD_CTX_MAX (ctx_bytes > 0; 0: read from HBM): VNI slots at 0, then
+  // the others at these offsets (16-byte aligned)
+  uint32_t n_pair_recs;
+  uint32_t ctx_bytes;
+  uint32_t ctx_pslots, ctx_prec, ctx_nh;
 };
+constexpr uint32_t DPD_CTX_MAX = 7168;
 
 // 32-bit mixing hash for the open-addressing maps (host and device agree)
 __host__ __device__ inline uint32_t hmix(uint32_t a, uint32_t b, uint32_t c) {

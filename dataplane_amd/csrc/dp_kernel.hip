@@ -42,7 +42,7 @@ using namespace dpd;
 // the non-flow pipeline without them, parts 7 and 8 with them, and
 // dpk_launch_pipeline picks by the image; every other unit has them.
 #ifndef DP_V6W
-#if DP_PART == 1 || DP_PART == 2 || DP_PART == 9 || DP_PART == 10
+#if DP_PART == 1 || DP_PART == 2 || DP_PART == 9 || DP_PART == 10 || DP_PART == 11 || DP_PART == 12
 #define DP_V6W 0
 #else
 #define DP_V6W 1
@@ -61,8 +61,25 @@ using namespace dpd;
 #endif
 #endif
 constexpr bool SNAT = DP_SNAT;
+// DP_CTX: the context tables (VNI slots, pair map, PairRecs, NhRecs) read
+// from a per-workgroup LDS copy (Image.ctx_bytes > 0).  Parts 1 and 2 build
+// the non-flow pipeline so, at 256 work-items per workgroup (the copy is
+// amortised over more packets and three workgroups' LDS still fit a CU at 3
+// waves per SIMD); parts 11 and 12 without it, for images whose context
+// tables do not fit DPD_CTX_MAX.
+#ifndef DP_CTX
+#if DP_PART == 1 || DP_PART == 2
+#define DP_CTX 1
+#else
+#define DP_CTX 0
+#endif
+#endif
 #ifndef DP_TPB
+#if DP_CTX
+#define DP_TPB 256
+#else
 #define DP_TPB 128
+#endif
 #endif
 constexpr int TPB = DP_TPB;  // work-items (packets) per workgroup
 // LDS pointers carry their address space explicitly so every access is a
@@ -170,23 +187,61 @@ struct ImgBase {
 };
 struct Img : ImgBase {
   const Image &im;  // in HBM on the device (read where used), host memory in the emulator
+  const LDS_AS uint8_t *ctx = nullptr;  // DP_CTX: the workgroup's copy of the context tables
   __device__ __forceinline__ Img(const uint8_t *b, const Image &i) : ImgBase{b}, im(i) {}
+  __device__ __forceinline__ Img(const uint8_t *b, const Image &i, const LDS_AS uint8_t *c)
+      : ImgBase{b}, im(i), ctx(c) {}
 };
+// The context tables, from the workgroup's LDS copy (DP_CTX) or HBM
+#if DP_CTX
+#define CTX_AS LDS_AS
+#define CTX_TAB(T, lds_off, hbm_off) reinterpret_cast<const CTX_AS T *>(g.ctx + (lds_off))
+#else
+#define CTX_AS
+#define CTX_TAB(T, lds_off, hbm_off) g.at<T>(hbm_off)
+#endif
+// a record of a context table as a value (DP_CTX: word by word out of LDS;
+// the compiler drops the words nobody reads), else a reference into HBM
+#if DP_CTX
+template <class T> __device__ __forceinline__ T ctx_val(const CTX_AS T &x) {
+  static_assert(sizeof(T) % 4 == 0, "word copy");
+  T r;
+  const CTX_AS uint32_t *src = reinterpret_cast<const CTX_AS uint32_t *>(&x);
+  uint32_t *dst = reinterpret_cast<uint32_t *>(&r);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) dst[k] = src[k];
+  return r;
+}
+#define CTX_REC(T, lds_off, hbm_off, idx) ctx_val(CTX_TAB(T, lds_off, hbm_off)[idx])
+#else
+#define CTX_REC(T, lds_off, hbm_off, idx) g.at<T>(hbm_off)[idx]
+#endif
+#define VNI_REC(idx) CTX_REC(VniRec, 0, g.im.vni_slots, idx)
+#define PAIR_REC(idx) CTX_REC(PairRec, g.im.ctx_prec, g.im.pair_recs, idx)
 
+template <class SP>
+__device__ __forceinline__ bool hash_probe(SP s, uint32_t mask, uint32_t k0, uint32_t k1, uint32_t k2,
+                                           uint32_t &val) {
+  uint32_t key2 = k2 | 0x80000000u;
+  uint32_t i = hmix(k0, k1, k2) & mask;
+  for (uint32_t probe = 0; probe <= mask; probe++) {
+    TRIP();
+    const uint32_t e2 = s[i].k2;
+    if (!(e2 & 0x80000000u)) return false;
+    if (s[i].k0 == k0 && s[i].k1 == k1 && e2 == key2) { val = s[i].val; return true; }
+    i = (i + 1) & mask;
+  }
+  return false;
+}
 __device__ __forceinline__ bool hash_find(const Img &g, const HashMap &m, uint32_t k0,
                                           uint32_t k1, uint32_t k2, uint32_t &val) {
   if (m.count == 0) return false;
-  const HashSlot *s = g.at<HashSlot>(m.slots);
-  uint32_t key2 = k2 | 0x80000000u;
-  uint32_t i = hmix(k0, k1, k2) & m.mask;
-  for (uint32_t probe = 0; probe <= m.mask; probe++) {
-    TRIP();
-    HashSlot e = s[i];
-    if (!(e.k2 & 0x80000000u)) return false;
-    if (e.k0 == k0 && e.k1 == k1 && e.k2 == key2) { val = e.val; return true; }
-    i = (i + 1) & m.mask;
-  }
-  return false;
+  return hash_probe(g.at<HashSlot>(m.slots), m.mask, k0, k1, k2, val);
+}
+// the (src VNI, dst VNI) -> PairRec map (a context table)
+__device__ __forceinline__ bool pair_find(const Img &g, uint32_t k0, uint32_t k1, uint32_t &val) {
+  if (g.im.pairs.count == 0) return false;
+  return hash_probe(CTX_TAB(HashSlot, g.im.ctx_pslots, g.im.pairs.slots), g.im.pairs.mask, k0, k1, 0, val);
 }
 
 // ---------------------------------------------------------------------------
@@ -1846,7 +1901,7 @@ __device__ __forceinline__ void stage_ingress(const Img &g, const Frame &F, cons
 // VNI map probe: the slots are the VniRecs themselves (vni 0 = empty)
 __device__ __forceinline__ int32_t find_vni(const Img &g, uint32_t vni) {
   if (vni == 0) return -1;
-  const VniRec *slots = g.at<VniRec>(g.im.vni_slots);
+  const CTX_AS VniRec *slots = CTX_TAB(VniRec, 0, g.im.vni_slots);
   const uint32_t mask = g.im.vni_mask;
   uint32_t i = hmix(vni, 0, 0) & mask;
   for (uint32_t probe = 0; probe <= mask; probe++) {
@@ -1862,7 +1917,7 @@ __device__ __forceinline__ int32_t find_vni(const Img &g, uint32_t vni) {
 __device__ __forceinline__ bool enter_vni(const Img &g, State &S, uint32_t vni) {
   const int32_t vi = find_vni(g, vni);
   if (vi < 0) return false;
-  const VniRec R = g.at<VniRec>(g.im.vni_slots)[vi];
+  const auto &R = VNI_REC(vi);
   S.src_vni = vni;
   S.has_vrf = true;
   S.vrf = R.vrf_id;
@@ -1876,7 +1931,7 @@ __device__ __forceinline__ bool enter_vni(const Img &g, State &S, uint32_t vni) 
 __device__ __forceinline__ int32_t pair_of(const Img &g, State &S) {
   if (S.pair < 0) {
     uint32_t pi;
-    if (hash_find(g, g.im.pairs, S.src_vni, S.dst_vni, 0, pi)) S.pair = (int32_t)pi;
+    if (pair_find(g, S.src_vni, S.dst_vni, pi)) S.pair = (int32_t)pi;
   }
   return S.pair;
 }
@@ -2042,14 +2097,14 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
     if (H.net == 0 && !S.encap) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
     int32_t pi = pair_of(g, S);
     if (pi >= 0) {
-      const PairRec &PR = g.at<PairRec>(g.im.pair_recs)[pi];
+      const auto &PR = PAIR_REC(pi);
       fi = PR.dst_fib;
       d4 = PR.lpm4_direct;
       b4 = PR.lpm4_dbits;
       k4 = PR.lpm4_blocks;
     } else {
       const int32_t vi = find_vni(g, S.dst_vni);
-      fi = vi >= 0 ? (int32_t)g.at<VniRec>(g.im.vni_slots)[vi].fib : -1;
+      fi = vi >= 0 ? (int32_t)CTX_TAB(VniRec, 0, g.im.vni_slots)[vi].fib : -1;
     }
     if (fi < 0) { done(S, DP_DONE_INTERNAL_FAILURE); return; }
   } else if (S.has_vrf) {
@@ -2082,7 +2137,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   if (!sel) sel = lpm_sel(b4, 64 - b4, b4);
   const uint32_t nhi = lpm_walk(g, d4, sel, k4, dst);
   TRIP();
-  const NhRec nr = g.at<NhRec>(g.im.nh_recs)[nhi];
+  const auto &nr = CTX_REC(NhRec, g.im.ctx_nh, g.im.nh_recs, nhi);
   if (nr.kind != DPD_NH_CHAIN) {
     // a single Egress / Drop instruction, resolved at publish (NhRec)
     S.fib_entry = nr.entry;
@@ -2187,8 +2242,8 @@ __device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_
   P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
   // the index descriptors ride in the pair / VNI contexts (Mbi): the four
   // walks start right after the pair context arrives
-  const PairRec &PR = g.at<PairRec>(g.im.pair_recs)[pi];
-  const VniRec &VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
+  const auto &PR = PAIR_REC(pi);
+  const auto &VR = VNI_REC(S.vni_idx);
 #ifndef DP_TWO_ACL_INDEX
   constexpr int NW = 4;
   Mbi m[NW] = {PR.ffl4, PR.acl4, PR.nsrc, VR.ndst};
@@ -2265,7 +2320,7 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   uint8_t proto = net_proto(F, H);
   int t = H.net == 4 ? 0 : 1;
   Key128 src = key_of(F, H, S, true), dst = key_of(F, H, S, false);
-  const VniRec &VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
+  const auto &VR = VNI_REC(S.vni_idx);
   int32_t rg = VR.ffr[t];
   // v4 candidate-list group: walk its index straight from the VNI context
   uint32_t pre = (t == 0 && VR.ffr4.root) ? mbi_walk(g, VR.ffr4, mbi_key(S, VR.ffr4.field, false) *
@@ -2288,7 +2343,7 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   int32_t pi = (int32_t)rh.aux;
   TRIP_ST(3);
   TRIP();
-  int32_t lg = g.at<PairRec>(g.im.pair_recs)[pi].ffl[t];
+  int32_t lg = CTX_TAB(PairRec, g.im.ctx_prec, g.im.pair_recs)[pi].ffl[t];
   if (t == 0) hoist_walks(g, S, pi, P);
   uint32_t lpre = P.ffl;
   if (gate) {  // the (src, dst, PortFwdReply) group: no hoisted walk, the classifier walks it
@@ -2359,7 +2414,7 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
   uint8_t proto = net_proto(F, H);
   int t = H.net == 4 ? 0 : 1;
   const int32_t pi = pair_of(g, S);
-  const int32_t ag = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].acl[t] : -1;
+  const int32_t ag = pi >= 0 ? CTX_TAB(PairRec, g.im.ctx_prec, g.im.pair_recs)[pi].acl[t] : -1;
   const Hit ah = classify<W_ACTION | W_ORIG>(g, CLS_ARRAYS(acl, t), ag, t, proto, key_of(F, H, S, true),
                                              key_of(F, H, S, false), S.sport, S.dport, t == 0 ? P.acl : NO_PRE);
   uint32_t action;
@@ -2368,7 +2423,7 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
     S.acl_rule = ah.orig;
     S.acl = action == DP_ACL_DENY ? 2 : 1;
   } else {
-    uint32_t v = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].acl_def : 0;
+    uint32_t v = pi >= 0 ? CTX_TAB(PairRec, g.im.ctx_prec, g.im.pair_recs)[pi].acl_def : 0;
     const uint8_t def = v ? ((v - 1) == DP_ACL_DENY ? 4 : 3) : 5;
     action = v ? v - 1 : DP_ACL_ALLOW;
     S.acl = def;
@@ -2388,8 +2443,8 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
         const uint8_t rproto = kind == DP_FLOW_TCP ? 6 : kind == DP_FLOW_UDP ? 17 : fam == 4 ? 1 : 58;
         const int rt = fam == 4 ? 0 : 1;
         uint32_t rpi;
-        const int32_t rg = hash_find(g, g.im.pairs, S.dst_vni, S.src_vni, 0, rpi)
-                               ? g.at<PairRec>(g.im.pair_recs)[rpi].acl[rt] : -1;
+        const int32_t rg = pair_find(g, S.dst_vni, S.src_vni, rpi)
+                               ? CTX_TAB(PairRec, g.im.ctx_prec, g.im.pair_recs)[rpi].acl[rt] : -1;
         Key128 ks, kd;
         if (fam == 4) {
           ks = Key128{0, __builtin_bswap32(b.x)};
@@ -2617,11 +2672,11 @@ __device__ __forceinline__ void stage_static_nat(const Img &g, const Frame &F, c
   const bool ie = has_emb(H) && icmp_err_at(F, H.l4_off, H.l4 == L4_ICMP6);
   if ((S.flags & (DP_META_NATTED_SRC | DP_META_NATTED_DST)) && !ie) return;
   if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
-  const VniRec VR = g.at<VniRec>(g.im.vni_slots)[S.vni_idx];
+  const auto &VR = VNI_REC(S.vni_idx);
   if (!VR.pervni) { done(S, DP_DONE_UNROUTABLE); return; }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
   const int32_t pi = pair_of(g, S);
-  const int32_t st = pi >= 0 ? g.at<PairRec>(g.im.pair_recs)[pi].nat_src : -1;
+  const int32_t st = pi >= 0 ? CTX_TAB(PairRec, g.im.ctx_prec, g.im.pair_recs)[pi].nat_src : -1;
   bool has_p = H.l4 == L4_TCP || H.l4 == L4_UDP;
   bool modified = false;
   NatQ q[2];
@@ -3289,6 +3344,23 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
                    dp_pkt_out_t *__restrict__ out, dp_pkt_meta_t *__restrict__ meta, uint32_t n,
                    unsigned long long *__restrict__ part, dpf::FlowCtx fc) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_all[TPB * (SLAB + HS)];
+#if DP_CTX
+  // the context tables' copy, loaded beside the header windows (the one
+  // barrier below covers both)
+  __shared__ __attribute__((aligned(16))) uint8_t ctx_lds[DPD_CTX_MAX];
+  {
+    const uint32_t seg_lds[4] = {0u, im->ctx_pslots, im->ctx_prec, im->ctx_nh};
+    const uint64_t seg_hbm[4] = {im->vni_slots, im->pairs.slots, im->pair_recs, im->nh_recs};
+    const uint32_t seg_len[4] = {(im->vni_mask + 1) * (uint32_t)sizeof(VniRec),
+                                 (im->pairs.mask + 1) * (uint32_t)sizeof(HashSlot),
+                                 im->n_pair_recs * (uint32_t)sizeof(PairRec), im->n_nh * (uint32_t)sizeof(NhRec)};
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      for (uint32_t u = threadIdx.x; u < seg_len[q] / 16; u += TPB)
+        *reinterpret_cast<uint4 *>(ctx_lds + seg_lds[q] + 16 * u) =
+            *reinterpret_cast<const uint4 *>(img_base + seg_hbm[q] + 16 * u);
+  }
+#endif
   uint8_t *slab_all = lds_all;
   uint8_t *hash_all = lds_all + TPB * SLAB;
   const int tid = threadIdx.x;
@@ -3324,7 +3396,11 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   FlowPk fp;
   fp.slot = dpf::kNoSlot;
   if (live) {
+#if DP_CTX
+    Img g{img_base, *im, (const lds_u8 *)ctx_lds};
+#else
     Img g{img_base, *im};
+#endif
     dp_pkt_out_t o;
     lds_u8 *hs = (lds_u8 *)(hash_all + tid * HS);
     dp_pkt_meta_t *pm = MT ? meta + i : nullptr;
@@ -4437,10 +4513,12 @@ extern "C" void dpemu_trips_out(uint16_t *p) { dp_trip_out = p; }
       const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n, unsigned long long *part,   \
       const dpf::FlowCtx &fc
 // (the kernel's last template argument names the unit's build: DP_V6W, + 2
-// without stateful NAT)
+// without stateful NAT, + 4 with the context tables in LDS; each unit sizes
+// its own grid by its TPB, the `blocks` argument is unused)
 #define DP_RUNNER(NAME, FL, MT, RP)                                                                   \
   extern "C" void NAME(DP_RUN_ARGS) {                                                                 \
-    hipLaunchKernelGGL((dp_pipeline_kernel<FL, MT, RP, DP_V6W + (DP_SNAT ? 0 : 2)>), dim3(blocks), dim3(TPB), 0, s, img_base, im, \
+    hipLaunchKernelGGL((dp_pipeline_kernel<FL, MT, RP, DP_V6W + (DP_SNAT ? 0 : 2) + (DP_CTX ? 4 : 0)>),      \
+                       dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, img_base, im,                     \
                        buf, buf_bytes, in, out, meta, n, part, fc);                                   \
   }
 extern "C" {
@@ -4454,6 +4532,8 @@ void dpk_run_pipeline_101(DP_RUN_ARGS);
 void dpk_run_pipeline_111(DP_RUN_ARGS);
 void dpk_run_pipeline_100s(DP_RUN_ARGS);
 void dpk_run_pipeline_110s(DP_RUN_ARGS);
+void dpk_run_pipeline_000n(DP_RUN_ARGS);
+void dpk_run_pipeline_010n(DP_RUN_ARGS);
 }
 #if DP_IN_PART(1)
 DP_RUNNER(dpk_run_pipeline_000, false, false, false)
@@ -4478,6 +4558,12 @@ DP_RUNNER(dpk_run_pipeline_101, true, false, true)
 #endif
 #if DP_IN_PART(6)
 DP_RUNNER(dpk_run_pipeline_111, true, true, true)
+#endif
+#if DP_PART == 11 || DP_PART < 0  // (a one-unit build: the one instantiation under every name)
+DP_RUNNER(dpk_run_pipeline_000n, false, false, false)
+#endif
+#if DP_PART == 12 || DP_PART < 0
+DP_RUNNER(dpk_run_pipeline_010n, false, true, false)
 #endif
 #if DP_PART == 9 || DP_PART < 0  // (a one-unit build: the full variant under the lean name)
 DP_RUNNER(dpk_run_pipeline_100s, true, false, false)
@@ -4573,17 +4659,18 @@ extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
-                                   int v6w, hipStream_t stream) {
+                                   int v6w, int ctx, hipStream_t stream) {
   if (n == 0) return 0;
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
   const dpf::FlowCtx nofc{};
-  // an image with v6 windows needs the units that look them up
-  if (meta) (v6w ? dpk_run_pipeline_010w : dpk_run_pipeline_010)(blocks, stream, img_base, im, buf, buf_bytes, in,
-                                                                  out, meta, n, part, nofc);
-  else (v6w ? dpk_run_pipeline_000w : dpk_run_pipeline_000)(blocks, stream, img_base, im, buf, buf_bytes, in, out,
-                                                             meta, n, part, nofc);
+  // an image with v6 windows needs the units that look them up; the others
+  // read the context tables from LDS when they fit (ctx != 0)
+  if (meta) (v6w ? dpk_run_pipeline_010w : ctx ? dpk_run_pipeline_010 : dpk_run_pipeline_010n)(
+      blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, nofc);
+  else (v6w ? dpk_run_pipeline_000w : ctx ? dpk_run_pipeline_000 : dpk_run_pipeline_000n)(
+      blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, nofc);
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,
                        reinterpret_cast<unsigned long long *>(stats));

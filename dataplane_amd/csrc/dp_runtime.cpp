@@ -39,7 +39,7 @@
 extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                    uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                    dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
-                                   int v6w, hipStream_t stream);
+                                   int v6w, int ctx, hipStream_t stream);
 extern "C" int dpk_acl_classify(const uint8_t *img_base, const void *image_dev, const dp_acl_key_t *keys,
                                 dp_acl_result_t *out, uint32_t n, hipStream_t stream);
 extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
@@ -143,6 +143,7 @@ std::atomic<uint64_t> g_serial{1};
 std::atomic<uint32_t> g_nat_seq{0};  // dpf_debug_nat_sequential
 std::atomic<uint32_t> g_flows_full{0};  // dpf_debug_flows_full
 std::atomic<uint32_t> g_last_lean{0};   // dpf_debug_last_lean
+std::atomic<uint32_t> g_no_ctx{0};      // dpf_debug_no_ctx
 
 std::mutex g_dev_mu;
 std::map<int, std::unique_ptr<DeviceTables>> g_dev;
@@ -707,7 +708,8 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     }
   } else {
     rc = dpk_launch_pipeline(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out, dev_meta, n,
-                             dev_stats, part, img->im.v6w_c || img->im.v6w_fib, s);
+                             dev_stats, part, img->im.v6w_c || img->im.v6w_fib,
+                             img->im.ctx_bytes != 0 && !g_no_ctx.load(std::memory_order_relaxed), s);
   }
   if (rc) {
     hipError_t e = hipGetLastError();
@@ -800,6 +802,9 @@ void dpf_debug_nat_sequential(int on) { g_nat_seq.store(on ? 1u : 0u, std::memor
 // Test hook (not part of dpgpu.h): 1 runs every flows burst through the full
 // flows variant (stateful NAT compiled in) even where the lean one serves.
 void dpf_debug_flows_full(int on) { g_flows_full.store(on ? 1u : 0u, std::memory_order_relaxed); }
+// Test hook (not part of dpgpu.h): 1 runs the non-flow pipeline without the
+// LDS copy of the context tables even where they fit (A/Bs, parity of both).
+void dpf_debug_no_ctx(int on) { g_no_ctx.store(on ? 1u : 0u, std::memory_order_relaxed); }
 // Test hook: 1 if the last flows burst launched ran the lean variant.
 int dpf_debug_last_lean() { return (int)g_last_lean.load(std::memory_order_relaxed); }
 

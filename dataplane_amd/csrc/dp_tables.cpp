@@ -998,6 +998,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
     nhrecs.push_back(r);
   }
   im.nh_recs = ib.put(nhrecs);
+  im.n_nh = (uint32_t)nhrecs.size();
 
   section("fib");
   // --- interfaces / adjacencies
@@ -1410,6 +1411,23 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   for (auto &e : ntkv) if (e.k0 == 1) pair_of(e.k1, e.k2);
   im.pairs = build_hash(ib, pkv);
   im.pair_recs = ib.put(prs);
+  im.n_pair_recs = (uint32_t)prs.size();
+  {
+    // the per-workgroup LDS copy of the context tables (dp_kernel.hip DP_CTX)
+    auto a16 = [](uint64_t x) { return (x + 15) & ~15ull; };
+    const uint64_t vni = a16((uint64_t)(im.vni_mask + 1) * sizeof(VniRec));
+    const uint64_t psl = a16((uint64_t)(im.pairs.mask + 1) * sizeof(HashSlot));
+    const uint64_t prc = a16((uint64_t)im.n_pair_recs * sizeof(PairRec));
+    const uint64_t nh = a16((uint64_t)im.n_nh * sizeof(NhRec));
+    // (only where packets read them: an image without VPC peerings routes
+    // in the underlay, and there the copy cost C1 5 %)
+    if (im.n_pair_recs && vni + psl + prc + nh <= DPD_CTX_MAX) {
+      im.ctx_pslots = (uint32_t)vni;
+      im.ctx_prec = (uint32_t)(vni + psl);
+      im.ctx_nh = (uint32_t)(vni + psl + prc);
+      im.ctx_bytes = (uint32_t)(vni + psl + prc + nh);
+    }
+  }
   im.nat_tab_recs = ib.put(ntabs);
   im.nat_ents = ib.put(nents);
   im.nat_prs = ib.put(nprs);

@@ -28,6 +28,14 @@ extern "C" int dpemu_process(const dp_tables_desc_t *d, uint8_t *buf, uint64_t b
   return 0;
 }
 
+// (n_vni_slots, pair map slots, pair records, next hops, LDS context bytes)
+extern "C" int dpemu_image_ctx(const dp_tables_desc_t *d, uint32_t *o) {
+  dpd::BuiltImage bi;
+  if (dpd::build_image(d, bi)) return -1;
+  const dpd::Image &im = bi.im;
+  o[0] = im.vni_mask + 1; o[1] = im.pairs.mask + 1; o[2] = im.n_pair_recs; o[3] = im.n_nh; o[4] = im.ctx_bytes;
+  return 0;
+}
 extern "C" uint64_t dpemu_image_bytes(const dp_tables_desc_t *d) {
   dpd::BuiltImage bi;
   if (dpd::build_image(d, bi)) return 0;

@@ -47,6 +47,24 @@ def test_gpu_matches_oracle(nf, cfg, form, layout, cls_form):
     assert int(stats[A.DONE["Delivered"]]) == h.get("Delivered", 0)
 
 
+@pytest.mark.parametrize("cfg", [1, 2, 4])
+def test_gpu_matches_oracle_without_lds_context(nf, cfg):
+    """The same through the units that read the context tables from HBM
+    (parts 11 / 12; images whose tables fit DPD_CTX_MAX run parts 1 / 2,
+    with a per-workgroup LDS copy)."""
+    lib = A.gpu_lib()
+    w = Workload(cfg, 20000, seed=300 + cfg, n_routes_v4=20000, n_acl=1000, n_nat=64, tcp_percent=25)
+    nf.publish(w.tables)
+    b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
+    o_ref = Oracle(w.tables).process(b_ref, w.inp)
+    lib.dpf_debug_no_ctx(1)
+    try:
+        o_dut = nf.process_arrays(b_dut, w.inp)
+    finally:
+        lib.dpf_debug_no_ctx(0)
+    compare(o_ref, b_ref, o_dut, b_dut, w.inp, f"C{cfg} without LDS context")
+
+
 @pytest.fixture(scope="module")
 def edge():
     t = edge_tables()
