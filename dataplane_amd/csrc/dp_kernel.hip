@@ -62,13 +62,13 @@ using namespace dpd;
 #endif
 constexpr bool SNAT = DP_SNAT;
 // DP_CTX: the context tables (VNI slots, pair map, PairRecs, NhRecs) read
-// from a per-workgroup LDS copy (Image.ctx_bytes > 0).  Parts 1 and 2 build
-// the non-flow pipeline so, at 256 work-items per workgroup (the copy is
-// amortised over more packets and three workgroups' LDS still fit a CU at 3
-// waves per SIMD); parts 11 and 12 without it, for images whose context
-// tables do not fit DPD_CTX_MAX.
+// from a per-workgroup LDS copy (Image.ctx_bytes > 0).  Parts 1, 2 (and 7,
+// 8 with the v6 windows) build the non-flow pipeline so, at 256 work-items
+// per workgroup (the copy is amortised over more packets and three
+// workgroups' LDS still fit a CU at 3 waves per SIMD); parts 11, 12 (13, 14)
+// without it, for images whose context tables do not fit DPD_CTX_MAX.
 #ifndef DP_CTX
-#if DP_PART == 1 || DP_PART == 2
+#if DP_PART == 1 || DP_PART == 2 || DP_PART == 7 || DP_PART == 8
 #define DP_CTX 1
 #else
 #define DP_CTX 0
@@ -4534,6 +4534,8 @@ void dpk_run_pipeline_100s(DP_RUN_ARGS);
 void dpk_run_pipeline_110s(DP_RUN_ARGS);
 void dpk_run_pipeline_000n(DP_RUN_ARGS);
 void dpk_run_pipeline_010n(DP_RUN_ARGS);
+void dpk_run_pipeline_000wn(DP_RUN_ARGS);
+void dpk_run_pipeline_010wn(DP_RUN_ARGS);
 }
 #if DP_IN_PART(1)
 DP_RUNNER(dpk_run_pipeline_000, false, false, false)
@@ -4564,6 +4566,12 @@ DP_RUNNER(dpk_run_pipeline_000n, false, false, false)
 #endif
 #if DP_PART == 12 || DP_PART < 0
 DP_RUNNER(dpk_run_pipeline_010n, false, true, false)
+#endif
+#if DP_PART == 13 || DP_PART < 0
+DP_RUNNER(dpk_run_pipeline_000wn, false, false, false)
+#endif
+#if DP_PART == 14 || DP_PART < 0
+DP_RUNNER(dpk_run_pipeline_010wn, false, true, false)
 #endif
 #if DP_PART == 9 || DP_PART < 0  // (a one-unit build: the full variant under the lean name)
 DP_RUNNER(dpk_run_pipeline_100s, true, false, false)
@@ -4667,9 +4675,11 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_de
   const dpf::FlowCtx nofc{};
   // an image with v6 windows needs the units that look them up; the others
   // read the context tables from LDS when they fit (ctx != 0)
-  if (meta) (v6w ? dpk_run_pipeline_010w : ctx ? dpk_run_pipeline_010 : dpk_run_pipeline_010n)(
+  if (meta) (v6w ? (ctx ? dpk_run_pipeline_010w : dpk_run_pipeline_010wn)
+                 : (ctx ? dpk_run_pipeline_010 : dpk_run_pipeline_010n))(
       blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, nofc);
-  else (v6w ? dpk_run_pipeline_000w : ctx ? dpk_run_pipeline_000 : dpk_run_pipeline_000n)(
+  else (v6w ? (ctx ? dpk_run_pipeline_000w : dpk_run_pipeline_000wn)
+            : (ctx ? dpk_run_pipeline_000 : dpk_run_pipeline_000n))(
       blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, nofc);
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,

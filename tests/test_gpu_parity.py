@@ -47,13 +47,14 @@ def test_gpu_matches_oracle(nf, cfg, form, layout, cls_form):
     assert int(stats[A.DONE["Delivered"]]) == h.get("Delivered", 0)
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 4])
+@pytest.mark.parametrize("cfg", [2, 4, 5])
 def test_gpu_matches_oracle_without_lds_context(nf, cfg):
     """The same through the units that read the context tables from HBM
-    (parts 11 / 12; images whose tables fit DPD_CTX_MAX run parts 1 / 2,
-    with a per-workgroup LDS copy)."""
+    (parts 11 / 12, 13 / 14 with v6 windows; an overlay image whose tables
+    fit DPD_CTX_MAX runs parts 1 / 2 or 7 / 8, with a per-workgroup LDS copy)."""
     lib = A.gpu_lib()
-    w = Workload(cfg, 20000, seed=300 + cfg, n_routes_v4=20000, n_acl=1000, n_nat=64, tcp_percent=25)
+    w = Workload(cfg, 20000, seed=300 + cfg, n_routes_v4=20000, n_routes_v6=8000, n_acl=1000, n_nat=64,
+                 tcp_percent=25)
     nf.publish(w.tables)
     b_ref, b_dut = w.fresh_buf(), w.fresh_buf()
     o_ref = Oracle(w.tables).process(b_ref, w.inp)
