@@ -66,9 +66,11 @@ constexpr bool SNAT = DP_SNAT;
 // 8 with the v6 windows) build the non-flow pipeline so, at 256 work-items
 // per workgroup (the copy is amortised over more packets and three
 // workgroups' LDS still fit a CU at 3 waves per SIMD); parts 11, 12 (13, 14)
-// without it, for images whose context tables do not fit DPD_CTX_MAX.
+// without it, for images whose context tables do not fit DPD_CTX_MAX.  The
+// lean flows units (9, 10) have it too: an image whose tables do not fit
+// runs the full flows variant.
 #ifndef DP_CTX
-#if DP_PART == 1 || DP_PART == 2 || DP_PART == 7 || DP_PART == 8
+#if DP_PART == 1 || DP_PART == 2 || DP_PART == 7 || DP_PART == 8 || DP_PART == 9 || DP_PART == 10
 #define DP_CTX 1
 #else
 #define DP_CTX 0

@@ -678,9 +678,11 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.force_seq = g_nat_seq.load(std::memory_order_relaxed);
     // the flows variant without stateful NAT: an image without it, on a table
     // no such image's burst ever ran on (only those bursts make NAT state),
-    // and no v6 windows (the lean units leave those lookups out)
+    // no v6 windows (the lean units leave those lookups out) and context
+    // tables that fit the lean units' LDS copy
     if (img->im.snat) ft->snat_seen = true;
-    fc.lean = !ft->snat_seen && !img->im.v6w_c && !img->im.v6w_fib && !g_flows_full.load(std::memory_order_relaxed);
+    fc.lean = !ft->snat_seen && !img->im.v6w_c && !img->im.v6w_fib && img->im.ctx_bytes &&
+              !g_flows_full.load(std::memory_order_relaxed);
     g_last_lean.store(fc.lean, std::memory_order_relaxed);
     if (words + sum_words > c->pf_bits_n) {
       c->pf_bits.release();
