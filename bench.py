@@ -220,7 +220,7 @@ def flows_leg(nf, w, dev, stream, steps: int) -> dict:
                     "(median of %d launches)" % steps}
 
 
-def nat_leg(dev, stream, steps: int, n: int) -> dict:
+def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
     """Port forwarding under load: a burst of n 64-byte
     packets of which a share opens new port-forwarded connections
     (dataplane_amd/natwork.py), through the flows variant with its NAT pass
@@ -233,7 +233,7 @@ def nat_leg(dev, stream, steps: int, n: int) -> dict:
     from dataplane_amd.flows import FlowTable
     lib = A.gpu_lib()
     nf2 = GpuPathNf(dev.index)
-    nf2.publish(W.tables().build())
+    nf2.publish((W.masq_tables() if kind == "masq" else W.tables()).build())
     slots = 1 << max(12, int(np.ceil(np.log2(max(1, 4 * n)))))
     ft = FlowTable(dev.index, slots)
     nf2.attach_flows(ft)
@@ -243,7 +243,7 @@ def nat_leg(dev, stream, steps: int, n: int) -> dict:
     clock = [0]
 
     def run(share, reps, one_lane=False):
-        buf, inp, npf = W.burst(n, share, 0)
+        buf, inp, npf = W.burst(n, share, 0, kind=kind)
         pristine = torch.from_numpy(buf).to(dev)
         b = torch.empty_like(pristine)
         dinp = torch.from_numpy(inp.view(np.uint8)).to(dev)
@@ -274,17 +274,23 @@ def nat_leg(dev, stream, steps: int, n: int) -> dict:
                 "mpps_median": round(n / (med / 1e3) / 1e6, 3), "flows_after": int(flows), "launches": len(keep),
                 "done_histogram": done}
 
-    for share in (0.0, 0.01, 0.05, 0.25):
-        res["legs"].append(run(share, steps + 1))
-        log(0, f"[bench] NAT leg share {share}: {res['legs'][-1]['launch_ms_median']} ms")
-    res["legs"].append(run(0.25, 2, one_lane=True))
-    log(0, f"[bench] NAT leg one lane: {res['legs'][-1]['launch_ms_median']} ms")
+    if kind == "masq":  # (one lane in packet order: every masquerading burst)
+        for share in (0.001, 0.01):
+            res["legs"].append(run(share, min(steps, 3) + 1))
+            log(0, f"[bench] masquerade leg share {share}: {res['legs'][-1]['launch_ms_median']} ms")
+    else:
+        for share in (0.0, 0.01, 0.05, 0.25):
+            res["legs"].append(run(share, steps + 1))
+            log(0, f"[bench] NAT leg share {share}: {res['legs'][-1]['launch_ms_median']} ms")
+        res["legs"].append(run(0.25, 2, one_lane=True))
+        log(0, f"[bench] NAT leg one lane: {res['legs'][-1]['launch_ms_median']} ms")
     nf2.attach_flows(None)
     ft.close()
     nf2.close()
-    res["what"] = ("flows variant with port-forwarding creations: first pass, NAT pass (dp_nat_prep + "
+    res["what"] = ("flows variant with %s creations: first pass, NAT pass (dp_nat_prep + "
                    "dp_nat_resolve), replay, fix-up, invalidation, per launch (HIP events, median); "
-                   "per-kernel times: profiles/ rocprofv3 stats of this leg")
+                   "per-kernel times: profiles/ rocprofv3 stats of this leg"
+                   % ("masquerade (allocations from a 256-address pool)" if kind == "masq" else "port-forwarding"))
     return res
 
 
@@ -330,8 +336,10 @@ def main() -> None:
         if world > 1:
             torch.distributed.barrier()
 
-    if args.nat_only:  # the NAT leg alone (rocprofv3 of its kernels)
-        print(json.dumps({"nat_portfw": nat_leg(dev, torch.cuda.Stream(dev), min(args.steps, 10), args.packets)}),
+    if args.nat_only:  # the NAT legs alone (rocprofv3 of their kernels)
+        st = torch.cuda.Stream(dev)
+        print(json.dumps({"nat_portfw": nat_leg(dev, st, min(args.steps, 10), args.packets),
+                          "nat_masquerade": nat_leg(dev, st, min(args.steps, 10), args.packets, kind="masq")}),
               flush=True)
         return
     cfg = args.config
@@ -491,6 +499,7 @@ def main() -> None:
             result["flow_table"] = flows_leg(nf, w, dev, stream, args.steps)
         if world == 1 and not args.no_nat:
             result["nat_portfw"] = nat_leg(dev, stream, min(args.steps, 10), n)
+            result["nat_masquerade"] = nat_leg(dev, stream, min(args.steps, 10), n, kind="masq")
         if world == 1 and not args.no_host:
             # host-origin rate (dp_process_burst): pinned host burst buffer and
             # records, chunked H2D / kernel / D2H overlapped on several streams

@@ -3675,7 +3675,7 @@ struct Seq {
 __device__ inline uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
 // PortForwarder for one record, in packet order.
-__device__ void resolve_pf(const Seq &q, dpf::PfReq &R) {
+__device__ __forceinline__ void resolve_pf(const Seq &q, dpf::PfReq &R) {
   const dpf::FlowCtx &fc = q.fc;
   const Img &g = q.g;
   const uint32_t idx = R.idx;
@@ -3854,7 +3854,7 @@ __device__ uint32_t masq_done(uint32_t e) {
 
 // Masquerade::masquerade_packet (nf.rs:384-475) for one record, after its
 // PortForwarder decision (the packet as PortForwarder left it).
-__device__ void resolve_masq(const Seq &q, dpf::PfReq &R) {
+__device__ __forceinline__ void resolve_masq(const Seq &q, dpf::PfReq &R) {
   const dpf::FlowCtx &fc = q.fc;
   const uint32_t idx = R.idx;
   const uint32_t fam = (R.proto >> 8) & 0xffu, proto = R.proto & 0xffu, tfl = R.proto >> 16;
@@ -4013,7 +4013,7 @@ __device__ void resolve_masq(const Seq &q, dpf::PfReq &R) {
 }
 
 // One record, in packet order: PortForwarder, then Masquerade on what it left.
-__device__ void resolve_one(const Seq &q, dpf::PfReq &R) {
+__device__ __forceinline__ void resolve_one(const Seq &q, dpf::PfReq &R) {
   R.mverdict = dpf::kPfForward;
   resolve_pf(q, R);
   if ((R.bits & dpf::kPqMasq) && R.verdict == dpf::kPfForward) resolve_masq(q, R);
@@ -4251,19 +4251,56 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
 // the 7/8 bound (the admissions of insert_common,
 // flow-entry/src/flow_table/table.rs:215-260, then cannot depend on the
 // order of connections); else one lane over all records in packet order.
-__global__ void __launch_bounds__(256) dp_nat_resolve(const uint8_t *__restrict__ img_base,
-                                                      const Image *__restrict__ im, dpf::FlowCtx fc) {
+// Two instantiations, one launch each: SEQ (one wave) runs the burst when
+// it needs the sequential pass, the other (the grid) when it does not; each
+// leaves at once otherwise.  Apart, each is compiled for its own mode: the
+// sequential lane's records inlined (no call frame to save and restore per
+// record), the parallel lanes at 6 waves per SIMD.
+template <bool SEQ>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEQ ? 1 : 6)))
+dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ im, dpf::FlowCtx fc) {
   const uint32_t total = fc.pf_cnt[1];
   if (!total) return;
   const Img g{img_base, *im};
   const uint64_t len0 = ((uint64_t)fc.pf_cnt[7] << 32) | fc.pf_cnt[6];
   const bool seq = fc.force_seq || fc.pf_cnt[5] || len0 + 2ull * total > fc.capacity ||
                    len0 + 2ull * total > fc.hard;
+  if (seq != SEQ) return;
   const uint32_t gt = blockIdx.x * 256 + threadIdx.x;
-  if (seq) {
-    if (gt != 0) return;
+  if constexpr (SEQ) {
+    // one lane in packet order; the other 63 lanes of its wave run ahead,
+    // loading what the next 64 records will read -- the record, its flow and
+    // that flow's related flow, the home slot of the key a creation inserts
+    // first -- so the lane's chain of dependent accesses meets L2 lines
+    // instead of HBM ones (values unused: the loads only warm the cache)
+    if (gt >= 64) return;
     const pfw::Seq q{fc, g, false};
-    for (uint32_t k = 0; k < total; k++) pfw::resolve_one(q, fc.pf[fc.pf_of[fc.pf_order[k]]]);
+    for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+      if (k0 + gt < total) {
+        const dpf::PfReq &P = fc.pf[fc.pf_of[fc.pf_order[k0 + gt]]];
+        uint32_t acc = P.bits ^ P.proto;
+        if (P.slot <= fc.mask) {
+          const uint4 a = ld4(&fc.slots[P.slot].state);
+          acc ^= a.x;
+          if (P.related0 <= fc.mask) acc ^= ld4(&fc.slots[P.related0].state).x;
+        }
+        dpf::FKey k;
+        if (P.bits & dpf::kPqIkey) {
+          for (int j = 0; j < 11; j++) k.w[j] = P.ikey[j];
+        } else {
+          const uint32_t kind = (P.bits & dpf::kPqTcp) ? DP_FLOW_TCP : (P.bits & dpf::kPqUdp) ? DP_FLOW_UDP
+                                                                                         : DP_FLOW_ICMP_QUERY;
+          k.w[0] = P.src_vni;
+          k.w[1] = ((P.proto >> 8) & 0xffu) | (kind << 8);
+          k.w[2] = P.ports;
+          for (int j = 0; j < 4; j++) { k.w[3 + j] = pfw::bswap(P.src[j]); k.w[7 + j] = pfw::bswap(P.dst[j]); }
+        }
+        acc ^= ld4(&fc.slots[dpf::fkey_hash(k) & fc.mask].state).x;
+        asm volatile("" ::"v"(acc));
+      }
+      if (gt == 0)
+        for (uint32_t k = k0; k < total && k < k0 + 64; k++) pfw::resolve_one(q, fc.pf[fc.pf_of[fc.pf_order[k]]]);
+    }
     // the flows replaced during the burst are dropped after it, with the
     // allocations their masquerade state owns
     if (fc.mq) {
@@ -4723,7 +4760,8 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   const uint32_t pb = (n + 1023) / 1024 < 256 ? (n + 1023) / 1024 : 256;
   hipLaunchKernelGGL(dp_nat_prep, dim3(pb), dim3(1024), 0, stream, img_base, im, fc);
   const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
-  hipLaunchKernelGGL(dp_nat_resolve, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
+  hipLaunchKernelGGL(dp_nat_resolve<true>, dim3(1), dim3(64), 0, stream, img_base, im, fc);
+  hipLaunchKernelGGL(dp_nat_resolve<false>, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   fc.replay = 1;
   if (meta) dpk_run_pipeline_111(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   else dpk_run_pipeline_101(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
