@@ -4302,8 +4302,8 @@ dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ i
         for (uint32_t k = k0; k < total && k < k0 + 64; k++) pfw::resolve_one(q, fc.pf[fc.pf_of[fc.pf_order[k]]]);
     }
     // the flows replaced during the burst are dropped after it, with the
-    // allocations their masquerade state owns
-    if (fc.mq) {
+    // allocations their masquerade state owns (by the one lane)
+    if (gt == 0 && fc.mq) {
       const dpm::View V{fc.mq};
       for (uint32_t k = 0; k < fc.pf_cnt[3]; k++) dpm::release(V, fc.mq_rel[2 * k], fc.mq_rel[2 * k + 1]);
     }
