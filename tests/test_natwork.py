@@ -56,14 +56,16 @@ def test_gpu_natwork(kind):
     try:
         nf.publish(tp)
         nf.attach_flows(gft)
+        pairs = 0
         for step in range(2):
             buf, inp, npf = W.burst(N, 0.05, step, kind=kind)
+            pairs += npf
             ob, gb = buf.copy(), buf.copy()
             oout, _ = o.process_flows(ob, inp, oft)
             gout = nf.process_arrays(gb, inp)
             compare(oout, ob, gout, gb, inp, f"{kind} burst {step}")
             assert gft.count() == oft.count()
-            assert gft.count()[0] == 2 * npf * (step + 1)
+            assert gft.count()[0] == 2 * pairs
     finally:
         nf.attach_flows(None)
         gft.close()
