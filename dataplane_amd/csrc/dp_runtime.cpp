@@ -1159,9 +1159,17 @@ int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf
   }
   for (uint32_t k = 0; k < n_ctx; k++) {
     if (!ctxs[k]) { mark_failed_host(in, out, meta, n); return fail(DP_EINVAL, "null context"); }
-    // one flow table per device cannot give the shards the reference's
-    // shared Arc<FlowTable> (flows shard by 5-tuple hash)
-    if (ctxs[k]->ft) { mark_failed_host(in, out, meta, n); return fail(DP_ENOTSUP, "sharded bursts with a flow table"); }
+    // With a flow table, every context shares it (the reference's one
+    // Arc<FlowTable> behind every worker's pipeline, packet_processor/mod.rs:
+    // 68,100-120): the shards are the workers' bursts, and the table's order
+    // (its last_burst event, taken under its lock) runs their flows launches
+    // one after the other in shard order -- one of the orders the reference's
+    // concurrent workers may take.  A table lives on one device, so such
+    // shards share it (contexts of one GPU); the copies still overlap.
+    if (ctxs[k]->ft != ctxs[0]->ft) {
+      mark_failed_host(in, out, meta, n);
+      return fail(DP_EINVAL, "sharded bursts: every context attached to the same flow table, or none");
+    }
   }
   struct Shard {
     uint32_t first, cnt;

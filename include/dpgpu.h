@@ -554,6 +554,13 @@ int dp_process_burst_device(dp_ctx_t *ctx, uint8_t *dev_buf, uint64_t buf_bytes,
  * so the result equals dp_process_burst on one device bit for bit
  * (tests/test_shard.py).  The analogue of the reference's per-worker fan-out
  * (dataplane/src/drivers/kernel/fanout.rs:49-73, worker.rs:175).
+ * With a flow table: every context must be attached to the same one (else
+ * DP_EINVAL) -- the reference's one Arc<FlowTable> shared by every worker --
+ * and the shards are the workers' bursts, their flows launches run on the
+ * table one after the other in shard order (one of the orders the
+ * reference's concurrent workers may take): the result equals
+ * dp_process_burst of each shard in turn on one context.  A flow table lives
+ * on one device, so those contexts are contexts of one GPU.
  * Synchronous; `stats` (may be NULL) receives the summed DoneReason counts.
  * A whole-burst failure marks every packet DP_DONE_INTERNAL_FAILURE. */
 int dp_process_burst_sharded(dp_ctx_t *const *ctxs, uint32_t n_ctx, uint8_t *buf,

@@ -191,7 +191,8 @@ def test_gpu_flows_host_origin(nf):
     """With a flow table attached, the host-origin entry (dp_process_burst:
     the burst is one launch, never chunked, since flow-filter invalidations
     must reach every later packet of the burst) matches the oracle on a burst
-    larger than the host path's chunk; the sharded entry refuses flow tables."""
+    larger than the host path's chunk; the sharded entry refuses contexts
+    attached to different flow tables."""
     from dataplane_amd.flows import burst_request_flows
     w = Workload(2, 150_000, seed=11, n_routes_v4=5000, n_acl=500, n_nat=24, tcp_percent=30)
     ora = Oracle(w.tables)
@@ -207,8 +208,12 @@ def test_gpu_flows_host_origin(nf):
         obuf, hbuf = w.fresh_buf(), w.fresh_buf()
         oout, _ = ora.process_flows(obuf, w.inp, oft)
         hout = nf.process_arrays(hbuf, w.inp)
-        with pytest.raises(RuntimeError):
-            GpuPathNf.process_sharded([nf], w.fresh_buf(), w.inp)
+        other = GpuPathNf(0)
+        try:
+            with pytest.raises(RuntimeError):
+                GpuPathNf.process_sharded([nf, other], w.fresh_buf(), w.inp)
+        finally:
+            other.close()
     finally:
         nf.attach_flows(None)
     compare(oout, obuf, hout, hbuf, w.inp, "flows host-origin")

@@ -6,7 +6,9 @@ packet one translated flow pair (port forwarding: destination 192.168.0.0/16
 ports 5000-5999; masquerade: source in the 203.0.113.0/24 pool).
 GPU: the C ABI's flows variant (parallel NAT pass for port forwarding, one
 lane for masquerade) == the oracle on the same bursts, bit-exact, two
-bursts in a row, flow counts included."""
+bursts in a row, flow counts included; and a burst sharded over two
+contexts sharing one flow table (dp_process_burst_sharded) == the same
+shards as consecutive bursts of one context."""
 import ipaddress
 
 import numpy as np
@@ -70,3 +72,46 @@ def test_gpu_natwork(kind):
         nf.attach_flows(None)
         gft.close()
         nf.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["pf", "masq"])
+def test_gpu_natwork_sharded_shared_table(kind):
+    """The reference's workers share one Arc<FlowTable>
+    (dataplane/src/packet_processor/mod.rs:68,100-120): shards of a burst
+    over two contexts attached to one table run as the workers' bursts in
+    shard order -- bit-exact against one context taking the shards as
+    consecutive bursts on its own table: outputs, bytes, every flow's
+    presence and state, the flow counts, and the masquerade allocations
+    (the translated sources)."""
+    import torch
+    torch.cuda.init()
+    from dataplane_amd import GpuPathNf
+    from dataplane_amd.flows import FlowTable
+    tp = world(kind)
+    a, b, ref = GpuPathNf(0), GpuPathNf(0), GpuPathNf(0)
+    ft, ft_ref = FlowTable(0, 1 << 16), FlowTable(0, 1 << 16)
+    try:
+        for nf in (a, b, ref):
+            nf.publish(tp)
+        a.attach_flows(ft)
+        b.attach_flows(ft)
+        ref.attach_flows(ft_ref)
+        for step in range(2):
+            buf, inp, npf = W.burst(N, 0.05, step, kind=kind)
+            rb, db = buf.copy(), buf.copy()
+            h = len(inp) // 2
+            r0 = ref.process_arrays(rb, inp[:h].copy())
+            r1 = ref.process_arrays(rb, inp[h:].copy())
+            rout = np.concatenate([r0, r1])
+            dout = GpuPathNf.process_sharded([a, b], db, inp)
+            compare(rout, rb, dout, db, inp, f"{kind} sharded burst {step}")
+            assert ft.count() == ft_ref.count()
+            assert ft.count()[0] > 0
+    finally:
+        for nf in (a, b, ref):
+            nf.attach_flows(None)
+        ft.close()
+        ft_ref.close()
+        for nf in (a, b, ref):
+            nf.close()
