@@ -4256,8 +4256,11 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
 // leaves at once otherwise.  Apart, each is compiled for its own mode: the
 // sequential lane's records inlined (no call frame to save and restore per
 // record), the parallel lanes at 6 waves per SIMD.
+#ifndef DP_RESOLVE_WAVES
+#define DP_RESOLVE_WAVES 6
+#endif
 template <bool SEQ>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEQ ? 1 : 6)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEQ ? 1 : DP_RESOLVE_WAVES)))
 dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ im, dpf::FlowCtx fc) {
   const uint32_t total = fc.pf_cnt[1];
   if (!total) return;
