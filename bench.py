@@ -9,6 +9,12 @@ contains only the kernel launches.  Multi-GPU: one process per GPU, each
 processing its own shard (packets are independent: weak scaling, no
 data-path collective).
 
+Beside `value` (never inside it), rank 0 at N=1 reports legs: the same burst
+with meta records, with a flow table attached (flow_table), port forwarding
+and masquerade under load (nat_portfw, nat_masquerade: a share of a 2M burst
+opening new stateful-NAT connections), host-origin bursts (host_inclusive),
+and the CPU baseline.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
 """
 from __future__ import annotations
