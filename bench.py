@@ -240,7 +240,7 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
     lib = A.gpu_lib()
     nf2 = GpuPathNf(dev.index)
     nf2.publish((W.masq_tables() if kind == "masq" else W.tables()).build())
-    slots = 1 << max(12, int(np.ceil(np.log2(max(1, 4 * n)))))
+    slots = 1 << max(12, int(np.ceil(np.log2(max(1, 4 * n)))))  # (8M for 2M packets: 1 GiB)
     ft = FlowTable(dev.index, slots)
     nf2.attach_flows(ft)
     sptr = stream.cuda_stream
@@ -280,10 +280,67 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
                 "mpps_median": round(n / (med / 1e3) / 1e6, 3), "flows_after": int(flows), "launches": len(keep),
                 "done_histogram": done}
 
-    if kind == "masq":  # (one lane in packet order: every masquerading burst)
+    def counters():
+        import ctypes as C
+        c = (C.c_uint32 * 24)()
+        lib.dpf_debug_nat_counters(nf2.ctx, c, 24)
+        return {"mode": int(c[12]), "records": int(c[1]), "lane_records": int(c[11]),
+                "left_by_connections": int(c[13]), "allocations_batched": int(c[14]),
+                "allocations_alone": int(c[15])}
+
+    def run_established(reps, conns=200_000, new_share=0.01, fwd_share=0.6):
+        """Every packet masqueraded: `conns` connections opened by an untimed
+        burst, then 2M-packet bursts of which 99 % belong to them (the
+        clients' packets and the servers' answers to the public tuples,
+        shuffled) and 1 % open new connections (fresh clients every launch)."""
+        nf2.publish(W.masq_world().build())
+        clock[0] += hour
+        nf2.set_option(A.OPT_CLOCK, clock[0])
+        ft.sweep(clock[0])
+        c = W.MasqConns(conns)
+        buf, inp = c.first()
+        b = torch.from_numpy(buf).to(dev)
+        dinp = torch.from_numpy(inp.view(np.uint8)).to(dev)
+        dout = torch.empty(len(inp) * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+        nf2.process_device(b.data_ptr(), b.numel(), dinp.data_ptr(), dout.data_ptr(), len(inp), None, sptr)
+        torch.cuda.synchronize(dev)
+        out0 = np.frombuffer(dout.cpu().numpy().tobytes(), dtype=A.PKT_OUT)
+        learnt = c.learn(b.cpu().numpy(), out0)
+        ms, cnts, done = [], [], {}
+        for k in range(reps):
+            buf, inp, nn = c.burst(n, new_share, fwd_share, step=k + 1)
+            b = torch.from_numpy(buf).to(dev)
+            dinp = torch.from_numpy(inp.view(np.uint8)).to(dev)
+            dout = torch.empty(n * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+            clock[0] += 10 ** 6
+            nf2.set_option(A.OPT_CLOCK, clock[0])
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            nf2.process_device(b.data_ptr(), b.numel(), dinp.data_ptr(), dout.data_ptr(), n, None, sptr)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            ms.append(e0.elapsed_time(e1))
+            cnts.append(counters())
+            out = np.frombuffer(dout.cpu().numpy().tobytes(), dtype=A.PKT_OUT)
+            done = {A.DONE_NAMES[d]: int(x) for d, x in zip(*np.unique(out["done"], return_counts=True))}
+        keep = ms[1:] if len(ms) > 1 else ms
+        med = sorted(keep)[len(keep) // 2]
+        return {"established_connections": conns, "learnt": learnt, "new_share": new_share,
+                "client_share": fwd_share, "launch_ms_median": round(med, 4), "launch_ms": [round(x, 4) for x in ms],
+                "mpps_median": round(n / (med / 1e3) / 1e6, 3), "flows_after": int(ft.count()[0]),
+                "launches": len(keep), "nat_pass": cnts[-1], "done_histogram": done}
+
+    if kind == "masq":
+        # first packets of new connections only (the allocating lane), then
+        # every packet masqueraded (connection lanes + the allocating lane)
         for share in (0.001, 0.01):
             res["legs"].append(run(share, min(steps, 3) + 1))
+            res["legs"][-1]["nat_pass"] = counters()
             log(0, f"[bench] masquerade leg share {share}: {res['legs'][-1]['launch_ms_median']} ms")
+        res["established"] = run_established(min(steps, 4) + 1)
+        log(0, f"[bench] masquerade leg, every packet masqueraded (99% established, 1% new): "
+               f"{res['established']['launch_ms_median']} ms")
     else:
         for share in (0.0, 0.01, 0.05, 0.25):
             res["legs"].append(run(share, steps + 1))
@@ -294,9 +351,10 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
     ft.close()
     nf2.close()
     res["what"] = ("flows variant with %s creations: first pass, NAT pass (dp_nat_prep + "
-                   "dp_nat_resolve), replay, fix-up, invalidation, per launch (HIP events, median); "
+                   "dp_nat_resolve%s), replay, fix-up, invalidation, per launch (HIP events, median); "
                    "per-kernel times: profiles/ rocprofv3 stats of this leg"
-                   % ("masquerade (allocations from a 256-address pool)" if kind == "masq" else "port-forwarding"))
+                   % (("masquerade (allocations from a 256-address pool)", " + dp_nat_lane_order + dp_nat_lane")
+                      if kind == "masq" else ("port-forwarding", "")))
     return res
 
 
@@ -325,6 +383,8 @@ def main() -> None:
     ap.add_argument("--layout", choices=["dpdk", "packed"], default="dpdk",
                     help="burst buffer layout: DPDK mbuf data (128 B headroom, 64-byte aligned "
                          "frames) or packed (96 B headroom, 16-byte aligned)")
+    ap.add_argument("--nat-kind", choices=["both", "pf", "masq"], default="both",
+                    help="with --nat-only: which NAT legs")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -344,9 +404,12 @@ def main() -> None:
 
     if args.nat_only:  # the NAT legs alone (rocprofv3 of their kernels)
         st = torch.cuda.Stream(dev)
-        print(json.dumps({"nat_portfw": nat_leg(dev, st, min(args.steps, 10), args.packets),
-                          "nat_masquerade": nat_leg(dev, st, min(args.steps, 10), args.packets, kind="masq")}),
-              flush=True)
+        legs = {}
+        if args.nat_kind in ("both", "pf"):
+            legs["nat_portfw"] = nat_leg(dev, st, min(args.steps, 10), args.packets)
+        if args.nat_kind in ("both", "masq"):
+            legs["nat_masquerade"] = nat_leg(dev, st, min(args.steps, 10), args.packets, kind="masq")
+        print(json.dumps(legs), flush=True)
         return
     cfg = args.config
     t0 = time.perf_counter()

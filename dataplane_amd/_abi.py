@@ -341,6 +341,8 @@ def gpu_lib() -> C.CDLL:
         lib.dp_acl_classify.argtypes = [_VP, _VP, _VP, C.c_uint32]
         lib.dp_acl_classify_device.argtypes = [_VP, _VP, _VP, C.c_uint32, _VP]
         lib.dpf_debug_nat_sequential.argtypes = [C.c_int]
+        lib.dpf_debug_nat_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32]
+        lib.dpf_debug_nat_counters.restype = C.c_int
         lib.dpf_debug_flows_full.argtypes = [C.c_int]
         lib.dpf_debug_last_lean.restype = C.c_int
         lib.dpf_debug_no_ctx.argtypes = [C.c_int]

@@ -113,7 +113,16 @@ constexpr uint32_t kPqPf = 1u << 9;       // PortForwarder runs on it (REQ_PORT_
 constexpr uint32_t kPqMasq = 1u << 10;    // Masquerade runs on it (REQ_MASQUERADE)
 constexpr uint32_t kPqIcmp = 1u << 11;    // an ICMP v4 / v6 header
 constexpr uint32_t kPqQuery = 1u << 12;   // its flow key is an ICMP query's (echo, code 0)
+// the masquerading burst's split pass (dp_nat_resolve / dp_nat_lane): the
+// record runs on the burst's one allocating lane; PortForwarder's part of it
+// already ran (its connection's lane left it there)
+constexpr uint32_t kPqLane = 1u << 13;
+constexpr uint32_t kPqPfDone = 1u << 14;
 constexpr uint32_t kPfForward = 0xffu;
+
+// words of FlowCtx::pf_cnt
+constexpr uint32_t kCntWords = 24;
+#define DPF_CNT_WORDS 24
 
 // The launch-time view of a flow table for one burst.
 struct FlowCtx {
@@ -140,7 +149,7 @@ struct FlowCtx {
   // bitmap of packets that reached PortForwarder (+ its summary, 1 bit per
   // 1024 packets), the order of the records (resolve), replaced fills
   PfReq *pf;
-  uint32_t *pf_cnt;     // [0] records, [1] replay packets, [2] replaced fills, [3] releases, [4..7] below
+  uint32_t *pf_cnt;     // [0] records, [1] replay packets, [2] replaced fills, [3] releases, [4..15] below
   uint32_t *pf_of;      // packet -> record
   uint32_t *pf_bits;
   uint32_t *pf_sum;
@@ -157,7 +166,14 @@ struct FlowCtx {
   // (burst << 32 | connection key) and (burst << 32 | its last record), per
   // record (packet index << 32 | the connection's record before it), the
   // slots claimed this burst; [4] their count, [5] a record the parallel
-  // pass cannot take, [6..7] the table length as the pass starts
+  // pass cannot take, [6..7] the table length as the pass starts.
+  // Masquerade (dp_nat_resolve, dp_nat_lane): [8] masquerade records, [9]
+  // PortForwarder records, [10] a masqueraded packet whose peer could
+  // masquerade back (pfw::masq_back), [11] records on the allocating lane,
+  // [12] the mode that ran (1 one lane, 2 connections, 3 split), [13] records
+  // a connection lane left to the allocating lane, [14] allocations served in
+  // wave batches, [15] allocations on the lane alone, [16] pairs the split
+  // pass could not create (never: it runs only with room; counters for tests)
   unsigned long long *grp_tab, *grp_head, *grp_next;
   uint32_t *grp_list;
   uint32_t grp_mask;
@@ -165,7 +181,11 @@ struct FlowCtx {
   // keyed index of the replaced fills: (burst, slot, old state, pf_repl index)
   uint4 *repl;
   uint32_t rmask;
-  uint32_t force_seq;   // test hook (dpf_debug_nat_sequential): the one-lane NAT pass always
+  uint32_t force_seq;   // test hook (dpf_debug_nat_sequential): 1 the one-lane NAT pass always,
+                        // 2 the split pass with every allocation on the lane alone (no wave batches)
+  // the masquerading burst's allocating lane: its packets (bitmap by packet
+  // index + summary, as pf_bits) and their order
+  uint32_t *lane_bits, *lane_sum, *lane_order;
   uint32_t lean;        // the launch runs the flows variant without stateful NAT (dp_kernel.hip DP_SNAT)
 };
 

@@ -3622,7 +3622,7 @@ struct Seq {
       // allocation its masquerade state owns
       const dpf::FlowSlot &o = fc.slots[sl];
       if ((o.flags & dpf::kFlagMasq) && o.mq_rec && o.mq_gen == fc.mq_gen && fc.mq) {
-        const uint32_t k = fc.pf_cnt[3]++;
+        const uint32_t k = bump(&fc.pf_cnt[3]);
         fc.mq_rel[2 * k] = o.mq_rec - 1;
         fc.mq_rel[2 * k + 1] = o.pf >> 16;
       }
@@ -3852,6 +3852,197 @@ __device__ uint32_t masq_done(uint32_t e) {
   }
 }
 
+// The allocation path of Masquerade::masquerade_packet (nf.rs:384-475) in
+// three parts, so the masquerading burst's allocating lane (dp_nat_lane) can
+// serve a wave of records with one allocator step: masq_plan (what the record
+// asks of the allocator, or its verdict without one), the allocation, masq_post
+// (the checks between the allocation and the new pair, which give the tuple
+// back) and masq_pair (the pair, create_flow_pair nf.rs:265-325).
+struct MPlan {
+  dpf::FKey ck, ik;       // the current key; the initial one (before static NAT)
+  uint32_t kind, ikind, ifam, set, dport;
+  bool allow_null;
+  uint32_t sfail;         // a verdict masq_post gives whatever the tuple (0: none)
+  bool eqp;               // the reverse key may equal the initial one (related_pair)
+};
+
+// Is the record's flow valid for Masquerade with state (get_masquerade_state,
+// nf.rs:198-213): the attached fill, Active for this packet (its own
+// PortForwarder step included), holding masquerade state.
+__device__ __forceinline__ bool masq_valid(const Seq &q, const dpf::PfReq &R) {
+  const bool same = R.slot != dpf::kNoSlot && q.alive(R.slot, R.state);
+  return same && R.status0 == DP_FLOW_ACTIVE && q.pair_valid(R.slot, R.idx + 1) &&
+         (q.fc.slots[R.slot].flags & dpf::kFlagMasq);
+}
+
+// The record's current addresses and ports: PortForwarder's translation applied
+__device__ __forceinline__ void masq_cur(const dpf::PfReq &R, uint32_t src[4], uint32_t dst[4], uint32_t &sport,
+                                         uint32_t &dport) {
+  const bool tcp = R.bits & dpf::kPqTcp, udp = R.bits & dpf::kPqUdp;
+  sport = R.ports >> 16;
+  dport = R.ports & 0xffffu;
+  for (int j = 0; j < 4; j++) { src[j] = R.src[j]; dst[j] = R.dst[j]; }
+  if ((R.bits & dpf::kPqPf) && (R.nat & 0xffu)) {
+    const bool s = (R.nat & 0xffu) == DP_PF_SRC_NAT;
+    for (int j = 0; j < 4; j++) (s ? src : dst)[j] = R.nat_ip[j];
+    if (tcp || udp) (s ? sport : dport) = R.nat >> 16;
+  }
+}
+
+// What the record asks of the allocator; false: it is decided without one
+// (R.mverdict set).
+__device__ __forceinline__ bool masq_plan(const dpf::FlowCtx &fc, dpf::PfReq &R, MPlan &m) {
+  const uint32_t fam = (R.proto >> 8) & 0xffu, tfl = R.proto >> 16;
+  const bool tcp = R.bits & dpf::kPqTcp, udp = R.bits & dpf::kPqUdp, icmp = R.bits & dpf::kPqIcmp;
+  uint32_t src[4], dst[4], sport, dport;
+  masq_cur(R, src, dst, sport, dport);
+  dpm::View V{fc.mq};
+  if (!fc.mq) { R.mverdict = DP_DONE_NAT_FAILURE; return false; }  // NoAllocator
+  if (tcp && !((tfl & 2) && !(tfl & 0x3du))) { R.mverdict = DP_DONE_FILTERED; return false; }  // TCP without SYN
+  // FlowKey::try_from(&Packet) (flow_key.rs:589-621): the current key
+  if (tcp) m.kind = DP_FLOW_TCP;
+  else if (udp) m.kind = DP_FLOW_UDP;
+  else if (icmp) m.kind = (R.bits & dpf::kPqQuery) ? DP_FLOW_ICMP_QUERY : DP_FLOW_ICMP_OTHER;
+  else { R.mverdict = DP_DONE_MALFORMED; return false; }  // FlowKeyError
+  const uint32_t cports = m.kind == DP_FLOW_ICMP_OTHER ? 0u : ((sport << 16) | dport);
+  m.ck.w[0] = R.src_vni;
+  m.ck.w[1] = fam | (m.kind << 8);
+  m.ck.w[2] = cports;
+  for (int j = 0; j < 4; j++) { m.ck.w[3 + j] = bswap(src[j]); m.ck.w[7 + j] = bswap(dst[j]); }
+  // the initial key: the one before static NAT, else the current one
+  if (R.bits & dpf::kPqIkey) for (int j = 0; j < 11; j++) m.ik.w[j] = R.ikey[j];
+  else m.ik = m.ck;
+  m.ifam = m.ik.w[1] & 0xffu;
+  m.ikind = m.ik.w[1] >> 8;
+  m.dport = dport;
+  const uint32_t iproto = m.ikind == DP_FLOW_TCP ? 6u : m.ikind == DP_FLOW_UDP ? 17u : m.ifam == 4 ? 1u : 58u;
+  // NatAllocator::allocate (apalloc/mod.rs:317-375): the pool of (protocol,
+  // VPCs, original source); a port, or an ICMP identifier (port 0 allowed)
+  dpm::A128 sip{};
+  if (m.ifam == 4) sip.w[3] = bswap(m.ik.w[3]);
+  else for (int j = 0; j < 4; j++) sip.w[j] = bswap(m.ik.w[3 + j]);
+  m.set = dpm::lookup(V, iproto | (m.ifam << 8), R.src_vni, R.dst_vni, sip);
+  if (m.set == dpm::kNone) { R.mverdict = DP_DONE_FILTERED; return false; }  // Denied
+  m.allow_null = iproto == 1 || iproto == 58;
+  // masq_post's verdicts that do not rest on the tuple
+  m.sfail = m.kind == DP_FLOW_ICMP_OTHER ? (uint32_t)DP_DONE_NAT_FAILURE  // UnexpectedKeyVariant
+          : (m.ikind != DP_FLOW_TCP && m.ikind != DP_FLOW_UDP && m.ikind != DP_FLOW_ICMP_QUERY)
+              ? (uint32_t)DP_DONE_NAT_FAILURE  // IcmpUnsupportedCategory
+              : 0u;
+  // related_pair's equal keys need the reverse key's source (the current
+  // destination) to be the initial source, in the destination VPC
+  bool eq = m.ik.w[0] == R.dst_vni && m.ik.w[1] == m.ck.w[1];
+  for (int j = 0; j < 4; j++) eq = eq && m.ik.w[3 + j] == m.ck.w[7 + j];
+  m.eqp = eq;
+  return true;
+}
+
+// The reverse of the current key towards the allocated tuple
+// (new_reverse_session, nf.rs:327-373)
+__device__ __forceinline__ void masq_rk(const dpf::PfReq &R, const MPlan &m, const uint32_t aip[4], uint32_t aport,
+                                        dpf::FKey &rk) {
+  rk.w[0] = R.dst_vni;
+  rk.w[1] = m.ck.w[1];
+  for (int j = 0; j < 4; j++) { rk.w[3 + j] = m.ck.w[7 + j]; rk.w[7 + j] = bswap(aip[j]); }
+  rk.w[2] = m.kind == DP_FLOW_ICMP_QUERY ? aport << 16 : (m.dport << 16) | aport;
+}
+
+// The checks between the allocation and the pair: a verdict that gives the
+// tuple back, or 0.
+__device__ __forceinline__ uint32_t masq_post(const dpf::PfReq &R, const MPlan &m, const uint32_t aip[4],
+                                              uint32_t aport) {
+  const uint32_t fam = (R.proto >> 8) & 0xffu;
+  if (!unicast(fam, aip)) return DP_DONE_FILTERED;
+  if (m.kind == DP_FLOW_TCP || m.kind == DP_FLOW_UDP) {
+    if (aport == 0) return DP_DONE_MALFORMED;  // InvalidPort
+  } else if (m.kind != DP_FLOW_ICMP_QUERY) {
+    return DP_DONE_NAT_FAILURE;  // UnexpectedKeyVariant
+  }
+  // get_reverse_mapping: the original source tuple
+  if (m.ikind != DP_FLOW_TCP && m.ikind != DP_FLOW_UDP && m.ikind != DP_FLOW_ICMP_QUERY)
+    return DP_DONE_NAT_FAILURE;  // IcmpUnsupportedCategory
+  dpf::FKey rk;
+  masq_rk(R, m, aip, aport, rk);
+  bool eq = true;
+  for (int j = 0; j < 11; j++) eq = eq && m.ik.w[j] == rk.w[j];
+  return eq ? (uint32_t)DP_DONE_INTERNAL_FAILURE : 0u;  // related_pair
+}
+
+__device__ __forceinline__ void masq_aip(const dpf::FlowCtx &fc, const dpf::PfReq &R, uint32_t rec, uint32_t aip[4]) {
+  const dpm::View V{fc.mq};
+  const dpm::A128 aa = dpm::addr_of(V, V.recs()[rec]);
+  const uint32_t fam = (R.proto >> 8) & 0xffu;
+  for (int j = 0; j < 4; j++) aip[j] = 0;  // big-endian words, v4 in word 0
+  if (fam == 4) aip[0] = aa.w[3];
+  else for (int j = 0; j < 4; j++) aip[j] = aa.w[j];
+}
+
+// create_flow_pair (nf.rs:265-325) for an allocation that passed masq_post.
+// false: refused at capacity (the allocation is the caller's to give back
+// when the forward flow was refused; R.mverdict set).
+__device__ __forceinline__ bool masq_pair(const Seq &q, dpf::PfReq &R, const MPlan &m, uint32_t rec,
+                                          uint32_t aport, const uint32_t aip[4], bool &give_back) {
+  const dpf::FlowCtx &fc = q.fc;
+  const uint32_t idx = R.idx;
+  const uint32_t fam = (R.proto >> 8) & 0xffu;
+  dpf::FKey rk;
+  masq_rk(R, m, aip, aport, rk);
+  const uint32_t rport = m.ik.w[2] >> 16;
+  const bool rident = m.ikind == DP_FLOW_ICMP_QUERY;
+  const bool ss = R.bits & dpf::kPqSnatSrc, sd = R.bits & dpf::kPqSnatDst;
+  const uint32_t fw_flags = DP_FLOW_INITIATOR | (ss ? DP_FLOW_REQ_STATIC_NAT_SRC : 0u) |
+                            (sd ? DP_FLOW_REQ_STATIC_NAT_DST : 0u);
+  const uint32_t rv_flags = (ss ? DP_FLOW_REQ_STATIC_NAT_DST : 0u) | (sd ? DP_FLOW_REQ_STATIC_NAT_SRC : 0u);
+  const dpm::View V{fc.mq};
+  const int64_t genid = V.h().genid;  // set_genid_pair(allocator.genid())
+  const uint64_t exp = fc.now + kMasqOneWayNs;
+  const uint32_t idle_s = (uint32_t)(V.sets()[m.set].idle_ns / 1000000000ull);
+  give_back = false;
+  const uint32_t sf = q.insert(m.ik, false, idx);
+  if (sf == dpf::kNoSlot) {  // the allocation drops here
+    give_back = true;
+    R.mverdict = DP_DONE_FLOW_CAPACITY_EXCEEDED;
+    return false;
+  }
+  dpf::FlowSlot &F = fc.slots[sf];
+  F.flags = fw_flags | dpf::kFlagMasq | (m.allow_null ? dpf::kFlagMasqIdent : 0u);
+  F.dst_vni = R.dst_vni;  // setup_flow_masquerade_state: the forward flow to dst_vpcd
+  F.genid = genid;
+  F.expires_at = exp;
+  F.pf = DP_PF_SRC_NAT | (aport << 16);  // NatFlowStatus::OneWay
+  F.pf_rule = idle_s;
+  for (int j = 0; j < 4; j++) F.pf_ip[j] = aip[j];
+  F.pf_fam = fam;
+  F.mq_rec = rec + 1;
+  F.mq_gen = fc.mq_gen;
+  const uint32_t sr = q.insert(rk, true, idx);  // admitted at capacity: its related flow is Active
+  if (sr == dpf::kNoSlot) {
+    q.invalidate(sf, idx);
+    R.mverdict = DP_DONE_FLOW_CAPACITY_EXCEEDED;
+    return false;
+  }
+  dpf::FlowSlot &Rv = fc.slots[sr];
+  Rv.flags = rv_flags | dpf::kFlagMasq | (rident ? dpf::kFlagMasqIdent : 0u);
+  Rv.dst_vni = R.src_vni;  // the reverse one to src_vpcd
+  Rv.genid = genid;
+  Rv.expires_at = exp;
+  Rv.pf = DP_PF_DST_NAT | (rport << 16);
+  Rv.pf_rule = idle_s;
+  for (int j = 0; j < 4; j++) Rv.pf_ip[j] = 0;
+  if (m.ifam == 4) Rv.pf_ip[0] = bswap(m.ik.w[3]);
+  else for (int j = 0; j < 4; j++) Rv.pf_ip[j] = bswap(m.ik.w[3 + j]);
+  Rv.pf_fam = m.ifam;
+  F.related = sr;
+  F.related_tag = Rv.state;
+  Rv.related = sf;
+  Rv.related_tag = F.state;
+  // the packet with the forward state (no Ethernet header: a failure that
+  // invalidates the new pair -- never here, every frame has one)
+  R.mnat = DP_PF_SRC_NAT | (m.allow_null ? 0x100u : 0u) | (aport << 16);
+  for (int j = 0; j < 4; j++) R.mnat_ip[j] = aip[j];
+  return true;
+}
+
 // Masquerade::masquerade_packet (nf.rs:384-475) for one record, after its
 // PortForwarder decision (the packet as PortForwarder left it).
 __device__ __forceinline__ void resolve_masq(const Seq &q, dpf::PfReq &R) {
@@ -3859,20 +4050,11 @@ __device__ __forceinline__ void resolve_masq(const Seq &q, dpf::PfReq &R) {
   const uint32_t idx = R.idx;
   const uint32_t fam = (R.proto >> 8) & 0xffu, proto = R.proto & 0xffu, tfl = R.proto >> 16;
   const bool tcp = R.bits & dpf::kPqTcp, udp = R.bits & dpf::kPqUdp, icmp = R.bits & dpf::kPqIcmp;
-  // the current addresses and ports: PortForwarder's translation applied
-  uint32_t src[4], dst[4];
-  uint32_t sport = R.ports >> 16, dport = R.ports & 0xffffu;
-  for (int j = 0; j < 4; j++) { src[j] = R.src[j]; dst[j] = R.dst[j]; }
-  if ((R.bits & dpf::kPqPf) && (R.nat & 0xffu)) {
-    const bool s = (R.nat & 0xffu) == DP_PF_SRC_NAT;
-    for (int j = 0; j < 4; j++) (s ? src : dst)[j] = R.nat_ip[j];
-    if (tcp || udp) (s ? sport : dport) = R.nat >> 16;
-  }
   // get_masquerade_state (nf.rs:198-213): the attached flow, still that fill,
   // Active for this packet (its own PortForwarder step included), with state
-  const bool same = R.slot != dpf::kNoSlot && q.alive(R.slot, R.state);
-  const bool valid = same && R.status0 == DP_FLOW_ACTIVE && q.pair_valid(R.slot, idx + 1);
-  if (valid && (fc.slots[R.slot].flags & dpf::kFlagMasq)) {
+  if (masq_valid(q, R)) {
+    uint32_t src[4], dst[4], sport, dport;
+    masq_cur(R, src, dst, sport, dport);
     dpf::FlowSlot &f = fc.slots[R.slot];
     const uint32_t act = f.pf & 0xffu, port = f.pf >> 16;
     const bool ident = f.flags & dpf::kFlagMasqIdent;
@@ -3898,118 +4080,18 @@ __device__ __forceinline__ void resolve_masq(const Seq &q, dpf::PfReq &R) {
     for (int j = 0; j < 4; j++) R.mnat_ip[j] = f.pf_ip[j];
     return;
   }
-  dpm::View V{fc.mq};
-  if (!fc.mq) { R.mverdict = DP_DONE_NAT_FAILURE; return; }  // NoAllocator
-  if (tcp && !((tfl & 2) && !(tfl & 0x3du))) { R.mverdict = DP_DONE_FILTERED; return; }  // TCP without SYN
-  // FlowKey::try_from(&Packet) (flow_key.rs:589-621): the current key
-  uint32_t kind;
-  if (tcp) kind = DP_FLOW_TCP;
-  else if (udp) kind = DP_FLOW_UDP;
-  else if (icmp) kind = (R.bits & dpf::kPqQuery) ? DP_FLOW_ICMP_QUERY : DP_FLOW_ICMP_OTHER;
-  else { R.mverdict = DP_DONE_MALFORMED; return; }  // FlowKeyError
-  const uint32_t cports = kind == DP_FLOW_ICMP_OTHER ? 0u : ((sport << 16) | dport);
-  dpf::FKey ck, ik;
-  ck.w[0] = R.src_vni;
-  ck.w[1] = fam | (kind << 8);
-  ck.w[2] = cports;
-  for (int j = 0; j < 4; j++) { ck.w[3 + j] = bswap(src[j]); ck.w[7 + j] = bswap(dst[j]); }
-  // the initial key: the one before static NAT, else the current one
-  if (R.bits & dpf::kPqIkey) for (int j = 0; j < 11; j++) ik.w[j] = R.ikey[j];
-  else ik = ck;
-  const uint32_t ifam = ik.w[1] & 0xffu, ikind = ik.w[1] >> 8;
-  const uint32_t iproto = ikind == DP_FLOW_TCP ? 6u : ikind == DP_FLOW_UDP ? 17u : ifam == 4 ? 1u : 58u;
-  // NatAllocator::allocate (apalloc/mod.rs:317-375): the pool of (protocol,
-  // VPCs, original source); a port, or an ICMP identifier (port 0 allowed)
-  dpm::A128 sip{};
-  if (ifam == 4) sip.w[3] = bswap(ik.w[3]);
-  else for (int j = 0; j < 4; j++) sip.w[j] = bswap(ik.w[3 + j]);
-  const uint32_t set = dpm::lookup(V, iproto | (ifam << 8), R.src_vni, R.dst_vni, sip);
-  if (set == dpm::kNone) { R.mverdict = DP_DONE_FILTERED; return; }  // Denied
+  MPlan m;
+  if (!masq_plan(fc, R, m)) return;
+  const dpm::View V{fc.mq};
   uint32_t rec = 0, aport = 0;
-  const bool allow_null = iproto == 1 || iproto == 58;
-  const uint32_t e = dpm::set_alloc(V, set, allow_null, rec, aport);
+  const uint32_t e = dpm::set_alloc(V, m.set, m.allow_null, rec, aport);
   if (e != dpm::OK) { R.mverdict = masq_done(e); return; }
-  const dpm::A128 aa = dpm::addr_of(V, V.recs()[rec]);
-  uint32_t aip[4] = {0, 0, 0, 0};  // big-endian words, v4 in word 0
-  if (fam == 4) aip[0] = aa.w[3];
-  else for (int j = 0; j < 4; j++) aip[j] = aa.w[j];
-  if (!unicast(fam, aip)) { dpm::release(V, rec, aport); R.mverdict = DP_DONE_FILTERED; return; }
-  // create_flow_pair (nf.rs:265-325): the reverse of the current key towards
-  // the allocated tuple (new_reverse_session, :327-373)
-  dpf::FKey rk;
-  rk.w[0] = R.dst_vni;
-  rk.w[1] = ck.w[1];
-  for (int j = 0; j < 4; j++) { rk.w[3 + j] = ck.w[7 + j]; rk.w[7 + j] = bswap(aip[j]); }
-  if (kind == DP_FLOW_TCP || kind == DP_FLOW_UDP) {
-    if (aport == 0) { dpm::release(V, rec, aport); R.mverdict = DP_DONE_MALFORMED; return; }  // InvalidPort
-    rk.w[2] = (dport << 16) | aport;
-  } else if (kind == DP_FLOW_ICMP_QUERY) {
-    rk.w[2] = aport << 16;
-  } else {
-    dpm::release(V, rec, aport);
-    R.mverdict = DP_DONE_NAT_FAILURE;  // UnexpectedKeyVariant
-    return;
-  }
-  // get_reverse_mapping: the original source tuple
-  if (ikind != DP_FLOW_TCP && ikind != DP_FLOW_UDP && ikind != DP_FLOW_ICMP_QUERY) {
-    dpm::release(V, rec, aport);
-    R.mverdict = DP_DONE_NAT_FAILURE;  // IcmpUnsupportedCategory
-    return;
-  }
-  const uint32_t rport = ik.w[2] >> 16;
-  const bool rident = ikind == DP_FLOW_ICMP_QUERY;
-  bool eq = true;
-  for (int j = 0; j < 11; j++) eq = eq && ik.w[j] == rk.w[j];
-  if (eq) { dpm::release(V, rec, aport); R.mverdict = DP_DONE_INTERNAL_FAILURE; return; }  // related_pair
-  const bool ss = R.bits & dpf::kPqSnatSrc, sd = R.bits & dpf::kPqSnatDst;
-  const uint32_t fw_flags = DP_FLOW_INITIATOR | (ss ? DP_FLOW_REQ_STATIC_NAT_SRC : 0u) |
-                            (sd ? DP_FLOW_REQ_STATIC_NAT_DST : 0u);
-  const uint32_t rv_flags = (ss ? DP_FLOW_REQ_STATIC_NAT_DST : 0u) | (sd ? DP_FLOW_REQ_STATIC_NAT_SRC : 0u);
-  const int64_t genid = V.h().genid;  // set_genid_pair(allocator.genid())
-  const uint64_t exp = fc.now + kMasqOneWayNs;
-  const uint32_t idle_s = (uint32_t)(V.sets()[set].idle_ns / 1000000000ull);
-  const uint32_t sf = q.insert(ik, false, idx);
-  if (sf == dpf::kNoSlot) {  // the allocation drops here
-    dpm::release(V, rec, aport);
-    R.mverdict = DP_DONE_FLOW_CAPACITY_EXCEEDED;
-    return;
-  }
-  dpf::FlowSlot &F = fc.slots[sf];
-  F.flags = fw_flags | dpf::kFlagMasq | (allow_null ? dpf::kFlagMasqIdent : 0u);
-  F.dst_vni = R.dst_vni;  // setup_flow_masquerade_state: the forward flow to dst_vpcd
-  F.genid = genid;
-  F.expires_at = exp;
-  F.pf = DP_PF_SRC_NAT | (aport << 16);  // NatFlowStatus::OneWay
-  F.pf_rule = idle_s;
-  for (int j = 0; j < 4; j++) F.pf_ip[j] = aip[j];
-  F.pf_fam = fam;
-  F.mq_rec = rec + 1;
-  F.mq_gen = fc.mq_gen;
-  const uint32_t sr = q.insert(rk, true, idx);  // admitted at capacity: its related flow is Active
-  if (sr == dpf::kNoSlot) {
-    q.invalidate(sf, idx);
-    R.mverdict = DP_DONE_FLOW_CAPACITY_EXCEEDED;
-    return;
-  }
-  dpf::FlowSlot &Rv = fc.slots[sr];
-  Rv.flags = rv_flags | dpf::kFlagMasq | (rident ? dpf::kFlagMasqIdent : 0u);
-  Rv.dst_vni = R.src_vni;  // the reverse one to src_vpcd
-  Rv.genid = genid;
-  Rv.expires_at = exp;
-  Rv.pf = DP_PF_DST_NAT | (rport << 16);
-  Rv.pf_rule = idle_s;
-  for (int j = 0; j < 4; j++) Rv.pf_ip[j] = 0;
-  if (ifam == 4) Rv.pf_ip[0] = bswap(ik.w[3]);
-  else for (int j = 0; j < 4; j++) Rv.pf_ip[j] = bswap(ik.w[3 + j]);
-  Rv.pf_fam = ifam;
-  F.related = sr;
-  F.related_tag = Rv.state;
-  Rv.related = sf;
-  Rv.related_tag = F.state;
-  // the packet with the forward state (no Ethernet header: a failure that
-  // invalidates the new pair -- never here, every frame has one)
-  R.mnat = DP_PF_SRC_NAT | (allow_null ? 0x100u : 0u) | (aport << 16);
-  for (int j = 0; j < 4; j++) R.mnat_ip[j] = aip[j];
+  uint32_t aip[4];
+  masq_aip(fc, R, rec, aip);
+  const uint32_t v = masq_post(R, m, aip, aport);
+  if (v) { dpm::release(V, rec, aport); R.mverdict = v; return; }
+  bool give_back;
+  if (!masq_pair(q, R, m, rec, aport, aip, give_back) && give_back) dpm::release(V, rec, aport);
 }
 
 // One record, in packet order: PortForwarder, then Masquerade on what it left.
@@ -4144,61 +4226,222 @@ __device__ uint32_t sort_conn(unsigned long long *nx, uint32_t list) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The masquerading burst, split (dp_nat_prep, dp_nat_resolve, dp_nat_lane)
+// ---------------------------------------------------------------------------
+// Masquerade couples a burst's records through one allocator only where a
+// record allocates, and the flows a record reads are its own connection's
+// except where an allocation's new pair replaces them.  So a masquerading
+// burst is run in two parts whose outcome is the one-lane pass's in packet
+// order:
+//  - connection lanes (dp_nat_resolve): the records attached to one flow pair
+//    that holds masquerade state with a live allocation, in packet order --
+//    refreshes of NatFlowStatus and expiry, closes and resets, the ACL's flow
+//    verdicts -- up to the first record that would allocate (its flow no
+//    longer valid); that record and the rest of the connection go to
+//  - the allocating lane (dp_nat_lane): every other masquerading record, in
+//    packet order: first packets, packets on flows without (valid) state,
+//    what the connection lanes left.  Its records are taken 64 at a time;
+//    runs of records that allocate are served by one allocator step for the
+//    whole wave (the k-th of them takes the k-th free port of the address's
+//    thread block, as one after the other would) and create their pairs in
+//    parallel; a record whose outcome rests on live flow state runs alone.
+// Why the parts commute: a connection lane's pair keeps its tuple allocated
+// for the whole burst (the forward flow owns it; a replaced fill gives it
+// back only when the burst ends), so no allocation of the burst hands it out
+// again, and a record whose initial key is the pair's key is attached to the
+// pair (FlowLookup found it) and so runs in the connection's order.  What
+// would break that is refused at dp_nat_prep: a port-forwarding record in the
+// burst, or a masquerading packet whose own peer could masquerade towards a
+// public address (masq_back: a reverse key allocated this burst could then be
+// another record's initial key); those bursts run on one lane.  The table's
+// capacity and 7/8 bound concern the allocating lane alone (the connection
+// lanes insert nothing): without room for every pair it could create, it
+// takes its records one by one.
+
+// The NAT pass's mode for this burst: 1 one lane in packet order, 2
+// connections in parallel (port forwarding: when no insert of the burst can
+// meet the capacity or the 7/8 bound), 3 split (masquerade: only the
+// allocating lane inserts, and it takes its records one by one in packet
+// order when room is short -- dp_nat_lane).
+__device__ __forceinline__ uint32_t nat_mode(const dpf::FlowCtx &fc) {
+  if (fc.force_seq == 1 || fc.pf_cnt[5]) return 1u;
+  if (fc.pf_cnt[8]) return fc.pf_cnt[9] || fc.pf_cnt[10] ? 1u : 3u;
+  const uint64_t len0 = ((uint64_t)fc.pf_cnt[7] << 32) | fc.pf_cnt[6];
+  const uint64_t total = fc.pf_cnt[1];
+  return len0 + 2ull * total > fc.capacity || len0 + 2ull * total > fc.hard ? 1u : 2u;
+}
+
+__device__ __forceinline__ void flag_once(uint32_t *w) {
+  if (!__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicOr(w, 1u);
+}
+
+// Could this record's packet be given a tuple (an expose covers its initial
+// source) while its initial destination is a public address of the
+// allocator?  Then its initial key may be the reverse key of a pair another
+// record creates this burst, and the allocating lane's order would matter
+// beyond it: the burst runs on one lane.
+__device__ bool masq_back(const dpf::FlowCtx &fc, const dpf::PfReq &R) {
+  if (!fc.mq) return false;
+  const dpm::View V{fc.mq};
+  dpf::FKey ik;
+  const uint32_t fam = (R.proto >> 8) & 0xffu;
+  const uint32_t kind = (R.bits & dpf::kPqTcp) ? DP_FLOW_TCP : (R.bits & dpf::kPqUdp) ? DP_FLOW_UDP : DP_FLOW_ICMP_QUERY;
+  if (R.bits & dpf::kPqIkey) {
+    for (int j = 0; j < 11; j++) ik.w[j] = R.ikey[j];
+  } else {
+    ik.w[1] = fam | (kind << 8);
+    for (int j = 0; j < 4; j++) { ik.w[3 + j] = bswap(R.src[j]); ik.w[7 + j] = bswap(R.dst[j]); }
+  }
+  const uint32_t ifam = ik.w[1] & 0xffu, ikind = ik.w[1] >> 8;
+  dpm::A128 d{};
+  if (ifam == 4) d.w[3] = bswap(ik.w[7]);
+  else for (int j = 0; j < 4; j++) d.w[j] = bswap(ik.w[7 + j]);
+  bool pub = false;
+  const dpm::Region *G = V.regions();
+  for (uint32_t k = 0; k < V.h().n_regions && !pub; k++)
+    pub = G[k].fam == ifam && dpm::a_cmp(G[k].start, d) <= 0 && dpm::a_cmp(d, G[k].last) <= 0;
+  if (!pub) return false;
+  const uint32_t iproto = ikind == DP_FLOW_TCP ? 6u : ikind == DP_FLOW_UDP ? 17u : ifam == 4 ? 1u : 58u;
+  dpm::A128 a{};
+  if (ifam == 4) a.w[3] = bswap(ik.w[3]);
+  else for (int j = 0; j < 4; j++) a.w[j] = bswap(ik.w[3 + j]);
+  return dpm::lookup(V, iproto | (ifam << 8), R.src_vni, R.dst_vni, a) != dpm::kNone;
+}
+
+// The masquerading record's connection: the lower slot of the flow pair it is
+// attached to (the pair's two flows name each other while both live); false:
+// no live attached flow (the record goes to the allocating lane).
+__device__ bool masq_conn(const dpf::FlowCtx &fc, const dpf::PfReq &R, uint32_t &key) {
+  if (R.slot > fc.mask || fc.slots[R.slot].state != R.state) return false;
+  const dpf::FlowSlot &A = fc.slots[R.slot];
+  key = R.slot;
+  if (A.related <= fc.mask && fc.slots[A.related].state == A.related_tag && A.related < key) key = A.related;
+  return true;
+}
+
+// A record for the allocating lane: its bit by packet index (dp_nat_lane_order)
+__device__ __forceinline__ void lane_mark(const dpf::FlowCtx &fc, dpf::PfReq &R, uint32_t more) {
+  R.bits |= dpf::kPqLane | more;
+  const uint32_t i = R.idx;
+  atomicOr(&fc.lane_bits[i >> 5], 1u << (i & 31));
+  uint32_t *sw = &fc.lane_sum[i >> 15];
+  const uint32_t sb = 1u << ((i >> 10) & 31);
+  if (!(__hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & sb)) atomicOr(sw, sb);
+}
+
+// Can a connection lane run this connection (the records of `list`)?  Every
+// record masquerades without port forwarding, is attached to one of the
+// pair's two flows (still the fills it attached) and was Active as the burst
+// started; the pair holds masquerade state (the forward flow SrcNat, the
+// reverse DstNat) and the forward flow owns a live allocation.
+__device__ bool masq_conn_ok(const Seq &q, uint32_t list) {
+  const dpf::FlowCtx &fc = q.fc;
+  if (!fc.mq) return false;
+  const uint32_t S = fc.pf[list].slot;
+  if (S > fc.mask) return false;
+  const dpf::FlowSlot &A = fc.slots[S];
+  if (!q.alive(A.related, A.related_tag)) return false;
+  const uint32_t T = A.related;
+  const dpf::FlowSlot &B = fc.slots[T];
+  if (B.related != S || !q.alive(S, B.related_tag)) return false;
+  if (!(A.flags & dpf::kFlagMasq) || !(B.flags & dpf::kFlagMasq)) return false;
+  const bool a_fw = (A.pf & 0xffu) == DP_PF_SRC_NAT;
+  const dpf::FlowSlot &F = a_fw ? A : B, &Rv = a_fw ? B : A;
+  if ((F.pf & 0xffu) != DP_PF_SRC_NAT || (Rv.pf & 0xffu) != DP_PF_DST_NAT) return false;
+  if (!F.mq_rec || F.mq_gen != fc.mq_gen) return false;
+  for (uint32_t r = list; r != dpf::kNoSlot; r = (uint32_t)link_ld(&fc.grp_next[r])) {
+    const dpf::PfReq &R = fc.pf[r];
+    if ((R.bits & (dpf::kPqMasq | dpf::kPqPf)) != dpf::kPqMasq) return false;
+    if ((R.slot != S && R.slot != T) || !q.alive(R.slot, R.state) || R.status0 != DP_FLOW_ACTIVE) return false;
+  }
+  return true;
+}
+
+// One masquerading connection on its lane (dp_nat_resolve, mode 3).
+__device__ void masq_conn_run(const Seq &q, uint32_t list) {
+  const dpf::FlowCtx &fc = q.fc;
+  bool lane = !masq_conn_ok(q, list);
+  for (uint32_t r = list; r != dpf::kNoSlot; r = (uint32_t)link_ld(&fc.grp_next[r])) {
+    dpf::PfReq &R = fc.pf[r];
+    if (lane) { lane_mark(fc, R, 0u); continue; }
+    R.mverdict = dpf::kPfForward;
+    resolve_pf(q, R);  // (no port forwarding here: the ACL's flow verdict only)
+    if (R.verdict != dpf::kPfForward) continue;
+    if (masq_valid(q, R)) { resolve_masq(q, R); continue; }
+    // the flow is no longer valid for it: it allocates, on the allocating lane
+    lane_mark(fc, R, dpf::kPqPfDone);
+    atomicAdd(&fc.pf_cnt[13], 1u);
+    lane = true;
+  }
+}
+
 }  // namespace pfw
 
 #if DP_IN_PART(0)
+// The packets a bitmap marks (by packet index, 1024 per summary bit) in
+// packet order, by one workgroup of 1024: a prefix sum over regions of 1024
+// packets; the bits are cleared for the next burst.  Returns the count.
+__device__ uint32_t order_bits(uint32_t *bits, uint32_t *sum, uint32_t n, uint32_t *order) {
+  const uint32_t t = threadIdx.x;
+  __shared__ uint32_t cnt[1024];
+  __shared__ uint32_t total;
+  if (t == 0) total = 0;
+  const uint32_t regions = (n + 1023) / 1024;
+  for (uint32_t r0 = 0; r0 < regions; r0 += 1024) {
+    __syncthreads();
+    const uint32_t r = r0 + t;
+    uint32_t c = 0;
+    const bool hit = r < regions && ((sum[r >> 5] >> (r & 31)) & 1u);
+    // the region's 32 words, loaded together and kept (the stores below
+    // may alias them for the compiler: reloading serialised 32 round trips)
+    uint32_t bw[32];
+#pragma unroll
+    for (int w = 0; w < 32; w++) bw[w] = hit ? bits[r * 32 + w] : 0u;
+#pragma unroll
+    for (int w = 0; w < 32; w++) c += __popc(bw[w]);
+    cnt[t] = c;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan
+      const uint32_t v = t >= o ? cnt[t - o] : 0u;
+      __syncthreads();
+      cnt[t] += v;
+      __syncthreads();
+    }
+    uint32_t pos = total + cnt[t] - c;
+    if (hit) {
+#pragma unroll
+      for (int w = 0; w < 32; w++) {
+        uint32_t b = bw[w];
+        if (b) bits[r * 32 + w] = 0;
+        while (b) {
+          const int k = __ffs(b) - 1;
+          b &= b - 1;
+          order[pos++] = r * 1024 + w * 32 + k;  // < n: only packets set bits
+        }
+      }
+    }
+    __syncthreads();
+    if (t == 1023) total += cnt[1023];
+  }
+  __syncthreads();
+  for (uint32_t w = t; w < (regions + 31) / 32; w += 1024) sum[w] = 0;
+  return total;
+}
+
 // dp_nat_prep: the records of the burst's NAT pass.  Workgroup 0 puts the
 // packets that reached PortForwarder / Masquerade in packet order (their
 // bitmap, scanned 1024 packets per summary bit; the bits are cleared for the
 // next burst) for the replay pass; every workgroup files each record under its
-// connection (pfw::conn_key) -- a hash slot claimed for this burst by CAS on
-// (burst, key), a list of its records pushed by CAS on (burst, last record).
+// connection -- port forwarding: pfw::conn_key; masquerade: the flow pair it is
+// attached to (pfw::masq_conn), or the allocating lane -- a hash slot claimed
+// for this burst by CAS on (burst, key), a list of its records pushed by CAS
+// on (burst, last record).
 __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ img_base,
                                                     const Image *__restrict__ im, dpf::FlowCtx fc) {
   const uint32_t t = threadIdx.x;
   if (blockIdx.x == 0) {
-    __shared__ uint32_t cnt[1024];
-    __shared__ uint32_t total;
-    if (t == 0) total = 0;
-    const uint32_t regions = (fc.n + 1023) / 1024;
-    for (uint32_t r0 = 0; r0 < regions; r0 += 1024) {
-      __syncthreads();
-      const uint32_t r = r0 + t;
-      uint32_t c = 0;
-      const bool hit = r < regions && ((fc.pf_sum[r >> 5] >> (r & 31)) & 1u);
-      // the region's 32 words, loaded together and kept (the stores below
-      // may alias them for the compiler: reloading serialised 32 round trips)
-      uint32_t bw[32];
-#pragma unroll
-      for (int w = 0; w < 32; w++) bw[w] = hit ? fc.pf_bits[r * 32 + w] : 0u;
-#pragma unroll
-      for (int w = 0; w < 32; w++) c += __popc(bw[w]);
-      cnt[t] = c;
-      __syncthreads();
-      for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan
-        const uint32_t v = t >= o ? cnt[t - o] : 0u;
-        __syncthreads();
-        cnt[t] += v;
-        __syncthreads();
-      }
-      uint32_t pos = total + cnt[t] - c;
-      if (hit) {
-#pragma unroll
-        for (int w = 0; w < 32; w++) {
-          uint32_t b = bw[w];
-          if (b) fc.pf_bits[r * 32 + w] = 0;
-          while (b) {
-            const int k = __ffs(b) - 1;
-            b &= b - 1;
-            fc.pf_order[pos++] = r * 1024 + w * 32 + k;  // < n: only packets set bits
-          }
-        }
-      }
-      __syncthreads();
-      if (t == 1023) total += cnt[1023];
-    }
-    __syncthreads();
-    for (uint32_t w = t; w < (regions + 31) / 32; w += 1024) fc.pf_sum[w] = 0;
+    const uint32_t total = order_bits(fc.pf_bits, fc.pf_sum, fc.n, fc.pf_order);
     if (t == 0) {
       fc.pf_cnt[1] = total;
       fc.pf_cnt[6] = fc.tmeta[2];  // the table length before the pass
@@ -4210,11 +4453,19 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
   const Img g{img_base, *im};
   const unsigned long long tag = (unsigned long long)fc.burst << 32;
   for (uint32_t rec = blockIdx.x * 1024 + t; rec < nrec; rec += gridDim.x * 1024) {
-    const dpf::PfReq &R = fc.pf[rec];
+    dpf::PfReq &R = fc.pf[rec];
     if (!(R.bits & dpf::kPqReached)) continue;  // a flow-filter record of a packet dropped before NAT
     uint32_t key;
-    if (!pfw::conn_key(g, fc, R, key)) {
-      if (!__hip_atomic_load(&fc.pf_cnt[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicOr(&fc.pf_cnt[5], 1u);
+    if (R.bits & dpf::kPqPf) pfw::flag_once(&fc.pf_cnt[9]);
+    if (R.bits & dpf::kPqMasq) {
+      pfw::flag_once(&fc.pf_cnt[8]);
+      if (pfw::masq_back(fc, R)) pfw::flag_once(&fc.pf_cnt[10]);
+      if (!pfw::masq_conn(fc, R, key)) {
+        pfw::lane_mark(fc, R, 0u);
+        continue;
+      }
+    } else if (!pfw::conn_key(g, fc, R, key)) {
+      pfw::flag_once(&fc.pf_cnt[5]);
       continue;
     }
     const unsigned long long want = tag | key;
@@ -4245,17 +4496,18 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
 // dp_nat_resolve: the reference's PortForwarder and Masquerade over the
 // records -- NatFlowStatus, expiries, invalidation marks and events, rule
 // revalidation, allocations, the inserts of new pairs -- leaving each
-// packet's decision in its record for the replay pass.  In parallel, one
-// lane per connection (its records in packet order), when no record needs
-// the sequential pass and no insert of the burst can meet the capacity or
-// the 7/8 bound (the admissions of insert_common,
+// packet's decision in its record for the replay pass.  Mode 2 (port
+// forwarding): one lane per connection (its records in packet order), when no
+// record needs the one-lane pass and no insert of the burst can meet the
+// capacity or the 7/8 bound (the admissions of insert_common,
 // flow-entry/src/flow_table/table.rs:215-260, then cannot depend on the
-// order of connections); else one lane over all records in packet order.
-// Two instantiations, one launch each: SEQ (one wave) runs the burst when
-// it needs the sequential pass, the other (the grid) when it does not; each
-// leaves at once otherwise.  Apart, each is compiled for its own mode: the
-// sequential lane's records inlined (no call frame to save and restore per
-// record), the parallel lanes at 6 waves per SIMD.
+// order of connections).  Mode 3 (masquerade): the connection lanes of the
+// split pass (above).  Mode 1: one lane over all records in packet order.
+// Two instantiations, one launch each: SEQ (one wave) runs mode 1, the other
+// (the grid) modes 2 and 3; each leaves at once otherwise.  Apart, each is
+// compiled for its own mode: the sequential lane's records inlined (no call
+// frame to save and restore per record), the parallel lanes at 6 waves per
+// SIMD.
 #ifndef DP_RESOLVE_WAVES
 #define DP_RESOLVE_WAVES 6
 #endif
@@ -4265,11 +4517,10 @@ dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ i
   const uint32_t total = fc.pf_cnt[1];
   if (!total) return;
   const Img g{img_base, *im};
-  const uint64_t len0 = ((uint64_t)fc.pf_cnt[7] << 32) | fc.pf_cnt[6];
-  const bool seq = fc.force_seq || fc.pf_cnt[5] || len0 + 2ull * total > fc.capacity ||
-                   len0 + 2ull * total > fc.hard;
-  if (seq != SEQ) return;
+  const uint32_t mode = pfw::nat_mode(fc);
+  if ((mode == 1) != SEQ) return;
   const uint32_t gt = blockIdx.x * 256 + threadIdx.x;
+  if (gt == 0) fc.pf_cnt[12] = mode;
   if constexpr (SEQ) {
     // one lane in packet order; the other 63 lanes of its wave run ahead,
     // loading what the next 64 records will read -- the record, its flow and
@@ -4321,6 +4572,10 @@ dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ i
 #else
     uint32_t r = pfw::sort_conn(fc.grp_next, (uint32_t)fc.grp_head[h]);
 #endif
+    if (mode == 3) {
+      pfw::masq_conn_run(q, r);
+      continue;
+    }
     for (; r != dpf::kNoSlot; r = (uint32_t)pfw::link_ld(&fc.grp_next[r])) {
 #ifdef DP_DEBUG_NAT
       fc.pf[r].mnat_ip[0] = e;
@@ -4334,6 +4589,250 @@ dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ i
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   if ((threadIdx.x & 63) == 0 && v)
     atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), (unsigned long long)v);
+}
+
+// dp_nat_lane_order: the allocating lane's records in packet order (every
+// burst: it clears the bits the connection lanes and dp_nat_prep set)
+__global__ void __launch_bounds__(1024) dp_nat_lane_order(dpf::FlowCtx fc) {
+  const uint32_t total = order_bits(fc.lane_bits, fc.lane_sum, fc.n, fc.lane_order);
+  if (threadIdx.x == 0) fc.pf_cnt[11] = total;
+}
+
+__device__ __forceinline__ void agent_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); }
+
+// dp_nat_lane: the split pass's allocating lane (mode 3), one wave over its
+// records in packet order, 64 at a time.  A record whose outcome rests on
+// live flow state (a valid flow with masquerade state, the ACL's flow
+// verdict) runs alone, as the one-lane pass runs it.  The others are decided
+// without one (masq_plan) or allocate; a run of them (cut before a record
+// whose initial key an earlier one of the run inserts) is served in packet
+// order: where the set's first region's first address with free ports has a
+// thread block with free ports, the next records of that set take its free
+// ports in order in one step (PortAllocator::allocate_port, port_alloc.rs:
+// 264-284, record after record: a record whose checks fail gives its port
+// back at once, so it takes none), else one record allocates alone (a new
+// block, address or region); then the run's pairs are created in parallel.
+__global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ img_base,
+                                                  const Image *__restrict__ im, dpf::FlowCtx fc) {
+  if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3) return;
+  const uint32_t nl = fc.pf_cnt[11];
+  const int t = threadIdx.x;
+  // room for every pair the lane could create (the connection lanes insert
+  // nothing): else each record alone, so insert_common's admissions fall in
+  // packet order
+  const uint64_t len0 = ((uint64_t)fc.tmeta[3] << 32) | fc.tmeta[2];
+  const bool room = len0 + 2ull * nl <= fc.capacity && len0 + 2ull * nl <= fc.hard;
+  const Img g{img_base, *im};
+  const pfw::Seq qs{fc, g, false}, qp{fc, g, true};
+  const dpm::View V{fc.mq};
+  __shared__ uint32_t s_ik[64][12];  // the run's initial keys (+ hash)
+  __shared__ int s_pd[64];           // the lane's latest earlier lane with the same initial key
+  __shared__ uint32_t s_bm[8];       // the thread block's usage bitmap
+  __shared__ uint32_t s_b[8];        // (fast, address record, block, free ports, address words)
+  uint32_t fast_n = 0, lone_n = 0;
+  for (uint32_t k0 = 0; k0 < nl; k0 += 64) {
+    const uint32_t cnt = nl - k0 < 64 ? nl - k0 : 64;
+    const bool has = (uint32_t)t < cnt;
+    const uint32_t ri = has ? fc.pf_of[fc.lane_order[k0 + t]] : 0u;
+    dpf::PfReq &R = fc.pf[ri];
+    // 1 alone, 2 decided, 3 allocates
+    uint32_t cls = 0;
+    pfw::MPlan m;
+    if (has) {
+      const bool pfdone = R.bits & dpf::kPqPfDone;
+      if (!room || (!pfdone && (R.bits & dpf::kPqSens)) || pfw::masq_valid(qs, R)) {
+        cls = 1;
+      } else {
+        R.mverdict = dpf::kPfForward;
+        if (!pfdone) { R.verdict = dpf::kPfForward; R.acl_over = 0; }
+        cls = pfw::masq_plan(fc, R, m) ? 3u : 2u;
+      }
+    }
+    if (cls == 3) {
+      for (int j = 0; j < 11; j++) s_ik[t][j] = m.ik.w[j];
+      s_ik[t][11] = dpf::fkey_hash(m.ik);
+    }
+    __syncthreads();
+    const uint64_t c1 = __ballot(cls == 1), c3 = __ballot(cls == 3);
+    {
+      int pd = -1;
+      if (cls == 3)
+        for (int q = t - 1; q >= 0 && pd < 0; q--) {
+          if (!((c3 >> q) & 1) || s_ik[q][11] != s_ik[t][11]) continue;
+          bool eq = true;
+          for (int j = 0; j < 11; j++) eq = eq && s_ik[q][j] == s_ik[t][j];
+          if (eq) pd = q;
+        }
+      s_pd[t] = pd;
+    }
+    __syncthreads();
+    // the lane's allocation: ok (a pair to create), else its verdict is set
+    bool ok = false, done = cls != 3;
+    uint32_t rec = 0, aport = 0, aip[4] = {0, 0, 0, 0};
+    uint32_t i = 0;
+    while (i < cnt) {
+      if ((c1 >> i) & 1) {
+        if (t == (int)i) {
+          if (R.bits & dpf::kPqPfDone) {
+            R.mverdict = dpf::kPfForward;
+            pfw::resolve_masq(qs, R);
+          } else {
+            pfw::resolve_one(qs, R);
+          }
+        }
+        agent_fence();
+        i++;
+        continue;
+      }
+      uint32_t j = i + 1;
+      while (j < cnt && !((c1 >> j) & 1) && !(((c3 >> j) & 1) && s_pd[j] >= (int)i)) j++;
+      const uint64_t run = (j == 64 ? ~0ull : ((1ull << j) - 1)) & ~((1ull << i) - 1);
+      // the run's allocations, in packet order
+      for (;;) {
+        const uint64_t pend = __ballot(!done) & c3 & run;
+        if (!pend) break;
+        const int p = __ffsll((long long)pend) - 1;
+        const uint32_t set_p = (uint32_t)__shfl((int)m.set, p);
+        if (t == p) {
+          // the set's first region: its first address in use with free ports
+          // and that address's thread block
+          uint32_t f = 0;
+          if (fc.force_seq != 2) {
+            const dpm::Set &S = V.sets()[set_p];
+            const dpm::Region &G = V.regions()[V.setreg()[S.first_reg]];
+            uint32_t a = dpm::kNone;
+            for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
+              if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
+            if (a != dpm::kNone && V.recs()[a].thread_block >= 0) {
+              const dpm::Addr &A = V.recs()[a];
+              const uint32_t tb = (uint32_t)A.thread_block;
+              if ((A.bflag[tb] & 2) && tb != 0) {
+                uint32_t fr = 0;
+                for (int k = 0; k < 8; k++) { s_bm[k] = A.bm[tb][k]; fr += __popc(~A.bm[tb][k]); }
+                const dpm::A128 aa = dpm::addr_of(V, A);
+                uint32_t w[4] = {0, 0, 0, 0};
+                if (G.fam == 4) w[0] = aa.w[3];
+                else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
+                if (fr && pfw::unicast(G.fam, w)) {
+                  f = 1;
+                  s_b[1] = a; s_b[2] = tb; s_b[3] = fr;
+                  for (int k = 0; k < 4; k++) s_b[4 + k] = w[k];
+                }
+              }
+            }
+          }
+          s_b[0] = f;
+        }
+        __syncthreads();
+        // (a first record that could meet related_pair at this address allocates alone)
+        bool p_eq = false;
+        if (t == p && s_b[0]) {
+          p_eq = m.eqp;
+          for (int k = 0; k < 4; k++) p_eq = p_eq && m.ik.w[7 + k] == pfw::bswap(s_b[4 + k]);
+        }
+        if (s_b[0] && !((__ballot(p_eq) >> p) & 1)) {
+          // the records from p on asking the same set, up to one whose
+          // reverse key could equal its initial key (related_pair) at this
+          // address: served while the block has free ports
+          const uint32_t a = s_b[1], tb = s_b[2], fr = s_b[3];
+          uint32_t w[4];
+          for (int k = 0; k < 4; k++) w[k] = s_b[4 + k];
+          bool stop = false;
+          if (!done && ((pend >> t) & 1)) {
+            bool eqa = m.eqp;
+            for (int k = 0; k < 4; k++) eqa = eqa && m.ik.w[7 + k] == pfw::bswap(w[k]);
+            stop = m.set != set_p || eqa;
+          }
+          const uint64_t st = __ballot(stop) & pend;
+          const uint64_t grp = st ? pend & ((1ull << (__ffsll((long long)st) - 1)) - 1) : pend;
+          const bool mine = (grp >> t) & 1;
+          const uint64_t cons = __ballot(mine && !m.sfail) & grp;
+          const uint32_t before = (uint32_t)__popcll(cons & lanes_below(t));
+          const bool served = mine && before < fr;
+          const uint32_t taken = (uint32_t)__popcll(cons) < fr ? (uint32_t)__popcll(cons) : fr;
+          if (served) {
+            if (m.sfail) {
+              R.mverdict = m.sfail;
+            } else {
+              // the before-th free port of the block
+              uint32_t k = before, port = 0;
+              for (int x = 0; x < 8; x++) {
+                const uint32_t fw = ~s_bm[x];
+                const uint32_t c = (uint32_t)__popc(fw);
+                if (k < c) {
+                  uint32_t b = fw;
+                  for (uint32_t y = 0; y < k; y++) b &= b - 1;
+                  port = 32 * x + (uint32_t)__ffs(b) - 1;
+                  break;
+                }
+                k -= c;
+              }
+              rec = a;
+              aport = (tb << 8) + port;
+              for (int x = 0; x < 4; x++) aip[x] = w[x];
+              ok = true;
+            }
+            done = true;
+          }
+          __syncthreads();
+          if (t == p) {
+            // the block's bitmap after `taken` allocations: its lowest free ports
+            dpm::Addr &A = V.recs()[a];
+            uint32_t left = taken;
+            for (int x = 0; x < 8 && left; x++)
+              while (left && ~A.bm[tb][x]) {
+                A.bm[tb][x] |= 1u << (__ffs(~A.bm[tb][x]) - 1);
+                left--;
+              }
+            A.blive[tb] = (uint16_t)(A.blive[tb] + taken);
+            if (dpm::bm_full(A.bm[tb])) A.nonfull--;
+            fast_n += taken;
+          }
+        } else if (t == p) {
+          // alone: as resolve_masq allocates
+          const uint32_t e = dpm::set_alloc(V, m.set, m.allow_null, rec, aport);
+          if (e != dpm::OK) {
+            R.mverdict = pfw::masq_done(e);
+          } else {
+            pfw::masq_aip(fc, R, rec, aip);
+            const uint32_t v = pfw::masq_post(R, m, aip, aport);
+            if (v) { dpm::release(V, rec, aport); R.mverdict = v; }
+            else ok = true;
+          }
+          done = true;
+          lone_n++;
+        }
+        agent_fence();
+        __syncthreads();
+      }
+      // the run's pairs, in parallel (distinct initial keys; distinct tuples)
+      bool give_back = false;
+      if (ok && ((run >> t) & 1)) {
+        if (!pfw::masq_pair(qp, R, m, rec, aport, aip, give_back)) atomicAdd(&fc.pf_cnt[16], 1u);
+        ok = false;
+      }
+      agent_fence();
+      for (uint64_t gb = __ballot(give_back); gb; gb &= gb - 1) {
+        if (t == __ffsll((long long)gb) - 1) dpm::release(V, rec, aport);
+        agent_fence();
+      }
+      i = j;
+    }
+  }
+  if (t == 0) {
+    // the flows replaced during the burst are dropped after it, with the
+    // allocations their masquerade state owns
+    for (uint32_t k = 0; k < fc.pf_cnt[3]; k++) dpm::release(V, fc.mq_rel[2 * k], fc.mq_rel[2 * k + 1]);
+  }
+  uint32_t ln = lone_n, fn = fast_n;
+  for (int o = 32; o > 0; o >>= 1) { ln += __shfl_xor(ln, o); fn += __shfl_xor(fn, o); }
+  if (t == 0) fc.pf_cnt[14] += fn;
+  uint32_t v = qp.added;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (t == 0) {
+    fc.pf_cnt[15] += ln;
+    if (v) atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), (unsigned long long)v);
+  }
 }
 
 // dp_acl_classify: AclFilter's classification alone (dpgpu.h "The ACL
@@ -4740,7 +5239,7 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   dpf::FlowCtx fc = *reinterpret_cast<const dpf::FlowCtx *>(fc_host);
   if (hipMemsetAsync(fc.events, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
   if (hipMemsetAsync(fc.sens, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
-  if (hipMemsetAsync(fc.pf_cnt, 0, sizeof(uint32_t) * 8, stream) != hipSuccess) return -5;
+  if (hipMemsetAsync(fc.pf_cnt, 0, sizeof(uint32_t) * DPF_CNT_WORDS, stream) != hipSuccess) return -5;
   const Image *im = reinterpret_cast<const Image *>(image_dev);
   uint32_t blocks = (n + TPB - 1) / TPB;
   unsigned long long *part = stats ? reinterpret_cast<unsigned long long *>(stats_part) : nullptr;
@@ -4765,6 +5264,9 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
   hipLaunchKernelGGL(dp_nat_resolve<true>, dim3(1), dim3(64), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_resolve<false>, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
+  // a masquerading burst's allocating lane (its records in packet order)
+  hipLaunchKernelGGL(dp_nat_lane_order, dim3(1), dim3(1024), 0, stream, fc);
+  hipLaunchKernelGGL(dp_nat_lane, dim3(1), dim3(64), 0, stream, img_base, im, fc);
   fc.replay = 1;
   if (meta) dpk_run_pipeline_111(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   else dpk_run_pipeline_101(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);

@@ -223,7 +223,7 @@ struct dp_ctx {
   FlowScratch fl_ev, fl_sens;
   // port forwarding scratch (dpf::FlowCtx pf*): records, counters, packet ->
   // record, bitmaps (kept zero between bursts), order, replaced fills
-  FlowScratch pf_req, pf_cnt, pf_of, pf_bits, pf_order, pf_repl, mq_rel;
+  FlowScratch pf_req, pf_cnt, pf_of, pf_bits, pf_order, pf_repl, mq_rel, lane_order;
   // the NAT pass's connection tables and the keyed index of replaced fills:
   // entries carry the burst's tag, so they are zeroed only when allocated
   FlowScratch grp_tab, grp_head, grp_next, grp_list, repl;
@@ -485,6 +485,7 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   c->fl_ev.release();
   c->fl_sens.release();
   for (FlowScratch *x : {&c->pf_req, &c->pf_cnt, &c->pf_of, &c->pf_bits, &c->pf_order, &c->pf_repl, &c->mq_rel,
+                         &c->lane_order,
                          &c->grp_tab, &c->grp_head, &c->grp_next, &c->grp_list, &c->repl})
     x->release();
   if (c->ft) {
@@ -635,7 +636,7 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     // whole regions; the summary words sit after them
     const uint64_t words = ((uint64_t)n + 1023) / 1024 * 32, sum_words = ((uint64_t)n + 32767) / 32768;
     fc.pf = static_cast<dpf::PfReq *>(c->pf_req.get(sizeof(dpf::PfReq) * (uint64_t)n));
-    fc.pf_cnt = static_cast<uint32_t *>(c->pf_cnt.get(sizeof(uint32_t) * 8));
+    fc.pf_cnt = static_cast<uint32_t *>(c->pf_cnt.get(sizeof(uint32_t) * DPF_CNT_WORDS));
     fc.pf_of = static_cast<uint32_t *>(c->pf_of.get(sizeof(uint32_t) * (uint64_t)n));
     fc.pf_order = static_cast<uint32_t *>(c->pf_order.get(sizeof(uint32_t) * (uint64_t)n));
     fc.pf_repl = static_cast<uint32_t *>(c->pf_repl.get(sizeof(uint32_t) * 8 * ((uint64_t)n + 1)));
@@ -684,16 +685,22 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.lean = !ft->snat_seen && !img->im.v6w_c && !img->im.v6w_fib && img->im.ctx_bytes &&
               !g_flows_full.load(std::memory_order_relaxed);
     g_last_lean.store(fc.lean, std::memory_order_relaxed);
+    // (two bitmaps: the packets that reached the NAT stages, then the
+    // masquerading burst's allocating lane, dp_nat_lane_order)
     if (words + sum_words > c->pf_bits_n) {
       c->pf_bits.release();
       c->pf_bits_n = 0;
-      void *b = c->pf_bits.get(sizeof(uint32_t) * (words + sum_words));
-      if (b && hipMemsetAsync(b, 0, sizeof(uint32_t) * (words + sum_words), s) == hipSuccess)
+      void *b = c->pf_bits.get(2 * sizeof(uint32_t) * (words + sum_words));
+      if (b && hipMemsetAsync(b, 0, 2 * sizeof(uint32_t) * (words + sum_words), s) == hipSuccess)
         c->pf_bits_n = words + sum_words;
     }
     fc.pf_bits = static_cast<uint32_t *>(c->pf_bits.p);
     fc.pf_sum = fc.pf_bits ? fc.pf_bits + words : nullptr;
+    fc.lane_bits = fc.pf_bits ? fc.pf_bits + words + sum_words : nullptr;
+    fc.lane_sum = fc.lane_bits ? fc.lane_bits + words : nullptr;
+    fc.lane_order = static_cast<uint32_t *>(c->lane_order.get(sizeof(uint32_t) * ((uint64_t)n + 1)));
     if (!fc.events || !fc.sens || !fc.pf || !fc.pf_cnt || !fc.pf_of || !fc.pf_order || !fc.pf_repl || !fc.mq_rel ||
+        !fc.lane_order ||
         !fc.grp_tab || !fc.grp_head || !fc.grp_next || !fc.grp_list || !fc.repl ||
         c->pf_bits_n < words + sum_words) {
       (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
@@ -799,8 +806,23 @@ int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
 }
 
 // Test hook (not part of dpgpu.h): 1 runs every burst's NAT pass on one lane
-// in packet order (the parallel pass's reference in the parity tests and A/Bs).
-void dpf_debug_nat_sequential(int on) { g_nat_seq.store(on ? 1u : 0u, std::memory_order_relaxed); }
+// in packet order (the parallel pass's reference in the parity tests and A/Bs);
+// 2 runs masquerading bursts' split pass with every allocation on the
+// allocating lane alone (no wave batches).
+void dpf_debug_nat_sequential(int on) {
+  g_nat_seq.store(on == 1 || on == 2 ? (uint32_t)on : 0u, std::memory_order_relaxed);
+}
+// Test hook (not part of dpgpu.h): the context's last flows burst's NAT-pass
+// counters (dp_flow.h FlowCtx::pf_cnt: the mode that ran, the split pass's
+// lane records and allocations), up to `n` words.
+int dpf_debug_nat_counters(dp_ctx_t *c, uint32_t *out, uint32_t n) {
+  if (!c || !out) return DP_EINVAL;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (!c->pf_cnt.p) return DP_EINVAL;
+  if (n > DPF_CNT_WORDS) n = DPF_CNT_WORDS;
+  return hipMemcpy(out, c->pf_cnt.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : DP_EIO;
+}
 // Test hook (not part of dpgpu.h): 1 runs every flows burst through the full
 // flows variant (stateful NAT compiled in) even where the lean one serves.
 void dpf_debug_flows_full(int on) { g_flows_full.store(on ? 1u : 0u, std::memory_order_relaxed); }

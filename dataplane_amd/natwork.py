@@ -69,9 +69,131 @@ def masq_tables(genid: int = 1) -> TB:
     return t
 
 
+def masq_world(genid: int = 1) -> TB:
+    """masq_tables with the way back: VPC 200's answers to the public pool
+    (203.0.113.0/24, gated on VPC 100, requiring masquerade) reach VPC 100's
+    clients -- the reference's lowering of a masquerading peering's return
+    direction (flow-filter/src/context/tables.rs:583-662)."""
+    t = masq_tables(genid)
+    t.add_ff_remote(VPC_S, "203.0.113.0/24", VPC_C, NAT_MASQUERADE, gate_vni=VPC_C)
+    t.add_ff_local(VPC_S, VPC_C, "198.18.0.0/15")
+    return t
+
+
 def _ip(a: np.ndarray) -> np.ndarray:
     """u32 addresses -> (n, 4) big-endian bytes"""
     return a.astype(">u4").view(np.uint8).reshape(-1, 4)
+
+
+def frames(src, dst, sport, dport, vni):
+    """(buf, inp): 64-byte Ethernet / IPv4 / UDP frames in SLOT-byte slots,
+    one per row of the u32 / u16 arrays, arriving in VPC `vni` (per packet)."""
+    n = len(src)
+    fr = np.zeros((n, FRAME), dtype=np.uint8)
+    mac = lambda s: np.frombuffer(bytes(int(x, 16) for x in s.split(":")), np.uint8)
+    fr[:, 0:6] = mac(IF_MAC)
+    fr[:, 6:12] = mac(PEER_MAC)
+    fr[:, 12:14] = (0x08, 0x00)
+    ip = fr[:, 14:34]
+    ip[:, 0] = 0x45
+    ip[:, 2:4] = np.array([0, FRAME - 14], np.uint8)
+    ip[:, 8] = 64
+    ip[:, 9] = 17
+    ip[:, 12:16] = _ip(np.asarray(src, np.uint32))
+    ip[:, 16:20] = _ip(np.asarray(dst, np.uint32))
+    words = ip.reshape(n, 10, 2).astype(np.uint32)
+    s = (words[:, :, 0] << 8 | words[:, :, 1]).sum(axis=1)
+    s = (s & 0xffff) + (s >> 16)
+    s = (s & 0xffff) + (s >> 16)
+    ck = (~s & 0xffff).astype(np.uint16)
+    ip[:, 10] = ck >> 8
+    ip[:, 11] = ck & 0xff
+    udp = fr[:, 34:42]
+    udp[:, 0:2] = np.asarray(sport, np.uint16).astype(">u2").view(np.uint8).reshape(-1, 2)
+    udp[:, 2:4] = np.asarray(dport, np.uint16).astype(">u2").view(np.uint8).reshape(-1, 2)
+    udp[:, 4:6] = np.array([0, FRAME - 34], np.uint8)  # checksum 0: none (IPv4)
+    head = SLOT - FRAME
+    buf = np.zeros(n * SLOT + 64, dtype=np.uint8)
+    buf[: n * SLOT].reshape(n, SLOT)[:, head:] = fr
+    inp = np.zeros(n, dtype=A.PKT_IN)
+    inp["off"] = np.arange(n, dtype=np.uint32) * SLOT + head
+    inp["len"] = FRAME
+    inp["flags"] = A.IN_SEEDED_OVERLAY
+    inp["iif"] = 1
+    inp["src_vni"] = vni
+    return buf, inp
+
+
+class MasqConns:
+    """`e` masqueraded UDP connections of masq_world (VPC 100 clients in
+    10.250.0.0/16 to VPC 200 servers in 198.18.0.0/15) for the masquerade-heavy
+    bursts: their first packets (every one allocates a tuple), then bursts in
+    which nearly every packet belongs to one of them -- the client's packets
+    and the server's answers to the public tuple -- beside a share of new
+    connections."""
+
+    def __init__(self, e: int, seed: int = 7):
+        rng = np.random.default_rng(seed)
+        idx = np.arange(e, dtype=np.uint64)
+        self.e = e
+        self.src = (np.uint64(10 << 24 | 250 << 16) + (idx >> np.uint64(6))).astype(np.uint32)
+        self.sport = (1024 + (idx & np.uint64(63)) * 900 + np.uint64(7)).astype(np.uint16)
+        self.dst = (np.uint32(198 << 24 | 18 << 16) + rng.integers(1, 1 << 17, e).astype(np.uint32))
+        dp = rng.integers(1000, 65535, e)
+        self.dport = np.where(np.isin(dp, (53, 853, 8853)), dp + 1, dp).astype(np.uint16)
+        self.pub = np.zeros(e, np.uint32)    # the public tuple each was given (learn)
+        self.pport = np.zeros(e, np.uint16)
+
+    def first(self):
+        """(buf, inp): every connection's first packet, in order."""
+        return frames(self.src, self.dst, self.sport, self.dport, VPC_C)
+
+    def learn(self, buf: np.ndarray, out: np.ndarray) -> int:
+        """The public tuples from the delivered first packets; returns how many."""
+        ok = out["done"] == A.DONE["Delivered"]
+        k = np.nonzero(ok)[0]
+        off = out["off"][k].astype(np.int64)
+        b = lambda o: buf[off + o].astype(np.uint32)
+        self.pub[k] = (b(26) << 24) | (b(27) << 16) | (b(28) << 8) | b(29)
+        self.pport[k] = ((b(34) << 8) | b(35)).astype(np.uint16)
+        return len(k)
+
+    def keys(self):
+        """Each connection's forward flow key (FlowKey, dp_flow_key_t)."""
+        k = np.zeros(self.e, A.FLOW_KEY)
+        k["src_vni"], k["family"], k["kind"] = VPC_C, 4, A.FLOW_UDP
+        k["sport"], k["dport"] = self.sport, self.dport
+        k["src"][:, :4] = _ip(self.src)
+        k["dst"][:, :4] = _ip(self.dst)
+        return k
+
+    def burst(self, n: int, new_share: float, fwd_share: float, step: int, seed: int = 1):
+        """(buf, inp, n_new): n packets in random order -- a share of them first
+        packets of new connections (distinct clients 10.<step>.x.y), the rest
+        on the learnt connections, the client's (fwd_share) or the server's."""
+        rng = np.random.default_rng(seed * 7919 + step)
+        nn = int(round(n * new_share))
+        ne = n - nn
+        c = rng.integers(0, self.e, ne)
+        fwd = (rng.random(ne) < fwd_share) | (self.pport[c] == 0)  # answers only where a tuple was learnt
+        src = np.where(fwd, self.src[c], self.dst[c])
+        dst = np.where(fwd, self.dst[c], self.pub[c])
+        sp = np.where(fwd, self.sport[c], self.dport[c])
+        dpt = np.where(fwd, self.dport[c], self.pport[c])
+        vni = np.where(fwd, VPC_C, VPC_S)
+        j = np.arange(nn, dtype=np.uint64)
+        nsrc = (np.uint64(10 << 24) + np.uint64((step % 200) << 16) + (j >> np.uint64(6))).astype(np.uint32)
+        nsp = (1024 + (j & np.uint64(63)) * 900 + np.uint64(step % 900)).astype(np.uint16)
+        ndst = (np.uint32(198 << 24 | 18 << 16) + rng.integers(1, 1 << 17, nn).astype(np.uint32))
+        ndp = rng.integers(1000, 50000, nn).astype(np.uint16)
+        allsrc = np.concatenate([src, nsrc]).astype(np.uint32)
+        alldst = np.concatenate([dst, ndst]).astype(np.uint32)
+        allsp = np.concatenate([sp, nsp]).astype(np.uint16)
+        alldp = np.concatenate([dpt, ndp]).astype(np.uint16)
+        allvni = np.concatenate([vni, np.full(nn, VPC_C)]).astype(np.uint32)
+        perm = rng.permutation(len(allsrc))
+        buf, inp = frames(allsrc[perm], alldst[perm], allsp[perm], alldp[perm], allvni[perm])
+        return buf, inp, nn
 
 
 def burst(n: int, pf_share: float, step: int, seed: int = 1, kind: str = "pf"):

@@ -314,6 +314,17 @@ class GpuRunner:
     def lookup(self, keys):
         return self.ft.lookup(keys)
 
+    def nat_counters(self):
+        """The last burst's NAT-pass counters (dp_flow.h FlowCtx::pf_cnt):
+        [12] the mode that ran (1 one lane, 2 connections, 3 split), [11]
+        records on the allocating lane, [13] left there by connection lanes,
+        [14] allocations in wave batches, [15] alone, [16] pairs refused."""
+        import ctypes as C
+        out = (C.c_uint32 * 24)()
+        n = A.gpu_lib().dpf_debug_nat_counters(self.nf.ctx, out, 24)
+        assert n == 24, n
+        return np.array(out[:], dtype=np.uint32)
+
     def close(self):
         self.nf.attach_flows(None)
         self.nf.close()

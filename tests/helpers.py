@@ -41,6 +41,28 @@ def compare(out_ref, buf_ref, out_dut, buf_dut, inp, label=""):
                              f"(packet {owner}: {out_ref[owner]} / {out_dut[owner]})")
 
 
+def compare_bulk(out_ref, buf_ref, out_dut, buf_dut, inp, label=""):
+    """compare() for large bursts, vectorised: every dp_pkt_out_t field, and
+    the whole buffer outside the slots of dropped packets (which holds every
+    byte of every delivered frame)."""
+    a, b = common_fields(out_ref, out_dut)
+    mism = np.nonzero(a != b)[0]
+    assert len(mism) == 0, f"{label}: {len(mism)} records differ, first pkt {mism[0]}: {a[mism[0]]} vs {b[mism[0]]}"
+    diff = buf_ref != buf_dut
+    dropped = np.nonzero(out_ref["done"] != A.DONE["Delivered"])[0]
+    if len(dropped):
+        mark = np.zeros(len(diff) + 1, np.int32)
+        s = (inp["off"][dropped].astype(np.int64) - A.HEADROOM).clip(0)
+        e = inp["off"][dropped].astype(np.int64) + inp["len"][dropped].astype(np.int64)
+        np.add.at(mark, s, 1)
+        np.add.at(mark, e, -1)
+        diff &= np.cumsum(mark)[:-1] == 0
+    if diff.any():
+        d = np.nonzero(diff)[0]
+        owner = int(np.searchsorted(inp["off"].astype(np.int64) - A.HEADROOM, d[0], "right")) - 1
+        raise AssertionError(f"{label}: buffers differ at {d[:8]} (packet {owner}: {out_ref[owner]} / {out_dut[owner]})")
+
+
 def common_fields(a, b):
     """Both record arrays projected onto the fields they share (a device run
     without a meta array yields dp_pkt_out_t alone).  flow_ref is left out:

@@ -54,24 +54,38 @@ def test_gpu_masquerade_kat(s):
             same_info(io, ig, f"step {i}")
 
 
+NAT_MODES = {"split": 0, "one-lane": 1, "split-alone": 2}
+
+
+@pytest.mark.parametrize("nat", list(NAT_MODES))
 @pytest.mark.parametrize("seed,n_conn,capacity", [(1, 600, None), (2, 3000, None), (3, 800, 500)])
-def test_gpu_masquerade_random_bursts(seed, n_conn, capacity):
+def test_gpu_masquerade_random_bursts(seed, n_conn, capacity, nat):
     """Seeded bursts (tests/masqgen.py): allocations from a shared, claimed
     public range until it runs out, repeats, replies, TCP handshakes /
     teardowns / resets, DNS answers, ICMP echo, uncovered sources, sweeps that
     return tuples, a same-config republish, a narrowed config and none -- and,
-    with a small capacity, pairs refused at capacity; GPU == oracle per burst."""
+    with a small capacity, pairs refused at capacity; GPU == oracle per burst.
+    nat: the masquerading bursts' split pass (connection lanes + the
+    allocating lane with wave batches), the same with every allocation alone,
+    or the one-lane pass (the test hook dpf_debug_nat_sequential)."""
     import masqgen
     from golden.masqkat import GpuRunner, OracleRunner
-    got = {}
+    got, modes = {}, []
     for name, mk in (("oracle", OracleRunner), ("gpu", GpuRunner)):
         r = mk(slots=1 << 15) if name == "gpu" else mk()
         steps = []
+
+        def on(k, res, buf, infos, look, rel, pkts):
+            steps.append((res.copy(), buf.copy(), infos.copy(), look.copy(), rel.copy(), r.count()))
+            if name == "gpu":
+                modes.append(r.nat_counters())
+        if name == "gpu":
+            A.gpu_lib().dpf_debug_nat_sequential(NAT_MODES[nat])
         try:
-            masqgen.run(r, seed, n_conn, capacity, lambda k, res, buf, infos, look, rel, pkts: steps.append(
-                (res.copy(), buf.copy(), infos.copy(), look.copy(), rel.copy(), r.count())))
+            masqgen.run(r, seed, n_conn, capacity, on)
         finally:
             if name == "gpu":
+                A.gpu_lib().dpf_debug_nat_sequential(0)
                 r.close()
         got[name] = steps
     hist = {}
@@ -92,6 +106,19 @@ def test_gpu_masquerade_random_bursts(seed, n_conn, capacity):
         for d in ro["done"]:
             hist[A.DONE_NAMES[d]] = hist.get(A.DONE_NAMES[d], 0) + 1
     assert hist.get("Delivered", 0) > n_conn
+    ran = [int(c[12]) for c in modes]
+    assert all(int(c[16]) == 0 for c in modes), "split pass refused a pair"
+    if nat == "one-lane" or capacity is not None:
+        assert set(ran) <= {0, 1}, ran
+    else:
+        # the masquerading bursts ran split: connection lanes and the
+        # allocating lane, its allocations in wave batches or alone
+        assert ran.count(3) >= 4, ran
+        assert sum(int(c[11]) for c in modes) > 0
+        if nat == "split":
+            assert sum(int(c[14]) for c in modes) > 0
+        else:
+            assert sum(int(c[14]) for c in modes) == 0 and sum(int(c[15]) for c in modes) > 0
     if n_conn >= 3000:
         assert hist.get("NatOutOfResources", 0) > 0
     if capacity is not None:

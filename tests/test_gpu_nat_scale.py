@@ -1,0 +1,115 @@
+"""GPU: the parallel NAT passes at scale -- hundreds of
+thousands of new connections per burst, where the concurrency bugs of the
+parallel passes showed themselves (DESIGN.md §3 "What the GPU found") --
+bit-exact against the oracle: every record, every byte of the buffers, every
+connection's two flows by key (FlowStatus, NAT state, allocation, expiry,
+generation) and the flow counts.
+
+- masquerade (dataplane_amd/natwork.py masq_world / MasqConns): 250k first
+  packets (250k allocations: the split pass's allocating lane, its wave
+  batches), then a burst of 300k packets on those connections -- the clients'
+  and the servers' answers, shuffled -- with 1 % new ones (connection lanes
+  for the established, the allocating lane for the rest);
+- port forwarding (natwork.tables): 270k new connections in one burst (one
+  lane per connection), and the same near the table's capacity (the one-lane
+  pass: the inserts can meet the capacity, pairs refused)."""
+import numpy as np
+import pytest
+
+from dataplane_amd import _abi as A
+from dataplane_amd import natwork as W
+from golden.masqkat import GpuRunner, OracleRunner
+from helpers import compare_bulk, hist
+
+pytestmark = pytest.mark.gpu
+
+INFO = ("status", "flags", "dst_vni", "genid", "expires_at", "pf", "masq", "masq_alloc", "pf_status",
+        "pf_port", "pf_family", "pf_ip", "idle_timeout_s")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def torch_first():
+    import torch
+    torch.cuda.init()
+
+
+def same_flows(ro, rg, keys, label):
+    lo, lg = ro.lookup(keys), rg.lookup(keys)
+    assert np.array_equal(lo["ref"] == A.FLOW_NONE, lg["ref"] == A.FLOW_NONE), f"{label}: presence"
+    for k in INFO:
+        d = np.nonzero(lo[k] != lg[k])[0] if lo[k].ndim == 1 else np.nonzero((lo[k] != lg[k]).any(axis=1))[0]
+        assert len(d) == 0, f"{label}: flow {k} differs for {len(d)} keys, first {d[0]}: {lo[d[0]]} vs {lg[d[0]]}"
+    has = lo["ref"] != A.FLOW_NONE
+    xo, xg = ro.get(lo["related"][has]), rg.get(lg["related"][has])
+    for k in INFO:
+        assert np.array_equal(xo[k], xg[k]), f"{label}: related flows' {k}"
+    return int(has.sum())
+
+
+def both(ro, rg, buf, inp, label):
+    ob, gb = buf.copy(), buf.copy()
+    oo = ro.burst(ob, inp)
+    go = rg.burst(gb, inp)
+    compare_bulk(oo, ob, go, gb, inp, label)
+    assert ro.count() == rg.count(), f"{label}: counts {ro.count()} vs {rg.count()}"
+    return oo, ob, rg.nat_counters()
+
+
+def test_gpu_masquerade_at_scale():
+    ro, rg = OracleRunner(), GpuRunner(slots=1 << 21)
+    try:
+        for r in (ro, rg):
+            r.publish(W.masq_world())
+            r.set_clock(10 ** 12)
+        c = W.MasqConns(250_000)
+        buf, inp = c.first()
+        out, ob, cnt = both(ro, rg, buf, inp, "first packets")
+        assert hist(out) == {"Delivered": 250_000}
+        assert int(cnt[12]) == 3 and int(cnt[11]) == 250_000, cnt
+        assert int(cnt[14]) > 200_000, cnt  # served in wave batches
+        assert c.learn(ob, out) == 250_000
+        keys = c.keys()
+        assert same_flows(ro, rg, keys, "first packets") == 250_000
+        for r in (ro, rg):
+            r.set_clock(10 ** 12 + 10 ** 9)
+        buf, inp, nn = c.burst(300_000, 0.01, 0.6, step=1)
+        out, ob, cnt = both(ro, rg, buf, inp, "established burst")
+        assert hist(out) == {"Delivered": 300_000}
+        assert int(cnt[12]) == 3, cnt
+        assert nn <= int(cnt[11]) < nn + 20_000, cnt  # the allocating lane: the new connections (+ few)
+        assert same_flows(ro, rg, keys, "established burst") == 250_000
+        # the same near the capacity: the allocating lane takes its records
+        # one by one (pairs refused at capacity), the connection lanes as before
+        for r in (ro, rg):
+            r.set_clock(10 ** 12 + 2 * 10 ** 9)
+            (r.fl if hasattr(r, "fl") else r.ft).set_capacity(r.count()[0] + 1000)
+        buf, inp, nn = c.burst(300_000, 0.01, 0.6, step=2)
+        out, ob, cnt = both(ro, rg, buf, inp, "established burst near capacity")
+        h = hist(out)
+        assert int(cnt[12]) == 3 and int(cnt[14]) == 0 and int(cnt[15]) > 0, cnt
+        assert h.get("FlowCapacityExceeded", 0) > 1000 and h["Delivered"] > 290_000, h
+        assert same_flows(ro, rg, keys, "established burst near capacity") == 250_000
+    finally:
+        rg.close()
+
+
+@pytest.mark.parametrize("near_capacity", [False, True], ids=["room", "near-capacity"])
+def test_gpu_portfw_at_scale(near_capacity):
+    ro, rg = OracleRunner(), GpuRunner(slots=1 << 21)
+    try:
+        for r in (ro, rg):
+            r.publish(W.tables())
+            r.set_clock(10 ** 12)
+            if near_capacity:
+                (r.fl if hasattr(r, "fl") else r.ft).set_capacity(400_000)
+        buf, inp, npf = W.burst(300_000, 0.9, 0)
+        out, ob, cnt = both(ro, rg, buf, inp, "port forwarding")
+        assert int(cnt[12]) == (1 if near_capacity else 2), cnt
+        h = hist(out)
+        if near_capacity:
+            assert h.get("FlowCapacityExceeded", 0) > 50_000, h
+        else:
+            assert h == {"Delivered": 300_000}, h
+        assert ro.count()[0] in ((400_000, 400_001) if near_capacity else (2 * npf,))
+    finally:
+        rg.close()
