@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 HEADROOM = 96
 
 # DoneReason (net/src/packet/meta.rs:84-119)
@@ -242,7 +242,8 @@ class TablesDesc(C.Structure):
                 ("masq", C.POINTER(MasqExpose)), ("n_masq", C.c_uint32),
                 ("masq_prefixes", C.POINTER(Prefix)), ("n_masq_prefixes", C.c_uint32),
                 ("masq_claims", C.POINTER(MasqClaim)), ("n_masq_claims", C.c_uint32),
-                ("masq_config_tag", C.c_uint64)]
+                ("masq_config_tag", C.c_uint64), ("masq_randomize", C.c_uint32), ("pad1", C.c_uint32),
+                ("masq_seed", C.c_uint64)]
 
 
 STRUCTS = dict(dp_ipaddr_t=IpAddr, dp_prefix_t=Prefix, dp_fib_t=Fib, dp_vni_fib_t=VniFib,

@@ -687,6 +687,8 @@ std::vector<uint8_t> masq_build(const dpd::MasqConfig &cfg, int64_t genid, uint3
   H.free_top = n_recs;
   H.live = 0;
   H.max_live = DP_MASQ_ADDRS;
+  H.randomize = cfg.randomize ? 1u : 0u;
+  H.seed = cfg.seed;
   uint64_t off = (sizeof(dpm::Header) + 63) & ~63ull;
   auto place = [&](uint64_t bytes) { const uint64_t o = off; off = (off + bytes + 63) & ~63ull; return o; };
   H.o_keys = place(sizeof(dpm::KeySlot) * keys.size());

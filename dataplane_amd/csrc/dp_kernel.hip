@@ -4706,7 +4706,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
             if (a != dpm::kNone && V.recs()[a].thread_block >= 0) {
               const dpm::Addr &A = V.recs()[a];
               const uint32_t tb = (uint32_t)A.thread_block;
-              if ((A.bflag[tb] & 2) && tb != 0) {
+              if ((A.bflag[tb] & 2) && dpm::block_base(A, tb) != 0) {
                 uint32_t fr = 0;
                 for (int k = 0; k < 8; k++) { s_bm[k] = A.bm[tb][k]; fr += __popc(~A.bm[tb][k]); }
                 const dpm::A128 aa = dpm::addr_of(V, A);
@@ -4715,7 +4715,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
                 else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
                 if (fr && pfw::unicast(G.fam, w)) {
                   f = 1;
-                  s_b[1] = a; s_b[2] = tb; s_b[3] = fr;
+                  s_b[1] = a; s_b[2] = dpm::block_base(A, tb) | tb; s_b[3] = fr;
                   for (int k = 0; k < 4; k++) s_b[4 + k] = w[k];
                 }
               }
@@ -4734,7 +4734,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           // the records from p on asking the same set, up to one whose
           // reverse key could equal its initial key (related_pair) at this
           // address: served while the block has free ports
-          const uint32_t a = s_b[1], tb = s_b[2], fr = s_b[3];
+          const uint32_t a = s_b[1], tb = s_b[2] & 0xffu, base = s_b[2] & ~0xffu, fr = s_b[3];
           uint32_t w[4];
           for (int k = 0; k < 4; k++) w[k] = s_b[4 + k];
           bool stop = false;
@@ -4768,7 +4768,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
                 k -= c;
               }
               rec = a;
-              aport = (tb << 8) + port;
+              aport = base + port;
               for (int x = 0; x < 4; x++) aip[x] = w[x];
               ok = true;
             }

@@ -18,8 +18,11 @@
 // per address.  A block whose last port goes is free again; an address whose
 // last block goes returns to the bitmap and leaves the in-use list (the
 // reference skips and later drops its Weak; the order of the others is the
-// same).  Deterministic mode (randomize = false): block i covers ports
-// [256 i, 256 i + 255].  One thread: ThreadPortMap is one slot per address.
+// same).  Block i of an address covers ports [256 perm[i], 256 perm[i] + 255]:
+// perm is the identity (randomize = false) or the permutation dpgpu.h defines
+// from the allocator's seed and the address (randomize = true, drawn when the
+// address is put to use, as PortAllocator::new shuffles, port_alloc.rs:
+// 105-113).  One thread: ThreadPortMap is one slot per address.
 #pragma once
 #include <stdint.h>
 
@@ -128,6 +131,8 @@ struct Addr {
   uint32_t cur;                           // current_alloc_index
   uint32_t pad[3];
   uint8_t bflag[256];                     // bit 0: free, bit 1: alive (an AllocatedPortBlock lives)
+  uint8_t perm[256];                      // AllocatorPortBlock::random_index of block i
+  uint8_t inv[256];                       // the block whose random_index is j
   uint16_t blive[256];                    // live ports of an alive block
   uint32_t bm[256][8];                    // Bitmap256 of an alive block
 };
@@ -138,9 +143,10 @@ struct Header {
   uint32_t key_mask, n_keys;
   uint32_t n_regions, n_recs;
   uint32_t free_top, live;                // free-record stack top, addresses in use
-  uint32_t max_live, pad;
+  uint32_t max_live, randomize;           // MasqueradeConfig::randomize
   uint64_t o_keys, o_ents, o_sets, o_setreg, o_regions, o_claims, o_bits, o_free, o_recs;
   uint64_t bytes;
+  uint64_t seed;                          // the permutations' seed (dpgpu.h masq_seed)
 };
 
 // A view of one allocator buffer (device or host memory).
@@ -228,6 +234,33 @@ __host__ __device__ inline bool claimed(const View &v, const Region &R, const A1
   return false;
 }
 
+__host__ __device__ inline uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// The order of an address's port blocks (dpgpu.h: the shuffle of
+// PortAllocator::new, port_alloc.rs:105-113, drawn from the seed and the
+// address); the identity without randomize
+__host__ __device__ inline void block_order(const Header &H, const A128 &a, uint8_t perm[256], uint8_t inv[256]) {
+  for (uint32_t i = 0; i < 256; i++) perm[i] = (uint8_t)i;
+  if (H.randomize) {
+    uint64_t x = H.seed;
+    for (int k = 0; k < 4; k++) x = splitmix64(x ^ a.w[k]);
+    for (uint32_t i = 255; i >= 1; i--) {
+      x = splitmix64(x);
+      const uint32_t j = (uint32_t)(x % (i + 1));
+      const uint8_t t = perm[i];
+      perm[i] = perm[j];
+      perm[j] = t;
+    }
+  }
+  for (uint32_t i = 0; i < 256; i++) inv[perm[i]] = (uint8_t)i;
+}
+// the first port of block i
+__host__ __device__ inline uint32_t block_base(const Addr &A, uint32_t i) { return (uint32_t)A.perm[i] << 8; }
+
 // NatPool::use_new_ip / reserve_from_pool's new address: an AllocatedIp with
 // its PortAllocator::new (port_alloc.rs:100-145), at the back of in_use
 __host__ __device__ inline uint32_t addr_new(const View &v, uint32_t region, uint32_t offset) {
@@ -250,8 +283,9 @@ __host__ __device__ inline uint32_t addr_new(const View &v, uint32_t region, uin
   A.thread_block = -1;
   A.cur = 0;
   const A128 a = a_add(R.start, offset);
+  block_order(H, a, A.perm, A.inv);
   for (uint32_t i = 0; i < 256; i++) {
-    const uint32_t base = i << 8;
+    const uint32_t base = block_base(A, i);
     bool off = R.excl_wk && base < 1024;
     if (!off) {
       uint32_t bm[8];
@@ -291,7 +325,7 @@ __host__ __device__ inline void block_new(const View &v, uint32_t r, uint32_t id
   A.blive[idx] = 0;
   A.usable--;
   A.live_blocks++;
-  block_init(v, R, a_add(R.start, A.offset), idx << 8, !allow_null, A.bm[idx]);
+  block_init(v, R, a_add(R.start, A.offset), block_base(A, idx), !allow_null, A.bm[idx]);
   if (!bm_full(A.bm[idx])) A.nonfull++;
 }
 // The block's last port went (Drop of AllocatedPortBlock: deallocate_block,
@@ -311,7 +345,7 @@ __host__ __device__ inline uint32_t block_take(const View &v, uint32_t r, uint32
   for (int k = 0; k < 8; k++) {
     if (bm[k] == 0xffffffffu) continue;
     const uint32_t off = 32 * k + (uint32_t)__builtin_ctz(~bm[k]);
-    const uint32_t p = (idx << 8) + off;
+    const uint32_t p = block_base(A, idx) + off;
     if (!allow_null && p == 0) return PORT_ALLOC_FAILED;  // new_port_checked (never: bit 0 is preset)
     bm[k] |= 1u << (off & 31);
     A.blive[idx]++;
@@ -328,7 +362,7 @@ __host__ __device__ inline void release(const View &v, uint32_t r, uint32_t port
   if (r >= v.h().n_recs) return;
   Addr &A = v.recs()[r];
   if (A.region == kNone) return;
-  const uint32_t idx = port >> 8, off = port & 0xffu;
+  const uint32_t idx = A.inv[port >> 8], off = port & 0xffu;
   if (!(A.bflag[idx] & 2)) return;
   uint32_t *bm = A.bm[idx];
   if (!(bm[off >> 5] & (1u << (off & 31)))) return;  // never taken (the reference logs it)
@@ -436,7 +470,7 @@ __host__ __device__ inline uint32_t set_reserve(const View &v, uint32_t set, con
   }
   Addr &A = v.recs()[r];
   uint32_t e = OK;
-  const uint32_t idx = port >> 8;
+  const uint32_t idx = A.inv[port >> 8];  // try_to_reserve_block: the block covering the port
   if (R.excl_wk && port < 1024) e = DENIED;
   else if (claimed(v, R, a, port)) e = DENIED;
   else if (A.bflag[idx] & 1) {

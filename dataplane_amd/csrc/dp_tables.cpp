@@ -1518,6 +1518,8 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
     mc->exposes.push_back(std::move(e));
   }
   mc->tag = d->masq_config_tag;
+  mc->randomize = d->masq_randomize != 0;
+  mc->seed = d->masq_seed;
   ib.alloc(64);
   im.bytes = ib.b.size();
   // context records carry 32-bit image offsets (Mbi)

@@ -30,7 +30,10 @@ struct MasqConfig {
   std::vector<MasqExpose> exposes;
   std::string canon;
   uint64_t tag = 0;
+  bool randomize = false;  // MasqueradeConfig::set_randomize, and the permutations' seed
+  uint64_t seed = 0;
   bool same(const MasqConfig &o) const {
+    if (randomize != o.randomize || seed != o.seed) return false;
     return tag || o.tag ? tag == o.tag && o.tag != 0 : canon == o.canon;
   }
 };

@@ -83,6 +83,10 @@ class TablesBuilder:
         self.masq_prefixes: List[A.Prefix] = []
         self.masq_claims: List[A.MasqClaim] = []
         self.masq_config_tag = 0
+        # MasqueradeConfig::set_randomize (dpgpu.h dp_masq_expose_t): the port
+        # blocks of each address in a permuted order drawn from masq_seed
+        self.masq_randomize = False
+        self.masq_seed = 0
         self._keep = []
 
     # -- routing --------------------------------------------------------------
@@ -313,5 +317,7 @@ class TablesBuilder:
         d.masq_prefixes, d.n_masq_prefixes = self._arr(A.Prefix, self.masq_prefixes)
         d.masq_claims, d.n_masq_claims = self._arr(A.MasqClaim, self.masq_claims)
         d.masq_config_tag = self.masq_config_tag
+        d.masq_randomize = 1 if self.masq_randomize else 0
+        d.masq_seed = self.masq_seed
         self._desc = d
         return C.pointer(d)

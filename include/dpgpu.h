@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define DPGPU_ABI_VERSION 4u
+#define DPGPU_ABI_VERSION 5u
 
 /* Bytes every frame must have in front of it (its own scratch, owned by the
  * packet).  Output headers are written in place into this headroom: VXLAN
@@ -403,10 +403,22 @@ typedef struct dp_portfw_rule {
  * tuples the port-forwarding exposes of the same local manifest may claim
  * (claims_for, setup.rs:73-92), which the pools never hand out
  * (apalloc/reserved.rs).  An expose is one address family: its private and
- * public prefixes are all v4 (NAT44) or all v6 (NAT66).  The allocator is
- * the reference's deterministic one (MasqueradeConfig::set_randomize(false),
- * the mode its own collision test runs, nat/src/masquerade/test.rs:1399-1406):
- * port blocks in index order, ports in bitmap order, addresses lowest first. */
+ * public prefixes are all v4 (NAT44) or all v6 (NAT66).  Ports come in
+ * bitmap order within a port block and addresses lowest first; the blocks of
+ * an address come in index order (MasqueradeConfig::set_randomize(false), the
+ * mode the reference's collision test runs, nat/src/masquerade/test.rs:
+ * 1399-1406) or, with dp_tables_desc_t.masq_randomize, in a shuffled order
+ * (the default, allocator_writer.rs:58; mgmt sets it, proc.rs:541): when an
+ * address is put to use, its 256 blocks are permuted (PortAllocator::new,
+ * port_alloc.rs:105-113).  The permutation is a function of masq_seed and
+ * the address, so the device and any restatement agree:
+ *   splitmix64(z): z += 0x9E3779B97F4A7C15; z = (z ^ z >> 30) * 0xBF58476D1CE4E5B9;
+ *                  z = (z ^ z >> 27) * 0x94D049BB133111EB; return z ^ z >> 31
+ *   x = masq_seed; for each 32-bit word w of the address as a 128-bit number,
+ *   most significant first (v4: three zero words, then the address):
+ *   x = splitmix64(x ^ w); perm = 0..255; for i = 255 down to 1:
+ *   x = splitmix64(x); swap(perm[i], perm[x % (i + 1)])
+ * and block i of the address covers ports [256 perm[i], 256 perm[i] + 255]. */
 typedef struct dp_masq_expose {
     uint32_t src_vni;          /* MasqueradePeering.src_vpcd */
     uint32_t dst_vni;          /* MasqueradePeering.dst_vpcd */
@@ -477,6 +489,12 @@ typedef struct dp_tables_desc {
      * are the same configuration (the allocator and its flows are kept, only
      * the generation advances); 0: compared by the exposes and claims above */
     uint64_t masq_config_tag;
+    /* MasqueradeConfig::set_randomize (dp_masq_expose_t above): 1 shuffles
+     * each address's port blocks by masq_seed; part of the configuration's
+     * identity (a change rebuilds the allocators) */
+    uint32_t masq_randomize;
+    uint32_t pad1;
+    uint64_t masq_seed;
 } dp_tables_desc_t;
 
 /* ------------------------------------------------------------------------ */

@@ -1040,9 +1040,13 @@ struct Trie {  // binary trie with LPM (prefix-trie get_lpm semantics)
 // reference's ownership: an allocated port holds its port block, a block its
 // address, an address its pool (Arc back-references); dropping the last holder
 // releases the tuple (the Drop impls, port_alloc.rs:513-565, alloc.rs:322-326).
-// The deterministic mode (randomize = false): block i covers ports
-// [256 i, 256 i + 255].  A region's offsets are bounded by
-// DP_MASQ_REGION_ADDRS (dpgpu.h), as the reference bounds them by u32.
+// Block i of an address covers ports [256 r, 256 r + 255] for its
+// random_index r: i itself (randomize = false), or the shuffle PortAllocator::
+// new draws (port_alloc.rs:105-113) -- here the permutation dpgpu.h specifies
+// from the configuration's seed and the address (the reference's rand::rng()
+// is not reproducible; its draw is replaced by a specified one).  A region's
+// offsets are bounded by DP_MASQ_REGION_ADDRS (dpgpu.h), as the reference
+// bounds them by u32.
 // ---------------------------------------------------------------------------
 typedef unsigned __int128 u128;
 
@@ -1115,6 +1119,8 @@ struct MBlock;
 // PortAllocator (port_alloc.rs:84-93); one thread: ThreadPortMap is one slot
 struct MPortAlloc {
   bool free[256];
+  uint8_t random_index[256];                           // AllocatorPortBlock::random_index
+  uint8_t index_of[256];                               // the block with random_index j
   uint16_t usable = 0;
   size_t cur = 0;                                      // current_alloc_index
   int thread_block = -1;
@@ -1133,6 +1139,8 @@ struct MPool {
   std::vector<MClaim> claims;               // ReservedPorts of the region
   bool excl_wk = false;
   std::shared_ptr<uint32_t> live;           // addresses in use over the allocator (DP_MASQ_ADDRS)
+  bool randomize = false;                   // MasqueradeConfig::randomize, and the seed of the shuffles
+  uint64_t seed = 0;
 };
 
 struct MIp {  // AllocatedIp (alloc.rs:251-255)
@@ -1175,6 +1183,27 @@ std::vector<std::pair<uint16_t, uint16_t>> m_reserved_for(const MPool &P, u128 b
   return out;
 }
 
+// The shuffle of PortAllocator::new as dpgpu.h specifies it: splitmix64 over
+// the seed and the address's 32-bit words (most significant first), then
+// Fisher-Yates from the last position down
+uint64_t m_splitmix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+void m_shuffle_blocks(uint64_t seed, u128 addr, uint8_t out[256]) {
+  std::vector<int> base_ports(256);
+  for (int i = 0; i < 256; i++) base_ports[i] = i;
+  uint64_t x = seed;
+  for (int k = 3; k >= 0; k--) x = m_splitmix(x ^ (uint32_t)(addr >> (32 * k)));
+  for (int i = 255; i >= 1; i--) {
+    x = m_splitmix(x);
+    std::swap(base_ports[i], base_ports[x % (uint64_t)(i + 1)]);
+  }
+  for (int i = 0; i < 256; i++) out[i] = (uint8_t)base_ports[i];
+}
+
 // AllocatedIp::new -> PortAllocator::new (port_alloc.rs:100-145)
 std::shared_ptr<MIp> m_new_ip(const std::shared_ptr<MPool> &P, uint32_t offset) {
   if (*P->live >= DP_MASQ_ADDRS) return nullptr;
@@ -1185,8 +1214,11 @@ std::shared_ptr<MIp> m_new_ip(const std::shared_ptr<MPool> &P, uint32_t offset) 
   ip->pool = P;
   ip->pa.reserved = m_reserved_for(*P, ip->bits);
   ip->pa.excl_wk = P->excl_wk;
+  if (P->randomize) m_shuffle_blocks(P->seed, ip->bits, ip->pa.random_index);
+  else for (int i = 0; i < 256; i++) ip->pa.random_index[i] = (uint8_t)i;
+  for (int i = 0; i < 256; i++) ip->pa.index_of[ip->pa.random_index[i]] = (uint8_t)i;
   for (int i = 0; i < 256; i++) {
-    const uint16_t base = (uint16_t)(i * 256);
+    const uint16_t base = (uint16_t)(ip->pa.random_index[i] * 256);
     const bool wk = P->excl_wk && base < 1024;
     const bool whole = Bitmap256::for_block(base, ip->pa.reserved, false).full();
     ip->pa.free[i] = !(wk || whole);
@@ -1244,7 +1276,7 @@ MErr m_allocate_port(const std::shared_ptr<MIp> &ip, bool allow_null, std::share
   auto b = std::make_shared<MBlock>();
   b->ip = ip;
   b->index = (size_t)idx;
-  b->base = (uint16_t)(idx * 256);
+  b->base = (uint16_t)(pa.random_index[idx] * 256);  // AllocatorPortBlock::to_port_number
   b->bm = Bitmap256::for_block(b->base, pa.reserved, !allow_null);
   pa.allocated[(size_t)idx] = b;
   return m_port_from_block(b, allow_null, out);
@@ -1333,7 +1365,7 @@ MErr m_set_reserve(const MPoolSet &S, const Ip &a, uint16_t port, bool ident, st
   for (auto &r : pa.reserved) if (r.first <= port && port <= r.second) return M_DENIED;
   // find_block_for_port: the block covering the port, taken if free, else the
   // live block holding it (the retries change nothing single-threaded)
-  const size_t idx = port >> 8;
+  const size_t idx = pa.index_of[port >> 8];  // try_to_reserve_block: the block that covers it
   std::shared_ptr<MBlock> b;
   if (pa.free[idx]) {
     pa.free[idx] = false;
@@ -1341,7 +1373,7 @@ MErr m_set_reserve(const MPoolSet &S, const Ip &a, uint16_t port, bool ident, st
     b = std::make_shared<MBlock>();
     b->ip = ip;
     b->index = idx;
-    b->base = (uint16_t)(idx * 256);
+    b->base = (uint16_t)((port >> 8) * 256);
     b->bm = Bitmap256::for_block(b->base, pa.reserved, !ident);
     pa.allocated[idx] = b;
   } else {
@@ -1389,6 +1421,8 @@ struct MAlloc {
   std::string config;  // MasqueradeConfig, as its canonical bytes
   uint64_t tag = 0;
   int64_t genid = 0;
+  bool randomize = false;
+  uint64_t seed = 0;
   std::vector<MExpose> exposes;
   std::map<MPoolKey, MPoolSet> pools[2];  // [0] src44, [1] src66
 
@@ -1437,11 +1471,13 @@ std::vector<MRegionSpec> m_decompose(const std::vector<std::vector<std::pair<u12
 
 // NatAllocator::new -> build_pools_generic (apalloc/setup.rs:158-204)
 std::shared_ptr<MAlloc> m_build(const std::vector<MExpose> &ex, const std::string &cfg, uint64_t tag,
-                                int64_t genid) {
+                                int64_t genid, bool randomize, uint64_t seed) {
   auto A = std::make_shared<MAlloc>();
   A->config = cfg;
   A->tag = tag;
   A->genid = genid;
+  A->randomize = randomize;
+  A->seed = seed;
   A->exposes = ex;
   auto live = std::make_shared<uint32_t>(0);
   for (int fam : {4, 6}) {
@@ -1466,6 +1502,8 @@ std::shared_ptr<MAlloc> m_build(const std::vector<MExpose> &ex, const std::strin
           for (uint32_t o = 0; o < P->cap; o++) P->free.insert(o);
           P->excl_wk = proto == 6 || proto == 17;
           P->live = live;
+          P->randomize = randomize;
+          P->seed = seed;
           // claims_for: the claims of every owner, for this protocol (TCP / UDP only)
           const uint32_t bit = proto == 6 ? DP_MASQ_TCP : proto == 17 ? DP_MASQ_UDP : 0;
           for (size_t o : R.owners)
@@ -1557,6 +1595,8 @@ struct dpo_tables {
   std::vector<MExpose> masq;
   std::string masq_cfg;
   uint64_t masq_tag = 0;
+  bool masq_random = false;  // MasqueradeConfig::randomize and the shuffles' seed
+  uint64_t masq_seed = 0;
   uint64_t serial = 0;      // this build (a flow table syncs its allocator once per build)
 };
 
@@ -2805,8 +2845,9 @@ void masq_sync(const dpo_tables &T, dpo_flows *FL) {
   if (FL->synced == T.serial) return;
   FL->synced = T.serial;
   const std::shared_ptr<MAlloc> cur = FL->alloc;
-  const bool same = cur && (cur->tag || T.masq_tag ? cur->tag == T.masq_tag && T.masq_tag != 0
-                                                   : cur->config == T.masq_cfg);
+  const bool same = cur && cur->randomize == T.masq_random && cur->seed == T.masq_seed &&
+                    (cur->tag || T.masq_tag ? cur->tag == T.masq_tag && T.masq_tag != 0
+                                            : cur->config == T.masq_cfg);
   if (same) {  // upgrade_all_masquerading_flows (flows.rs:30-44)
     cur->genid = T.genid;
     for (auto &kv : FL->map) {
@@ -2823,7 +2864,7 @@ void masq_sync(const dpo_tables &T, dpo_flows *FL) {
     }
     return;
   }
-  auto A = m_build(T.masq, T.masq_cfg, T.masq_tag, T.genid);
+  auto A = m_build(T.masq, T.masq_cfg, T.masq_tag, T.genid, T.masq_random, T.masq_seed);
   std::vector<int64_t> fwd;
   for (auto &kv : FL->map) {
     const OFlow &f = FL->f[kv.second];
@@ -3394,6 +3435,8 @@ int dpo_tables_build2(const dp_tables_desc_t *d, const dpo_tables_t *prev, dpo_t
     T->masq.push_back(std::move(e));
   }
   T->masq_tag = d->masq_config_tag;
+  T->masq_random = d->masq_randomize != 0;
+  T->masq_seed = d->masq_seed;
   static std::atomic<uint64_t> serials{1};
   T->serial = serials++;
   *out = T.release();

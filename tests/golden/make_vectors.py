@@ -36,7 +36,8 @@ def tables_digest(tp) -> str:
     d = tp.contents
     h = hashlib.sha256()
     for name, _ in A.TablesDesc._fields_:
-        if name.startswith("n_") or name in ("abi_version", "pad0", "genid", "masq_config_tag"):
+        if name.startswith("n_") or name in ("abi_version", "pad0", "genid", "masq_config_tag",
+                                              "masq_randomize", "pad1", "masq_seed"):
             continue
         n = getattr(d, "n_" + name)
         if n:

@@ -38,8 +38,10 @@ M.OVERLAYS.setdefault("gen_narrow", lambda: [
 PEERS = [(V1, V2), (V3, V2), (V2, V1), (V2, V3)]
 
 
-def world(overlay: str, genid: int):
+def world(overlay: str, genid: int, randomize_seed=None):
     t = M.world(overlay, genid, PEERS)
+    if randomize_seed is not None:  # MasqueradeConfig::set_randomize(true)
+        t.masq_randomize, t.masq_seed = True, randomize_seed
     # the claims ride on the exposes of 2.2.2.0/31 (rebuild them with claims)
     t.masq, t.masq_prefixes, t.masq_claims = [], [], []
     for (s, d, priv, pub, idle) in M.OVERLAYS[overlay]():
@@ -81,13 +83,14 @@ def rev_of(c: Conn, out: dict, flags=0) -> Pkt:
     return Pkt(M.l4_frame(out["dst"], out["src"], c.proto, out["dport"], out["sport"], flags), V2)
 
 
-def run(r, seed: int, n_conn: int, capacity=None, on_burst=None, before_burst=None):
+def run(r, seed: int, n_conn: int, capacity=None, on_burst=None, before_burst=None, randomize_seed=None):
     """The bursts of one seed on runner r (masqkat.OracleRunner / GpuRunner);
     on_burst(k, res, buf, infos, lookups, related_infos) after each.  Replies
-    are built from the runner's own translated packets."""
+    are built from the runner's own translated packets.  randomize_seed: the
+    allocator shuffles each address's port blocks (dpgpu.h masq_randomize)."""
     rng = random.Random(seed)
     cs = [Conn(rng, k) for k in range(n_conn)]
-    r.publish(world("gen", 1))
+    r.publish(world("gen", 1, randomize_seed))
     if capacity is not None:
         (r.fl if hasattr(r, "fl") else r.ft).set_capacity(capacity)
     keys = np.array([c.key() for c in cs], dtype=A.FLOW_KEY)
@@ -139,7 +142,7 @@ def run(r, seed: int, n_conn: int, capacity=None, on_burst=None, before_burst=No
         now += adv
         r.set_clock(now)
         if pub is not None:
-            r.publish(world(*pub))
+            r.publish(world(*pub, randomize_seed))
         if sweep:
             r.sweep(now)
         if before_burst:
