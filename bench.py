@@ -248,8 +248,36 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
     hour = 3600 * 10**9
     clock = [0]
 
-    def run(share, reps, one_lane=False):
+    def counters():
+        import ctypes as C
+        c = (C.c_uint32 * 24)()
+        lib.dpf_debug_nat_counters(nf2.ctx, c, 24)
+        return {"mode": int(c[12]), "records": int(c[1]), "lane_records": int(c[11]),
+                "left_by_connections": int(c[13]), "allocations_batched": int(c[14]),
+                "allocations_alone": int(c[15])}
+
+    def run(share, reps, one_lane=False, near_capacity=False):
         buf, inp, npf = W.burst(n, share, 0, kind=kind)
+        filled = 0
+        if near_capacity:
+            # the table pre-filled with flows that never expire, up to `npf`
+            # slots below its capacity: half of the burst's pairs fit, the
+            # rest are refused (insert_common's admissions, decided in packet
+            # order before the connections run: mode 4)
+            cap = min(10_000_000, slots // 2)  # FlowTable::DEFAULT_CAPACITY, at most half the slots
+            ft.set_capacity(cap)
+            filled = max(0, cap - npf - int(ft.count()[0]))
+            fl = np.zeros(filled, A.FLOW)
+            i = np.arange(filled, dtype=np.uint64)
+            fl["key"]["src_vni"], fl["key"]["family"], fl["key"]["kind"] = W.VPC_P, 4, A.FLOW_UDP
+            fl["key"]["sport"], fl["key"]["dport"] = 1000, 53
+            fl["key"]["src"][:, :4] = W._ip((np.uint64(172 << 24 | 16 << 16) + i).astype(np.uint32))
+            fl["key"]["dst"][:, :4] = (198, 51, 100, 1)
+            fl["dst_vni"] = W.VPC_C
+            fl["expires_at"] = (1 << 63) - 1
+            for k in range(0, filled, 1 << 20):
+                ft.insert(fl[k:k + (1 << 20)])
+            log(0, f"[bench] NAT leg: table pre-filled with {filled} flows, capacity {cap}")
         pristine = torch.from_numpy(buf).to(dev)
         b = torch.empty_like(pristine)
         dinp = torch.from_numpy(inp.view(np.uint8)).to(dev)
@@ -276,17 +304,12 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
         done = {A.DONE_NAMES[d]: int(c) for d, c in zip(*np.unique(out["done"], return_counts=True))}
         keep = ms[1:] if len(ms) > 1 else ms
         med = sorted(keep)[len(keep) // 2]
-        return {"pf_share": share, "pf_packets": npf, "one_lane": one_lane, "launch_ms_median": round(med, 4),
+        if filled:
+            ft.remove(fl["key"])
+        return {"pf_share": share, "pf_packets": npf, "one_lane": one_lane, "prefilled_flows": filled,
+                "nat_pass": counters(), "launch_ms_median": round(med, 4),
                 "mpps_median": round(n / (med / 1e3) / 1e6, 3), "flows_after": int(flows), "launches": len(keep),
                 "done_histogram": done}
-
-    def counters():
-        import ctypes as C
-        c = (C.c_uint32 * 24)()
-        lib.dpf_debug_nat_counters(nf2.ctx, c, 24)
-        return {"mode": int(c[12]), "records": int(c[1]), "lane_records": int(c[11]),
-                "left_by_connections": int(c[13]), "allocations_batched": int(c[14]),
-                "allocations_alone": int(c[15])}
 
     def run_established(reps, conns=200_000, new_share=0.01, fwd_share=0.6):
         """Every packet masqueraded: `conns` connections opened by an untimed
@@ -347,6 +370,8 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
             log(0, f"[bench] NAT leg share {share}: {res['legs'][-1]['launch_ms_median']} ms")
         res["legs"].append(run(0.25, 2, one_lane=True))
         log(0, f"[bench] NAT leg one lane: {res['legs'][-1]['launch_ms_median']} ms")
+        res["legs"].append(run(0.25, steps + 1, near_capacity=True))
+        log(0, f"[bench] NAT leg near capacity: {res['legs'][-1]['launch_ms_median']} ms")
     nf2.attach_flows(None)
     ft.close()
     nf2.close()

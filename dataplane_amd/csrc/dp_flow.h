@@ -173,7 +173,9 @@ struct FlowCtx {
   // [12] the mode that ran (1 one lane, 2 connections, 3 split), [13] records
   // a connection lane left to the allocating lane, [14] allocations served in
   // wave batches, [15] allocations on the lane alone, [16] pairs the split
-  // pass could not create (never: it runs only with room; counters for tests)
+  // pass could not create (never: it runs only with room; counters for tests).
+  // Port forwarding without room for every pair (dp_nat_admit_*): [17] a
+  // connection whose creations the admission pass cannot foresee
   unsigned long long *grp_tab, *grp_head, *grp_next;
   uint32_t *grp_list;
   uint32_t grp_mask;
@@ -186,6 +188,10 @@ struct FlowCtx {
   // the masquerading burst's allocating lane: its packets (bitmap by packet
   // index + summary, as pf_bits) and their order
   uint32_t *lane_bits, *lane_sum, *lane_order;
+  // port forwarding near the capacity (mode 4): per record the new slots its
+  // creation adds, then the sum of those of the records before it in packet
+  // order (the table length its first insert meets); per 4096 records a sum
+  uint32_t *adm, *adm_blk;
   uint32_t lean;        // the launch runs the flows variant without stateful NAT (dp_kernel.hip DP_SNAT)
 };
 

@@ -3528,6 +3528,11 @@ struct Seq {
   // the pass ends (no insert of a parallel pass reads the length: it cannot
   // reach the capacity)
   mutable uint32_t added = 0;
+  // mode 4 (port forwarding near the capacity): the table length this
+  // record's first insert meets, as the burst's earlier creations leave it
+  // (dp_nat_admit_*: their new slots summed in packet order); kNoSlot: the
+  // length as the table holds it
+  mutable uint32_t adm = dpf::kNoSlot;
   __device__ uint32_t bump(uint32_t *c) const { return par ? atomicAdd(c, 1u) : (*c)++; }
   __device__ bool alive(uint32_t sl, uint32_t tag) const { return sl <= fc.mask && fc.slots[sl].state == tag; }
   // the pair is invalid for packet idx: either flow's burst-local mark says
@@ -3583,6 +3588,7 @@ struct Seq {
   // key's probe sequence.  Returns the slot, kNoSlot when refused.
   __device__ uint32_t insert(const dpf::FKey &k, bool exception, uint32_t idx) const {
     uint64_t len = ((uint64_t)fc.tmeta[3] << 32) | fc.tmeta[2];
+    if (par && adm != dpf::kNoSlot) len = (((uint64_t)fc.pf_cnt[7] << 32) | fc.pf_cnt[6]) + adm;
     if (len >= fc.capacity && !exception) return dpf::kNoSlot;
     const uint32_t home = dpf::fkey_hash(k) & fc.mask;
     const uint32_t bound = fc.tmeta[0];
@@ -4263,13 +4269,22 @@ __device__ uint32_t sort_conn(unsigned long long *nx, uint32_t list) {
 // connections in parallel (port forwarding: when no insert of the burst can
 // meet the capacity or the 7/8 bound), 3 split (masquerade: only the
 // allocating lane inserts, and it takes its records one by one in packet
-// order when room is short -- dp_nat_lane).
-__device__ __forceinline__ uint32_t nat_mode(const dpf::FlowCtx &fc) {
+// order when room is short -- dp_nat_lane), 4 connections in parallel with
+// insert_common's capacity admissions decided beforehand in packet order
+// (port forwarding without room for every pair: dp_nat_admit_*).  pre: the
+// mode before dp_nat_admit_plan has looked at the connections (4 may turn 1).
+__device__ __forceinline__ uint32_t nat_mode(const dpf::FlowCtx &fc, bool pre = false) {
   if (fc.force_seq == 1 || fc.pf_cnt[5]) return 1u;
   if (fc.pf_cnt[8]) return fc.pf_cnt[9] || fc.pf_cnt[10] ? 1u : 3u;
   const uint64_t len0 = ((uint64_t)fc.pf_cnt[7] << 32) | fc.pf_cnt[6];
   const uint64_t total = fc.pf_cnt[1];
-  return len0 + 2ull * total > fc.capacity || len0 + 2ull * total > fc.hard ? 1u : 2u;
+  if (len0 + 2ull * total <= fc.capacity && len0 + 2ull * total <= fc.hard) return 2u;
+  // (the 7/8 bound out of reach: only the capacity can refuse, and only a
+  // creation's first insert)
+  if (fc.force_seq != 3 && len0 + 2ull * total <= fc.hard && fc.capacity <= fc.hard && total <= (4u << 20) &&
+      (pre || !fc.pf_cnt[17]))
+    return 4u;
+  return 1u;
 }
 
 __device__ __forceinline__ void flag_once(uint32_t *w) {
@@ -4374,6 +4389,80 @@ __device__ void masq_conn_run(const Seq &q, uint32_t list) {
     atomicAdd(&fc.pf_cnt[13], 1u);
     lane = true;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Port forwarding near the capacity (mode 4)
+// ---------------------------------------------------------------------------
+// insert_common refuses a flow when the table holds `capacity` flows (the
+// second of a pair excepted), so once the burst's creations fill the table,
+// every later creation in packet order is refused; before that point every
+// one is admitted.  Which one first meets the capacity follows from how many
+// new slots each creation adds, summed in packet order -- known before any
+// runs when each connection's creations are: a connection whose records are
+// all without a flow (its first creation adds a slot for each of its two
+// keys not in the table, a repeat replaces those), or one that creates
+// nothing (each record that could is on a valid flow with port-forwarding
+// state whose rule lives, and no earlier record of it can close the pair).
+// Any other connection (pf_cnt[17]) leaves the burst to the one-lane pass.
+
+// A record on its connection's valid port-forwarding pair, which refreshes
+// rather than creates (resolve_pf's first branch, no rule to revalidate, no
+// ACL flow verdict)
+__device__ bool pf_held(const Seq &q, const dpf::PfReq &R) {
+  if (R.slot == dpf::kNoSlot || !q.alive(R.slot, R.state) || R.status0 != DP_FLOW_ACTIVE) return false;
+  if ((R.bits & dpf::kPqSens) || !q.pair_valid(R.slot, R.idx)) return false;
+  const dpf::FlowSlot &f = q.fc.slots[R.slot];
+  return (f.flags & dpf::kFlagPf) && by_id(q.g, f.pf_rule) >= 0;
+}
+
+// The creation's forward key (resolve_pf: the key before static NAT, else the
+// current one)
+__device__ void creation_fk(const dpf::PfReq &R, dpf::FKey &fk) {
+  if (R.bits & dpf::kPqIkey) {
+    for (int j = 0; j < 11; j++) fk.w[j] = R.ikey[j];
+  } else {
+    const uint32_t fam = (R.proto >> 8) & 0xffu;
+    fk.w[0] = R.src_vni;
+    fk.w[1] = fam | (((R.bits & dpf::kPqTcp) ? DP_FLOW_TCP : DP_FLOW_UDP) << 8);
+    fk.w[2] = R.ports;
+    for (int j = 0; j < 4; j++) { fk.w[3 + j] = bswap(R.src[j]); fk.w[7 + j] = bswap(R.dst[j]); }
+  }
+}
+
+// One connection (its records sorted): fc.adm[record] = the new slots its
+// creation adds; false: its creations cannot be foreseen.
+__device__ bool admit_plan(const Seq &q, uint32_t list) {
+  const dpf::FlowCtx &fc = q.fc;
+  bool pure = true, held = true, closing = false;
+  for (uint32_t r = list; r != dpf::kNoSlot; r = (uint32_t)link_ld(&fc.grp_next[r])) {
+    const dpf::PfReq &R = fc.pf[r];
+    dpf::FKey rk;
+    const bool cand = creation_rk(q.g, R, rk), h = pf_held(q, R);
+    if (R.slot != dpf::kNoSlot) pure = false;
+    if (cand && (closing || !h)) held = false;
+    // a record after which the pair may be invalid: a TCP FIN / RST, the ACL's
+    // flow verdict, a flow that is not held (a rule to revalidate, ...)
+    if (((R.bits & dpf::kPqTcp) && ((R.proto >> 16) & 5u)) || (R.bits & dpf::kPqSens) ||
+        (R.slot != dpf::kNoSlot && !h))
+      closing = true;
+  }
+  if (!pure && !held) return false;
+  bool first = pure;
+  for (uint32_t r = list; r != dpf::kNoSlot; r = (uint32_t)link_ld(&fc.grp_next[r])) {
+    const dpf::PfReq &R = fc.pf[r];
+    uint32_t w = 0;
+    dpf::FKey rk, fk;
+    if (first && creation_rk(q.g, R, rk)) {
+      creation_fk(R, fk);
+      uint32_t st;
+      uint4 v, x;
+      w = (flow_probe(fc, fk, st, v, x) == dpf::kNoSlot ? 1u : 0u) + (flow_probe(fc, rk, st, v, x) == dpf::kNoSlot ? 1u : 0u);
+      first = false;
+    }
+    fc.adm[r] = w;
+  }
+  return true;
 }
 
 }  // namespace pfw
@@ -4570,7 +4659,8 @@ dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ i
 #ifdef DP_DEBUG_NAT_NOSORT
     uint32_t r = (uint32_t)fc.grp_head[h];
 #else
-    uint32_t r = pfw::sort_conn(fc.grp_next, (uint32_t)fc.grp_head[h]);
+    // (mode 4: dp_nat_admit_plan sorted the list already)
+    uint32_t r = mode == 4 ? (uint32_t)fc.grp_head[h] : pfw::sort_conn(fc.grp_next, (uint32_t)fc.grp_head[h]);
 #endif
     if (mode == 3) {
       pfw::masq_conn_run(q, r);
@@ -4581,6 +4671,7 @@ dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ i
       fc.pf[r].mnat_ip[0] = e;
       atomicAdd(&fc.pf[r].mnat_ip[1], 1u);
 #endif
+      if (mode == 4) q.adm = fc.adm[r];
       pfw::resolve_one(q, fc.pf[r]);
     }
   }
@@ -4589,6 +4680,70 @@ dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ i
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   if ((threadIdx.x & 63) == 0 && v)
     atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), (unsigned long long)v);
+}
+
+// dp_nat_admit_plan (mode 4): each connection's creations and the new slots
+// each adds (pfw::admit_plan), or pf_cnt[17]: the burst runs on one lane.
+__global__ void __launch_bounds__(256) dp_nat_admit_plan(const uint8_t *__restrict__ img_base,
+                                                         const Image *__restrict__ im, dpf::FlowCtx fc) {
+  if (!fc.pf_cnt[1] || pfw::nat_mode(fc, true) != 4) return;
+  const Img g{img_base, *im};
+  const pfw::Seq q{fc, g, true};
+  const uint32_t ng = fc.pf_cnt[4];
+  for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < ng; e += gridDim.x * 256) {
+    const uint32_t h = fc.grp_list[e];
+    const uint32_t r = pfw::sort_conn(fc.grp_next, (uint32_t)fc.grp_head[h]);
+    // (the sorted list's head, for dp_nat_resolve)
+    fc.grp_head[h] = ((unsigned long long)fc.burst << 32) | r;
+    if (!pfw::admit_plan(q, r)) pfw::flag_once(&fc.pf_cnt[17]);
+  }
+}
+
+// dp_nat_admit_scan (mode 4): the new slots of the records before each, in
+// packet order -- three launches: (0) each 4096 records' sum, (1) their
+// exclusive prefix, (2) each record's.
+constexpr uint32_t kAdmChunk = 4096;
+__global__ void __launch_bounds__(1024) dp_nat_admit_scan(dpf::FlowCtx fc, int step) {
+  if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 4) return;
+  const uint32_t total = fc.pf_cnt[1], t = threadIdx.x;
+  __shared__ uint32_t sh[1024];
+  if (step == 1) {
+    const uint32_t nb = (total + kAdmChunk - 1) / kAdmChunk;  // <= 1024 (n <= 4M)
+    const uint32_t v = t < nb ? fc.adm_blk[t] : 0u;
+    sh[t] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+      const uint32_t x = t >= o ? sh[t - o] : 0u;
+      __syncthreads();
+      sh[t] += x;
+      __syncthreads();
+    }
+    if (t < nb) fc.adm_blk[t] = sh[t] - v;
+    return;
+  }
+  const uint32_t k0 = blockIdx.x * kAdmChunk + t * 4;
+  uint32_t w[4], c = 0;
+  for (int j = 0; j < 4; j++) {
+    w[j] = k0 + j < total ? fc.adm[fc.pf_of[fc.pf_order[k0 + j]]] : 0u;
+    c += w[j];
+  }
+  sh[t] = c;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    const uint32_t x = t >= o ? sh[t - o] : 0u;
+    __syncthreads();
+    sh[t] += x;
+    __syncthreads();
+  }
+  if (step == 0) {
+    if (t == 1023) fc.adm_blk[blockIdx.x] = sh[1023];
+    return;
+  }
+  uint32_t s = fc.adm_blk[blockIdx.x] + sh[t] - c;
+  for (int j = 0; j < 4; j++) {
+    if (k0 + j < total) fc.adm[fc.pf_of[fc.pf_order[k0 + j]]] = s;
+    s += w[j];
+  }
 }
 
 // dp_nat_lane_order: the allocating lane's records in packet order (every
@@ -5262,6 +5417,12 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   const uint32_t pb = (n + 1023) / 1024 < 256 ? (n + 1023) / 1024 : 256;
   hipLaunchKernelGGL(dp_nat_prep, dim3(pb), dim3(1024), 0, stream, img_base, im, fc);
   const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  // port forwarding near the capacity: the creations' admissions in packet order
+  hipLaunchKernelGGL(dp_nat_admit_plan, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
+  const uint32_t ab = (n + kAdmChunk - 1) / kAdmChunk;
+  hipLaunchKernelGGL(dp_nat_admit_scan, dim3(ab), dim3(1024), 0, stream, fc, 0);
+  hipLaunchKernelGGL(dp_nat_admit_scan, dim3(1), dim3(1024), 0, stream, fc, 1);
+  hipLaunchKernelGGL(dp_nat_admit_scan, dim3(ab), dim3(1024), 0, stream, fc, 2);
   hipLaunchKernelGGL(dp_nat_resolve<true>, dim3(1), dim3(64), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_resolve<false>, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   // a masquerading burst's allocating lane (its records in packet order)

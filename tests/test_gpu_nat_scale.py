@@ -93,23 +93,43 @@ def test_gpu_masquerade_at_scale():
         rg.close()
 
 
-@pytest.mark.parametrize("near_capacity", [False, True], ids=["room", "near-capacity"])
-def test_gpu_portfw_at_scale(near_capacity):
+@pytest.mark.parametrize("case", ["room", "near-capacity", "near-capacity-one-lane", "full"])
+def test_gpu_portfw_at_scale(case):
+    """270k new port-forwarded connections: with room (one lane per
+    connection), with room for 200k pairs (the admissions decided beforehand
+    in packet order, mode 4; and the same on one lane), and in a table already
+    at its capacity (every pair refused).  The table is pre-filled with 100k
+    unrelated flows."""
+    from dataplane_amd.flows import make_flow, flow_key
     ro, rg = OracleRunner(), GpuRunner(slots=1 << 21)
+    near = case.startswith("near")
+    fill = np.array([make_flow(flow_key(W.VPC_P, f"172.20.{i >> 8 & 255}.{i & 255}", f"172.21.{i >> 16}.1",
+                                        A.FLOW_UDP, 1000 + (i & 1023), 53), W.VPC_C) for i in range(100_000)])
     try:
         for r in (ro, rg):
             r.publish(W.tables())
             r.set_clock(10 ** 12)
-            if near_capacity:
-                (r.fl if hasattr(r, "fl") else r.ft).set_capacity(400_000)
+            ft = r.fl if hasattr(r, "fl") else r.ft
+            ft.insert(fill)
+            if near:
+                ft.set_capacity(100_000 + 400_000)
+            elif case == "full":
+                ft.set_capacity(90_000)
+        A.gpu_lib().dpf_debug_nat_sequential(3 if case.endswith("one-lane") else 0)
         buf, inp, npf = W.burst(300_000, 0.9, 0)
         out, ob, cnt = both(ro, rg, buf, inp, "port forwarding")
-        assert int(cnt[12]) == (1 if near_capacity else 2), cnt
+        want = {"room": 2, "near-capacity": 4, "near-capacity-one-lane": 1, "full": 4}[case]
+        assert int(cnt[12]) == want, cnt
         h = hist(out)
-        if near_capacity:
+        if near:
             assert h.get("FlowCapacityExceeded", 0) > 50_000, h
+            assert ro.count()[0] in (500_000, 500_001)
+        elif case == "full":
+            assert h.get("FlowCapacityExceeded", 0) == npf, h
+            assert ro.count()[0] == 100_000
         else:
             assert h == {"Delivered": 300_000}, h
-        assert ro.count()[0] in ((400_000, 400_001) if near_capacity else (2 * npf,))
+            assert ro.count()[0] == 100_000 + 2 * npf
     finally:
+        A.gpu_lib().dpf_debug_nat_sequential(0)
         rg.close()

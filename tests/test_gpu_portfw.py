@@ -82,19 +82,24 @@ def test_gpu_portfw_random_bursts(seed, n_conn, capacity, one_lane):
     and, with a small capacity, flow-pair creation refused at capacity; GPU ==
     oracle per burst (records, bytes, each packet's flow, every connection's
     two flows by key) and the flow counts.  The NAT pass runs one lane per
-    connection unless the capacity could bind (then, and with one_lane, one
-    lane in packet order)."""
+    connection, with the capacity admissions decided beforehand when the
+    capacity could bind (mode 4) -- unless a connection's creations cannot be
+    foreseen (then, and with one_lane, one lane in packet order)."""
     import pfgen
-    got = {}
+    got, modes = {}, []
     lib = A.gpu_lib()
     lib.dpf_debug_nat_sequential(1 if one_lane else 0)
     try:
         for name, mk in (("oracle", pfkat.OracleRunner), ("gpu", pfkat.GpuRunner)):
             r = mk(slots=1 << 14) if name == "gpu" else mk()
             steps = []
+
+            def on(k, res, buf, infos, look):
+                steps.append((res.copy(), buf.copy(), infos.copy(), look.copy(), r.count()))
+                if name == "gpu":
+                    modes.append(int(r.nat_counters()[12]))
             try:
-                pfgen.run(r, seed, n_conn, capacity, lambda k, res, buf, infos, look: steps.append(
-                    (res.copy(), buf.copy(), infos.copy(), look.copy(), r.count())))
+                pfgen.run(r, seed, n_conn, capacity, on)
             finally:
                 if name == "gpu":
                     r.close()
@@ -120,3 +125,8 @@ def test_gpu_portfw_random_bursts(seed, n_conn, capacity, one_lane):
     assert hist.get("Delivered", 0) > n_conn
     if capacity is not None:
         assert hist.get("FlowCapacityExceeded", 0) > 0
+        # bursts of first packets decide their admissions beforehand (mode 4)
+        if not one_lane:
+            assert 4 in modes, modes
+    elif not one_lane:
+        assert 2 in modes and 1 not in modes, modes
