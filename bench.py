@@ -199,24 +199,42 @@ def flows_leg(nf, w, dev, stream, steps: int) -> dict:
     _, res = ft.insert(fl)
     t_ins = time.perf_counter() - t0
     nf.attach_flows(ft)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps + 2)]
-    for k2 in range(steps + 2):
-        with torch.cuda.stream(stream):  # on the launch stream: no copy overlaps a launch
-            b[:w.buf.nbytes].copy_(pristine)
-        ev[k2][0].record(stream)
-        nf.process_device(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None, sptr,
-                          dev_meta=dmeta.data_ptr())
-        ev[k2][1].record(stream)
-    torch.cuda.synchronize(dev)
-    ms = sorted(a.elapsed_time(c) for a, c in ev[2:])
+    lib = A.gpu_lib()
+
+    def launches(full):
+        # full: the units an image with stateful NAT runs (a port-forwarding
+        # rule or a masquerade expose; dpf_debug_flows_full forces them here)
+        lib.dpf_debug_flows_full(1 if full else 0)
+        try:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(steps + 2)]
+            for k2 in range(steps + 2):
+                with torch.cuda.stream(stream):  # on the launch stream: no copy overlaps a launch
+                    b[:w.buf.nbytes].copy_(pristine)
+                ev[k2][0].record(stream)
+                nf.process_device(b.data_ptr(), bb, dinp.data_ptr(), dout.data_ptr(), n, None, sptr,
+                                  dev_meta=dmeta.data_ptr())
+                ev[k2][1].record(stream)
+            torch.cuda.synchronize(dev)
+            lean = lib.dpf_debug_last_lean()
+        finally:
+            lib.dpf_debug_flows_full(0)
+        ms = sorted(a.elapsed_time(c) for a, c in ev[2:])
+        return ms[len(ms) // 2], lean
+
+    med_full, lean_f = launches(True)
+    med, lean = launches(False)
     refs = dmeta.cpu().numpy().view(A.PKT_META)["flow_ref"]
     hit = int((refs != np.uint64(A.FLOW_NONE)).sum())
     nf.attach_flows(None)
     ln, act = ft.count()
     ft.close()
-    med = ms[len(ms) // 2]
     return {"mpps_median": round(n / (med / 1e3) / 1e6, 3), "launch_ms_median": round(med, 4),
+            "lean_units": bool(lean),
+            "full_units": {"mpps_median": round(n / (med_full / 1e3) / 1e6, 3),
+                           "launch_ms_median": round(med_full, 4), "lean_units": bool(lean_f),
+                           "what": "the same launches through the units an image with stateful NAT runs "
+                                   "(port forwarding / masquerade compiled in; context tables in LDS)"},
             "flows": int((res == A.FLOW_INSERTED).sum()), "table_slots": slots,
             "insert_s": round(t_ins, 3), "packets_with_flow": hit, "flows_active_after": int(act),
             "what": "the same burst with a flow table attached: every other packet's flow pair "

@@ -193,6 +193,7 @@ struct FlowCtx {
   // order (the table length its first insert meets); per 4096 records a sum
   uint32_t *adm, *adm_blk;
   uint32_t lean;        // the launch runs the flows variant without stateful NAT (dp_kernel.hip DP_SNAT)
+  uint32_t ctx;         // the image's context tables fit the LDS copy (Image.ctx_bytes; the full units 15 / 16)
 };
 
 // A packet whose ACL verdict was "allow: reply of a flow-scope-allowed flow";

@@ -70,7 +70,8 @@ constexpr bool SNAT = DP_SNAT;
 // lean flows units (9, 10) have it too: an image whose tables do not fit
 // runs the full flows variant.
 #ifndef DP_CTX
-#if DP_PART == 1 || DP_PART == 2 || DP_PART == 7 || DP_PART == 8 || DP_PART == 9 || DP_PART == 10
+#if DP_PART == 1 || DP_PART == 2 || DP_PART == 7 || DP_PART == 8 || DP_PART == 9 || DP_PART == 10 || \
+    DP_PART == 15 || DP_PART == 16
 #define DP_CTX 1
 #else
 #define DP_CTX 0
@@ -5228,6 +5229,8 @@ void dpk_run_pipeline_101(DP_RUN_ARGS);
 void dpk_run_pipeline_111(DP_RUN_ARGS);
 void dpk_run_pipeline_100s(DP_RUN_ARGS);
 void dpk_run_pipeline_110s(DP_RUN_ARGS);
+void dpk_run_pipeline_100c(DP_RUN_ARGS);
+void dpk_run_pipeline_110c(DP_RUN_ARGS);
 void dpk_run_pipeline_000n(DP_RUN_ARGS);
 void dpk_run_pipeline_010n(DP_RUN_ARGS);
 void dpk_run_pipeline_000wn(DP_RUN_ARGS);
@@ -5274,6 +5277,12 @@ DP_RUNNER(dpk_run_pipeline_100s, true, false, false)
 #endif
 #if DP_PART == 10 || DP_PART < 0
 DP_RUNNER(dpk_run_pipeline_110s, true, true, false)
+#endif
+#if DP_PART == 15 || DP_PART < 0  // (the full flows first pass with the context tables in LDS)
+DP_RUNNER(dpk_run_pipeline_100c, true, false, false)
+#endif
+#if DP_PART == 16 || DP_PART < 0
+DP_RUNNER(dpk_run_pipeline_110c, true, true, false)
 #endif
 #if DP_IN_PART(0)
 #if defined(DP_TIMING)
@@ -5406,10 +5415,13 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
     if (meta) dpk_run_pipeline_110s(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
     else dpk_run_pipeline_100s(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   } else {
-  // first pass; PortForwarder's records in packet order; the replay of the
-  // packets that reached it (dp_nat_resolve's decisions)
-  if (meta) dpk_run_pipeline_110(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
-  else dpk_run_pipeline_100(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+  // first pass (the context tables from LDS when they fit); PortForwarder's
+  // records in packet order; the replay of the packets that reached it
+  // (dp_nat_resolve's decisions)
+  if (meta) (fc.ctx ? dpk_run_pipeline_110c : dpk_run_pipeline_110)(blocks, stream, img_base, im, buf, buf_bytes, in,
+                                                                    out, meta, n, part, fc);
+  else (fc.ctx ? dpk_run_pipeline_100c : dpk_run_pipeline_100)(blocks, stream, img_base, im, buf, buf_bytes, in, out,
+                                                               meta, n, part, fc);
   // the NAT pass: records filed by connection, then resolved
   // (grids of about one chip's worth of resident lanes: a burst with no
   // records leaves at once -- 8192 empty workgroups cost 76 us; more lanes

@@ -685,6 +685,7 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.lean = !ft->snat_seen && !img->im.v6w_c && !img->im.v6w_fib && img->im.ctx_bytes &&
               !g_flows_full.load(std::memory_order_relaxed);
     g_last_lean.store(fc.lean, std::memory_order_relaxed);
+    fc.ctx = img->im.ctx_bytes != 0 && !g_no_ctx.load(std::memory_order_relaxed);
     // (two bitmaps: the packets that reached the NAT stages, then the
     // masquerading burst's allocating lane, dp_nat_lane_order)
     if (words + sum_words > c->pf_bits_n) {
