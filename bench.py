@@ -284,7 +284,9 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
             # order before the connections run: mode 4)
             cap = min(10_000_000, slots // 2)  # FlowTable::DEFAULT_CAPACITY, at most half the slots
             ft.set_capacity(cap)
-            filled = max(0, cap - npf - int(ft.count()[0]))
+            clock[0] += hour
+            ft.sweep(clock[0])  # (the last leg's flows gone)
+            filled = max(0, cap - npf)
             fl = np.zeros(filled, A.FLOW)
             i = np.arange(filled, dtype=np.uint64)
             fl["key"]["src_vni"], fl["key"]["family"], fl["key"]["kind"] = W.VPC_P, 4, A.FLOW_UDP
@@ -329,7 +331,7 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
                 "mpps_median": round(n / (med / 1e3) / 1e6, 3), "flows_after": int(flows), "launches": len(keep),
                 "done_histogram": done}
 
-    def run_established(reps, conns=200_000, new_share=0.01, fwd_share=0.6):
+    def run_established(reps, conns=500_000, new_share=0.01, fwd_share=0.6):
         """Every packet masqueraded: `conns` connections opened by an untimed
         burst, then 2M-packet bursts of which 99 % belong to them (the
         clients' packets and the servers' answers to the public tuples,
@@ -367,7 +369,18 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
             done = {A.DONE_NAMES[d]: int(x) for d, x in zip(*np.unique(out["done"], return_counts=True))}
         keep = ms[1:] if len(ms) > 1 else ms
         med = sorted(keep)[len(keep) // 2]
+        # every flow expires: the sweep drops them and gives their tuples back
+        # (the release kernels, one lane per address record)
+        flows_before = int(ft.count()[0])
+        clock[0] += hour
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        swept = ft.sweep(clock[0])
+        sweep_ms = (time.perf_counter() - t0) * 1e3
         return {"established_connections": conns, "learnt": learnt, "new_share": new_share,
+                "sweep": {"flows": flows_before, "removed": int(swept) if swept is not None else None,
+                          "ms": round(sweep_ms, 3),
+                          "what": "dp_flow_sweep of every flow (expired), its allocations released"},
                 "client_share": fwd_share, "launch_ms_median": round(med, 4), "launch_ms": [round(x, 4) for x in ms],
                 "mpps_median": round(n / (med / 1e3) / 1e6, 3), "flows_after": int(ft.count()[0]),
                 "launches": len(keep), "nat_pass": cnts[-1], "done_histogram": done}

@@ -175,7 +175,8 @@ struct FlowCtx {
   // wave batches, [15] allocations on the lane alone, [16] pairs the split
   // pass could not create (never: it runs only with room; counters for tests).
   // Port forwarding without room for every pair (dp_nat_admit_*): [17] a
-  // connection whose creations the admission pass cannot foresee
+  // connection whose creations the admission pass cannot foresee.  [18]
+  // records the allocating lane ran alone (live flow state, or no room)
   unsigned long long *grp_tab, *grp_head, *grp_next;
   uint32_t *grp_list;
   uint32_t grp_mask;

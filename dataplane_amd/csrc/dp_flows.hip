@@ -94,9 +94,14 @@ __device__ void fill_info(const FlowSlot *slots, uint32_t mask, uint32_t sl, dp_
 // A flow leaving the table drops its FlowInfo, and with it the allocation its
 // masquerade state owns (the Drop of its AllocatedPort, port_alloc.rs:
 // 553-565): the (address record, port) goes on the call's release list, which
-// one thread of fl_release_k works through afterwards (the allocator is
-// sequential state).  false: the list is full -- the caller keeps the flow
-// for a later round.
+// the release kernels work through afterwards: the entries chained per address
+// record and port block (fl_rel_link_k), each block's releases by one lane
+// (fl_rel_run_k: a block's bitmap and count are its own, the address's
+// counters atomic), then the addresses left
+// without a block leave their region's list and bitmap one by one
+// (fl_rel_kill_k: shared state; their order changes only which free record a
+// later address takes).  false: the list is full -- the caller keeps the
+// flow for a later round.
 struct MqRel {
   uint32_t gen;   // the table's allocator generation (allocations of older ones are gone)
   uint32_t cap;
@@ -111,10 +116,44 @@ __device__ __forceinline__ bool mq_depart(const MqRel &r, const FlowSlot &s) {
   r.list[2 * k + 1] = s.pf >> 16;
   return true;
 }
+// per (address record, port block): the head of its chain of releases
+// (kNone: none); per entry the next one; after the heads, the count of
+// addresses to kill, then them
+__global__ void __launch_bounds__(kTB) fl_rel_link_k(uint8_t *mq, const uint32_t *list, const uint32_t *cnt,
+                                                    uint32_t cap, uint32_t *head, uint32_t *next) {
+  const dpm::View V{mq};
+  const uint32_t n = *cnt < cap ? *cnt : cap;
+  for (uint32_t k = blockIdx.x * kTB + threadIdx.x; k < n; k += gridDim.x * kTB) {
+    const uint32_t r = list[2 * k];
+    next[k] = r < V.h().n_recs ? atomicExch(&head[256 * r + (list[2 * k + 1] >> 8)], k) : dpm::kNone;
+  }
+}
+__global__ void __launch_bounds__(kTB) fl_rel_run_k(uint8_t *mq, const uint32_t *list, uint32_t *head,
+                                                   const uint32_t *next, uint32_t *kill) {
+  const dpm::View V{mq};
+  const uint32_t nb = V.h().n_recs * 256;
+  for (uint32_t b = blockIdx.x * kTB + threadIdx.x; b < nb; b += gridDim.x * kTB) {
+    uint32_t k = head[b];
+    if (k == dpm::kNone) continue;
+    head[b] = dpm::kNone;  // (ready for the next call)
+    bool dead = false;
+    for (; k != dpm::kNone; k = next[k]) dead |= dpm::release_par(V, b >> 8, list[2 * k + 1]);
+    if (dead) kill[1 + atomicAdd(&kill[0], 1u)] = b >> 8;
+  }
+}
+// (without the chains' memory: every release by one lane, in list order)
 __global__ void fl_release_k(uint8_t *mq, const uint32_t *list, const uint32_t *cnt, uint32_t cap) {
   const dpm::View V{mq};
   const uint32_t n = *cnt < cap ? *cnt : cap;
   for (uint32_t k = 0; k < n; k++) dpm::release(V, list[2 * k], list[2 * k + 1]);
+}
+__global__ void fl_rel_kill_k(uint8_t *mq, uint32_t *kill) {
+  const dpm::View V{mq};
+  for (uint32_t k = 0; k < kill[0]; k++) {
+    const uint32_t r = kill[1 + k];
+    if (V.recs()[r].region != dpm::kNone && V.recs()[r].live_blocks == 0) dpm::addr_kill(V, r);
+  }
+  kill[0] = 0;
 }
 
 __global__ void __launch_bounds__(kTB) fl_find_k(const FlowSlot *slots, uint32_t mask, uint32_t max_probe,
@@ -391,7 +430,27 @@ bool rel_list(dp_flow_table *ft, uint32_t cap, hipStream_t st, MqRel &r) {
   return true;
 }
 void rel_run(dp_flow_table *ft, const MqRel &r, hipStream_t st) {
-  if (r.list) hipLaunchKernelGGL(fl_release_k, dim3(1), dim3(1), 0, st, ft->mq, r.list, r.cnt, r.cap);
+  if (!r.list) return;
+  // per-record chains: heads (all kNone between calls) and the kill list,
+  // sized for the allocator's records; links per release entry
+  const uint32_t nr = ft->mq_recs;
+  uint32_t *h = static_cast<uint32_t *>(ft->mq_heads.get(sizeof(uint32_t) * (257 * (size_t)nr + 2)));
+  uint32_t *nx = static_cast<uint32_t *>(ft->mq_next.get(sizeof(uint32_t) * ((size_t)r.cap + 1)));
+  if (!h || !nx || !nr) {  // (no memory for the chains: one lane, in list order)
+    hipLaunchKernelGGL(fl_release_k, dim3(1), dim3(1), 0, st, ft->mq, r.list, r.cnt, r.cap);
+    return;
+  }
+  if (h != ft->mq_heads_at || nr != ft->mq_heads_n) {  // fresh buffer: no chain, no kill list
+    (void)hipMemsetAsync(h, 0xff, sizeof(uint32_t) * 256 * (size_t)nr, st);
+    (void)hipMemsetAsync(h + 256 * (size_t)nr, 0, sizeof(uint32_t) * (nr + 2), st);
+    ft->mq_heads_at = h;
+    ft->mq_heads_n = nr;
+  }
+  const uint32_t gb = blocks_for(r.cap) < 1024 ? blocks_for(r.cap) : 1024;
+  hipLaunchKernelGGL(fl_rel_link_k, dim3(gb ? gb : 1), dim3(kTB), 0, st, ft->mq, r.list, r.cnt, r.cap, h, nx);
+  const uint32_t rb = blocks_for(256ull * nr) < 4096 ? blocks_for(256ull * nr) : 4096;
+  hipLaunchKernelGGL(fl_rel_run_k, dim3(rb ? rb : 1), dim3(kTB), 0, st, ft->mq, r.list, h, nx, h + 256 * (size_t)nr);
+  hipLaunchKernelGGL(fl_rel_kill_k, dim3(1), dim3(1), 0, st, ft->mq, h + 256 * (size_t)nr);
 }
 
 // The table's device words ([0] probe bound, [2..3] len): bursts that create
@@ -823,6 +882,7 @@ int dpf_masq_sync(dp_flow_table *ft, const std::shared_ptr<const dpd::MasqConfig
       if (rc) return rc;
       (void)hipFree(ft->mq);
       ft->mq = nullptr;
+      ft->mq_recs = 0;
       ft->mq_cfg.reset();
       ft->mq_gen = 0;
     }
@@ -924,6 +984,7 @@ int dpf_masq_sync(dp_flow_table *ft, const std::shared_ptr<const dpd::MasqConfig
   if (ft->mq) (void)hipFree(ft->mq);
   ft->mq = dev;
   ft->mq_gen = gen;
+  ft->mq_recs = reinterpret_cast<const dpm::Header *>(buf.data())->n_recs;
   ft->mq_cfg = cfg;
   ft->mq_serial = serial;
   return 0;
@@ -976,6 +1037,8 @@ int dp_flow_table_destroy(dp_flow_table_t *ft) {
   (void)hipFree(ft->d_meta);
   if (ft->mq) (void)hipFree(ft->mq);
   ft->mq_rel.release();
+  ft->mq_heads.release();
+  ft->mq_next.release();
   for (auto &x : ft->scr) x.release();
   (void)hipEventDestroy(ft->last_burst);
   (void)hipStreamDestroy(ft->stream);

@@ -66,6 +66,13 @@ struct dp_flow_table {
   std::shared_ptr<const dpd::MasqConfig> mq_cfg;
   uint64_t mq_serial = 0;
   FlowScratch mq_rel;
+  // the release kernels' per-record chain heads and kill list (dp_flows.hip
+  // rel_run; all heads kNone between calls), per-entry links; the allocator's
+  // address records
+  FlowScratch mq_heads, mq_next;
+  uint32_t *mq_heads_at = nullptr;
+  uint32_t mq_heads_n = 0;
+  uint32_t mq_recs = 0;
   // a burst under an image that configures stateful NAT ran on the table (its
   // flows may carry NAT state from then on): bursts keep the full flows variant
   bool snat_seen = false;

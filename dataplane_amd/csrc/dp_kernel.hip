@@ -4291,6 +4291,16 @@ __device__ __forceinline__ uint32_t nat_mode(const dpf::FlowCtx &fc, bool pre = 
 __device__ __forceinline__ void flag_once(uint32_t *w) {
   if (!__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicOr(w, 1u);
 }
+// flag_once for the wave: one lane of those that want it (a chip's worth of
+// lanes reading one word would queue at its L2 channel)
+__device__ __forceinline__ void flag_wave(uint32_t *w, bool want) {
+#ifdef DP_EMU
+  if (want) flag_once(w);
+#else
+  const uint64_t m = __ballot(want);
+  if (m && (int)(threadIdx.x & 63) == __ffsll((long long)m) - 1) flag_once(w);
+#endif
+}
 
 // Could this record's packet be given a tuple (an expose covers its initial
 // source) while its initial destination is a public address of the
@@ -4449,17 +4459,28 @@ __device__ bool admit_plan(const Seq &q, uint32_t list) {
       closing = true;
   }
   if (!pure && !held) return false;
-  bool first = pure;
+  // (a group may hold several connections -- keys that collide in the hash
+  // merge them: a creation adds slots unless an earlier one of the group
+  // made the same pair)
   for (uint32_t r = list; r != dpf::kNoSlot; r = (uint32_t)link_ld(&fc.grp_next[r])) {
     const dpf::PfReq &R = fc.pf[r];
     uint32_t w = 0;
     dpf::FKey rk, fk;
-    if (first && creation_rk(q.g, R, rk)) {
-      creation_fk(R, fk);
-      uint32_t st;
-      uint4 v, x;
-      w = (flow_probe(fc, fk, st, v, x) == dpf::kNoSlot ? 1u : 0u) + (flow_probe(fc, rk, st, v, x) == dpf::kNoSlot ? 1u : 0u);
-      first = false;
+    if (pure && creation_rk(q.g, R, rk)) {
+      bool again = false;
+      for (uint32_t p = list; p != r && !again; p = (uint32_t)link_ld(&fc.grp_next[p])) {
+        dpf::FKey pk;
+        if (!creation_rk(q.g, fc.pf[p], pk)) continue;
+        again = true;
+        for (int j = 0; j < 11; j++) again = again && pk.w[j] == rk.w[j];
+      }
+      if (!again) {
+        creation_fk(R, fk);
+        uint32_t st;
+        uint4 v, x;
+        w = (flow_probe(fc, fk, st, v, x) == dpf::kNoSlot ? 1u : 0u) +
+            (flow_probe(fc, rk, st, v, x) == dpf::kNoSlot ? 1u : 0u);
+      }
     }
     fc.adm[r] = w;
   }
@@ -4546,10 +4567,10 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
     dpf::PfReq &R = fc.pf[rec];
     if (!(R.bits & dpf::kPqReached)) continue;  // a flow-filter record of a packet dropped before NAT
     uint32_t key;
-    if (R.bits & dpf::kPqPf) pfw::flag_once(&fc.pf_cnt[9]);
+    pfw::flag_wave(&fc.pf_cnt[9], R.bits & dpf::kPqPf);
+    pfw::flag_wave(&fc.pf_cnt[8], R.bits & dpf::kPqMasq);
     if (R.bits & dpf::kPqMasq) {
-      pfw::flag_once(&fc.pf_cnt[8]);
-      if (pfw::masq_back(fc, R)) pfw::flag_once(&fc.pf_cnt[10]);
+      pfw::flag_wave(&fc.pf_cnt[10], pfw::masq_back(fc, R));
       if (!pfw::masq_conn(fc, R, key)) {
         pfw::lane_mark(fc, R, 0u);
         continue;
@@ -4754,7 +4775,10 @@ __global__ void __launch_bounds__(1024) dp_nat_lane_order(dpf::FlowCtx fc) {
   if (threadIdx.x == 0) fc.pf_cnt[11] = total;
 }
 
-__device__ __forceinline__ void agent_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); }
+// The allocating lane is one workgroup: its lanes' stores and later loads
+// need workgroup-scope order only (an agent-scope fence would write back and
+// invalidate the XCD's L2 every time)
+__device__ __forceinline__ void lane_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
 // dp_nat_lane: the split pass's allocating lane (mode 3), one wave over its
 // records in packet order, 64 at a time.  A record whose outcome rests on
@@ -4785,7 +4809,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   __shared__ int s_pd[64];           // the lane's latest earlier lane with the same initial key
   __shared__ uint32_t s_bm[8];       // the thread block's usage bitmap
   __shared__ uint32_t s_b[8];        // (fast, address record, block, free ports, address words)
-  uint32_t fast_n = 0, lone_n = 0;
+  uint32_t fast_n = 0, lone_n = 0, solo_n = 0;
   for (uint32_t k0 = 0; k0 < nl; k0 += 64) {
     const uint32_t cnt = nl - k0 < 64 ? nl - k0 : 64;
     const bool has = (uint32_t)t < cnt;
@@ -4835,8 +4859,9 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           } else {
             pfw::resolve_one(qs, R);
           }
+          solo_n++;
         }
-        agent_fence();
+        lane_fence();
         i++;
         continue;
       }
@@ -4932,16 +4957,21 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           }
           __syncthreads();
           if (t == p) {
-            // the block's bitmap after `taken` allocations: its lowest free ports
+            // the block's bitmap after `taken` allocations: its lowest free
+            // ports (built from the copy, stored once)
             dpm::Addr &A = V.recs()[a];
-            uint32_t left = taken;
-            for (int x = 0; x < 8 && left; x++)
-              while (left && ~A.bm[tb][x]) {
-                A.bm[tb][x] |= 1u << (__ffs(~A.bm[tb][x]) - 1);
+            uint32_t left = taken, full = 0xffffffffu;
+            for (int x = 0; x < 8; x++) {
+              uint32_t w = s_bm[x];
+              while (left && ~w) {
+                w |= ~w & (w + 1);  // the lowest clear bit
                 left--;
               }
+              A.bm[tb][x] = w;
+              full &= w;
+            }
             A.blive[tb] = (uint16_t)(A.blive[tb] + taken);
-            if (dpm::bm_full(A.bm[tb])) A.nonfull--;
+            if (full == 0xffffffffu) A.nonfull--;
             fast_n += taken;
           }
         } else if (t == p) {
@@ -4958,7 +4988,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           done = true;
           lone_n++;
         }
-        agent_fence();
+        lane_fence();
         __syncthreads();
       }
       // the run's pairs, in parallel (distinct initial keys; distinct tuples)
@@ -4967,10 +4997,10 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         if (!pfw::masq_pair(qp, R, m, rec, aport, aip, give_back)) atomicAdd(&fc.pf_cnt[16], 1u);
         ok = false;
       }
-      agent_fence();
+      lane_fence();
       for (uint64_t gb = __ballot(give_back); gb; gb &= gb - 1) {
         if (t == __ffsll((long long)gb) - 1) dpm::release(V, rec, aport);
-        agent_fence();
+        lane_fence();
       }
       i = j;
     }
@@ -4980,9 +5010,9 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
     // allocations their masquerade state owns
     for (uint32_t k = 0; k < fc.pf_cnt[3]; k++) dpm::release(V, fc.mq_rel[2 * k], fc.mq_rel[2 * k + 1]);
   }
-  uint32_t ln = lone_n, fn = fast_n;
-  for (int o = 32; o > 0; o >>= 1) { ln += __shfl_xor(ln, o); fn += __shfl_xor(fn, o); }
-  if (t == 0) fc.pf_cnt[14] += fn;
+  uint32_t ln = lone_n, fn = fast_n, sn = solo_n;
+  for (int o = 32; o > 0; o >>= 1) { ln += __shfl_xor(ln, o); fn += __shfl_xor(fn, o); sn += __shfl_xor(sn, o); }
+  if (t == 0) { fc.pf_cnt[14] += fn; fc.pf_cnt[18] += sn; }
   uint32_t v = qp.added;
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   if (t == 0) {

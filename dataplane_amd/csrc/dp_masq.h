@@ -329,13 +329,15 @@ __host__ __device__ inline void block_new(const View &v, uint32_t r, uint32_t id
   if (!bm_full(A.bm[idx])) A.nonfull++;
 }
 // The block's last port went (Drop of AllocatedPortBlock: deallocate_block,
-// port_alloc.rs:200-212), and with its last block the address
-__host__ __device__ inline void block_die(const View &v, uint32_t r, uint32_t idx) {
+// port_alloc.rs:200-212), and with its last block the address (unless
+// `keep`: the caller kills it later -- releases run per address in parallel,
+// the address list and bitmap are shared)
+__host__ __device__ inline void block_die(const View &v, uint32_t r, uint32_t idx, bool keep = false) {
   Addr &A = v.recs()[r];
   if (!bm_full(A.bm[idx])) A.nonfull--;
   A.bflag[idx] = 1;  // free again
   A.usable++;
-  if (--A.live_blocks == 0) addr_kill(v, r);
+  if (--A.live_blocks == 0 && !keep) addr_kill(v, r);
 }
 // allocate_port_from_block (port_alloc.rs:449-471): the lowest free port
 __host__ __device__ inline uint32_t block_take(const View &v, uint32_t r, uint32_t idx, bool allow_null,
@@ -356,20 +358,48 @@ __host__ __device__ inline uint32_t block_take(const View &v, uint32_t r, uint32
   return NO_FREE_PORT;
 }
 
-// Drop of an AllocatedPort (port_alloc.rs:553-565): the port, then possibly
-// its block and address
-__host__ __device__ inline void release(const View &v, uint32_t r, uint32_t port) {
-  if (r >= v.h().n_recs) return;
+// The releases of one block of one address, run beside other blocks'
+// (dp_flows.hip fl_rel_run_k): the block's bitmap and live count are the
+// caller's own, the address's counters are shared with the lanes of its other
+// blocks (atomic).  Returns true when the address lost its last block (the
+// caller kills it afterwards).
+__device__ inline bool release_par(const View &v, uint32_t r, uint32_t port) {
   Addr &A = v.recs()[r];
-  if (A.region == kNone) return;
+  if (A.region == kNone) return false;
   const uint32_t idx = A.inv[port >> 8], off = port & 0xffu;
-  if (!(A.bflag[idx] & 2)) return;
+  if (!(A.bflag[idx] & 2)) return false;
   uint32_t *bm = A.bm[idx];
-  if (!(bm[off >> 5] & (1u << (off & 31)))) return;  // never taken (the reference logs it)
+  if (!(bm[off >> 5] & (1u << (off & 31)))) return false;
+  const bool was_full = bm_full(bm);
+  bm[off >> 5] &= ~(1u << (off & 31));
+  if (was_full) atomicAdd(&A.nonfull, 1u);
+  if (--A.blive[idx] != 0) return false;
+  // block_die, the address's counters shared
+  atomicSub(&A.nonfull, 1u);  // (not full: a port just went)
+  A.bflag[idx] = 1;
+  atomicAdd(&A.usable, 1u);
+  return atomicSub(&A.live_blocks, 1u) == 1u;
+}
+
+// Drop of an AllocatedPort (port_alloc.rs:553-565): the port, then possibly
+// its block and address.  keep: as block_die; returns true when the address
+// lost its last block (and was kept).
+__host__ __device__ inline bool release(const View &v, uint32_t r, uint32_t port, bool keep = false) {
+  if (r >= v.h().n_recs) return false;
+  Addr &A = v.recs()[r];
+  if (A.region == kNone) return false;
+  const uint32_t idx = A.inv[port >> 8], off = port & 0xffu;
+  if (!(A.bflag[idx] & 2)) return false;
+  uint32_t *bm = A.bm[idx];
+  if (!(bm[off >> 5] & (1u << (off & 31)))) return false;  // never taken (the reference logs it)
   const bool was_full = bm_full(bm);
   bm[off >> 5] &= ~(1u << (off & 31));
   if (was_full) A.nonfull++;
-  if (--A.blive[idx] == 0) block_die(v, r, idx);
+  if (--A.blive[idx] == 0) {
+    block_die(v, r, idx, keep);
+    return keep && A.live_blocks == 0;
+  }
+  return false;
 }
 
 // PortAllocator::allocate_port (port_alloc.rs:264-284): the thread block if it

@@ -543,14 +543,19 @@ int dp_tables_publish(dp_ctx_t *c, const dp_tables_desc_t *tables) {
     dt.pf = std::move(pf);
   }
   // the attached flow tables' allocators follow the new config now (a table
-  // attached later syncs at its first burst)
+  // attached later syncs at its first burst).  Every table is tried; the first
+  // failure is returned, with the new image already published: a table that
+  // failed keeps its old allocator and tries again at its next burst (which
+  // fails the burst, whole, while the sync does)
   {
     std::lock_guard<std::mutex> reg(dt.reg_mu);
+    int first = 0;
     for (auto &kv : dt.fts) {
       std::lock_guard<std::mutex> lk(kv.first->mu);
-      if ((rc = dpf_masq_sync(kv.first, img->masq, img->im.genid, img->serial)))
-        return fail(rc, "masquerade allocator update");
+      const int r = dpf_masq_sync(kv.first, img->masq, img->im.genid, img->serial);
+      if (r && !first) first = r;
     }
+    if (first) return fail(first, "masquerade allocator update (the new tables are published)");
   }
   // `old` is retired here only if no in-flight burst still references it
   return 0;

@@ -526,7 +526,12 @@ int dp_ctx_destroy(dp_ctx_t *ctx);
  * Replaces left-right FibWriter publish / NatTablesWriter::update_nat_tables /
  * FlowFilterContextWriter::store / AclFilterContextWriter::store
  *  for every context on the device.  Never blocks a burst
- * beyond a pointer swap; the old image is retired once bursts using it end. */
+ * beyond a pointer swap; the old image is retired once bursts using it end.
+ * The attached flow tables' masquerade allocators follow the new
+ * configuration within the call; if one cannot (device memory), the call
+ * still publishes the tables, updates every other flow table, and returns the
+ * first error -- the failed table tries again at its next burst, and that
+ * burst fails whole (DP_DONE_INTERNAL_FAILURE) while it cannot. */
 int dp_tables_publish(dp_ctx_t *ctx, const dp_tables_desc_t *tables);
 
 /* Current generation id (PipelineData::genid). */

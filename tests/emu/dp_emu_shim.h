@@ -28,6 +28,7 @@ static inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long l
 // single-threaded host emulation: plain read-modify-write
 static inline uint32_t atomicAdd(uint32_t *p, uint32_t v) { uint32_t o = *p; *p = o + v; return o; }
 static inline uint32_t atomicOr(uint32_t *p, uint32_t v) { uint32_t o = *p; *p = o | v; return o; }
+static inline uint32_t atomicSub(uint32_t *p, uint32_t v) { uint32_t o = *p; *p = o - v; return o; }
 static inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) {
   unsigned long long o = *p; *p = o + v; return o;
 }

@@ -86,7 +86,7 @@ def test_gpu_masquerade_at_scale():
         buf, inp, nn = c.burst(300_000, 0.01, 0.6, step=2)
         out, ob, cnt = both(ro, rg, buf, inp, "established burst near capacity")
         h = hist(out)
-        assert int(cnt[12]) == 3 and int(cnt[14]) == 0 and int(cnt[15]) > 0, cnt
+        assert int(cnt[12]) == 3 and int(cnt[14]) == 0 and int(cnt[18]) == int(cnt[11]), cnt
         assert h.get("FlowCapacityExceeded", 0) > 1000 and h["Delivered"] > 290_000, h
         assert same_flows(ro, rg, keys, "established burst near capacity") == 250_000
     finally:
