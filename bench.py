@@ -268,11 +268,12 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
 
     def counters():
         import ctypes as C
-        c = (C.c_uint32 * 24)()
-        lib.dpf_debug_nat_counters(nf2.ctx, c, 24)
+        c = (C.c_uint32 * 32)()
+        lib.dpf_debug_nat_counters(nf2.ctx, c, 32)
         return {"mode": int(c[12]), "records": int(c[1]), "lane_records": int(c[11]),
                 "left_by_connections": int(c[13]), "allocations_batched": int(c[14]),
-                "allocations_alone": int(c[15])}
+                "allocations_alone": int(c[15]), "lane_kticks": [int(c[19 + k]) for k in range(7)],
+                "allocation_steps": int(c[26]), "steady_refreshes": bool(c[27])}
 
     def run(share, reps, one_lane=False, near_capacity=False):
         buf, inp, npf = W.burst(n, share, 0, kind=kind)

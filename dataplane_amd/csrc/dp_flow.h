@@ -52,7 +52,10 @@ struct alignas(128) FlowSlot {
   // address record + 1 (0: none) and the allocator generation it lives in
   uint32_t mq_rec;
   uint32_t mq_gen;
-  uint32_t pad;
+  // the burst (FlowCtx::burst) in which a masquerading record of this flow's
+  // pair may change its NatFlowStatus (dp_nat_mark: its refreshes are then
+  // not order-free)
+  uint32_t nat_tag;
 };
 static_assert(sizeof(FlowSlot) == 128, "one L2 line per slot");
 
@@ -118,11 +121,15 @@ constexpr uint32_t kPqQuery = 1u << 12;   // its flow key is an ICMP query's (ec
 // already ran (its connection's lane left it there)
 constexpr uint32_t kPqLane = 1u << 13;
 constexpr uint32_t kPqPfDone = 1u << 14;
+// a masquerading refresh that commutes with every other record of the burst
+// (dp_nat_prep: no record of its connection changes the pair's state this
+// burst); dp_nat_steady resolves it
+constexpr uint32_t kPqSteady = 1u << 15;
 constexpr uint32_t kPfForward = 0xffu;
 
 // words of FlowCtx::pf_cnt
-constexpr uint32_t kCntWords = 24;
-#define DPF_CNT_WORDS 24
+constexpr uint32_t kCntWords = 32;
+#define DPF_CNT_WORDS 32
 
 // The launch-time view of a flow table for one burst.
 struct FlowCtx {
@@ -176,7 +183,11 @@ struct FlowCtx {
   // pass could not create (never: it runs only with room; counters for tests).
   // Port forwarding without room for every pair (dp_nat_admit_*): [17] a
   // connection whose creations the admission pass cannot foresee.  [18]
-  // records the allocating lane ran alone (live flow state, or no room)
+  // records the allocating lane ran alone (live flow state, or no room);
+  // [19..22] its time in plans, allocations, pairs and records alone (1024
+  // clock64 ticks), [23..25] the allocations' parts (the set's address and
+  // block, serving the records, the block's update), [26] allocation steps,
+  // [27] a steady refresh in the burst (kPqSteady)
   unsigned long long *grp_tab, *grp_head, *grp_next;
   uint32_t *grp_list;
   uint32_t grp_mask;
@@ -189,6 +200,7 @@ struct FlowCtx {
   // the masquerading burst's allocating lane: its packets (bitmap by packet
   // index + summary, as pf_bits) and their order
   uint32_t *lane_bits, *lane_sum, *lane_order;
+  uint4 *lane_plan;     // per lane record: its class and plan (dp_nat_lane_plan, 128 B)
   // port forwarding near the capacity (mode 4): per record the new slots its
   // creation adds, then the sum of those of the records before it in packet
   // order (the table length its first insert meets); per 4096 records a sum

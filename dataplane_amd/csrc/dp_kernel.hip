@@ -3873,6 +3873,14 @@ struct MPlan {
   bool eqp;               // the reverse key may equal the initial one (related_pair)
 };
 
+// A record of the allocating lane as dp_nat_lane_plan leaves it: 1 alone
+// (live flow state decides it, or no room), 2 decided, 3 allocates
+struct LanePlan {
+  uint32_t rec, cls;
+  MPlan m;
+};
+static_assert(sizeof(LanePlan) == 128, "one plan: eight 16-byte words");
+
 // Is the record's flow valid for Masquerade with state (get_masquerade_state,
 // nf.rs:198-213): the attached fill, Active for this packet (its own
 // PortForwarder step included), holding masquerade state.
@@ -4346,7 +4354,7 @@ __device__ bool masq_conn(const dpf::FlowCtx &fc, const dpf::PfReq &R, uint32_t 
   return true;
 }
 
-// A record for the allocating lane: its bit by packet index (dp_nat_lane_order)
+// A record for the allocating lane: its bit by packet index (dp_bits_*, which 1)
 __device__ __forceinline__ void lane_mark(const dpf::FlowCtx &fc, dpf::PfReq &R, uint32_t more) {
   R.bits |= dpf::kPqLane | more;
   const uint32_t i = R.idx;
@@ -4354,6 +4362,59 @@ __device__ __forceinline__ void lane_mark(const dpf::FlowCtx &fc, dpf::PfReq &R,
   uint32_t *sw = &fc.lane_sum[i >> 15];
   const uint32_t sb = 1u << ((i >> 10) & 31);
   if (!(__hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & sb)) atomicOr(sw, sb);
+}
+
+// A masquerading record whose refresh leaves its pair's state as it is:
+// valid with masquerade state (get_masquerade_state), no ACL flow verdict, a
+// NatFlowStatus that the packet does not move (refresh_masquerade_state, nf.rs:
+// 151-194, with nw == cur, neither closed nor reset) on a pair that holds a
+// live allocation (masq_conn_ok's conditions for the record's own pair).  Its
+// outcome is a function of the pair as the burst found it -- if no other
+// record of the connection moves the state -- and its one write, the expiry's
+// push forward, is a maximum: it commutes with the burst's other records.
+// move: the record may move the state (its pair is tagged for the burst).
+__device__ bool masq_steady(const Seq &q, const dpf::PfReq &R, bool &move) {
+  const dpf::FlowCtx &fc = q.fc;
+  move = false;
+  if ((R.bits & (dpf::kPqMasq | dpf::kPqPf | dpf::kPqSens)) != dpf::kPqMasq) return false;
+  if (R.slot > fc.mask || !fc.mq || !masq_valid(q, R)) return false;
+  const dpf::FlowSlot &f = fc.slots[R.slot];
+  const uint32_t proto = R.proto & 0xffu, tfl = R.proto >> 16;
+  uint32_t src[4], dst[4], sport, dport;
+  masq_cur(R, src, dst, sport, dport);
+  const uint32_t act = f.pf & 0xffu, cur = (f.pf >> 8) & 0xffu;
+  const uint32_t nw = masq_next_status(proto, R.bits & dpf::kPqUdp, sport, tfl, R.bits & dpf::kPqTcp, act, cur);
+  if (nw != cur || nw == DP_NFS_CLOSED || nw == DP_NFS_RESET) { move = true; return false; }
+  // the pair: mutual, both with masquerade state, the forward flow's allocation live
+  if (!q.alive(f.related, f.related_tag)) return false;
+  const dpf::FlowSlot &o = fc.slots[f.related];
+  if (o.related != R.slot || !q.alive(R.slot, o.related_tag) || !(o.flags & dpf::kFlagMasq)) return false;
+  const dpf::FlowSlot &F = act == DP_PF_SRC_NAT ? f : o, &Rv = act == DP_PF_SRC_NAT ? o : f;
+  if ((F.pf & 0xffu) != DP_PF_SRC_NAT || (Rv.pf & 0xffu) != DP_PF_DST_NAT) return false;
+  return F.mq_rec && F.mq_gen == fc.mq_gen;
+}
+
+// resolve_masq's refresh for a steady record (the expiry by atomicMax)
+__device__ void masq_steady_run(const dpf::FlowCtx &fc, dpf::PfReq &R) {
+  R.verdict = dpf::kPfForward;
+  R.acl_over = 0;
+  R.mverdict = dpf::kPfForward;
+  const dpf::FlowSlot &f = fc.slots[R.slot];
+  const uint32_t fam = (R.proto >> 8) & 0xffu;
+  const bool tcp = R.bits & dpf::kPqTcp, udp = R.bits & dpf::kPqUdp, icmp = R.bits & dpf::kPqIcmp;
+  const uint32_t act = f.pf & 0xffu, port = f.pf >> 16, cur = (f.pf >> 8) & 0xffu;
+  if (cur != DP_NFS_ONE_WAY) {
+    const uint64_t ext = cur == DP_NFS_TWO_WAY ? kMasqTwoWayNs
+                       : cur == DP_NFS_ESTABLISHED ? (uint64_t)f.pf_rule * 1000000000ull : kMasqClosingNs;
+    atomicMax(reinterpret_cast<unsigned long long *>(&fc.slots[R.slot].expires_at),
+              (unsigned long long)(fc.now + ext));
+  }
+  if ((act == DP_PF_SRC_NAT && !unicast(f.pf_fam, f.pf_ip)) || f.pf_fam != fam || !(tcp || udp || icmp)) {
+    R.mverdict = DP_DONE_NAT_FAILURE;
+    return;
+  }
+  R.mnat = act | ((f.flags & dpf::kFlagMasqIdent) ? 0x100u : 0u) | (port << 16);
+  for (int j = 0; j < 4; j++) R.mnat_ip[j] = f.pf_ip[j];
 }
 
 // Can a connection lane run this connection (the records of `list`)?  Every
@@ -4491,59 +4552,123 @@ __device__ bool admit_plan(const Seq &q, uint32_t list) {
 
 #if DP_IN_PART(0)
 // The packets a bitmap marks (by packet index, 1024 per summary bit) in
-// packet order, by one workgroup of 1024: a prefix sum over regions of 1024
-// packets; the bits are cleared for the next burst.  Returns the count.
-__device__ uint32_t order_bits(uint32_t *bits, uint32_t *sum, uint32_t n, uint32_t *order) {
-  const uint32_t t = threadIdx.x;
-  __shared__ uint32_t cnt[1024];
-  __shared__ uint32_t total;
-  if (t == 0) total = 0;
-  const uint32_t regions = (n + 1023) / 1024;
-  for (uint32_t r0 = 0; r0 < regions; r0 += 1024) {
-    __syncthreads();
-    const uint32_t r = r0 + t;
+// packet order, in three launches: each 1024-packet region's count (one
+// work-item per region, its 32 words), their exclusive prefix (one
+// workgroup), each region's packets written at its offset (one wave per
+// region, a lane per word); the bits are cleared for the next burst.
+// which: 0 the NAT stages' packets (pf_bits -> pf_order, pf_cnt[1], and the
+// table length as the pass starts in pf_cnt[6..7]), 1 the allocating lane's
+// (lane_bits -> lane_order, pf_cnt[11]).  The region counts live in adm (per
+// 1024 packets, free until dp_nat_admit_plan).
+__global__ void __launch_bounds__(256) dp_bits_count(dpf::FlowCtx fc, int which) {
+  const uint32_t *bits = which ? fc.lane_bits : fc.pf_bits, *sum = which ? fc.lane_sum : fc.pf_sum;
+  const uint32_t regions = (fc.n + 1023) / 1024;
+  for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < regions; r += gridDim.x * 256) {
     uint32_t c = 0;
-    const bool hit = r < regions && ((sum[r >> 5] >> (r & 31)) & 1u);
-    // the region's 32 words, loaded together and kept (the stores below
-    // may alias them for the compiler: reloading serialised 32 round trips)
-    uint32_t bw[32];
+    if ((sum[r >> 5] >> (r & 31)) & 1u) {
+      const uint4 *w = reinterpret_cast<const uint4 *>(bits + 32 * (uint64_t)r);
 #pragma unroll
-    for (int w = 0; w < 32; w++) bw[w] = hit ? bits[r * 32 + w] : 0u;
-#pragma unroll
-    for (int w = 0; w < 32; w++) c += __popc(bw[w]);
-    cnt[t] = c;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan
-      const uint32_t v = t >= o ? cnt[t - o] : 0u;
-      __syncthreads();
-      cnt[t] += v;
-      __syncthreads();
-    }
-    uint32_t pos = total + cnt[t] - c;
-    if (hit) {
-#pragma unroll
-      for (int w = 0; w < 32; w++) {
-        uint32_t b = bw[w];
-        if (b) bits[r * 32 + w] = 0;
-        while (b) {
-          const int k = __ffs(b) - 1;
-          b &= b - 1;
-          order[pos++] = r * 1024 + w * 32 + k;  // < n: only packets set bits
-        }
+      for (int j = 0; j < 8; j++) {
+        const uint4 x = w[j];
+        c += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
       }
     }
+    fc.adm[r] = c;
+  }
+}
+__global__ void __launch_bounds__(1024) dp_bits_scan(dpf::FlowCtx fc, int which) {
+  const uint32_t t = threadIdx.x, regions = (fc.n + 1023) / 1024;
+  __shared__ uint32_t sh[1024];
+  __shared__ uint32_t base;
+  if (t == 0) base = 0;
+  for (uint32_t r0 = 0; r0 < regions; r0 += 1024) {
     __syncthreads();
-    if (t == 1023) total += cnt[1023];
+    const uint32_t v = r0 + t < regions ? fc.adm[r0 + t] : 0u;
+    sh[t] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+      const uint32_t x = t >= o ? sh[t - o] : 0u;
+      __syncthreads();
+      sh[t] += x;
+      __syncthreads();
+    }
+    if (r0 + t < regions) fc.adm[r0 + t] = base + sh[t] - v;
+    __syncthreads();
+    if (t == 1023) base += sh[1023];
   }
   __syncthreads();
-  for (uint32_t w = t; w < (regions + 31) / 32; w += 1024) sum[w] = 0;
-  return total;
+  if (t == 0) {
+    if (which) {
+      fc.pf_cnt[11] = base;
+    } else {
+      fc.pf_cnt[1] = base;
+      fc.pf_cnt[6] = fc.tmeta[2];  // the table length before the pass
+      fc.pf_cnt[7] = fc.tmeta[3];
+    }
+  }
+}
+__global__ void __launch_bounds__(256) dp_bits_emit(dpf::FlowCtx fc, int which) {
+  uint32_t *bits = which ? fc.lane_bits : fc.pf_bits, *sum = which ? fc.lane_sum : fc.pf_sum;
+  uint32_t *order = which ? fc.lane_order : fc.pf_order;
+  const uint32_t regions = (fc.n + 1023) / 1024, lane = threadIdx.x & 63;
+  for (uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6); r < regions; r += gridDim.x * 4) {
+    if (!((sum[r >> 5] >> (r & 31)) & 1u)) continue;  // (uniform per wave)
+    const uint32_t w = lane < 32 ? bits[32 * (uint64_t)r + lane] : 0u;
+    // the word's offset in the region: the words before it (wave prefix)
+    uint32_t c = (uint32_t)__popc(w), x = c;
+    for (int o = 1; o < 32; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if ((int)lane >= o) x += y;
+    }
+    uint32_t pos = fc.adm[r] + x - c;
+    if (w) {
+      bits[32 * (uint64_t)r + lane] = 0;
+      for (uint32_t b = w; b; b &= b - 1) order[pos++] = r * 1024 + lane * 32 + (uint32_t)(__ffs(b) - 1);
+    }
+  }
+}
+// (then the summary words, once every region is emitted)
+__global__ void __launch_bounds__(256) dp_bits_clear(dpf::FlowCtx fc, int which) {
+  uint32_t *sum = which ? fc.lane_sum : fc.pf_sum;
+  const uint32_t words = ((fc.n + 1023) / 1024 + 31) / 32;
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < words; k += gridDim.x * 256) sum[k] = 0;
 }
 
-// dp_nat_prep: the records of the burst's NAT pass.  Workgroup 0 puts the
-// packets that reached PortForwarder / Masquerade in packet order (their
-// bitmap, scanned 1024 packets per summary bit; the bits are cleared for the
-// next burst) for the replay pass; every workgroup files each record under its
+// dp_nat_mark: every masquerading record that is not a steady refresh
+// (pfw::masq_steady) tags its flow pair for the burst: that connection's
+// records run in its order (dp_nat_prep files them), not as steady ones.
+__global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ img_base,
+                                                   const Image *__restrict__ im, dpf::FlowCtx fc) {
+  const uint32_t nrec = fc.pf_cnt[0];
+  if (!nrec || !fc.mq) return;
+  const Img g{img_base, *im};
+  const pfw::Seq q{fc, g, true};
+  for (uint32_t rec = blockIdx.x * 256 + threadIdx.x; rec < nrec; rec += gridDim.x * 256) {
+    const dpf::PfReq &R = fc.pf[rec];
+    if ((R.bits & (dpf::kPqReached | dpf::kPqMasq)) != (dpf::kPqReached | dpf::kPqMasq)) continue;
+    if (R.slot > fc.mask || !q.alive(R.slot, R.state)) continue;
+    bool move;
+    if (pfw::masq_steady(q, R, move)) continue;
+    dpf::FlowSlot &f = fc.slots[R.slot];
+    f.nat_tag = fc.burst;
+    if (q.alive(f.related, f.related_tag)) fc.slots[f.related].nat_tag = fc.burst;
+  }
+}
+
+// dp_nat_steady: the steady refreshes dp_nat_prep set aside (mode 3; the
+// one-lane pass runs them in its order)
+__global__ void __launch_bounds__(256) dp_nat_steady(dpf::FlowCtx fc) {
+  const uint32_t nrec = fc.pf_cnt[0];
+  if (!nrec || !fc.pf_cnt[27] || pfw::nat_mode(fc) != 3) return;
+  for (uint32_t rec = blockIdx.x * 256 + threadIdx.x; rec < nrec; rec += gridDim.x * 256) {
+    dpf::PfReq &R = fc.pf[rec];
+    if ((R.bits & (dpf::kPqReached | dpf::kPqSteady)) == (dpf::kPqReached | dpf::kPqSteady))
+      pfw::masq_steady_run(fc, R);
+  }
+}
+
+// dp_nat_prep: the records of the burst's NAT pass (their packet order for
+// the one-lane pass and the replay: dp_bits_*); each record is filed under its
 // connection -- port forwarding: pfw::conn_key; masquerade: the flow pair it is
 // attached to (pfw::masq_conn), or the allocating lane -- a hash slot claimed
 // for this burst by CAS on (burst, key), a list of its records pushed by CAS
@@ -4551,17 +4676,10 @@ __device__ uint32_t order_bits(uint32_t *bits, uint32_t *sum, uint32_t n, uint32
 __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ img_base,
                                                     const Image *__restrict__ im, dpf::FlowCtx fc) {
   const uint32_t t = threadIdx.x;
-  if (blockIdx.x == 0) {
-    const uint32_t total = order_bits(fc.pf_bits, fc.pf_sum, fc.n, fc.pf_order);
-    if (t == 0) {
-      fc.pf_cnt[1] = total;
-      fc.pf_cnt[6] = fc.tmeta[2];  // the table length before the pass
-      fc.pf_cnt[7] = fc.tmeta[3];
-    }
-  }
   const uint32_t nrec = fc.pf_cnt[0];
   if (!nrec) return;
   const Img g{img_base, *im};
+  const pfw::Seq sq{fc, g, true};
   const unsigned long long tag = (unsigned long long)fc.burst << 32;
   for (uint32_t rec = blockIdx.x * 1024 + t; rec < nrec; rec += gridDim.x * 1024) {
     dpf::PfReq &R = fc.pf[rec];
@@ -4571,6 +4689,15 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
     pfw::flag_wave(&fc.pf_cnt[8], R.bits & dpf::kPqMasq);
     if (R.bits & dpf::kPqMasq) {
       pfw::flag_wave(&fc.pf_cnt[10], pfw::masq_back(fc, R));
+      // a steady refresh whose connection no record moves: set aside
+      bool move;
+      const bool steady = pfw::masq_steady(sq, R, move) && fc.slots[R.slot].nat_tag != fc.burst &&
+                          fc.slots[fc.slots[R.slot].related].nat_tag != fc.burst;
+      pfw::flag_wave(&fc.pf_cnt[27], steady);
+      if (steady) {
+        R.bits |= dpf::kPqSteady;
+        continue;
+      }
       if (!pfw::masq_conn(fc, R, key)) {
         pfw::lane_mark(fc, R, 0u);
         continue;
@@ -4768,11 +4895,36 @@ __global__ void __launch_bounds__(1024) dp_nat_admit_scan(dpf::FlowCtx fc, int s
   }
 }
 
-// dp_nat_lane_order: the allocating lane's records in packet order (every
-// burst: it clears the bits the connection lanes and dp_nat_prep set)
-__global__ void __launch_bounds__(1024) dp_nat_lane_order(dpf::FlowCtx fc) {
-  const uint32_t total = order_bits(fc.lane_bits, fc.lane_sum, fc.n, fc.lane_order);
-  if (threadIdx.x == 0) fc.pf_cnt[11] = total;
+// dp_nat_lane_plan: the allocating lane's records planned in parallel before
+// it runs: a record whose flow is valid with masquerade state (or carries the
+// ACL's flow verdict) runs alone, on live state; so do all when the table
+// lacks room for every pair the lane could create; the others are decided
+// without the allocator or ask it for a tuple (masq_plan: configuration only).
+// Validity only ever falls during the pass, so a plan made now errs only
+// towards "alone", which re-decides live.
+__global__ void __launch_bounds__(256) dp_nat_lane_plan(const uint8_t *__restrict__ img_base,
+                                                        const Image *__restrict__ im, dpf::FlowCtx fc) {
+  if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3) return;
+  const uint32_t nl = fc.pf_cnt[11];
+  const Img g{img_base, *im};
+  const pfw::Seq qs{fc, g, false};
+  const uint64_t len0 = ((uint64_t)fc.tmeta[3] << 32) | fc.tmeta[2];
+  const bool room = len0 + 2ull * nl <= fc.capacity && len0 + 2ull * nl <= fc.hard;
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < nl; k += gridDim.x * 256) {
+    pfw::LanePlan L{};
+    L.rec = fc.pf_of[fc.lane_order[k]];
+    dpf::PfReq &R = fc.pf[L.rec];
+    const bool pfdone = R.bits & dpf::kPqPfDone;
+    if (!room || (!pfdone && (R.bits & dpf::kPqSens)) || pfw::masq_valid(qs, R)) {
+      L.cls = 1;
+    } else {
+      R.mverdict = dpf::kPfForward;
+      if (!pfdone) { R.verdict = dpf::kPfForward; R.acl_over = 0; }
+      L.cls = pfw::masq_plan(fc, R, L.m) ? 3u : 2u;
+    }
+    const uint4 *w = reinterpret_cast<const uint4 *>(&L);
+    for (int j = 0; j < 8; j++) fc.lane_plan[8 * (uint64_t)k + j] = w[j];
+  }
 }
 
 // The allocating lane is one workgroup: its lanes' stores and later loads
@@ -4797,46 +4949,43 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3) return;
   const uint32_t nl = fc.pf_cnt[11];
   const int t = threadIdx.x;
-  // room for every pair the lane could create (the connection lanes insert
-  // nothing): else each record alone, so insert_common's admissions fall in
-  // packet order
-  const uint64_t len0 = ((uint64_t)fc.tmeta[3] << 32) | fc.tmeta[2];
-  const bool room = len0 + 2ull * nl <= fc.capacity && len0 + 2ull * nl <= fc.hard;
   const Img g{img_base, *im};
   const pfw::Seq qs{fc, g, false}, qp{fc, g, true};
   const dpm::View V{fc.mq};
   __shared__ uint32_t s_ik[64][12];  // the run's initial keys (+ hash)
   __shared__ int s_pd[64];           // the lane's latest earlier lane with the same initial key
+  __shared__ uint32_t s_hc[1024];    // initial keys per hash bucket (most lanes: alone in theirs)
   __shared__ uint32_t s_bm[8];       // the thread block's usage bitmap
   __shared__ uint32_t s_b[8];        // (fast, address record, block, free ports, address words)
   uint32_t fast_n = 0, lone_n = 0, solo_n = 0;
+  // where the lane's time goes (clock64 ticks: plans, allocations, pairs,
+  // records alone), for the counters [19..22] in units of 1024 ticks
+  uint64_t tk[7] = {0, 0, 0, 0, 0, 0, 0}, t0 = clock64(), ta;
+  uint32_t steps = 0;
   for (uint32_t k0 = 0; k0 < nl; k0 += 64) {
     const uint32_t cnt = nl - k0 < 64 ? nl - k0 : 64;
     const bool has = (uint32_t)t < cnt;
-    const uint32_t ri = has ? fc.pf_of[fc.lane_order[k0 + t]] : 0u;
-    dpf::PfReq &R = fc.pf[ri];
-    // 1 alone, 2 decided, 3 allocates
-    uint32_t cls = 0;
-    pfw::MPlan m;
+    // the record's plan (dp_nat_lane_plan: 1 alone, 2 decided, 3 allocates)
+    pfw::LanePlan P{};
     if (has) {
-      const bool pfdone = R.bits & dpf::kPqPfDone;
-      if (!room || (!pfdone && (R.bits & dpf::kPqSens)) || pfw::masq_valid(qs, R)) {
-        cls = 1;
-      } else {
-        R.mverdict = dpf::kPfForward;
-        if (!pfdone) { R.verdict = dpf::kPfForward; R.acl_over = 0; }
-        cls = pfw::masq_plan(fc, R, m) ? 3u : 2u;
-      }
+      uint4 *w = reinterpret_cast<uint4 *>(&P);
+      for (int j = 0; j < 8; j++) w[j] = fc.lane_plan[8 * (uint64_t)(k0 + t) + j];
     }
+    const uint32_t ri = P.rec, cls = P.cls;
+    const pfw::MPlan &m = P.m;
+    dpf::PfReq &R = fc.pf[ri];
+    for (int j = t; j < 1024; j += 64) s_hc[j] = 0;
+    __syncthreads();
     if (cls == 3) {
       for (int j = 0; j < 11; j++) s_ik[t][j] = m.ik.w[j];
       s_ik[t][11] = dpf::fkey_hash(m.ik);
+      atomicAdd(&s_hc[s_ik[t][11] & 1023], 1u);
     }
     __syncthreads();
     const uint64_t c1 = __ballot(cls == 1), c3 = __ballot(cls == 3);
     {
       int pd = -1;
-      if (cls == 3)
+      if (cls == 3 && s_hc[s_ik[t][11] & 1023] > 1)
         for (int q = t - 1; q >= 0 && pd < 0; q--) {
           if (!((c3 >> q) & 1) || s_ik[q][11] != s_ik[t][11]) continue;
           bool eq = true;
@@ -4846,6 +4995,8 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
       s_pd[t] = pd;
     }
     __syncthreads();
+    const uint64_t cuts = __ballot(cls == 1 || (cls == 3 && s_pd[t] >= 0));
+    { const uint64_t x = clock64(); tk[0] += x - t0; t0 = x; }
     // the lane's allocation: ok (a pair to create), else its verdict is set
     bool ok = false, done = cls != 3;
     uint32_t rec = 0, aport = 0, aip[4] = {0, 0, 0, 0};
@@ -4862,11 +5013,18 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           solo_n++;
         }
         lane_fence();
+        { const uint64_t x = clock64(); tk[3] += x - t0; t0 = x; }
         i++;
         continue;
       }
-      uint32_t j = i + 1;
-      while (j < cnt && !((c1 >> j) & 1) && !(((c3 >> j) & 1) && s_pd[j] >= (int)i)) j++;
+      // the run [i, j): up to the next record alone, or one whose initial
+      // key an earlier record of the run inserts (candidates: cuts)
+      uint32_t j = cnt;
+      for (uint64_t c = cuts & ~((2ull << i) - 1); c; c &= c - 1) {
+        const uint32_t q = (uint32_t)__ffsll((long long)c) - 1;
+        if (q >= cnt) break;
+        if (((c1 >> q) & 1) || s_pd[q] >= (int)i) { j = q; break; }
+      }
       const uint64_t run = (j == 64 ? ~0ull : ((1ull << j) - 1)) & ~((1ull << i) - 1);
       // the run's allocations, in packet order
       for (;;) {
@@ -4874,6 +5032,8 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         if (!pend) break;
         const int p = __ffsll((long long)pend) - 1;
         const uint32_t set_p = (uint32_t)__shfl((int)m.set, p);
+        ta = clock64();
+        steps++;
         if (t == p) {
           // the set's first region: its first address in use with free ports
           // and that address's thread block
@@ -4905,6 +5065,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           s_b[0] = f;
         }
         __syncthreads();
+        { const uint64_t x = clock64(); tk[4] += x - ta; ta = x; }
         // (a first record that could meet related_pair at this address allocates alone)
         bool p_eq = false;
         if (t == p && s_b[0]) {
@@ -4956,6 +5117,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
             done = true;
           }
           __syncthreads();
+          { const uint64_t x = clock64(); tk[5] += x - ta; ta = x; }
           if (t == p) {
             // the block's bitmap after `taken` allocations: its lowest free
             // ports (built from the copy, stored once)
@@ -4990,7 +5152,9 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         }
         lane_fence();
         __syncthreads();
+        { const uint64_t x = clock64(); tk[6] += x - ta; ta = x; }
       }
+      { const uint64_t x = clock64(); tk[1] += x - t0; t0 = x; }
       // the run's pairs, in parallel (distinct initial keys; distinct tuples)
       bool give_back = false;
       if (ok && ((run >> t) & 1)) {
@@ -5002,6 +5166,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         if (t == __ffsll((long long)gb) - 1) dpm::release(V, rec, aport);
         lane_fence();
       }
+      { const uint64_t x = clock64(); tk[2] += x - t0; t0 = x; }
       i = j;
     }
   }
@@ -5012,7 +5177,12 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   }
   uint32_t ln = lone_n, fn = fast_n, sn = solo_n;
   for (int o = 32; o > 0; o >>= 1) { ln += __shfl_xor(ln, o); fn += __shfl_xor(fn, o); sn += __shfl_xor(sn, o); }
-  if (t == 0) { fc.pf_cnt[14] += fn; fc.pf_cnt[18] += sn; }
+  if (t == 0) {
+    fc.pf_cnt[14] += fn;
+    fc.pf_cnt[18] += sn;
+    for (int k = 0; k < 7; k++) fc.pf_cnt[19 + k] = (uint32_t)(tk[k] >> 10);
+    fc.pf_cnt[26] = steps;
+  }
   uint32_t v = qp.added;
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   if (t == 0) {
@@ -5457,7 +5627,21 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   // records leaves at once -- 8192 empty workgroups cost 76 us; more lanes
   // than that did not make the 500k-record burst faster)
   const uint32_t pb = (n + 1023) / 1024 < 256 ? (n + 1023) / 1024 : 256;
+  const uint32_t rb0 = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  // the records' packets in packet order (dp_bits_*), then the records
+  const uint32_t regions = (n + 1023) / 1024;
+  const uint32_t cb = (regions + 255) / 256 < 1024 ? (regions + 255) / 256 : 1024;
+  const uint32_t eb = (regions + 3) / 4 < 4096 ? (regions + 3) / 4 : 4096;
+  auto order = [&](int which) {
+    hipLaunchKernelGGL(dp_bits_count, dim3(cb), dim3(256), 0, stream, fc, which);
+    hipLaunchKernelGGL(dp_bits_scan, dim3(1), dim3(1024), 0, stream, fc, which);
+    hipLaunchKernelGGL(dp_bits_emit, dim3(eb), dim3(256), 0, stream, fc, which);
+    hipLaunchKernelGGL(dp_bits_clear, dim3(cb), dim3(256), 0, stream, fc, which);
+  };
+  order(0);
+  hipLaunchKernelGGL(dp_nat_mark, dim3(rb0), dim3(256), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_prep, dim3(pb), dim3(1024), 0, stream, img_base, im, fc);
+  hipLaunchKernelGGL(dp_nat_steady, dim3(rb0), dim3(256), 0, stream, fc);
   const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
   // port forwarding near the capacity: the creations' admissions in packet order
   hipLaunchKernelGGL(dp_nat_admit_plan, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
@@ -5468,7 +5652,8 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   hipLaunchKernelGGL(dp_nat_resolve<true>, dim3(1), dim3(64), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_resolve<false>, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   // a masquerading burst's allocating lane (its records in packet order)
-  hipLaunchKernelGGL(dp_nat_lane_order, dim3(1), dim3(1024), 0, stream, fc);
+  order(1);
+  hipLaunchKernelGGL(dp_nat_lane_plan, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_lane, dim3(1), dim3(64), 0, stream, img_base, im, fc);
   fc.replay = 1;
   if (meta) dpk_run_pipeline_111(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);

@@ -77,13 +77,24 @@ def test_gpu_masquerade_at_scale():
         assert hist(out) == {"Delivered": 300_000}
         assert int(cnt[12]) == 3, cnt
         assert nn <= int(cnt[11]) < nn + 20_000, cnt  # the allocating lane: the new connections (+ few)
+        # (the connections the first packets opened: one-way, their answers move them)
         assert same_flows(ro, rg, keys, "established burst") == 250_000
+        # twice more: the pairs two-way, then established -- steady refreshes
+        for step in (3, 4):
+            for r in (ro, rg):
+                r.set_clock(10 ** 12 + step * 10 ** 9)
+            buf, inp, nn = c.burst(300_000, 0.01, 0.6, step=step)
+            out, ob, cnt = both(ro, rg, buf, inp, f"established burst {step}")
+            assert hist(out) == {"Delivered": 300_000}
+            assert int(cnt[12]) == 3, cnt
+        assert int(cnt[27]) == 1, cnt
+        assert same_flows(ro, rg, keys, "established bursts") == 250_000
         # the same near the capacity: the allocating lane takes its records
         # one by one (pairs refused at capacity), the connection lanes as before
         for r in (ro, rg):
-            r.set_clock(10 ** 12 + 2 * 10 ** 9)
+            r.set_clock(10 ** 12 + 5 * 10 ** 9)
             (r.fl if hasattr(r, "fl") else r.ft).set_capacity(r.count()[0] + 1000)
-        buf, inp, nn = c.burst(300_000, 0.01, 0.6, step=2)
+        buf, inp, nn = c.burst(300_000, 0.01, 0.6, step=5)
         out, ob, cnt = both(ro, rg, buf, inp, "established burst near capacity")
         h = hist(out)
         assert int(cnt[12]) == 3 and int(cnt[14]) == 0 and int(cnt[18]) == int(cnt[11]), cnt
