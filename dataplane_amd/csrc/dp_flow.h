@@ -123,7 +123,7 @@ constexpr uint32_t kPqLane = 1u << 13;
 constexpr uint32_t kPqPfDone = 1u << 14;
 // a masquerading refresh that commutes with every other record of the burst
 // (dp_nat_prep: no record of its connection changes the pair's state this
-// burst); dp_nat_steady resolves it
+// burst); dp_nat_prep resolves it in place
 constexpr uint32_t kPqSteady = 1u << 15;
 constexpr uint32_t kPfForward = 0xffu;
 
@@ -187,7 +187,8 @@ struct FlowCtx {
   // [19..22] its time in plans, allocations, pairs and records alone (1024
   // clock64 ticks), [23..25] the allocations' parts (the set's address and
   // block, serving the records, the block's update), [26] allocation steps,
-  // [27] a steady refresh in the burst (kPqSteady)
+  // [27] a steady refresh in the burst (kPqSteady), [28] an initial key of
+  // the lane's allocating records repeats, [29] a lane record runs alone
   unsigned long long *grp_tab, *grp_head, *grp_next;
   uint32_t *grp_list;
   uint32_t grp_mask;
@@ -201,6 +202,8 @@ struct FlowCtx {
   // index + summary, as pf_bits) and their order
   uint32_t *lane_bits, *lane_sum, *lane_order;
   uint4 *lane_plan;     // per lane record: its class and plan (dp_nat_lane_plan, 128 B)
+  uint4 *lane_res;      // per lane record: its allocation for dp_nat_pairs (32 B)
+  unsigned long long *dup_tab;  // (burst << 32 | initial key hash) of the lane's allocating records
   // port forwarding near the capacity (mode 4): per record the new slots its
   // creation adds, then the sum of those of the records before it in packet
   // order (the table length its first insert meets); per 4096 records a sum

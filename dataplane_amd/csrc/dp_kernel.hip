@@ -4634,36 +4634,31 @@ __global__ void __launch_bounds__(256) dp_bits_clear(dpf::FlowCtx fc, int which)
   for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < words; k += gridDim.x * 256) sum[k] = 0;
 }
 
-// dp_nat_mark: every masquerading record that is not a steady refresh
-// (pfw::masq_steady) tags its flow pair for the burst: that connection's
-// records run in its order (dp_nat_prep files them), not as steady ones.
+// dp_nat_mark: the burst's kinds of record (port forwarding, masquerade, a
+// peer that could masquerade back: the NAT pass's mode), and every
+// masquerading record that is not a steady refresh (pfw::masq_steady) tags
+// its flow pair for the burst: that connection's records run in its order
+// (dp_nat_prep files them), not as steady ones.
 __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ img_base,
                                                    const Image *__restrict__ im, dpf::FlowCtx fc) {
   const uint32_t nrec = fc.pf_cnt[0];
-  if (!nrec || !fc.mq) return;
+  if (!nrec) return;
   const Img g{img_base, *im};
   const pfw::Seq q{fc, g, true};
   for (uint32_t rec = blockIdx.x * 256 + threadIdx.x; rec < nrec; rec += gridDim.x * 256) {
     const dpf::PfReq &R = fc.pf[rec];
-    if ((R.bits & (dpf::kPqReached | dpf::kPqMasq)) != (dpf::kPqReached | dpf::kPqMasq)) continue;
+    // the burst's kinds of record (the NAT pass's mode rests on them)
+    const bool reached = R.bits & dpf::kPqReached;
+    pfw::flag_wave(&fc.pf_cnt[9], reached && (R.bits & dpf::kPqPf));
+    pfw::flag_wave(&fc.pf_cnt[8], reached && (R.bits & dpf::kPqMasq));
+    pfw::flag_wave(&fc.pf_cnt[10], reached && (R.bits & dpf::kPqMasq) && pfw::masq_back(fc, R));
+    if (!fc.mq || (R.bits & (dpf::kPqReached | dpf::kPqMasq)) != (dpf::kPqReached | dpf::kPqMasq)) continue;
     if (R.slot > fc.mask || !q.alive(R.slot, R.state)) continue;
     bool move;
     if (pfw::masq_steady(q, R, move)) continue;
     dpf::FlowSlot &f = fc.slots[R.slot];
     f.nat_tag = fc.burst;
     if (q.alive(f.related, f.related_tag)) fc.slots[f.related].nat_tag = fc.burst;
-  }
-}
-
-// dp_nat_steady: the steady refreshes dp_nat_prep set aside (mode 3; the
-// one-lane pass runs them in its order)
-__global__ void __launch_bounds__(256) dp_nat_steady(dpf::FlowCtx fc) {
-  const uint32_t nrec = fc.pf_cnt[0];
-  if (!nrec || !fc.pf_cnt[27] || pfw::nat_mode(fc) != 3) return;
-  for (uint32_t rec = blockIdx.x * 256 + threadIdx.x; rec < nrec; rec += gridDim.x * 256) {
-    dpf::PfReq &R = fc.pf[rec];
-    if ((R.bits & (dpf::kPqReached | dpf::kPqSteady)) == (dpf::kPqReached | dpf::kPqSteady))
-      pfw::masq_steady_run(fc, R);
   }
 }
 
@@ -4680,22 +4675,22 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
   if (!nrec) return;
   const Img g{img_base, *im};
   const pfw::Seq sq{fc, g, true};
+  const bool split = pfw::nat_mode(fc) == 3;  // (dp_nat_mark's flags decide it)
   const unsigned long long tag = (unsigned long long)fc.burst << 32;
   for (uint32_t rec = blockIdx.x * 1024 + t; rec < nrec; rec += gridDim.x * 1024) {
     dpf::PfReq &R = fc.pf[rec];
     if (!(R.bits & dpf::kPqReached)) continue;  // a flow-filter record of a packet dropped before NAT
     uint32_t key;
-    pfw::flag_wave(&fc.pf_cnt[9], R.bits & dpf::kPqPf);
-    pfw::flag_wave(&fc.pf_cnt[8], R.bits & dpf::kPqMasq);
     if (R.bits & dpf::kPqMasq) {
-      pfw::flag_wave(&fc.pf_cnt[10], pfw::masq_back(fc, R));
-      // a steady refresh whose connection no record moves: set aside
+      // a steady refresh whose connection no record moves: resolved here
+      // (split pass; the one-lane pass runs it in its order)
       bool move;
-      const bool steady = pfw::masq_steady(sq, R, move) && fc.slots[R.slot].nat_tag != fc.burst &&
+      const bool steady = split && pfw::masq_steady(sq, R, move) && fc.slots[R.slot].nat_tag != fc.burst &&
                           fc.slots[fc.slots[R.slot].related].nat_tag != fc.burst;
       pfw::flag_wave(&fc.pf_cnt[27], steady);
       if (steady) {
         R.bits |= dpf::kPqSteady;
+        pfw::masq_steady_run(fc, R);
         continue;
       }
       if (!pfw::masq_conn(fc, R, key)) {
@@ -4901,7 +4896,13 @@ __global__ void __launch_bounds__(1024) dp_nat_admit_scan(dpf::FlowCtx fc, int s
 // lacks room for every pair the lane could create; the others are decided
 // without the allocator or ask it for a tuple (masq_plan: configuration only).
 // Validity only ever falls during the pass, so a plan made now errs only
-// towards "alone", which re-decides live.
+// towards "alone", which re-decides live.  Each wave plans one 64-record
+// chunk of the lane (the lane's unit) and finds, per allocating record, the
+// latest earlier one of the chunk with the same initial key (its pair replaces
+// that one's: the lane cuts its runs there); burst-wide, pf_cnt[28] says
+// some initial key repeats, pf_cnt[29] that some record runs alone -- without
+// either, every pair commutes with the others and dp_nat_pairs creates them
+// after the lane's allocations.
 __global__ void __launch_bounds__(256) dp_nat_lane_plan(const uint8_t *__restrict__ img_base,
                                                         const Image *__restrict__ im, dpf::FlowCtx fc) {
   if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3) return;
@@ -4910,20 +4911,74 @@ __global__ void __launch_bounds__(256) dp_nat_lane_plan(const uint8_t *__restric
   const pfw::Seq qs{fc, g, false};
   const uint64_t len0 = ((uint64_t)fc.tmeta[3] << 32) | fc.tmeta[2];
   const bool room = len0 + 2ull * nl <= fc.capacity && len0 + 2ull * nl <= fc.hard;
-  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < nl; k += gridDim.x * 256) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ uint32_t s_ik[4][64][12];
+  __shared__ uint32_t s_hc[4][256];
+  const unsigned long long tag = (unsigned long long)fc.burst << 32;
+  for (uint32_t b0 = blockIdx.x * 256; b0 < nl; b0 += gridDim.x * 256) {  // (uniform per block)
+    const uint32_t k = b0 + 64 * wv + lane;
+    const bool has = k < nl;
     pfw::LanePlan L{};
-    L.rec = fc.pf_of[fc.lane_order[k]];
-    dpf::PfReq &R = fc.pf[L.rec];
-    const bool pfdone = R.bits & dpf::kPqPfDone;
-    if (!room || (!pfdone && (R.bits & dpf::kPqSens)) || pfw::masq_valid(qs, R)) {
-      L.cls = 1;
-    } else {
-      R.mverdict = dpf::kPfForward;
-      if (!pfdone) { R.verdict = dpf::kPfForward; R.acl_over = 0; }
-      L.cls = pfw::masq_plan(fc, R, L.m) ? 3u : 2u;
+    if (has) {
+      L.rec = fc.pf_of[fc.lane_order[k]];
+      dpf::PfReq &R = fc.pf[L.rec];
+      const bool pfdone = R.bits & dpf::kPqPfDone;
+      if (!room || (!pfdone && (R.bits & dpf::kPqSens)) || pfw::masq_valid(qs, R)) {
+        L.cls = 1;
+      } else {
+        R.mverdict = dpf::kPfForward;
+        if (!pfdone) { R.verdict = dpf::kPfForward; R.acl_over = 0; }
+        L.cls = pfw::masq_plan(fc, R, L.m) ? 3u : 2u;
+      }
     }
-    const uint4 *w = reinterpret_cast<const uint4 *>(&L);
-    for (int j = 0; j < 8; j++) fc.lane_plan[8 * (uint64_t)k + j] = w[j];
+    // the chunk's initial keys; per allocating record the latest earlier one
+    // with the same key (pd, in bits 8.. of cls as pd + 1)
+    for (int x = lane; x < 256; x += 64) s_hc[wv][x] = 0;
+    uint32_t h = 0;
+    if (L.cls == 3) {
+      h = dpf::fkey_hash(L.m.ik);
+      for (int x = 0; x < 11; x++) s_ik[wv][lane][x] = L.m.ik.w[x];
+      s_ik[wv][lane][11] = h;
+    }
+    __syncthreads();
+    if (L.cls == 3) atomicAdd(&s_hc[wv][h & 255], 1u);
+    __syncthreads();
+    const uint64_t c3 = __ballot(L.cls == 3);
+    int pd = -1;
+    if (L.cls == 3 && s_hc[wv][h & 255] > 1)
+      for (int q = lane - 1; q >= 0 && pd < 0; q--) {
+        if (!((c3 >> q) & 1) || s_ik[wv][q][11] != h) continue;
+        bool eq = true;
+        for (int x = 0; x < 11; x++) eq = eq && s_ik[wv][q][x] == L.m.ik.w[x];
+        if (eq) pd = q;
+      }
+    L.cls |= (uint32_t)(pd + 1) << 8;
+    // burst-wide: does any initial key repeat (by its hash), does any record run alone
+    bool rep = false;
+    if ((L.cls & 0xffu) == 3) {
+      // (the slot from one hash of the key, the tag from another)
+      const uint32_t h2 = dpm::kmix(dpm::kmix(L.m.ik.w[0], L.m.ik.w[1], L.m.ik.w[2]),
+                                    dpm::kmix(L.m.ik.w[3], L.m.ik.w[4], L.m.ik.w[5]) ^ L.m.ik.w[6],
+                                    dpm::kmix(L.m.ik.w[7], L.m.ik.w[8], L.m.ik.w[9]) ^ L.m.ik.w[10]);
+      const unsigned long long want = tag | h2;
+      uint32_t x = dpm::kmix(h, 0x5bd1e995u, 0u) & fc.grp_mask;
+      for (uint32_t p = 0;; p++) {
+        if (p > fc.grp_mask) { rep = true; break; }  // (full: say so)
+        const unsigned long long cur = __hip_atomic_load(&fc.dup_tab[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == want) { rep = true; break; }
+        if ((cur >> 32) == fc.burst) { x = (x + 1) & fc.grp_mask; continue; }
+        const unsigned long long got = atomicCAS(&fc.dup_tab[x], cur, want);
+        if (got == cur) break;
+        if (got == want) { rep = true; break; }
+      }
+    }
+    pfw::flag_wave(&fc.pf_cnt[28], rep);
+    pfw::flag_wave(&fc.pf_cnt[29], (L.cls & 0xffu) == 1);
+    if (has) {
+      const uint4 *w = reinterpret_cast<const uint4 *>(&L);
+      for (int x = 0; x < 8; x++) fc.lane_plan[8 * (uint64_t)k + x] = w[x];
+    }
+    __syncthreads();
   }
 }
 
@@ -4933,30 +4988,51 @@ __global__ void __launch_bounds__(256) dp_nat_lane_plan(const uint8_t *__restric
 __device__ __forceinline__ void lane_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
 // dp_nat_lane: the split pass's allocating lane (mode 3), one wave over its
-// records in packet order, 64 at a time.  A record whose outcome rests on
-// live flow state (a valid flow with masquerade state, the ACL's flow
-// verdict) runs alone, as the one-lane pass runs it.  The others are decided
-// without one (masq_plan) or allocate; a run of them (cut before a record
-// whose initial key an earlier one of the run inserts) is served in packet
-// order: where the set's first region's first address with free ports has a
-// thread block with free ports, the next records of that set take its free
-// ports in order in one step (PortAllocator::allocate_port, port_alloc.rs:
-// 264-284, record after record: a record whose checks fail gives its port
-// back at once, so it takes none), else one record allocates alone (a new
-// block, address or region); then the run's pairs are created in parallel.
+// records in packet order, 64 at a time (dp_nat_lane_plan's chunks).  A
+// record whose outcome rests on live flow state (a valid flow with masquerade
+// state, the ACL's flow verdict) runs alone, as the one-lane pass runs it.
+// The others are decided without the allocator (masq_plan) or allocate; a run
+// of them (cut before a record whose initial key an earlier one of the run
+// inserts) is served in packet order: where the set's first region's first
+// address with free ports has a thread block with free ports, the next
+// records of that set take its free ports in order in one step
+// (PortAllocator::allocate_port, port_alloc.rs:264-284, record after record:
+// a record whose checks fail gives its port back at once, so it takes none),
+// else one record allocates alone (a new block, address or region).  The
+// block being served stays in LDS from step to step (written back before
+// anything else reads the allocator).  Then the run's pairs are created in
+// parallel -- or, when no record runs alone and no initial key repeats, every
+// pair after the lane (dp_nat_pairs; the allocations go to lane_res).
 __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ img_base,
                                                   const Image *__restrict__ im, dpf::FlowCtx fc) {
   if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3) return;
   const uint32_t nl = fc.pf_cnt[11];
+  const bool post = !fc.pf_cnt[28] && !fc.pf_cnt[29];
   const int t = threadIdx.x;
   const Img g{img_base, *im};
   const pfw::Seq qs{fc, g, false}, qp{fc, g, true};
   const dpm::View V{fc.mq};
-  __shared__ uint32_t s_ik[64][12];  // the run's initial keys (+ hash)
-  __shared__ int s_pd[64];           // the lane's latest earlier lane with the same initial key
-  __shared__ uint32_t s_hc[1024];    // initial keys per hash bucket (most lanes: alone in theirs)
-  __shared__ uint32_t s_bm[8];       // the thread block's usage bitmap
-  __shared__ uint32_t s_b[8];        // (fast, address record, block, free ports, address words)
+  __shared__ uint32_t s_bm[8];  // the block being served: its usage bitmap
+  // the block being served: [0] valid, [1] region, [2] address record,
+  // [3] block | its first port, [4..7] the address, [8] ports taken since it
+  // was loaded, [9] the first step of the step: 1 fast
+  __shared__ uint32_t s_c[10];
+  if (t == 0) s_c[0] = 0;
+  __syncthreads();
+  // the cached block back to the allocator (the lane p that holds it)
+  auto flush = [&]() {
+    if (t == 0 && s_c[0]) {
+      dpm::Addr &A = V.recs()[s_c[2]];
+      const uint32_t tb = s_c[3] & 0xffu;
+      uint32_t full = 0xffffffffu;
+      for (int x = 0; x < 8; x++) { A.bm[tb][x] = s_bm[x]; full &= s_bm[x]; }
+      A.blive[tb] = (uint16_t)(A.blive[tb] + s_c[8]);
+      if (full == 0xffffffffu && s_c[8]) A.nonfull--;
+      s_c[0] = 0;
+    }
+    lane_fence();
+    __syncthreads();
+  };
   uint32_t fast_n = 0, lone_n = 0, solo_n = 0;
   // where the lane's time goes (clock64 ticks: plans, allocations, pairs,
   // records alone), for the counters [19..22] in units of 1024 ticks
@@ -4965,37 +5041,19 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   for (uint32_t k0 = 0; k0 < nl; k0 += 64) {
     const uint32_t cnt = nl - k0 < 64 ? nl - k0 : 64;
     const bool has = (uint32_t)t < cnt;
-    // the record's plan (dp_nat_lane_plan: 1 alone, 2 decided, 3 allocates)
+    // the record's plan (dp_nat_lane_plan: 1 alone, 2 decided, 3 allocates;
+    // the latest earlier record of the chunk with its initial key)
     pfw::LanePlan P{};
     if (has) {
       uint4 *w = reinterpret_cast<uint4 *>(&P);
       for (int j = 0; j < 8; j++) w[j] = fc.lane_plan[8 * (uint64_t)(k0 + t) + j];
     }
-    const uint32_t ri = P.rec, cls = P.cls;
+    const uint32_t ri = P.rec, cls = P.cls & 0xffu;
+    const int pd = (int)(P.cls >> 8) - 1;
     const pfw::MPlan &m = P.m;
     dpf::PfReq &R = fc.pf[ri];
-    for (int j = t; j < 1024; j += 64) s_hc[j] = 0;
-    __syncthreads();
-    if (cls == 3) {
-      for (int j = 0; j < 11; j++) s_ik[t][j] = m.ik.w[j];
-      s_ik[t][11] = dpf::fkey_hash(m.ik);
-      atomicAdd(&s_hc[s_ik[t][11] & 1023], 1u);
-    }
-    __syncthreads();
     const uint64_t c1 = __ballot(cls == 1), c3 = __ballot(cls == 3);
-    {
-      int pd = -1;
-      if (cls == 3 && s_hc[s_ik[t][11] & 1023] > 1)
-        for (int q = t - 1; q >= 0 && pd < 0; q--) {
-          if (!((c3 >> q) & 1) || s_ik[q][11] != s_ik[t][11]) continue;
-          bool eq = true;
-          for (int j = 0; j < 11; j++) eq = eq && s_ik[q][j] == s_ik[t][j];
-          if (eq) pd = q;
-        }
-      s_pd[t] = pd;
-    }
-    __syncthreads();
-    const uint64_t cuts = __ballot(cls == 1 || (cls == 3 && s_pd[t] >= 0));
+    const uint64_t cuts = __ballot(cls == 1 || (cls == 3 && pd >= 0));
     { const uint64_t x = clock64(); tk[0] += x - t0; t0 = x; }
     // the lane's allocation: ok (a pair to create), else its verdict is set
     bool ok = false, done = cls != 3;
@@ -5003,6 +5061,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
     uint32_t i = 0;
     while (i < cnt) {
       if ((c1 >> i) & 1) {
+        flush();
         if (t == (int)i) {
           if (R.bits & dpf::kPqPfDone) {
             R.mverdict = dpf::kPfForward;
@@ -5023,7 +5082,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
       for (uint64_t c = cuts & ~((2ull << i) - 1); c; c &= c - 1) {
         const uint32_t q = (uint32_t)__ffsll((long long)c) - 1;
         if (q >= cnt) break;
-        if (((c1 >> q) & 1) || s_pd[q] >= (int)i) { j = q; break; }
+        if (((c1 >> q) & 1) || (int)__shfl(pd, (int)q) >= (int)i) { j = q; break; }
       }
       const uint64_t run = (j == 64 ? ~0ull : ((1ull << j) - 1)) & ~((1ull << i) - 1);
       // the run's allocations, in packet order
@@ -5035,12 +5094,22 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         ta = clock64();
         steps++;
         if (t == p) {
-          // the set's first region: its first address in use with free ports
-          // and that address's thread block
-          uint32_t f = 0;
-          if (fc.force_seq != 2) {
-            const dpm::Set &S = V.sets()[set_p];
-            const dpm::Region &G = V.regions()[V.setreg()[S.first_reg]];
+          // the set's first region, and its block being served: the cached
+          // one, else (written back first) its first address in use with free
+          // ports and that address's thread block
+          const dpm::Set &S = V.sets()[set_p];
+          const uint32_t reg = V.setreg()[S.first_reg];
+          if (!(s_c[0] && s_c[1] == reg) && fc.force_seq != 2) {
+            if (s_c[0]) {
+              dpm::Addr &A0 = V.recs()[s_c[2]];
+              const uint32_t tb0 = s_c[3] & 0xffu;
+              uint32_t full = 0xffffffffu;
+              for (int x = 0; x < 8; x++) { A0.bm[tb0][x] = s_bm[x]; full &= s_bm[x]; }
+              A0.blive[tb0] = (uint16_t)(A0.blive[tb0] + s_c[8]);
+              if (full == 0xffffffffu && s_c[8]) A0.nonfull--;
+              s_c[0] = 0;
+            }
+            const dpm::Region &G = V.regions()[reg];
             uint32_t a = dpm::kNone;
             for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
               if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
@@ -5048,37 +5117,79 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
               const dpm::Addr &A = V.recs()[a];
               const uint32_t tb = (uint32_t)A.thread_block;
               if ((A.bflag[tb] & 2) && dpm::block_base(A, tb) != 0) {
-                uint32_t fr = 0;
-                for (int k = 0; k < 8; k++) { s_bm[k] = A.bm[tb][k]; fr += __popc(~A.bm[tb][k]); }
                 const dpm::A128 aa = dpm::addr_of(V, A);
                 uint32_t w[4] = {0, 0, 0, 0};
                 if (G.fam == 4) w[0] = aa.w[3];
                 else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
-                if (fr && pfw::unicast(G.fam, w)) {
-                  f = 1;
-                  s_b[1] = a; s_b[2] = dpm::block_base(A, tb) | tb; s_b[3] = fr;
-                  for (int k = 0; k < 4; k++) s_b[4 + k] = w[k];
+                if (pfw::unicast(G.fam, w)) {
+                  for (int k = 0; k < 8; k++) s_bm[k] = A.bm[tb][k];
+                  s_c[0] = 1; s_c[1] = reg; s_c[2] = a; s_c[3] = dpm::block_base(A, tb) | tb;
+                  for (int k = 0; k < 4; k++) s_c[4 + k] = w[k];
+                  s_c[8] = 0;
                 }
               }
             }
           }
-          s_b[0] = f;
+          uint32_t fr = 0;
+          if (s_c[0] && s_c[1] == reg)
+            for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~s_bm[k]);
+          if (!fr && fc.force_seq != 2 && !m.sfail) {
+            // the address's next block, as port_alloc opens it (its thread
+            // block full or gone: the first free block from current_alloc_index)
+            // for a record that keeps its port (so no block dies on the way)
+            if (s_c[0]) {
+              dpm::Addr &A0 = V.recs()[s_c[2]];
+              const uint32_t tb0 = s_c[3] & 0xffu;
+              uint32_t full = 0xffffffffu;
+              for (int x = 0; x < 8; x++) { A0.bm[tb0][x] = s_bm[x]; full &= s_bm[x]; }
+              A0.blive[tb0] = (uint16_t)(A0.blive[tb0] + s_c[8]);
+              if (full == 0xffffffffu && s_c[8]) A0.nonfull--;
+              s_c[0] = 0;
+            }
+            const dpm::Region &G = V.regions()[reg];
+            uint32_t a = dpm::kNone;
+            for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
+              if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
+            if (a != dpm::kNone) {
+              dpm::Addr &A = V.recs()[a];
+              const int32_t tb = A.thread_block;
+              const bool spent = tb < 0 || !(A.bflag[tb] & 2) || dpm::bm_full(A.bm[tb]);
+              uint32_t idx = dpm::kNone;
+              if (spent)
+                for (uint32_t k = 0; k < 256; k++) {
+                  const uint32_t x = (A.cur + k) & 0xffu;
+                  if (A.bflag[x] & 1) { idx = x; break; }
+                }
+              const dpm::A128 aa = dpm::addr_of(V, A);
+              uint32_t w[4] = {0, 0, 0, 0};
+              if (G.fam == 4) w[0] = aa.w[3];
+              else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
+              if (idx != dpm::kNone && dpm::block_base(A, idx) != 0 && pfw::unicast(G.fam, w)) {
+                A.thread_block = (int32_t)idx;
+                A.cur = idx;
+                dpm::block_new(V, a, idx, m.allow_null);
+                for (int k = 0; k < 8; k++) s_bm[k] = A.bm[idx][k];
+                s_c[0] = 1; s_c[1] = reg; s_c[2] = a; s_c[3] = dpm::block_base(A, idx) | idx;
+                for (int k = 0; k < 4; k++) s_c[4 + k] = w[k];
+                s_c[8] = 0;
+                for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~s_bm[k]);
+              }
+            }
+          }
+          bool p_eq = m.eqp;
+          for (int k = 0; k < 4; k++) p_eq = p_eq && m.ik.w[7 + k] == pfw::bswap(s_c[4 + k]);
+          s_c[9] = fr && !p_eq ? fr : 0u;
         }
         __syncthreads();
         { const uint64_t x = clock64(); tk[4] += x - ta; ta = x; }
-        // (a first record that could meet related_pair at this address allocates alone)
-        bool p_eq = false;
-        if (t == p && s_b[0]) {
-          p_eq = m.eqp;
-          for (int k = 0; k < 4; k++) p_eq = p_eq && m.ik.w[7 + k] == pfw::bswap(s_b[4 + k]);
-        }
-        if (s_b[0] && !((__ballot(p_eq) >> p) & 1)) {
+        const uint32_t fr = s_c[9];
+        if (fr) {
           // the records from p on asking the same set, up to one whose
           // reverse key could equal its initial key (related_pair) at this
           // address: served while the block has free ports
-          const uint32_t a = s_b[1], tb = s_b[2] & 0xffu, base = s_b[2] & ~0xffu, fr = s_b[3];
+          const uint32_t a = s_c[2], base = s_c[3] & ~0xffu;
           uint32_t w[4];
-          for (int k = 0; k < 4; k++) w[k] = s_b[4 + k];
+          for (int k = 0; k < 4; k++) w[k] = s_c[4 + k];
           bool stop = false;
           if (!done && ((pend >> t) & 1)) {
             bool eqa = m.eqp;
@@ -5119,58 +5230,70 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           __syncthreads();
           { const uint64_t x = clock64(); tk[5] += x - ta; ta = x; }
           if (t == p) {
-            // the block's bitmap after `taken` allocations: its lowest free
-            // ports (built from the copy, stored once)
-            dpm::Addr &A = V.recs()[a];
-            uint32_t left = taken, full = 0xffffffffu;
+            // the block's bitmap after `taken` allocations: its lowest free ports
+            uint32_t left = taken;
             for (int x = 0; x < 8; x++) {
-              uint32_t w = s_bm[x];
-              while (left && ~w) {
-                w |= ~w & (w + 1);  // the lowest clear bit
+              uint32_t v = s_bm[x];
+              while (left && ~v) {
+                v |= ~v & (v + 1);  // the lowest clear bit
                 left--;
               }
-              A.bm[tb][x] = w;
-              full &= w;
+              s_bm[x] = v;
             }
-            A.blive[tb] = (uint16_t)(A.blive[tb] + taken);
-            if (full == 0xffffffffu) A.nonfull--;
+            s_c[8] += taken;
             fast_n += taken;
           }
-        } else if (t == p) {
-          // alone: as resolve_masq allocates
-          const uint32_t e = dpm::set_alloc(V, m.set, m.allow_null, rec, aport);
-          if (e != dpm::OK) {
-            R.mverdict = pfw::masq_done(e);
-          } else {
-            pfw::masq_aip(fc, R, rec, aip);
-            const uint32_t v = pfw::masq_post(R, m, aip, aport);
-            if (v) { dpm::release(V, rec, aport); R.mverdict = v; }
-            else ok = true;
+          __syncthreads();
+        } else {
+          // alone, as resolve_masq allocates (on the allocator as it is)
+          flush();
+          if (t == p) {
+            const uint32_t e = dpm::set_alloc(V, m.set, m.allow_null, rec, aport);
+            if (e != dpm::OK) {
+              R.mverdict = pfw::masq_done(e);
+            } else {
+              pfw::masq_aip(fc, R, rec, aip);
+              const uint32_t v = pfw::masq_post(R, m, aip, aport);
+              if (v) { dpm::release(V, rec, aport); R.mverdict = v; }
+              else ok = true;
+            }
+            done = true;
+            lone_n++;
           }
-          done = true;
-          lone_n++;
+          lane_fence();
+          __syncthreads();
         }
-        lane_fence();
-        __syncthreads();
         { const uint64_t x = clock64(); tk[6] += x - ta; ta = x; }
       }
       { const uint64_t x = clock64(); tk[1] += x - t0; t0 = x; }
-      // the run's pairs, in parallel (distinct initial keys; distinct tuples)
-      bool give_back = false;
-      if (ok && ((run >> t) & 1)) {
-        if (!pfw::masq_pair(qp, R, m, rec, aport, aip, give_back)) atomicAdd(&fc.pf_cnt[16], 1u);
+      if (post) {
+        // the allocation, for dp_nat_pairs
+        if ((run >> t) & 1)
+          fc.lane_res[2 * (uint64_t)(k0 + t)] = make_uint4(ok ? 1u : 0u, rec, aport, 0u),
+          fc.lane_res[2 * (uint64_t)(k0 + t) + 1] = make_uint4(aip[0], aip[1], aip[2], aip[3]);
         ok = false;
-      }
-      lane_fence();
-      for (uint64_t gb = __ballot(give_back); gb; gb &= gb - 1) {
-        if (t == __ffsll((long long)gb) - 1) dpm::release(V, rec, aport);
+      } else {
+        // the run's pairs, in parallel (distinct initial keys; distinct tuples)
+        bool give_back = false;
+        if (ok && ((run >> t) & 1)) {
+          if (!pfw::masq_pair(qp, R, m, rec, aport, aip, give_back)) atomicAdd(&fc.pf_cnt[16], 1u);
+          ok = false;
+        }
         lane_fence();
+        if (__ballot(give_back)) {
+          flush();
+          for (uint64_t gb = __ballot(give_back); gb; gb &= gb - 1) {
+            if (t == __ffsll((long long)gb) - 1) dpm::release(V, rec, aport);
+            lane_fence();
+          }
+        }
       }
       { const uint64_t x = clock64(); tk[2] += x - t0; t0 = x; }
       i = j;
     }
   }
-  if (t == 0) {
+  flush();
+  if (t == 0 && !post) {
     // the flows replaced during the burst are dropped after it, with the
     // allocations their masquerade state owns
     for (uint32_t k = 0; k < fc.pf_cnt[3]; k++) dpm::release(V, fc.mq_rel[2 * k], fc.mq_rel[2 * k + 1]);
@@ -5189,6 +5312,39 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
     fc.pf_cnt[15] += ln;
     if (v) atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), (unsigned long long)v);
   }
+}
+
+// dp_nat_pairs: the allocating lane's pairs, all at once, when no record of
+// it ran alone and no initial key repeats (dp_nat_lane_plan): then no pair's
+// inserts meet another's keys or any record's live flow state, and the lane's
+// allocations never depended on them (the table has room: no insert is
+// refused).  dp_nat_lane_end then drops the replaced fills' allocations.
+__global__ void __launch_bounds__(256) dp_nat_pairs(const uint8_t *__restrict__ img_base,
+                                                    const Image *__restrict__ im, dpf::FlowCtx fc) {
+  if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3 || fc.pf_cnt[28] || fc.pf_cnt[29]) return;
+  const uint32_t nl = fc.pf_cnt[11];
+  const Img g{img_base, *im};
+  const pfw::Seq qp{fc, g, true};
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < nl; k += gridDim.x * 256) {
+    const uint4 r0 = fc.lane_res[2 * (uint64_t)k];
+    if (!r0.x) continue;
+    const uint4 r1 = fc.lane_res[2 * (uint64_t)k + 1];
+    pfw::LanePlan P;
+    uint4 *w = reinterpret_cast<uint4 *>(&P);
+    for (int j = 0; j < 8; j++) w[j] = fc.lane_plan[8 * (uint64_t)k + j];
+    const uint32_t aip[4] = {r1.x, r1.y, r1.z, r1.w};
+    bool give_back = false;
+    if (!pfw::masq_pair(qp, fc.pf[P.rec], P.m, r0.y, r0.z, aip, give_back)) atomicAdd(&fc.pf_cnt[16], 1u);
+  }
+  uint32_t v = qp.added;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0 && v)
+    atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), (unsigned long long)v);
+}
+__global__ void dp_nat_lane_end(dpf::FlowCtx fc) {
+  if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3 || fc.pf_cnt[28] || fc.pf_cnt[29] || !fc.mq) return;
+  const dpm::View V{fc.mq};
+  for (uint32_t k = 0; k < fc.pf_cnt[3]; k++) dpm::release(V, fc.mq_rel[2 * k], fc.mq_rel[2 * k + 1]);
 }
 
 // dp_acl_classify: AclFilter's classification alone (dpgpu.h "The ACL
@@ -5641,7 +5797,6 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   order(0);
   hipLaunchKernelGGL(dp_nat_mark, dim3(rb0), dim3(256), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_prep, dim3(pb), dim3(1024), 0, stream, img_base, im, fc);
-  hipLaunchKernelGGL(dp_nat_steady, dim3(rb0), dim3(256), 0, stream, fc);
   const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
   // port forwarding near the capacity: the creations' admissions in packet order
   hipLaunchKernelGGL(dp_nat_admit_plan, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
@@ -5655,6 +5810,8 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   order(1);
   hipLaunchKernelGGL(dp_nat_lane_plan, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_lane, dim3(1), dim3(64), 0, stream, img_base, im, fc);
+  hipLaunchKernelGGL(dp_nat_pairs, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
+  hipLaunchKernelGGL(dp_nat_lane_end, dim3(1), dim3(1), 0, stream, fc);
   fc.replay = 1;
   if (meta) dpk_run_pipeline_111(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
   else dpk_run_pipeline_101(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);

@@ -67,6 +67,7 @@ def test_gpu_masquerade_at_scale():
         assert hist(out) == {"Delivered": 250_000}
         assert int(cnt[12]) == 3 and int(cnt[11]) == 250_000, cnt
         assert int(cnt[14]) > 200_000, cnt  # served in wave batches
+        assert int(cnt[28]) == 0 and int(cnt[29]) == 0, cnt  # their pairs after the lane (dp_nat_pairs)
         assert c.learn(ob, out) == 250_000
         keys = c.keys()
         assert same_flows(ro, rg, keys, "first packets") == 250_000
