@@ -203,6 +203,7 @@ struct FlowCtx {
   uint32_t *lane_bits, *lane_sum, *lane_order;
   uint4 *lane_plan;     // per lane record: its class and plan (dp_nat_lane_plan, 128 B)
   uint4 *lane_res;      // per lane record: its allocation for dp_nat_pairs (32 B)
+  uint4 *lane_key;      // per lane record: what the lane's allocation step reads of its plan (48 B)
   unsigned long long *dup_tab;  // (burst << 32 | initial key hash) of the lane's allocating records
   // port forwarding near the capacity (mode 4): per record the new slots its
   // creation adds, then the sum of those of the records before it in packet

@@ -4909,6 +4909,7 @@ __global__ void __launch_bounds__(256) dp_nat_lane_plan(const uint8_t *__restric
   const uint32_t nl = fc.pf_cnt[11];
   const Img g{img_base, *im};
   const pfw::Seq qs{fc, g, false};
+  const dpm::View V{fc.mq};
   const uint64_t len0 = ((uint64_t)fc.tmeta[3] << 32) | fc.tmeta[2];
   const bool room = len0 + 2ull * nl <= fc.capacity && len0 + 2ull * nl <= fc.hard;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -4977,6 +4978,15 @@ __global__ void __launch_bounds__(256) dp_nat_lane_plan(const uint8_t *__restric
     if (has) {
       const uint4 *w = reinterpret_cast<const uint4 *>(&L);
       for (int x = 0; x < 8; x++) fc.lane_plan[8 * (uint64_t)k + x] = w[x];
+      // what the lane's step reads of it (dp_nat_lane): the record, class |
+      // (pd + 1) << 8 | eqp << 16 | allow_null << 17, the set and its first
+      // region, sfail, the initial key's address words the eqp test compares
+      const bool c3r = (L.cls & 0xffu) == 3;
+      const uint32_t reg = c3r ? V.setreg()[V.sets()[L.m.set].first_reg] : 0u;
+      const uint32_t fl = L.cls | (c3r && L.m.eqp ? 1u << 16 : 0u) | (c3r && L.m.allow_null ? 1u << 17 : 0u);
+      fc.lane_key[3 * (uint64_t)k] = make_uint4(L.rec, fl, L.m.set, reg);
+      fc.lane_key[3 * (uint64_t)k + 1] = make_uint4(L.m.sfail, L.m.ik.w[7], L.m.ik.w[8], L.m.ik.w[9]);
+      fc.lane_key[3 * (uint64_t)k + 2] = make_uint4(L.m.ik.w[10], 0u, 0u, 0u);
     }
     __syncthreads();
   }
@@ -5003,6 +5013,16 @@ __device__ __forceinline__ void lane_fence() { __builtin_amdgcn_fence(__ATOMIC_S
 // anything else reads the allocator).  Then the run's pairs are created in
 // parallel -- or, when no record runs alone and no initial key repeats, every
 // pair after the lane (dp_nat_pairs; the allocations go to lane_res).
+// The k-th (from 0) set bit of x (k < popc(x))
+__device__ __forceinline__ uint32_t nth_bit(uint32_t x, uint32_t k) {
+  uint32_t pos = 0;
+  for (uint32_t sh = 16; sh; sh >>= 1) {
+    const uint32_t c = (uint32_t)__popc(x & ((1u << sh) - 1));
+    if (k >= c) { k -= c; x >>= sh; pos += sh; }
+  }
+  return pos;
+}
+
 __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ img_base,
                                                   const Image *__restrict__ im, dpf::FlowCtx fc) {
   if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3) return;
@@ -5015,42 +5035,64 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   __shared__ uint32_t s_bm[8];  // the block being served: its usage bitmap
   // the block being served: [0] valid, [1] region, [2] address record,
   // [3] block | its first port, [4..7] the address, [8] ports taken since it
-  // was loaded, [9] the first step of the step: 1 fast
+  // was loaded
   __shared__ uint32_t s_c[10];
   if (t == 0) s_c[0] = 0;
   __syncthreads();
-  // the cached block back to the allocator (the lane p that holds it)
-  auto flush = [&]() {
-    if (t == 0 && s_c[0]) {
-      dpm::Addr &A = V.recs()[s_c[2]];
-      const uint32_t tb = s_c[3] & 0xffu;
+  // the cached block back to the allocator (by the calling lane)
+  auto write_back = [&]() {
+    if (s_c[0]) {
+      dpm::Addr &A0 = V.recs()[s_c[2]];
+      const uint32_t tb0 = s_c[3] & 0xffu;
       uint32_t full = 0xffffffffu;
-      for (int x = 0; x < 8; x++) { A.bm[tb][x] = s_bm[x]; full &= s_bm[x]; }
-      A.blive[tb] = (uint16_t)(A.blive[tb] + s_c[8]);
-      if (full == 0xffffffffu && s_c[8]) A.nonfull--;
+      for (int x = 0; x < 8; x++) { A0.bm[tb0][x] = s_bm[x]; full &= s_bm[x]; }
+      A0.blive[tb0] = (uint16_t)(A0.blive[tb0] + s_c[8]);
+      if (full == 0xffffffffu && s_c[8]) A0.nonfull--;
       s_c[0] = 0;
     }
+  };
+  auto flush = [&]() {
+    if (t == 0) write_back();
     lane_fence();
     __syncthreads();
   };
+  // a record's full plan (the allocation alone, the pairs in the lane)
+  auto plan_of = [&](uint32_t k) {
+    pfw::LanePlan P;
+    uint4 *w = reinterpret_cast<uint4 *>(&P);
+    for (int j = 0; j < 8; j++) w[j] = fc.lane_plan[8 * (uint64_t)k + j];
+    return P;
+  };
+  // what a step needs of the chunk's records (dp_nat_lane_plan's lane_key),
+  // the next chunk's loaded while this one is served
+  auto key_of = [&](uint32_t k0, uint4 &a, uint4 &b, uint4 &c) {
+    if (k0 + t < nl) {
+      const uint64_t k = 3 * (uint64_t)(k0 + t);
+      a = fc.lane_key[k]; b = fc.lane_key[k + 1]; c = fc.lane_key[k + 2];
+    } else {
+      a = b = c = make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
   uint32_t fast_n = 0, lone_n = 0, solo_n = 0;
-  // where the lane's time goes (clock64 ticks: plans, allocations, pairs,
-  // records alone), for the counters [19..22] in units of 1024 ticks
+  // where the lane's time goes (clock64 ticks: chunk keys, allocations, pairs,
+  // records alone, the step's block, the batch served, allocations alone),
+  // for the counters [19..25] in units of 1024 ticks
   uint64_t tk[7] = {0, 0, 0, 0, 0, 0, 0}, t0 = clock64(), ta;
   uint32_t steps = 0;
+  uint4 N0, N1, N2;
+  key_of(0, N0, N1, N2);
   for (uint32_t k0 = 0; k0 < nl; k0 += 64) {
     const uint32_t cnt = nl - k0 < 64 ? nl - k0 : 64;
-    const bool has = (uint32_t)t < cnt;
-    // the record's plan (dp_nat_lane_plan: 1 alone, 2 decided, 3 allocates;
-    // the latest earlier record of the chunk with its initial key)
-    pfw::LanePlan P{};
-    if (has) {
-      uint4 *w = reinterpret_cast<uint4 *>(&P);
-      for (int j = 0; j < 8; j++) w[j] = fc.lane_plan[8 * (uint64_t)(k0 + t) + j];
-    }
-    const uint32_t ri = P.rec, cls = P.cls & 0xffu;
-    const int pd = (int)(P.cls >> 8) - 1;
-    const pfw::MPlan &m = P.m;
+    const uint4 K0 = N0, K1 = N1, K2 = N2;
+    if (k0 + 64 < nl) key_of(k0 + 64, N0, N1, N2);
+    // the record's class (1 alone, 2 decided, 3 allocates), the latest earlier
+    // record of the chunk with its initial key, its set and that set's first
+    // region, the verdict its checks give whatever the tuple, its address
+    const uint32_t ri = K0.x, cls = K0.y & 0xffu;
+    const int pd = (int)((K0.y >> 8) & 0xffu) - 1;
+    const bool eqp = (K0.y >> 16) & 1u;
+    const uint32_t mset = K0.z, mreg = K0.w, sfail = K1.x;
+    const uint32_t ia[4] = {K1.y, K1.z, K1.w, K2.x};
     dpf::PfReq &R = fc.pf[ri];
     const uint64_t c1 = __ballot(cls == 1), c3 = __ballot(cls == 3);
     const uint64_t cuts = __ballot(cls == 1 || (cls == 3 && pd >= 0));
@@ -5090,170 +5132,146 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         const uint64_t pend = __ballot(!done) & c3 & run;
         if (!pend) break;
         const int p = __ffsll((long long)pend) - 1;
-        const uint32_t set_p = (uint32_t)__shfl((int)m.set, p);
+        const uint32_t set_p = (uint32_t)__shfl((int)mset, p), reg_p = (uint32_t)__shfl((int)mreg, p);
         ta = clock64();
         steps++;
-        if (t == p) {
-          // the set's first region, and its block being served: the cached
-          // one, else (written back first) its first address in use with free
-          // ports and that address's thread block
-          const dpm::Set &S = V.sets()[set_p];
-          const uint32_t reg = V.setreg()[S.first_reg];
-          if (!(s_c[0] && s_c[1] == reg) && fc.force_seq != 2) {
-            if (s_c[0]) {
-              dpm::Addr &A0 = V.recs()[s_c[2]];
-              const uint32_t tb0 = s_c[3] & 0xffu;
-              uint32_t full = 0xffffffffu;
-              for (int x = 0; x < 8; x++) { A0.bm[tb0][x] = s_bm[x]; full &= s_bm[x]; }
-              A0.blive[tb0] = (uint16_t)(A0.blive[tb0] + s_c[8]);
-              if (full == 0xffffffffu && s_c[8]) A0.nonfull--;
-              s_c[0] = 0;
+        // the set's first region's block being served: the cached one while
+        // it has free ports, else (the cached one written back first) the
+        // region's first address in use with free ports and its thread block,
+        // or for a record that keeps its port (so no block dies on the way)
+        // the address's next block, as port_alloc opens it (its thread block
+        // full or gone: the first free block from current_alloc_index)
+        uint32_t f = 0;
+        const bool hit = s_c[0] && s_c[1] == reg_p;
+        if (hit && t < 8) f = ~s_bm[t];
+        if ((!hit || !__ballot(f != 0)) && fc.force_seq != 2) {
+          if (t == p) {
+            if (!hit) {
+              write_back();
+              const dpm::Region &G = V.regions()[reg_p];
+              uint32_t a = dpm::kNone;
+              for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
+                if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
+              if (a != dpm::kNone && V.recs()[a].thread_block >= 0) {
+                const dpm::Addr &A = V.recs()[a];
+                const uint32_t tb = (uint32_t)A.thread_block;
+                if ((A.bflag[tb] & 2) && dpm::block_base(A, tb) != 0) {
+                  const dpm::A128 aa = dpm::addr_of(V, A);
+                  uint32_t w[4] = {0, 0, 0, 0};
+                  if (G.fam == 4) w[0] = aa.w[3];
+                  else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
+                  if (pfw::unicast(G.fam, w)) {
+                    for (int k = 0; k < 8; k++) s_bm[k] = A.bm[tb][k];
+                    s_c[0] = 1; s_c[1] = reg_p; s_c[2] = a; s_c[3] = dpm::block_base(A, tb) | tb;
+                    for (int k = 0; k < 4; k++) s_c[4 + k] = w[k];
+                    s_c[8] = 0;
+                  }
+                }
+              }
             }
-            const dpm::Region &G = V.regions()[reg];
-            uint32_t a = dpm::kNone;
-            for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
-              if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
-            if (a != dpm::kNone && V.recs()[a].thread_block >= 0) {
-              const dpm::Addr &A = V.recs()[a];
-              const uint32_t tb = (uint32_t)A.thread_block;
-              if ((A.bflag[tb] & 2) && dpm::block_base(A, tb) != 0) {
+            uint32_t fr = 0;
+            if (s_c[0])
+              for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~s_bm[k]);
+            if (!fr && !sfail) {
+              write_back();
+              const dpm::Region &G = V.regions()[reg_p];
+              uint32_t a = dpm::kNone;
+              for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
+                if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
+              if (a != dpm::kNone) {
+                dpm::Addr &A = V.recs()[a];
+                const int32_t tb = A.thread_block;
+                const bool spent = tb < 0 || !(A.bflag[tb] & 2) || dpm::bm_full(A.bm[tb]);
+                uint32_t idx = dpm::kNone;
+                if (spent)
+                  for (uint32_t k = 0; k < 256; k++) {
+                    const uint32_t x = (A.cur + k) & 0xffu;
+                    if (A.bflag[x] & 1) { idx = x; break; }
+                  }
                 const dpm::A128 aa = dpm::addr_of(V, A);
                 uint32_t w[4] = {0, 0, 0, 0};
                 if (G.fam == 4) w[0] = aa.w[3];
                 else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
-                if (pfw::unicast(G.fam, w)) {
-                  for (int k = 0; k < 8; k++) s_bm[k] = A.bm[tb][k];
-                  s_c[0] = 1; s_c[1] = reg; s_c[2] = a; s_c[3] = dpm::block_base(A, tb) | tb;
+                if (idx != dpm::kNone && dpm::block_base(A, idx) != 0 && pfw::unicast(G.fam, w)) {
+                  A.thread_block = (int32_t)idx;
+                  A.cur = idx;
+                  dpm::block_new(V, a, idx, (K0.y >> 17) & 1u);
+                  for (int k = 0; k < 8; k++) s_bm[k] = A.bm[idx][k];
+                  s_c[0] = 1; s_c[1] = reg_p; s_c[2] = a; s_c[3] = dpm::block_base(A, idx) | idx;
                   for (int k = 0; k < 4; k++) s_c[4 + k] = w[k];
                   s_c[8] = 0;
                 }
               }
             }
           }
-          uint32_t fr = 0;
-          if (s_c[0] && s_c[1] == reg)
-            for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~s_bm[k]);
-          if (!fr && fc.force_seq != 2 && !m.sfail) {
-            // the address's next block, as port_alloc opens it (its thread
-            // block full or gone: the first free block from current_alloc_index)
-            // for a record that keeps its port (so no block dies on the way)
-            if (s_c[0]) {
-              dpm::Addr &A0 = V.recs()[s_c[2]];
-              const uint32_t tb0 = s_c[3] & 0xffu;
-              uint32_t full = 0xffffffffu;
-              for (int x = 0; x < 8; x++) { A0.bm[tb0][x] = s_bm[x]; full &= s_bm[x]; }
-              A0.blive[tb0] = (uint16_t)(A0.blive[tb0] + s_c[8]);
-              if (full == 0xffffffffu && s_c[8]) A0.nonfull--;
-              s_c[0] = 0;
-            }
-            const dpm::Region &G = V.regions()[reg];
-            uint32_t a = dpm::kNone;
-            for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
-              if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
-            if (a != dpm::kNone) {
-              dpm::Addr &A = V.recs()[a];
-              const int32_t tb = A.thread_block;
-              const bool spent = tb < 0 || !(A.bflag[tb] & 2) || dpm::bm_full(A.bm[tb]);
-              uint32_t idx = dpm::kNone;
-              if (spent)
-                for (uint32_t k = 0; k < 256; k++) {
-                  const uint32_t x = (A.cur + k) & 0xffu;
-                  if (A.bflag[x] & 1) { idx = x; break; }
-                }
-              const dpm::A128 aa = dpm::addr_of(V, A);
-              uint32_t w[4] = {0, 0, 0, 0};
-              if (G.fam == 4) w[0] = aa.w[3];
-              else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
-              if (idx != dpm::kNone && dpm::block_base(A, idx) != 0 && pfw::unicast(G.fam, w)) {
-                A.thread_block = (int32_t)idx;
-                A.cur = idx;
-                dpm::block_new(V, a, idx, m.allow_null);
-                for (int k = 0; k < 8; k++) s_bm[k] = A.bm[idx][k];
-                s_c[0] = 1; s_c[1] = reg; s_c[2] = a; s_c[3] = dpm::block_base(A, idx) | idx;
-                for (int k = 0; k < 4; k++) s_c[4 + k] = w[k];
-                s_c[8] = 0;
-                for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~s_bm[k]);
-              }
-            }
-          }
-          bool p_eq = m.eqp;
-          for (int k = 0; k < 4; k++) p_eq = p_eq && m.ik.w[7 + k] == pfw::bswap(s_c[4 + k]);
-          s_c[9] = fr && !p_eq ? fr : 0u;
+          __syncthreads();
+          f = s_c[0] && s_c[1] == reg_p && t < 8 ? ~s_bm[t] : 0u;
         }
-        __syncthreads();
+        // the block's free ports: per word (lanes 0..7) and before it
+        const uint32_t fc_n = (uint32_t)__popc(f);
+        uint32_t pre = fc_n;
+        for (int o = 1; o < 8; o <<= 1) {
+          const uint32_t v = (uint32_t)__shfl_up((int)pre, o);
+          if (t >= o) pre += v;
+        }
+        const uint32_t fr_all = (uint32_t)__builtin_amdgcn_readlane((int)pre, 7);
+        // a record whose reverse key could equal its initial key (related_pair)
+        // at the block's address goes alone, and stops the batch before it
+        bool eqa = eqp;
+        for (int k = 0; k < 4; k++) eqa = eqa && ia[k] == pfw::bswap(s_c[4 + k]);
+        const bool p_eq = (__ballot(eqa) >> p) & 1;
+        const uint32_t fr = fr_all && !p_eq ? fr_all : 0u;
         { const uint64_t x = clock64(); tk[4] += x - ta; ta = x; }
-        const uint32_t fr = s_c[9];
         if (fr) {
           // the records from p on asking the same set, up to one whose
-          // reverse key could equal its initial key (related_pair) at this
-          // address: served while the block has free ports
+          // reverse key could equal its initial key: served while the block
+          // has free ports, in packet order
           const uint32_t a = s_c[2], base = s_c[3] & ~0xffu;
-          uint32_t w[4];
-          for (int k = 0; k < 4; k++) w[k] = s_c[4 + k];
           bool stop = false;
-          if (!done && ((pend >> t) & 1)) {
-            bool eqa = m.eqp;
-            for (int k = 0; k < 4; k++) eqa = eqa && m.ik.w[7 + k] == pfw::bswap(w[k]);
-            stop = m.set != set_p || eqa;
-          }
+          if (!done && ((pend >> t) & 1)) stop = mset != set_p || eqa;
           const uint64_t st = __ballot(stop) & pend;
           const uint64_t grp = st ? pend & ((1ull << (__ffsll((long long)st) - 1)) - 1) : pend;
           const bool mine = (grp >> t) & 1;
-          const uint64_t cons = __ballot(mine && !m.sfail) & grp;
+          const uint64_t cons = __ballot(mine && !sfail) & grp;
           const uint32_t before = (uint32_t)__popcll(cons & lanes_below(t));
           const bool served = mine && before < fr;
           const uint32_t taken = (uint32_t)__popcll(cons) < fr ? (uint32_t)__popcll(cons) : fr;
+          // the before-th free port: its word, then its bit
+          uint32_t wsel = 0;
+          for (int x = 0; x < 7; x++) wsel += (uint32_t)__builtin_amdgcn_readlane((int)pre, x) <= before ? 1u : 0u;
+          const uint32_t fw = (uint32_t)__shfl((int)f, (int)wsel), fb = (uint32_t)__shfl((int)(pre - fc_n), (int)wsel);
           if (served) {
-            if (m.sfail) {
-              R.mverdict = m.sfail;
+            if (sfail) {
+              R.mverdict = sfail;
             } else {
-              // the before-th free port of the block
-              uint32_t k = before, port = 0;
-              for (int x = 0; x < 8; x++) {
-                const uint32_t fw = ~s_bm[x];
-                const uint32_t c = (uint32_t)__popc(fw);
-                if (k < c) {
-                  uint32_t b = fw;
-                  for (uint32_t y = 0; y < k; y++) b &= b - 1;
-                  port = 32 * x + (uint32_t)__ffs(b) - 1;
-                  break;
-                }
-                k -= c;
-              }
               rec = a;
-              aport = base + port;
-              for (int x = 0; x < 4; x++) aip[x] = w[x];
+              aport = base + 32 * wsel + nth_bit(fw, before - fb);
+              for (int x = 0; x < 4; x++) aip[x] = s_c[4 + x];
               ok = true;
             }
             done = true;
           }
+          // the block's bitmap after `taken` allocations: its lowest free ports
+          if (t < 8) {
+            const uint32_t below = pre - fc_n;
+            const uint32_t n = taken > below ? (taken - below < fc_n ? taken - below : fc_n) : 0u;
+            if (n) s_bm[t] = ~f | (n == fc_n ? f : f & ((1u << nth_bit(f, n)) - 1));
+          }
+          if (t == 0) s_c[8] += taken;
+          if (t == p) fast_n += taken;
           __syncthreads();
           { const uint64_t x = clock64(); tk[5] += x - ta; ta = x; }
-          if (t == p) {
-            // the block's bitmap after `taken` allocations: its lowest free ports
-            uint32_t left = taken;
-            for (int x = 0; x < 8; x++) {
-              uint32_t v = s_bm[x];
-              while (left && ~v) {
-                v |= ~v & (v + 1);  // the lowest clear bit
-                left--;
-              }
-              s_bm[x] = v;
-            }
-            s_c[8] += taken;
-            fast_n += taken;
-          }
-          __syncthreads();
         } else {
           // alone, as resolve_masq allocates (on the allocator as it is)
           flush();
           if (t == p) {
-            const uint32_t e = dpm::set_alloc(V, m.set, m.allow_null, rec, aport);
+            const pfw::LanePlan P = plan_of(k0 + p);
+            const uint32_t e = dpm::set_alloc(V, P.m.set, P.m.allow_null, rec, aport);
             if (e != dpm::OK) {
               R.mverdict = pfw::masq_done(e);
             } else {
               pfw::masq_aip(fc, R, rec, aip);
-              const uint32_t v = pfw::masq_post(R, m, aip, aport);
+              const uint32_t v = pfw::masq_post(R, P.m, aip, aport);
               if (v) { dpm::release(V, rec, aport); R.mverdict = v; }
               else ok = true;
             }
@@ -5262,8 +5280,8 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           }
           lane_fence();
           __syncthreads();
+          { const uint64_t x = clock64(); tk[6] += x - ta; ta = x; }
         }
-        { const uint64_t x = clock64(); tk[6] += x - ta; ta = x; }
       }
       { const uint64_t x = clock64(); tk[1] += x - t0; t0 = x; }
       if (post) {
@@ -5276,7 +5294,8 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         // the run's pairs, in parallel (distinct initial keys; distinct tuples)
         bool give_back = false;
         if (ok && ((run >> t) & 1)) {
-          if (!pfw::masq_pair(qp, R, m, rec, aport, aip, give_back)) atomicAdd(&fc.pf_cnt[16], 1u);
+          const pfw::LanePlan P = plan_of(k0 + t);
+          if (!pfw::masq_pair(qp, R, P.m, rec, aport, aip, give_back)) atomicAdd(&fc.pf_cnt[16], 1u);
           ok = false;
         }
         lane_fence();
