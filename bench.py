@@ -271,7 +271,7 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
         c = (C.c_uint32 * 32)()
         lib.dpf_debug_nat_counters(nf2.ctx, c, 32)
         return {"mode": int(c[12]), "records": int(c[1]), "lane_records": int(c[11]),
-                "left_by_connections": int(c[13]), "allocations_batched": int(c[14]),
+                "connections": int(c[4]), "left_by_connections": int(c[13]), "allocations_batched": int(c[14]),
                 "allocations_alone": int(c[15]), "lane_kticks": [int(c[19 + k]) for k in range(7)],
                 "allocation_steps": int(c[26]), "steady_refreshes": bool(c[27])}
 

@@ -4310,6 +4310,23 @@ __device__ __forceinline__ void flag_wave(uint32_t *w, bool want) {
 #endif
 }
 
+// Burst-wide flags raised inside a grid-stride loop: each lane gathers its
+// bits over the loop (flags), the workgroup ORs them in LDS after it, and one
+// lane raises each word (flag_once) -- one access per workgroup, where a
+// per-wave access per iteration queued tens of thousands of accesses to one
+// word.  Every thread of the workgroup calls it once, after its loop.
+__device__ __forceinline__ void flags_block(uint32_t *s_fl, uint32_t fl, uint32_t *const *words, int nw) {
+#ifdef DP_EMU
+  for (int k = 0; k < nw; k++) if (fl & (1u << k)) flag_once(words[k]);
+#else
+  if (fl) atomicOr(s_fl, fl);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int k = 0; k < nw; k++)
+      if (*s_fl & (1u << k)) flag_once(words[k]);
+#endif
+}
+
 // Could this record's packet be given a tuple (an expose covers its initial
 // source) while its initial destination is a public address of the
 // allocator?  Then its initial key may be the reverse key of a pair another
@@ -4364,6 +4381,40 @@ __device__ __forceinline__ void lane_mark(const dpf::FlowCtx &fc, dpf::PfReq &R,
   if (!(__hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & sb)) atomicOr(sw, sb);
 }
 
+// A record's leading words (through dst_vni: what the burst-wide NAT kernels
+// read of it; the fields after it are left undefined) and a flow slot, read
+// into registers at once.  The empty asm takes every word where the loads are
+// issued, so the compiler cannot sink them to their uses: a line read again
+// later, with a chip's worth of lanes in flight, has mostly left L2 and is
+// fetched from memory again.
+__device__ __forceinline__ dpf::PfReq load_req(const dpf::PfReq *p) {
+  constexpr int kW = (int)((offsetof(dpf::PfReq, dst_vni) + 4 + 7) / 8);
+  uint2 w[kW];
+  const uint2 *q = reinterpret_cast<const uint2 *>(p);
+#pragma unroll
+  for (int i = 0; i < kW; i++) w[i] = q[i];
+#ifndef DP_EMU
+#pragma unroll
+  for (int i = 0; i < kW; i++) asm volatile("" : "+v"(w[i].x), "+v"(w[i].y));
+#endif
+  dpf::PfReq R;
+  __builtin_memcpy(&R, w, sizeof w);
+  return R;
+}
+__device__ __forceinline__ dpf::FlowSlot load_slot(const dpf::FlowSlot *p) {
+  uint4 w[8];
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = q[i];
+#ifndef DP_EMU
+#pragma unroll
+  for (int i = 0; i < 8; i++) asm volatile("" : "+v"(w[i].x), "+v"(w[i].y), "+v"(w[i].z), "+v"(w[i].w));
+#endif
+  dpf::FlowSlot f;
+  __builtin_memcpy(&f, w, sizeof w);
+  return f;
+}
+
 // A masquerading record whose refresh leaves its pair's state as it is:
 // valid with masquerade state (get_masquerade_state), no ACL flow verdict, a
 // NatFlowStatus that the packet does not move (refresh_masquerade_state, nf.rs:
@@ -4373,33 +4424,41 @@ __device__ __forceinline__ void lane_mark(const dpf::FlowCtx &fc, dpf::PfReq &R,
 // record of the connection moves the state -- and its one write, the expiry's
 // push forward, is a maximum: it commutes with the burst's other records.
 // move: the record may move the state (its pair is tagged for the burst).
-__device__ bool masq_steady(const Seq &q, const dpf::PfReq &R, bool &move) {
-  const dpf::FlowCtx &fc = q.fc;
+//
+// Over copies of the record, its flow and the flow's related one
+// (o: fc.slots[f.related] when f.related <= fc.mask).  The burst-wide kernels
+// read each record and flow once into registers: with a chip's worth of lanes
+// in flight, a line read again later has mostly left L2 and is fetched again.
+__device__ bool masq_steady_v(const dpf::FlowCtx &fc, const dpf::PfReq &R, const dpf::FlowSlot &f,
+                              const dpf::FlowSlot &o, bool &move) {
   move = false;
   if ((R.bits & (dpf::kPqMasq | dpf::kPqPf | dpf::kPqSens)) != dpf::kPqMasq) return false;
-  if (R.slot > fc.mask || !fc.mq || !masq_valid(q, R)) return false;
-  const dpf::FlowSlot &f = fc.slots[R.slot];
+  if (R.slot > fc.mask || !fc.mq) return false;
+  // masq_valid: the attached fill, Active, its pair not invalidated for this
+  // packet, with masquerade state
+  if (f.state != R.state || R.status0 != DP_FLOW_ACTIVE) return false;
+  const bool rel = f.related <= fc.mask && o.state == f.related_tag;
+  const uint32_t pi = R.idx + 1;
+  if (f.mark <= pi || (rel && o.mark <= pi) || !(f.flags & dpf::kFlagMasq)) return false;
   const uint32_t proto = R.proto & 0xffu, tfl = R.proto >> 16;
   uint32_t src[4], dst[4], sport, dport;
   masq_cur(R, src, dst, sport, dport);
   const uint32_t act = f.pf & 0xffu, cur = (f.pf >> 8) & 0xffu;
   const uint32_t nw = masq_next_status(proto, R.bits & dpf::kPqUdp, sport, tfl, R.bits & dpf::kPqTcp, act, cur);
   if (nw != cur || nw == DP_NFS_CLOSED || nw == DP_NFS_RESET) { move = true; return false; }
-  // the pair: mutual, both with masquerade state, the forward flow's allocation live
-  if (!q.alive(f.related, f.related_tag)) return false;
-  const dpf::FlowSlot &o = fc.slots[f.related];
-  if (o.related != R.slot || !q.alive(R.slot, o.related_tag) || !(o.flags & dpf::kFlagMasq)) return false;
+  if (!rel) return false;
+  if (o.related != R.slot || f.state != o.related_tag || !(o.flags & dpf::kFlagMasq)) return false;
   const dpf::FlowSlot &F = act == DP_PF_SRC_NAT ? f : o, &Rv = act == DP_PF_SRC_NAT ? o : f;
   if ((F.pf & 0xffu) != DP_PF_SRC_NAT || (Rv.pf & 0xffu) != DP_PF_DST_NAT) return false;
   return F.mq_rec && F.mq_gen == fc.mq_gen;
 }
 
-// resolve_masq's refresh for a steady record (the expiry by atomicMax)
-__device__ void masq_steady_run(const dpf::FlowCtx &fc, dpf::PfReq &R) {
+// resolve_masq's refresh for a steady record (the expiry by atomicMax); f: a
+// copy of its flow
+__device__ void masq_steady_run(const dpf::FlowCtx &fc, dpf::PfReq &R, const dpf::FlowSlot &f) {
   R.verdict = dpf::kPfForward;
   R.acl_over = 0;
   R.mverdict = dpf::kPfForward;
-  const dpf::FlowSlot &f = fc.slots[R.slot];
   const uint32_t fam = (R.proto >> 8) & 0xffu;
   const bool tcp = R.bits & dpf::kPqTcp, udp = R.bits & dpf::kPqUdp, icmp = R.bits & dpf::kPqIcmp;
   const uint32_t act = f.pf & 0xffu, port = f.pf >> 16, cur = (f.pf >> 8) & 0xffu;
@@ -4643,23 +4702,31 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
                                                    const Image *__restrict__ im, dpf::FlowCtx fc) {
   const uint32_t nrec = fc.pf_cnt[0];
   if (!nrec) return;
-  const Img g{img_base, *im};
-  const pfw::Seq q{fc, g, true};
+  __shared__ uint32_t s_fl;
+  if (threadIdx.x == 0) s_fl = 0;
+  __syncthreads();
+  uint32_t fl = 0;  // the kinds seen: 1 port forwarding, 2 masquerade, 4 masq_back
   for (uint32_t rec = blockIdx.x * 256 + threadIdx.x; rec < nrec; rec += gridDim.x * 256) {
-    const dpf::PfReq &R = fc.pf[rec];
+    const dpf::PfReq R = pfw::load_req(&fc.pf[rec]);  // (the record, its flow and the related flow read once)
     // the burst's kinds of record (the NAT pass's mode rests on them)
-    const bool reached = R.bits & dpf::kPqReached;
-    pfw::flag_wave(&fc.pf_cnt[9], reached && (R.bits & dpf::kPqPf));
-    pfw::flag_wave(&fc.pf_cnt[8], reached && (R.bits & dpf::kPqMasq));
-    pfw::flag_wave(&fc.pf_cnt[10], reached && (R.bits & dpf::kPqMasq) && pfw::masq_back(fc, R));
-    if (!fc.mq || (R.bits & (dpf::kPqReached | dpf::kPqMasq)) != (dpf::kPqReached | dpf::kPqMasq)) continue;
-    if (R.slot > fc.mask || !q.alive(R.slot, R.state)) continue;
+    if (!(R.bits & dpf::kPqReached)) continue;
+    if (R.bits & dpf::kPqPf) fl |= 1u;
+    if (!(R.bits & dpf::kPqMasq)) continue;
+    fl |= 2u;
+    if (!(fl & 4u) && pfw::masq_back(fc, R)) fl |= 4u;
+    if (!fc.mq || R.slot > fc.mask) continue;
+    const dpf::FlowSlot f = pfw::load_slot(&fc.slots[R.slot]);
+    if (f.state != R.state) continue;
+    dpf::FlowSlot o;
+    if (f.related <= fc.mask) o = pfw::load_slot(&fc.slots[f.related]);
+    else o.state = 0;
     bool move;
-    if (pfw::masq_steady(q, R, move)) continue;
-    dpf::FlowSlot &f = fc.slots[R.slot];
-    f.nat_tag = fc.burst;
-    if (q.alive(f.related, f.related_tag)) fc.slots[f.related].nat_tag = fc.burst;
+    if (pfw::masq_steady_v(fc, R, f, o, move)) continue;
+    fc.slots[R.slot].nat_tag = fc.burst;
+    if (f.related <= fc.mask && o.state == f.related_tag) fc.slots[f.related].nat_tag = fc.burst;
   }
+  uint32_t *const words[3] = {&fc.pf_cnt[9], &fc.pf_cnt[8], &fc.pf_cnt[10]};
+  pfw::flags_block(&s_fl, fl, words, 3);
 }
 
 // dp_nat_prep: the records of the burst's NAT pass (their packet order for
@@ -4674,31 +4741,42 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
   const uint32_t nrec = fc.pf_cnt[0];
   if (!nrec) return;
   const Img g{img_base, *im};
-  const pfw::Seq sq{fc, g, true};
   const bool split = pfw::nat_mode(fc) == 3;  // (dp_nat_mark's flags decide it)
   const unsigned long long tag = (unsigned long long)fc.burst << 32;
+  __shared__ uint32_t s_fl;
+  if (t == 0) s_fl = 0;
+  __syncthreads();
+  uint32_t fl = 0;  // 1 a steady refresh, 2 a record the parallel pass cannot place
   for (uint32_t rec = blockIdx.x * 1024 + t; rec < nrec; rec += gridDim.x * 1024) {
     dpf::PfReq &R = fc.pf[rec];
     if (!(R.bits & dpf::kPqReached)) continue;  // a flow-filter record of a packet dropped before NAT
     uint32_t key;
     if (R.bits & dpf::kPqMasq) {
       // a steady refresh whose connection no record moves: resolved here
-      // (split pass; the one-lane pass runs it in its order)
-      bool move;
-      const bool steady = split && pfw::masq_steady(sq, R, move) && fc.slots[R.slot].nat_tag != fc.burst &&
-                          fc.slots[fc.slots[R.slot].related].nat_tag != fc.burst;
-      pfw::flag_wave(&fc.pf_cnt[27], steady);
-      if (steady) {
-        R.bits |= dpf::kPqSteady;
-        pfw::masq_steady_run(fc, R);
-        continue;
+      // (split pass; the one-lane pass runs it in its order).  The record,
+      // its flow and the related flow read once (masq_steady_v)
+      bool steady = false;
+      if (split && R.slot <= fc.mask && fc.mq) {
+        const dpf::PfReq Rc = pfw::load_req(&R);
+        const dpf::FlowSlot f = pfw::load_slot(&fc.slots[Rc.slot]);
+        dpf::FlowSlot o;
+        if (f.related <= fc.mask) o = pfw::load_slot(&fc.slots[f.related]);
+        else o.state = 0;
+        bool move;
+        steady = pfw::masq_steady_v(fc, Rc, f, o, move) && f.nat_tag != fc.burst && o.nat_tag != fc.burst;
+        if (steady) {
+          fl |= 1u;
+          R.bits = Rc.bits | dpf::kPqSteady;
+          pfw::masq_steady_run(fc, R, f);
+        }
       }
+      if (steady) continue;
       if (!pfw::masq_conn(fc, R, key)) {
         pfw::lane_mark(fc, R, 0u);
         continue;
       }
     } else if (!pfw::conn_key(g, fc, R, key)) {
-      pfw::flag_once(&fc.pf_cnt[5]);
+      fl |= 2u;
       continue;
     }
     const unsigned long long want = tag | key;
@@ -4724,6 +4802,8 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
       old = got;
     }
   }
+  uint32_t *const words[2] = {&fc.pf_cnt[27], &fc.pf_cnt[5]};
+  pfw::flags_block(&s_fl, fl, words, 2);
 }
 
 // dp_nat_resolve: the reference's PortForwarder and Masquerade over the
