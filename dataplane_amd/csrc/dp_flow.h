@@ -121,10 +121,6 @@ constexpr uint32_t kPqQuery = 1u << 12;   // its flow key is an ICMP query's (ec
 // already ran (its connection's lane left it there)
 constexpr uint32_t kPqLane = 1u << 13;
 constexpr uint32_t kPqPfDone = 1u << 14;
-// a masquerading refresh that commutes with every other record of the burst
-// (dp_nat_prep: no record of its connection changes the pair's state this
-// burst); dp_nat_prep resolves it in place
-constexpr uint32_t kPqSteady = 1u << 15;
 constexpr uint32_t kPfForward = 0xffu;
 
 // words of FlowCtx::pf_cnt
@@ -187,7 +183,7 @@ struct FlowCtx {
   // [19..22] its time in plans, allocations, pairs and records alone (1024
   // clock64 ticks), [23..25] the allocations' parts (the set's address and
   // block, serving the records, the block's update), [26] allocation steps,
-  // [27] a steady refresh in the burst (kPqSteady), [28] an initial key of
+  // [27] a steady refresh in the burst (dp_nat_prep), [28] an initial key of
   // the lane's allocating records repeats, [29] a lane record runs alone
   unsigned long long *grp_tab, *grp_head, *grp_next;
   uint32_t *grp_list;

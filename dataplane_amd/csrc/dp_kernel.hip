@@ -4455,25 +4455,32 @@ __device__ bool masq_steady_v(const dpf::FlowCtx &fc, const dpf::PfReq &R, const
 
 // resolve_masq's refresh for a steady record (the expiry by atomicMax); f: a
 // copy of its flow
-__device__ void masq_steady_run(const dpf::FlowCtx &fc, dpf::PfReq &R, const dpf::FlowSlot &f) {
-  R.verdict = dpf::kPfForward;
-  R.acl_over = 0;
-  R.mverdict = dpf::kPfForward;
-  const uint32_t fam = (R.proto >> 8) & 0xffu;
-  const bool tcp = R.bits & dpf::kPqTcp, udp = R.bits & dpf::kPqUdp, icmp = R.bits & dpf::kPqIcmp;
+__device__ void masq_steady_run(const dpf::FlowCtx &fc, const dpf::PfReq &Rc, dpf::PfReq &R,
+                                const dpf::FlowSlot &f) {
+  // (Rc: the record as read, R: where its decision goes -- Masquerade's
+  // verdict, action and tuple, 24 contiguous bytes; PortForwarder's verdict
+  // and the ACL override keep the values the first pass recorded: a steady
+  // record has no port forwarding)
+  const uint32_t fam = (Rc.proto >> 8) & 0xffu;
+  const bool tcp = Rc.bits & dpf::kPqTcp, udp = Rc.bits & dpf::kPqUdp, icmp = Rc.bits & dpf::kPqIcmp;
   const uint32_t act = f.pf & 0xffu, port = f.pf >> 16, cur = (f.pf >> 8) & 0xffu;
   if (cur != DP_NFS_ONE_WAY) {
     const uint64_t ext = cur == DP_NFS_TWO_WAY ? kMasqTwoWayNs
                        : cur == DP_NFS_ESTABLISHED ? (uint64_t)f.pf_rule * 1000000000ull : kMasqClosingNs;
-    atomicMax(reinterpret_cast<unsigned long long *>(&fc.slots[R.slot].expires_at),
+    atomicMax(reinterpret_cast<unsigned long long *>(&fc.slots[Rc.slot].expires_at),
               (unsigned long long)(fc.now + ext));
   }
+  static_assert(offsetof(dpf::PfReq, mnat) == offsetof(dpf::PfReq, mverdict) + 4 &&
+                offsetof(dpf::PfReq, mnat_ip) == offsetof(dpf::PfReq, mverdict) + 8 &&
+                offsetof(dpf::PfReq, mverdict) % 8 == 0, "the masquerade decision: 24 contiguous bytes");
+  uint2 *d = reinterpret_cast<uint2 *>(&R.mverdict);
   if ((act == DP_PF_SRC_NAT && !unicast(f.pf_fam, f.pf_ip)) || f.pf_fam != fam || !(tcp || udp || icmp)) {
     R.mverdict = DP_DONE_NAT_FAILURE;
     return;
   }
-  R.mnat = act | ((f.flags & dpf::kFlagMasqIdent) ? 0x100u : 0u) | (port << 16);
-  for (int j = 0; j < 4; j++) R.mnat_ip[j] = f.pf_ip[j];
+  d[0] = make_uint2(dpf::kPfForward, act | ((f.flags & dpf::kFlagMasqIdent) ? 0x100u : 0u) | (port << 16));
+  d[1] = make_uint2(f.pf_ip[0], f.pf_ip[1]);
+  d[2] = make_uint2(f.pf_ip[2], f.pf_ip[3]);
 }
 
 // Can a connection lane run this connection (the records of `list`)?  Every
@@ -4766,8 +4773,7 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
         steady = pfw::masq_steady_v(fc, Rc, f, o, move) && f.nat_tag != fc.burst && o.nat_tag != fc.burst;
         if (steady) {
           fl |= 1u;
-          R.bits = Rc.bits | dpf::kPqSteady;
-          pfw::masq_steady_run(fc, R, f);
+          pfw::masq_steady_run(fc, Rc, R, f);
         }
       }
       if (steady) continue;
