@@ -55,9 +55,11 @@ struct PtNode {
   uint64_t pad;
 };
 
+#define DPD_LPM_D16 0x100u
 struct Lpm {
   uint64_t direct;     // offset of uint32_t[1 << dbits]; bit31 = leaf(nh) else node idx
-  uint32_t dbits;      // direct-pointing bits (16..24)
+  uint32_t dbits;      // direct-pointing bits (16..24); | DPD_LPM_D16: DIR-24-8 with 16-bit
+                       // direct entries (bit 15 leaf, else the block)
   uint32_t width;      // 32 or 128
   uint64_t blocks;     // != 0: DIR-24-8 -- a non-leaf direct entry is the index of a
                        // uint16_t[256] block of next hops for the last 8 bits (v4 with a

@@ -1001,13 +1001,25 @@ __device__ __forceinline__ uint32_t key6(uint64_t hi, uint64_t lo, int off) {
 __device__ __forceinline__ uint32_t lpm_sel(uint32_t off, uint32_t shift, uint32_t bits) {
   return off | (shift << 8) | (bits << 16);
 }
+// the selector of an Lpm's direct table (its dbits, DPD_LPM_D16 in bit 24)
+__device__ __forceinline__ uint32_t lpm_dsel(uint32_t dbits) {
+  const uint32_t b = dbits & 0xffu;
+  return lpm_sel(b, 64 - b, b) | ((dbits & DPD_LPM_D16) << 16);
+}
 __device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t table_off, uint32_t sel, uint64_t blocks,
                                              const Addr16 &a) {
   const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1], klo = ((uint64_t)a.w[2] << 32) | a.w[3];
   int off = (int)(sel & 0xffu);
+  if (sel >> 24) {  // DIR-24-8 with 16-bit direct entries (v4)
+    const uint32_t e = g.at<uint16_t>(table_off)[a.w[0] >> 8];
+    TRIP();
+    if (e & 0x8000u) return e & 0x7fffu;
+    TRIP();
+    return g.at<uint16_t>(blocks)[(e << 8) | (a.w[0] & 0xff)];
+  }
 #if DP_V6W
   const uint32_t e = g.at<uint32_t>(table_off)[(uint32_t)(khi >> ((sel >> 8) & 0xffu)) &
-                                               ((1u << (sel >> 16)) - 1u)];
+                                               ((1u << ((sel >> 16) & 0xffu)) - 1u)];
 #else
   const uint32_t e = g.at<uint32_t>(table_off)[a.w[0] >> (32 - off)];  // the direct table (dbits <= 32)
 #endif
@@ -1038,7 +1050,7 @@ __device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const
   const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1];
   if (DP_V6W && L.wtab && (khi >> (64 - L.wbits)) == L.wpfx)
     return lpm_walk(g, L.wtab, lpm_sel(L.wbits + L.wtb, 64 - L.wbits - L.wtb, L.wtb), 0, a);
-  return lpm_walk(g, L.direct, lpm_sel(L.dbits, 64 - L.dbits, L.dbits), L.blocks, a);
+  return lpm_walk(g, L.direct, lpm_dsel(L.dbits), L.blocks, a);
 }
 
 // Multibit index walk from a context record's descriptor (Mbi): leaf value
@@ -2137,7 +2149,7 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
       sel = lpm_sel(L.wbits + L.wtb, 64 - L.wbits - L.wtb, L.wtb);
     }
   }
-  if (!sel) sel = lpm_sel(b4, 64 - b4, b4);
+  if (!sel) sel = lpm_dsel(b4);
   const uint32_t nhi = lpm_walk(g, d4, sel, k4, dst);
   TRIP();
   const auto &nr = CTX_REC(NhRec, g.im.ctx_nh, g.im.nh_recs, nhi);
@@ -5121,24 +5133,48 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   __shared__ uint32_t s_bm[8];  // the block being served: its usage bitmap
   // the block being served: [0] valid, [1] region, [2] address record,
   // [3] block | its first port, [4..7] the address, [8] ports taken since it
-  // was loaded
+  // was loaded, [9] its live ports when loaded
   __shared__ uint32_t s_c[10];
-  if (t == 0) s_c[0] = 0;
+  // the served block's address, as the lane leaves it (every change written
+  // through to the allocator as well, never read back while cached): [0]
+  // usable blocks, [1] live blocks, [2] not-full blocks, [3] current_alloc_index,
+  // [4] the thread block, [5..8] the address (A128), [9] its block flags and
+  // order not loaded yet, [10] its record + 1 (0: none); its block flags and
+  // block order (bflag, perm)
+  __shared__ uint32_t s_a[11];
+  __shared__ uint32_t s_flag[64], s_perm[64];
+  if (t == 0) { s_c[0] = 0; s_a[10] = 0; s_a[9] = 0; }
   __syncthreads();
-  // the cached block back to the allocator (by the calling lane)
+  // the cached block back to the allocator (by the calling lane); the
+  // address's counters stay cached
   auto write_back = [&]() {
     if (s_c[0]) {
       dpm::Addr &A0 = V.recs()[s_c[2]];
       const uint32_t tb0 = s_c[3] & 0xffu;
       uint32_t full = 0xffffffffu;
       for (int x = 0; x < 8; x++) { A0.bm[tb0][x] = s_bm[x]; full &= s_bm[x]; }
-      A0.blive[tb0] = (uint16_t)(A0.blive[tb0] + s_c[8]);
-      if (full == 0xffffffffu && s_c[8]) A0.nonfull--;
+      A0.blive[tb0] = (uint16_t)(s_c[9] + s_c[8]);
+      if (full == 0xffffffffu && s_c[8]) A0.nonfull = --s_a[2];
       s_c[0] = 0;
     }
   };
+  // the block tb of address a becomes the served one (by the calling lane;
+  // the flags and order follow, loaded by the whole wave: s_a[9])
+  auto cache_block = [&](uint32_t a, const dpm::Addr &A, uint32_t tb, uint32_t reg, const uint32_t w[4],
+                         const dpm::A128 &aa) {
+    for (int k = 0; k < 8; k++) s_bm[k] = A.bm[tb][k];
+    s_c[0] = 1; s_c[1] = reg; s_c[2] = a; s_c[3] = dpm::block_base(A, tb) | tb;
+    for (int k = 0; k < 4; k++) s_c[4 + k] = w[k];
+    s_c[8] = 0;
+    s_c[9] = A.blive[tb];
+    s_a[0] = A.usable; s_a[1] = A.live_blocks; s_a[2] = A.nonfull; s_a[3] = A.cur;
+    s_a[4] = (uint32_t)A.thread_block;
+    for (int k = 0; k < 4; k++) s_a[5 + k] = aa.w[k];
+    s_a[9] = 1;
+    s_a[10] = a + 1;
+  };
   auto flush = [&]() {
-    if (t == 0) write_back();
+    if (t == 0) { write_back(); s_a[10] = 0; }  // (what runs next changes the allocator itself)
     lane_fence();
     __syncthreads();
   };
@@ -5234,6 +5270,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           if (t == p) {
             if (!hit) {
               write_back();
+              s_a[10] = 0;
               const dpm::Region &G = V.regions()[reg_p];
               uint32_t a = dpm::kNone;
               for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
@@ -5246,12 +5283,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
                   uint32_t w[4] = {0, 0, 0, 0};
                   if (G.fam == 4) w[0] = aa.w[3];
                   else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
-                  if (pfw::unicast(G.fam, w)) {
-                    for (int k = 0; k < 8; k++) s_bm[k] = A.bm[tb][k];
-                    s_c[0] = 1; s_c[1] = reg_p; s_c[2] = a; s_c[3] = dpm::block_base(A, tb) | tb;
-                    for (int k = 0; k < 4; k++) s_c[4 + k] = w[k];
-                    s_c[8] = 0;
-                  }
+                  if (pfw::unicast(G.fam, w)) cache_block(a, A, tb, reg_p, w, aa);
                 }
               }
             }
@@ -5259,38 +5291,91 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
             if (s_c[0])
               for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~s_bm[k]);
             if (!fr && !sfail) {
+              // the address's next block, as port_alloc opens it (its thread
+              // block full or gone: the first free block from
+              // current_alloc_index) for a record that keeps its port (so no
+              // block dies on the way).  The served block full on an address
+              // whose flags are cached: the region's first address with free
+              // ports is still that one if it has any (the addresses before
+              // it had none, and only this lane allocates), and the next
+              // block comes from the cached flags and order
+              bool opened = false;
+              const uint32_t a0 = s_c[2];
+              const bool cached = s_c[0] && s_a[10] == a0 + 1 && !s_a[9];
               write_back();
-              const dpm::Region &G = V.regions()[reg_p];
-              uint32_t a = dpm::kNone;
-              for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
-                if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
-              if (a != dpm::kNone) {
-                dpm::Addr &A = V.recs()[a];
-                const int32_t tb = A.thread_block;
-                const bool spent = tb < 0 || !(A.bflag[tb] & 2) || dpm::bm_full(A.bm[tb]);
+              if (cached && (s_a[0] > 0 || s_a[2] > 0)) {
+                const uint8_t *fl = reinterpret_cast<const uint8_t *>(s_flag);
+                const uint8_t *pm = reinterpret_cast<const uint8_t *>(s_perm);
                 uint32_t idx = dpm::kNone;
-                if (spent)
-                  for (uint32_t k = 0; k < 256; k++) {
-                    const uint32_t x = (A.cur + k) & 0xffu;
-                    if (A.bflag[x] & 1) { idx = x; break; }
-                  }
-                const dpm::A128 aa = dpm::addr_of(V, A);
-                uint32_t w[4] = {0, 0, 0, 0};
-                if (G.fam == 4) w[0] = aa.w[3];
-                else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
-                if (idx != dpm::kNone && dpm::block_base(A, idx) != 0 && pfw::unicast(G.fam, w)) {
+                for (uint32_t k = 0; k < 256; k++) {
+                  const uint32_t x = (s_a[3] + k) & 0xffu;
+                  if (fl[x] & 1) { idx = x; break; }
+                }
+                if (idx != dpm::kNone && pm[idx] != 0) {
+                  // block_new, from the cache, written through
+                  dpm::Addr &A = V.recs()[a0];
+                  const dpm::Region &G = V.regions()[reg_p];
+                  dpm::A128 aa;
+                  for (int k = 0; k < 4; k++) aa.w[k] = s_a[5 + k];
+                  const uint32_t base = (uint32_t)pm[idx] << 8;
+                  uint32_t bm[8];
+                  dpm::block_init(V, G, aa, base, !((K0.y >> 17) & 1u), bm);
                   A.thread_block = (int32_t)idx;
                   A.cur = idx;
-                  dpm::block_new(V, a, idx, (K0.y >> 17) & 1u);
-                  for (int k = 0; k < 8; k++) s_bm[k] = A.bm[idx][k];
-                  s_c[0] = 1; s_c[1] = reg_p; s_c[2] = a; s_c[3] = dpm::block_base(A, idx) | idx;
-                  for (int k = 0; k < 4; k++) s_c[4 + k] = w[k];
-                  s_c[8] = 0;
+                  A.bflag[idx] = 2;
+                  A.blive[idx] = 0;
+                  A.usable = --s_a[0];
+                  A.live_blocks = ++s_a[1];
+                  if (!dpm::bm_full(bm)) A.nonfull = ++s_a[2];
+                  for (int k = 0; k < 8; k++) { A.bm[idx][k] = bm[k]; s_bm[k] = bm[k]; }
+                  reinterpret_cast<uint8_t *>(s_flag)[idx] = 2;
+                  s_a[3] = idx;
+                  s_a[4] = idx;
+                  s_c[0] = 1; s_c[3] = base | idx; s_c[8] = 0; s_c[9] = 0;
+                  for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~bm[k]);
+                  opened = true;
+                }
+              }
+              if (!opened) {
+                s_a[10] = 0;
+                const dpm::Region &G = V.regions()[reg_p];
+                uint32_t a = dpm::kNone;
+                for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
+                  if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
+                if (a != dpm::kNone) {
+                  dpm::Addr &A = V.recs()[a];
+                  const int32_t tb = A.thread_block;
+                  const bool spent = tb < 0 || !(A.bflag[tb] & 2) || dpm::bm_full(A.bm[tb]);
+                  uint32_t idx = dpm::kNone;
+                  if (spent)
+                    for (uint32_t k = 0; k < 256; k++) {
+                      const uint32_t x = (A.cur + k) & 0xffu;
+                      if (A.bflag[x] & 1) { idx = x; break; }
+                    }
+                  const dpm::A128 aa = dpm::addr_of(V, A);
+                  uint32_t w[4] = {0, 0, 0, 0};
+                  if (G.fam == 4) w[0] = aa.w[3];
+                  else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
+                  if (idx != dpm::kNone && dpm::block_base(A, idx) != 0 && pfw::unicast(G.fam, w)) {
+                    A.thread_block = (int32_t)idx;
+                    A.cur = idx;
+                    dpm::block_new(V, a, idx, (K0.y >> 17) & 1u);
+                    cache_block(a, A, idx, reg_p, w, aa);
+                  }
                 }
               }
             }
           }
           __syncthreads();
+          // a newly cached address: its block flags and order, by the wave
+          if (s_a[9] && s_c[0]) {
+            const dpm::Addr &A = V.recs()[s_c[2]];
+            s_flag[t] = reinterpret_cast<const uint32_t *>(A.bflag)[t];
+            s_perm[t] = reinterpret_cast<const uint32_t *>(A.perm)[t];
+            __syncthreads();
+            if (t == 0) s_a[9] = 0;
+            __syncthreads();
+          }
           f = s_c[0] && s_c[1] == reg_p && t < 8 ? ~s_bm[t] : 0u;
         }
         // the block's free ports: per word (lanes 0..7) and before it

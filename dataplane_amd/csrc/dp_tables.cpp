@@ -299,9 +299,22 @@ Lpm build_lpm(ImgBuf &ib, PtBuilder &pb, std::vector<PRoute> &routes, int width,
     }
     if (blocks.empty()) blocks.resize(256, 0);
     L.blocks = ib.put(blocks);
-    L.direct = ib.put(direct);
     L.dbits = dbits;
     L.width = (uint32_t)width;
+#ifdef DP_DIR16
+    // 16-bit direct entries where the next hops and the blocks fit 15 bits:
+    // bit 15 = leaf (next hop), else the block -- a 32 MiB table, half the
+    // lines per lookup's working set
+    if (max_nh < 0x8000u && blocks.size() / 256 <= 0x8000u) {
+      std::vector<uint16_t> d16(direct.size());
+      for (size_t k = 0; k < direct.size(); k++)
+        d16[k] = (direct[k] & 0x80000000u) ? (uint16_t)(0x8000u | (direct[k] & 0x7fffu)) : (uint16_t)direct[k];
+      L.direct = ib.put(d16);
+      L.dbits = dbits | DPD_LPM_D16;
+      return L;
+    }
+#endif
+    L.direct = ib.put(direct);
     return L;
   }
   // long routes: one node per direct slot

@@ -46,8 +46,9 @@ def _bench():
     return m
 
 
-def runs(process, w: Workload, n_run: int, reps: int) -> list:
-    """reps timed runs of n_run packets (passes over the burst); Mpps each"""
+def runs(process, w: Workload, n_run: int, reps: int, tag: str = "") -> list:
+    """reps timed runs of n_run packets (passes over the burst); Mpps each
+    (one progress line per run: a long silent run reads as hung)"""
     out = []
     inp = w.inp.copy()
     res = np.zeros(w.n, dtype=A.PKT_OUT)
@@ -61,6 +62,7 @@ def runs(process, w: Workload, n_run: int, reps: int) -> list:
             t += time.perf_counter() - t0
             done += m
         out.append(done / t / 1e6)
+        print(f"[cpu-plan] {tag} run {len(out)}/{reps}: {out[-1]:.4f} Mpps", flush=True)
     return out
 
 
@@ -92,8 +94,8 @@ def main() -> None:
         def port(th):
             return lambda buf, inp, out: o.process_parallel(buf, inp, out, threads=th, burst=64)
         t0 = time.perf_counter()
-        pr = runs(port(threads), w, args.packets, args.runs)
-        p1 = runs(port(1), w, args.one_thread_packets, args.one_thread_runs)
+        pr = runs(port(threads), w, args.packets, args.runs, f"C{cfg} port")
+        p1 = runs(port(1), w, args.one_thread_packets, args.one_thread_runs, f"C{cfg} port 1-thread")
         o.close()
         entry["port"] = {"median_mpps": round(statistics.median(pr), 4), "min": round(min(pr), 4),
                          "max": round(max(pr), 4), "runs": len(pr), "threads": threads,
@@ -112,8 +114,8 @@ def main() -> None:
                 emu.run(ebuf, buf.nbytes, inp, out, threads=th, burst=64)
             return run
         t0 = time.perf_counter()
-        cr = runs(compiled(threads), w, args.packets, args.runs)
-        c1 = runs(compiled(1), w, args.one_thread_packets, args.one_thread_runs)
+        cr = runs(compiled(threads), w, args.packets, args.runs, f"C{cfg} compiled")
+        c1 = runs(compiled(1), w, args.one_thread_packets, args.one_thread_runs, f"C{cfg} compiled 1-thread")
         emu.close()
         entry["compiled"] = {"median_mpps": round(statistics.median(cr), 4), "min": round(min(cr), 4),
                              "max": round(max(cr), 4), "runs": len(cr), "threads": threads,

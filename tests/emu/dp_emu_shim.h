@@ -19,6 +19,7 @@
 #else
 #define __forceinline__ inline
 #endif
+#define __noinline__ __attribute__((noinline))
 #define __launch_bounds__(x)
 #define __shared__
 struct uint4 { uint32_t x, y, z, w; };
