@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 HEADROOM = 96
 
 # DoneReason (net/src/packet/meta.rs:84-119)
@@ -262,11 +262,14 @@ GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_p
                "dp_flow_insert_pair", "dp_flow_lookup", "dp_flow_get", "dp_flow_remove",
                "dp_flow_invalidate", "dp_flow_set_status", "dp_flow_sweep", "dp_flow_count",
                "dp_ctx_attach_flow_table", "dp_mbuf_burst_in", "dp_mbuf_burst_out",
-               "dp_process_mbufs", "dp_acl_classify", "dp_acl_classify_device"]
+               "dp_process_mbufs", "dp_acl_classify", "dp_acl_classify_device",
+               "dp_acl_key_from_match", "dp_acl_classify_match"]
 # dp_acl_key_t / dp_acl_result_t (the ACL classifier alone)
 ACL_KEY = np.dtype([("src_vni", "<u4"), ("dst_vni", "<u4"), ("family", "u1"), ("proto", "u1"),
                     ("sport", "<u2"), ("dport", "<u2"), ("pad", "u1", 2), ("src", "u1", 16),
                     ("dst", "u1", 16)])
+# the reference's AclKey bytes (MatchKey::as_key_into; dp_acl_key_from_match)
+ACL_MATCH_KEY_V4, ACL_MATCH_KEY_V6 = 21, 45
 ACL_RESULT = np.dtype([("rule", "<u4"), ("action", "u1"), ("scope", "u1"), ("acl", "u1"), ("pad", "u1")])
 NP_STRUCTS = dict(dp_flow_key_t=FLOW_KEY, dp_flow_t=FLOW, dp_flow_info_t=FLOW_INFO, dp_acl_key_t=ACL_KEY,
                   dp_acl_result_t=ACL_RESULT)
@@ -341,6 +344,8 @@ def gpu_lib() -> C.CDLL:
                                          C.POINTER(MbufLayout), _VP, C.c_uint32, _VP, _VP, _VP]
         lib.dp_acl_classify.argtypes = [_VP, _VP, _VP, C.c_uint32]
         lib.dp_acl_classify_device.argtypes = [_VP, _VP, _VP, C.c_uint32, _VP]
+        lib.dp_acl_key_from_match.argtypes = [_VP, C.c_uint32, C.c_uint32, C.c_uint32, _VP]
+        lib.dp_acl_classify_match.argtypes = [_VP, _VP, C.c_uint32, C.c_uint32, C.c_uint32, _VP]
         lib.dpf_debug_nat_sequential.argtypes = [C.c_int]
         lib.dpf_debug_nat_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32]
         lib.dpf_debug_nat_counters.restype = C.c_int

@@ -121,6 +121,10 @@ constexpr uint32_t kPqQuery = 1u << 12;   // its flow key is an ICMP query's (ec
 // already ran (its connection's lane left it there)
 constexpr uint32_t kPqLane = 1u << 13;
 constexpr uint32_t kPqPfDone = 1u << 14;
+// dp_nat_mark found the record a steady refresh (pfw::masq_steady_v) as the
+// burst started; dp_nat_prep resolves it in place unless its flow was tagged
+// for the burst (a tag reaches both flows of a pair at once)
+constexpr uint32_t kPqSteadyCand = 1u << 15;
 constexpr uint32_t kPfForward = 0xffu;
 
 // words of FlowCtx::pf_cnt

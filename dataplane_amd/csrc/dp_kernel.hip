@@ -4469,7 +4469,8 @@ __device__ bool masq_steady_v(const dpf::FlowCtx &fc, const dpf::PfReq &R, const
 // copy of its flow
 __device__ void masq_steady_run(const dpf::FlowCtx &fc, const dpf::PfReq &Rc, dpf::PfReq &R,
                                 const dpf::FlowSlot &f) {
-  // (Rc: the record as read, R: where its decision goes -- Masquerade's
+  // (Rc: the record as read -- its bits, slot and proto --, R: where its
+  // decision goes -- Masquerade's
   // verdict, action and tuple, 24 contiguous bytes; PortForwarder's verdict
   // and the ACL override keep the values the first pass recorded: a steady
   // record has no port forwarding)
@@ -4740,7 +4741,10 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
     if (f.related <= fc.mask) o = pfw::load_slot(&fc.slots[f.related]);
     else o.state = 0;
     bool move;
-    if (pfw::masq_steady_v(fc, R, f, o, move)) continue;
+    if (pfw::masq_steady_v(fc, R, f, o, move)) {
+      fc.pf[rec].bits = R.bits | dpf::kPqSteadyCand;
+      continue;
+    }
     fc.slots[R.slot].nat_tag = fc.burst;
     if (f.related <= fc.mask && o.state == f.related_tag) fc.slots[f.related].nat_tag = fc.burst;
   }
@@ -4768,27 +4772,32 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
   uint32_t fl = 0;  // 1 a steady refresh, 2 a record the parallel pass cannot place
   for (uint32_t rec = blockIdx.x * 1024 + t; rec < nrec; rec += gridDim.x * 1024) {
     dpf::PfReq &R = fc.pf[rec];
-    if (!(R.bits & dpf::kPqReached)) continue;  // a flow-filter record of a packet dropped before NAT
+    // (the record's first words: bits, slot, state ... proto, read at once)
+    dpf::PfReq Rc;
+    {
+      const uint2 *q = reinterpret_cast<const uint2 *>(&R);  // (records are 8-byte aligned)
+      uint2 w[4] = {q[0], q[1], q[2], q[3]};
+#ifndef DP_EMU
+      for (int i = 0; i < 4; i++) asm volatile("" : "+v"(w[i].x), "+v"(w[i].y));
+#endif
+      static_assert(offsetof(dpf::PfReq, proto) < 32, "bits, slot and proto in the first 32 bytes");
+      __builtin_memcpy(&Rc, w, sizeof w);
+    }
+    if (!(Rc.bits & dpf::kPqReached)) continue;  // a flow-filter record of a packet dropped before NAT
     uint32_t key;
-    if (R.bits & dpf::kPqMasq) {
-      // a steady refresh whose connection no record moves: resolved here
-      // (split pass; the one-lane pass runs it in its order).  The record,
-      // its flow and the related flow read once (masq_steady_v)
-      bool steady = false;
-      if (split && R.slot <= fc.mask && fc.mq) {
-        const dpf::PfReq Rc = pfw::load_req(&R);
+    if (Rc.bits & dpf::kPqMasq) {
+      // a steady refresh (dp_nat_mark) whose connection no record moves (its
+      // flow untagged: a tag reaches both flows of the pair): resolved here
+      // (split pass; the one-lane pass runs it in its order) from its flow
+      // alone
+      if (split && (Rc.bits & dpf::kPqSteadyCand)) {
         const dpf::FlowSlot f = pfw::load_slot(&fc.slots[Rc.slot]);
-        dpf::FlowSlot o;
-        if (f.related <= fc.mask) o = pfw::load_slot(&fc.slots[f.related]);
-        else o.state = 0;
-        bool move;
-        steady = pfw::masq_steady_v(fc, Rc, f, o, move) && f.nat_tag != fc.burst && o.nat_tag != fc.burst;
-        if (steady) {
+        if (f.nat_tag != fc.burst) {
           fl |= 1u;
           pfw::masq_steady_run(fc, Rc, R, f);
+          continue;
         }
       }
-      if (steady) continue;
       if (!pfw::masq_conn(fc, R, key)) {
         pfw::lane_mark(fc, R, 0u);
         continue;

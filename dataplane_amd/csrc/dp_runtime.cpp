@@ -196,6 +196,10 @@ struct dp_ctx {
   dp_pkt_out_t *d_out = nullptr;
   dp_pkt_meta_t *d_meta = nullptr;
   uint64_t *d_stats = nullptr;
+  // dp_acl_classify's device keys and results (grown as needed)
+  dp_acl_key_t *acl_keys = nullptr;
+  dp_acl_result_t *acl_res = nullptr;
+  uint32_t acl_cap = 0;
   uint32_t cap_n = 0;
   uint32_t *d_pos = nullptr;           // staged copies: span positions (16-byte units)
   // staged copies: pinned host side (records, positions, packed spans in and
@@ -482,6 +486,8 @@ int dp_ctx_destroy(dp_ctx_t *c) {
     if (p) (void)hipHostFree(p);
   for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
   if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->acl_keys) (void)hipFree(c->acl_keys);
+  if (c->acl_res) (void)hipFree(c->acl_res);
   c->fl_ev.release();
   c->fl_sens.release();
   for (FlowScratch *x : {&c->pf_req, &c->pf_cnt, &c->pf_of, &c->pf_bits, &c->pf_order, &c->pf_repl, &c->mq_rel,
@@ -780,25 +786,66 @@ int dp_acl_classify(dp_ctx_t *c, const dp_acl_key_t *keys, dp_acl_result_t *out,
   if (n == 0) return 0;
   if (!keys || !out) return fail(DP_EINVAL, "null keys / results");
   (void)hipSetDevice(c->device);
-  dp_acl_key_t *dk = nullptr;
-  dp_acl_result_t *dr = nullptr;
   hipError_t e;
-  if ((e = hipMallocAsync((void **)&dk, sizeof(dp_acl_key_t) * (size_t)n, c->stream)) != hipSuccess ||
-      (e = hipMallocAsync((void **)&dr, sizeof(dp_acl_result_t) * (size_t)n, c->stream)) != hipSuccess) {
-    if (dk) (void)hipFreeAsync(dk, c->stream);
-    return fail(DP_ENOMEM, "ACL classify buffers", e);
+  if (n > c->acl_cap) {
+    // (the context's stream first: an earlier classify may still read them)
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return fail(DP_EIO, "ACL classify", e);
+    if (c->acl_keys) (void)hipFree(c->acl_keys);
+    if (c->acl_res) (void)hipFree(c->acl_res);
+    c->acl_keys = nullptr;
+    c->acl_res = nullptr;
+    c->acl_cap = 0;
+    const uint32_t cap = n < 4096 ? 4096 : n;
+    if ((e = hipMalloc((void **)&c->acl_keys, sizeof(dp_acl_key_t) * (size_t)cap)) != hipSuccess ||
+        (e = hipMalloc((void **)&c->acl_res, sizeof(dp_acl_result_t) * (size_t)cap)) != hipSuccess)
+      return fail(DP_ENOMEM, "ACL classify buffers", e);
+    c->acl_cap = cap;
   }
-  int rc = 0;
-  if ((e = hipMemcpyAsync(dk, keys, sizeof(dp_acl_key_t) * (size_t)n, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
-    rc = fail(DP_EIO, "ACL keys copy", e);
-  if (!rc) rc = dp_acl_classify_device(c, dk, dr, n, c->stream);
-  if (!rc && (e = hipMemcpyAsync(out, dr, sizeof(dp_acl_result_t) * (size_t)n, hipMemcpyDeviceToHost, c->stream)) !=
+  // keys and results in pageable host memory: blocking copies, the results'
+  // after the context's stream has drained (an asynchronous copy into pageable
+  // memory was seen to leave `out` unwritten after the stream synchronised)
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return fail(DP_EIO, "ACL classify", e);
+  if ((e = hipMemcpy(c->acl_keys, keys, sizeof(dp_acl_key_t) * (size_t)n, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail(DP_EIO, "ACL keys copy", e);
+  int rc = dp_acl_classify_device(c, c->acl_keys, c->acl_res, n, c->stream);
+  if (!rc && (e = hipStreamSynchronize(c->stream)) != hipSuccess) rc = fail(DP_EIO, "ACL classify", e);
+  if (!rc && (e = hipMemcpy(out, c->acl_res, sizeof(dp_acl_result_t) * (size_t)n, hipMemcpyDeviceToHost)) !=
                  hipSuccess)
     rc = fail(DP_EIO, "ACL results copy", e);
-  (void)hipFreeAsync(dk, c->stream);
-  (void)hipFreeAsync(dr, c->stream);
-  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess && !rc) rc = fail(DP_EIO, "ACL classify", e);
   return rc;
+}
+
+int dp_acl_key_from_match(const uint8_t *match, uint32_t key_size, uint32_t stride, uint32_t n,
+                          dp_acl_key_t *out) {
+  if (key_size != DP_ACL_MATCH_KEY_V4 && key_size != DP_ACL_MATCH_KEY_V6)
+    return fail(DP_EINVAL, "ACL match key: 21 (v4) or 45 (v6) bytes");
+  if (stride < key_size) return fail(DP_EINVAL, "ACL match key stride shorter than the key");
+  if (n && (!match || !out)) return fail(DP_EINVAL, "null keys / output");
+  const uint32_t al = key_size == DP_ACL_MATCH_KEY_V4 ? 4 : 16;
+  auto be32 = [](const uint8_t *b) { return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3]; };
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t *b = match + (size_t)i * stride;
+    dp_acl_key_t k{};
+    k.proto = b[0];
+    k.src_vni = be32(b + 1);
+    k.dst_vni = be32(b + 5);
+    k.family = al == 4 ? 4 : 6;
+    std::memcpy(k.src, b + 9, al);
+    std::memcpy(k.dst, b + 9 + al, al);
+    k.sport = (uint16_t)(b[9 + 2 * al] << 8 | b[10 + 2 * al]);
+    k.dport = (uint16_t)(b[11 + 2 * al] << 8 | b[12 + 2 * al]);
+    out[i] = k;
+  }
+  return 0;
+}
+
+int dp_acl_classify_match(dp_ctx_t *c, const uint8_t *match, uint32_t key_size, uint32_t stride, uint32_t n,
+                          dp_acl_result_t *out) {
+  if (!c) return fail(DP_EINVAL, "null ctx");
+  std::vector<dp_acl_key_t> keys(n);
+  const int rc = dp_acl_key_from_match(match, key_size, stride, n, keys.data());
+  if (rc || !n) return rc;
+  return dp_acl_classify(c, keys.data(), out, n);
 }
 
 int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {

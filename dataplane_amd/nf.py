@@ -214,6 +214,20 @@ class GpuPathNf:
                 "dp_acl_classify", self.lib)
         return out
 
+    def acl_classify_match(self, match: np.ndarray, key_size: int, stride: int = 0) -> np.ndarray:
+        """The same over the reference's own key bytes (dp_acl_classify_match):
+        AclKey::as_key() output, key_size 21 (v4) or 45 (v6), keys `stride`
+        bytes apart (default: packed)."""
+        match = np.ascontiguousarray(match, dtype=np.uint8).reshape(-1)
+        stride = stride or key_size
+        n = len(match) // stride if len(match) >= key_size else 0
+        if n and (n - 1) * stride + key_size > len(match):
+            n -= 1
+        out = np.zeros(n, dtype=A.ACL_RESULT)
+        A.check(self.lib.dp_acl_classify_match(self.ctx, match.ctypes.data, key_size, stride, n,
+                                               out.ctypes.data), "dp_acl_classify_match", self.lib)
+        return out
+
     def close(self) -> None:
         if self.ctx:
             self.lib.dp_ctx_destroy(self.ctx)

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define DPGPU_ABI_VERSION 5u
+#define DPGPU_ABI_VERSION 6u
 
 /* Bytes every frame must have in front of it (its own scratch, owned by the
  * packet).  Output headers are written in place into this headroom: VXLAN
@@ -654,6 +654,25 @@ int dp_acl_classify_device(dp_ctx_t *ctx, const dp_acl_key_t *dev_keys, dp_acl_r
                            uint32_t n, void *stream);
 /* The same for keys and results in host memory (synchronous). */
 int dp_acl_classify(dp_ctx_t *ctx, const dp_acl_key_t *keys, dp_acl_result_t *out, uint32_t n);
+
+/* The reference's own key bytes.  AclKey<Ipv4Addr> / AclKey<Ipv6Addr>
+ * (acl-filter/src/context.rs:168-190) as MatchKey::as_key_into writes them
+ * (match-action-derive/src/lib.rs:191-206, 341-347): its fields back to back,
+ * each big-endian (net/src/fixed_size.rs: NextHeader 1 byte, Vni right-aligned
+ * in 4) -- proto, src_vni, dst_vni, src address, dst address, src port, dst
+ * port: DP_ACL_MATCH_KEY_V4 (21) or DP_ACL_MATCH_KEY_V6 (45) bytes a key, the
+ * key size naming the family.  Keys lie `stride` bytes apart (>= key_size;
+ * lookup_batch's arena packs them at its layout's stride, lookup.rs:131-138),
+ * so a binding hands over AclKey::as_key() output as it is.
+ * dp_acl_key_from_match converts n of them to dp_acl_key_t (host code: no
+ * device, no context); dp_acl_classify_match classifies them as
+ * dp_acl_classify does.  DP_EINVAL: another key size, stride < key_size. */
+#define DP_ACL_MATCH_KEY_V4 21u
+#define DP_ACL_MATCH_KEY_V6 45u
+int dp_acl_key_from_match(const uint8_t *match, uint32_t key_size, uint32_t stride, uint32_t n,
+                          dp_acl_key_t *out);
+int dp_acl_classify_match(dp_ctx_t *ctx, const uint8_t *match, uint32_t key_size, uint32_t stride,
+                          uint32_t n, dp_acl_result_t *out);
 
 /* ------------------------------------------------------------------------ */
 /* Flow table: FlowTable                              */

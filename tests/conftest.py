@@ -15,6 +15,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_runtime_first(request):
+    """GPU runs: torch (plumbing for the device-path tests) bundles its own
+    HIP runtime, which must initialise before libdpgpu's runtime claims the
+    device -- whichever test file runs first."""
+    expr = request.config.getoption("markexpr") or ""
+    if "gpu" in expr and "not gpu" not in expr:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield
+
+
 CLS_FORMS = {"auto": 0, "bv": 1, "list": 2}
 
 

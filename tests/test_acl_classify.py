@@ -6,7 +6,12 @@ the oracle's whole path gave the same packets (out.acl, acl_rule), over the
 C2 and C5 workload shapes -- the checker is the stage.
 GPU: dp_acl_classify through the C ABI == the oracle on those keys and on
 perturbed ones (other ports, addresses, peerings: misses, defaults, peerings
-without an ACL), both classifier forms, v4 and v6."""
+without an ACL), both classifier forms, v4 and v6; and over the reference's own
+key bytes (AclKey::as_key, dp_acl_classify_match) with BASELINE's 10k rules.
+The conversion of those bytes (dp_acl_key_from_match, host code) is pinned on
+the CPU against a restatement of MatchKey::as_key_into's layout."""
+import struct
+
 import numpy as np
 import pytest
 
@@ -100,3 +105,83 @@ def test_gpu_acl_classify(cfg, form, cls_form):
         assert len(bad) == 0, f"{f}: {len(bad)} keys differ, first {keys[bad[0]]}: {got[bad[0]]} vs {want[bad[0]]}"
     h = {int(c): int((want["acl"] == c).sum()) for c in np.unique(want["acl"])}
     assert h.get(1, 0) and h.get(2, 0) and h.get(0, 0), h
+
+
+def as_key(k) -> bytes:
+    """AclKey::as_key (acl-filter/src/context.rs:168-190 through
+    match-action-derive/src/lib.rs:191-206, 341-347): proto (NextHeader, 1 B),
+    src_vni and dst_vni (Vni: 4 B, net/src/fixed_size.rs:61-74), the two
+    addresses, the two ports -- every field big-endian, back to back."""
+    al = 4 if int(k["family"]) == 4 else 16
+    return (struct.pack(">BII", int(k["proto"]), int(k["src_vni"]), int(k["dst_vni"])) +
+            bytes(k["src"][:al]) + bytes(k["dst"][:al]) + struct.pack(">HH", int(k["sport"]), int(k["dport"])))
+
+
+def match_keys(keys: np.ndarray, fam: int, stride: int = 0) -> tuple:
+    sel = keys[keys["family"] == fam]
+    size = A.ACL_MATCH_KEY_V4 if fam == 4 else A.ACL_MATCH_KEY_V6
+    stride = stride or size
+    buf = np.zeros(len(sel) * stride, np.uint8)
+    for i, k in enumerate(sel):
+        buf[i * stride:i * stride + size] = np.frombuffer(as_key(k), np.uint8)
+    return sel, buf, size, stride
+
+
+@pytest.mark.parametrize("stride", [0, 64])
+def test_acl_key_from_match(stride):
+    import ctypes as C
+    lib = A.gpu_lib()  # (host code of the library: no device is touched)
+    r = np.random.default_rng(7 + stride)
+    n = 500
+    keys = np.zeros(n, A.ACL_KEY)
+    keys["family"] = np.where(r.random(n) < 0.5, 4, 6)
+    keys["proto"] = r.choice([1, 6, 17, 58], n)
+    keys["src_vni"] = r.integers(1, 1 << 24, n)
+    keys["dst_vni"] = r.integers(1, 1 << 24, n)
+    keys["sport"] = r.integers(0, 65536, n)
+    keys["dport"] = r.integers(0, 65536, n)
+    keys["src"] = r.integers(0, 256, (n, 16))
+    keys["dst"] = r.integers(0, 256, (n, 16))
+    keys["src"][keys["family"] == 4, 4:] = 0
+    keys["dst"][keys["family"] == 4, 4:] = 0
+    for fam in (4, 6):
+        sel, buf, size, st = match_keys(keys, fam, stride)
+        assert len(buf) == len(sel) * st and size == (21 if fam == 4 else 45)
+        got = np.zeros(len(sel), A.ACL_KEY)
+        assert lib.dp_acl_key_from_match(buf.ctypes.data, size, st, len(sel), got.ctypes.data) == 0
+        assert got.tobytes() == sel.tobytes()
+    out = np.zeros(1, A.ACL_KEY)
+    buf = np.zeros(64, np.uint8)
+    assert lib.dp_acl_key_from_match(buf.ctypes.data, 20, 20, 1, out.ctypes.data) == -22  # DP_EINVAL
+    assert lib.dp_acl_key_from_match(buf.ctypes.data, 21, 20, 1, out.ctypes.data) == -22  # DP_EINVAL
+    assert lib.dp_acl_key_from_match(C.c_void_p(0), 45, 45, 0, C.c_void_p(0)) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_gpu_acl_classify_match_10k(cfg):
+    """BASELINE's ACL size (10k rules) through the reference's key bytes:
+    dp_acl_classify_match == dp_acl_classify == the oracle, per family."""
+    from dataplane_amd import GpuPathNf
+    w = Workload(cfg, 20000, seed=90 + cfg, n_routes_v4=4000, n_routes_v6=2000, n_acl=10000, n_nat=16)
+    o = Oracle(w.tables)
+    res = o.process(w.fresh_buf(), w.inp)
+    _, keys = keys_of(w, res, res)
+    keys = np.concatenate([keys, perturb(keys, 10 + cfg)])
+    keys = keys[np.isin(keys["family"], [4, 6])]
+    want = o.acl_classify(keys)
+    nf = GpuPathNf(0)
+    try:
+        nf.publish(w.tables)
+        direct = nf.acl_classify(keys)
+        for fam in ((4, 6) if cfg == 5 else (4,)):
+            sel, buf, size, st = match_keys(keys, fam, 48)
+            got = nf.acl_classify_match(buf, size, st)
+            m = keys["family"] == fam
+            for f in ("rule", "action", "scope", "acl"):
+                assert np.array_equal(got[f], want[f][m]), (fam, f)
+                assert np.array_equal(direct[f][m], want[f][m]), (fam, f)
+    finally:
+        nf.close()
+    h = {int(c): int((want["acl"] == c).sum()) for c in np.unique(want["acl"])}
+    assert h.get(1, 0) and h.get(2, 0), h
