@@ -121,10 +121,6 @@ constexpr uint32_t kPqQuery = 1u << 12;   // its flow key is an ICMP query's (ec
 // already ran (its connection's lane left it there)
 constexpr uint32_t kPqLane = 1u << 13;
 constexpr uint32_t kPqPfDone = 1u << 14;
-// dp_nat_mark found the record a steady refresh (pfw::masq_steady_v) as the
-// burst started; dp_nat_prep resolves it in place unless its flow was tagged
-// for the burst (a tag reaches both flows of a pair at once)
-constexpr uint32_t kPqSteadyCand = 1u << 15;
 constexpr uint32_t kPfForward = 0xffu;
 
 // words of FlowCtx::pf_cnt
@@ -204,6 +200,10 @@ struct FlowCtx {
   uint4 *lane_plan;     // per lane record: its class and plan (dp_nat_lane_plan, 128 B)
   uint4 *lane_res;      // per lane record: its allocation for dp_nat_pairs (32 B)
   uint4 *lane_key;      // per lane record: what the lane's allocation step reads of its plan (48 B)
+  // per record, a bit: dp_nat_mark found it a steady refresh (pfw::masq_steady_v)
+  // as the burst started -- dp_nat_prep resolves it in place unless its flow
+  // was tagged for the burst (a tag reaches both flows of a pair at once)
+  unsigned long long *steady;
   unsigned long long *dup_tab;  // (burst << 32 | initial key hash) of the lane's allocating records
   // port forwarding near the capacity (mode 4): per record the new slots its
   // creation adds, then the sum of those of the records before it in packet

@@ -4478,10 +4478,11 @@ __device__ void masq_steady_run(const dpf::FlowCtx &fc, const dpf::PfReq &Rc, dp
   const bool tcp = Rc.bits & dpf::kPqTcp, udp = Rc.bits & dpf::kPqUdp, icmp = Rc.bits & dpf::kPqIcmp;
   const uint32_t act = f.pf & 0xffu, port = f.pf >> 16, cur = (f.pf >> 8) & 0xffu;
   if (cur != DP_NFS_ONE_WAY) {
+    // (every steady record of this flow sees the same status and rule, so
+    // writes the same value: a plain store, no atomic)
     const uint64_t ext = cur == DP_NFS_TWO_WAY ? kMasqTwoWayNs
                        : cur == DP_NFS_ESTABLISHED ? (uint64_t)f.pf_rule * 1000000000ull : kMasqClosingNs;
-    atomicMax(reinterpret_cast<unsigned long long *>(&fc.slots[Rc.slot].expires_at),
-              (unsigned long long)(fc.now + ext));
+    if (fc.now + ext > f.expires_at) fc.slots[Rc.slot].expires_at = fc.now + ext;
   }
   static_assert(offsetof(dpf::PfReq, mnat) == offsetof(dpf::PfReq, mverdict) + 4 &&
                 offsetof(dpf::PfReq, mnat_ip) == offsetof(dpf::PfReq, mverdict) + 8 &&
@@ -4727,26 +4728,36 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
   __syncthreads();
   uint32_t fl = 0;  // the kinds seen: 1 port forwarding, 2 masquerade, 4 masq_back
   for (uint32_t rec = blockIdx.x * 256 + threadIdx.x; rec < nrec; rec += gridDim.x * 256) {
-    const dpf::PfReq R = pfw::load_req(&fc.pf[rec]);  // (the record, its flow and the related flow read once)
-    // the burst's kinds of record (the NAT pass's mode rests on them)
-    if (!(R.bits & dpf::kPqReached)) continue;
-    if (R.bits & dpf::kPqPf) fl |= 1u;
-    if (!(R.bits & dpf::kPqMasq)) continue;
-    fl |= 2u;
-    if (!(fl & 4u) && pfw::masq_back(fc, R)) fl |= 4u;
-    if (!fc.mq || R.slot > fc.mask) continue;
-    const dpf::FlowSlot f = pfw::load_slot(&fc.slots[R.slot]);
-    if (f.state != R.state) continue;
-    dpf::FlowSlot o;
-    if (f.related <= fc.mask) o = pfw::load_slot(&fc.slots[f.related]);
-    else o.state = 0;
-    bool move;
-    if (pfw::masq_steady_v(fc, R, f, o, move)) {
-      fc.pf[rec].bits = R.bits | dpf::kPqSteadyCand;
-      continue;
-    }
-    fc.slots[R.slot].nat_tag = fc.burst;
-    if (f.related <= fc.mask && o.state == f.related_tag) fc.slots[f.related].nat_tag = fc.burst;
+    // the record's kinds; a steady refresh (its bit in fc.steady, a word per
+    // wave: the wave's 64 records are consecutive), else its pair's tag
+    auto visit = [&]() -> bool {
+      const dpf::PfReq R = pfw::load_req(&fc.pf[rec]);  // (the record, its flow and the related flow read once)
+      // the burst's kinds of record (the NAT pass's mode rests on them)
+      if (!(R.bits & dpf::kPqReached)) return false;
+      if (R.bits & dpf::kPqPf) fl |= 1u;
+      if (!(R.bits & dpf::kPqMasq)) return false;
+      fl |= 2u;
+      if (!(fl & 4u) && pfw::masq_back(fc, R)) fl |= 4u;
+      if (!fc.mq || R.slot > fc.mask) return false;
+      const dpf::FlowSlot f = pfw::load_slot(&fc.slots[R.slot]);
+      if (f.state != R.state) return false;
+      dpf::FlowSlot o;
+      if (f.related <= fc.mask) o = pfw::load_slot(&fc.slots[f.related]);
+      else o.state = 0;
+      bool move;
+      if (pfw::masq_steady_v(fc, R, f, o, move)) return true;
+      fc.slots[R.slot].nat_tag = fc.burst;
+      if (f.related <= fc.mask && o.state == f.related_tag) fc.slots[f.related].nat_tag = fc.burst;
+      return false;
+    };
+    const bool st = visit();
+#ifdef DP_EMU
+    if (st) fc.steady[rec >> 6] |= 1ull << (rec & 63);
+    else fc.steady[rec >> 6] &= ~(1ull << (rec & 63));
+#else
+    const uint64_t m = __ballot(st);
+    if ((threadIdx.x & 63) == 0) fc.steady[rec >> 6] = m;
+#endif
   }
   uint32_t *const words[3] = {&fc.pf_cnt[9], &fc.pf_cnt[8], &fc.pf_cnt[10]};
   pfw::flags_block(&s_fl, fl, words, 3);
@@ -4770,7 +4781,11 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
   if (t == 0) s_fl = 0;
   __syncthreads();
   uint32_t fl = 0;  // 1 a steady refresh, 2 a record the parallel pass cannot place
-  for (uint32_t rec = blockIdx.x * 1024 + t; rec < nrec; rec += gridDim.x * 1024) {
+  // the connections new this burst: their list entries claimed once per
+  // workgroup and pass (a claim per wave queued ~10k same-word atomics)
+  __shared__ uint32_t s_cnt[16], s_base;
+  // file one record; fresh: its connection is new (h: its hash slot)
+  auto visit = [&](uint32_t rec, uint32_t &h, bool &fresh) {
     dpf::PfReq &R = fc.pf[rec];
     // (the record's first words: bits, slot, state ... proto, read at once)
     dpf::PfReq Rc;
@@ -4783,32 +4798,31 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
       static_assert(offsetof(dpf::PfReq, proto) < 32, "bits, slot and proto in the first 32 bytes");
       __builtin_memcpy(&Rc, w, sizeof w);
     }
-    if (!(Rc.bits & dpf::kPqReached)) continue;  // a flow-filter record of a packet dropped before NAT
+    if (!(Rc.bits & dpf::kPqReached)) return;  // a flow-filter record of a packet dropped before NAT
     uint32_t key;
     if (Rc.bits & dpf::kPqMasq) {
       // a steady refresh (dp_nat_mark) whose connection no record moves (its
       // flow untagged: a tag reaches both flows of the pair): resolved here
       // (split pass; the one-lane pass runs it in its order) from its flow
       // alone
-      if (split && (Rc.bits & dpf::kPqSteadyCand)) {
+      if (split && ((fc.steady[rec >> 6] >> (rec & 63)) & 1u)) {
         const dpf::FlowSlot f = pfw::load_slot(&fc.slots[Rc.slot]);
         if (f.nat_tag != fc.burst) {
           fl |= 1u;
           pfw::masq_steady_run(fc, Rc, R, f);
-          continue;
+          return;
         }
       }
       if (!pfw::masq_conn(fc, R, key)) {
         pfw::lane_mark(fc, R, 0u);
-        continue;
+        return;
       }
     } else if (!pfw::conn_key(g, fc, R, key)) {
       fl |= 2u;
-      continue;
+      return;
     }
     const unsigned long long want = tag | key;
-    uint32_t h = dpm::kmix(key, 0x2545f491u, 0u) & fc.grp_mask;
-    bool fresh = false;
+    h = dpm::kmix(key, 0x2545f491u, 0u) & fc.grp_mask;
     for (uint32_t p = 0; p <= fc.grp_mask;) {
       const unsigned long long cur = __hip_atomic_load(&fc.grp_tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (cur == want) break;
@@ -4818,8 +4832,6 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
         break;
       }
     }
-    const uint32_t at = wave_claim(&fc.pf_cnt[4], fresh);
-    if (fresh) fc.grp_list[at] = h;
     unsigned long long old = __hip_atomic_load(&fc.grp_head[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
       const uint32_t prev = (old >> 32) == fc.burst ? (uint32_t)old : dpf::kNoSlot;
@@ -4828,6 +4840,28 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
       if (got == old) break;
       old = got;
     }
+  };
+  for (uint32_t b0 = blockIdx.x * 1024; b0 < nrec; b0 += gridDim.x * 1024) {  // (uniform per workgroup)
+    const uint32_t rec = b0 + t;
+    uint32_t h = 0;
+    bool fresh = false;
+    if (rec < nrec) visit(rec, h, fresh);
+#ifdef DP_EMU
+    if (fresh) fc.grp_list[atomicAdd(&fc.pf_cnt[4], 1u)] = h;
+#else
+    const uint64_t m = __ballot(fresh);
+    const uint32_t wv = t >> 6;
+    if ((t & 63) == 0) s_cnt[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (t == 0) {
+      uint32_t sum = 0;
+      for (int k = 0; k < 16; k++) { const uint32_t c = s_cnt[k]; s_cnt[k] = sum; sum += c; }
+      s_base = sum ? atomicAdd(&fc.pf_cnt[4], sum) : 0u;
+    }
+    __syncthreads();
+    if (fresh) fc.grp_list[s_base + s_cnt[wv] + (uint32_t)__popcll(m & lanes_below((int)(t & 63)))] = h;
+    __syncthreads();
+#endif
   }
   uint32_t *const words[2] = {&fc.pf_cnt[27], &fc.pf_cnt[5]};
   pfw::flags_block(&s_fl, fl, words, 2);

@@ -227,7 +227,7 @@ struct dp_ctx {
   FlowScratch fl_ev, fl_sens;
   // port forwarding scratch (dpf::FlowCtx pf*): records, counters, packet ->
   // record, bitmaps (kept zero between bursts), order, replaced fills
-  FlowScratch pf_req, pf_cnt, pf_of, pf_bits, pf_order, pf_repl, mq_rel, lane_order, lane_plan, lane_res, lane_key, adm, adm_blk;
+  FlowScratch pf_req, pf_cnt, pf_of, pf_bits, pf_order, pf_repl, mq_rel, lane_order, lane_plan, lane_res, lane_key, steady, adm, adm_blk;
   // the NAT pass's connection tables and the keyed index of replaced fills:
   // entries carry the burst's tag, so they are zeroed only when allocated
   FlowScratch grp_tab, grp_head, grp_next, grp_list, repl, dup_tab;
@@ -491,7 +491,7 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   c->fl_ev.release();
   c->fl_sens.release();
   for (FlowScratch *x : {&c->pf_req, &c->pf_cnt, &c->pf_of, &c->pf_bits, &c->pf_order, &c->pf_repl, &c->mq_rel,
-                         &c->lane_order, &c->lane_plan, &c->lane_res, &c->lane_key, &c->adm, &c->adm_blk, &c->dup_tab,
+                         &c->lane_order, &c->lane_plan, &c->lane_res, &c->lane_key, &c->steady, &c->adm, &c->adm_blk, &c->dup_tab,
                          &c->grp_tab, &c->grp_head, &c->grp_next, &c->grp_list, &c->repl})
     x->release();
   if (c->ft) {
@@ -715,10 +715,11 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.lane_plan = static_cast<uint4 *>(c->lane_plan.get(128 * ((uint64_t)n + 1)));
     fc.lane_res = static_cast<uint4 *>(c->lane_res.get(32 * ((uint64_t)n + 1)));
     fc.lane_key = static_cast<uint4 *>(c->lane_key.get(48 * ((uint64_t)n + 1)));
+    fc.steady = static_cast<unsigned long long *>(c->steady.get(8 * ((uint64_t)n / 64 + 2)));
     fc.adm = static_cast<uint32_t *>(c->adm.get(sizeof(uint32_t) * ((uint64_t)n + 1)));
     fc.adm_blk = static_cast<uint32_t *>(c->adm_blk.get(sizeof(uint32_t) * 1024));
     if (!fc.events || !fc.sens || !fc.pf || !fc.pf_cnt || !fc.pf_of || !fc.pf_order || !fc.pf_repl || !fc.mq_rel ||
-        !fc.lane_order || !fc.lane_plan || !fc.lane_res || !fc.lane_key || !fc.dup_tab || !fc.adm || !fc.adm_blk ||
+        !fc.lane_order || !fc.lane_plan || !fc.lane_res || !fc.lane_key || !fc.steady || !fc.dup_tab || !fc.adm || !fc.adm_blk ||
         !fc.grp_tab || !fc.grp_head || !fc.grp_next || !fc.grp_list || !fc.repl ||
         c->pf_bits_n < words + sum_words) {
       (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
