@@ -138,6 +138,11 @@ __device__ unsigned long long g_stage_cycles[16];
 #ifndef DP_WAVES
 #define DP_WAVES 3
 #endif
+// DP_PERSIST: the non-flow pipeline kernel's workgroups stay resident and take
+// chunk after chunk (pipeline_grid); A/B flag
+#ifndef DP_PERSIST
+#define DP_PERSIST 0
+#endif
 constexpr int WIN = DP_WIN;       // header window bytes per packet (rest read from HBM)
 constexpr int SLAB = WIN + 4;     // odd dword stride: conflict-free byte reads
 constexpr int HS = DP_HS;         // hash input scratch (packet_hash_vxlan's stream <= 75 B)
@@ -3385,13 +3390,20 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   // the replay pass (port forwarding, FL only): thread t finishes packet
   // pf_order[t] of the records dp_nat_prep ordered
   constexpr bool rep = FL && RP;
-  uint32_t i = blockIdx.x * TPB + tid;
+  // chunk after chunk of TPB packets (DP_PERSIST), else the workgroup's one
+#if DP_PERSIST
+  for (uint32_t chunk = blockIdx.x; chunk * TPB < n; chunk += gridDim.x) {
+#else
+  {
+  const uint32_t chunk = blockIdx.x;
+#endif
+  uint32_t i = chunk * TPB + tid;
   bool live = i < n;
   const dpf::PfReq *rp = nullptr;
   if constexpr (FL) {
     // the replay grid is the burst's; workgroups past the replayed packets
     // leave at once (uniform per workgroup: before any barrier)
-    if (rep && blockIdx.x * TPB >= fc.pf_cnt[1]) return;
+    if (rep && chunk * TPB >= fc.pf_cnt[1]) return;
     if (rep) {
       live = i < fc.pf_cnt[1];
       i = live ? fc.pf_order[i] : n;
@@ -3435,7 +3447,7 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   // into one of DPD_STAT_SLOTS partial histograms (dp_stats_reduce sums them)
   if (part) {
     unsigned long long pending = __ballot(live && done_code < DP_DONE_COUNT);
-    const int slot = (int)((blockIdx.x * (TPB / 64) + (tid >> 6)) & (DPD_STAT_SLOTS - 1));
+    const int slot = (int)((chunk * (TPB / 64) + (tid >> 6)) & (DPD_STAT_SLOTS - 1));
     while (pending) {
       const int leader = __ffsll(pending) - 1;
       const int r = __shfl((int)done_code, leader);
@@ -3443,6 +3455,8 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
       if (lane == leader) atomicAdd(&part[r * DPD_STAT_SLOTS + slot], (unsigned long long)__popcll(m));
       pending &= ~m;
     }
+  }
+  if (DP_PERSIST) __syncthreads();  // (the next chunk's windows reuse the slabs)
   }
 }
 
@@ -5801,10 +5815,24 @@ extern "C" void dpemu_trips_out(uint16_t *p) { dp_trip_out = p; }
 // (the kernel's last template argument names the unit's build: DP_V6W, + 2
 // without stateful NAT, + 4 with the context tables in LDS; each unit sizes
 // its own grid by its TPB, the `blocks` argument is unused)
+// The grid of a pipeline launch: one workgroup per TPB packets, or (DP_PERSIST,
+// the non-flow kernel) as many as the chip keeps resident -- each then takes
+// chunk after chunk, its context-table copy loaded once
+static inline uint32_t pipeline_grid(uint32_t chunks, bool fl) {
+  if (!DP_PERSIST || fl) return chunks;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    cus = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }
+  const uint32_t k = (uint32_t)cus * (768u / TPB);  // 3 waves / SIMD: 12 waves per CU
+  return chunks < k ? chunks : k;
+}
 #define DP_RUNNER(NAME, FL, MT, RP)                                                                   \
   extern "C" void NAME(DP_RUN_ARGS) {                                                                 \
     hipLaunchKernelGGL((dp_pipeline_kernel<FL, MT, RP, DP_V6W + (DP_SNAT ? 0 : 2) + (DP_CTX ? 4 : 0)>),      \
-                       dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, img_base, im,                     \
+                       dim3(pipeline_grid((n + TPB - 1) / TPB, FL)), dim3(TPB), 0, s, img_base, im,  \
                        buf, buf_bytes, in, out, meta, n, part, fc);                                   \
   }
 extern "C" {
