@@ -4441,6 +4441,27 @@ __device__ __forceinline__ dpf::FlowSlot load_slot(const dpf::FlowSlot *p) {
   return f;
 }
 
+// The words of a flow a steady refresh reads (flags; expiry, pf, pf_rule;
+// pf_ip; pf_fam .. nat_tag): four of the slot's eight 16-byte words, the rest
+// zero
+__device__ __forceinline__ dpf::FlowSlot load_slot_steady(const dpf::FlowSlot *p) {
+  static_assert(offsetof(dpf::FlowSlot, flags) / 16 == 3 && offsetof(dpf::FlowSlot, expires_at) / 16 == 5 &&
+                offsetof(dpf::FlowSlot, pf_rule) / 16 == 5 && offsetof(dpf::FlowSlot, pf_ip) / 16 == 6 &&
+                offsetof(dpf::FlowSlot, pf_fam) / 16 == 7 && offsetof(dpf::FlowSlot, nat_tag) / 16 == 7,
+                "the words a steady refresh reads");
+  uint4 w[8];
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+  w[0] = w[1] = w[2] = w[4] = make_uint4(0u, 0u, 0u, 0u);
+  w[3] = q[3]; w[5] = q[5]; w[6] = q[6]; w[7] = q[7];
+#ifndef DP_EMU
+  for (int i = 3; i < 8; i++)
+    if (i != 4) asm volatile("" : "+v"(w[i].x), "+v"(w[i].y), "+v"(w[i].z), "+v"(w[i].w));
+#endif
+  dpf::FlowSlot f;
+  __builtin_memcpy(&f, w, sizeof w);
+  return f;
+}
+
 // A masquerading record whose refresh leaves its pair's state as it is:
 // valid with masquerade state (get_masquerade_state), no ACL flow verdict, a
 // NatFlowStatus that the packet does not move (refresh_masquerade_state, nf.rs:
@@ -4820,7 +4841,7 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
       // (split pass; the one-lane pass runs it in its order) from its flow
       // alone
       if (split && ((fc.steady[rec >> 6] >> (rec & 63)) & 1u)) {
-        const dpf::FlowSlot f = pfw::load_slot(&fc.slots[Rc.slot]);
+        const dpf::FlowSlot f = pfw::load_slot_steady(&fc.slots[Rc.slot]);
         if (f.nat_tag != fc.burst) {
           fl |= 1u;
           pfw::masq_steady_run(fc, Rc, R, f);
