@@ -415,6 +415,52 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
     return res
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list, port: int = 0) -> int:
+    """`bench.py --gpus N` started without a launcher: start N rank processes of
+    this same command line (one per GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N,
+    rendezvous on 127.0.0.1), wait for all of them and return the worst exit
+    status.  Runs before anything touches the GPU, and starts children rather
+    than replacing this process.  The per-worker split it stands for is the
+    reference's fan-out of one rx stream over N workers
+    (dataplane/src/drivers/kernel/fanout.rs:49-73); here each rank is a GPU
+    processing its own shard."""
+    import subprocess
+    port = port or _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    worst = 0
+    for p in procs:
+        rc = p.wait()
+        if rc != 0 and worst == 0:
+            worst = rc if rc > 0 else 1
+    return worst
+
+
+def check_world(gpus: int, env=os.environ) -> int:
+    """The world size this run will use; exits non-zero when --gpus and the
+    launcher's WORLD_SIZE disagree (a run that would time another N)."""
+    if "WORLD_SIZE" not in env:
+        return 1
+    world = int(env["WORLD_SIZE"])
+    if world != gpus:
+        print(f"bench.py: --gpus {gpus} but WORLD_SIZE={world} (launcher started {world} ranks)",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    return world
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -442,11 +488,23 @@ def main() -> None:
                          "frames) or packed (96 B headroom, 16-byte aligned)")
     ap.add_argument("--nat-kind", choices=["both", "pf", "masq"], default="both",
                     help="with --nat-only: which NAT legs")
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="test hook: each rank prints its rank / world as JSON and exits before "
+                         "any GPU call")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks ourselves (before any GPU call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = check_world(args.gpus)
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_probe:
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world,
+                          "master": os.environ.get("MASTER_ADDR")}), flush=True)
+        return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
