@@ -12,8 +12,8 @@ data-path collective).
 Beside `value` (never inside it), rank 0 at N=1 reports legs: the same burst
 with meta records, with a flow table attached (flow_table), port forwarding
 and masquerade under load (nat_portfw, nat_masquerade: a share of a 2M burst
-opening new stateful-NAT connections), host-origin bursts (host_inclusive),
-and the CPU baseline.
+opening new stateful-NAT connections; nat_mixed: both on one public range),
+host-origin bursts (host_inclusive), and the CPU baseline.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
 """
@@ -268,8 +268,8 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
 
     def counters():
         import ctypes as C
-        c = (C.c_uint32 * 32)()
-        lib.dpf_debug_nat_counters(nf2.ctx, c, 32)
+        c = (C.c_uint32 * 40)()
+        lib.dpf_debug_nat_counters(nf2.ctx, c, 40)
         return {"mode": int(c[12]), "records": int(c[1]), "lane_records": int(c[11]),
                 "connections": int(c[4]), "left_by_connections": int(c[13]), "allocations_batched": int(c[14]),
                 "allocations_alone": int(c[15]), "lane_kticks": [int(c[19 + k]) for k in range(7)],
@@ -386,7 +386,63 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
                 "mpps_median": round(n / (med / 1e3) / 1e6, 3), "flows_after": int(ft.count()[0]),
                 "launches": len(keep), "nat_pass": cnts[-1], "done_histogram": done}
 
-    if kind == "masq":
+    def run_mixed(reps, conns=250_000, new_share=0.02, one_lane=False):
+        """Port forwarding and masquerade on one public range (natwork.
+        mixed_world: the reference's overlapping-expose configuration):
+        `conns` port-forwarded and `conns` masqueraded connections opened by
+        an untimed burst, then 2M-packet bursts, 1 % new port-forwarded and
+        1 % new masqueraded connections, the rest on the known ones (both
+        sides, the answers included).  The first two timed bursts move the
+        new pairs two-way and established; the median is over the rest."""
+        clock[0] += hour
+        nf2.set_option(A.OPT_CLOCK, clock[0])
+        ft.sweep(clock[0])
+        nf2.publish(W.mixed_world().build())
+        c = W.MixedConns(conns, conns)
+        buf, inp = c.first()
+        b = torch.from_numpy(buf).to(dev)
+        dinp = torch.from_numpy(inp.view(np.uint8)).to(dev)
+        dout = torch.empty(len(inp) * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+        nf2.process_device(b.data_ptr(), b.numel(), dinp.data_ptr(), dout.data_ptr(), len(inp), None, sptr)
+        torch.cuda.synchronize(dev)
+        first = counters()
+        out0 = np.frombuffer(dout.cpu().numpy().tobytes(), dtype=A.PKT_OUT)
+        learnt = c.learn(b.cpu().numpy(), out0)
+        ms, cnts, done = [], [], {}
+        lib.dpf_debug_nat_sequential(4 if one_lane else 0)
+        try:
+            for k in range(reps):
+                buf, inp, npf, nm = c.burst(n, new_share, step=k + 1)
+                b = torch.from_numpy(buf).to(dev)
+                dinp = torch.from_numpy(inp.view(np.uint8)).to(dev)
+                dout = torch.empty(n * A.PKT_OUT.itemsize, dtype=torch.uint8, device=dev)
+                clock[0] += 10 ** 6
+                nf2.set_option(A.OPT_CLOCK, clock[0])
+                torch.cuda.synchronize(dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                nf2.process_device(b.data_ptr(), b.numel(), dinp.data_ptr(), dout.data_ptr(), n, None, sptr)
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                ms.append(e0.elapsed_time(e1))
+                cnts.append(counters())
+                out = np.frombuffer(dout.cpu().numpy().tobytes(), dtype=A.PKT_OUT)
+                done = {A.DONE_NAMES[d]: int(x) for d, x in zip(*np.unique(out["done"], return_counts=True))}
+        finally:
+            lib.dpf_debug_nat_sequential(0)
+        keep = ms[2:] if len(ms) > 2 else ms
+        med = sorted(keep)[len(keep) // 2]
+        return {"connections": {"port_forwarded": conns, "masqueraded": conns, "learnt": learnt},
+                "first_burst_nat_pass": first, "new_share": new_share, "one_lane": one_lane,
+                "launch_ms_median": round(med, 4), "launch_ms": [round(x, 4) for x in ms],
+                "mpps_median": round(n / (med / 1e3) / 1e6, 3), "flows_after": int(ft.count()[0]),
+                "launches": len(keep), "nat_pass": cnts[-1], "done_histogram": done}
+
+    if kind == "mixed":
+        res["mixed"] = run_mixed(min(steps, 4) + 2)
+        log(0, f"[bench] mixed leg (port forwarding + masquerade, 1 % + 1 % new): "
+               f"{res['mixed']['launch_ms_median']} ms, mode {res['mixed']['nat_pass']['mode']}")
+    elif kind == "masq":
         # first packets of new connections only (the allocating lane), then
         # every packet masqueraded (connection lanes + the allocating lane)
         for share in (0.001, 0.01):
@@ -410,8 +466,9 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
     res["what"] = ("flows variant with %s creations: first pass, NAT pass (dp_nat_prep + "
                    "dp_nat_resolve%s), replay, fix-up, invalidation, per launch (HIP events, median); "
                    "per-kernel times: profiles/ rocprofv3 stats of this leg"
-                   % (("masquerade (allocations from a 256-address pool)", " + dp_nat_lane_order + dp_nat_lane")
-                      if kind == "masq" else ("port-forwarding", "")))
+                   % ({"masq": ("masquerade (allocations from a 256-address pool)", " + dp_nat_lane_order + dp_nat_lane"),
+                       "mixed": ("port-forwarding and masquerade (one public /24, forwarded ports claimed)",
+                                 " + dp_nat_cross + dp_nat_lane")}.get(kind, ("port-forwarding", ""))))
     return res
 
 
@@ -486,7 +543,7 @@ def main() -> None:
     ap.add_argument("--layout", choices=["dpdk", "packed"], default="dpdk",
                     help="burst buffer layout: DPDK mbuf data (128 B headroom, 64-byte aligned "
                          "frames) or packed (96 B headroom, 16-byte aligned)")
-    ap.add_argument("--nat-kind", choices=["both", "pf", "masq"], default="both",
+    ap.add_argument("--nat-kind", choices=["both", "pf", "masq", "mixed"], default="both",
                     help="with --nat-only: which NAT legs")
     ap.add_argument("--launch-probe", action="store_true",
                     help="test hook: each rank prints its rank / world as JSON and exits before "
@@ -524,6 +581,8 @@ def main() -> None:
             legs["nat_portfw"] = nat_leg(dev, st, min(args.steps, 10), args.packets)
         if args.nat_kind in ("both", "masq"):
             legs["nat_masquerade"] = nat_leg(dev, st, min(args.steps, 10), args.packets, kind="masq")
+        if args.nat_kind in ("both", "mixed"):
+            legs["nat_mixed"] = nat_leg(dev, st, min(args.steps, 10), args.packets, kind="mixed")
         print(json.dumps(legs), flush=True)
         return
     cfg = args.config
@@ -684,6 +743,7 @@ def main() -> None:
         if world == 1 and not args.no_nat:
             result["nat_portfw"] = nat_leg(dev, stream, min(args.steps, 10), n)
             result["nat_masquerade"] = nat_leg(dev, stream, min(args.steps, 10), n, kind="masq")
+            result["nat_mixed"] = nat_leg(dev, stream, min(args.steps, 10), n, kind="mixed")
         if world == 1 and not args.no_host:
             # host-origin rate (dp_process_burst): pinned host burst buffer and
             # records, chunked H2D / kernel / D2H overlapped on several streams

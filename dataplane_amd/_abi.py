@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 import numpy as np
 
@@ -16,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 HEADROOM = 96
 
 # DoneReason (net/src/packet/meta.rs:84-119)
@@ -263,7 +264,8 @@ GPU_SYMBOLS = ["dp_abi_version", "dp_ctx_create", "dp_ctx_destroy", "dp_tables_p
                "dp_flow_invalidate", "dp_flow_set_status", "dp_flow_sweep", "dp_flow_count",
                "dp_ctx_attach_flow_table", "dp_mbuf_burst_in", "dp_mbuf_burst_out",
                "dp_process_mbufs", "dp_acl_classify", "dp_acl_classify_device",
-               "dp_acl_key_from_match", "dp_acl_classify_match"]
+               "dp_acl_key_from_match", "dp_acl_classify_match", "dp_ff_classify",
+               "dp_ff_classify_device", "dp_ff_key_from_match", "dp_ff_classify_match"]
 # dp_acl_key_t / dp_acl_result_t (the ACL classifier alone)
 ACL_KEY = np.dtype([("src_vni", "<u4"), ("dst_vni", "<u4"), ("family", "u1"), ("proto", "u1"),
                     ("sport", "<u2"), ("dport", "<u2"), ("pad", "u1", 2), ("src", "u1", 16),
@@ -271,8 +273,19 @@ ACL_KEY = np.dtype([("src_vni", "<u4"), ("dst_vni", "<u4"), ("family", "u1"), ("
 # the reference's AclKey bytes (MatchKey::as_key_into; dp_acl_key_from_match)
 ACL_MATCH_KEY_V4, ACL_MATCH_KEY_V6 = 21, 45
 ACL_RESULT = np.dtype([("rule", "<u4"), ("action", "u1"), ("scope", "u1"), ("acl", "u1"), ("pad", "u1")])
+# dp_ff_input_t / dp_ff_result_t (the flow-filter classifier alone:
+# LookupInput / LookupResult, flow-filter/src/context/tables.rs:70-97)
+FF_INPUT = np.dtype([("src_vni", "<u4"), ("dst_vni", "<u4"), ("src_family", "u1"), ("dst_family", "u1"),
+                     ("proto", "u1"), ("gate", "u1"), ("sport", "<u2"), ("dport", "<u2"), ("pad", "u1", 4),
+                     ("src", "u1", 16), ("dst", "u1", 16)])
+FF_RESULT = np.dtype([("outcome", "u1"), ("dst_nat", "u1"), ("src_nat", "u1"), ("pad", "u1"),
+                      ("dst_vni", "<u4")])
+FF_DESTINATION_MISS, FF_SOURCE_MISS, FF_ROUTE = 0, 1, 2
+FF_REMOTE, FF_LOCAL = 1, 2
+# the reference's RemoteKey / LocalKey bytes (MatchKey::as_key_into; dp_ff_key_from_match)
+FF_REMOTE_KEY_V4, FF_REMOTE_KEY_V6, FF_LOCAL_KEY_V4, FF_LOCAL_KEY_V6 = 15, 27, 16, 28
 NP_STRUCTS = dict(dp_flow_key_t=FLOW_KEY, dp_flow_t=FLOW, dp_flow_info_t=FLOW_INFO, dp_acl_key_t=ACL_KEY,
-                  dp_acl_result_t=ACL_RESULT)
+                  dp_acl_result_t=ACL_RESULT, dp_ff_input_t=FF_INPUT, dp_ff_result_t=FF_RESULT)
 
 
 class MbufLayout(C.Structure):
@@ -299,6 +312,33 @@ def _load(path: str) -> C.CDLL:
     return C.CDLL(path)
 
 
+def _one_hip_runtime() -> None:
+    """One HIP runtime per process (dp_ctx_create refuses two).
+    PyTorch bundles its own libamdhip64 / libhsa-runtime64 and its libraries
+    ask for them by the unversioned name, which libdpgpu.so's
+    libamdhip64.so.7 (the ROCm runtime it was linked against) does not
+    answer: with libdpgpu.so loaded first, a later `import torch` would map a
+    second runtime beside it.  So where PyTorch is installed its runtime is
+    loaded first; libdpgpu.so's libamdhip64.so.7 then resolves to it by its
+    soname, and PyTorch finds the same files already mapped.  Nothing is
+    imported, nothing touches the GPU."""
+    if "torch" in sys.modules:
+        return  # (its runtime is mapped already; libdpgpu.so resolves to it)
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    d = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        if not os.path.exists(os.path.join(d, name)):
+            return
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        C.CDLL(os.path.join(d, name), mode=C.RTLD_GLOBAL)
+
+
 _gpu = None
 
 
@@ -307,6 +347,8 @@ def gpu_lib() -> C.CDLL:
     global _gpu
     if _gpu is None:
         # DPGPU_LIB selects a diagnostic build (e.g. lib/libdpgpu_timing.so)
+        if not os.environ.get("DPGPU_NO_RUNTIME_PRELOAD"):  # (hip_runtimes_diag.py's two-runtime leg)
+            _one_hip_runtime()
         lib = _load(os.environ.get("DPGPU_LIB") or os.path.join(LIB_DIR, "libdpgpu.so"))
         lib.dp_abi_version.restype = C.c_uint32
         lib.dp_ctx_create.argtypes = [C.c_int, C.POINTER(_VP)]
@@ -346,6 +388,12 @@ def gpu_lib() -> C.CDLL:
         lib.dp_acl_classify_device.argtypes = [_VP, _VP, _VP, C.c_uint32, _VP]
         lib.dp_acl_key_from_match.argtypes = [_VP, C.c_uint32, C.c_uint32, C.c_uint32, _VP]
         lib.dp_acl_classify_match.argtypes = [_VP, _VP, C.c_uint32, C.c_uint32, C.c_uint32, _VP]
+        lib.dp_ff_classify.argtypes = [_VP, _VP, _VP, C.c_uint32]
+        lib.dp_ff_classify_device.argtypes = [_VP, _VP, _VP, C.c_uint32, _VP]
+        lib.dp_ff_key_from_match.argtypes = [C.c_int, _VP, C.c_uint32, C.c_uint32, C.c_uint32, _VP]
+        lib.dp_ff_classify_match.argtypes = [_VP, C.c_int, _VP, C.c_uint32, C.c_uint32, C.c_uint32, _VP]
+        lib.dpd_debug_classify_copies.argtypes = [C.c_int]
+        lib.dpd_debug_hip_runtimes.restype = C.c_int
         lib.dpf_debug_nat_sequential.argtypes = [C.c_int]
         lib.dpf_debug_nat_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32]
         lib.dpf_debug_nat_counters.restype = C.c_int

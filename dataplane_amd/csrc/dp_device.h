@@ -399,6 +399,10 @@ struct Image {
   // forwarding or masquerade, a port-forwarding rule or a masquerade expose
   // (the flows variant without that code serves tables that never held it)
   uint32_t snat;
+  // 1: the image configures masquerade (a flow-filter rule requiring it or a
+  // masquerade expose): a flows burst sizes the masquerade split's lane
+  // scratch (dp_runtime.cpp)
+  uint32_t masq;
   uint32_t n_nh;             // NhRec count
   // The context tables every packet reads -- VNI slots, the pair map's slots,
   // PairRecs, NhRecs -- copied into each workgroup's LDS when together they

@@ -124,8 +124,8 @@ constexpr uint32_t kPqPfDone = 1u << 14;
 constexpr uint32_t kPfForward = 0xffu;
 
 // words of FlowCtx::pf_cnt
-constexpr uint32_t kCntWords = 32;
-#define DPF_CNT_WORDS 32
+constexpr uint32_t kCntWords = 40;
+#define DPF_CNT_WORDS 40
 
 // The launch-time view of a flow table for one burst.
 struct FlowCtx {
@@ -173,7 +173,8 @@ struct FlowCtx {
   // Masquerade (dp_nat_resolve, dp_nat_lane): [8] masquerade records, [9]
   // PortForwarder records, [10] a masqueraded packet whose peer could
   // masquerade back (pfw::masq_back), [11] records on the allocating lane,
-  // [12] the mode that ran (1 one lane, 2 connections, 3 split), [13] records
+  // [12] the mode that ran (1 one lane, 2 connections, 3 split, 4 connections
+  // near the capacity, 5 connections beside the split), [13] records
   // a connection lane left to the allocating lane, [14] allocations served in
   // wave batches, [15] allocations on the lane alone, [16] pairs the split
   // pass could not create (never: it runs only with room; counters for tests).
@@ -184,7 +185,12 @@ struct FlowCtx {
   // clock64 ticks), [23..25] the allocations' parts (the set's address and
   // block, serving the records, the block's update), [26] allocation steps,
   // [27] a steady refresh in the burst (dp_nat_prep), [28] an initial key of
-  // the lane's allocating records repeats, [29] a lane record runs alone
+  // the lane's allocating records repeats, [29] a lane record runs alone,
+  // [30] a mixed burst (port forwarding and masquerade) that cannot run its
+  // port-forwarding connections beside the split (dp_nat_mark, dp_nat_cross),
+  // [31] a mixed burst's bound on the slots its inserts may add (dp_nat_prep),
+  // [32] its creations' reverse keys registered, [33] masquerading records
+  // dp_nat_cross looked up, [34] of them found (test counters)
   unsigned long long *grp_tab, *grp_head, *grp_next;
   uint32_t *grp_list;
   uint32_t grp_mask;
@@ -193,7 +199,8 @@ struct FlowCtx {
   uint4 *repl;
   uint32_t rmask;
   uint32_t force_seq;   // test hook (dpf_debug_nat_sequential): 1 the one-lane NAT pass always,
-                        // 2 the split pass with every allocation on the lane alone (no wave batches)
+                        // 2 the split pass with every allocation on the lane alone (no wave batches),
+                        // 3 no mode 4, 4 no mode 5 (a mixed burst on one lane)
   // the masquerading burst's allocating lane: its packets (bitmap by packet
   // index + summary, as pf_bits) and their order
   uint32_t *lane_bits, *lane_sum, *lane_order;

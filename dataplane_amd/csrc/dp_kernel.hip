@@ -4182,10 +4182,96 @@ __device__ inline dpf::FKey slot_key(const dpf::FlowSlot &s) {
   return k;
 }
 
+// A burst with both kinds of record (mode 5): port forwarding's connections
+// run as connection lanes beside the masquerade split's (dp_nat_resolve),
+// before the allocating lane (dp_nat_lane).  That is the one-lane pass's
+// outcome when no port-forwarding connection meets a masquerade record's
+// flows and the inserts cannot meet the capacity (room for every pair):
+//  - a port-forwarding record on a masqueraded flow (its creation would
+//    replace it) or a creation whose reverse key another flow holds: no
+//    connection key (conn_key), the burst runs on one lane (pf_cnt[5]);
+//  - a masquerading record on a port-forwarded flow (its allocation would
+//    replace that flow), a record that both forwards and masquerades: one
+//    lane (dp_nat_mark, pf_cnt[30]);
+//  - a masquerading record without a live flow whose initial key is the
+//    reverse key a creation of the burst inserts (the forwarded host's first
+//    packet back in the same burst, before FlowLookup could see the new pair):
+//    one lane (dp_nat_prep registers the creations' reverse keys, dp_nat_cross
+//    looks the initial keys up, pf_cnt[30]);
+//  - a masquerade allocation never hands out a forwarded public tuple of its
+//    manifest (the claims, apalloc/setup.rs:73-91), so no pair the lane
+//    creates meets a key a creation inserts.
+// A record's initial key cannot be a creation's forward key: the same key
+// from the same VPC gets the same flow-filter decision, so the same kind.
+// Port-forwarding connection keys carry bit 31, masquerade ones (a slot
+// index) never do, so the two kinds never share a connection.
+[[maybe_unused]] constexpr uint32_t kPfConnBit = 0x80000000u;
+
+// The key a masquerading record's allocation inserts first (masq_plan's
+// initial key) when it has no port forwarding; false: it inserts none.
+__device__ bool masq_ik(const dpf::PfReq &R, dpf::FKey &k) {
+  if (R.bits & dpf::kPqIkey) {
+    for (int j = 0; j < 11; j++) k.w[j] = R.ikey[j];
+    return true;
+  }
+  const uint32_t fam = (R.proto >> 8) & 0xffu;
+  uint32_t kind;
+  if (R.bits & dpf::kPqTcp) kind = DP_FLOW_TCP;
+  else if (R.bits & dpf::kPqUdp) kind = DP_FLOW_UDP;
+  else if (R.bits & dpf::kPqIcmp) kind = (R.bits & dpf::kPqQuery) ? DP_FLOW_ICMP_QUERY : DP_FLOW_ICMP_OTHER;
+  else return false;
+  k.w[0] = R.src_vni;
+  k.w[1] = fam | (kind << 8);
+  k.w[2] = kind == DP_FLOW_ICMP_OTHER ? 0u : R.ports;
+  for (int j = 0; j < 4; j++) { k.w[3 + j] = bswap(R.src[j]); k.w[7 + j] = bswap(R.dst[j]); }
+  return true;
+}
+
+// The creations' reverse keys of a mixed burst, in dup_tab under the tag
+// ~burst (dp_nat_lane_plan later claims entries under the tag burst and takes
+// these for empty ones): the slot from one hash of the key, the tag word from
+// another, as dp_nat_lane_plan keys its entries.
+__device__ __forceinline__ void cross_hash(const dpf::FlowCtx &fc, const dpf::FKey &k, uint32_t &x,
+                                           unsigned long long &want) {
+  x = dpm::kmix(dpf::fkey_hash(k), 0x5bd1e995u, 0u) & fc.grp_mask;
+  const uint32_t h2 = dpm::kmix(dpm::kmix(k.w[0], k.w[1], k.w[2]), dpm::kmix(k.w[3], k.w[4], k.w[5]) ^ k.w[6],
+                                dpm::kmix(k.w[7], k.w[8], k.w[9]) ^ k.w[10]);
+  want = ((unsigned long long)~fc.burst << 32) | h2;
+}
+// false: the table is full (the caller sends the burst to one lane)
+__device__ bool cross_put(const dpf::FlowCtx &fc, const dpf::FKey &k) {
+  uint32_t x;
+  unsigned long long want;
+  cross_hash(fc, k, x, want);
+  for (uint32_t p = 0; p <= fc.grp_mask; p++, x = (x + 1) & fc.grp_mask) {
+    const unsigned long long cur = __hip_atomic_load(&fc.dup_tab[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == want) return true;
+    if ((uint32_t)(cur >> 32) == ~fc.burst) continue;
+    const unsigned long long got = atomicCAS(&fc.dup_tab[x], cur, want);
+    if (got == cur || got == want) return true;
+  }
+  return false;
+}
+// may `k` be a registered reverse key (hash equality; a full table: yes)
+__device__ bool cross_has(const dpf::FlowCtx &fc, const dpf::FKey &k) {
+  uint32_t x;
+  unsigned long long want;
+  cross_hash(fc, k, x, want);
+  for (uint32_t p = 0; p <= fc.grp_mask; p++, x = (x + 1) & fc.grp_mask) {
+    const unsigned long long cur = __hip_atomic_load(&fc.dup_tab[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == want) return true;
+    if ((uint32_t)(cur >> 32) != ~fc.burst) return false;
+  }
+  return true;
+}
+
 // The record's connection key; false: the record needs the sequential pass
 // (masquerade: one allocator; a flow without port-forwarding state; a pair it
 // may create that is not its flow's).
-__device__ bool conn_key(const Img &g, const dpf::FlowCtx &fc, const dpf::PfReq &R, uint32_t &key) {
+// cross: a mixed burst (mode 5): a creation's reverse key is registered for
+// dp_nat_cross (cross_put; a full table refuses the record).
+__device__ bool conn_key(const Img &g, const dpf::FlowCtx &fc, const dpf::PfReq &R, uint32_t &key,
+                         bool cross = false) {
   if (R.bits & dpf::kPqMasq) return false;
   dpf::FKey rk;
   const bool cand = creation_rk(g, R, rk);
@@ -4199,6 +4285,10 @@ __device__ bool conn_key(const Img &g, const dpf::FlowCtx &fc, const dpf::PfReq 
     if (z != dpf::kNoSlot && !((v.y & dpf::kFlagPf) && (fc.slots[z].pf & 0xffu) == DP_PF_SRC_NAT)) return false;
   }
   if (R.slot == dpf::kNoSlot) {
+    if (cand && cross) {
+      if (!cross_put(fc, rk)) return false;
+      atomicAdd(&fc.pf_cnt[32], 1u);
+    }
     key = cand ? dpf::fkey_hash(rk) : (R.idx * 0x9E3779B1u) ^ 0x5bd1e995u;  // no flow, no pair: alone
     return true;
   }
@@ -4218,6 +4308,10 @@ __device__ bool conn_key(const Img &g, const dpf::FlowCtx &fc, const dpf::PfReq 
   if (cand)
     for (int j = 0; j < 11; j++)
       if (rk.w[j] != ak.w[j]) return false;
+  if (cand && cross) {
+    if (!cross_put(fc, rk)) return false;
+    atomicAdd(&fc.pf_cnt[32], 1u);
+  }
   key = dpf::fkey_hash(ak);
   return true;
 }
@@ -4306,14 +4400,26 @@ __device__ uint32_t sort_conn(unsigned long long *nx, uint32_t list) {
 // allocating lane inserts, and it takes its records one by one in packet
 // order when room is short -- dp_nat_lane), 4 connections in parallel with
 // insert_common's capacity admissions decided beforehand in packet order
-// (port forwarding without room for every pair: dp_nat_admit_*).  pre: the
-// mode before dp_nat_admit_plan has looked at the connections (4 may turn 1).
+// (port forwarding without room for every pair: dp_nat_admit_*), 5 mixed:
+// port-forwarding connections in parallel beside the masquerade split (a
+// burst holding both kinds of record, with room for every pair; below).  pre:
+// the mode before dp_nat_admit_plan has looked at the connections (4 may turn
+// 1); dp_nat_prep and dp_nat_cross may still turn 5 into 1.
 __device__ __forceinline__ uint32_t nat_mode(const dpf::FlowCtx &fc, bool pre = false) {
   if (fc.force_seq == 1 || fc.pf_cnt[5]) return 1u;
-  if (fc.pf_cnt[8]) return fc.pf_cnt[9] || fc.pf_cnt[10] ? 1u : 3u;
   const uint64_t len0 = ((uint64_t)fc.pf_cnt[7] << 32) | fc.pf_cnt[6];
   const uint64_t total = fc.pf_cnt[1];
-  if (len0 + 2ull * total <= fc.capacity && len0 + 2ull * total <= fc.hard) return 2u;
+  const bool room = len0 + 2ull * total <= fc.capacity && len0 + 2ull * total <= fc.hard;
+  if (fc.pf_cnt[8]) {
+    if (fc.pf_cnt[10] || !fc.lane_plan) return 1u;
+    if (!fc.pf_cnt[9]) return 3u;
+    // (mixed: room for every slot the burst may add, pf_cnt[31] as dp_nat_prep
+    // bounds it -- before it has, the mode prep runs in)
+    const uint64_t add = fc.pf_cnt[31];
+    const bool mroom = len0 + add <= fc.capacity && len0 + add <= fc.hard;
+    return mroom && !fc.pf_cnt[30] && fc.force_seq != 4 ? 5u : 1u;
+  }
+  if (room) return 2u;
   // (the 7/8 bound out of reach: only the capacity can refuse, and only a
   // creation's first insert)
   if (fc.force_seq != 3 && len0 + 2ull * total <= fc.hard && fc.capacity <= fc.hard && total <= (4u << 20) &&
@@ -4321,6 +4427,9 @@ __device__ __forceinline__ uint32_t nat_mode(const dpf::FlowCtx &fc, bool pre = 
     return 4u;
   return 1u;
 }
+
+// the modes that run the masquerade split (connection lanes, the allocating lane)
+__device__ __forceinline__ bool split_mode(uint32_t m) { return m == 3u || m == 5u; }
 
 __device__ __forceinline__ void flag_once(uint32_t *w) {
   if (!__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicOr(w, 1u);
@@ -4761,7 +4870,10 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
   __shared__ uint32_t s_fl;
   if (threadIdx.x == 0) s_fl = 0;
   __syncthreads();
-  uint32_t fl = 0;  // the kinds seen: 1 port forwarding, 2 masquerade, 4 masq_back
+  // the kinds seen: 1 port forwarding, 2 masquerade, 4 masq_back, 8 what a
+  // mixed burst cannot run beside the split (a record that both forwards and
+  // masquerades, a masquerading record on a port-forwarded flow)
+  uint32_t fl = 0;
   for (uint32_t rec = blockIdx.x * 256 + threadIdx.x; rec < nrec; rec += gridDim.x * 256) {
     // the record's kinds; a steady refresh (its bit in fc.steady, a word per
     // wave: the wave's 64 records are consecutive), else its pair's tag
@@ -4770,12 +4882,26 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
       // the burst's kinds of record (the NAT pass's mode rests on them)
       if (!(R.bits & dpf::kPqReached)) return false;
       if (R.bits & dpf::kPqPf) fl |= 1u;
-      if (!(R.bits & dpf::kPqMasq)) return false;
+      if (!(R.bits & dpf::kPqMasq)) {
+        // a port-forwarding record on a masqueraded pair (a creation replaces
+        // its flow): that pair's refreshes are not order-free
+        if (fc.mq && R.slot <= fc.mask) {
+          const dpf::FlowSlot f = pfw::load_slot(&fc.slots[R.slot]);
+          if (f.state == R.state && (f.flags & dpf::kFlagMasq)) {
+            fc.slots[R.slot].nat_tag = fc.burst;
+            if (f.related <= fc.mask && fc.slots[f.related].state == f.related_tag)
+              fc.slots[f.related].nat_tag = fc.burst;
+          }
+        }
+        return false;
+      }
       fl |= 2u;
+      if (R.bits & dpf::kPqPf) fl |= 8u;
       if (!(fl & 4u) && pfw::masq_back(fc, R)) fl |= 4u;
       if (!fc.mq || R.slot > fc.mask) return false;
       const dpf::FlowSlot f = pfw::load_slot(&fc.slots[R.slot]);
       if (f.state != R.state) return false;
+      if (f.flags & dpf::kFlagPf) fl |= 8u;
       dpf::FlowSlot o;
       if (f.related <= fc.mask) o = pfw::load_slot(&fc.slots[f.related]);
       else o.state = 0;
@@ -4794,8 +4920,8 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
     if ((threadIdx.x & 63) == 0) fc.steady[rec >> 6] = m;
 #endif
   }
-  uint32_t *const words[3] = {&fc.pf_cnt[9], &fc.pf_cnt[8], &fc.pf_cnt[10]};
-  pfw::flags_block(&s_fl, fl, words, 3);
+  uint32_t *const words[4] = {&fc.pf_cnt[9], &fc.pf_cnt[8], &fc.pf_cnt[10], &fc.pf_cnt[30]};
+  pfw::flags_block(&s_fl, fl, words, 4);
 }
 
 // dp_nat_prep: the records of the burst's NAT pass (their packet order for
@@ -4810,7 +4936,8 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
   const uint32_t nrec = fc.pf_cnt[0];
   if (!nrec) return;
   const Img g{img_base, *im};
-  const bool split = pfw::nat_mode(fc) == 3;  // (dp_nat_mark's flags decide it)
+  const uint32_t mode0 = pfw::nat_mode(fc);  // (dp_nat_mark's flags decide it)
+  const bool split = pfw::split_mode(mode0), mixed = mode0 == 5;
   const unsigned long long tag = (unsigned long long)fc.burst << 32;
   __shared__ uint32_t s_fl;
   if (t == 0) s_fl = 0;
@@ -4819,6 +4946,13 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
   // the connections new this burst: their list entries claimed once per
   // workgroup and pass (a claim per wave queued ~10k same-word atomics)
   __shared__ uint32_t s_cnt[16], s_base;
+  // a mixed burst: a bound on the slots its inserts may add (pf_cnt[31]) --
+  // two per port-forwarding connection (its creations insert the same two
+  // keys) and two per masquerading record that is not a steady refresh (an
+  // allocation inserts its initial key and a new reverse key)
+  __shared__ uint32_t s_add;
+  if (t == 0) s_add = 0;
+  uint32_t add = 0;
   // file one record; fresh: its connection is new (h: its hash slot)
   auto visit = [&](uint32_t rec, uint32_t &h, bool &fresh) {
     dpf::PfReq &R = fc.pf[rec];
@@ -4848,11 +4982,14 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
           return;
         }
       }
+      if (mixed) add += 2;
       if (!pfw::masq_conn(fc, R, key)) {
         pfw::lane_mark(fc, R, 0u);
         return;
       }
-    } else if (!pfw::conn_key(g, fc, R, key)) {
+    } else if (pfw::conn_key(g, fc, R, key, mixed)) {
+      key |= pfw::kPfConnBit;
+    } else {
       fl |= 2u;
       return;
     }
@@ -4881,6 +5018,7 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
     uint32_t h = 0;
     bool fresh = false;
     if (rec < nrec) visit(rec, h, fresh);
+    if (mixed && fresh && (fc.grp_tab[h] & pfw::kPfConnBit)) add += 2;
 #ifdef DP_EMU
     if (fresh) fc.grp_list[atomicAdd(&fc.pf_cnt[4], 1u)] = h;
 #else
@@ -4898,8 +5036,49 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
     __syncthreads();
 #endif
   }
+  if (mixed) {
+#ifdef DP_EMU
+    if (add) atomicAdd(&fc.pf_cnt[31], add);
+#else
+    if (add) atomicAdd(&s_add, add);
+    __syncthreads();
+    if (t == 0 && s_add) atomicAdd(&fc.pf_cnt[31], s_add);
+#endif
+  }
   uint32_t *const words[2] = {&fc.pf_cnt[27], &fc.pf_cnt[5]};
   pfw::flags_block(&s_fl, fl, words, 2);
+}
+
+// dp_nat_cross (mode 5): a masquerading record without a live attached flow
+// may allocate, and its pair's first insert is its initial key; when that is
+// the reverse key of a port-forwarding creation of the burst (dp_nat_prep
+// registered them), the allocating lane and the connection lanes would meet
+// in one key: the burst runs on one lane (pf_cnt[30]).  A record on a live
+// flow needs no look: its initial key is that flow's, which a creation's
+// reverse key cannot be (conn_key).
+__global__ void __launch_bounds__(256) dp_nat_cross(dpf::FlowCtx fc) {
+  const uint32_t nrec = fc.pf_cnt[0];
+  if (!nrec || !fc.pf_cnt[1] || pfw::nat_mode(fc) != 5) return;
+  __shared__ uint32_t s_fl;
+  if (threadIdx.x == 0) s_fl = 0;
+  __syncthreads();
+  uint32_t fl = 0, looked = 0, found = 0;
+  // (the record read in place: a copy through load_req gave wrong keys in
+  // this kernel's optimised build -- an unexplained codegen interaction;
+  // DESIGN.md §3)
+  for (uint32_t rec = blockIdx.x * 256 + threadIdx.x; rec < nrec; rec += gridDim.x * 256) {
+    const dpf::PfReq &R = fc.pf[rec];
+    if ((R.bits & (dpf::kPqReached | dpf::kPqMasq)) != (dpf::kPqReached | dpf::kPqMasq)) continue;
+    if (R.slot <= fc.mask && fc.slots[R.slot].state == R.state) continue;
+    dpf::FKey ik;
+    if (!pfw::masq_ik(R, ik)) continue;
+    looked++;
+    if (pfw::cross_has(fc, ik)) { fl = 1u; found++; }
+  }
+  if (looked) atomicAdd(&fc.pf_cnt[33], looked);
+  if (found) atomicAdd(&fc.pf_cnt[34], found);
+  uint32_t *const words[1] = {&fc.pf_cnt[30]};
+  pfw::flags_block(&s_fl, fl, words, 1);
 }
 
 // dp_nat_resolve: the reference's PortForwarder and Masquerade over the
@@ -4982,7 +5161,9 @@ dp_nat_resolve(const uint8_t *__restrict__ img_base, const Image *__restrict__ i
     // (mode 4: dp_nat_admit_plan sorted the list already)
     uint32_t r = mode == 4 ? (uint32_t)fc.grp_head[h] : pfw::sort_conn(fc.grp_next, (uint32_t)fc.grp_head[h]);
 #endif
-    if (mode == 3) {
+    // (mode 5: a masquerading connection, or a port-forwarding one -- never
+    // both: their keys differ in bit 31)
+    if (mode == 3 || (mode == 5 && (fc.pf[r].bits & dpf::kPqMasq))) {
       pfw::masq_conn_run(q, r);
       continue;
     }
@@ -5041,6 +5222,9 @@ __global__ void __launch_bounds__(1024) dp_nat_admit_scan(dpf::FlowCtx fc, int s
     if (t < nb) fc.adm_blk[t] = sh[t] - v;
     return;
   }
+  // (the grid covers the burst; only the blocks over records take part, so
+  // adm_blk's 1024 words hold any burst size: nat_mode keeps total <= 4M)
+  if (blockIdx.x * kAdmChunk >= total) return;
   const uint32_t k0 = blockIdx.x * kAdmChunk + t * 4;
   uint32_t w[4], c = 0;
   for (int j = 0; j < 4; j++) {
@@ -5081,7 +5265,7 @@ __global__ void __launch_bounds__(1024) dp_nat_admit_scan(dpf::FlowCtx fc, int s
 // after the lane's allocations.
 __global__ void __launch_bounds__(256) dp_nat_lane_plan(const uint8_t *__restrict__ img_base,
                                                         const Image *__restrict__ im, dpf::FlowCtx fc) {
-  if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3) return;
+  if (!fc.pf_cnt[1] || !pfw::split_mode(pfw::nat_mode(fc))) return;
   const uint32_t nl = fc.pf_cnt[11];
   const Img g{img_base, *im};
   const pfw::Seq qs{fc, g, false};
@@ -5201,7 +5385,7 @@ __device__ __forceinline__ uint32_t nth_bit(uint32_t x, uint32_t k) {
 
 __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ img_base,
                                                   const Image *__restrict__ im, dpf::FlowCtx fc) {
-  if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3) return;
+  if (!fc.pf_cnt[1] || !pfw::split_mode(pfw::nat_mode(fc))) return;
   const uint32_t nl = fc.pf_cnt[11];
   const bool post = !fc.pf_cnt[28] && !fc.pf_cnt[29];
   const int t = threadIdx.x;
@@ -5589,7 +5773,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
 // refused).  dp_nat_lane_end then drops the replaced fills' allocations.
 __global__ void __launch_bounds__(256) dp_nat_pairs(const uint8_t *__restrict__ img_base,
                                                     const Image *__restrict__ im, dpf::FlowCtx fc) {
-  if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3 || fc.pf_cnt[28] || fc.pf_cnt[29]) return;
+  if (!fc.pf_cnt[1] || !pfw::split_mode(pfw::nat_mode(fc)) || fc.pf_cnt[28] || fc.pf_cnt[29]) return;
   const uint32_t nl = fc.pf_cnt[11];
   const Img g{img_base, *im};
   const pfw::Seq qp{fc, g, true};
@@ -5609,8 +5793,13 @@ __global__ void __launch_bounds__(256) dp_nat_pairs(const uint8_t *__restrict__ 
   if ((threadIdx.x & 63) == 0 && v)
     atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), (unsigned long long)v);
 }
+// (also after the connection-parallel port-forwarding pass, modes 2 and 4:
+// a creation there may replace a masqueraded flow, whose allocation then goes
+// when the burst ends, as in the one-lane pass)
 __global__ void dp_nat_lane_end(dpf::FlowCtx fc) {
-  if (!fc.pf_cnt[1] || pfw::nat_mode(fc) != 3 || fc.pf_cnt[28] || fc.pf_cnt[29] || !fc.mq) return;
+  if (!fc.pf_cnt[1] || !fc.mq || !fc.pf_cnt[3]) return;
+  const uint32_t mode = pfw::nat_mode(fc);
+  if (mode == 1 || (pfw::split_mode(mode) && (fc.pf_cnt[28] || fc.pf_cnt[29]))) return;
   const dpm::View V{fc.mq};
   for (uint32_t k = 0; k < fc.pf_cnt[3]; k++) dpm::release(V, fc.mq_rel[2 * k], fc.mq_rel[2 * k + 1]);
 }
@@ -5661,6 +5850,54 @@ __global__ void __launch_bounds__(256) dp_acl_classify_k(const uint8_t *__restri
   } else {
     r.action = DP_ACL_ALLOW;
     r.acl = 5;
+  }
+  out[i] = r;
+}
+
+// dp_ff_classify: FlowFilterContext::lookup_batch alone (dpgpu.h "The
+// flow-filter classifier alone"), one input per work-item -- stage_flow_filter's
+// two lookups without a packet around them: stage 1 over the (src VNI,
+// GateVni) group of the remote rules, on a hit stage 2 over the (src VNI,
+// verdict VPC, SourceGate) group of the local rules (flow-filter/src/context/
+// tables.rs:854-915).  stage: 0 both (lookup_batch), 1 the remote rules alone,
+// 2 the local rules alone (dst_vni is then the local key's VPC).
+__global__ void __launch_bounds__(256) dp_ff_classify_k(const uint8_t *__restrict__ img_base,
+                                                        const Image *__restrict__ im,
+                                                        const dp_ff_input_t *__restrict__ in,
+                                                        dp_ff_result_t *__restrict__ out, uint32_t n, int stage) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const dp_ff_input_t q = in[i];
+  dp_ff_result_t r{};
+  r.outcome = stage == 2 ? DP_FF_SOURCE_MISS : DP_FF_DESTINATION_MISS;
+  if (q.src_family != q.dst_family || (q.src_family != 4 && q.src_family != 6)) { out[i] = r; return; }
+  const Img g{img_base, *im};
+  const int t = q.src_family == 4 ? 0 : 1;
+  auto be = [&](const uint8_t *a, int o) {
+    return ((uint32_t)a[o] << 24) | ((uint32_t)a[o + 1] << 16) | ((uint32_t)a[o + 2] << 8) | a[o + 3];
+  };
+  auto key = [&](const uint8_t *a) {
+    return t == 0 ? Key128{0, be(a, 0)}
+                  : Key128{((uint64_t)be(a, 0) << 32) | be(a, 4), ((uint64_t)be(a, 8) << 32) | be(a, 12)};
+  };
+  uint32_t gi, dvni = q.dst_vni;
+  if (stage != 2) {
+    const int32_t rg = hash_find(g, g.im.ff_remote[t].groups, q.src_vni, q.dst_vni, 0, gi) ? (int32_t)gi : -1;
+    const Hit rh = classify<W_ACTION | W_ACTION2>(g, CLS_ARRAYS(ff_remote, t), rg, t, q.proto, Key128{0, 0},
+                                                  key(q.dst), 0, q.dport);
+    if (rh.rule < 0) { out[i] = r; return; }
+    r.dst_vni = rh.action;
+    r.dst_nat = (uint8_t)rh.action2;
+    dvni = rh.action;
+    r.outcome = stage == 1 ? DP_FF_ROUTE : DP_FF_SOURCE_MISS;
+    if (stage == 1) { out[i] = r; return; }
+  }
+  const int32_t lg = hash_find(g, g.im.ff_local[t].groups, q.src_vni, dvni, q.gate, gi) ? (int32_t)gi : -1;
+  const Hit lh = classify<W_ACTION>(g, CLS_ARRAYS(ff_local, t), lg, t, q.proto, key(q.src), Key128{0, 0},
+                                    q.sport, 0);
+  if (lh.rule >= 0) {
+    r.src_nat = (uint8_t)lh.action;
+    r.outcome = DP_FF_ROUTE;
   }
   out[i] = r;
 }
@@ -6000,6 +6237,14 @@ extern "C" int dpk_acl_classify(const uint8_t *img_base, const void *image_dev, 
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+extern "C" int dpk_ff_classify(const uint8_t *img_base, const void *image_dev, const dp_ff_input_t *in,
+                               dp_ff_result_t *out, uint32_t n, int stage, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dp_ff_classify_k, dim3((n + 255) / 256), dim3(256), 0, stream, img_base,
+                     reinterpret_cast<const Image *>(image_dev), in, out, n, stage);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
                                hipStream_t stream) {
   if (n == 0 || !in || !out) return 0;
@@ -6080,6 +6325,8 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   hipLaunchKernelGGL(dp_nat_mark, dim3(rb0), dim3(256), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_prep, dim3(pb), dim3(1024), 0, stream, img_base, im, fc);
   const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  // a mixed burst: may the allocating lane meet a port-forwarding creation's key
+  hipLaunchKernelGGL(dp_nat_cross, dim3(rb), dim3(256), 0, stream, fc);
   // port forwarding near the capacity: the creations' admissions in packet order
   hipLaunchKernelGGL(dp_nat_admit_plan, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   const uint32_t ab = (n + kAdmChunk - 1) / kAdmChunk;

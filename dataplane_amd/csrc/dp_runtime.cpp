@@ -42,6 +42,8 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_de
                                    int v6w, int ctx, hipStream_t stream);
 extern "C" int dpk_acl_classify(const uint8_t *img_base, const void *image_dev, const dp_acl_key_t *keys,
                                 dp_acl_result_t *out, uint32_t n, hipStream_t stream);
+extern "C" int dpk_ff_classify(const uint8_t *img_base, const void *image_dev, const dp_ff_input_t *in,
+                               dp_ff_result_t *out, uint32_t n, int stage, hipStream_t stream);
 extern "C" int dpk_mark_failed(const dp_pkt_in_t *in, dp_pkt_out_t *out, dp_pkt_meta_t *meta, uint32_t n,
                                hipStream_t stream);
 extern "C" int dpk_stage_expand(const uint8_t *cin, const uint32_t *pos, const dp_pkt_in_t *in, uint8_t *buf,
@@ -64,6 +66,30 @@ int fail(int rc, const char *what, hipError_t e = hipSuccess) {
     g_err += hipGetErrorString(e);
   }
   return rc;
+}
+
+// How many distinct HIP runtimes (libamdhip64 files) the process maps.  Two
+// appear when another library brings its own copy after this one loaded
+// (PyTorch bundles one and asks for it by the unversioned name, which this
+// library's libamdhip64.so.7 does not answer): two HIP and two HSA runtimes
+// then each manage the process's one KFD state, and host-memory copies of
+// one went unwritten.  1 when /proc is unreadable.
+int hip_runtimes_mapped() {
+  FILE *f = std::fopen("/proc/self/maps", "r");
+  if (!f) return 1;
+  std::vector<std::string> seen;
+  char line[4096];
+  while (std::fgets(line, sizeof line, f)) {
+    const char *p = std::strchr(line, '/');
+    if (!p) continue;
+    std::string path(p);
+    while (!path.empty() && (path.back() == '\n' || path.back() == ' ')) path.pop_back();
+    const size_t b = path.rfind('/');
+    if (path.compare(b + 1, 14, "libamdhip64.so") != 0) continue;
+    if (std::find(seen.begin(), seen.end(), path) == seen.end()) seen.push_back(path);
+  }
+  std::fclose(f);
+  return seen.empty() ? 1 : (int)seen.size();
 }
 
 }  // namespace
@@ -196,10 +222,11 @@ struct dp_ctx {
   dp_pkt_out_t *d_out = nullptr;
   dp_pkt_meta_t *d_meta = nullptr;
   uint64_t *d_stats = nullptr;
-  // dp_acl_classify's device keys and results (grown as needed)
-  dp_acl_key_t *acl_keys = nullptr;
-  dp_acl_result_t *acl_res = nullptr;
-  uint32_t acl_cap = 0;
+  // the classifiers alone on host memory (dp_acl_classify, dp_ff_classify):
+  // device inputs and results, and their pinned host staging (grown as needed)
+  void *cls_dev = nullptr;
+  void *cls_host = nullptr;
+  size_t cls_cap = 0;
   uint32_t cap_n = 0;
   uint32_t *d_pos = nullptr;           // staged copies: span positions (16-byte units)
   // staged copies: pinned host side (records, positions, packed spans in and
@@ -435,10 +462,24 @@ extern "C" {
 
 uint32_t dp_abi_version(void) { return DPGPU_ABI_VERSION; }
 
+// Test hook (not part of dpgpu.h): the classifiers' host-memory copies -- 0
+// pinned staging, stream-ordered on the context's stream (the default); 1 the
+// round-5 path, hipMemcpyAsync between pageable memory and stream-ordered
+// allocations (scripts/dev/hip_runtimes_diag.py reproduces its anomaly).
+// Test hook (not part of dpgpu.h): the HIP runtimes this process maps
+// (dp_ctx_create refuses more than one)
+int dpd_debug_hip_runtimes(void) { return hip_runtimes_mapped(); }
+
+static std::atomic<int> g_cls_copies{0};
+void dpd_debug_classify_copies(int mode) { g_cls_copies.store(mode == 1 ? 1 : 0, std::memory_order_relaxed); }
+
 const char *dp_last_error(void) { return g_err.c_str(); }
 
 int dp_ctx_create(int device_ordinal, dp_ctx_t **out) {
   if (!out) return fail(DP_EINVAL, "null out");
+  if (hip_runtimes_mapped() > 1 && !std::getenv("DPGPU_ALLOW_TWO_HIP_RUNTIMES"))
+    return fail(DP_ENOTSUP, "two HIP runtimes mapped in this process (load the one PyTorch bundles before "
+                            "libdpgpu.so, or none: DESIGN.md §5)");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0) return fail(DP_ENODEV, "no HIP device", e);
@@ -486,8 +527,8 @@ int dp_ctx_destroy(dp_ctx_t *c) {
     if (p) (void)hipHostFree(p);
   for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
   if (c->d_stats) (void)hipFree(c->d_stats);
-  if (c->acl_keys) (void)hipFree(c->acl_keys);
-  if (c->acl_res) (void)hipFree(c->acl_res);
+  if (c->cls_dev) (void)hipFree(c->cls_dev);
+  if (c->cls_host) (void)hipHostFree(c->cls_host);
   c->fl_ev.release();
   c->fl_sens.release();
   for (FlowScratch *x : {&c->pf_req, &c->pf_cnt, &c->pf_of, &c->pf_bits, &c->pf_order, &c->pf_repl, &c->mq_rel,
@@ -712,14 +753,21 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
     fc.lane_bits = fc.pf_bits ? fc.pf_bits + words + sum_words : nullptr;
     fc.lane_sum = fc.lane_bits ? fc.lane_bits + words : nullptr;
     fc.lane_order = static_cast<uint32_t *>(c->lane_order.get(sizeof(uint32_t) * ((uint64_t)n + 1)));
-    fc.lane_plan = static_cast<uint4 *>(c->lane_plan.get(128 * ((uint64_t)n + 1)));
-    fc.lane_res = static_cast<uint4 *>(c->lane_res.get(32 * ((uint64_t)n + 1)));
-    fc.lane_key = static_cast<uint4 *>(c->lane_key.get(48 * ((uint64_t)n + 1)));
+    // the masquerade split's lane scratch (208 B a packet) only for an image
+    // that configures masquerade; without it a masquerading record (a flow
+    // that kept masquerade state from an earlier configuration) sends the
+    // burst to the one-lane pass (pfw::nat_mode)
+    if (img->im.masq) {
+      fc.lane_plan = static_cast<uint4 *>(c->lane_plan.get(128 * ((uint64_t)n + 1)));
+      fc.lane_res = static_cast<uint4 *>(c->lane_res.get(32 * ((uint64_t)n + 1)));
+      fc.lane_key = static_cast<uint4 *>(c->lane_key.get(48 * ((uint64_t)n + 1)));
+    }
+    const bool lane_ok = !img->im.masq || (fc.lane_plan && fc.lane_res && fc.lane_key);
     fc.steady = static_cast<unsigned long long *>(c->steady.get(8 * ((uint64_t)n / 64 + 2)));
     fc.adm = static_cast<uint32_t *>(c->adm.get(sizeof(uint32_t) * ((uint64_t)n + 1)));
     fc.adm_blk = static_cast<uint32_t *>(c->adm_blk.get(sizeof(uint32_t) * 1024));
     if (!fc.events || !fc.sens || !fc.pf || !fc.pf_cnt || !fc.pf_of || !fc.pf_order || !fc.pf_repl || !fc.mq_rel ||
-        !fc.lane_order || !fc.lane_plan || !fc.lane_res || !fc.lane_key || !fc.steady || !fc.dup_tab || !fc.adm || !fc.adm_blk ||
+        !fc.lane_order || !lane_ok || !fc.steady || !fc.dup_tab || !fc.adm || !fc.adm_blk ||
         !fc.grp_tab || !fc.grp_head || !fc.grp_next || !fc.grp_list || !fc.repl ||
         c->pf_bits_n < words + sum_words) {
       (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
@@ -782,38 +830,69 @@ int dp_acl_classify_device(dp_ctx_t *c, const dp_acl_key_t *dev_keys, dp_acl_res
   return 0;
 }
 
+// A classifier over keys and results in host memory: the keys staged through
+// pinned memory onto the device, the lookups, the results back -- every copy
+// ordered on the context's stream, one synchronisation at the end.
+// `launch(dev_in, dev_out)` enqueues the lookups on the context's stream.
+static int classify_host(dp_ctx_t *c, const void *in, size_t in_bytes, void *out, size_t out_bytes,
+                         const std::function<int(const void *, void *)> &launch) {
+  (void)hipSetDevice(c->device);
+  hipError_t e;
+  const size_t in_al = (in_bytes + 255) & ~(size_t)255, need = in_al + out_bytes;
+  if (g_cls_copies.load(std::memory_order_relaxed) == 1) {
+    // the round-5 path: stream-ordered allocations, asynchronous copies
+    // to and from pageable memory
+    void *d = nullptr;
+    if ((e = hipMallocAsync(&d, need, c->stream)) != hipSuccess) return fail(DP_ENOMEM, "classify buffers", e);
+    int rc = 0;
+    if ((e = hipMemcpyAsync(d, in, in_bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+      rc = fail(DP_EIO, "classify keys copy", e);
+    if (!rc) rc = launch(d, (uint8_t *)d + in_al);
+    if (!rc && (e = hipMemcpyAsync(out, (uint8_t *)d + in_al, out_bytes, hipMemcpyDeviceToHost, c->stream)) !=
+                   hipSuccess)
+      rc = fail(DP_EIO, "classify results copy", e);
+    (void)hipFreeAsync(d, c->stream);
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess && !rc) rc = fail(DP_EIO, "classify", e);
+    return rc;
+  }
+  if (need > c->cls_cap) {
+    // (the context's stream first: an earlier lookup may still use them)
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return fail(DP_EIO, "classify", e);
+    if (c->cls_dev) (void)hipFree(c->cls_dev);
+    if (c->cls_host) (void)hipHostFree(c->cls_host);
+    c->cls_dev = c->cls_host = nullptr;
+    c->cls_cap = 0;
+    const size_t cap = std::max(need, (size_t)1 << 20);
+    if ((e = hipMalloc(&c->cls_dev, cap)) != hipSuccess || (e = hipHostMalloc(&c->cls_host, cap)) != hipSuccess)
+      return fail(DP_ENOMEM, "classify buffers", e);
+    c->cls_cap = cap;
+  }
+  uint8_t *hin = static_cast<uint8_t *>(c->cls_host), *din = static_cast<uint8_t *>(c->cls_dev);
+  // (the staging is the context's: nothing of an earlier call is in flight
+  // once this call's copies are enqueued behind it on the same stream -- but
+  // the host may only overwrite it after that call's results were read,
+  // which the synchronisation below guarantees)
+  std::memcpy(hin, in, in_bytes);
+  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return fail(DP_EIO, "classify keys copy", e);
+  int rc = launch(din, din + in_al);
+  if (!rc && (e = hipMemcpyAsync(hin + in_al, din + in_al, out_bytes, hipMemcpyDeviceToHost, c->stream)) !=
+                 hipSuccess)
+    rc = fail(DP_EIO, "classify results copy", e);
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess && !rc) rc = fail(DP_EIO, "classify", e);
+  if (!rc) std::memcpy(out, hin + in_al, out_bytes);
+  return rc;
+}
+
 int dp_acl_classify(dp_ctx_t *c, const dp_acl_key_t *keys, dp_acl_result_t *out, uint32_t n) {
   if (!c) return fail(DP_EINVAL, "null ctx");
   if (n == 0) return 0;
   if (!keys || !out) return fail(DP_EINVAL, "null keys / results");
-  (void)hipSetDevice(c->device);
-  hipError_t e;
-  if (n > c->acl_cap) {
-    // (the context's stream first: an earlier classify may still read them)
-    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return fail(DP_EIO, "ACL classify", e);
-    if (c->acl_keys) (void)hipFree(c->acl_keys);
-    if (c->acl_res) (void)hipFree(c->acl_res);
-    c->acl_keys = nullptr;
-    c->acl_res = nullptr;
-    c->acl_cap = 0;
-    const uint32_t cap = n < 4096 ? 4096 : n;
-    if ((e = hipMalloc((void **)&c->acl_keys, sizeof(dp_acl_key_t) * (size_t)cap)) != hipSuccess ||
-        (e = hipMalloc((void **)&c->acl_res, sizeof(dp_acl_result_t) * (size_t)cap)) != hipSuccess)
-      return fail(DP_ENOMEM, "ACL classify buffers", e);
-    c->acl_cap = cap;
-  }
-  // keys and results in pageable host memory: blocking copies, the results'
-  // after the context's stream has drained (an asynchronous copy into pageable
-  // memory was seen to leave `out` unwritten after the stream synchronised)
-  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return fail(DP_EIO, "ACL classify", e);
-  if ((e = hipMemcpy(c->acl_keys, keys, sizeof(dp_acl_key_t) * (size_t)n, hipMemcpyHostToDevice)) != hipSuccess)
-    return fail(DP_EIO, "ACL keys copy", e);
-  int rc = dp_acl_classify_device(c, c->acl_keys, c->acl_res, n, c->stream);
-  if (!rc && (e = hipStreamSynchronize(c->stream)) != hipSuccess) rc = fail(DP_EIO, "ACL classify", e);
-  if (!rc && (e = hipMemcpy(out, c->acl_res, sizeof(dp_acl_result_t) * (size_t)n, hipMemcpyDeviceToHost)) !=
-                 hipSuccess)
-    rc = fail(DP_EIO, "ACL results copy", e);
-  return rc;
+  return classify_host(c, keys, sizeof(dp_acl_key_t) * (size_t)n, out, sizeof(dp_acl_result_t) * (size_t)n,
+                       [&](const void *dk, void *dr) {
+                         return dp_acl_classify_device(c, static_cast<const dp_acl_key_t *>(dk),
+                                                       static_cast<dp_acl_result_t *>(dr), n, c->stream);
+                       });
 }
 
 int dp_acl_key_from_match(const uint8_t *match, uint32_t key_size, uint32_t stride, uint32_t n,
@@ -849,6 +928,88 @@ int dp_acl_classify_match(dp_ctx_t *c, const uint8_t *match, uint32_t key_size, 
   return dp_acl_classify(c, keys.data(), out, n);
 }
 
+namespace {
+int ff_classify_device(dp_ctx_t *c, const dp_ff_input_t *dev_in, dp_ff_result_t *dev_out, uint32_t n, int stage,
+                       void *stream) {
+  if (!c) return fail(DP_EINVAL, "null ctx");
+  if (n == 0) return 0;
+  if (!dev_in || !dev_out) return fail(DP_EINVAL, "null inputs / results");
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  reap(c);
+  auto img = current(c);
+  if (!img) return fail(DP_ENOTABLES, "no tables published");
+  if (dpk_ff_classify(img->dev, img->dev + img->im_off, dev_in, dev_out, n, stage, s))
+    return fail(DP_EIO, "flow-filter classify launch failed", hipGetLastError());
+  InFlight f;
+  f.img = img;
+  f.done = take_event(c);
+  if (f.done) (void)hipEventRecord(f.done, s);
+  c->inflight.push_back(std::move(f));
+  return 0;
+}
+int ff_classify_host(dp_ctx_t *c, const dp_ff_input_t *in, dp_ff_result_t *out, uint32_t n, int stage) {
+  if (!c) return fail(DP_EINVAL, "null ctx");
+  if (n == 0) return 0;
+  if (!in || !out) return fail(DP_EINVAL, "null inputs / results");
+  return classify_host(c, in, sizeof(dp_ff_input_t) * (size_t)n, out, sizeof(dp_ff_result_t) * (size_t)n,
+                       [&](const void *di, void *dr) {
+                         return ff_classify_device(c, static_cast<const dp_ff_input_t *>(di),
+                                                   static_cast<dp_ff_result_t *>(dr), n, stage, c->stream);
+                       });
+}
+}  // namespace
+
+int dp_ff_classify_device(dp_ctx_t *c, const dp_ff_input_t *dev_in, dp_ff_result_t *dev_out, uint32_t n,
+                          void *stream) {
+  return ff_classify_device(c, dev_in, dev_out, n, 0, stream);
+}
+
+int dp_ff_classify(dp_ctx_t *c, const dp_ff_input_t *in, dp_ff_result_t *out, uint32_t n) {
+  return ff_classify_host(c, in, out, n, 0);
+}
+
+int dp_ff_key_from_match(int table, const uint8_t *match, uint32_t key_size, uint32_t stride, uint32_t n,
+                         dp_ff_input_t *out) {
+  uint32_t al;
+  if (table == DP_FF_REMOTE && (key_size == DP_FF_REMOTE_KEY_V4 || key_size == DP_FF_REMOTE_KEY_V6))
+    al = key_size == DP_FF_REMOTE_KEY_V4 ? 4 : 16;
+  else if (table == DP_FF_LOCAL && (key_size == DP_FF_LOCAL_KEY_V4 || key_size == DP_FF_LOCAL_KEY_V6))
+    al = key_size == DP_FF_LOCAL_KEY_V4 ? 4 : 16;
+  else
+    return fail(DP_EINVAL, "flow-filter match key: remote 15 / 27, local 16 / 28 bytes");
+  if (stride < key_size) return fail(DP_EINVAL, "flow-filter match key stride shorter than the key");
+  if (n && (!match || !out)) return fail(DP_EINVAL, "null keys / output");
+  auto be32 = [](const uint8_t *b) { return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3]; };
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t *b = match + (size_t)i * stride;
+    dp_ff_input_t k{};
+    k.proto = b[0];
+    k.src_vni = be32(b + 1);
+    k.dst_vni = be32(b + 5);
+    k.src_family = k.dst_family = al == 4 ? 4 : 6;
+    const uint16_t port = (uint16_t)(b[9 + al] << 8 | b[10 + al]);
+    if (table == DP_FF_REMOTE) {  // RemoteKey: proto, src_vni, dst_vni (GateVni), dst_ip, dst_port
+      std::memcpy(k.dst, b + 9, al);
+      k.dport = port;
+    } else {  // LocalKey: proto, src_vni, dst_vni, src_ip, src_port, gate
+      std::memcpy(k.src, b + 9, al);
+      k.sport = port;
+      k.gate = b[11 + al];
+    }
+    out[i] = k;
+  }
+  return 0;
+}
+
+int dp_ff_classify_match(dp_ctx_t *c, int table, const uint8_t *match, uint32_t key_size, uint32_t stride,
+                         uint32_t n, dp_ff_result_t *out) {
+  if (!c) return fail(DP_EINVAL, "null ctx");
+  std::vector<dp_ff_input_t> in(n);
+  const int rc = dp_ff_key_from_match(table, match, key_size, stride, n, in.data());
+  if (rc || !n) return rc;
+  return ff_classify_host(c, in.data(), out, n, table);
+}
+
 int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
   if (!c) return fail(DP_EINVAL, "null ctx");
   if (ft && ft->device != c->device) return fail(DP_EINVAL, "flow table on another device");
@@ -871,7 +1032,7 @@ int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
 // allocating lane alone (no wave batches); 3 runs port-forwarding bursts
 // without room for every pair on one lane (no admission pass).
 void dpf_debug_nat_sequential(int on) {
-  g_nat_seq.store(on >= 1 && on <= 3 ? (uint32_t)on : 0u, std::memory_order_relaxed);
+  g_nat_seq.store(on >= 1 && on <= 4 ? (uint32_t)on : 0u, std::memory_order_relaxed);
 }
 // Test hook (not part of dpgpu.h): the context's last flows burst's NAT-pass
 // counters (dp_flow.h FlowCtx::pf_cnt: the mode that ran, the split pass's

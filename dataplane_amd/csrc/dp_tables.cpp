@@ -1105,6 +1105,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
     for (uint32_t i = 0; i < tabs[ti].n; i++) {
       const uint32_t m = tabs[ti].kind == 1 ? tabs[ti].r[i].action2 : tabs[ti].r[i].action;
       if (m == DP_NAT_PORT_FORWARDING || m == DP_NAT_MASQUERADE) im.snat = 1;
+      if (m == DP_NAT_MASQUERADE) im.masq = 1;
     }
   // the v6 window: the longest prefix (17..48 bits) holding every v6 rule
   // prefix of every classifier -- one site's rules share their top bits, and
@@ -1488,6 +1489,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   im.pf_rules = pfrecs.empty() ? ib.alloc(sizeof(PfRuleRec)) : ib.put(pfrecs);
   im.n_pf = (uint32_t)pfrecs.size();
   if (im.n_pf || d->n_masq) im.snat = 1;
+  if (d->n_masq) im.masq = 1;
 
   section("portfw");
   // --- masquerade exposes (nat/src/masquerade/): validated and kept with the

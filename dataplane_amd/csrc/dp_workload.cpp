@@ -682,6 +682,7 @@ extern "C" uint32_t dpw_sizeof(const char *name) {
       {"dp_port_range_t", sizeof(dp_port_range_t)}, {"dp_nat_range_t", sizeof(dp_nat_range_t)}, {"dp_portfw_rule_t", sizeof(dp_portfw_rule_t)},
       {"dp_masq_expose_t", sizeof(dp_masq_expose_t)}, {"dp_masq_claim_t", sizeof(dp_masq_claim_t)},
       {"dp_acl_key_t", sizeof(dp_acl_key_t)}, {"dp_acl_result_t", sizeof(dp_acl_result_t)},
+      {"dp_ff_input_t", sizeof(dp_ff_input_t)}, {"dp_ff_result_t", sizeof(dp_ff_result_t)},
       {"dp_tables_desc_t", sizeof(dp_tables_desc_t)}, {"dp_pkt_in_t", sizeof(dp_pkt_in_t)},
       {"dp_pkt_out_t", sizeof(dp_pkt_out_t)}, {"dp_pkt_meta_t", sizeof(dp_pkt_meta_t)},
       {"dp_flow_key_t", sizeof(dp_flow_key_t)},

@@ -228,6 +228,30 @@ class GpuPathNf:
                                                out.ctypes.data), "dp_acl_classify_match", self.lib)
         return out
 
+    def ff_classify(self, inputs: np.ndarray) -> np.ndarray:
+        """The flow-filter classifier alone (dp_ff_classify): A.FF_INPUT
+        records (LookupInput) -> A.FF_RESULT records (LookupResult) --
+        FlowFilterContext::lookup_batch, flow-filter/src/context/tables.rs:800-848."""
+        inputs = np.ascontiguousarray(np.atleast_1d(inputs), dtype=A.FF_INPUT)
+        out = np.zeros(len(inputs), dtype=A.FF_RESULT)
+        A.check(self.lib.dp_ff_classify(self.ctx, inputs.ctypes.data, out.ctypes.data, len(inputs)),
+                "dp_ff_classify", self.lib)
+        return out
+
+    def ff_classify_match(self, table: int, match: np.ndarray, key_size: int, stride: int = 0) -> np.ndarray:
+        """One table alone over the reference's key bytes (dp_ff_classify_match):
+        RemoteKey::as_key() (table A.FF_REMOTE, 15 / 27 bytes) or LocalKey::as_key()
+        (A.FF_LOCAL, 16 / 28 bytes), keys `stride` bytes apart (default: packed)."""
+        match = np.ascontiguousarray(match, dtype=np.uint8).reshape(-1)
+        stride = stride or key_size
+        n = len(match) // stride if len(match) >= key_size else 0
+        if n and (n - 1) * stride + key_size > len(match):
+            n -= 1
+        out = np.zeros(n, dtype=A.FF_RESULT)
+        A.check(self.lib.dp_ff_classify_match(self.ctx, table, match.ctypes.data, key_size, stride, n,
+                                              out.ctypes.data), "dp_ff_classify_match", self.lib)
+        return out
+
     def close(self) -> None:
         if self.ctx:
             self.lib.dp_ctx_destroy(self.ctx)

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define DPGPU_ABI_VERSION 6u
+#define DPGPU_ABI_VERSION 7u
 
 /* Bytes every frame must have in front of it (its own scratch, owned by the
  * packet).  Output headers are written in place into this headroom: VXLAN
@@ -519,6 +519,10 @@ uint32_t dp_abi_version(void);
 /* One context per worker thread (worker.rs:175 builds one pipeline per
  * worker); owns one HIP stream and the device-side staging scratch.  Tables
  * are shared by all contexts on the same device (refcounted image). */
+/* DP_ENOTSUP: the process maps two HIP runtimes (two copies of
+ * libamdhip64 / libhsa-runtime64 -- e.g. PyTorch's bundled one loaded after
+ * this library's); one runtime per process is required (DESIGN.md §5,
+ * INTEGRATION.md §6). */
 int dp_ctx_create(int device_ordinal, dp_ctx_t **out);
 int dp_ctx_destroy(dp_ctx_t *ctx);
 
@@ -673,6 +677,74 @@ int dp_acl_key_from_match(const uint8_t *match, uint32_t key_size, uint32_t stri
                           dp_acl_key_t *out);
 int dp_acl_classify_match(dp_ctx_t *ctx, const uint8_t *match, uint32_t key_size, uint32_t stride,
                           uint32_t n, dp_acl_result_t *out);
+
+/* ------------------------------------------------------------------------ */
+/* The flow-filter classifier alone (the narrower drop-in for */
+/* A13): FlowFilterContext::lookup_batch (flow-filter/src/context/tables.rs: */
+/* 800-848) over the published ff_remote_* / ff_local_* rules.  Per input,   */
+/* stage 1 matches the destination (RemoteKey: proto, src VNI, the GateVni   */
+/* dst_vni -- 0 for an ungated lookup --, destination, destination port)     */
+/* against the remote rules in priority order; on a hit, stage 2 matches the */
+/* source (LocalKey: proto, src VNI, the verdict's VPC, source, source port, */
+/* SourceGate) against the local rules (lookup_versioned, :854-915).  The    */
+/* outcome is LookupResult (:70-81): Route (the verdict's VPC and NAT mode,  */
+/* the source's NAT mode), SourceMiss (the verdict's VPC) or                 */
+/* DestinationMiss -- also for an input whose two addresses are of different */
+/* families.  Inputs are never reordered.                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct dp_ff_input {        /* LookupInput (tables.rs:88-97) */
+    uint32_t src_vni;               /* src_vpcd */
+    uint32_t dst_vni;               /* dst_vpcd: stage 1's GateVni (0: None, an ungated lookup) */
+    uint8_t src_family, dst_family; /* 4 or 6 each (IpAddr::V4 / V6) */
+    uint8_t proto;                  /* NextHeader */
+    uint8_t gate;                   /* SourceGate: 0 Ungated, 1 PortFwdReply */
+    uint16_t sport, dport;          /* ports; None is (0, 0) */
+    uint8_t pad[4];
+    uint8_t src[16], dst[16];       /* network byte order; v4 in the first 4 bytes */
+} dp_ff_input_t;                    /* 48 B */
+
+enum dp_ff_outcome { DP_FF_DESTINATION_MISS = 0, DP_FF_SOURCE_MISS = 1, DP_FF_ROUTE = 2 };
+typedef struct dp_ff_result {       /* LookupResult */
+    uint8_t outcome;                /* enum dp_ff_outcome */
+    uint8_t dst_nat;                /* Route: the verdict's NatMode (enum dp_nat_mode) */
+    uint8_t src_nat;                /* Route: the source's NatMode */
+    uint8_t pad;
+    uint32_t dst_vni;               /* Route / SourceMiss: the verdict's dst_vpcd */
+} dp_ff_result_t;                   /* 8 B */
+
+/* n inputs resident on the context's device (stream as in
+ * dp_process_burst_device; asynchronous there). */
+int dp_ff_classify_device(dp_ctx_t *ctx, const dp_ff_input_t *dev_in, dp_ff_result_t *dev_out,
+                          uint32_t n, void *stream);
+/* The same for inputs and results in host memory (synchronous). */
+int dp_ff_classify(dp_ctx_t *ctx, const dp_ff_input_t *in, dp_ff_result_t *out, uint32_t n);
+
+/* The two tables alone over the reference's own key bytes -- what the
+ * rte_acl classifiers behind lookup_batch are handed (AnyTable::lookup_batch,
+ * tables.rs:313-326; MatchKey::as_key_into's fields back to back, big-endian,
+ * match-action-derive/src/lib.rs:191-206):
+ *   table DP_FF_REMOTE, RemoteKey<I>: proto 1, src_vni 4, dst_vni (GateVni, 0
+ *     None) 4, destination 4 / 16, destination port 2 -- DP_FF_REMOTE_KEY_V4
+ *     (15) or DP_FF_REMOTE_KEY_V6 (27) bytes;
+ *   table DP_FF_LOCAL, LocalKey<I>: proto 1, src_vni 4, dst_vni 4, source 4 /
+ *     16, source port 2, gate (SourceGate) 1 -- DP_FF_LOCAL_KEY_V4 (16) or
+ *     DP_FF_LOCAL_KEY_V6 (28) bytes;
+ * keys `stride` bytes apart (>= key_size), the key size naming the family.
+ * dp_ff_key_from_match converts n of them to dp_ff_input_t (host code: no
+ * device, no context; a remote key leaves the source zero, a local key the
+ * destination); dp_ff_classify_match runs that table alone: per key
+ * DP_FF_ROUTE with the matching rule's action (remote: dst_vni + dst_nat;
+ * local: src_nat), else DP_FF_DESTINATION_MISS (remote) / DP_FF_SOURCE_MISS
+ * (local).  DP_EINVAL: another table, key size, stride < key_size. */
+enum dp_ff_table { DP_FF_REMOTE = 1, DP_FF_LOCAL = 2 };
+#define DP_FF_REMOTE_KEY_V4 15u
+#define DP_FF_REMOTE_KEY_V6 27u
+#define DP_FF_LOCAL_KEY_V4 16u
+#define DP_FF_LOCAL_KEY_V6 28u
+int dp_ff_key_from_match(int table, const uint8_t *match, uint32_t key_size, uint32_t stride, uint32_t n,
+                         dp_ff_input_t *out);
+int dp_ff_classify_match(dp_ctx_t *ctx, int table, const uint8_t *match, uint32_t key_size,
+                         uint32_t stride, uint32_t n, dp_ff_result_t *out);
 
 /* ------------------------------------------------------------------------ */
 /* Flow table: FlowTable                              */

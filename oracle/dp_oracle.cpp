@@ -3679,6 +3679,47 @@ int dpo_acl_classify(const dpo_tables_t *t, const dp_acl_key_t *keys, dp_acl_res
   return 0;
 }
 
+// The flow-filter classifier alone (dpgpu.h dp_ff_classify):
+// FlowFilterContext::lookup_batch (flow-filter/src/context/tables.rs:800-848,
+// lookup_versioned :854-915) -- per input, the remote rules in priority order
+// over (proto, src VNI, GateVni, destination, destination port), then on a
+// hit the local rules over (proto, src VNI, the verdict's VPC, source, source
+// port, SourceGate); addresses of different families: DestinationMiss.
+// stage: 0 both, 1 the remote rules alone, 2 the local rules alone (dst_vni
+// is then the local key's VPC), as dp_ff_classify_match runs them.
+int dpo_ff_classify(const dpo_tables_t *t, const dp_ff_input_t *in, dp_ff_result_t *out, uint32_t n, int stage) {
+  static const uint8_t zero16[16] = {0};
+  for (uint32_t i = 0; i < n; i++) {
+    const dp_ff_input_t &q = in[i];
+    dp_ff_result_t r{};
+    r.outcome = stage == 2 ? DP_FF_SOURCE_MISS : DP_FF_DESTINATION_MISS;
+    out[i] = r;
+    if (q.src_family != q.dst_family || (q.src_family != 4 && q.src_family != 6)) continue;
+    const int fam = q.src_family;
+    const auto &rem = fam == 4 ? t->ffr4 : t->ffr6;
+    const auto &loc = fam == 4 ? t->ffl4 : t->ffl6;
+    uint32_t dvni = q.dst_vni;
+    if (stage != 2) {
+      const Key k{q.proto, q.src_vni, q.dst_vni, 0, zero16, q.dst, 0, q.dport};
+      const int64_t ri = classify(rem, k, fam);
+      if (ri < 0) continue;
+      r.dst_vni = rem[ri].r.action;
+      r.dst_nat = (uint8_t)rem[ri].r.action2;
+      dvni = r.dst_vni;
+      r.outcome = stage == 1 ? DP_FF_ROUTE : DP_FF_SOURCE_MISS;
+      out[i] = r;
+      if (stage == 1) continue;
+    }
+    const Key k2{q.proto, q.src_vni, dvni, q.gate, q.src, zero16, q.sport, 0};
+    const int64_t li = classify(loc, k2, fam);
+    if (li < 0) continue;
+    r.src_nat = (uint8_t)loc[li].r.action;
+    r.outcome = DP_FF_ROUTE;
+    out[i] = r;
+  }
+  return 0;
+}
+
 int dpo_nat_lookup(const dpo_tables_t *t, uint32_t kind, uint32_t src_vni, uint32_t dst_vni,
                    const uint8_t *addr4, int has_port, uint16_t port, uint8_t *new_addr4,
                    uint16_t *new_port) {

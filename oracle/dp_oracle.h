@@ -99,6 +99,9 @@ int64_t dpo_acl_lookup(const dpo_tables_t *t, uint8_t family, uint8_t proto,
                        uint16_t dport);
 /* AclFilter's decision for each key (dpgpu.h dp_acl_classify). */
 int dpo_acl_classify(const dpo_tables_t *t, const dp_acl_key_t *keys, dp_acl_result_t *out, uint32_t n);
+// FlowFilterContext::lookup_batch (dpgpu.h dp_ff_classify); stage 0 both
+// tables, 1 the remote rules alone, 2 the local rules alone
+int dpo_ff_classify(const dpo_tables_t *t, const dp_ff_input_t *in, dp_ff_result_t *out, uint32_t n, int stage);
 /* Static NAT find_{src,dst}_mapping: returns 1 if mapped (new addr/port
  * written, port 0 = unchanged), 0 if not. kind: 0 dst, 1 src. */
 int dpo_nat_lookup(const dpo_tables_t *t, uint32_t kind, uint32_t src_vni,

@@ -41,6 +41,7 @@ def lib() -> C.CDLL:
                                      C.c_int, C.c_uint16, C.c_uint16]
         l.dpo_acl_lookup.restype = C.c_int64
         l.dpo_acl_classify.argtypes = [V, V, V, C.c_uint32]
+        l.dpo_ff_classify.argtypes = [V, V, V, C.c_uint32, C.c_int]
         l.dpo_nat_lookup.argtypes = [V, C.c_uint32, C.c_uint32, C.c_uint32, V, C.c_int,
                                      C.c_uint16, V, V]
         l.dpo_checksum_ipv4_header.argtypes = [V, C.c_uint32]
@@ -87,6 +88,15 @@ class Oracle:
         out = np.zeros(len(keys), dtype=A.ACL_RESULT)
         if lib().dpo_acl_classify(self.h, keys.ctypes.data, out.ctypes.data, len(keys)) != 0:
             raise RuntimeError("oracle acl_classify failed")
+        return out
+
+    def ff_classify(self, inputs: np.ndarray, stage: int = 0) -> np.ndarray:
+        """FlowFilterContext::lookup_batch per A.FF_INPUT record (dpgpu.h
+        dp_ff_classify); stage 1 / 2: the remote / local rules alone."""
+        inputs = np.ascontiguousarray(np.atleast_1d(inputs), dtype=A.FF_INPUT)
+        out = np.zeros(len(inputs), dtype=A.FF_RESULT)
+        if lib().dpo_ff_classify(self.h, inputs.ctypes.data, out.ctypes.data, len(inputs), stage) != 0:
+            raise RuntimeError("oracle ff_classify failed")
         return out
 
     def process(self, buf: np.ndarray, inp: np.ndarray, stats: bool = False):

@@ -179,6 +179,8 @@ def out_fields(fr: bytes) -> dict:
             f["isrc"] = str(ipaddress.ip_address(fr[e + 12:e + 16]))
             f["idst"] = str(ipaddress.ip_address(fr[e + 16:e + 20]))
             f["iid"], f["iseq"] = struct.unpack("!HH", fr[e + eihl + 4:e + eihl + 8])
+            # (an embedded TCP / UDP header: its ports)
+            f["isport"], f["idport"] = struct.unpack("!HH", fr[e + eihl:e + eihl + 4])
     return f
 
 
@@ -208,6 +210,9 @@ class Scenario:
     peers: Optional[list] = None
     real_ff: bool = False
     routes: Optional[dict] = None
+    # (overlay name, genid) -> TablesBuilder, instead of world(): the NAT
+    # composition scenarios (tests/golden/natcombo.py) lower whole overlays
+    build: Optional[Callable[[str, int], TablesBuilder]] = None
 
 
 def establish() -> List[Step]:  # establish_tcp_connection (test.rs:1651-1687)
@@ -437,14 +442,15 @@ GpuRunner = _PfGpuRunner
 def run_scenario(s: Scenario, r, on_step=None) -> List[str]:
     errs: List[str] = []
     now = 0
-    r.publish(world(s.overlay, 1, s.peers, s.real_ff, s.routes))
+    mk = s.build or (lambda ov, g: world(ov, g, s.peers, s.real_ff, s.routes))
+    r.publish(mk(s.overlay, 1))
     last = None            # (fields, dst_vni) of the previous delivered output
     saved: Dict[str, tuple] = {}
     for i, st in enumerate(s.steps):
         now += st.advance
         r.set_clock(now)
         if st.publish is not None:
-            r.publish(world(st.publish[0], st.publish[1], s.peers, s.real_ff, s.routes))
+            r.publish(mk(st.publish[0], st.publish[1]))
         if st.sweep:
             r.sweep(now)
         tag = f"{s.name} step {i}"
@@ -457,6 +463,8 @@ def run_scenario(s: Scenario, r, on_step=None) -> List[str]:
             if "flows" in e and ln != e["flows"]:
                 errs.append(f"{tag}: flows {ln} != {e['flows']}")
             continue
+        if callable(pkt):  # built from what earlier steps delivered
+            pkt = pkt(saved, last)
         if isinstance(pkt, tuple) and pkt[0] in (REPLY, "reply_of"):
             if pkt[0] == REPLY:
                 base, fset, fclr = last, pkt[1], pkt[2]
@@ -493,12 +501,15 @@ def run_scenario(s: Scenario, r, on_step=None) -> List[str]:
             on_step(i, res, buf, info)
         if "done" in e and done != e["done"]:
             errs.append(f"{tag}: done {done} != {e['done']}")
-        for k in ("src", "dst", "sport", "dport", "ident", "isrc", "idst", "iid", "iseq"):
+        for k in ("src", "dst", "sport", "dport", "ident", "isrc", "idst", "iid", "iseq", "isport",
+                  "idport"):
             if k in e and (out is None or out.get(k) != e[k]):
                 errs.append(f"{tag}: {k} {None if out is None else out.get(k)} != {e[k]}")
         if "dst_vni" in e and int(o["dst_vni"]) != e["dst_vni"]:
             errs.append(f"{tag}: dst_vni {int(o['dst_vni'])} != {e['dst_vni']}")
         if out is not None:
+            if "not_sport" in e and out["sport"] == e["not_sport"]:
+                errs.append(f"{tag}: sport {out['sport']} is the excluded {e['not_sport']}")
             if "ident_mod256" in e and out["ident"] % 256 != e["ident_mod256"]:
                 errs.append(f"{tag}: identifier {out['ident']} not the first of a block")
             if "sport_mod256" in e and out["sport"] % 256 != e["sport_mod256"]:
@@ -516,7 +527,7 @@ def run_scenario(s: Scenario, r, on_step=None) -> List[str]:
             for k in e.get("differs", ()):
                 if (out["src"], out["sport"]) == saved[k][:2]:
                     errs.append(f"{tag}: translation {(out['src'], out['sport'])} reuses {k}'s")
-        elif any(k in e for k in ("same", "differs", "src_net", "same_ident", "ident_next")):
+        elif any(k in e for k in ("same", "differs", "src_net", "same_ident", "ident_next", "not_sport")):
             errs.append(f"{tag}: not delivered ({done})")
         if "flow" in e and (info is not None and info["ref"] != A.FLOW_NONE) != e["flow"]:
             errs.append(f"{tag}: flow attached {info is not None} != {e['flow']}")

@@ -320,9 +320,9 @@ class GpuRunner:
         records on the allocating lane, [13] left there by connection lanes,
         [14] allocations in wave batches, [15] alone, [16] pairs refused."""
         import ctypes as C
-        out = (C.c_uint32 * 32)()
-        n = A.gpu_lib().dpf_debug_nat_counters(self.nf.ctx, out, 32)
-        assert n == 32, n
+        out = (C.c_uint32 * 40)()
+        n = A.gpu_lib().dpf_debug_nat_counters(self.nf.ctx, out, 40)
+        assert n == 40, n
         return np.array(out[:], dtype=np.uint32)
 
     def close(self):

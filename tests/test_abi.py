@@ -45,3 +45,45 @@ def test_ctx_create_without_gpu_fails_loudly():
     lib = A.gpu_lib()
     h = C.c_void_p()
     assert lib.dp_ctx_create(0, C.byref(h)) == -19  # DP_ENODEV
+
+
+_RUNTIME_PROBE = '''
+import ctypes as C, os, sys
+sys.path.insert(0, {root!r})
+{pre}
+from dataplane_amd import _abi as A
+lib = A.gpu_lib()
+import torch
+h = C.c_void_p()
+print(lib.dpd_debug_hip_runtimes(), lib.dp_ctx_create(0, C.byref(h)) if not torch.cuda.is_available() else 0)
+'''
+
+
+def _runtime_probe(pre: str, env: dict):
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", _RUNTIME_PROBE.format(root=ROOT, pre=pre)],
+                       env=dict(os.environ, **env), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return [int(x) for x in r.stdout.split()]
+
+
+def test_one_hip_runtime_per_process():
+    """libdpgpu.so loaded before PyTorch: the Python mirror maps PyTorch's
+    HIP runtime first, so one runtime serves both (DESIGN.md §5); either
+    import order gives one."""
+    n, rc = _runtime_probe("", {})
+    assert n == 1
+    n, rc = _runtime_probe("import torch", {})
+    assert n == 1
+
+
+def test_two_hip_runtimes_refused():
+    """Without that (the preload disabled, the library first), PyTorch maps a
+    second runtime beside the library's; dp_ctx_create refuses the process
+    (DP_ENOTSUP) before touching any device."""
+    n, rc = _runtime_probe("", {"DPGPU_NO_RUNTIME_PRELOAD": "1"})
+    assert n == 2
+    import torch
+    if not torch.cuda.is_available():
+        assert rc == -95  # DP_ENOTSUP
