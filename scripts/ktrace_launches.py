@@ -7,7 +7,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 KEYS = [("first", "dp_pipeline_kernel<true, false, false"), ("first", "dp_pipeline_kernel<true, true, false"),
-        ("mark", "dp_nat_mark"), ("prep", "dp_nat_prep"), ("resolve1", "dp_nat_resolve<true>"),
+        ("mark", "dp_nat_mark"), ("prep", "dp_nat_prep"), ("cross", "dp_nat_cross"), ("resolve1", "dp_nat_resolve<true>"),
         ("resolve", "dp_nat_resolve<false>"), ("plan", "dp_nat_lane_plan"), ("lane", "dp_nat_lane("),
         ("pairs", "dp_nat_pairs"), ("replay", "dp_pipeline_kernel<true, false, true"),
         ("replay", "dp_pipeline_kernel<true, true, true")]
@@ -27,5 +27,5 @@ for r in rows:
         k += 1
         span = (b - cur.pop("t0")) / 1e3
         print(f"{k:3d} span {span:8.1f} us  " + "  ".join(f"{x} {cur[x]:.1f}" for x in
-              ["first", "mark", "prep", "resolve1", "resolve", "plan", "lane", "pairs", "replay"] if x in cur))
+              ["first", "mark", "prep", "cross", "resolve1", "resolve", "plan", "lane", "pairs", "replay"] if x in cur))
         cur = None
