@@ -273,7 +273,8 @@ def nat_leg(dev, stream, steps: int, n: int, kind: str = "pf") -> dict:
         return {"mode": int(c[12]), "records": int(c[1]), "lane_records": int(c[11]),
                 "connections": int(c[4]), "left_by_connections": int(c[13]), "allocations_batched": int(c[14]),
                 "allocations_alone": int(c[15]), "lane_kticks": [int(c[19 + k]) for k in range(7)],
-                "allocation_steps": int(c[26]), "steady_refreshes": bool(c[27])}
+                "allocation_steps": int(c[26]), "steady_refreshes": bool(c[27]),
+                "bulk_served_lane_records": int(c[35]), "bulk_blocks": int(c[39])}
 
     def run(share, reps, one_lane=False, near_capacity=False):
         buf, inp, npf = W.burst(n, share, 0, kind=kind)

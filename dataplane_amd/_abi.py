@@ -400,6 +400,7 @@ def gpu_lib() -> C.CDLL:
         lib.dpf_debug_flows_full.argtypes = [C.c_int]
         lib.dpf_debug_last_lean.restype = C.c_int
         lib.dpf_debug_no_ctx.argtypes = [C.c_int]
+        lib.dpf_debug_replay_fork.argtypes = [C.c_int]
         if lib.dp_abi_version() != ABI_VERSION:
             raise RuntimeError("libdpgpu.so ABI version mismatch")
         _gpu = lib

@@ -158,7 +158,8 @@ struct FlowCtx {
   uint32_t *pf_sum;
   uint32_t *pf_order;
   uint32_t *pf_repl;    // (slot, old state, packet index, old mark) of each fill replaced
-  uint32_t replay;      // 1: the replay pass (packets pf_order[0..pf_cnt[1]))
+  uint32_t replay;      // the replay pass: 1 packets pf_order[0..pf_cnt[1]), 2 those off a masquerade
+                        // split's allocating lane, 3 the lane's (lane_order[0..pf_cnt[11]))
   // masquerade: the table's allocator (dp_masq.h; nullptr: none) and its
   // generation, the allocations of fills replaced in the burst (record,
   // port), released when the sequential pass ends
@@ -190,7 +191,13 @@ struct FlowCtx {
   // port-forwarding connections beside the split (dp_nat_mark, dp_nat_cross),
   // [31] a mixed burst's bound on the slots its inserts may add (dp_nat_prep),
   // [32] its creations' reverse keys registered, [33] masquerading records
-  // dp_nat_cross looked up, [34] of them found (test counters)
+  // dp_nat_cross looked up, [34] of them found (test counters).  The
+  // allocating lane's bulk serve (dp_nat_lane, dp_nat_lane_assign): [35] the
+  // lane records it served (the steps start after them), [36] the largest set
+  // an allocating record asks + 1, [37] the complement of the smallest, [38]
+  // an allocating record whose checks fail whatever the tuple or whose
+  // reverse key may equal its initial key (no bulk serve), [39] the blocks it
+  // logged
   unsigned long long *grp_tab, *grp_head, *grp_next;
   uint32_t *grp_list;
   uint32_t grp_mask;
@@ -200,7 +207,8 @@ struct FlowCtx {
   uint32_t rmask;
   uint32_t force_seq;   // test hook (dpf_debug_nat_sequential): 1 the one-lane NAT pass always,
                         // 2 the split pass with every allocation on the lane alone (no wave batches),
-                        // 3 no mode 4, 4 no mode 5 (a mixed burst on one lane)
+                        // 3 no mode 4, 4 no mode 5 (a mixed burst on one lane), 5 the
+                        // allocating lane without its bulk serve (every allocation in its steps)
   // the masquerading burst's allocating lane: its packets (bitmap by packet
   // index + summary, as pf_bits) and their order
   uint32_t *lane_bits, *lane_sum, *lane_order;

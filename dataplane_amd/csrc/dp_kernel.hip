@@ -3388,7 +3388,10 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   uint8_t *slab_wave = slab_all + (tid - lane) * SLAB;
   lds_u8 *slab = (lds_u8 *)(slab_all + tid * SLAB);
   // the replay pass (port forwarding, FL only): thread t finishes packet
-  // pf_order[t] of the records dp_nat_prep ordered
+  // pf_order[t] of the records dp_nat_prep ordered (fc.replay 1), of those
+  // off the allocating lane (2: a masquerade split's, pf_cnt[12] 3 or 5 --
+  // their decisions are dp_nat_resolve's, so this replay may run beside the
+  // lane), or packet lane_order[t] (3: the lane's records, after it)
   constexpr bool rep = FL && RP;
   // chunk after chunk of TPB packets (DP_PERSIST), else the workgroup's one
 #if DP_PERSIST
@@ -3403,11 +3406,19 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   if constexpr (FL) {
     // the replay grid is the burst's; workgroups past the replayed packets
     // leave at once (uniform per workgroup: before any barrier)
-    if (rep && chunk * TPB >= fc.pf_cnt[1]) return;
-    if (rep) {
-      live = i < fc.pf_cnt[1];
-      i = live ? fc.pf_order[i] : n;
+    if constexpr (rep) {
+      const bool split = fc.pf_cnt[12] == 3u || fc.pf_cnt[12] == 5u;
+      const bool lanes = fc.replay == 3;
+      const uint32_t cnt = !lanes ? fc.pf_cnt[1] : split ? fc.pf_cnt[11] : 0u;
+      if (chunk * TPB >= cnt) return;
+      live = i < cnt;
+      i = live ? (lanes ? fc.lane_order[i] : fc.pf_order[i]) : n;
       if (live) rp = fc.pf + fc.pf_of[i];
+      if (live && fc.replay == 2 && split && (rp->bits & dpf::kPqLane)) {
+        live = false;
+        i = n;
+        rp = nullptr;
+      }
     }
   }
   dp_pkt_in_t pin{};
@@ -5335,6 +5346,26 @@ __global__ void __launch_bounds__(256) dp_nat_lane_plan(const uint8_t *__restric
     }
     pfw::flag_wave(&fc.pf_cnt[28], rep);
     pfw::flag_wave(&fc.pf_cnt[29], (L.cls & 0xffu) == 1);
+    // what the lane's bulk serve needs (dp_nat_lane): per 64-record chunk its
+    // allocating records (adm[k / 64]; adm is free again once dp_bits_emit has
+    // run); burst-wide, the sets they ask (pf_cnt[36] the largest + 1,
+    // pf_cnt[37] the complement of the smallest) and whether one's checks fail
+    // whatever the tuple or its reverse key may equal its initial key ([38])
+    {
+      const bool c3 = (L.cls & 0xffu) == 3;
+      const uint64_t cm = __ballot(c3);
+      if (lane == 0 && b0 + 64 * wv < nl) fc.adm[(b0 >> 6) + wv] = (uint32_t)__popcll(cm);
+      pfw::flag_wave(&fc.pf_cnt[38], c3 && (L.m.sfail || L.m.eqp));
+      uint32_t hi = c3 ? L.m.set + 1 : 0u, lo = c3 ? ~L.m.set : 0u;
+      for (int o = 32; o > 0; o >>= 1) {
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+        lo = max(lo, (uint32_t)__shfl_xor((int)lo, o));
+      }
+      if (lane == 0 && cm) {
+        atomicMax(&fc.pf_cnt[36], hi);
+        atomicMax(&fc.pf_cnt[37], lo);
+      }
+    }
     if (has) {
       const uint4 *w = reinterpret_cast<const uint4 *>(&L);
       for (int x = 0; x < 8; x++) fc.lane_plan[8 * (uint64_t)k + x] = w[x];
@@ -5440,6 +5471,124 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
     lane_fence();
     __syncthreads();
   };
+  // A block of region reg_p to serve (by one lane): the cached one while it
+  // has free ports, else (the cached one written back first) the region's
+  // first address in use with free ports and its thread block, or for a
+  // record that keeps its port (keep: so no block dies on the way) the
+  // address's next block, as port_alloc opens it (its thread block full or
+  // gone: the first free block from current_alloc_index); anull: the
+  // record's allow_null (blocks at port 0 are never opened here)
+  auto seek = [&](uint32_t reg_p, bool hit, bool keep, bool anull) {
+    if (!hit) {
+      write_back();
+      s_a[10] = 0;
+      const dpm::Region &G = V.regions()[reg_p];
+      uint32_t a = dpm::kNone;
+      for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
+        if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
+      if (a != dpm::kNone && V.recs()[a].thread_block >= 0) {
+        const dpm::Addr &A = V.recs()[a];
+        const uint32_t tb = (uint32_t)A.thread_block;
+        if ((A.bflag[tb] & 2) && dpm::block_base(A, tb) != 0) {
+          const dpm::A128 aa = dpm::addr_of(V, A);
+          uint32_t w[4] = {0, 0, 0, 0};
+          if (G.fam == 4) w[0] = aa.w[3];
+          else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
+          if (pfw::unicast(G.fam, w)) cache_block(a, A, tb, reg_p, w, aa);
+        }
+      }
+    }
+    uint32_t fr = 0;
+    if (s_c[0])
+      for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~s_bm[k]);
+    if (!fr && keep) {
+      // the address's next block, as port_alloc opens it (its thread
+      // block full or gone: the first free block from
+      // current_alloc_index) for a record that keeps its port (so no
+      // block dies on the way).  The served block full on an address
+      // whose flags are cached: the region's first address with free
+      // ports is still that one if it has any (the addresses before
+      // it had none, and only this lane allocates), and the next
+      // block comes from the cached flags and order
+      bool opened = false;
+      const uint32_t a0 = s_c[2];
+      const bool cached = s_c[0] && s_a[10] == a0 + 1 && !s_a[9];
+      write_back();
+      if (cached && (s_a[0] > 0 || s_a[2] > 0)) {
+        const uint8_t *fl = reinterpret_cast<const uint8_t *>(s_flag);
+        const uint8_t *pm = reinterpret_cast<const uint8_t *>(s_perm);
+        uint32_t idx = dpm::kNone;
+        for (uint32_t k = 0; k < 256; k++) {
+          const uint32_t x = (s_a[3] + k) & 0xffu;
+          if (fl[x] & 1) { idx = x; break; }
+        }
+        if (idx != dpm::kNone && pm[idx] != 0) {
+          // block_new, from the cache, written through
+          dpm::Addr &A = V.recs()[a0];
+          const dpm::Region &G = V.regions()[reg_p];
+          dpm::A128 aa;
+          for (int k = 0; k < 4; k++) aa.w[k] = s_a[5 + k];
+          const uint32_t base = (uint32_t)pm[idx] << 8;
+          uint32_t bm[8];
+          dpm::block_init(V, G, aa, base, !anull, bm);
+          A.thread_block = (int32_t)idx;
+          A.cur = idx;
+          A.bflag[idx] = 2;
+          A.blive[idx] = 0;
+          A.usable = --s_a[0];
+          A.live_blocks = ++s_a[1];
+          if (!dpm::bm_full(bm)) A.nonfull = ++s_a[2];
+          for (int k = 0; k < 8; k++) { A.bm[idx][k] = bm[k]; s_bm[k] = bm[k]; }
+          reinterpret_cast<uint8_t *>(s_flag)[idx] = 2;
+          s_a[3] = idx;
+          s_a[4] = idx;
+          s_c[0] = 1; s_c[3] = base | idx; s_c[8] = 0; s_c[9] = 0;
+          for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~bm[k]);
+          opened = true;
+        }
+      }
+      if (!opened) {
+        s_a[10] = 0;
+        const dpm::Region &G = V.regions()[reg_p];
+        uint32_t a = dpm::kNone;
+        for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
+          if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
+        if (a != dpm::kNone) {
+          dpm::Addr &A = V.recs()[a];
+          const int32_t tb = A.thread_block;
+          const bool spent = tb < 0 || !(A.bflag[tb] & 2) || dpm::bm_full(A.bm[tb]);
+          uint32_t idx = dpm::kNone;
+          if (spent)
+            for (uint32_t k = 0; k < 256; k++) {
+              const uint32_t x = (A.cur + k) & 0xffu;
+              if (A.bflag[x] & 1) { idx = x; break; }
+            }
+          const dpm::A128 aa = dpm::addr_of(V, A);
+          uint32_t w[4] = {0, 0, 0, 0};
+          if (G.fam == 4) w[0] = aa.w[3];
+          else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
+          if (idx != dpm::kNone && dpm::block_base(A, idx) != 0 && pfw::unicast(G.fam, w)) {
+            A.thread_block = (int32_t)idx;
+            A.cur = idx;
+            dpm::block_new(V, a, idx, anull);
+            cache_block(a, A, idx, reg_p, w, aa);
+          }
+        }
+      }
+    }
+  };
+  // then, by the wave: a newly cached address's block flags and order
+  auto seek_flags = [&]() {
+    __syncthreads();
+    if (s_a[9] && s_c[0]) {
+      const dpm::Addr &A = V.recs()[s_c[2]];
+      s_flag[t] = reinterpret_cast<const uint32_t *>(A.bflag)[t];
+      s_perm[t] = reinterpret_cast<const uint32_t *>(A.perm)[t];
+      __syncthreads();
+      if (t == 0) s_a[9] = 0;
+      __syncthreads();
+    }
+  };
   // a record's full plan (the allocation alone, the pairs in the lane)
   auto plan_of = [&](uint32_t k) {
     pfw::LanePlan P;
@@ -5463,9 +5612,145 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   // for the counters [19..25] in units of 1024 ticks
   uint64_t tk[7] = {0, 0, 0, 0, 0, 0, 0}, t0 = clock64(), ta;
   uint32_t steps = 0;
+  // The bulk serve (post: no record alone, no initial key repeated; every
+  // allocating record of one set, none whose checks fail whatever the tuple
+  // or whose reverse key may equal its initial key).  Then the steps below
+  // hand the allocating records the set's first region's ports in packet
+  // order whatever the records are: the served block's lowest free ports
+  // first, block after block as they open them.  So the wave walks the blocks
+  // alone, logging per block its free ports and the allocation ranks it
+  // serves (adm: the chunks' allocating records, made a prefix, then the
+  // log), and dp_nat_lane_assign gives each record its port in parallel.
+  // Where no block is to be had that way, the record of the next rank
+  // allocates alone, as the steps would (a one-rank entry, or one without a
+  // port); with the log full, the steps take over from that record.
+  uint32_t kstart = 0;
+  if (post && fc.force_seq != 2 && fc.force_seq != 5 && !fc.pf_cnt[38] &&
+      (!fc.pf_cnt[36] || ~fc.pf_cnt[37] + 1u == fc.pf_cnt[36])) {
+    const uint32_t nch = (nl + 63) / 64;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nch; c0 += 64) {
+      const uint32_t v = c0 + t < nch ? fc.adm[c0 + t] : 0u;
+      uint32_t x = v;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (t >= o) x += y;
+      }
+      if (c0 + t < nch) fc.adm[c0 + t] = carry + x - v;
+      carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    }
+    const uint32_t total = carry;
+    if (t == 0) fc.adm[nch] = total;
+    lane_fence();
+    __syncthreads();
+    // the lane record of allocation rank r < total: in the last chunk whose
+    // prefix is at most r (adm[nch] = total), by the wave
+    auto rank_rec = [&](uint32_t r) {
+      uint32_t lo = 0, hi = nch;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (fc.adm[mid] <= r) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t k = 64 * lo + t;
+      const bool c3 = k < nl && (fc.lane_key[3 * (uint64_t)k].y & 0xffu) == 3;
+      const uint64_t cm = __ballot(c3);
+      const uint32_t j = r - fc.adm[lo], lo32 = (uint32_t)__popc((uint32_t)cm);
+      return 64 * lo + (j < lo32 ? nth_bit((uint32_t)cm, j) : 32 + nth_bit((uint32_t)(cm >> 32), j - lo32));
+    };
+    const uint32_t off = (nch + 1 + 15) & ~15u;
+    const uint32_t cap = fc.n + 1 > off ? (fc.n + 1 - off) / 16 : 0u;
+    uint32_t *blog = fc.adm + off;
+    uint32_t served = 0, ents = 0;
+    if (total) {
+      const uint32_t reg = V.setreg()[V.sets()[fc.pf_cnt[36] - 1].first_reg];
+      while (served < total && ents < cap) {
+        ta = clock64();
+        uint32_t f = 0;
+        const bool hit = s_c[0] && s_c[1] == reg;
+        if (hit && t < 8) f = ~s_bm[t];
+        if (!hit || !__ballot(f != 0)) {
+          if (t == 0) seek(reg, hit, true, false);
+          seek_flags();
+          f = s_c[0] && s_c[1] == reg && t < 8 ? ~s_bm[t] : 0u;
+        }
+        const uint32_t fc_n = (uint32_t)__popc(f);
+        uint32_t pre = fc_n;
+        for (int o = 1; o < 8; o <<= 1) {
+          const uint32_t v = (uint32_t)__shfl_up((int)pre, o);
+          if (t >= o) pre += v;
+        }
+        const uint32_t fr = (uint32_t)__builtin_amdgcn_readlane((int)pre, 7);
+        { const uint64_t x = clock64(); tk[4] += x - ta; ta = x; }
+        uint32_t *e = blog + 16 * (uint64_t)ents;
+        if (!fr) {
+          // alone, as resolve_masq allocates (on the allocator as it is): the
+          // entry's base all ones when the record gets no port
+          const uint32_t k = rank_rec(served);
+          flush();
+          if (t == 0) {
+            const pfw::LanePlan P = plan_of(k);
+            dpf::PfReq &Rk = fc.pf[P.rec];
+            uint32_t rec = 0, aport = 0, aip[4] = {0, 0, 0, 0};
+            bool got = false;
+            const uint32_t er = dpm::set_alloc(V, P.m.set, P.m.allow_null, rec, aport);
+            if (er != dpm::OK) {
+              Rk.mverdict = pfw::masq_done(er);
+            } else {
+              pfw::masq_aip(fc, Rk, rec, aip);
+              const uint32_t v = pfw::masq_post(Rk, P.m, aip, aport);
+              if (v) { dpm::release(V, rec, aport); Rk.mverdict = v; }
+              else got = true;
+            }
+            e[0] = served; e[1] = 1; e[2] = rec; e[3] = got ? aport & ~0xffu : 0xffffffffu;
+            for (int x = 0; x < 4; x++) e[4 + x] = aip[x];
+            for (int x = 0; x < 8; x++) e[8 + x] = got && x == (int)((aport & 0xffu) >> 5) ? 1u << (aport & 31) : 0u;
+            lone_n++;
+          }
+          lane_fence();
+          __syncthreads();
+          served++;
+          ents++;
+          { const uint64_t x = clock64(); tk[6] += x - ta; ta = x; }
+          continue;
+        }
+        const uint32_t taken = total - served < fr ? total - served : fr;
+        // the log entry: first rank, ranks served, address record, block
+        // base, the address, the block's free ports before
+        const uint32_t fw = (uint32_t)__shfl((int)f, t & 7);
+        uint32_t ev = 0;
+        if (t == 0) ev = served;
+        else if (t == 1) ev = taken;
+        else if (t == 2) ev = s_c[2];
+        else if (t == 3) ev = s_c[3] & ~0xffu;
+        else if (t < 8) ev = s_c[t];
+        else ev = fw;
+        if (t < 16) e[t] = ev;
+        // the block's bitmap after `taken` allocations: its lowest free ports
+        if (t < 8) {
+          const uint32_t below = pre - fc_n;
+          const uint32_t n = taken > below ? (taken - below < fc_n ? taken - below : fc_n) : 0u;
+          if (n) s_bm[t] = ~f | (n == fc_n ? f : f & ((1u << nth_bit(f, n)) - 1));
+        }
+        if (t == 0) { s_c[8] += taken; fast_n += taken; }
+        served += taken;
+        ents++;
+        steps++;
+        __syncthreads();
+        { const uint64_t x = clock64(); tk[5] += x - ta; ta = x; }
+      }
+    }
+    // the steps below start at the record of rank `served` (the log full)
+    kstart = served < total ? rank_rec(served) : nl;
+    if (t == 0) {
+      fc.pf_cnt[35] = kstart;
+      fc.pf_cnt[39] = ents;
+    }
+    t0 = clock64();
+  }
   uint4 N0, N1, N2;
-  key_of(0, N0, N1, N2);
-  for (uint32_t k0 = 0; k0 < nl; k0 += 64) {
+  key_of(kstart, N0, N1, N2);
+  for (uint32_t k0 = kstart; k0 < nl; k0 += 64) {
     const uint32_t cnt = nl - k0 < 64 ? nl - k0 : 64;
     const uint4 K0 = N0, K1 = N1, K2 = N2;
     if (k0 + 64 < nl) key_of(k0 + 64, N0, N1, N2);
@@ -5529,115 +5814,8 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         const bool hit = s_c[0] && s_c[1] == reg_p;
         if (hit && t < 8) f = ~s_bm[t];
         if ((!hit || !__ballot(f != 0)) && fc.force_seq != 2) {
-          if (t == p) {
-            if (!hit) {
-              write_back();
-              s_a[10] = 0;
-              const dpm::Region &G = V.regions()[reg_p];
-              uint32_t a = dpm::kNone;
-              for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
-                if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
-              if (a != dpm::kNone && V.recs()[a].thread_block >= 0) {
-                const dpm::Addr &A = V.recs()[a];
-                const uint32_t tb = (uint32_t)A.thread_block;
-                if ((A.bflag[tb] & 2) && dpm::block_base(A, tb) != 0) {
-                  const dpm::A128 aa = dpm::addr_of(V, A);
-                  uint32_t w[4] = {0, 0, 0, 0};
-                  if (G.fam == 4) w[0] = aa.w[3];
-                  else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
-                  if (pfw::unicast(G.fam, w)) cache_block(a, A, tb, reg_p, w, aa);
-                }
-              }
-            }
-            uint32_t fr = 0;
-            if (s_c[0])
-              for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~s_bm[k]);
-            if (!fr && !sfail) {
-              // the address's next block, as port_alloc opens it (its thread
-              // block full or gone: the first free block from
-              // current_alloc_index) for a record that keeps its port (so no
-              // block dies on the way).  The served block full on an address
-              // whose flags are cached: the region's first address with free
-              // ports is still that one if it has any (the addresses before
-              // it had none, and only this lane allocates), and the next
-              // block comes from the cached flags and order
-              bool opened = false;
-              const uint32_t a0 = s_c[2];
-              const bool cached = s_c[0] && s_a[10] == a0 + 1 && !s_a[9];
-              write_back();
-              if (cached && (s_a[0] > 0 || s_a[2] > 0)) {
-                const uint8_t *fl = reinterpret_cast<const uint8_t *>(s_flag);
-                const uint8_t *pm = reinterpret_cast<const uint8_t *>(s_perm);
-                uint32_t idx = dpm::kNone;
-                for (uint32_t k = 0; k < 256; k++) {
-                  const uint32_t x = (s_a[3] + k) & 0xffu;
-                  if (fl[x] & 1) { idx = x; break; }
-                }
-                if (idx != dpm::kNone && pm[idx] != 0) {
-                  // block_new, from the cache, written through
-                  dpm::Addr &A = V.recs()[a0];
-                  const dpm::Region &G = V.regions()[reg_p];
-                  dpm::A128 aa;
-                  for (int k = 0; k < 4; k++) aa.w[k] = s_a[5 + k];
-                  const uint32_t base = (uint32_t)pm[idx] << 8;
-                  uint32_t bm[8];
-                  dpm::block_init(V, G, aa, base, !((K0.y >> 17) & 1u), bm);
-                  A.thread_block = (int32_t)idx;
-                  A.cur = idx;
-                  A.bflag[idx] = 2;
-                  A.blive[idx] = 0;
-                  A.usable = --s_a[0];
-                  A.live_blocks = ++s_a[1];
-                  if (!dpm::bm_full(bm)) A.nonfull = ++s_a[2];
-                  for (int k = 0; k < 8; k++) { A.bm[idx][k] = bm[k]; s_bm[k] = bm[k]; }
-                  reinterpret_cast<uint8_t *>(s_flag)[idx] = 2;
-                  s_a[3] = idx;
-                  s_a[4] = idx;
-                  s_c[0] = 1; s_c[3] = base | idx; s_c[8] = 0; s_c[9] = 0;
-                  for (int k = 0; k < 8; k++) fr += (uint32_t)__popc(~bm[k]);
-                  opened = true;
-                }
-              }
-              if (!opened) {
-                s_a[10] = 0;
-                const dpm::Region &G = V.regions()[reg_p];
-                uint32_t a = dpm::kNone;
-                for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
-                  if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
-                if (a != dpm::kNone) {
-                  dpm::Addr &A = V.recs()[a];
-                  const int32_t tb = A.thread_block;
-                  const bool spent = tb < 0 || !(A.bflag[tb] & 2) || dpm::bm_full(A.bm[tb]);
-                  uint32_t idx = dpm::kNone;
-                  if (spent)
-                    for (uint32_t k = 0; k < 256; k++) {
-                      const uint32_t x = (A.cur + k) & 0xffu;
-                      if (A.bflag[x] & 1) { idx = x; break; }
-                    }
-                  const dpm::A128 aa = dpm::addr_of(V, A);
-                  uint32_t w[4] = {0, 0, 0, 0};
-                  if (G.fam == 4) w[0] = aa.w[3];
-                  else for (int k = 0; k < 4; k++) w[k] = aa.w[k];
-                  if (idx != dpm::kNone && dpm::block_base(A, idx) != 0 && pfw::unicast(G.fam, w)) {
-                    A.thread_block = (int32_t)idx;
-                    A.cur = idx;
-                    dpm::block_new(V, a, idx, (K0.y >> 17) & 1u);
-                    cache_block(a, A, idx, reg_p, w, aa);
-                  }
-                }
-              }
-            }
-          }
-          __syncthreads();
-          // a newly cached address: its block flags and order, by the wave
-          if (s_a[9] && s_c[0]) {
-            const dpm::Addr &A = V.recs()[s_c[2]];
-            s_flag[t] = reinterpret_cast<const uint32_t *>(A.bflag)[t];
-            s_perm[t] = reinterpret_cast<const uint32_t *>(A.perm)[t];
-            __syncthreads();
-            if (t == 0) s_a[9] = 0;
-            __syncthreads();
-          }
+          if (t == p) seek(reg_p, hit, !sfail, (K0.y >> 17) & 1u);
+          seek_flags();
           f = s_c[0] && s_c[1] == reg_p && t < 8 ? ~s_bm[t] : 0u;
         }
         // the block's free ports: per word (lanes 0..7) and before it
@@ -5763,6 +5941,51 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   if (t == 0) {
     fc.pf_cnt[15] += ln;
     if (v) atomicAdd(reinterpret_cast<unsigned long long *>(&fc.tmeta[2]), (unsigned long long)v);
+  }
+}
+
+// dp_nat_lane_assign: the lane's bulk-served records (lane records before
+// pf_cnt[35], dp_nat_lane) their allocations for dp_nat_pairs, in parallel:
+// an allocating record's rank (its chunk's prefix in adm, plus those before it
+// in the chunk) names the logged block serving it and its free port there --
+// the ranks a block serves take its lowest free ports in order.
+__global__ void __launch_bounds__(256) dp_nat_lane_assign(dpf::FlowCtx fc) {
+  if (!fc.pf_cnt[1] || !pfw::split_mode(pfw::nat_mode(fc))) return;
+  const uint32_t kend = fc.pf_cnt[35];
+  if (!kend) return;
+  const uint32_t nl = fc.pf_cnt[11], nch = (nl + 63) / 64, ents = fc.pf_cnt[39];
+  const uint32_t *blog = fc.adm + ((nch + 1 + 15) & ~15u);
+  const int lane = threadIdx.x & 63;
+  for (uint32_t b0 = blockIdx.x * 256; b0 < kend; b0 += gridDim.x * 256) {  // (uniform per block)
+    const uint32_t k = b0 + (threadIdx.x & ~63u) + lane;  // (a wave: one 64-record chunk)
+    const bool has = k < kend;
+    const uint32_t cls = has ? fc.lane_key[3 * (uint64_t)k].y & 0xffu : 0u;
+    const uint64_t cm = __ballot(cls == 3);
+    uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
+    if (cls == 3) {
+      const uint32_t rank = fc.adm[k >> 6] + (uint32_t)__popcll(cm & lanes_below(lane));
+      uint32_t lo = 0, hi = ents;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (blog[16 * (uint64_t)mid] <= rank) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t *e = blog + 16 * (uint64_t)lo;
+      if (e[3] != 0xffffffffu) {  // (else an allocation alone that got no port)
+        uint32_t j = rank - e[0], port = 0;
+        for (int w = 0; w < 8; w++) {
+          const uint32_t f = e[8 + w], c = (uint32_t)__popc(f);
+          if (j < c) { port = e[3] + 32 * w + nth_bit(f, j); break; }
+          j -= c;
+        }
+        r0 = make_uint4(1u, e[2], port, 0u);
+        r1 = make_uint4(e[4], e[5], e[6], e[7]);
+      }
+    }
+    if (has) {
+      fc.lane_res[2 * (uint64_t)k] = r0;
+      fc.lane_res[2 * (uint64_t)k + 1] = r1;
+    }
   }
 }
 
@@ -6281,7 +6504,8 @@ extern "C" int dpk_launch_pipeline(const uint8_t *img_base, const void *image_de
 extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                          dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
-                                         const void *fc_host, hipStream_t stream) {
+                                         const void *fc_host, hipStream_t stream, hipStream_t side,
+                                         hipEvent_t fork, hipEvent_t join, int fork_at) {
   if (n == 0) return 0;
   dpf::FlowCtx fc = *reinterpret_cast<const dpf::FlowCtx *>(fc_host);
   if (hipMemsetAsync(fc.events, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
@@ -6335,15 +6559,37 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   hipLaunchKernelGGL(dp_nat_admit_scan, dim3(ab), dim3(1024), 0, stream, fc, 2);
   hipLaunchKernelGGL(dp_nat_resolve<true>, dim3(1), dim3(64), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_resolve<false>, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
+  // The replay of the records off the allocating lane (every record but a
+  // masquerade split's lane records: dp_nat_resolve decided them) on the side
+  // stream, beside the lane -- forked after the resolve (fork_at 1) or after
+  // the lane's plan (2); then the lane's records after it.  Without a side
+  // stream, one replay of every record after the lane.
+  auto replay = [&](hipStream_t s, uint32_t which) {
+    fc.replay = which;
+    if (meta) dpk_run_pipeline_111(blocks, s, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+    else dpk_run_pipeline_101(blocks, s, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+  };
+  const bool forked = side && fork && join && (fork_at == 1 || fork_at == 2);
+  auto fork_off = [&]() {
+    if (hipEventRecord(fork, stream) != hipSuccess || hipStreamWaitEvent(side, fork, 0) != hipSuccess) return false;
+    replay(side, 2);
+    return hipEventRecord(join, side) == hipSuccess;
+  };
+  if (forked && fork_at == 1 && !fork_off()) return -5;
   // a masquerading burst's allocating lane (its records in packet order)
   order(1);
   hipLaunchKernelGGL(dp_nat_lane_plan, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
+  if (forked && fork_at == 2 && !fork_off()) return -5;
   hipLaunchKernelGGL(dp_nat_lane, dim3(1), dim3(64), 0, stream, img_base, im, fc);
+  hipLaunchKernelGGL(dp_nat_lane_assign, dim3(rb), dim3(256), 0, stream, fc);
   hipLaunchKernelGGL(dp_nat_pairs, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_lane_end, dim3(1), dim3(1), 0, stream, fc);
-  fc.replay = 1;
-  if (meta) dpk_run_pipeline_111(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
-  else dpk_run_pipeline_101(blocks, stream, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+  if (forked) {
+    if (hipStreamWaitEvent(stream, join, 0) != hipSuccess) return -5;
+    replay(stream, 3);
+  } else {
+    replay(stream, 1);
+  }
   }
   if (stats)
     hipLaunchKernelGGL(dp_stats_reduce, dim3(DP_DONE_COUNT), dim3(DPD_STAT_SLOTS), 0, stream, part,

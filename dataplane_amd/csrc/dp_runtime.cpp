@@ -53,7 +53,8 @@ extern "C" int dpk_stage_collect(const uint8_t *buf, const uint32_t *pos, const 
 extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *image_dev, uint8_t *buf,
                                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                          dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
-                                         const void *fc_host, hipStream_t stream);
+                                         const void *fc_host, hipStream_t stream, hipStream_t side,
+                                         hipEvent_t fork, hipEvent_t join, int fork_at);
 
 namespace {
 
@@ -170,6 +171,19 @@ std::atomic<uint32_t> g_nat_seq{0};  // dpf_debug_nat_sequential
 std::atomic<uint32_t> g_flows_full{0};  // dpf_debug_flows_full
 std::atomic<uint32_t> g_last_lean{0};   // dpf_debug_last_lean
 std::atomic<uint32_t> g_no_ctx{0};      // dpf_debug_no_ctx
+// where the NAT pass forks the replay of the records off the allocating lane
+// to the side stream: 0 never (one replay after the lane), 1 after the
+// resolve, 2 after the lane's plan (dpf_debug_replay_fork; DPGPU_REPLAY_FORK)
+std::atomic<int> g_replay_fork{-1};
+int replay_fork() {
+  int v = g_replay_fork.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("DPGPU_REPLAY_FORK");
+    v = e && *e >= '0' && *e <= '2' && !e[1] ? *e - '0' : 1;
+    g_replay_fork.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
 
 std::mutex g_dev_mu;
 std::map<int, std::unique_ptr<DeviceTables>> g_dev;
@@ -262,6 +276,11 @@ struct dp_ctx {
   uint64_t pf_bits_n = 0;
   hipEvent_t fl_used = nullptr;
   bool fl_armed = false;
+  // the NAT pass's side stream (lowest priority): the replay of the records
+  // off the allocating lane runs on it beside the lane (fork / join events)
+  hipStream_t side = nullptr;
+  hipEvent_t side_fork = nullptr, side_join = nullptr;
+  bool side_tried = false;
   uint64_t clock = 0;                  // dp_ctx_set_option(DP_OPT_CLOCK)
   // host threads of the staged-copy path, the context's own: a staged burst
   // waits for its own chunks only, never for another worker's
@@ -545,6 +564,9 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->mb_out) (void)hipHostFree(c->mb_out);
   if (c->mb_meta) (void)hipHostFree(c->mb_meta);
   if (c->fl_used) (void)hipEventDestroy(c->fl_used);
+  if (c->side) { (void)hipStreamSynchronize(c->side); (void)hipStreamDestroy(c->side); }
+  if (c->side_fork) (void)hipEventDestroy(c->side_fork);
+  if (c->side_join) (void)hipEventDestroy(c->side_join);
   for (auto &h : c->hs) if (h) { (void)hipStreamSynchronize(h); (void)hipStreamDestroy(h); }
   for (auto &e : c->hev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -773,8 +795,20 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
       (void)dpk_mark_failed(dev_in, dev_out, dev_meta, n, s);
       return fail(DP_ENOMEM, "flow burst scratch");
     }
+    const int fork_at = fc.lean ? 0 : replay_fork();
+    if (fork_at && !c->side_tried) {
+      // (made once; without it the replay runs after the lane, on `s`)
+      c->side_tried = true;
+      int lo = 0, hi = 0;
+      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
+      if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, lo) != hipSuccess ||
+          hipEventCreateWithFlags(&c->side_fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c->side_join, hipEventDisableTiming) != hipSuccess)
+        (void)hipGetLastError();
+    }
     rc = dpk_launch_pipeline_flows(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out,
-                                   dev_meta, n, dev_stats, part, &fc, s);
+                                   dev_meta, n, dev_stats, part, &fc, s, fork_at ? c->side : nullptr,
+                                   c->side_fork, c->side_join, fork_at);
     if (!rc) {
       if (!c->fl_used && hipEventCreateWithFlags(&c->fl_used, hipEventDisableTiming) != hipSuccess)
         return fail(DP_EIO, "hipEventCreate");
@@ -1030,9 +1064,11 @@ int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
 // in packet order (the parallel pass's reference in the parity tests and A/Bs);
 // 2 runs masquerading bursts' split pass with every allocation on the
 // allocating lane alone (no wave batches); 3 runs port-forwarding bursts
-// without room for every pair on one lane (no admission pass).
+// without room for every pair on one lane (no admission pass); 4 runs mixed
+// bursts on one lane (no mode 5); 5 runs the allocating lane without its bulk
+// serve (every allocation in the lane's steps).
 void dpf_debug_nat_sequential(int on) {
-  g_nat_seq.store(on >= 1 && on <= 4 ? (uint32_t)on : 0u, std::memory_order_relaxed);
+  g_nat_seq.store(on >= 1 && on <= 5 ? (uint32_t)on : 0u, std::memory_order_relaxed);
 }
 // Test hook (not part of dpgpu.h): the context's last flows burst's NAT-pass
 // counters (dp_flow.h FlowCtx::pf_cnt: the mode that ran, the split pass's
@@ -1051,6 +1087,10 @@ void dpf_debug_flows_full(int on) { g_flows_full.store(on ? 1u : 0u, std::memory
 // Test hook (not part of dpgpu.h): 1 runs the non-flow pipeline without the
 // LDS copy of the context tables even where they fit (A/Bs, parity of both).
 void dpf_debug_no_ctx(int on) { g_no_ctx.store(on ? 1u : 0u, std::memory_order_relaxed); }
+// Test hook (not part of dpgpu.h): where the NAT pass forks the replay off the
+// allocating lane (0 never, 1 after the resolve, 2 after the lane's plan;
+// -1 back to DPGPU_REPLAY_FORK / the default, 1).
+void dpf_debug_replay_fork(int at) { g_replay_fork.store(at >= 0 && at <= 2 ? at : -1, std::memory_order_relaxed); }
 // Test hook: 1 if the last flows burst launched ran the lean variant.
 int dpf_debug_last_lean() { return (int)g_last_lean.load(std::memory_order_relaxed); }
 

@@ -54,7 +54,11 @@ def test_gpu_masquerade_kat(s):
             same_info(io, ig, f"step {i}")
 
 
-NAT_MODES = {"split": 0, "one-lane": 1, "split-alone": 2}
+# (dpf_debug_nat_sequential, dpf_debug_replay_fork): the split pass with the
+# replay off the allocating lane forked after the resolve (the default), after
+# the lane's plan, or not forked (one replay after the lane)
+NAT_MODES = {"split": (0, 1), "split-fork-plan": (0, 2), "split-no-fork": (0, 0), "one-lane": (1, 1),
+             "split-alone": (2, 1), "split-steps": (5, 1)}
 
 
 @pytest.mark.parametrize("nat", list(NAT_MODES))
@@ -67,7 +71,9 @@ def test_gpu_masquerade_random_bursts(seed, n_conn, capacity, nat):
     with a small capacity, pairs refused at capacity; GPU == oracle per burst.
     nat: the masquerading bursts' split pass (connection lanes + the
     allocating lane with wave batches), the same with every allocation alone,
-    or the one-lane pass (the test hook dpf_debug_nat_sequential)."""
+    or the one-lane pass (the test hook dpf_debug_nat_sequential); the replay
+    of the records off the allocating lane beside it (forked at either point)
+    or after it (dpf_debug_replay_fork)."""
     import masqgen
     from golden.masqkat import GpuRunner, OracleRunner
     got, modes = {}, []
@@ -80,12 +86,14 @@ def test_gpu_masquerade_random_bursts(seed, n_conn, capacity, nat):
             if name == "gpu":
                 modes.append(r.nat_counters())
         if name == "gpu":
-            A.gpu_lib().dpf_debug_nat_sequential(NAT_MODES[nat])
+            A.gpu_lib().dpf_debug_nat_sequential(NAT_MODES[nat][0])
+            A.gpu_lib().dpf_debug_replay_fork(NAT_MODES[nat][1])
         try:
             masqgen.run(r, seed, n_conn, capacity, on)
         finally:
             if name == "gpu":
                 A.gpu_lib().dpf_debug_nat_sequential(0)
+                A.gpu_lib().dpf_debug_replay_fork(-1)
                 r.close()
         got[name] = steps
     hist = {}
@@ -119,8 +127,13 @@ def test_gpu_masquerade_random_bursts(seed, n_conn, capacity, nat):
         assert sum(int(c[11]) for c in modes) > 0
         if capacity is not None:
             assert any(int(c[18]) == int(c[11]) > 0 for c in modes)
-        elif nat == "split":
+        elif nat != "split-alone":
             assert sum(int(c[14]) for c in modes) > 0
+            # (these bursts mix closes, resets and repeats into the lane: the
+            # bulk serve rarely qualifies -- test_gpu_nat_scale covers it;
+            # with it off, the lane's steps serve every allocation)
+            if nat == "split-steps":
+                assert sum(int(c[39]) for c in modes) == 0
         else:
             assert sum(int(c[14]) for c in modes) == 0 and sum(int(c[15]) for c in modes) > 0
     if n_conn >= 3000:

@@ -68,6 +68,10 @@ def test_gpu_masquerade_at_scale():
         assert int(cnt[12]) == 3 and int(cnt[11]) == 250_000, cnt
         assert int(cnt[14]) > 200_000, cnt  # served in wave batches
         assert int(cnt[28]) == 0 and int(cnt[29]) == 0, cnt  # their pairs after the lane (dp_nat_pairs)
+        # the lane's bulk serve: blocks walked and logged, the ports given out
+        # in parallel (dp_nat_lane_assign); the steps take over only where a
+        # new address is opened
+        assert int(cnt[39]) > 0 and int(cnt[35]) > 0, cnt
         assert c.learn(ob, out) == 250_000
         keys = c.keys()
         assert same_flows(ro, rg, keys, "first packets") == 250_000
@@ -88,6 +92,7 @@ def test_gpu_masquerade_at_scale():
             out, ob, cnt = both(ro, rg, buf, inp, f"established burst {step}")
             assert hist(out) == {"Delivered": 300_000}
             assert int(cnt[12]) == 3, cnt
+            assert int(cnt[39]) > 0, cnt  # the bulk serve
         assert int(cnt[27]) == 1, cnt
         assert same_flows(ro, rg, keys, "established bursts") == 250_000
         # the same near the capacity: the allocating lane takes its records
