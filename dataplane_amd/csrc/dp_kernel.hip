@@ -4652,6 +4652,55 @@ __device__ void masq_steady_run(const dpf::FlowCtx &fc, const dpf::PfReq &Rc, dp
   d[2] = make_uint2(f.pf_ip[2], f.pf_ip[3]);
 }
 
+// A port-forwarding record whose refresh leaves its pair's state as it is
+// (round 6): no masquerade, no ACL flow verdict; attached to the fill it found,
+// Active, the pair whole (the two flows name each other) and valid for the
+// packet, with port-forwarding state whose rule still exists (by_id); a
+// NatFlowStatus the packet does not move (refresh_port_fw_entry, flow_state.
+// rs:216-264, with nw == cur, neither closed nor reset).  resolve_pf's outcome
+// for it is then a function of the pair as the burst found it -- if no other
+// record of the connection moves the state, and no creation of the burst
+// replaces a flow of the pair (both tag it: dp_nat_mark) -- and its writes (the
+// expiry pushed to the same value, the generation) commute with every other
+// record's.  Over copies of the record, its flow and the related one.
+__device__ bool pf_steady_v(const Img &g, const dpf::FlowCtx &fc, const dpf::PfReq &R, const dpf::FlowSlot &f,
+                            const dpf::FlowSlot &o) {
+  if ((R.bits & (dpf::kPqMasq | dpf::kPqPf | dpf::kPqSens)) != dpf::kPqPf) return false;
+  if (R.slot > fc.mask || f.state != R.state || R.status0 != DP_FLOW_ACTIVE) return false;
+  if (f.related > fc.mask || o.state != f.related_tag || o.related != R.slot || o.related_tag != f.state) return false;
+  if (f.mark <= R.idx || o.mark <= R.idx || !(f.flags & dpf::kFlagPf)) return false;
+  if (by_id(g, f.pf_rule) < 0) return false;
+  const uint32_t act = f.pf & 0xffu, cur = (f.pf >> 8) & 0xffu;
+  const uint32_t nw = next_status(R.bits & dpf::kPqTcp, R.proto >> 16, act, cur);
+  return nw == cur && nw != DP_NFS_CLOSED && nw != DP_NFS_RESET;
+}
+
+// resolve_pf for a steady record: the translation from its flow's state, the
+// expiry (every steady record of the flow writes the same value: a plain
+// store), the flow's generation; f: a copy of its flow
+__device__ void pf_steady_run(const Img &g, const dpf::FlowCtx &fc, const dpf::PfReq &Rc, dpf::PfReq &R,
+                              const dpf::FlowSlot &f) {
+  const int32_t e = by_id(g, f.pf_rule);  // (>= 0: rules do not change within a burst)
+  const uint32_t act = f.pf & 0xffu, cur = (f.pf >> 8) & 0xffu;
+  R.verdict = dpf::kPfForward;
+  R.acl_over = 0;
+  R.nat = act | (f.pf & 0xffff0000u);
+  for (int j = 0; j < 4; j++) R.nat_ip[j] = f.pf_ip[j];
+  const PfRuleRec &E = g.at<PfRuleRec>(g.im.pf_rules)[e];
+  const uint64_t nw = fc.now + (cur == DP_NFS_ESTABLISHED ? E.estab_ns : E.init_ns);
+  if (nw >= f.expires_at) fc.slots[Rc.slot].expires_at = nw;
+  if (f.genid != fc.genid) fc.slots[Rc.slot].genid = fc.genid;
+}
+
+// dp_nat_prep's half: the record's flow untagged (no record of the burst
+// moves or replaces its pair), then its refresh
+__device__ bool pf_steady_here(const Img &g, const dpf::FlowCtx &fc, const dpf::PfReq &Rc, dpf::PfReq &R) {
+  const dpf::FlowSlot f = load_slot(&fc.slots[Rc.slot]);
+  if (f.nat_tag == fc.burst) return false;
+  pf_steady_run(g, fc, Rc, R, f);
+  return true;
+}
+
 // Can a connection lane run this connection (the records of `list`)?  Every
 // record masquerades without port forwarding, is attached to one of the
 // pair's two flows (still the fills it attached) and was Active as the burst
@@ -4878,6 +4927,7 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
                                                    const Image *__restrict__ im, dpf::FlowCtx fc) {
   const uint32_t nrec = fc.pf_cnt[0];
   if (!nrec) return;
+  const Img g{img_base, *im};
   __shared__ uint32_t s_fl;
   if (threadIdx.x == 0) s_fl = 0;
   __syncthreads();
@@ -4894,14 +4944,31 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
       if (!(R.bits & dpf::kPqReached)) return false;
       if (R.bits & dpf::kPqPf) fl |= 1u;
       if (!(R.bits & dpf::kPqMasq)) {
-        // a port-forwarding record on a masqueraded pair (a creation replaces
-        // its flow): that pair's refreshes are not order-free
-        if (fc.mq && R.slot <= fc.mask) {
+        // a port-forwarding steady refresh (pfw::pf_steady_v); any other
+        // record tags the pair it is attached to -- a port-forwarding record
+        // on a masqueraded pair (a creation replaces its flow) too: that
+        // pair's refreshes are not order-free -- and a creation the pair whose
+        // reverse flow holds its reverse key (it replaces that flow)
+        if (R.slot <= fc.mask) {
           const dpf::FlowSlot f = pfw::load_slot(&fc.slots[R.slot]);
-          if (f.state == R.state && (f.flags & dpf::kFlagMasq)) {
+          if (f.state == R.state) {
+            dpf::FlowSlot o;
+            if (f.related <= fc.mask) o = pfw::load_slot(&fc.slots[f.related]);
+            else o.state = 0;
+            if (pfw::pf_steady_v(g, fc, R, f, o)) return true;
             fc.slots[R.slot].nat_tag = fc.burst;
-            if (f.related <= fc.mask && fc.slots[f.related].state == f.related_tag)
-              fc.slots[f.related].nat_tag = fc.burst;
+            if (f.related <= fc.mask && o.state == f.related_tag) fc.slots[f.related].nat_tag = fc.burst;
+          }
+        }
+        dpf::FKey rk;
+        if ((R.bits & dpf::kPqPf) && pfw::creation_rk(g, R, rk)) {
+          uint32_t st;
+          uint4 v, w;
+          const uint32_t z = flow_probe(fc, rk, st, v, w);
+          if (z != dpf::kNoSlot) {
+            fc.slots[z].nat_tag = fc.burst;
+            const uint32_t zr = fc.slots[z].related;
+            if (zr <= fc.mask && fc.slots[zr].state == fc.slots[z].related_tag) fc.slots[zr].nat_tag = fc.burst;
           }
         }
         return false;
@@ -4949,6 +5016,9 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
   const Img g{img_base, *im};
   const uint32_t mode0 = pfw::nat_mode(fc);  // (dp_nat_mark's flags decide it)
   const bool split = pfw::split_mode(mode0), mixed = mode0 == 5;
+  // (port-forwarding steady refreshes: the connection lanes' modes without
+  // admissions -- mode 4 counts its creations' slots over whole connections)
+  const bool pfsteady = mode0 == 2 || mode0 == 5;
   const unsigned long long tag = (unsigned long long)fc.burst << 32;
   __shared__ uint32_t s_fl;
   if (t == 0) s_fl = 0;
@@ -4998,6 +5068,13 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
         pfw::lane_mark(fc, R, 0u);
         return;
       }
+    } else if (pfsteady && ((fc.steady[rec >> 6] >> (rec & 63)) & 1u) &&
+               pfw::pf_steady_here(g, fc, Rc, R)) {
+      // a port-forwarding steady refresh whose pair no record moves: resolved
+      // here (the one-lane pass, should the burst fall back to it, runs it
+      // again in its order, to the same outcome)
+      fl |= 1u;
+      return;
     } else if (pfw::conn_key(g, fc, R, key, mixed)) {
       key |= pfw::kPfConnBit;
     } else {
@@ -5436,13 +5513,23 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   // block order (bflag, perm)
   __shared__ uint32_t s_a[11];
   __shared__ uint32_t s_flag[64], s_perm[64];
-  if (t == 0) { s_c[0] = 0; s_a[10] = 0; s_a[9] = 0; }
+  // the allocator's address records and regions (their offsets read once),
+  // and the claims of the region last opened a block in (kClaimsL of them at
+  // most; s_cl_n all ones: more, read from the allocator), for block_init
+  // (no allocator -- a configuration whose flow-filter rules still ask for
+  // masquerade -- and no record here allocates: nothing to read)
+  dpm::Addr *const RECS = fc.mq ? V.recs() : nullptr;
+  dpm::Region *const REGS = fc.mq ? V.regions() : nullptr;
+  constexpr uint32_t kClaimsL = 16;
+  __shared__ dpm::Claim s_cl[kClaimsL];
+  __shared__ uint32_t s_cl_reg, s_cl_n, s_cl_fam;
+  if (t == 0) { s_c[0] = 0; s_a[10] = 0; s_a[9] = 0; s_cl_reg = dpm::kNone; }
   __syncthreads();
   // the cached block back to the allocator (by the calling lane); the
   // address's counters stay cached
   auto write_back = [&]() {
     if (s_c[0]) {
-      dpm::Addr &A0 = V.recs()[s_c[2]];
+      dpm::Addr &A0 = RECS[s_c[2]];
       const uint32_t tb0 = s_c[3] & 0xffu;
       uint32_t full = 0xffffffffu;
       for (int x = 0; x < 8; x++) { A0.bm[tb0][x] = s_bm[x]; full &= s_bm[x]; }
@@ -5482,12 +5569,12 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
     if (!hit) {
       write_back();
       s_a[10] = 0;
-      const dpm::Region &G = V.regions()[reg_p];
+      const dpm::Region &G = REGS[reg_p];
       uint32_t a = dpm::kNone;
-      for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
-        if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
-      if (a != dpm::kNone && V.recs()[a].thread_block >= 0) {
-        const dpm::Addr &A = V.recs()[a];
+      for (uint32_t x = G.head; x != dpm::kNone; x = RECS[x].next)
+        if (dpm::has_free_ports(RECS[x])) { a = x; break; }
+      if (a != dpm::kNone && RECS[a].thread_block >= 0) {
+        const dpm::Addr &A = RECS[a];
         const uint32_t tb = (uint32_t)A.thread_block;
         if ((A.bflag[tb] & 2) && dpm::block_base(A, tb) != 0) {
           const dpm::A128 aa = dpm::addr_of(V, A);
@@ -5524,13 +5611,33 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         }
         if (idx != dpm::kNone && pm[idx] != 0) {
           // block_new, from the cache, written through
-          dpm::Addr &A = V.recs()[a0];
-          const dpm::Region &G = V.regions()[reg_p];
+          dpm::Addr &A = RECS[a0];
           dpm::A128 aa;
           for (int k = 0; k < 4; k++) aa.w[k] = s_a[5 + k];
           const uint32_t base = (uint32_t)pm[idx] << 8;
           uint32_t bm[8];
-          dpm::block_init(V, G, aa, base, !anull, bm);
+          if (s_cl_reg != reg_p) {
+            const dpm::Region &G = REGS[reg_p];
+            const uint32_t n = G.claim_n;
+            s_cl_fam = G.fam;
+            s_cl_n = n <= kClaimsL ? n : 0xffffffffu;
+            const dpm::Claim *C = V.claims() + G.claim_first;
+            for (uint32_t c = 0; c < n && c < kClaimsL; c++) s_cl[c] = C[c];
+            s_cl_reg = reg_p;
+          }
+          if (s_cl_n != 0xffffffffu) {
+            // dpm::block_init from the claims' copy
+            for (int k = 0; k < 8; k++) bm[k] = 0;
+            if (!anull && base == 0) bm[0] |= 1u;
+            for (uint32_t c = 0; c < s_cl_n; c++) {
+              const dpm::Claim &C = s_cl[c];
+              if (C.fam != s_cl_fam || !dpm::a_covers(C.net, C.len, C.fam, aa)) continue;
+              const uint32_t lo = C.lo > base ? C.lo : base, hi = C.hi < (base | 0xffu) ? C.hi : (base | 0xffu);
+              for (uint32_t q = lo; q <= hi && lo <= hi; q++) bm[(q - base) >> 5] |= 1u << ((q - base) & 31);
+            }
+          } else {
+            dpm::block_init(V, REGS[reg_p], aa, base, !anull, bm);
+          }
           A.thread_block = (int32_t)idx;
           A.cur = idx;
           A.bflag[idx] = 2;
@@ -5549,12 +5656,12 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
       }
       if (!opened) {
         s_a[10] = 0;
-        const dpm::Region &G = V.regions()[reg_p];
+        const dpm::Region &G = REGS[reg_p];
         uint32_t a = dpm::kNone;
-        for (uint32_t x = G.head; x != dpm::kNone; x = V.recs()[x].next)
-          if (dpm::has_free_ports(V.recs()[x])) { a = x; break; }
+        for (uint32_t x = G.head; x != dpm::kNone; x = RECS[x].next)
+          if (dpm::has_free_ports(RECS[x])) { a = x; break; }
         if (a != dpm::kNone) {
-          dpm::Addr &A = V.recs()[a];
+          dpm::Addr &A = RECS[a];
           const int32_t tb = A.thread_block;
           const bool spent = tb < 0 || !(A.bflag[tb] & 2) || dpm::bm_full(A.bm[tb]);
           uint32_t idx = dpm::kNone;
@@ -5581,7 +5688,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   auto seek_flags = [&]() {
     __syncthreads();
     if (s_a[9] && s_c[0]) {
-      const dpm::Addr &A = V.recs()[s_c[2]];
+      const dpm::Addr &A = RECS[s_c[2]];
       s_flag[t] = reinterpret_cast<const uint32_t *>(A.bflag)[t];
       s_perm[t] = reinterpret_cast<const uint32_t *>(A.perm)[t];
       __syncthreads();

@@ -1387,7 +1387,8 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
     for (uint32_t it; (it = next_item.fetch_add(1, std::memory_order_relaxed)) < item0[nch];) {
       while (item0[k + 1] <= it) k++;
       if (!landed[k].load(std::memory_order_acquire)) {
-        if (hipEventSynchronize(c->chunk_ev[k]) != hipSuccess) { werr = 1; continue; }
+        const hipError_t we = hipEventSynchronize(c->chunk_ev[k]);
+        if (we != hipSuccess) { werr = (int)we; continue; }
         landed[k].store(1, std::memory_order_release);
       }
       uint32_t first, cnt;
@@ -1416,7 +1417,7 @@ int dp_process_burst(dp_ctx_t *c, uint8_t *buf, uint64_t buf_bytes, const dp_pkt
   tr.done(n, T, nch);
   if (werr) {
     (void)hipStreamSynchronize(s);
-    return bail(DP_EIO, "chunk completion", hipSuccess);
+    return bail(DP_EIO, "chunk completion", (hipError_t)werr.load());
   }
   uint64_t hstats[DP_DONE_COUNT];
   if (stats && (e = hipMemcpyAsync(hstats, c->d_stats, sizeof(hstats), hipMemcpyDeviceToHost, s)) != hipSuccess) return bail(DP_EIO, "D2H stats", e);

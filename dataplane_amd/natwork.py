@@ -44,7 +44,7 @@ def tables(genid: int = 1) -> TB:
     return t
 
 
-def masq_tables(genid: int = 1) -> TB:
+def masq_tables(genid: int = 1, pool: str = "203.0.113.0/24") -> TB:
     """The masquerade world: VPC 100's clients (10.0.0.0/8) reach VPC 200's
     198.18.0.0/15 masqueraded behind the public pool 203.0.113.0/24 (256
     addresses, 64512 ports each: MasqueradeConfig, nat/src/masquerade/
@@ -60,7 +60,7 @@ def masq_tables(genid: int = 1) -> TB:
     t.add_route(t.add_fib(0), "0.0.0.0/0", nh)
     for v in (VPC_C, VPC_S, VPC_P):
         t.add_route(t.add_fib(v, vnis=[v]), "0.0.0.0/0", nh)
-    t.add_masquerade(VPC_C, VPC_S, ["10.0.0.0/8"], ["203.0.113.0/24"])
+    t.add_masquerade(VPC_C, VPC_S, ["10.0.0.0/8"], [pool])
     t.add_ff_remote(VPC_C, "198.18.0.0/15", VPC_S)
     t.add_ff_remote(VPC_C, "198.18.0.0/15", VPC_S, gate_vni=VPC_S)
     t.add_ff_local(VPC_C, VPC_S, "10.0.0.0/8", NAT_MASQUERADE)
@@ -69,13 +69,14 @@ def masq_tables(genid: int = 1) -> TB:
     return t
 
 
-def masq_world(genid: int = 1) -> TB:
+def masq_world(genid: int = 1, pool: str = "203.0.113.0/24") -> TB:
     """masq_tables with the way back: VPC 200's answers to the public pool
     (203.0.113.0/24, gated on VPC 100, requiring masquerade) reach VPC 100's
     clients -- the reference's lowering of a masquerading peering's return
-    direction (flow-filter/src/context/tables.rs:583-662)."""
-    t = masq_tables(genid)
-    t.add_ff_remote(VPC_S, "203.0.113.0/24", VPC_C, NAT_MASQUERADE, gate_vni=VPC_C)
+    direction (flow-filter/src/context/tables.rs:583-662).  `pool`: a part of
+    203.0.113.0/24 as the public pool instead (a small pool runs out)."""
+    t = masq_tables(genid, pool)
+    t.add_ff_remote(VPC_S, pool, VPC_C, NAT_MASQUERADE, gate_vni=VPC_C)
     t.add_ff_local(VPC_S, VPC_C, "198.18.0.0/15")
     return t
 

@@ -6,11 +6,11 @@ set -o pipefail
 mkdir -p gpurun_out/fork
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests/test_gpu_nat_scale.py tests/test_gpu_natmix.py tests/test_gpu_masquerade.py \
-  tests/test_gpu_portfw.py tests/test_gpu_natcombo.py -m gpu -x -v --timeout 300 --timeout-method thread \
+  tests/test_gpu_portfw.py tests/test_gpu_natcombo.py tests/test_gpu_flows.py -m gpu -x -v --timeout 300 --timeout-method thread \
   > gpurun_out/fork/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -60 gpurun_out/fork/pytest.log; exit 1; }
 echo PYTEST_OK
 grep -E "passed|failed" gpurun_out/fork/pytest.log | tail -2
-for F in ${FORKS:-2 0}; do
+for F in ${FORKS:-1 2 0}; do
   for K in masq mixed; do
     DPGPU_REPLAY_FORK=$F timeout -k 10 300 python bench.py --nat-only --nat-kind $K --steps 6 \
       > gpurun_out/fork/leg_${K}_$F.json 2> gpurun_out/fork/leg_${K}_$F.err \

@@ -110,6 +110,41 @@ def test_gpu_masquerade_at_scale():
         rg.close()
 
 
+def test_gpu_masquerade_bulk_runs_out():
+    """The allocating lane's bulk serve up to and past a pool's end: one public
+    address (64512 ports) for 70k first packets -- blocks walked and logged,
+    the address opened by an allocation alone, then every later record alone
+    and refused (NatOutOfResources) -- and a burst on the connections with 1 %
+    new ones (all refused); GPU == oracle, the bulk serve on and off."""
+    for force in (0, 5):
+        ro, rg = OracleRunner(), GpuRunner(slots=1 << 19)
+        A.gpu_lib().dpf_debug_nat_sequential(force)
+        try:
+            for r in (ro, rg):
+                r.publish(W.masq_world(pool="203.0.113.9/32"))
+                r.set_clock(10 ** 12)
+            c = W.MasqConns(70_000)
+            buf, inp = c.first()
+            out, ob, cnt = both(ro, rg, buf, inp, f"first packets ({force})")
+            h = hist(out)
+            assert h.get("NatOutOfResources", 0) == 70_000 - 64_512 and h["Delivered"] == 64_512, h
+            assert int(cnt[12]) == 3 and int(cnt[11]) == 70_000, cnt
+            assert (int(cnt[39]) > 0) == (force == 0), cnt
+            learnt = c.learn(ob, out)
+            assert learnt == 64_512
+            keys = c.keys()
+            assert same_flows(ro, rg, keys, f"first packets ({force})") == 64_512
+            for r in (ro, rg):
+                r.set_clock(10 ** 12 + 10 ** 9)
+            buf, inp, nn = c.burst(100_000, 0.01, 0.6, step=1)
+            out, ob, cnt = both(ro, rg, buf, inp, f"burst ({force})")
+            assert hist(out).get("NatOutOfResources", 0) >= nn, hist(out)
+            assert same_flows(ro, rg, keys, f"burst ({force})") == 64_512
+        finally:
+            A.gpu_lib().dpf_debug_nat_sequential(0)
+            rg.close()
+
+
 @pytest.mark.parametrize("case", ["room", "near-capacity", "near-capacity-one-lane", "full"])
 def test_gpu_portfw_at_scale(case):
     """270k new port-forwarded connections: with room (one lane per
