@@ -121,6 +121,8 @@ constexpr uint32_t kPqQuery = 1u << 12;   // its flow key is an ICMP query's (ec
 // already ran (its connection's lane left it there)
 constexpr uint32_t kPqLane = 1u << 13;
 constexpr uint32_t kPqPfDone = 1u << 14;
+// a steady refresh dp_nat_prep resolved in place (its replay may start then)
+constexpr uint32_t kPqSteady = 1u << 15;
 constexpr uint32_t kPfForward = 0xffu;
 
 // words of FlowCtx::pf_cnt
@@ -158,8 +160,9 @@ struct FlowCtx {
   uint32_t *pf_sum;
   uint32_t *pf_order;
   uint32_t *pf_repl;    // (slot, old state, packet index, old mark) of each fill replaced
-  uint32_t replay;      // the replay pass: 1 packets pf_order[0..pf_cnt[1]), 2 those off a masquerade
-                        // split's allocating lane, 3 the lane's (lane_order[0..pf_cnt[11]))
+  uint32_t replay;      // the replay pass: 1 packets pf_order[0..pf_cnt[1]), 4 the steady refreshes
+                        // among them (kPqSteady), 2 the others off a masquerade split's allocating
+                        // lane, 3 the lane's (lane_order[0..pf_cnt[11]))
   // masquerade: the table's allocator (dp_masq.h; nullptr: none) and its
   // generation, the allocations of fills replaced in the burst (record,
   // port), released when the sequential pass ends
@@ -208,7 +211,8 @@ struct FlowCtx {
   uint32_t force_seq;   // test hook (dpf_debug_nat_sequential): 1 the one-lane NAT pass always,
                         // 2 the split pass with every allocation on the lane alone (no wave batches),
                         // 3 no mode 4, 4 no mode 5 (a mixed burst on one lane), 5 the
-                        // allocating lane without its bulk serve (every allocation in its steps)
+                        // allocating lane without its bulk serve (every allocation in its steps),
+                        // 6 its bulk serve with every block opened by one lane
   // the masquerading burst's allocating lane: its packets (bitmap by packet
   // index + summary, as pf_bits) and their order
   uint32_t *lane_bits, *lane_sum, *lane_order;

@@ -3390,8 +3390,10 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
   // the replay pass (port forwarding, FL only): thread t finishes packet
   // pf_order[t] of the records dp_nat_prep ordered (fc.replay 1), of those
   // off the allocating lane (2: a masquerade split's, pf_cnt[12] 3 or 5 --
-  // their decisions are dp_nat_resolve's, so this replay may run beside the
-  // lane), or packet lane_order[t] (3: the lane's records, after it)
+  // their decisions are dp_nat_resolve's or dp_nat_prep's, so this replay may
+  // run beside the lane), of the steady refreshes dp_nat_prep resolved (4:
+  // beside dp_nat_resolve and the lane) and then the rest off the lane (5),
+  // or packet lane_order[t] (3: the lane's records, after it)
   constexpr bool rep = FL && RP;
   // chunk after chunk of TPB packets (DP_PERSIST), else the workgroup's one
 #if DP_PERSIST
@@ -3414,10 +3416,15 @@ dp_pipeline_kernel(const uint8_t *__restrict__ img_base, const Image *__restrict
       live = i < cnt;
       i = live ? (lanes ? fc.lane_order[i] : fc.pf_order[i]) : n;
       if (live) rp = fc.pf + fc.pf_of[i];
-      if (live && fc.replay == 2 && split && (rp->bits & dpf::kPqLane)) {
-        live = false;
-        i = n;
-        rp = nullptr;
+      if (live && fc.replay != 1 && fc.replay != 3) {
+        const uint32_t b = rp->bits;
+        const bool keep = fc.replay == 4 ? (b & dpf::kPqSteady) != 0
+                                         : !(fc.replay == 5 && (b & dpf::kPqSteady)) && !(split && (b & dpf::kPqLane));
+        if (!keep) {
+          live = false;
+          i = n;
+          rp = nullptr;
+        }
       }
     }
   }
@@ -4698,6 +4705,7 @@ __device__ bool pf_steady_here(const Img &g, const dpf::FlowCtx &fc, const dpf::
   const dpf::FlowSlot f = load_slot(&fc.slots[Rc.slot]);
   if (f.nat_tag == fc.burst) return false;
   pf_steady_run(g, fc, Rc, R, f);
+  R.bits = Rc.bits | dpf::kPqSteady;
   return true;
 }
 
@@ -5060,6 +5068,7 @@ __global__ void __launch_bounds__(1024) dp_nat_prep(const uint8_t *__restrict__ 
         if (f.nat_tag != fc.burst) {
           fl |= 1u;
           pfw::masq_steady_run(fc, Rc, R, f);
+          R.bits = Rc.bits | dpf::kPqSteady;
           return;
         }
       }
@@ -5460,10 +5469,16 @@ __global__ void __launch_bounds__(256) dp_nat_lane_plan(const uint8_t *__restric
   }
 }
 
-// The allocating lane is one workgroup: its lanes' stores and later loads
-// need workgroup-scope order only (an agent-scope fence would write back and
-// invalidate the XCD's L2 every time)
-__device__ __forceinline__ void lane_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+// The allocating lane is one wave (a 64-work-item workgroup): a wave's memory
+// operations are performed in order, so its lanes' stores and later loads
+// need wavefront-scope order only -- a compiler barrier, no wait.  (A
+// workgroup-scope fence or __syncthreads waits for every store the wave has
+// in flight to be acknowledged: ~1 us each, three per block served.)
+__device__ __forceinline__ void lane_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+__device__ __forceinline__ void lane_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // dp_nat_lane: the split pass's allocating lane (mode 3), one wave over its
 // records in packet order, 64 at a time (dp_nat_lane_plan's chunks).  A
@@ -5524,7 +5539,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   __shared__ dpm::Claim s_cl[kClaimsL];
   __shared__ uint32_t s_cl_reg, s_cl_n, s_cl_fam;
   if (t == 0) { s_c[0] = 0; s_a[10] = 0; s_a[9] = 0; s_cl_reg = dpm::kNone; }
-  __syncthreads();
+  lane_sync();
   // the cached block back to the allocator (by the calling lane); the
   // address's counters stay cached
   auto write_back = [&]() {
@@ -5556,7 +5571,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   auto flush = [&]() {
     if (t == 0) { write_back(); s_a[10] = 0; }  // (what runs next changes the allocator itself)
     lane_fence();
-    __syncthreads();
+    lane_sync();
   };
   // A block of region reg_p to serve (by one lane): the cached one while it
   // has free ports, else (the cached one written back first) the region's
@@ -5686,15 +5701,86 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
   };
   // then, by the wave: a newly cached address's block flags and order
   auto seek_flags = [&]() {
-    __syncthreads();
+    lane_sync();
     if (s_a[9] && s_c[0]) {
       const dpm::Addr &A = RECS[s_c[2]];
       s_flag[t] = reinterpret_cast<const uint32_t *>(A.bflag)[t];
       s_perm[t] = reinterpret_cast<const uint32_t *>(A.perm)[t];
-      __syncthreads();
+      lane_sync();
       if (t == 0) s_a[9] = 0;
-      __syncthreads();
+      lane_sync();
     }
+  };
+  // seek's common case for the bulk serve, by the whole wave: the served
+  // block full, the address's block flags and the region's claims cached --
+  // the block written back and the address's next block opened from the
+  // cache (the first free block from current_alloc_index, its bitmap a word
+  // per lane), as seek's cached path does.  false: nothing done (seek runs).
+  auto open_next = [&](uint32_t reg) -> bool {
+    if (!s_c[0] || s_c[1] != reg || s_a[10] != s_c[2] + 1 || s_a[9]) return false;
+    if (s_cl_reg != reg || s_cl_n == 0xffffffffu) return false;
+    const uint32_t a0 = s_c[2], tb0 = s_c[3] & 0xffu, taken = s_c[8];
+    // (the served block is full: its write-back drops the not-full count
+    // when this visit filled it)
+    const uint32_t nf = s_a[2] - (taken ? 1u : 0u);
+    if (!(s_a[0] > 0 || nf > 0)) return false;
+    const uint8_t *fl = reinterpret_cast<const uint8_t *>(s_flag);
+    const uint8_t *pm = reinterpret_cast<const uint8_t *>(s_perm);
+    const uint32_t cur = s_a[3];
+    uint32_t idx = dpm::kNone;
+    for (uint32_t k0 = 0; k0 < 256 && idx == dpm::kNone; k0 += 64) {
+      const uint64_t m = __ballot(fl[(cur + k0 + t) & 0xffu] & 1);
+      if (m) idx = (cur + k0 + (uint32_t)__ffsll((long long)m) - 1) & 0xffu;
+    }
+    if (idx == dpm::kNone || pm[idx] == 0) return false;
+    const uint32_t base = (uint32_t)pm[idx] << 8;
+    // the new block's bitmap (dpm::block_init: the claims covering the
+    // address; base != 0, so no null port), word t on lane t < 8
+    uint32_t w = 0;
+    if (t < 8) {
+      dpm::A128 aa;
+      for (int k = 0; k < 4; k++) aa.w[k] = s_a[5 + k];
+      const uint32_t wlo = base + 32u * t, whi = wlo + 31u;
+      for (uint32_t c = 0; c < s_cl_n; c++) {
+        const dpm::Claim &C = s_cl[c];
+        if (C.fam != s_cl_fam || !dpm::a_covers(C.net, C.len, C.fam, aa)) continue;
+        const uint32_t lo = C.lo > wlo ? C.lo : wlo, hi = C.hi < whi ? C.hi : whi;
+        if (lo <= hi) {
+          const uint32_t nb = hi - lo + 1;
+          w |= (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u)) << (lo - wlo);
+        }
+      }
+    }
+    const bool full = __ballot(t < 8 && w == 0xffffffffu) == 0xffull;
+    dpm::Addr &A = RECS[a0];
+    if (t < 8) {
+      A.bm[tb0][t] = s_bm[t];  // (write_back)
+      A.bm[idx][t] = w;
+    }
+    if (t == 0) {
+      A.blive[tb0] = (uint16_t)(s_c[9] + taken);
+      A.thread_block = (int32_t)idx;
+      A.cur = idx;
+      A.bflag[idx] = 2;
+      A.blive[idx] = 0;
+      A.usable = s_a[0] - 1;
+      A.live_blocks = s_a[1] + 1;
+      if (!full) A.nonfull = nf + 1;
+      else if (taken) A.nonfull = nf;
+    }
+    lane_sync();
+    if (t < 8) s_bm[t] = w;
+    if (t == 0) {
+      s_a[0] -= 1;
+      s_a[1] += 1;
+      s_a[2] = full ? nf : nf + 1;
+      reinterpret_cast<uint8_t *>(s_flag)[idx] = 2;
+      s_a[3] = idx;
+      s_a[4] = idx;
+      s_c[0] = 1; s_c[3] = base | idx; s_c[8] = 0; s_c[9] = 0;
+    }
+    lane_sync();
+    return true;
   };
   // a record's full plan (the allocation alone, the pairs in the lane)
   auto plan_of = [&](uint32_t k) {
@@ -5749,7 +5835,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
     const uint32_t total = carry;
     if (t == 0) fc.adm[nch] = total;
     lane_fence();
-    __syncthreads();
+    lane_sync();
     // the lane record of allocation rank r < total: in the last chunk whose
     // prefix is at most r (adm[nch] = total), by the wave
     auto rank_rec = [&](uint32_t r) {
@@ -5777,8 +5863,10 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         const bool hit = s_c[0] && s_c[1] == reg;
         if (hit && t < 8) f = ~s_bm[t];
         if (!hit || !__ballot(f != 0)) {
-          if (t == 0) seek(reg, hit, true, false);
-          seek_flags();
+          if (!(hit && fc.force_seq != 6 && open_next(reg))) {
+            if (t == 0) seek(reg, hit, true, false);
+            seek_flags();
+          }
           f = s_c[0] && s_c[1] == reg && t < 8 ? ~s_bm[t] : 0u;
         }
         const uint32_t fc_n = (uint32_t)__popc(f);
@@ -5815,7 +5903,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
             lone_n++;
           }
           lane_fence();
-          __syncthreads();
+          lane_sync();
           served++;
           ents++;
           { const uint64_t x = clock64(); tk[6] += x - ta; ta = x; }
@@ -5843,7 +5931,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
         served += taken;
         ents++;
         steps++;
-        __syncthreads();
+        lane_sync();
         { const uint64_t x = clock64(); tk[5] += x - ta; ta = x; }
       }
     }
@@ -5977,7 +6065,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
           }
           if (t == 0) s_c[8] += taken;
           if (t == p) fast_n += taken;
-          __syncthreads();
+          lane_sync();
           { const uint64_t x = clock64(); tk[5] += x - ta; ta = x; }
         } else {
           // alone, as resolve_masq allocates (on the allocator as it is)
@@ -5997,7 +6085,7 @@ __global__ void __launch_bounds__(64) dp_nat_lane(const uint8_t *__restrict__ im
             lone_n++;
           }
           lane_fence();
-          __syncthreads();
+          lane_sync();
           { const uint64_t x = clock64(); tk[6] += x - ta; ta = x; }
         }
       }
@@ -6612,7 +6700,7 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
                                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                          dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
                                          const void *fc_host, hipStream_t stream, hipStream_t side,
-                                         hipEvent_t fork, hipEvent_t join, int fork_at) {
+                                         hipEvent_t fork, hipEvent_t fork2, hipEvent_t join, int fork_at) {
   if (n == 0) return 0;
   dpf::FlowCtx fc = *reinterpret_cast<const dpf::FlowCtx *>(fc_host);
   if (hipMemsetAsync(fc.events, 0, sizeof(uint32_t), stream) != hipSuccess) return -5;
@@ -6658,6 +6746,18 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   const uint32_t rb = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
   // a mixed burst: may the allocating lane meet a port-forwarding creation's key
   hipLaunchKernelGGL(dp_nat_cross, dim3(rb), dim3(256), 0, stream, fc);
+  // (fork_at 3) the steady refreshes dp_nat_prep resolved replay on the side
+  // stream now, beside the rest of the NAT pass (fc.replay 4)
+  auto replay = [&](hipStream_t s, uint32_t which) {
+    fc.replay = which;
+    if (meta) dpk_run_pipeline_111(blocks, s, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+    else dpk_run_pipeline_101(blocks, s, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
+  };
+  const bool forked = side && fork && fork2 && join && fork_at >= 1 && fork_at <= 3;
+  if (forked && fork_at == 3) {
+    if (hipEventRecord(fork, stream) != hipSuccess || hipStreamWaitEvent(side, fork, 0) != hipSuccess) return -5;
+    replay(side, 4);
+  }
   // port forwarding near the capacity: the creations' admissions in packet order
   hipLaunchKernelGGL(dp_nat_admit_plan, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
   const uint32_t ab = (n + kAdmChunk - 1) / kAdmChunk;
@@ -6671,22 +6771,16 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
   // stream, beside the lane -- forked after the resolve (fork_at 1) or after
   // the lane's plan (2); then the lane's records after it.  Without a side
   // stream, one replay of every record after the lane.
-  auto replay = [&](hipStream_t s, uint32_t which) {
-    fc.replay = which;
-    if (meta) dpk_run_pipeline_111(blocks, s, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
-    else dpk_run_pipeline_101(blocks, s, img_base, im, buf, buf_bytes, in, out, meta, n, part, fc);
-  };
-  const bool forked = side && fork && join && (fork_at == 1 || fork_at == 2);
   auto fork_off = [&]() {
-    if (hipEventRecord(fork, stream) != hipSuccess || hipStreamWaitEvent(side, fork, 0) != hipSuccess) return false;
-    replay(side, 2);
+    if (hipEventRecord(fork2, stream) != hipSuccess || hipStreamWaitEvent(side, fork2, 0) != hipSuccess) return false;
+    replay(side, fork_at == 3 ? 5 : 2);
     return hipEventRecord(join, side) == hipSuccess;
   };
   if (forked && fork_at == 1 && !fork_off()) return -5;
   // a masquerading burst's allocating lane (its records in packet order)
   order(1);
   hipLaunchKernelGGL(dp_nat_lane_plan, dim3(rb), dim3(256), 0, stream, img_base, im, fc);
-  if (forked && fork_at == 2 && !fork_off()) return -5;
+  if (forked && fork_at >= 2 && !fork_off()) return -5;
   hipLaunchKernelGGL(dp_nat_lane, dim3(1), dim3(64), 0, stream, img_base, im, fc);
   hipLaunchKernelGGL(dp_nat_lane_assign, dim3(rb), dim3(256), 0, stream, fc);
   hipLaunchKernelGGL(dp_nat_pairs, dim3(rb), dim3(256), 0, stream, img_base, im, fc);

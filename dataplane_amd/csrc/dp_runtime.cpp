@@ -54,7 +54,7 @@ extern "C" int dpk_launch_pipeline_flows(const uint8_t *img_base, const void *im
                                          uint64_t buf_bytes, const dp_pkt_in_t *in, dp_pkt_out_t *out,
                                          dp_pkt_meta_t *meta, uint32_t n, uint64_t *stats, uint64_t *stats_part,
                                          const void *fc_host, hipStream_t stream, hipStream_t side,
-                                         hipEvent_t fork, hipEvent_t join, int fork_at);
+                                         hipEvent_t fork, hipEvent_t fork2, hipEvent_t join, int fork_at);
 
 namespace {
 
@@ -173,13 +173,14 @@ std::atomic<uint32_t> g_last_lean{0};   // dpf_debug_last_lean
 std::atomic<uint32_t> g_no_ctx{0};      // dpf_debug_no_ctx
 // where the NAT pass forks the replay of the records off the allocating lane
 // to the side stream: 0 never (one replay after the lane), 1 after the
-// resolve, 2 after the lane's plan (dpf_debug_replay_fork; DPGPU_REPLAY_FORK)
+// resolve, 2 after the lane's plan, 3 the steady refreshes after dp_nat_prep
+// and the rest after the lane's plan (dpf_debug_replay_fork; DPGPU_REPLAY_FORK)
 std::atomic<int> g_replay_fork{-1};
 int replay_fork() {
   int v = g_replay_fork.load(std::memory_order_relaxed);
   if (v < 0) {
     const char *e = getenv("DPGPU_REPLAY_FORK");
-    v = e && *e >= '0' && *e <= '2' && !e[1] ? *e - '0' : 1;
+    v = e && *e >= '0' && *e <= '3' && !e[1] ? *e - '0' : 2;
     g_replay_fork.store(v, std::memory_order_relaxed);
   }
   return v;
@@ -279,7 +280,7 @@ struct dp_ctx {
   // the NAT pass's side stream (lowest priority): the replay of the records
   // off the allocating lane runs on it beside the lane (fork / join events)
   hipStream_t side = nullptr;
-  hipEvent_t side_fork = nullptr, side_join = nullptr;
+  hipEvent_t side_fork = nullptr, side_fork2 = nullptr, side_join = nullptr;
   bool side_tried = false;
   uint64_t clock = 0;                  // dp_ctx_set_option(DP_OPT_CLOCK)
   // host threads of the staged-copy path, the context's own: a staged burst
@@ -566,6 +567,7 @@ int dp_ctx_destroy(dp_ctx_t *c) {
   if (c->fl_used) (void)hipEventDestroy(c->fl_used);
   if (c->side) { (void)hipStreamSynchronize(c->side); (void)hipStreamDestroy(c->side); }
   if (c->side_fork) (void)hipEventDestroy(c->side_fork);
+  if (c->side_fork2) (void)hipEventDestroy(c->side_fork2);
   if (c->side_join) (void)hipEventDestroy(c->side_join);
   for (auto &h : c->hs) if (h) { (void)hipStreamSynchronize(h); (void)hipStreamDestroy(h); }
   for (auto &e : c->hev) if (e) (void)hipEventDestroy(e);
@@ -803,12 +805,13 @@ static int launch_burst(dp_ctx_t *c, uint8_t *dev_buf, uint64_t buf_bytes, const
       if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
       if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, lo) != hipSuccess ||
           hipEventCreateWithFlags(&c->side_fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c->side_fork2, hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&c->side_join, hipEventDisableTiming) != hipSuccess)
         (void)hipGetLastError();
     }
     rc = dpk_launch_pipeline_flows(img->dev, img->dev + img->im_off, dev_buf, buf_bytes, dev_in, dev_out,
                                    dev_meta, n, dev_stats, part, &fc, s, fork_at ? c->side : nullptr,
-                                   c->side_fork, c->side_join, fork_at);
+                                   c->side_fork, c->side_fork2, c->side_join, fork_at);
     if (!rc) {
       if (!c->fl_used && hipEventCreateWithFlags(&c->fl_used, hipEventDisableTiming) != hipSuccess)
         return fail(DP_EIO, "hipEventCreate");
@@ -1066,9 +1069,10 @@ int dp_ctx_attach_flow_table(dp_ctx_t *c, dp_flow_table_t *ft) {
 // allocating lane alone (no wave batches); 3 runs port-forwarding bursts
 // without room for every pair on one lane (no admission pass); 4 runs mixed
 // bursts on one lane (no mode 5); 5 runs the allocating lane without its bulk
-// serve (every allocation in the lane's steps).
+// serve (every allocation in the lane's steps); 6 the bulk serve with every
+// block opened by one lane (no wave-wide open).
 void dpf_debug_nat_sequential(int on) {
-  g_nat_seq.store(on >= 1 && on <= 5 ? (uint32_t)on : 0u, std::memory_order_relaxed);
+  g_nat_seq.store(on >= 1 && on <= 6 ? (uint32_t)on : 0u, std::memory_order_relaxed);
 }
 // Test hook (not part of dpgpu.h): the context's last flows burst's NAT-pass
 // counters (dp_flow.h FlowCtx::pf_cnt: the mode that ran, the split pass's
@@ -1088,9 +1092,10 @@ void dpf_debug_flows_full(int on) { g_flows_full.store(on ? 1u : 0u, std::memory
 // LDS copy of the context tables even where they fit (A/Bs, parity of both).
 void dpf_debug_no_ctx(int on) { g_no_ctx.store(on ? 1u : 0u, std::memory_order_relaxed); }
 // Test hook (not part of dpgpu.h): where the NAT pass forks the replay off the
-// allocating lane (0 never, 1 after the resolve, 2 after the lane's plan;
-// -1 back to DPGPU_REPLAY_FORK / the default, 1).
-void dpf_debug_replay_fork(int at) { g_replay_fork.store(at >= 0 && at <= 2 ? at : -1, std::memory_order_relaxed); }
+// allocating lane (0 never, 1 after the resolve, 2 after the lane's plan, 3
+// the steady refreshes after dp_nat_prep and the rest after the plan;
+// -1 back to DPGPU_REPLAY_FORK / the default, 2).
+void dpf_debug_replay_fork(int at) { g_replay_fork.store(at >= 0 && at <= 3 ? at : -1, std::memory_order_relaxed); }
 // Test hook: 1 if the last flows burst launched ran the lean variant.
 int dpf_debug_last_lean() { return (int)g_last_lean.load(std::memory_order_relaxed); }
 

@@ -55,10 +55,12 @@ def test_gpu_masquerade_kat(s):
 
 
 # (dpf_debug_nat_sequential, dpf_debug_replay_fork): the split pass with the
-# replay off the allocating lane forked after the resolve (the default), after
-# the lane's plan, or not forked (one replay after the lane)
-NAT_MODES = {"split": (0, 1), "split-fork-plan": (0, 2), "split-no-fork": (0, 0), "one-lane": (1, 1),
-             "split-alone": (2, 1), "split-steps": (5, 1)}
+# replay off the allocating lane forked after the lane's plan (the default),
+# after the resolve, the steady refreshes after dp_nat_prep, or not forked (one
+# replay after the lane)
+NAT_MODES = {"split": (0, 2), "split-fork-resolve": (0, 1), "split-fork-prep": (0, 3), "split-no-fork": (0, 0),
+             "one-lane": (1, 2),
+             "split-alone": (2, 2), "split-steps": (5, 2)}
 
 
 @pytest.mark.parametrize("nat", list(NAT_MODES))

@@ -27,11 +27,15 @@ def torch_first():
     torch.cuda.init()
 
 
-@pytest.mark.parametrize("e,n,force", [(2_000, 20_000, 0), (2_000, 20_000, 4), (125_000, 300_000, 0)],
-                         ids=["small", "small-no-mode5", "250k-connections"])
-def test_gpu_mixed_bursts(e, n, force):
+@pytest.mark.parametrize("e,n,force,fork", [(2_000, 20_000, 0, 2), (2_000, 20_000, 0, 3), (2_000, 20_000, 4, 2),
+                                            (125_000, 300_000, 0, 2)],
+                         ids=["small", "small-steady-replay-early", "small-no-mode5", "250k-connections"])
+def test_gpu_mixed_bursts(e, n, force, fork):
+    """fork: where the replay leaves for the side stream (dpf_debug_replay_fork:
+    2 after the lane's plan, 3 the steady refreshes right after dp_nat_prep)."""
     ro, rg = OracleRunner(), GpuRunner(slots=1 << 22)
     A.gpu_lib().dpf_debug_nat_sequential(force)
+    A.gpu_lib().dpf_debug_replay_fork(fork)
     want = 1 if force == 4 else 5
     try:
         for r in (ro, rg):
@@ -81,4 +85,5 @@ def test_gpu_mixed_bursts(e, n, force):
         assert hist(out).get("FlowCapacityExceeded", 0) > 0, hist(out)
     finally:
         A.gpu_lib().dpf_debug_nat_sequential(0)
+        A.gpu_lib().dpf_debug_replay_fork(-1)
         rg.close()
