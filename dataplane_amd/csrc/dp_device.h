@@ -403,6 +403,10 @@ struct Image {
   // masquerade expose): a flows burst sizes the masquerade split's lane
   // scratch (dp_runtime.cpp)
   uint32_t masq;
+  // 1: two port-forwarding rules may map onto one internal address and port
+  // (their internal sides overlap): a creation's reverse key may then be a
+  // flow of another connection's pair (dp_nat_mark probes for it)
+  uint32_t pf_overlap;
   uint32_t n_nh;             // NhRec count
   // The context tables every packet reads -- VNI slots, the pair map's slots,
   // PairRecs, NhRecs -- copied into each workgroup's LDS when together they

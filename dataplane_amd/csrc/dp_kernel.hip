@@ -4956,7 +4956,11 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
         // record tags the pair it is attached to -- a port-forwarding record
         // on a masqueraded pair (a creation replaces its flow) too: that
         // pair's refreshes are not order-free -- and a creation the pair whose
-        // reverse flow holds its reverse key (it replaces that flow)
+        // reverse flow holds its reverse key (it replaces that flow).  Such a
+        // pair has another forward key than the creation's (the creation's
+        // own would have been found and attached), which only rules whose
+        // internal sides overlap allow (Image.pf_overlap); a pair whose
+        // forward flow is gone is never steady (pf_steady_v wants it whole)
         if (R.slot <= fc.mask) {
           const dpf::FlowSlot f = pfw::load_slot(&fc.slots[R.slot]);
           if (f.state == R.state) {
@@ -4969,7 +4973,7 @@ __global__ void __launch_bounds__(256) dp_nat_mark(const uint8_t *__restrict__ i
           }
         }
         dpf::FKey rk;
-        if ((R.bits & dpf::kPqPf) && pfw::creation_rk(g, R, rk)) {
+        if ((R.bits & dpf::kPqPf) && g.im.pf_overlap && pfw::creation_rk(g, R, rk)) {
           uint32_t st;
           uint4 v, w;
           const uint32_t z = flow_probe(fc, rk, st, v, w);

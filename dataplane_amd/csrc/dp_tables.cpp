@@ -1488,6 +1488,33 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
   im.pf_ids = build_hash(ib, pidkv);
   im.pf_rules = pfrecs.empty() ? ib.alloc(sizeof(PfRuleRec)) : ib.put(pfrecs);
   im.n_pf = (uint32_t)pfrecs.size();
+  // do two rules' internal sides overlap (the same destination VPC, family
+  // and protocol -- 0 any --, overlapping internal prefixes and port ranges)?
+  // (within one rule the mapping is one to one)
+  im.pf_overlap = 0;
+  if (pfrecs.size() > 2048) {
+    im.pf_overlap = 1;  // (not searched: assumed)
+  } else {
+    auto pre_meet = [](const PfRuleRec &a, const PfRuleRec &b) {
+      const uint32_t len = std::min<uint32_t>(a.plen, b.plen);
+      for (uint32_t w = 0; w < 4; w++) {
+        const uint32_t lo = 32 * w;
+        if (lo >= len) break;
+        const uint32_t bits = std::min<uint32_t>(32, len - lo);
+        const uint32_t m = bits == 32 ? 0xffffffffu : ~(0xffffffffu >> bits);
+        if ((a.inn[w] ^ b.inn[w]) & m) return false;
+      }
+      return true;
+    };
+    for (size_t i = 0; i < pfrecs.size() && !im.pf_overlap; i++)
+      for (size_t j = i + 1; j < pfrecs.size() && !im.pf_overlap; j++) {
+        const PfRuleRec &a = pfrecs[i], &b = pfrecs[j];
+        if (a.dst_vni != b.dst_vni || a.fam != b.fam) continue;
+        if (a.proto && b.proto && a.proto != b.proto) continue;
+        if (a.int_hi < b.int_lo || b.int_hi < a.int_lo) continue;
+        if (pre_meet(a, b)) im.pf_overlap = 1;
+      }
+  }
   if (im.n_pf || d->n_masq) im.snat = 1;
   if (d->n_masq) im.masq = 1;
 
