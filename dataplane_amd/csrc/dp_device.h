@@ -312,7 +312,9 @@ struct NatRange {
 // exactly one (the common case: the lookup then needs no range search).
 struct alignas(16) NatEnt {
   uint32_t net;              // prefix network (host order)
-  uint8_t len, is_pat, covers_all, inl;  // inl: the range is inline (n_ranges == 1, offset < 2^32)
+  // inl: bit 0 the range is inline (n_ranges == 1, offset < 2^32), bit 1
+  // the port range is (n_pr == 1: first_pr holds it, packed)
+  uint8_t len, is_pat, covers_all, inl;
   int32_t parent;            // next shorter covering entry in this table, -1
   uint32_t first_pr, n_pr;   // uint32_t packed (lo | hi<<16)
   uint32_t first_range, n_ranges;

@@ -1359,6 +1359,10 @@ struct NatQ {
   uint16_t np;
 };
 
+// the entry's j-th port range (packed lo | hi << 16): inline for one range
+__device__ __forceinline__ uint32_t nat_pr(const NatEnt &E, const uint32_t *prs, uint32_t j) {
+  return (E.inl & 2) ? E.first_pr : prs[E.first_pr + j];
+}
 __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port, const uint32_t pre[2]) {
   const NatTab *tabs = g.at<NatTab>(g.im.nat_tab_recs);
   const NatEnt *ents = g.at<NatEnt>(g.im.nat_ents);
@@ -1423,7 +1427,7 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
         if (!E[k].is_pat) cov = true;
         else
           for (uint32_t j = 0; j < E[k].n_pr; j++) {
-            uint32_t pr = prs[E[k].first_pr + j];
+            uint32_t pr = nat_pr(E[k], prs, j);
             if ((pr & 0xffff) <= q[k].port && q[k].port <= (pr >> 16)) { cov = true; break; }
           }
       }
@@ -1454,16 +1458,16 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
       if (!has_port) { live[k] = false; continue; }
       int pk = -1;
       for (uint32_t j = 0; j < E[k].n_pr; j++) {
-        uint32_t pr = prs[E[k].first_pr + j];
+        uint32_t pr = nat_pr(E[k], prs, j);
         if ((pr & 0xffff) <= q[k].port && q[k].port <= (pr >> 16)) { pk = (int)j; break; }
       }
       if (pk < 0) { live[k] = false; continue; }
-      uint32_t pr = prs[E[k].first_pr + pk];
+      uint32_t pr = nat_pr(E[k], prs, (uint32_t)pk);
       uint64_t plen = (uint64_t)(pr >> 16) - (pr & 0xffff) + 1;
       eo[k] = ip_off * plen + (uint64_t)(q[k].port - (pr & 0xffff));
       if (eo[k] >= esize) { live[k] = false; continue; }
     }
-    if (E[k].inl) {
+    if (E[k].inl & 1) {
       // the only range is inline in the entry: no search
       const bool le = E[k].is_pat ? (E[k].olo_ip < addr || (E[k].olo_ip == addr && E[k].olo_port <= q[k].port))
                                   : E[k].olo_ip <= addr;
@@ -1493,7 +1497,7 @@ __device__ __forceinline__ void nat_find2(const Img &g, NatQ q[2], bool has_port
     int sel = (int)rl[k] - 1;
     if (sel < 0) continue;
     NatRange R;
-    if (E[k].inl) {
+    if (E[k].inl & 1) {
       R.olo_ip = E[k].olo_ip; R.ohi_ip = E[k].ohi_ip; R.olo_port = E[k].olo_port; R.ohi_port = E[k].ohi_port;
       R.tlo_ip = E[k].tlo_ip; R.thi_ip = E[k].thi_ip; R.tlo_port = E[k].tlo_port; R.thi_port = E[k].thi_port;
       R.offset = E[k].offset;

@@ -1205,6 +1205,11 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
         tot += (uint64_t)pr.hi - pr.lo + 1;
       }
       ne.covers_all = (!e->is_pat || tot == 65536) ? 1 : 0;
+      // one port range: kept in the entry itself (inl bit 1), no second read
+      if (e->n_port_ranges == 1) {
+        ne.first_pr = nprs.back();
+        ne.inl |= 2;
+      }
       std::vector<NatRange> rs;
       for (uint32_t k = 0; k < e->n_ranges; k++) {
         const dp_nat_range_t &s = d->nat_ranges[e->first_range + k];
@@ -1224,7 +1229,7 @@ int build_image(const dp_tables_desc_t *d, BuiltImage &out, PfLineage *pf) {
       ne.n_ranges = (uint32_t)rs.size();
       if (rs.size() == 1 && rs[0].offset <= 0xffffffffull) {
         const NatRange &x = rs[0];
-        ne.inl = 1;
+        ne.inl |= 1;
         ne.olo_ip = x.olo_ip; ne.ohi_ip = x.ohi_ip; ne.olo_port = x.olo_port; ne.ohi_port = x.ohi_port;
         ne.tlo_ip = x.tlo_ip; ne.thi_ip = x.thi_ip; ne.tlo_port = x.tlo_port; ne.thi_port = x.thi_port;
         ne.offset = (uint32_t)x.offset;

@@ -130,3 +130,52 @@ def test_gpu_portfw_random_bursts(seed, n_conn, capacity, one_lane):
             assert 4 in modes, modes
     elif not one_lane:
         assert 2 in modes and 1 not in modes, modes
+
+
+def test_gpu_portfw_overlapping_rules_replace_a_steady_pair():
+    """Two port-forwarding rules onto one internal host and port (70.71.72.73
+    and .74, port 3022, both to 192.168.1.1:22: Image.pf_overlap).  A client's
+    connection through the first is established; then one burst holds its
+    steady refreshes (both directions) around the same client opening a
+    connection through the second rule -- whose reverse key is the established
+    pair's reverse flow, which that creation replaces (dp_nat_mark tags the
+    pair, so its refreshes run in the connection's order, not in dp_nat_prep).
+    GPU == oracle: records, bytes, every packet's flow."""
+    from edgecase import pack_burst
+    rules = [pfkat.tcp_rule(), pfkat.tcp_rule(ext="70.71.72.74/32")]
+    cl, sv = "10.0.0.2", "192.168.1.1"
+    c2a = lambda fl: (pfkat.frame(cl, "70.71.72.73", 6, 7777, 3022, fl), pfkat.VPC1)
+    c2b = lambda fl: (pfkat.frame(cl, "70.71.72.74", 6, 7777, 3022, fl), pfkat.VPC1)
+    s2c = lambda fl: (pfkat.frame(sv, cl, 6, 22, 7777, fl), pfkat.VPC2)
+    S, A_, P = pfkat.SYN, pfkat.ACK, pfkat.PSH
+    bursts = [[c2a(S)], [s2c(S | A_)], [c2a(A_)],
+              # established: steady refreshes around the second rule's creation
+              [c2a(A_ | P), s2c(A_ | P), c2a(A_), c2b(S), s2c(A_ | P), c2a(A_ | P), s2c(A_)],
+              [c2a(A_ | P), s2c(A_ | P), c2b(A_)]]
+    got = {}
+    for name, mk in (("oracle", pfkat.OracleRunner), ("gpu", pfkat.GpuRunner)):
+        r = mk()
+        steps = []
+        try:
+            r.publish(pfkat.world(rules)())
+            for k, pk in enumerate(bursts):
+                r.set_clock((k + 1) * pfkat.SEC)
+                buf, inp = pack_burst([(fr, 1, A.IN_SEEDED_OVERLAY, v) for fr, v in pk])
+                res = r.burst(buf, inp)
+                refs = [int(x) for x in res["flow_ref"]]
+                infos = [r.get([x])[0] if x != A.FLOW_NONE else None for x in refs]
+                steps.append((res.copy(), buf.copy(), infos, r.count()))
+        finally:
+            if name == "gpu":
+                r.close()
+        got[name] = steps
+    co, cg = IdCanon(), IdCanon()
+    for k, ((ro, bo, io, no), (rg, bg, ig, ng)) in enumerate(zip(got["oracle"], got["gpu"])):
+        a, b = common_fields(ro, rg)
+        assert np.array_equal(a, b), f"burst {k}: records {a} != {b}"
+        assert np.array_equal(bo, bg), f"burst {k}: bytes"
+        for i, (x, y) in enumerate(zip(io, ig)):
+            assert (x is None) == (y is None), f"burst {k} packet {i}: flow attached"
+            if x is not None:
+                same_info(x, y, co, cg, f"burst {k} packet {i}")
+        assert no == ng, f"burst {k}: counts {no} vs {ng}"
