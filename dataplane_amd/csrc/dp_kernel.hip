@@ -5173,7 +5173,8 @@ __global__ void __launch_bounds__(256) dp_nat_cross(dpf::FlowCtx fc) {
   // DESIGN.md §3)
   for (uint32_t rec = blockIdx.x * 256 + threadIdx.x; rec < nrec; rec += gridDim.x * 256) {
     const dpf::PfReq &R = fc.pf[rec];
-    if ((R.bits & (dpf::kPqReached | dpf::kPqMasq)) != (dpf::kPqReached | dpf::kPqMasq)) continue;
+    // (a steady refresh dp_nat_prep resolved has its live flow: no slot read)
+    if ((R.bits & (dpf::kPqReached | dpf::kPqMasq | dpf::kPqSteady)) != (dpf::kPqReached | dpf::kPqMasq)) continue;
     if (R.slot <= fc.mask && fc.slots[R.slot].state == R.state) continue;
     dpf::FKey ik;
     if (!pfw::masq_ik(R, ik)) continue;
