@@ -102,6 +102,11 @@ struct PfReq {
   uint32_t mverdict;     // Masquerade: DoneReason, or kPfForward
   uint32_t mnat;         // dp_pf_action | ident (1 << 8) | port << 16
   uint32_t mnat_ip[4];
+  // the first pass's ACL outcome (out.acl code, rule): the replay takes it
+  // (and the flow filter's, dst_vni and the kPq requirement bits) instead of
+  // classifying again
+  uint32_t acl_code;
+  uint32_t acl_rule;
 };
 constexpr uint32_t kPqReached = 1u << 0;  // the packet reached PortForwarder (else dropped on the way)
 constexpr uint32_t kPqTcp = 1u << 1;

@@ -2316,12 +2316,22 @@ __device__ __forceinline__ void hoist_walks(const Img &g, const State &S, int32_
 // :296-325) is the plain lookup.
 template <bool FL>
 __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, const Hdr &H, State &S, Pre &P,
-                                                  FlowPk &fp, const dpf::FlowCtx *fc) {
+                                                  FlowPk &fp, const dpf::FlowCtx *fc, const dpf::PfReq *rp) {
   P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY) || S.dst_vni) return;
   uint8_t gate = 0;  // SourceGate of the local lookup
   uint32_t gate_vni = 0;  // GateVni of the remote lookup (LookupInput.dst_vpcd; 0: None)
   if constexpr (FL) {
+    if (rp) {
+      // the replay: the first pass's verdict from the record (its
+      // destination VPC and requirements), no classifier walk
+      S.dst_vni = rp->dst_vni;
+      if (rp->bits & dpf::kPqSnatSrc) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
+      if (rp->bits & dpf::kPqSnatDst) S.flags |= DP_META_REQ_STATIC_NAT_DST;
+      if (SNAT && (rp->bits & dpf::kPqPf)) S.flags |= DP_META_REQ_PORT_FORWARDING;
+      if (SNAT && (rp->bits & dpf::kPqMasq)) S.flags |= DP_META_REQ_MASQUERADE;
+      return;
+    }
     if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid) {
       S.dst_vni = fp.dst_vni;
       if (SNAT && (fp.fflags & dpf::kFlagMasq)) S.flags |= DP_META_REQ_MASQUERADE;
@@ -2435,6 +2445,30 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY)) return;
   if (!S.src_vni || !S.dst_vni) { done(S, DP_DONE_UNROUTABLE); return; }
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
+  if constexpr (FL) {
+    if (rp) {
+      // the replay: the first pass's outcome from the record, no classifier
+      // walk -- for a packet whose verdict rests on a flow (verdict 6), the
+      // peering default unless the NAT pass kept the flow valid (acl_over 0)
+      uint32_t action;
+      if (rp->bits & dpf::kPqSens) {
+        const uint32_t def = rp->acl_def;
+        S.acl = (uint8_t)def;
+        action = def == 4 ? DP_ACL_DENY : DP_ACL_ALLOW;
+        if (rp->acl_over == 0) {
+          action = DP_ACL_ALLOW;
+          S.acl = 6;
+          S.acl_rule = rp->acl_rule6;
+        }
+      } else {
+        S.acl = (uint8_t)rp->acl_code;
+        S.acl_rule = rp->acl_rule;
+        action = (S.acl == 2 || S.acl == 4) ? DP_ACL_DENY : DP_ACL_ALLOW;
+      }
+      if (action == DP_ACL_DENY) done(S, DP_DONE_ACL_DROPPED);
+      return;
+    }
+  }
   uint8_t proto = net_proto(F, H);
   int t = H.net == 4 ? 0 : 1;
   const int32_t pi = pair_of(g, S);
@@ -2452,13 +2486,7 @@ __device__ __forceinline__ void stage_acl(const Img &g, const Frame &F, const Hd
     action = v ? v - 1 : DP_ACL_ALLOW;
     S.acl = def;
     if constexpr (FL) {
-      if (rp) {
-        if ((rp->bits & dpf::kPqSens) && rp->acl_over == 0) {
-          action = DP_ACL_ALLOW;
-          S.acl = 6;
-          S.acl_rule = rp->acl_rule6;
-        }
-      } else if (fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid && fp.related <= fc->mask) {
+      if (!rp && fp.slot != dpf::kNoSlot && fp.active && fp.genid >= fc->genid && fp.related <= fc->mask) {
         const dpf::FlowSlot *r = fc->slots + fp.related;
         const uint4 a = ld4(&r->state), b = ld4(&r->src[0]), c = ld4(&r->dst[0]);
         if (a.x == fp.related_tag) {  // the related flow is still in the table (Weak::upgrade)
@@ -2560,6 +2588,8 @@ __device__ __forceinline__ void nat_record(const Frame &F, const Hdr &H, const S
   }
   R->acl_def = fp.def_acl;
   R->acl_rule6 = fp.acl_rule6;
+  R->acl_code = S.acl;
+  R->acl_rule = S.acl_rule;
   R->acl_over = 0;
   fc->pf_of[idx] = rec;  // (its bit in the burst's bitmap: flow_effects, per wave)
   fp.pf_rec = rec;
@@ -3213,7 +3243,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
   Pre P;
   TRIP_ST(2);
 #ifndef DP_PROBE_NOFF
-  stage_flow_filter<FL>(g, F, H, S, P, fp, fc);
+  stage_flow_filter<FL>(g, F, H, S, P, fp, fc, rp);
 #else
   P.ffl = P.acl = P.nsrc = P.ndst = NO_PRE;
 #endif
