@@ -2321,6 +2321,11 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
   if (S.done != DONE_NONE || !(S.flags & DP_META_IS_OVERLAY) || S.dst_vni) return;
   uint8_t gate = 0;  // SourceGate of the local lookup
   uint32_t gate_vni = 0;  // GateVni of the remote lookup (LookupInput.dst_vpcd; 0: None)
+  // FL: a bypassing lane (its flow decides) skips the tables, but joins the
+  // other lanes where they start the ACL's and static NAT's hoisted index
+  // walks, so its walks go out with theirs instead of one after the other
+  // in those stages
+  bool byp = false;
   if constexpr (FL) {
     if (rp) {
       // the replay: the first pass's verdict from the record (its
@@ -2338,22 +2343,28 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
       if (SNAT && (fp.fflags & dpf::kFlagPf)) S.flags |= DP_META_REQ_PORT_FORWARDING;
       if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_SRC) S.flags |= DP_META_REQ_STATIC_NAT_SRC;
       if (fp.fflags & DP_FLOW_REQ_STATIC_NAT_DST) S.flags |= DP_META_REQ_STATIC_NAT_DST;
-      return;
+      byp = true;
     }
     // flow_revalidation_data (:296-325): the reply flow of a masqueraded pair
     // is revalidated against the remote rules gated on its destination VPC,
     // that of a port-forwarded pair against the local rules gated on
     // PortFwdReply
-    if (SNAT && fp.slot != dpf::kNoSlot && fp.active && fp.genid < fc->genid && !(fp.fflags & DP_FLOW_INITIATOR)) {
+    else if (SNAT && fp.slot != dpf::kNoSlot && fp.active && fp.genid < fc->genid && !(fp.fflags & DP_FLOW_INITIATOR)) {
       if (fp.fflags & dpf::kFlagMasq) gate_vni = fp.dst_vni;
       else if (fp.fflags & dpf::kFlagPf) gate = 1;
     }
   }
+  const int t = H.net == 4 ? 0 : 1;
+  uint32_t dvni = 0, dnat = 0;
+  int32_t pi = -1;
+  uint8_t proto = 0;
+  Key128 src{0, 0};
+  if (!byp) {
   if (H.net == 0) { done(S, DP_DONE_NOT_IP); return; }
   if (!S.src_vni) { done(S, DP_DONE_UNROUTABLE); return; }
-  uint8_t proto = net_proto(F, H);
-  int t = H.net == 4 ? 0 : 1;
-  Key128 src = key_of(F, H, S, true), dst = key_of(F, H, S, false);
+  proto = net_proto(F, H);
+  src = key_of(F, H, S, true);
+  const Key128 dst = key_of(F, H, S, false);
   const auto &VR = VNI_REC(S.vni_idx);
   int32_t rg = VR.ffr[t];
   // v4 candidate-list group: walk its index straight from the VNI context
@@ -2372,13 +2383,17 @@ __device__ __forceinline__ void stage_flow_filter(const Img &g, const Frame &F, 
     done(S, DP_DONE_FILTERED);
     return;
   }
-  uint32_t dvni = rh.action;
-  uint32_t dnat = rh.action2;
-  int32_t pi = (int32_t)rh.aux;
+  dvni = rh.action;
+  dnat = rh.action2;
+  pi = (int32_t)rh.aux;
   TRIP_ST(3);
   TRIP();
+  } else {
+    pi = pair_of(g, S);
+  }
+  if (t == 0 && pi >= 0) hoist_walks(g, S, pi, P);
+  if (byp) return;
   int32_t lg = CTX_TAB(PairRec, g.im.ctx_prec, g.im.pair_recs)[pi].ffl[t];
-  if (t == 0) hoist_walks(g, S, pi, P);
   uint32_t lpre = P.ffl;
   if (gate) {  // the (src, dst, PortFwdReply) group: no hoisted walk, the classifier walks it
     uint32_t gi;
@@ -3240,6 +3255,7 @@ __device__ __forceinline__ uint8_t process_packet(const Img &g, lds_u8 *slab, ld
       }
     }
   }
+  TS(9);  // (the ICMP-error handler and FlowLookup)
   Pre P;
   TRIP_ST(2);
 #ifndef DP_PROBE_NOFF
