@@ -10,6 +10,8 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_flows.py tests/test_gpu_por
 echo PYTEST_OK
 grep -E "passed|failed" gpurun_out/fab/pytest.log | tail -1
 VARIANTS="base head" CONFIGS="2 5" FLOWS=" " EXTRA="--no-nat" bash scripts/ab_bench.sh || exit 1
-for F in "" "--flows"; do
-  timeout -k 10 300 python scripts/stage_timing.py --config 2 --meta $F --reps 3 || exit 1
-done
+if [ -n "$TIMING" ]; then
+  for F in "" "--flows"; do
+    timeout -k 10 300 python scripts/stage_timing.py --config 2 --meta $F --reps 3 || exit 1
+  done
+fi
