@@ -3754,9 +3754,11 @@ struct Seq {
         if (atomicCAS(&fc.slots[j].state, st, (st & ~3u) | dpf::FS_BUSY) == st) { sl = j; break; }
       }
       if (sl == dpf::kNoSlot) return dpf::kNoSlot;
+      // (the bound only grows: a displacement within the one read at this
+      // insert's start needs nothing -- no agent-scope read of the one word
+      // every lane's insert would otherwise queue on)
       const uint32_t disp = (sl - home) & fc.mask;
-      if (disp > __hip_atomic_load(&fc.tmeta[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(&fc.tmeta[0], disp);
+      if (disp > bound) atomicMax(&fc.tmeta[0], disp);
       added++;
     }
     dpf::FlowSlot &s = fc.slots[sl];
