@@ -186,3 +186,25 @@ def test_gpu_portfw_at_scale(case):
     finally:
         A.gpu_lib().dpf_debug_nat_sequential(0)
         rg.close()
+
+
+def test_gpu_portfw_near_capacity_beyond_4m_packets():
+    """A port-forwarding burst near the capacity (mode 4: the creations'
+    admissions in packet order, dp_nat_admit_*) of 4.3M packets with ~2k
+    records: the admission scan's block sums (adm_blk, 1024 words: a block per
+    4096 records) are written only for blocks over records, not for every
+    4096 packets of the burst (round-5 ADVICE).  GPU == oracle."""
+    n = 4_300_000
+    buf, inp, npf = W.burst(n, 0.0005, 0)
+    ro, rg = OracleRunner(), GpuRunner(slots=1 << 16)
+    try:
+        for r in (ro, rg):
+            r.publish(W.tables())
+            r.set_clock(10 ** 12)
+            (r.fl if hasattr(r, "fl") else r.ft).set_capacity(npf)  # half the pairs fit
+        out, ob, cnt = both(ro, rg, buf, inp, "4.3M-packet burst near capacity")
+        assert int(cnt[12]) == 4, cnt
+        h = hist(out)
+        assert h.get("FlowCapacityExceeded", 0) > 0 and h["Delivered"] > n - npf, h
+    finally:
+        rg.close()
