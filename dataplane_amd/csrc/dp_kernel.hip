@@ -893,6 +893,27 @@ __device__ __forceinline__ void cur_dst(const Frame &F, const Hdr &H, const Stat
   else a = addr16(F, H.net_off + 24);
 }
 
+// the same destination as the LPM key's two 64-bit halves, built in
+// registers (an Addr16 filled in divergent branches was kept in scratch: a
+// store and a reload ahead of every direct-table load)
+__device__ __forceinline__ void cur_dst_key(const Frame &F, const Hdr &H, const State &S, uint8_t &fam,
+                                            uint64_t &khi, uint64_t &klo) {
+  auto w32 = [&](int o) {
+    return ((uint32_t)F.hs[o] << 24) | ((uint32_t)F.hs[o + 1] << 16) | ((uint32_t)F.hs[o + 2] << 8) | F.hs[o + 3];
+  };
+  if (S.encap) {
+    fam = S.o_fam;
+    if (S.o_fam == 4) { khi = (uint64_t)w32(16) << 32; klo = 0; }
+    else { khi = ((uint64_t)w32(24) << 32) | w32(28); klo = ((uint64_t)w32(32) << 32) | w32(36); }
+    return;
+  }
+  fam = (uint8_t)H.net;
+  if (H.net == 4) { khi = (uint64_t)S.v4dst << 32; klo = 0; return; }
+  const int o = H.net_off + 24;
+  khi = ((uint64_t)F.be32(o) << 32) | F.be32(o + 4);
+  klo = ((uint64_t)F.be32(o + 8) << 32) | F.be32(o + 12);
+}
+
 // ---------------------------------------------------------------------------
 // rapidhash-style hash (same restatement as the oracle; parity vs the
 // reference is UNPINNED)
@@ -1012,26 +1033,26 @@ __device__ __forceinline__ uint32_t lpm_dsel(uint32_t dbits) {
   return lpm_sel(b, 64 - b, b) | ((dbits & DPD_LPM_D16) << 16);
 }
 __device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t table_off, uint32_t sel, uint64_t blocks,
-                                             const Addr16 &a) {
-  const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1], klo = ((uint64_t)a.w[2] << 32) | a.w[3];
+                                             uint64_t khi, uint64_t klo) {
+  const uint32_t w0 = (uint32_t)(khi >> 32);
   int off = (int)(sel & 0xffu);
   if (sel >> 24) {  // DIR-24-8 with 16-bit direct entries (v4)
-    const uint32_t e = g.at<uint16_t>(table_off)[a.w[0] >> 8];
+    const uint32_t e = g.at<uint16_t>(table_off)[w0 >> 8];
     TRIP();
     if (e & 0x8000u) return e & 0x7fffu;
     TRIP();
-    return g.at<uint16_t>(blocks)[(e << 8) | (a.w[0] & 0xff)];
+    return g.at<uint16_t>(blocks)[(e << 8) | (w0 & 0xff)];
   }
 #if DP_V6W
   const uint32_t e = g.at<uint32_t>(table_off)[(uint32_t)(khi >> ((sel >> 8) & 0xffu)) &
                                                ((1u << ((sel >> 16) & 0xffu)) - 1u)];
 #else
-  const uint32_t e = g.at<uint32_t>(table_off)[a.w[0] >> (32 - off)];  // the direct table (dbits <= 32)
+  const uint32_t e = g.at<uint32_t>(table_off)[w0 >> (32 - off)];  // the direct table (dbits <= 32)
 #endif
   TRIP();
   if (e & 0x80000000u) return e & 0x7fffffffu;
   TRIP();
-  if (blocks) return g.at<uint16_t>(blocks)[(e << 8) | (a.w[0] & 0xff)];  // DIR-24-8 (v4)
+  if (blocks) return g.at<uint16_t>(blocks)[(e << 8) | (w0 & 0xff)];  // DIR-24-8 (v4)
   const PtNode *nodes = g.at<PtNode>(g.im.pt_nodes);
   const uint32_t *leaves = g.at<uint32_t>(g.im.pt_leaves);
   uint32_t ni = e;
@@ -1052,10 +1073,10 @@ __device__ __forceinline__ uint32_t lpm_walk(const Img &g, uint64_t table_off, u
   return g.im.drop_nh;  // unreachable for a well-formed image
 }
 __device__ __forceinline__ uint32_t lpm_lookup(const Img &g, const Lpm &L, const Addr16 &a) {
-  const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1];
+  const uint64_t khi = ((uint64_t)a.w[0] << 32) | a.w[1], klo = ((uint64_t)a.w[2] << 32) | a.w[3];
   if (DP_V6W && L.wtab && (khi >> (64 - L.wbits)) == L.wpfx)
-    return lpm_walk(g, L.wtab, lpm_sel(L.wbits + L.wtb, 64 - L.wbits - L.wtb, L.wtb), 0, a);
-  return lpm_walk(g, L.direct, lpm_dsel(L.dbits), L.blocks, a);
+    return lpm_walk(g, L.wtab, lpm_sel(L.wbits + L.wtb, 64 - L.wbits - L.wtb, L.wtb), 0, khi, klo);
+  return lpm_walk(g, L.direct, lpm_dsel(L.dbits), L.blocks, khi, klo);
 }
 
 // Multibit index walk from a context record's descriptor (Mbi): leaf value
@@ -2141,8 +2162,8 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
   }
   if (S.encap) { done(S, DP_DONE_INTERNAL_FAILURE); return; }  // routing an encapsulated packet again: unsupported
   const FibRec &fb = g.at<FibRec>(g.im.fibs)[fi];  // fields read where used (no struct copy)
-  uint8_t fam; Addr16 dst;
-  cur_dst(F, H, S, fam, dst);
+  uint8_t fam; uint64_t khi, klo;
+  cur_dst_key(F, H, S, fam, khi, klo);
   // one walk for every lane: v4 and v6 lanes of a wave issue their direct-table
   // loads together (two call sites would run one after the other)
   uint32_t sel = 0;
@@ -2152,14 +2173,14 @@ __device__ __forceinline__ void stage_ipforward(const Img &g, const Frame &F, Hd
     b4 = L.dbits;
     k4 = L.blocks;
     // a v6 key inside the FIB's window reads the window table instead
-    if (DP_V6W && fam == 6 && L.wtab && ((((uint64_t)dst.w[0] << 32) | dst.w[1]) >> (64 - L.wbits)) == L.wpfx) {
+    if (DP_V6W && fam == 6 && L.wtab && (khi >> (64 - L.wbits)) == L.wpfx) {
       d4 = L.wtab;
       k4 = 0;
       sel = lpm_sel(L.wbits + L.wtb, 64 - L.wbits - L.wtb, L.wtb);
     }
   }
   if (!sel) sel = lpm_dsel(b4);
-  const uint32_t nhi = lpm_walk(g, d4, sel, k4, dst);
+  const uint32_t nhi = lpm_walk(g, d4, sel, k4, khi, klo);
   TRIP();
   const auto &nr = CTX_REC(NhRec, g.im.ctx_nh, g.im.nh_recs, nhi);
   if (nr.kind != DPD_NH_CHAIN) {
