@@ -876,26 +876,10 @@ __device__ __forceinline__ Addr16 addr16(const Frame &F, int off) {
   return a;
 }
 
-// current destination address (after NAT) as a 16-byte key
-__device__ __forceinline__ void cur_dst(const Frame &F, const Hdr &H, const State &S, uint8_t &fam, Addr16 &a) {
-  if (S.encap) {  // the outer destination, from the deparsed outer IP header
-    fam = S.o_fam;
-    const int o = S.o_fam == 4 ? 16 : 24;
-    for (int i = 0; i < 4; i++)
-      a.w[i] = (S.o_fam == 6 || i == 0)
-                   ? ((uint32_t)F.hs[o + 4 * i] << 24) | ((uint32_t)F.hs[o + 4 * i + 1] << 16) |
-                         ((uint32_t)F.hs[o + 4 * i + 2] << 8) | F.hs[o + 4 * i + 3]
-                   : 0u;
-    return;
-  }
-  fam = (uint8_t)H.net;
-  if (H.net == 4) { a.w[0] = S.v4dst; a.w[1] = a.w[2] = a.w[3] = 0; }
-  else a = addr16(F, H.net_off + 24);
-}
-
-// the same destination as the LPM key's two 64-bit halves, built in
-// registers (an Addr16 filled in divergent branches was kept in scratch: a
-// store and a reload ahead of every direct-table load)
+// current destination address (after NAT) as the LPM key's two 64-bit
+// halves (network order, packed big-endian), built in registers: an Addr16
+// filled in divergent branches was kept in scratch memory -- a store and a
+// reload ahead of every direct-table load
 __device__ __forceinline__ void cur_dst_key(const Frame &F, const Hdr &H, const State &S, uint8_t &fam,
                                             uint64_t &khi, uint64_t &klo) {
   auto w32 = [&](int o) {
@@ -2850,9 +2834,10 @@ __device__ __forceinline__ void stage_egress(const Img &g, const Frame &F, const
   uint64_t dmac = S.eg_dmac;
   if (S.eg_code == DPD_EG_NEED_ADJ) {
     // no next-hop address: adjacency of the packet's (current) destination
-    uint8_t fam; Addr16 a;
-    if (S.encap || H.net) cur_dst(F, H, S, fam, a);
-    else { done(S, DP_DONE_NOT_IP); return; }
+    if (!S.encap && !H.net) { done(S, DP_DONE_NOT_IP); return; }
+    uint8_t fam; uint64_t khi, klo;
+    cur_dst_key(F, H, S, fam, khi, klo);
+    const Addr16 a{{(uint32_t)(khi >> 32), (uint32_t)khi, (uint32_t)(klo >> 32), (uint32_t)klo}};
     uint8_t m[6];
     if (!adj_find(g, S.oif, fam, a, m)) { done(S, DP_DONE_MISS_L2_RESOLUTION); return; }
     dmac = load_mac(m);
