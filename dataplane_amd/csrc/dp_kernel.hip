@@ -4239,11 +4239,16 @@ __device__ bool creation_rk(const Img &g, const dpf::PfReq &R, dpf::FKey &rk) {
   const bool first_seg = (tfl & 2) && !(tfl & 0x3du);
   if (!(R.bits & dpf::kPqEth) || !ports || (tcp && !first_seg) || !unicast(fam, R.dst)) return false;
   const uint32_t sport = R.ports >> 16, dport = R.ports & 0xffffu;
-  const int32_t e = lookup(g, R.src_vni, proto, fam, R.dst, dport);
+  // the address copied first: lookup / map index it with loop bounds the
+  // family sets, which would otherwise keep the whole record in scratch
+  uint32_t dst[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) dst[j] = R.dst[j];
+  const int32_t e = lookup(g, R.src_vni, proto, fam, dst, dport);
   if (e < 0) return false;
   const PfRuleRec &E = g.at<PfRuleRec>(g.im.pf_rules)[e];
   uint32_t na[4], np;
-  if (!map(E, R.dst, dport, na, np)) return false;
+  if (!map(E, dst, dport, na, np)) return false;
   rk.w[0] = E.dst_vni;
   rk.w[1] = fam | ((tcp ? DP_FLOW_TCP : DP_FLOW_UDP) << 8);
   rk.w[2] = (np << 16) | sport;
