@@ -1748,17 +1748,23 @@ __device__ __forceinline__ bool packet_fkey(const Frame &F, const Hdr &H, const 
   k.w[0] = S.src_vni;
   k.w[1] = (H.net == 4 ? 4u : 6u) | (kind << 8);
   k.w[2] = ports;
+  // the address words as plain values per branch, then stored once: the key
+  // written field by field in either branch was kept in scratch memory (a
+  // store and a reload ahead of the flow hash)
+  uint32_t a[8];
   if (H.net == 4) {
-    k.w[3] = __builtin_bswap32(S.v4src);
-    k.w[7] = __builtin_bswap32(S.v4dst);
-    k.w[4] = k.w[5] = k.w[6] = k.w[8] = k.w[9] = k.w[10] = 0;
+    a[0] = __builtin_bswap32(S.v4src);
+    a[4] = __builtin_bswap32(S.v4dst);
+    a[1] = a[2] = a[3] = a[5] = a[6] = a[7] = 0;
   } else {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      k.w[3 + j] = le32_at(F, H.net_off + 8 + 4 * j);
-      k.w[7 + j] = le32_at(F, H.net_off + 24 + 4 * j);
+      a[j] = le32_at(F, H.net_off + 8 + 4 * j);
+      a[4 + j] = le32_at(F, H.net_off + 24 + 4 * j);
     }
   }
+#pragma unroll
+  for (int j = 0; j < 8; j++) k.w[3 + j] = a[j];
   return true;
 }
 
